@@ -1,0 +1,515 @@
+"""SVG path-data parsing and segment geometry.
+
+Capability parity with the vendored ``svg.path`` package of the reference
+(``svg/path/path.py:9-449``, ``svg/path/parser.py:6-187``): the four segment
+kinds (line, cubic / quadratic Bezier, elliptical arc) with ``point(t)`` and
+``length()``, a mutable ``Path`` container with arc-length addressing and a
+``d()`` serializer, and ``parse_path`` for the full SVG command set
+(``MmZzLlHhVvCcSsQqTtAa``, relative forms, implicit repeats, S/T reflection).
+
+Implementation notes (this is an independent design, not a translation):
+
+* Curve and arc lengths are computed by adaptive 15-point Gauss-Kronrod
+  quadrature of ``|dP/dt|`` rather than by recursive chord subdivision; the
+  result agrees with the exact arc length to ~1e-12 relative.
+* Segments share one base class; equality is a tuple-key comparison.
+* The tokenizer is a single-pass scanner over one compiled regex.
+
+Geometry uses Python ``complex`` numbers for points (x + y*1j), the same
+convention as the reference, so callers can use ``p.start.real`` etc.
+"""
+from __future__ import annotations
+
+import math
+import re
+from collections.abc import MutableSequence
+from typing import Iterator, List, Optional
+
+__all__ = ["Line", "CubicBezier", "QuadraticBezier", "Arc", "Path", "parse_path"]
+
+# ----------------------------------------------------------------------------
+# numerical length: adaptive Gauss-Kronrod (G7/K15) on |derivative|
+# ----------------------------------------------------------------------------
+_XGK = (0.991455371120813, 0.949107912342759, 0.864864423359769, 0.741531185599394,
+        0.586087235467691, 0.405845151377397, 0.207784955007898, 0.000000000000000)
+_WGK = (0.022935322010529, 0.063092092629979, 0.104790010322250, 0.140653259715525,
+        0.169004726639267, 0.190350578064785, 0.204432940075298, 0.209482141084728)
+_WG = (0.129484966168870, 0.279705391489277, 0.381830050505119, 0.417959183673469)
+
+
+def _gk15(f, a: float, b: float):
+    c = 0.5 * (a + b)
+    h = 0.5 * (b - a)
+    fc = f(c)
+    k = fc * _WGK[7]
+    g = fc * _WG[3]
+    for j in range(7):
+        dx = h * _XGK[j]
+        s = f(c - dx) + f(c + dx)
+        k += _WGK[j] * s
+        if j % 2 == 1:
+            g += _WG[j // 2] * s
+    return k * h, abs((k - g) * h)
+
+
+def _integrate(f, a: float, b: float, tol: float = 1e-13, depth: int = 0) -> float:
+    val, err = _gk15(f, a, b)
+    if err <= tol * max(1.0, abs(val)) or depth > 40:
+        return val
+    m = 0.5 * (a + b)
+    return _integrate(f, a, m, tol, depth + 1) + _integrate(f, m, b, tol, depth + 1)
+
+
+def _fmt(v: float) -> str:
+    return format(v, "G")
+
+
+def _pt(p: complex) -> str:
+    return "%s,%s" % (_fmt(p.real), _fmt(p.imag))
+
+
+class _Segment:
+    __slots__ = ()
+    _fields: tuple = ()
+
+    def _key(self):
+        return tuple(getattr(self, f) for f in self._fields)
+
+    def __eq__(self, other):
+        if type(other) is not type(self):
+            return NotImplemented
+        return self._key() == other._key()
+
+    def __ne__(self, other):
+        r = self.__eq__(other)
+        return r if r is NotImplemented else not r
+
+    __hash__ = None  # mutable
+
+    def __repr__(self):
+        args = ", ".join("%s=%r" % (f, getattr(self, f)) for f in self._fields)
+        return "%s(%s)" % (type(self).__name__, args)
+
+    def derivative(self, t: float) -> complex:  # pragma: no cover - overridden
+        raise NotImplementedError
+
+    def length(self, error: Optional[float] = None, min_depth: Optional[int] = None) -> float:
+        tol = 1e-13 if error is None else max(min(error, 1e-6), 1e-15)
+        return _integrate(lambda t: abs(self.derivative(t)), 0.0, 1.0, tol)
+
+
+class Line(_Segment):
+    __slots__ = ("start", "end")
+    _fields = ("start", "end")
+
+    def __init__(self, start, end):
+        self.start = start
+        self.end = end
+
+    def point(self, pos: float) -> complex:
+        return self.start + (self.end - self.start) * pos
+
+    def derivative(self, t: float) -> complex:
+        return self.end - self.start
+
+    def length(self, error=None, min_depth=None) -> float:
+        return abs(complex(self.end) - complex(self.start))
+
+
+class CubicBezier(_Segment):
+    __slots__ = ("start", "control1", "control2", "end")
+    _fields = ("start", "control1", "control2", "end")
+
+    def __init__(self, start, control1, control2, end):
+        self.start = start
+        self.control1 = control1
+        self.control2 = control2
+        self.end = end
+
+    def point(self, pos: float) -> complex:
+        u = 1.0 - pos
+        return (u * u * u * self.start + 3.0 * u * u * pos * self.control1
+                + 3.0 * u * pos * pos * self.control2 + pos * pos * pos * self.end)
+
+    def derivative(self, t: float) -> complex:
+        u = 1.0 - t
+        return 3.0 * (u * u * (self.control1 - self.start) + 2.0 * u * t * (self.control2 - self.control1)
+                      + t * t * (self.end - self.control2))
+
+    def is_smooth_from(self, previous) -> bool:
+        if isinstance(previous, CubicBezier):
+            return self.start == previous.end and (self.control1 - self.start) == (previous.end - previous.control2)
+        return self.control1 == self.start
+
+
+class QuadraticBezier(_Segment):
+    __slots__ = ("start", "control", "end")
+    _fields = ("start", "control", "end")
+
+    def __init__(self, start, control, end):
+        self.start = start
+        self.control = control
+        self.end = end
+
+    def point(self, pos: float) -> complex:
+        u = 1.0 - pos
+        return u * u * self.start + 2.0 * u * pos * self.control + pos * pos * self.end
+
+    def derivative(self, t: float) -> complex:
+        return 2.0 * ((1.0 - t) * (self.control - self.start) + t * (self.end - self.control))
+
+    def is_smooth_from(self, previous) -> bool:
+        if isinstance(previous, QuadraticBezier):
+            return self.start == previous.end and (self.control - self.start) == (previous.end - previous.control)
+        return self.control == self.start
+
+    def length(self, error=None, min_depth=None) -> float:
+        # closed form: integral of |2a t + b| with a = P0 - 2P1 + P2, b = 2(P1 - P0)
+        p0, p1, p2 = complex(self.start), complex(self.control), complex(self.end)
+        a = p0 - 2.0 * p1 + p2
+        b = 2.0 * (p1 - p0)
+        la, lb = abs(a), abs(b)
+        if la < 1e-12:
+            return lb
+        dot = a.real * b.real + a.imag * b.imag
+        if abs(dot + la * lb) < 1e-12:
+            # a and b anti-parallel: the curve doubles back along a line
+            k = lb / la
+            return lb - la if k >= 2.0 else la * (k * k / 2.0 - k + 1.0)
+        if abs(dot - la * lb) < 1e-12:
+            return abs(p2 - p0)
+        # |2a t + b|^2 = A t^2 + B t + C
+        A = 4.0 * la * la
+        B = 4.0 * dot
+        C = lb * lb
+        sabc = 2.0 * math.sqrt(A + B + C)
+        a2 = math.sqrt(A)
+        a32 = 2.0 * A * a2
+        c2 = 2.0 * math.sqrt(C)
+        ba = B / a2
+        return (a32 * sabc + a2 * B * (sabc - c2)
+                + (4.0 * C * A - B * B) * math.log((2.0 * a2 + ba + sabc) / (ba + c2))) / (4.0 * a32)
+
+
+class Arc(_Segment):
+    """Elliptical arc in SVG endpoint form; converted to center form on init
+    (W3C SVG implementation notes F.6.5). ``theta`` is the start angle in
+    [0, 360) and ``delta`` the signed sweep in degrees."""
+
+    __slots__ = ("start", "radius", "rotation", "arc", "sweep", "end", "center", "theta", "delta",
+                 "_rx", "_ry", "_rot")
+    _fields = ("start", "radius", "rotation", "arc", "sweep", "end")
+
+    def __init__(self, start, radius, rotation, arc, sweep, end):
+        self.start = start
+        self.radius = radius
+        self.rotation = rotation
+        self.arc = bool(arc)
+        self.sweep = bool(sweep)
+        self.end = end
+        self._to_center()
+
+    def _to_center(self):
+        phi = math.radians(self.rotation)
+        rot = complex(math.cos(phi), math.sin(phi))
+        # half chord in the ellipse-aligned frame
+        hc = (complex(self.start) - complex(self.end)) / 2.0 / rot
+        x1, y1 = hc.real, hc.imag
+        rx, ry = abs(self.radius.real), abs(self.radius.imag)
+        lam = (x1 * x1) / (rx * rx) + (y1 * y1) / (ry * ry)
+        if lam > 1.0:
+            s = math.sqrt(lam)
+            rx *= s
+            ry *= s
+        num = rx * rx * ry * ry - rx * rx * y1 * y1 - ry * ry * x1 * x1
+        den = rx * rx * y1 * y1 + ry * ry * x1 * x1
+        coef = math.sqrt(abs(num / den)) if den != 0 else 0.0
+        if self.arc == self.sweep:
+            coef = -coef
+        cpx = coef * rx * y1 / ry
+        cpy = -coef * ry * x1 / rx
+        mid = (complex(self.start) + complex(self.end)) / 2.0
+        self.center = complex(cpx, cpy) * rot + mid
+        # unit-circle vectors from center to start / end
+        u = complex((x1 - cpx) / rx, (y1 - cpy) / ry)
+        v = complex((-x1 - cpx) / rx, (-y1 - cpy) / ry)
+        theta = math.degrees(math.atan2(u.imag, u.real))
+        self.theta = theta % 360.0
+        cross = u.real * v.imag - u.imag * v.real
+        dot = u.real * v.real + u.imag * v.imag
+        nuv = abs(u) * abs(v)
+        cosd = max(-1.0, min(1.0, dot / nuv)) if nuv else 0.0
+        delta = math.degrees(math.acos(cosd))
+        if cross < 0:
+            delta = -delta
+        delta %= 360.0
+        if not self.sweep:
+            delta -= 360.0
+        self.delta = delta
+        # out-of-range radii are scaled up (F.6.6); points use the corrected radii
+        self._rx, self._ry, self._rot = rx, ry, rot
+
+    def point(self, pos: float) -> complex:
+        ang = math.radians(self.theta + self.delta * pos)
+        local = complex(math.cos(ang) * self._rx, math.sin(ang) * self._ry)
+        return local * self._rot + self.center
+
+    def derivative(self, t: float) -> complex:
+        ang = math.radians(self.theta + self.delta * t)
+        dang = math.radians(self.delta)
+        local = complex(-math.sin(ang) * self._rx, math.cos(ang) * self._ry) * dang
+        return local * self._rot
+
+
+class Path(MutableSequence):
+    """An ordered, mutable collection of segments with arc-length addressing."""
+
+    _closed = False
+
+    def __init__(self, *segments, **kw):
+        self._segments: List[_Segment] = list(segments)
+        self._cum: Optional[List[float]] = None
+        self._total: Optional[float] = None
+        if "closed" in kw:
+            self.closed = kw["closed"]
+
+    # --- MutableSequence protocol ------------------------------------------------
+    def __getitem__(self, index):
+        return self._segments[index]
+
+    def __setitem__(self, index, value):
+        self._segments[index] = value
+        self._total = None
+
+    def __delitem__(self, index):
+        del self._segments[index]
+        self._total = None
+
+    def insert(self, index, value):
+        self._segments.insert(index, value)
+        self._total = None
+
+    def __len__(self):
+        return len(self._segments)
+
+    def __iter__(self) -> Iterator[_Segment]:
+        return iter(self._segments)
+
+    def reverse(self):
+        raise NotImplementedError("reversing a path would require reversing every segment")
+
+    def __repr__(self):
+        return "Path(%s, closed=%s)" % (", ".join(repr(s) for s in self._segments), self.closed)
+
+    def __eq__(self, other):
+        if not isinstance(other, Path):
+            return NotImplemented
+        return len(self) == len(other) and all(a == b for a, b in zip(self._segments, other._segments))
+
+    def __ne__(self, other):
+        r = self.__eq__(other)
+        return r if r is NotImplemented else not r
+
+    __hash__ = None
+
+    # --- geometry ---------------------------------------------------------------
+    def _lengths(self, error=None, min_depth=None):
+        if self._total is None:
+            lens = [s.length(error, min_depth) for s in self._segments]
+            total = sum(lens)
+            cum, acc = [], 0.0
+            for ln in lens:
+                acc += ln / total
+                cum.append(acc)
+            self._total, self._cum = total, cum
+        return self._total, self._cum
+
+    def length(self, error=None, min_depth=None) -> float:
+        return self._lengths(error, min_depth)[0]
+
+    def point(self, pos: float, error=None) -> complex:
+        if pos == 0.0:
+            return self._segments[0].point(0.0)
+        if pos == 1.0:
+            return self._segments[-1].point(1.0)
+        _, cum = self._lengths(error)
+        lo = 0.0
+        for seg, hi in zip(self._segments, cum):
+            if hi >= pos:
+                return seg.point((pos - lo) / (hi - lo))
+            lo = hi
+        return self._segments[-1].point(1.0)
+
+    # --- closure ------------------------------------------------------------------
+    def _is_closable(self) -> bool:
+        end = self._segments[-1].end
+        return any(s.start == end for s in self._segments)
+
+    @property
+    def closed(self) -> bool:
+        return bool(self._closed) and self._is_closable()
+
+    @closed.setter
+    def closed(self, value):
+        value = bool(value)
+        if value and not self._is_closable():
+            raise ValueError("End does not coincide with a segment start.")
+        self._closed = value
+
+    # --- serialization -------------------------------------------------------------
+    def d(self) -> str:
+        closed = self.closed
+        segs = self._segments[:-1] if closed else self._segments
+        end = self._segments[-1].end
+        out: List[str] = []
+        cur = None
+        prev = None
+        for seg in segs:
+            if cur != seg.start or (closed and seg.start == end):
+                out.append("M " + _pt(seg.start))
+            if isinstance(seg, Line):
+                out.append("L " + _pt(seg.end))
+            elif isinstance(seg, CubicBezier):
+                if seg.is_smooth_from(prev):
+                    out.append("S %s %s" % (_pt(seg.control2), _pt(seg.end)))
+                else:
+                    out.append("C %s %s %s" % (_pt(seg.control1), _pt(seg.control2), _pt(seg.end)))
+            elif isinstance(seg, QuadraticBezier):
+                if seg.is_smooth_from(prev):
+                    out.append("T " + _pt(seg.end))
+                else:
+                    out.append("Q %s %s" % (_pt(seg.control), _pt(seg.end)))
+            elif isinstance(seg, Arc):
+                out.append("A %s,%s %s %d,%d %s" % (_fmt(seg.radius.real), _fmt(seg.radius.imag),
+                                                     _fmt(seg.rotation), int(seg.arc), int(seg.sweep),
+                                                     _pt(seg.end)))
+            cur = seg.end
+            prev = seg
+        if closed:
+            out.append("Z")
+        return " ".join(out)
+
+
+# ----------------------------------------------------------------------------
+# parser
+# ----------------------------------------------------------------------------
+_TOKEN = re.compile(r"([MmZzLlHhVvCcSsQqTtAa])|([-+]?(?:[0-9]*\.?[0-9]+)(?:[eE][-+]?[0-9]+)?)")
+_ARITY = {"M": 2, "L": 2, "H": 1, "V": 1, "C": 6, "S": 4, "Q": 4, "T": 2, "A": 7, "Z": 0}
+
+
+def _tokens(d: str):
+    for m in _TOKEN.finditer(d):
+        if m.group(1):
+            yield m.group(1)
+        else:
+            yield float(m.group(2))
+
+
+def parse_path(pathdef: str, current_pos: complex = 0j) -> Path:
+    """Parse SVG path data into a :class:`Path`.
+
+    The first moveto is relative to ``current_pos`` (default origin) when
+    given in lower case, matching ``svg/path/parser.py:21-27``.
+    """
+    toks = list(_tokens(pathdef))
+    n = len(toks)
+    i = 0
+    path = Path()
+    cmd: Optional[str] = None
+    last_cmd: Optional[str] = None
+    absolute = True
+    start_pos: Optional[complex] = None
+    pos = complex(current_pos)
+
+    def take(k):
+        nonlocal i
+        vals = toks[i:i + k]
+        if len(vals) < k or any(isinstance(v, str) for v in vals):
+            raise ValueError("truncated arguments in path data %r" % pathdef)
+        i += k
+        return vals
+
+    while i < n:
+        t = toks[i]
+        if isinstance(t, str):
+            last_cmd = cmd
+            i += 1
+            absolute = t.isupper()
+            cmd = t.upper()
+        elif cmd is None:
+            raise ValueError("Unallowed implicit command in %s, position %d" % (pathdef, i))
+
+        if cmd == "M":
+            x, y = take(2)
+            p = complex(x, y)
+            pos = p if absolute else pos + p
+            start_pos = pos
+            cmd = "L"  # implicit repeats after a moveto are linetos
+        elif cmd == "Z":
+            path.append(Line(pos, start_pos))
+            path.closed = True
+            pos = start_pos
+            start_pos = None
+            cmd = None
+        elif cmd == "L":
+            x, y = take(2)
+            p = complex(x, y) if absolute else pos + complex(x, y)
+            path.append(Line(pos, p))
+            pos = p
+        elif cmd == "H":
+            (x,) = take(1)
+            p = complex(x if absolute else pos.real + x, pos.imag)
+            path.append(Line(pos, p))
+            pos = p
+        elif cmd == "V":
+            (y,) = take(1)
+            p = complex(pos.real, y if absolute else pos.imag + y)
+            path.append(Line(pos, p))
+            pos = p
+        elif cmd == "C":
+            a = take(6)
+            c1, c2, e = complex(a[0], a[1]), complex(a[2], a[3]), complex(a[4], a[5])
+            if not absolute:
+                c1, c2, e = c1 + pos, c2 + pos, e + pos
+            path.append(CubicBezier(pos, c1, c2, e))
+            pos = e
+        elif cmd == "S":
+            a = take(4)
+            if last_cmd in ("C", "S"):
+                c1 = 2 * pos - path[-1].control2
+            else:
+                c1 = pos
+            c2, e = complex(a[0], a[1]), complex(a[2], a[3])
+            if not absolute:
+                c2, e = c2 + pos, e + pos
+            path.append(CubicBezier(pos, c1, c2, e))
+            pos = e
+        elif cmd == "Q":
+            a = take(4)
+            c, e = complex(a[0], a[1]), complex(a[2], a[3])
+            if not absolute:
+                c, e = c + pos, e + pos
+            path.append(QuadraticBezier(pos, c, e))
+            pos = e
+        elif cmd == "T":
+            a = take(2)
+            if last_cmd in ("Q", "T"):
+                c = 2 * pos - path[-1].control
+            else:
+                c = pos
+            e = complex(a[0], a[1])
+            if not absolute:
+                e = e + pos
+            path.append(QuadraticBezier(pos, c, e))
+            pos = e
+        elif cmd == "A":
+            a = take(7)
+            e = complex(a[5], a[6])
+            if not absolute:
+                e = e + pos
+            path.append(Arc(pos, complex(a[0], a[1]), a[2], a[3], a[4], e))
+            pos = e
+        # S/T reflection looks at the command that produced the previous segment
+        if cmd is not None and i < n and not isinstance(toks[i], str):
+            last_cmd = cmd
+    return path

@@ -1,0 +1,114 @@
+"""The reference model: unconditional decoder-only MDN-RNN.
+
+Behaviour of ``model.py:7-184`` (reference capabilities R7-R12):
+
+* ``num_layers`` stacked cells of ``rnn_size`` (``lstm`` | ``gru`` | ``rnn``);
+* dropout (``keep_prob``) on the top-layer output in training only
+  (``DropoutWrapper(output_keep_prob)`` around the whole stack);
+* after consuming an input whose ``eoc`` flag is set, every layer's carried
+  state is reset to the *batch-initial* state (``model.py:82-92``) -- for
+  any number of layers (the reference hard-codes two);
+* ``xw_plus_b`` output projection to ``3 + 6M`` MDN parameters;
+* reference-mode MDN loss (:mod:`.mdn`).
+
+Execution is layer-by-layer: each layer's input projection is one hoisted
+GEMM over all ``T*B`` rows and only the recurrent part runs step by step
+(``ops.lstm_sequence``: fused HIP recurrence on the GPU).
+Inference mode (``infer=True``) is the single-step decoder used by the
+sampler (``model.py:9-11``).
+"""
+from __future__ import annotations
+
+from typing import List, Optional, Tuple
+
+import torch
+import torch.nn as nn
+
+from .. import ops
+from ..config import RefConfig
+from . import cells as C
+
+
+class SketchRNN(nn.Module):
+    def __init__(self, cfg: RefConfig, seed: Optional[int] = None):
+        super().__init__()
+        self.cfg = cfg
+        gen = torch.Generator().manual_seed(cfg.seed if seed is None else seed)
+        H = cfg.rnn_size
+        layers = []
+        for l in range(cfg.num_layers):
+            in_size = 5 if l == 0 else H
+            if cfg.model == "lstm":
+                layers.append(C.LSTMParams(in_size, H, gen=gen))
+            elif cfg.model == "gru":
+                layers.append(C.GRUParams(in_size, H, gen=gen))
+            elif cfg.model == "rnn":
+                layers.append(C.RNNParams(in_size, H, gen=gen))
+            else:
+                raise ValueError("model type not supported: %s" % cfg.model)
+        self.layers = nn.ModuleList(layers)
+        self.output_w = nn.Parameter(C.uniform_(torch.empty(H, cfg.n_out), gen))
+        self.output_b = nn.Parameter(torch.zeros(cfg.n_out))
+
+    # -- state --------------------------------------------------------------------
+    def zero_state(self, batch_size: int, device=None) -> List:
+        H = self.cfg.rnn_size
+        z = lambda: torch.zeros(batch_size, H, device=device)
+        return [(z(), z()) if self.cfg.model == "lstm" else z() for _ in self.layers]
+
+    @staticmethod
+    def detach_state(state):
+        return [tuple(s.detach() for s in st) if isinstance(st, tuple) else st.detach() for st in state]
+
+    # -- forward --------------------------------------------------------------------
+    def forward(self, x: torch.Tensor, state: Optional[List] = None, train: bool = True,
+                drop_seed: int = 0, reset_on_eoc: bool = True):
+        """``x [B, T, 5]`` (reference layout). Returns ``(z [T*B, NOUT], final_state)``
+        with rows in time-major order."""
+        cfg = self.cfg
+        B, T, _ = x.shape
+        if state is None:
+            state = self.zero_state(B, x.device)
+        xt = x.transpose(0, 1).contiguous()            # [T, B, 5]
+        reset = (xt[:, :, 3] > 0).to(torch.float32) if reset_on_eoc else None
+        inp = xt
+        final = []
+        for l, p in enumerate(self.layers):
+            if cfg.model == "lstm":
+                h0, c0 = state[l]
+                xp = torch.addmm(p.bias, inp.reshape(T * B, -1), p.W_x).view(T, B, -1)
+                out, (hT, cT) = ops.lstm_sequence(xp, p.W_h, h0, c0, forget_bias=1.0, reset=reset,
+                                                  reset_h=h0, reset_c=c0)
+                final.append((hT, cT))
+            elif cfg.model == "gru":
+                out, hT = ops.gru_sequence(p, inp, state[l], reset=reset, reset_h=state[l])
+                final.append(hT)
+            else:
+                out, hT = ops.rnn_sequence(p, inp, state[l], reset=reset, reset_h=state[l])
+                final.append(hT)
+            inp = out
+        out = inp.reshape(T * B, -1)
+        if train and cfg.keep_prob < 1.0:
+            out = out * C.dropout_mask(drop_seed, 7, 0, out.shape, cfg.keep_prob, out.device)
+        z = torch.addmm(self.output_b, out, self.output_w)
+        return z, final
+
+    def loss(self, x: torch.Tensor, y: torch.Tensor, state=None, train: bool = True, drop_seed: int = 0):
+        """Reference cost: ``(cost, cost_shape, cost_pen, final_state)``."""
+        z, final = self.forward(x, state, train=train, drop_seed=drop_seed)
+        tgt = y.transpose(0, 1).reshape(-1, 5)
+        cost, shape, pen = ops.mdn_loss(z, tgt, self.cfg.num_mixture, mode="reference",
+                                        stroke_importance=self.cfg.stroke_importance_factor,
+                                        clamp=self.cfg.loss_clamp)
+        return cost, shape, pen, final
+
+    # -- single step (sampling) --------------------------------------------------------
+    @torch.no_grad()
+    def step(self, x: torch.Tensor, state: List) -> Tuple[torch.Tensor, List]:
+        """One decoder step at ``B`` rows: ``x [B, 5]`` -> ``z [B, NOUT]``.
+
+        Applies the reference's T=1 eoc semantics: if the fed input has
+        ``eoc`` set, the returned carried state is the fed-in state
+        (``model.py:91`` with ``initial_state`` = the fed state)."""
+        z, final = self.forward(x.unsqueeze(1), state, train=False)
+        return z, final

@@ -1,0 +1,94 @@
+"""Op dispatch: fused HIP kernels on the GPU, PyTorch oracle on the CPU.
+
+Backend policy (``set_backend``):
+
+* ``"auto"`` (default) -- tensors on a HIP device use the native kernels in
+  ``libskrnn_hip.so``; if that library is missing on a GPU run this raises
+  (no silent eager fallback); CPU tensors use the PyTorch oracle.
+* ``"hip"`` -- force native (error on CPU tensors).
+* ``"torch"`` -- force the PyTorch implementation everywhere (used by the
+  numerics tests and by the eager comparator in ``bench.py --backend torch``).
+"""
+from __future__ import annotations
+
+import torch
+
+from .recurrent_torch import (gru_sequence_torch, hyper_sequence_torch, lstm_sequence_torch,
+                              rnn_sequence_torch)
+
+_BACKEND = "auto"
+_COMPUTE_DTYPE = "fp32"   # operand precision of the recurrent / head GEMMs on the GPU
+
+
+def set_compute_dtype(name: str) -> None:
+    """``fp32`` | ``bf16`` | ``fp8``: operand precision of the GPU GEMMs.
+    Accumulation, cell state and all pointwise math stay fp32."""
+    global _COMPUTE_DTYPE
+    if name not in ("fp32", "bf16", "fp8"):
+        raise ValueError(name)
+    _COMPUTE_DTYPE = name
+
+
+def get_compute_dtype() -> str:
+    return _COMPUTE_DTYPE
+
+
+def set_backend(name: str) -> None:
+    global _BACKEND
+    if name not in ("auto", "hip", "torch"):
+        raise ValueError(name)
+    _BACKEND = name
+
+
+def get_backend() -> str:
+    return _BACKEND
+
+
+def use_hip(t: torch.Tensor) -> bool:
+    if _BACKEND == "torch":
+        return False
+    if not t.is_cuda:
+        if _BACKEND == "hip":
+            raise RuntimeError("backend 'hip' requested for a CPU tensor")
+        return False
+    from ..utils import native
+    native.require_hip()  # raises loudly when the extension is missing
+    return True
+
+
+def lstm_sequence(xp, W_h, h0, c0, forget_bias: float = 1.0, reset=None, reset_h=None, reset_c=None,
+                  drop_keep: float = 1.0, drop_seed: int = 0, drop_stream: int = 0, ln=None):
+    if use_hip(xp):
+        from .recurrent import lstm_sequence_hip
+        return lstm_sequence_hip(xp, W_h, h0, c0, forget_bias, reset, reset_h, reset_c,
+                                 drop_keep, drop_seed, drop_stream, ln)
+    return lstm_sequence_torch(xp, W_h, h0, c0, forget_bias, reset, reset_h, reset_c,
+                               drop_keep, drop_seed, drop_stream, ln)
+
+
+def hyper_sequence(p, x, h0, c0, hh0, hc0, forget_bias: float = 1.0, drop_keep: float = 1.0,
+                   drop_seed: int = 0, drop_stream: int = 0, hyp_drop_keep: float = 1.0):
+    if use_hip(x):
+        from .recurrent import hyper_sequence_hip
+        return hyper_sequence_hip(p, x, h0, c0, hh0, hc0, forget_bias, drop_keep, drop_seed,
+                                  drop_stream, hyp_drop_keep)
+    return hyper_sequence_torch(p, x, h0, c0, hh0, hc0, forget_bias, drop_keep, drop_seed,
+                                drop_stream, hyp_drop_keep)
+
+
+def gru_sequence(p, x, h0, reset=None, reset_h=None):
+    return gru_sequence_torch(p, x, h0, reset, reset_h)
+
+
+def rnn_sequence(p, x, h0, reset=None, reset_h=None):
+    return rnn_sequence_torch(p, x, h0, reset, reset_h)
+
+
+def mdn_loss(z, target, M: int, mode: str = "magenta", stroke_importance: float = 200.0,
+             is_training: bool = True, clamp: float = 1e-20, eps: float = 1e-6):
+    """``(total, shape_term, pen_term)`` means over rows (see models.mdn)."""
+    if use_hip(z):
+        from .mdn_hip import mdn_loss_hip
+        return mdn_loss_hip(z, target, M, mode, stroke_importance, is_training, clamp, eps)
+    from ..models.mdn import mdn_loss_torch
+    return mdn_loss_torch(z, target, M, mode, stroke_importance, is_training, clamp, eps)

@@ -1,0 +1,53 @@
+"""HIP-graph capture of a whole training step (forward + backward + optimizer).
+
+On MI355X a recurrent training step is thousands of small dependent kernels
+(per time step: recurrent GEMM + fused cell kernel, forward and reverse).
+Replaying them from one captured ``hipGraph`` removes the per-launch host
+cost and the inter-kernel host gaps; this is the framework's replacement
+for a tracing compiler.
+
+Contract for a capturable step function ``fn(**static)``:
+* reads only from the static input tensors (refreshed by ``copy_`` before
+  each replay) and from device-resident state (weights, optimizer arena,
+  the dropout seed tensor, the lr scalar);
+* performs no host synchronisation and no allocation that depends on data.
+
+Warm-up runs needed before capture mutate the training state, so
+:class:`GraphedStep` snapshots the optimizer arena (weights, moments,
+scalars) and restores it after capture.
+"""
+from __future__ import annotations
+
+from typing import Callable, Dict, Optional
+
+import torch
+
+
+class GraphedStep:
+    def __init__(self, fn: Callable[..., Dict[str, torch.Tensor]], static_inputs: Dict[str, torch.Tensor],
+                 warmup: int = 2, snapshot: Optional[list] = None):
+        self.fn = fn
+        self.static = static_inputs
+        saved = [t.detach().clone() for t in (snapshot or [])]
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            for _ in range(max(1, warmup)):
+                fn(**self.static)
+        torch.cuda.current_stream().wait_stream(side)
+        torch.cuda.synchronize()
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph):
+            self.outputs = fn(**self.static)
+        torch.cuda.synchronize()
+        with torch.no_grad():
+            for t, s in zip(snapshot or [], saved):
+                t.copy_(s)
+
+    def __call__(self, **inputs) -> Dict[str, torch.Tensor]:
+        for k, v in inputs.items():
+            dst = self.static[k]
+            if v.data_ptr() != dst.data_ptr():
+                dst.copy_(v, non_blocking=True)
+        self.graph.replay()
+        return self.outputs

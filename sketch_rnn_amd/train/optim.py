@@ -1,0 +1,120 @@
+"""Flat-arena Adam with gradient clipping (reference capability R13).
+
+All trainable parameters live as views into ONE contiguous fp32 buffer and
+their gradients as views into ONE contiguous fp32 gradient buffer
+("arena"). That layout gives:
+
+* a single fused HIP kernel for clip + Adam over every parameter
+  (``csrc/optim.hip``) instead of one launch per tensor;
+* a single (bucketed) RCCL all-reduce for data parallelism
+  (:mod:`sketch_rnn_amd.parallel.dp`);
+* graph-capture safety: no allocation in the step; ``lr`` and the Adam
+  step count live in a device scalar block that the host updates before
+  each replay.
+
+Update rule is TF's ``AdamOptimizer`` (``model.py:183``): ``epsilon`` is
+added to ``sqrt(v)`` and the bias corrections are folded into the step
+size, ``lr_t = lr * sqrt(1 - b2^t) / (1 - b1^t)``.
+
+Clipping modes:
+* ``"global_norm"`` -- ``tf.clip_by_global_norm`` (reference, ``model.py:182``);
+* ``"value"`` -- per-element ``clip_by_value`` (sketch-rnn VAE).
+"""
+from __future__ import annotations
+
+import math
+from typing import Iterable, List, Optional
+
+import torch
+
+
+class FlatAdam:
+    def __init__(self, params: Iterable[torch.nn.Parameter], lr: float = 1e-3, betas=(0.9, 0.999),
+                 eps: float = 1e-8, clip_mode: Optional[str] = None, clip: float = 0.0,
+                 align: int = 64):
+        self.params: List[torch.nn.Parameter] = [p for p in params if p.requires_grad]
+        self.b1, self.b2 = betas
+        self.eps = eps
+        self.clip_mode = clip_mode
+        self.clip = float(clip)
+        dev = self.params[0].device
+        # 256-byte aligned slots per tensor: vector loads never straddle tensors
+        self.offsets, off = [], 0
+        for p in self.params:
+            self.offsets.append(off)
+            off += (p.numel() + align - 1) // align * align
+        self.numel = off
+        self.flat = torch.zeros(off, device=dev, dtype=torch.float32)
+        self.grad = torch.zeros(off, device=dev, dtype=torch.float32)
+        self.m = torch.zeros(off, device=dev, dtype=torch.float32)
+        self.v = torch.zeros(off, device=dev, dtype=torch.float32)
+        for p, o in zip(self.params, self.offsets):
+            n = p.numel()
+            self.flat[o:o + n].copy_(p.detach().reshape(-1))
+            p.data = self.flat[o:o + n].view_as(p)
+            p.grad = self.grad[o:o + n].view_as(p)
+        # device scalars: [lr, step, grad_norm, clip_scale]
+        self.scalars = torch.zeros(4, device=dev, dtype=torch.float32)
+        self.set_lr(lr)
+        self.step_count = 0
+
+    # ---------------------------------------------------------------------------------
+    def set_lr(self, lr: float) -> None:
+        self.lr = float(lr)
+        self.scalars[0].fill_(self.lr)
+
+    def zero_grad(self) -> None:
+        self.grad.zero_()
+
+    def named_slices(self):
+        for p, o in zip(self.params, self.offsets):
+            yield p, o, p.numel()
+
+    # ---------------------------------------------------------------------------------
+    def step(self) -> None:
+        """Clip + Adam. Capture-safe: the step count advances on device."""
+        from .. import ops
+        if ops.use_hip(self.flat):
+            from ..ops import optim_hip
+            optim_hip.flat_adam_step(self)
+        else:
+            self._step_torch()
+        self.step_count += 1
+
+    @torch.no_grad()
+    def _step_torch(self) -> None:
+        g = self.grad
+        sc = self.scalars
+        sc[1] += 1.0
+        if self.clip_mode == "global_norm":
+            norm = torch.sqrt((g.double() * g.double()).sum()).float()
+            sc[2] = norm
+            scale = self.clip / torch.clamp(norm, min=self.clip)
+            sc[3] = scale
+            g = g * scale
+        elif self.clip_mode == "value":
+            g = g.clamp(-self.clip, self.clip)
+        t = sc[1]
+        lr_t = sc[0] * torch.sqrt(1.0 - self.b2 ** t) / (1.0 - self.b1 ** t)
+        self.m.mul_(self.b1).add_(g, alpha=1.0 - self.b1)
+        self.v.mul_(self.b2).addcmul_(g, g, value=1.0 - self.b2)
+        self.flat.sub_(lr_t * self.m / (torch.sqrt(self.v) + self.eps))
+
+    # ---------------------------------------------------------------------------------
+    def state_dict(self):
+        return {"m": self.m, "v": self.v, "scalars": self.scalars, "step_count": self.step_count}
+
+    def load_state_dict(self, sd):
+        self.m.copy_(sd["m"])
+        self.v.copy_(sd["v"])
+        self.scalars.copy_(sd["scalars"])
+        self.step_count = int(sd["step_count"])
+        self.lr = float(self.scalars[0])
+
+
+def adam_reference_step(param, grad, m, v, t, lr, b1=0.9, b2=0.999, eps=1e-8):
+    """TF Adam on plain tensors (fp64 oracle for the fused kernel tests)."""
+    m = b1 * m + (1 - b1) * grad
+    v = b2 * v + (1 - b2) * grad * grad
+    lr_t = lr * math.sqrt(1 - b2 ** t) / (1 - b1 ** t)
+    return param - lr_t * m / (torch.sqrt(v) + eps), m, v

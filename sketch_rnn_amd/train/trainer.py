@@ -1,0 +1,280 @@
+"""Training drivers.
+
+* :class:`ReferenceTrainer` -- the reference's epoch loop (``train.py:47-97``):
+  per-epoch lr decay, reshuffle, zero state at epoch start, final state
+  carried into the next batch (TBPTT), progress line in the reference format,
+  divergence guard, periodic + final checkpoint, and (new) resume.
+* :class:`VAETrainer` -- step loop for the seq2seq VAE with lr decay, KL
+  annealing, per-element gradient clipping, periodic valid/test evaluation
+  (recon NLL) and checkpointing; data-parallel over RCCL when
+  ``torch.distributed`` is initialised.
+
+Both can capture their step into a HIP graph on the GPU (:mod:`.graph`).
+"""
+from __future__ import annotations
+
+import json
+import math
+import os
+import time
+from typing import Callable, Dict, Optional
+
+import numpy as np
+import torch
+
+from ..ckpt import checkpoint as ckpt
+from ..config import RefConfig, VAEConfig
+from ..models.reference import SketchRNN
+from ..models.vae import SketchVAE
+from ..parallel import dp
+from . import schedules
+from .graph import GraphedStep
+from .optim import FlatAdam
+
+
+class DivergenceError(RuntimeError):
+    pass
+
+
+def _to_device(a, device, dtype=torch.float32):
+    return torch.as_tensor(np.ascontiguousarray(a)).to(device=device, dtype=dtype, non_blocking=True)
+
+
+# =====================================================================================
+# reference decoder-only model
+# =====================================================================================
+class ReferenceTrainer:
+    def __init__(self, cfg: RefConfig, loader, device: str = "cpu", save_root: str = "save",
+                 use_graph: Optional[bool] = None, log: Callable[[str], None] = print,
+                 metrics_path: Optional[str] = None):
+        self.cfg = cfg
+        self.loader = loader
+        self.device = torch.device(device)
+        self.model = SketchRNN(cfg).to(self.device)
+        self.opt = FlatAdam(self.model.parameters(), lr=cfg.learning_rate, eps=cfg.adam_eps,
+                            clip_mode="global_norm", clip=cfg.grad_clip)
+        self.save_dir = os.path.join(save_root, cfg.dataset_name)
+        self.log = log
+        self.metrics_path = metrics_path
+        self.b_processed = 0
+        self.epoch = 0
+        self.use_graph = (self.device.type == "cuda") if use_graph is None else use_graph
+        self._graph = None
+        B = cfg.batch_size
+        self.state = self.model.zero_state(B, self.device)
+        self.seed = torch.zeros(1, dtype=torch.int64, device=self.device)
+
+    # ---------------------------------------------------------------------------------
+    def _step_fn(self, x, y, state_flat):
+        state = self._unflatten(state_flat)
+        self.opt.zero_grad()
+        cost, shape, pen, final = self.model.loss(x, y, state, train=True, drop_seed=self.seed)
+        cost.backward()
+        self.opt.step()
+        with torch.no_grad():
+            for dst, src in zip(state_flat, self._flatten(final)):
+                dst.copy_(src)
+        return {"cost": cost.detach(), "shape": shape.detach(), "pen": pen.detach()}
+
+    def _flatten(self, state):
+        out = []
+        for s in state:
+            out.extend(s if isinstance(s, tuple) else (s,))
+        return out
+
+    def _unflatten(self, flat):
+        if self.cfg.model == "lstm":
+            return [(flat[2 * i], flat[2 * i + 1]) for i in range(len(flat) // 2)]
+        return list(flat)
+
+    def train_step(self, x: torch.Tensor, y: torch.Tensor) -> Dict[str, torch.Tensor]:
+        state_flat = self._flatten(self.state)
+        if self.use_graph:
+            if self._graph is None:
+                static = {"x": x.clone(), "y": y.clone()}
+                snap = [self.opt.flat, self.opt.m, self.opt.v, self.opt.scalars] + \
+                       [s for s in state_flat]
+                self._graph = GraphedStep(lambda x, y: self._step_fn(x, y, state_flat), static,
+                                          snapshot=snap)
+            out = self._graph(x=x, y=y)
+        else:
+            out = self._step_fn(x, y, state_flat)
+        self.opt.step_count = int(self.opt.step_count)  # host mirror (device counter is authoritative)
+        self.seed.add_(1)
+        return out
+
+    # ---------------------------------------------------------------------------------
+    def save(self):
+        st = {"s%d" % i: t for i, t in enumerate(self._flatten(self.state))}
+        extra = {"epoch": self.epoch, "b_processed": self.b_processed,
+                 "pointer": int(self.loader.pointer), "rng": self.loader.rng.get_state()[1].tolist()[:4]}
+        path = ckpt.save_checkpoint(self.save_dir, self.b_processed, self.model, self.opt, self.cfg,
+                                    extra=extra, state=st)
+        self.log("model saved to {}".format(path))
+        return path
+
+    def resume(self) -> bool:
+        path = ckpt.latest_checkpoint(self.save_dir)
+        if path is None:
+            return False
+        step, extra, st = ckpt.load_checkpoint(path, self.model, self.opt)
+        self.b_processed = int(extra.get("b_processed", step))
+        self.epoch = int(extra.get("epoch", 0))
+        for i, t in enumerate(self._flatten(self.state)):
+            if "s%d" % i in st:
+                t.copy_(st["s%d" % i])
+        self.log("resumed from %s (epoch %d, batch %d)" % (path, self.epoch, self.b_processed))
+        return True
+
+    def train(self, num_epochs: Optional[int] = None, max_batches: Optional[int] = None):
+        cfg, loader = self.cfg, self.loader
+        num_epochs = cfg.num_epochs if num_epochs is None else num_epochs
+        done = 0
+        for e in range(self.epoch, num_epochs):
+            self.epoch = e
+            self.opt.set_lr(schedules.reference_lr(cfg, e))
+            loader.reset_index_pointer()
+            for s in self._flatten(self.state):
+                s.zero_()
+            while not loader.epoch_finished:
+                t0 = time.time()
+                x, y = loader.next_batch()
+                out = self.train_step(_to_device(x, self.device), _to_device(y, self.device))
+                cost, shape, pen = (float(out[k]) for k in ("cost", "shape", "pen"))
+                dt = time.time() - t0
+                self.b_processed += 1
+                self.log("{}/{} (epoch {} batch {}), cost = {:.2f} ({:.2f}+{:.4f}), time/batch = {:.2f}".format(
+                    loader.pointer + e * loader.num_samples, num_epochs * loader.num_samples,
+                    e, self.b_processed, cost, shape, pen, dt))
+                self._metrics({"step": self.b_processed, "epoch": e, "cost": cost, "shape": shape,
+                               "pen": pen, "time": dt, "lr": self.opt.lr,
+                               "strokes_per_s": cfg.batch_size * cfg.seq_length / max(dt, 1e-9)})
+                if not (cost < cfg.divergence_bound):  # NaN fails this too (train.py:93-94)
+                    raise DivergenceError("training diverged: cost=%r" % cost)
+                if self.b_processed % cfg.save_every == 0 and self.b_processed > 0:
+                    self.save()
+                done += 1
+                if max_batches is not None and done >= max_batches:
+                    return self.save()
+        return self.save()
+
+    def _metrics(self, rec):
+        if self.metrics_path:
+            with open(self.metrics_path, "a") as f:
+                f.write(json.dumps(rec) + "\n")
+
+
+# =====================================================================================
+# seq2seq VAE
+# =====================================================================================
+class VAETrainer:
+    def __init__(self, cfg: VAEConfig, train_set, valid_set=None, test_set=None, device: str = "cpu",
+                 save_dir: str = "save/vae", use_graph: Optional[bool] = None,
+                 log: Callable[[str], None] = print, metrics_path: Optional[str] = None,
+                 compute_dtype: str = "fp32"):
+        self.cfg = cfg
+        self.train_set, self.valid_set, self.test_set = train_set, valid_set, test_set
+        self.device = torch.device(device)
+        self.rank, self.world = dp.rank(), dp.world_size()
+        self.model = SketchVAE(cfg).to(self.device)
+        from .. import ops
+        ops.set_compute_dtype(compute_dtype)
+        self.opt = FlatAdam(self.model.parameters(), lr=cfg.learning_rate, eps=cfg.adam_eps,
+                            clip_mode="value", clip=cfg.grad_clip)
+        dp.broadcast_params(self.opt.flat)
+        self.reducer = dp.GradReducer(self.opt.grad) if self.world > 1 else None
+        self.save_dir = save_dir
+        self.log = log
+        self.metrics_path = metrics_path
+        self.step = 0
+        self.use_graph = (self.device.type == "cuda") if use_graph is None else use_graph
+        self._graph = None
+        self.seed = torch.zeros(1, dtype=torch.int64, device=self.device)
+        self.kl_w = torch.zeros((), device=self.device)
+
+    def _step_fn(self, strokes, lengths, labels):
+        self.opt.zero_grad()
+        out = self.model.loss(strokes, lengths, labels if self.cfg.num_classes > 0 else None,
+                              kl_weight=self.kl_w, train=True, seed=self.seed)
+        out["cost"].backward()
+        if self.reducer is not None:
+            self.reducer.all_reduce()
+        self.opt.step()
+        return {k: v.detach() for k, v in out.items()}
+
+    def train_step(self, strokes, lengths, labels):
+        self.opt.set_lr(schedules.vae_lr(self.cfg, self.step))
+        self.kl_w.fill_(schedules.kl_weight(self.cfg, self.step))
+        if self.use_graph and self.reducer is None:
+            if self._graph is None:
+                static = {"strokes": strokes.clone(), "lengths": lengths.clone(), "labels": labels.clone()}
+                snap = [self.opt.flat, self.opt.m, self.opt.v, self.opt.scalars]
+                self._graph = GraphedStep(self._step_fn, static, snapshot=snap)
+            out = self._graph(strokes=strokes, lengths=lengths, labels=labels)
+        else:
+            out = self._step_fn(strokes, lengths, labels)
+        self.seed.add_(1)
+        self.step += 1
+        return out
+
+    def batch_to_device(self, batch):
+        s, l, c = batch
+        return (_to_device(s, self.device), _to_device(l, self.device, torch.int64),
+                _to_device(c, self.device, torch.int64))
+
+    @torch.no_grad()
+    def evaluate(self, dataset, max_batches: Optional[int] = None) -> Dict[str, float]:
+        """Mean cost / recon NLL / KL over the dataset (no dropout, fixed eps seed)."""
+        tot = {"cost": 0.0, "r_cost": 0.0, "kl_cost": 0.0}
+        n = dataset.num_batches if max_batches is None else min(max_batches, dataset.num_batches)
+        gen = torch.Generator(device=self.device).manual_seed(1234)
+        for b in range(n):
+            s, l, c = self.batch_to_device(dataset.get_batch(b))
+            eps = torch.randn(s.shape[0], self.cfg.z_size, device=self.device, generator=gen)
+            out = self.model.loss(s, l, c if self.cfg.num_classes > 0 else None,
+                                  kl_weight=self.cfg.kl_weight, train=False, eps=eps)
+            for k in tot:
+                tot[k] += float(out[k])
+        res = {k: v / max(n, 1) for k, v in tot.items()}
+        return dp.average_scalars(res)
+
+    def save(self):
+        if self.rank != 0:
+            return None
+        return ckpt.save_checkpoint(self.save_dir, self.step, self.model, self.opt, self.cfg,
+                                    extra={"step": self.step})
+
+    def resume(self) -> bool:
+        path = ckpt.latest_checkpoint(self.save_dir)
+        if path is None:
+            return False
+        self.step, _, _ = ckpt.load_checkpoint(path, self.model, self.opt)
+        return True
+
+    def train(self, num_steps: Optional[int] = None, eval_every: int = 0, log_every: int = 20):
+        cfg = self.cfg
+        num_steps = cfg.num_steps if num_steps is None else num_steps
+        t0 = time.time()
+        while self.step < num_steps:
+            batch = self.batch_to_device(self.train_set.random_batch(self.rank, self.world))
+            out = self.train_step(*batch)
+            if self.step % log_every == 0 or self.step == num_steps:
+                vals = {k: float(v) for k, v in out.items()}
+                dt = (time.time() - t0) / log_every
+                t0 = time.time()
+                if self.rank == 0:
+                    self.log("step: %d, lr: %.6f, klw: %0.4f, cost: %.4f, recon: %.4f, kl: %.4f, time/step: %.4f" % (
+                        self.step, self.opt.lr, schedules.kl_weight(cfg, self.step - 1), vals["cost"],
+                        vals["r_cost"], vals["kl_cost"], dt))
+                    if self.metrics_path:
+                        with open(self.metrics_path, "a") as f:
+                            f.write(json.dumps(dict(step=self.step, **vals, time=dt)) + "\n")
+                if not math.isfinite(vals["cost"]):
+                    raise DivergenceError("non-finite cost at step %d" % self.step)
+            if eval_every and self.step % eval_every == 0 and self.valid_set is not None:
+                ev = self.evaluate(self.valid_set)
+                if self.rank == 0:
+                    self.log("valid: cost %.4f recon %.4f kl %.4f" % (ev["cost"], ev["r_cost"], ev["kl_cost"]))
+            if cfg.save_every and self.step % cfg.save_every == 0:
+                self.save()
+        return self.save()
