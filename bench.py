@@ -1,0 +1,133 @@
+#!/usr/bin/env python3
+"""Headline benchmark: seq2seq-VAE training throughput (strokes/s, whole job).
+
+Config (BASELINE.json "large"): bidirectional-LSTM encoder 512, HyperLSTM
+decoder 2048 (hyper 256 / embed 32, LayerNorm), z = 128, M = 20 mixtures,
+batch 100 per GPU, Nmax = 250, KL annealing, recurrent dropout 0.9,
+per-element gradient clip 1.0, Adam. Synthetic stroke-3 sketches (no network
+in this environment) and random-init weights. Every step is a full training
+step (encoder + decoder forward, backward, all-reduce, clip + Adam) over all
+250 decoder positions (the pen-state loss covers every position in training
+mode, so all B*Nmax positions are training targets).
+
+Usage: ``python bench.py --gpus N --steps K --warmup W``; for N > 1 launch
+with ``torch.distributed.run`` (one rank per GPU, RCCL). Rank 0 prints one
+JSON line; ``value`` = global_batch * Nmax * K / max-over-ranks(seconds).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="vae_large")
+    ap.add_argument("--batch", type=int, default=100, help="per-GPU batch")
+    ap.add_argument("--seq-len", type=int, default=250)
+    ap.add_argument("--dtype", default="bf16", choices=["fp32", "bf16"])
+    ap.add_argument("--backend", default="auto", choices=["auto", "hip", "torch"])
+    ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--no-eval", action="store_true")
+    ap.add_argument("--sketches", type=int, default=2000)
+    args = ap.parse_args()
+
+    import torch
+    from sketch_rnn_amd import ops
+    from sketch_rnn_amd.config import PRESETS
+    from sketch_rnn_amd.data.dataset import StrokeDataset
+    from sketch_rnn_amd.data.synthetic import synthetic_corpus
+    from sketch_rnn_amd.parallel import dp
+    from sketch_rnn_amd.train.trainer import VAETrainer
+
+    world_env = int(os.environ.get("WORLD_SIZE", "1"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    device = "cuda:%d" % local_rank if torch.cuda.is_available() else "cpu"
+    if device.startswith("cuda"):
+        torch.cuda.set_device(local_rank)
+    if world_env > 1:
+        dp.init_from_env(device=device)
+    world, rank = dp.world_size(), dp.rank()
+    ops.set_backend(args.backend)
+
+    cfg = PRESETS[args.config].replace(batch_size=args.batch, max_seq_len=args.seq_len, save_every=0)
+    strokes, labels = synthetic_corpus(args.sketches, seed=1234, max_len=args.seq_len,
+                                       n_classes=max(cfg.num_classes, 1))
+    n_test = max(args.batch, len(strokes) // 10)
+    train = StrokeDataset(strokes[n_test:], args.batch, args.seq_len, random_scale_factor=cfg.random_scale_factor,
+                          augment_stroke_prob=cfg.augment_stroke_prob, labels=labels[n_test:], seed=7, rank=rank)
+    scale = train.normalize()
+    test = StrokeDataset(strokes[:n_test], args.batch, args.seq_len, labels=labels[:n_test], seed=8)
+    test.normalize(scale)
+
+    trainer = VAETrainer(cfg, train, None, test, device=device, save_dir="/tmp/skr_bench",
+                         use_graph=(not args.no_graph) and device.startswith("cuda"),
+                         log=lambda s: None, compute_dtype=args.dtype)
+    nparam = sum(p.numel() for p in trainer.model.parameters())
+
+    def batch():
+        return trainer.batch_to_device(train.random_batch(rank, world))
+
+    batches = [batch() for _ in range(4)]
+    sync = torch.cuda.synchronize if device.startswith("cuda") else (lambda: None)
+    for i in range(args.warmup):
+        trainer.train_step(*batches[i % len(batches)])
+    sync()
+    dp.barrier()
+    sync()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        out = trainer.train_step(*batches[i % len(batches)])
+    sync()
+    dp.barrier()
+    sync()
+    elapsed = time.perf_counter() - t0
+    elapsed = dp.max_scalar(elapsed)
+    cost = float(out["cost"])
+    recon = None
+    if not args.no_eval:
+        ev = trainer.evaluate(test, max_batches=1)
+        recon = ev["r_cost"]
+    global_batch = args.batch * world
+    strokes_per_step = global_batch * args.seq_len
+    value = strokes_per_step * args.steps / elapsed
+    if rank == 0:
+        rec = {
+            "metric": "train strokes/sec (whole node) + test recon NLL, enc512/dec2048 QuickDraw",
+            "value": round(value, 1),
+            "unit": "strokes/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(1000.0 * elapsed / args.steps, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": args.dtype,
+            "data": "synthetic stroke-3 sketches (QuickDraw-like lengths, Nmax=%d), random-init weights" % args.seq_len,
+            "config": {
+                "model": "seq2seq-VAE %s: enc %d biLSTM / dec %d %s (hyper %d, emb %d), z %d, M=%d, %d params" % (
+                    args.config, cfg.enc_rnn_size, cfg.dec_rnn_size, cfg.dec_model, cfg.hyper_num_units,
+                    cfg.hyper_embedding_size, cfg.z_size, cfg.num_mixture, nparam),
+                "global_batch": global_batch,
+                "seq_len": args.seq_len,
+                "parallelism": "dp%d" % world,
+                "backend": ops.get_backend(),
+                "hip_graph": bool(trainer.use_graph),
+            },
+            "train_cost": round(cost, 4),
+            "test_recon_nll": None if recon is None else round(recon, 4),
+        }
+        print(json.dumps(rec), flush=True)
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,75 @@
+// Shared device helpers for the gfx950 (CDNA4, wave64) kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <hip/hip_bf16.h>
+#include <stdint.h>
+
+#define SKR_API extern "C" __attribute__((visibility("default")))
+
+namespace skr {
+
+constexpr int kWave = 64;  // CDNA wavefront width: never 32
+
+// ---------------------------------------------------------------------------
+// stateless dropout hash; bit-identical to sketch_rnn_amd/models/cells.py
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t mix32(uint32_t x) {
+    x ^= x >> 16;
+    x *= 0x7feb352du;
+    x ^= x >> 15;
+    x *= 0x846ca68bu;
+    x ^= x >> 16;
+    return x;
+}
+__device__ __forceinline__ uint32_t hash_key(int64_t seed, uint32_t stream, uint32_t step) {
+    uint32_t s = (uint32_t)(seed & 0xffffffffll);
+    return mix32(s * 0x9E3779B1u + stream * 0x85EBCA77u + step * 0xC2B2AE3Du);
+}
+__device__ __forceinline__ float hash_uniform(uint32_t key, uint32_t idx) {
+    uint32_t h = mix32(idx ^ key);
+    h = mix32(h + key);
+    return (float)(h >> 8) * (1.0f / 16777216.0f);
+}
+
+__device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + expf(-x)); }
+
+// ---------------------------------------------------------------------------
+// reductions (wave64 shuffles, then LDS across the block's waves)
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+    return v;
+}
+
+// Sums N values across a block of NW waves. `lds` must hold NW*N floats.
+template <int N, int NW>
+__device__ __forceinline__ void block_sum(float (&v)[N], float* lds) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+    for (int i = 0; i < N; ++i) v[i] = wave_sum(v[i]);
+    if (lane == 0) {
+#pragma unroll
+        for (int i = 0; i < N; ++i) lds[w * N + i] = v[i];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+        float s = 0.f;
+#pragma unroll
+        for (int k = 0; k < NW; ++k) s += lds[k * N + i];
+        v[i] = s;
+    }
+    __syncthreads();
+}
+
+__device__ __forceinline__ __hip_bfloat16 to_bf16(float x) { return __float2bfloat16(x); }
+
+}  // namespace skr
+
+#define SKR_CHECK_LAUNCH() (int)hipGetLastError()

@@ -1,0 +1,397 @@
+// Fused LSTM-family cell step (forward + backward) for gfx950.
+//
+// One workgroup (256 threads = 4 waves) owns one batch row; each thread owns
+// UPT = ceil(H / 256) hidden units and all four gates (i, j, f, o) of each.
+// Everything between the recurrent GEMM and the next step's GEMM is fused
+// into one launch per step:
+//
+//   g      = xp + R                              (plain / LN-LSTM)
+//          = xh*ax + R*ah + bh + bias            (HyperLSTM main cell, MOD)
+//   y      = LN_all(g)*gamma + beta              (LN: per gate block over H)
+//   c'     = c*sig(y_f + fb) + sig(y_i)*tanh(y_j)*mask
+//   h'     = tanh(LN(c')*gc + bc)*sig(y_o)  |  tanh(c')*sig(y_o)
+//   carry  = reset[b] ? init : (h', c')          (reference eoc reset)
+//
+// plus the saves the backward needs and a bf16 copy of the carried h written
+// straight into the next GEMM's A operand (which may be a column slice of a
+// concatenated [h | h_hyper] buffer, hence the explicit row stride).
+// The recurrent dropout mask is regenerated from a stateless hash of
+// (seed, stream, step, b*H + u) in both passes -- never stored.
+//
+// Reference semantics: model.py:19-23 (BasicLSTMCell), model.py:82-92 (eoc
+// reset); LayerNorm-/Hyper-LSTM semantics: sketch_rnn_amd/models/cells.py.
+#include "common.h"
+
+namespace {
+
+constexpr int kThreads = 256;
+constexpr int kWaves = kThreads / 64;
+constexpr float kLnEps = 1e-3f;
+
+struct FwdArgs {
+    int B, H;
+    const float* xp; int64_t ld_xp;    // [B, 4H]: x-projection (+bias unless MOD)
+    const float* R;  int64_t ld_R;     // [B, 4H]: h_prev @ W_h (fp32)
+    const float* vec; int64_t vec_gs;  // MOD: 12 blocks [B, H], block stride vec_gs
+    const float* bias;                 // MOD: [4H]
+    const float* c_prev;               // [B, H]
+    const float* ln_g; const float* ln_b; const float* lnc_g; const float* lnc_b;
+    const float* reset;                // [B] or null
+    const float* init_h; const float* init_c;
+    float forget_bias, keep;
+    const int64_t* seed; uint32_t stream, step;
+    float* h_out;                      // [B, H]
+    float* c_out;                      // [B, H]
+    float* act;                        // [B, 4H] sig(i), tanh(j), sig(f+fb), sig(o)
+    float* xhat;                       // LN: [B, 4H]
+    float* rstd;                       // LN: [B, 5]
+    float* chat;                       // LN: [B, H]
+    float* h_carry;                    // [B, H]
+    void* h_lp; int64_t ld_lp; int lp_kind;  // 0: none, 1: bf16, 2: fp32
+    float* c_carry;                    // [B, H]
+};
+
+struct BwdArgs {
+    int B, H;
+    const float* dh_out;               // [B, H] or null
+    const float* dh_rec;               // [B, H] (grad into carried h_t) or null
+    int64_t ld_dh_rec;
+    float* dc_rec;                     // [B, H] in: grad into carried c_t; out: into carried c_{t-1}
+    const float* act; const float* c_new; const float* c_prev;
+    const float* xhat; const float* rstd; const float* chat;
+    const float* ln_g; const float* lnc_g; const float* lnc_b;
+    const float* xp; int64_t ld_xp;    // MOD: xh
+    const float* R;  int64_t ld_R;     // MOD: R
+    const float* vec; int64_t vec_gs;  // MOD
+    const float* reset;
+    float keep; const int64_t* seed; uint32_t stream, step;
+    float* dG; int64_t ld_dG;          // non-MOD: d(preact) [B, 4H]; MOD: dR = dg*ah
+    void* dG_lp; int64_t ld_dG_lp; int dG_lp_kind;  // bf16 copy of dG for the next GEMM (1) or none (0)
+    float* dxp; int64_t ld_dxp;        // MOD: dxh = dg*ax
+    float* dvec;                       // MOD: 12 blocks [B, H] (block stride vec_gs)
+    float* dlny;                       // LN: [B, 4H] grad wrt LN-all output (for gamma/beta)
+    float* dlncy;                      // LN: [B, H]  grad wrt LN(c) output
+    float* dinit_h; float* dinit_c;    // [B, H] accumulated on reset rows (or null)
+};
+
+template <int UPT, bool LN, bool MOD>
+__global__ __launch_bounds__(kThreads) void lstm_fwd_kernel(const FwdArgs a) {
+    __shared__ float lds[kWaves * 8];
+    const int b = blockIdx.x, tid = threadIdx.x, H = a.H;
+    const bool keep_on = a.keep < 1.0f;
+    const uint32_t key = keep_on ? skr::hash_key(*a.seed, a.stream, a.step) : 0u;
+    float g[UPT][4];
+    bool act_u[UPT];
+#pragma unroll
+    for (int k = 0; k < UPT; ++k) {
+        const int u = tid + k * kThreads;
+        act_u[k] = u < H;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            float v = 0.f;
+            if (act_u[k]) {
+                const float xv = a.xp[b * a.ld_xp + q * H + u];
+                const float rv = a.R[b * a.ld_R + q * H + u];
+                if (MOD) {
+                    const int64_t o = (int64_t)b * H + u;
+                    v = xv * a.vec[q * a.vec_gs + o] + rv * a.vec[(4 + q) * a.vec_gs + o] +
+                        a.vec[(8 + q) * a.vec_gs + o] + a.bias[q * H + u];
+                } else {
+                    v = xv + rv;
+                }
+            }
+            g[k][q] = v;
+        }
+    }
+    if (LN) {
+        float mean[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            float s = 0.f;
+#pragma unroll
+            for (int k = 0; k < UPT; ++k) s += g[k][q];
+            mean[q] = s;
+        }
+        skr::block_sum<4, kWaves>(mean, lds);
+        float var[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            mean[q] /= (float)H;
+            float s = 0.f;
+#pragma unroll
+            for (int k = 0; k < UPT; ++k) {
+                const float d = act_u[k] ? g[k][q] - mean[q] : 0.f;
+                s += d * d;
+            }
+            var[q] = s;
+        }
+        skr::block_sum<4, kWaves>(var, lds);
+        float rs[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) rs[q] = rsqrtf(var[q] / (float)H + kLnEps);
+#pragma unroll
+        for (int k = 0; k < UPT; ++k) {
+            const int u = tid + k * kThreads;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const float xh = (g[k][q] - mean[q]) * rs[q];
+                if (act_u[k]) {
+                    a.xhat[(int64_t)b * 4 * H + q * H + u] = xh;
+                    g[k][q] = xh * a.ln_g[q * H + u] + a.ln_b[q * H + u];
+                }
+            }
+        }
+        if (tid < 4) a.rstd[b * 5 + tid] = rs[tid];
+    }
+    float c[UPT], o_[UPT];
+    float csum = 0.f;
+#pragma unroll
+    for (int k = 0; k < UPT; ++k) {
+        const int u = tid + k * kThreads;
+        const int64_t ro = (int64_t)b * H + u;
+        const float i = skr::sigmoidf_(g[k][0]);
+        const float tj = tanhf(g[k][1]);
+        const float f = skr::sigmoidf_(g[k][2] + a.forget_bias);
+        const float o = skr::sigmoidf_(g[k][3]);
+        float m = 1.f;
+        if (keep_on) m = skr::hash_uniform(key, (uint32_t)ro) < a.keep ? 1.0f / a.keep : 0.f;
+        float cn = 0.f;
+        if (act_u[k]) {
+            cn = a.c_prev[ro] * f + i * tj * m;
+            float* ap = a.act + (int64_t)b * 4 * H + u;
+            ap[0] = i;
+            ap[H] = tj;
+            ap[2 * H] = f;
+            ap[3 * H] = o;
+            a.c_out[ro] = cn;
+        }
+        c[k] = cn;
+        o_[k] = o;
+        csum += cn;
+    }
+    float th[UPT];
+    if (LN) {
+        float s1[1] = {csum};
+        skr::block_sum<1, kWaves>(s1, lds);
+        const float mc = s1[0] / (float)H;
+        float s2[1] = {0.f};
+#pragma unroll
+        for (int k = 0; k < UPT; ++k) {
+            const float d = act_u[k] ? c[k] - mc : 0.f;
+            s2[0] += d * d;
+        }
+        skr::block_sum<1, kWaves>(s2, lds);
+        const float rc = rsqrtf(s2[0] / (float)H + kLnEps);
+        if (tid == 0) a.rstd[b * 5 + 4] = rc;
+#pragma unroll
+        for (int k = 0; k < UPT; ++k) {
+            const int u = tid + k * kThreads;
+            const float ch = (c[k] - mc) * rc;
+            float t = 0.f;
+            if (act_u[k]) {
+                a.chat[(int64_t)b * H + u] = ch;
+                t = tanhf(ch * a.lnc_g[u] + a.lnc_b[u]);
+            }
+            th[k] = t;
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < UPT; ++k) th[k] = tanhf(c[k]);
+    }
+    const bool r = a.reset != nullptr && a.reset[b] != 0.f;
+#pragma unroll
+    for (int k = 0; k < UPT; ++k) {
+        if (!act_u[k]) continue;
+        const int u = tid + k * kThreads;
+        const int64_t ro = (int64_t)b * H + u;
+        const float h = th[k] * o_[k];
+        a.h_out[ro] = h;
+        const float hc = r ? a.init_h[ro] : h;
+        const float cc = r ? a.init_c[ro] : c[k];
+        a.h_carry[ro] = hc;
+        a.c_carry[ro] = cc;
+        if (a.lp_kind == 1) ((__hip_bfloat16*)a.h_lp)[b * a.ld_lp + u] = skr::to_bf16(hc);
+        else if (a.lp_kind == 2) ((float*)a.h_lp)[b * a.ld_lp + u] = hc;
+    }
+}
+
+template <int UPT, bool LN, bool MOD>
+__global__ __launch_bounds__(kThreads) void lstm_bwd_kernel(const BwdArgs a) {
+    __shared__ float lds[kWaves * 8];
+    const int b = blockIdx.x, tid = threadIdx.x, H = a.H;
+    const bool keep_on = a.keep < 1.0f;
+    const uint32_t key = keep_on ? skr::hash_key(*a.seed, a.stream, a.step) : 0u;
+    const bool r = a.reset != nullptr && a.reset[b] != 0.f;
+    bool act_u[UPT];
+    float dc[UPT], dout[UPT], dch[UPT], ch_[UPT];
+    float s1 = 0.f, s2 = 0.f;
+    // ---- output: h' = th * o ------------------------------------------------
+#pragma unroll
+    for (int k = 0; k < UPT; ++k) {
+        const int u = tid + k * kThreads;
+        act_u[k] = u < H;
+        const int64_t ro = (int64_t)b * H + u;
+        float dcv = 0.f, dov = 0.f, dchv = 0.f, chv = 0.f;
+        if (act_u[k]) {
+            const float dhc = a.dh_rec ? a.dh_rec[b * a.ld_dh_rec + u] : 0.f;
+            const float dcc = a.dc_rec[ro];
+            const float dh = (a.dh_out ? a.dh_out[ro] : 0.f) + (r ? 0.f : dhc);
+            dcv = r ? 0.f : dcc;
+            if (r && a.dinit_h) {
+                a.dinit_h[ro] += dhc;
+                a.dinit_c[ro] += dcc;
+            }
+            const float o = a.act[(int64_t)b * 4 * H + 3 * H + u];
+            float t;
+            if (LN) {
+                chv = a.chat[ro];
+                t = tanhf(chv * a.lnc_g[u] + a.lnc_b[u]);
+            } else {
+                t = tanhf(a.c_new[ro]);
+            }
+            dov = dh * t;
+            const float dcn = dh * o * (1.f - t * t);
+            if (LN) {
+                a.dlncy[ro] = dcn;
+                dchv = dcn * a.lnc_g[u];
+                s1 += dchv;
+                s2 += dchv * chv;
+            } else {
+                dcv += dcn;
+            }
+        }
+        dc[k] = dcv;
+        dout[k] = dov;
+        dch[k] = dchv;
+        ch_[k] = chv;
+    }
+    if (LN) {
+        float s[2] = {s1, s2};
+        skr::block_sum<2, kWaves>(s, lds);
+        const float m1 = s[0] / (float)H, m2 = s[1] / (float)H;
+        const float rc = a.rstd[b * 5 + 4];
+#pragma unroll
+        for (int k = 0; k < UPT; ++k) dc[k] += rc * (dch[k] - m1 - ch_[k] * m2);
+    }
+    // ---- cell: c' = c*f + i*tj*m ---------------------------------------------
+    float dy[UPT][4];
+#pragma unroll
+    for (int k = 0; k < UPT; ++k) {
+        const int u = tid + k * kThreads;
+        const int64_t ro = (int64_t)b * H + u;
+        dy[k][0] = dy[k][1] = dy[k][2] = dy[k][3] = 0.f;
+        if (!act_u[k]) continue;
+        const float* ap = a.act + (int64_t)b * 4 * H + u;
+        const float i = ap[0], tj = ap[H], f = ap[2 * H], o = ap[3 * H];
+        float m = 1.f;
+        if (keep_on) m = skr::hash_uniform(key, (uint32_t)ro) < a.keep ? 1.0f / a.keep : 0.f;
+        const float cp = a.c_prev[ro];
+        const float d = dc[k];
+        dy[k][0] = d * tj * m * i * (1.f - i);
+        dy[k][1] = d * i * m * (1.f - tj * tj);
+        dy[k][2] = d * cp * f * (1.f - f);
+        dy[k][3] = dout[k] * o * (1.f - o);
+        a.dc_rec[ro] = d * f;
+    }
+    // ---- layer norm over each gate block -----------------------------------------
+    if (LN) {
+        float acc[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) acc[q] = 0.f;
+        float xh[UPT][4];
+#pragma unroll
+        for (int k = 0; k < UPT; ++k) {
+            const int u = tid + k * kThreads;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                float x = 0.f;
+                if (act_u[k]) {
+                    const int64_t gi = (int64_t)b * 4 * H + q * H + u;
+                    x = a.xhat[gi];
+                    a.dlny[gi] = dy[k][q];
+                    const float dg = dy[k][q] * a.ln_g[q * H + u];
+                    dy[k][q] = dg;
+                    acc[q] += dg;
+                    acc[4 + q] += dg * x;
+                }
+                xh[k][q] = x;
+            }
+        }
+        skr::block_sum<8, kWaves>(acc, lds);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const float rs = a.rstd[b * 5 + q];
+            const float m1 = acc[q] / (float)H, m2 = acc[4 + q] / (float)H;
+#pragma unroll
+            for (int k = 0; k < UPT; ++k) dy[k][q] = rs * (dy[k][q] - m1 - xh[k][q] * m2);
+        }
+    }
+    // ---- outputs ------------------------------------------------------------------
+#pragma unroll
+    for (int k = 0; k < UPT; ++k) {
+        if (!act_u[k]) continue;
+        const int u = tid + k * kThreads;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const float dg = dy[k][q];
+            float dr = dg;
+            if (MOD) {
+                const int64_t o = (int64_t)b * H + u;
+                const float xv = a.xp[b * a.ld_xp + q * H + u];
+                const float rv = a.R[b * a.ld_R + q * H + u];
+                a.dxp[b * a.ld_dxp + q * H + u] = dg * a.vec[q * a.vec_gs + o];
+                dr = dg * a.vec[(4 + q) * a.vec_gs + o];
+                a.dvec[q * a.vec_gs + o] = dg * xv;
+                a.dvec[(4 + q) * a.vec_gs + o] = dg * rv;
+                a.dvec[(8 + q) * a.vec_gs + o] = dg;
+            }
+            a.dG[b * a.ld_dG + q * H + u] = dr;
+            if (a.dG_lp_kind == 1) ((__hip_bfloat16*)a.dG_lp)[b * a.ld_dG_lp + q * H + u] = skr::to_bf16(dr);
+        }
+    }
+}
+
+template <int UPT, bool LN, bool MOD>
+int launch_fwd(const FwdArgs& a, hipStream_t s) {
+    hipLaunchKernelGGL((lstm_fwd_kernel<UPT, LN, MOD>), dim3(a.B), dim3(kThreads), 0, s, a);
+    return SKR_CHECK_LAUNCH();
+}
+template <int UPT, bool LN, bool MOD>
+int launch_bwd(const BwdArgs& a, hipStream_t s) {
+    hipLaunchKernelGGL((lstm_bwd_kernel<UPT, LN, MOD>), dim3(a.B), dim3(kThreads), 0, s, a);
+    return SKR_CHECK_LAUNCH();
+}
+
+#define SKR_DISPATCH(FN, ARGS)                                                                \
+    do {                                                                                      \
+        const int upt = (H + kThreads - 1) / kThreads;                                        \
+        if (mod && !ln) return -3;                                                            \
+        if (upt <= 1) return ln ? (mod ? FN<1, true, true>(ARGS, s) : FN<1, true, false>(ARGS, s)) \
+                                : FN<1, false, false>(ARGS, s);                              \
+        if (upt <= 2) return ln ? (mod ? FN<2, true, true>(ARGS, s) : FN<2, true, false>(ARGS, s)) \
+                                : FN<2, false, false>(ARGS, s);                              \
+        if (upt <= 4) return ln ? (mod ? FN<4, true, true>(ARGS, s) : FN<4, true, false>(ARGS, s)) \
+                                : FN<4, false, false>(ARGS, s);                              \
+        if (upt <= 8) return ln ? (mod ? FN<8, true, true>(ARGS, s) : FN<8, true, false>(ARGS, s)) \
+                                : FN<8, false, false>(ARGS, s);                              \
+        return -2;                                                                            \
+    } while (0)
+
+}  // namespace
+
+// Host entry points: argument structs are passed by pointer from Python (ctypes
+// mirrors of FwdArgs / BwdArgs in sketch_rnn_amd/ops/_hipapi.py).
+SKR_API int skr_lstm_fwd_step(const FwdArgs* args, int ln, int mod, hipStream_t s) {
+    const FwdArgs& a = *args;
+    const int H = a.H;
+    SKR_DISPATCH(launch_fwd, a);
+}
+
+SKR_API int skr_lstm_bwd_step(const BwdArgs* args, int ln, int mod, hipStream_t s) {
+    const BwdArgs& a = *args;
+    const int H = a.H;
+    SKR_DISPATCH(launch_bwd, a);
+}
+
+SKR_API int skr_lstm_fwd_args_size() { return (int)sizeof(FwdArgs); }
+SKR_API int skr_lstm_bwd_args_size() { return (int)sizeof(BwdArgs); }

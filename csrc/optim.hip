@@ -1,0 +1,109 @@
+// Flat-arena optimizer kernels: global gradient norm + fused clip/Adam.
+//
+// The whole model's parameters, gradients and Adam moments are single
+// contiguous fp32 buffers (sketch_rnn_amd/train/optim.py), padded to a
+// multiple of 64 elements, so one float4-vectorised launch updates every
+// tensor. Scalars live on the device so the step is graph-capturable:
+//   scal[0] = lr, scal[1] = t (incremented on device), scal[2] = |g|, scal[3] = clip scale
+// Adam is TF's (model.py:183): eps added to sqrt(v), bias corrections folded
+// into lr_t = lr * sqrt(1 - b2^t) / (1 - b1^t).
+#include "common.h"
+
+namespace {
+
+constexpr int kBlock = 256;
+
+__global__ __launch_bounds__(kBlock) void sumsq_partial_kernel(const float4* __restrict__ g, int64_t n4,
+                                                               double* __restrict__ partial) {
+    __shared__ float lds[kBlock / 64];
+    float acc = 0.f;
+    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n4; i += (int64_t)gridDim.x * kBlock) {
+        const float4 v = g[i];
+        acc += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
+    }
+    float a1[1] = {acc};
+    skr::block_sum<1, kBlock / 64>(a1, lds);
+    if (threadIdx.x == 0) partial[blockIdx.x] = (double)a1[0];
+}
+
+__global__ void finalize_kernel(const double* __restrict__ partial, int nparts, float* __restrict__ scal,
+                                int clip_mode, float clip) {
+    // single wave: deterministic order
+    double s = 0.0;
+    for (int i = threadIdx.x; i < nparts; i += 64) s += partial[i];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+    if (threadIdx.x == 0) {
+        scal[1] += 1.0f;
+        if (clip_mode == 1) {
+            const float norm = (float)sqrt(s);
+            scal[2] = norm;
+            scal[3] = clip / fmaxf(norm, clip);
+        } else {
+            scal[3] = 1.0f;
+        }
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void adam_kernel(float4* __restrict__ p, const float4* __restrict__ g,
+                                                      float4* __restrict__ m, float4* __restrict__ v,
+                                                      const float* __restrict__ scal, int64_t n4, float b1,
+                                                      float b2, float eps, int clip_mode, float clip) {
+    const float t = scal[1];
+    const float lr_t = scal[0] * sqrtf(1.f - powf(b2, t)) / (1.f - powf(b1, t));
+    const float sc = scal[3];
+    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n4; i += (int64_t)gridDim.x * kBlock) {
+        float4 gg = g[i], mm = m[i], vv = v[i], pp = p[i];
+        float* gv = &gg.x;
+        float* mv = &mm.x;
+        float* vvv = &vv.x;
+        float* pv = &pp.x;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            float x = gv[k];
+            if (clip_mode == 1) x *= sc;
+            else if (clip_mode == 2) x = fminf(fmaxf(x, -clip), clip);
+            mv[k] = b1 * mv[k] + (1.f - b1) * x;
+            vvv[k] = b2 * vvv[k] + (1.f - b2) * x * x;
+            pv[k] -= lr_t * mv[k] / (sqrtf(vvv[k]) + eps);
+        }
+        m[i] = mm;
+        v[i] = vv;
+        p[i] = pp;
+    }
+}
+
+int grid_for(int64_t n4) {
+    int64_t g = (n4 + kBlock - 1) / kBlock;
+    if (g > 2048) g = 2048;  // grid-stride beyond 8 blocks per CU
+    if (g < 1) g = 1;
+    return (int)g;
+}
+
+}  // namespace
+
+// clip_mode: 0 none, 1 global norm, 2 per-element value. `partial` must hold 2048 doubles.
+SKR_API int skr_adam_step(float* p, const float* g, float* m, float* v, float* scal, double* partial, int64_t n,
+                          float b1, float b2, float eps, int clip_mode, float clip, hipStream_t s) {
+    if (n % 4 != 0) return -2;
+    const int64_t n4 = n / 4;
+    const int grid = grid_for(n4);
+    if (clip_mode == 1) {
+        hipLaunchKernelGGL(sumsq_partial_kernel, dim3(grid), dim3(kBlock), 0, s, (const float4*)g, n4, partial);
+    }
+    hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(64), 0, s, partial, clip_mode == 1 ? grid : 0, scal,
+                       clip_mode, clip);
+    hipLaunchKernelGGL(adam_kernel, dim3(grid), dim3(kBlock), 0, s, (float4*)p, (const float4*)g, (float4*)m,
+                       (float4*)v, (const float*)scal, n4, b1, b2, eps, clip_mode, clip);
+    return SKR_CHECK_LAUNCH();
+}
+
+// standalone global norm (diagnostics): writes sqrt(sum g^2) to out[0]
+SKR_API int skr_global_norm(const float* g, int64_t n, double* partial, float* scal_tmp, hipStream_t s) {
+    if (n % 4 != 0) return -2;
+    const int64_t n4 = n / 4;
+    const int grid = grid_for(n4);
+    hipLaunchKernelGGL(sumsq_partial_kernel, dim3(grid), dim3(kBlock), 0, s, (const float4*)g, n4, partial);
+    hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(64), 0, s, partial, grid, scal_tmp, 1, 1.0f);
+    return SKR_CHECK_LAUNCH();
+}

@@ -1,0 +1,39 @@
+#!/bin/bash
+# GPU validation session for gpurun: each step has its own time limit; a
+# crash / abort / timeout (anything other than a clean pass or an ordinary
+# test failure) ends the session so nothing else touches the GPU.
+# usage: scripts/gpu_check.sh [pytest|smoke|bench|prof ...]
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+export PYTHONUNBUFFERED=1
+steps=("$@")
+[ ${#steps[@]} -eq 0 ] && steps=(pytest smoke bench)
+
+run() {  # name, limit, cmd...
+    local name=$1 lim=$2
+    shift 2
+    echo "== $name (limit ${lim}s): $*"
+    timeout -k 10 "$lim" "$@" > "gpurun_out/$name.log" 2>&1
+    local rc=$?
+    echo "== $name rc=$rc"
+    tail -n 25 "gpurun_out/$name.log"
+    if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then
+        echo "== aborting session after $name (rc=$rc)"
+        exit $rc
+    fi
+    return 0
+}
+
+for s in "${steps[@]}"; do
+    case $s in
+        pytest) run pytest_gpu 900 python -m pytest tests -m gpu -x -q ;;
+        smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+        bench) run bench 600 python bench.py --steps 10 --warmup 2 ;;
+        bench_fp32) run bench_fp32 600 python bench.py --steps 5 --warmup 2 --dtype fp32 ;;
+        bench_small) run bench_small 600 python bench.py --steps 10 --warmup 2 --config vae_small ;;
+        prof) run prof 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --no-eval ;;
+        *) echo "unknown step $s"; exit 2 ;;
+    esac
+done
+echo "== session done"

@@ -25,6 +25,7 @@ import torch.nn as nn
 
 from .. import ops
 from ..config import VAEConfig
+from ..ops import gemm
 from . import cells as C
 
 # dropout hash streams
@@ -166,7 +167,7 @@ class SketchVAE(nn.Module):
                                             drop_stream=_S_DEC, hyp_drop_keep=hkeep)
         else:
             h0, c0 = state
-            xp = (x.reshape(T * B, -1) @ p.W_x).view(T, B, 4 * H)
+            xp = gemm.linear(x, p.W_x)
             if cfg.dec_model == "layer_norm":
                 ln = (p.ln_gamma, p.ln_beta, p.lnc_gamma, p.lnc_beta)
             else:
@@ -179,7 +180,7 @@ class SketchVAE(nn.Module):
         return out, final
 
     def head(self, out: torch.Tensor) -> torch.Tensor:
-        return torch.addmm(self.output_b, out.reshape(-1, out.shape[-1]), self.output_w)
+        return gemm.linear(out.reshape(-1, out.shape[-1]), self.output_w, self.output_b)
 
     # -- training objective -------------------------------------------------------------
     def loss(self, strokes: torch.Tensor, lengths: torch.Tensor, labels: Optional[torch.Tensor] = None,

@@ -1,0 +1,91 @@
+"""ctypes bindings for ``libskrnn_hip.so`` (C ABI, raw device pointers).
+
+The argument structs mirror ``FwdArgs`` / ``BwdArgs`` in
+``csrc/lstm_cell.hip`` field for field; :func:`bind` checks their sizes
+against the library so a layout drift fails at load time, not in a kernel.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+_p = C.c_void_p
+_i64 = C.c_int64
+_f = C.c_float
+_u32 = C.c_uint32
+_i = C.c_int
+
+
+class LstmFwdArgs(C.Structure):
+    _fields_ = [
+        ("B", _i), ("H", _i),
+        ("xp", _p), ("ld_xp", _i64),
+        ("R", _p), ("ld_R", _i64),
+        ("vec", _p), ("vec_gs", _i64),
+        ("bias", _p),
+        ("c_prev", _p),
+        ("ln_g", _p), ("ln_b", _p), ("lnc_g", _p), ("lnc_b", _p),
+        ("reset", _p),
+        ("init_h", _p), ("init_c", _p),
+        ("forget_bias", _f), ("keep", _f),
+        ("seed", _p), ("stream", _u32), ("step", _u32),
+        ("h_out", _p), ("c_out", _p), ("act", _p), ("xhat", _p), ("rstd", _p), ("chat", _p),
+        ("h_carry", _p),
+        ("h_lp", _p), ("ld_lp", _i64), ("lp_kind", _i),
+        ("c_carry", _p),
+    ]
+
+
+class LstmBwdArgs(C.Structure):
+    _fields_ = [
+        ("B", _i), ("H", _i),
+        ("dh_out", _p),
+        ("dh_rec", _p), ("ld_dh_rec", _i64),
+        ("dc_rec", _p),
+        ("act", _p), ("c_new", _p), ("c_prev", _p),
+        ("xhat", _p), ("rstd", _p), ("chat", _p),
+        ("ln_g", _p), ("lnc_g", _p), ("lnc_b", _p),
+        ("xp", _p), ("ld_xp", _i64),
+        ("R", _p), ("ld_R", _i64),
+        ("vec", _p), ("vec_gs", _i64),
+        ("reset", _p),
+        ("keep", _f), ("seed", _p), ("stream", _u32), ("step", _u32),
+        ("dG", _p), ("ld_dG", _i64),
+        ("dG_lp", _p), ("ld_dG_lp", _i64), ("dG_lp_kind", _i),
+        ("dxp", _p), ("ld_dxp", _i64),
+        ("dvec", _p),
+        ("dlny", _p), ("dlncy", _p),
+        ("dinit_h", _p), ("dinit_c", _p),
+    ]
+
+
+class HipLib:
+    def __init__(self, lib: C.CDLL):
+        self.lib = lib
+        lib.skr_lstm_fwd_step.argtypes = [C.POINTER(LstmFwdArgs), _i, _i, _p]
+        lib.skr_lstm_fwd_step.restype = _i
+        lib.skr_lstm_bwd_step.argtypes = [C.POINTER(LstmBwdArgs), _i, _i, _p]
+        lib.skr_lstm_bwd_step.restype = _i
+        lib.skr_lstm_fwd_args_size.restype = _i
+        lib.skr_lstm_bwd_args_size.restype = _i
+        lib.skr_mdn_loss.argtypes = [_p, _i64, _p, _i64, _i64, _i, _i, _f, _i, _f, _p, _p, _p, _p]
+        lib.skr_mdn_loss.restype = _i
+        lib.skr_adam_step.argtypes = [_p, _p, _p, _p, _p, _p, _i64, _f, _f, _f, _i, _f, _p]
+        lib.skr_adam_step.restype = _i
+        lib.skr_global_norm.argtypes = [_p, _i64, _p, _p, _p]
+        lib.skr_global_norm.restype = _i
+        for name in ("skr_sample_step", "skr_decode_lstm_step"):
+            if hasattr(lib, name):
+                getattr(lib, name).restype = _i
+        fs, bs = lib.skr_lstm_fwd_args_size(), lib.skr_lstm_bwd_args_size()
+        if fs != C.sizeof(LstmFwdArgs) or bs != C.sizeof(LstmBwdArgs):
+            raise RuntimeError("libskrnn_hip.so arg-struct layout mismatch: fwd %d vs %d, bwd %d vs %d"
+                               % (fs, C.sizeof(LstmFwdArgs), bs, C.sizeof(LstmBwdArgs)))
+
+    @staticmethod
+    def check(rc: int, what: str):
+        if rc != 0:
+            raise RuntimeError("%s failed with code %d" % (what, rc))
+
+
+def bind(lib: C.CDLL) -> HipLib:
+    return HipLib(lib)

@@ -1,0 +1,84 @@
+"""Library GEMMs (hipBLASLt via torch) with a selectable operand precision.
+
+Plain, unfused GEMMs -- the hoisted input projections, the recurrent
+``h @ W_h`` of each step, the weight-gradient reductions and the head --
+go to hipBLASLt. In ``bf16`` mode operands are bf16 and the result is
+written in fp32 (``torch.mm(..., out_dtype=float32)``: hipBLASLt bf16 x
+bf16 -> fp32), so accumulation and everything downstream stay fp32.
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+
+from . import get_compute_dtype
+
+_BF16 = torch.bfloat16
+
+
+def lp_dtype() -> torch.dtype:
+    return _BF16 if get_compute_dtype() in ("bf16", "fp8") else torch.float32
+
+
+def lp(t: torch.Tensor) -> torch.Tensor:
+    d = lp_dtype()
+    return t if t.dtype == d else t.to(d)
+
+
+def mm(a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """``a @ b`` with fp32 output; operands used as given (fp32 or bf16)."""
+    if a.dtype == torch.float32 and b.dtype == torch.float32:
+        return torch.mm(a, b, out=out) if out is not None else torch.mm(a, b)
+    if a.dtype != b.dtype:
+        a, b = a.to(_BF16), b.to(_BF16)
+    if out is not None:
+        return torch.mm(a, b, out_dtype=torch.float32, out=out)
+    return torch.mm(a, b, out_dtype=torch.float32)
+
+
+def bmm(a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    if a.dtype == torch.float32 and b.dtype == torch.float32:
+        return torch.bmm(a, b, out=out) if out is not None else torch.bmm(a, b)
+    if out is not None:
+        return torch.bmm(a, b, out_dtype=torch.float32, out=out)
+    return torch.bmm(a, b, out_dtype=torch.float32)
+
+
+class _Linear(torch.autograd.Function):
+    """``x @ W + b`` in the compute precision with fp32 outputs/grads."""
+
+    @staticmethod
+    def forward(ctx, x, W, b):
+        xs = x.reshape(-1, x.shape[-1])
+        xl, Wl = lp(xs), lp(W)
+        y = mm(xl, Wl)
+        if b is not None:
+            y.add_(b)
+        ctx.save_for_backward(xl, Wl)
+        ctx.has_b = b is not None
+        ctx.shape = x.shape
+        return y.view(*x.shape[:-1], W.shape[1])
+
+    @staticmethod
+    def backward(ctx, dy):
+        xl, Wl = ctx.saved_tensors
+        dy2 = dy.reshape(-1, dy.shape[-1]).contiguous()
+        dyl = lp(dy2)
+        dx = dW = db = None
+        if ctx.needs_input_grad[0]:
+            dx = mm(dyl, Wl.t()).view(ctx.shape)
+        if ctx.needs_input_grad[1]:
+            dW = mm(xl.t(), dyl)
+        if ctx.has_b and ctx.needs_input_grad[2]:
+            db = dy2.sum(0)
+        return dx, dW, db
+
+
+def linear(x: torch.Tensor, W: torch.Tensor, b: Optional[torch.Tensor] = None) -> torch.Tensor:
+    if lp_dtype() == torch.float32 or not x.is_cuda:
+        y = x.reshape(-1, x.shape[-1]) @ W
+        if b is not None:
+            y = y + b
+        return y.view(*x.shape[:-1], W.shape[1])
+    return _Linear.apply(x, W, b)

@@ -192,25 +192,44 @@ class VAETrainer:
         self.seed = torch.zeros(1, dtype=torch.int64, device=self.device)
         self.kl_w = torch.zeros((), device=self.device)
 
-    def _step_fn(self, strokes, lengths, labels):
+    def _fwd_bwd(self, strokes, lengths, labels):
         self.opt.zero_grad()
         out = self.model.loss(strokes, lengths, labels if self.cfg.num_classes > 0 else None,
                               kl_weight=self.kl_w, train=True, seed=self.seed)
         out["cost"].backward()
+        return {k: v.detach() for k, v in out.items()}
+
+    def _opt_step(self):
+        self.opt.step()
+        return {}
+
+    def _step_fn(self, strokes, lengths, labels):
+        out = self._fwd_bwd(strokes, lengths, labels)
         if self.reducer is not None:
             self.reducer.all_reduce()
         self.opt.step()
-        return {k: v.detach() for k, v in out.items()}
+        return out
 
     def train_step(self, strokes, lengths, labels):
+        """One optimisation step. On the GPU the forward+backward is one
+        captured HIP graph; with DP the bucketed RCCL all-reduce runs between
+        it and a second graph holding the fused clip+Adam update."""
         self.opt.set_lr(schedules.vae_lr(self.cfg, self.step))
         self.kl_w.fill_(schedules.kl_weight(self.cfg, self.step))
-        if self.use_graph and self.reducer is None:
+        if self.use_graph:
             if self._graph is None:
                 static = {"strokes": strokes.clone(), "lengths": lengths.clone(), "labels": labels.clone()}
                 snap = [self.opt.flat, self.opt.m, self.opt.v, self.opt.scalars]
-                self._graph = GraphedStep(self._step_fn, static, snapshot=snap)
+                if self.reducer is None:
+                    self._graph = GraphedStep(self._step_fn, static, snapshot=snap)
+                    self._graph_opt = None
+                else:
+                    self._graph = GraphedStep(self._fwd_bwd, static, snapshot=snap)
+                    self._graph_opt = GraphedStep(self._opt_step, {}, snapshot=snap)
             out = self._graph(strokes=strokes, lengths=lengths, labels=labels)
+            if self._graph_opt is not None:
+                self.reducer.all_reduce()
+                self._graph_opt()
         else:
             out = self._step_fn(strokes, lengths, labels)
         self.seed.add_(1)
