@@ -1,12 +1,15 @@
 // Fused LSTM-family cell step (forward + backward) for gfx950.
 //
-// One workgroup (256 threads = 4 waves) owns one batch row; each thread owns
-// UPT = ceil(H / 256) hidden units and all four gates (i, j, f, o) of each.
+// One workgroup owns one batch row; NT threads (NT = 64..1024, a power of
+// two chosen from H) each own UPT = ceil(H / NT) hidden units and all four
+// gates (i, j, f, o) of each. Wide workgroups (16 waves at H = 2048) keep
+// enough loads in flight per row: the step is latency-bound at B ~ 100 rows.
 // Everything between the recurrent GEMM and the next step's GEMM is fused
 // into one launch per step:
 //
 //   g      = xp + R                              (plain / LN-LSTM)
-//          = xh*ax + R*ah + bh + bias            (HyperLSTM main cell, MOD)
+//          = xh*ax + R*ah + bh + bias            (HyperLSTM main cell, MOD;
+//                                                 a/b = vec + vec_bias per gate)
 //   y      = LN_all(g)*gamma + beta              (LN: per gate block over H)
 //   c'     = c*sig(y_f + fb) + sig(y_i)*tanh(y_j)*mask
 //   h'     = tanh(LN(c')*gc + bc)*sig(y_o)  |  tanh(c')*sig(y_o)
@@ -15,6 +18,9 @@
 // plus the saves the backward needs and a bf16 copy of the carried h written
 // straight into the next GEMM's A operand (which may be a column slice of a
 // concatenated [h | h_hyper] buffer, hence the explicit row stride).
+// Rows can be split into parameter groups (grp_rows): the two directions of
+// the bidirectional encoder run as 2B rows of one launch with their own
+// LayerNorm parameters.
 // The recurrent dropout mask is regenerated from a stateless hash of
 // (seed, stream, step, b*H + u) in both passes -- never stored.
 //
@@ -24,15 +30,15 @@
 
 namespace {
 
-constexpr int kThreads = 256;
-constexpr int kWaves = kThreads / 64;
 constexpr float kLnEps = 1e-3f;
 
 struct FwdArgs {
     int B, H;
+    int grp_rows;                      // rows per parameter group (0: one group)
     const float* xp; int64_t ld_xp;    // [B, 4H]: x-projection (+bias unless MOD)
     const float* R;  int64_t ld_R;     // [B, 4H]: h_prev @ W_h (fp32)
-    const float* vec; int64_t vec_gs;  // MOD: 12 blocks [B, H], block stride vec_gs
+    const float* vec; int64_t vec_gs; int64_t vec_ld;  // MOD: element (k,b,u) at k*gs + b*ld + u
+    const float* vec_bias;             // MOD: [12, H] added to vec (or null)
     const float* bias;                 // MOD: [4H]
     const float* c_prev;               // [B, H]
     const float* ln_g; const float* ln_b; const float* lnc_g; const float* lnc_b;
@@ -53,6 +59,7 @@ struct FwdArgs {
 
 struct BwdArgs {
     int B, H;
+    int grp_rows;
     const float* dh_out;               // [B, H] or null
     const float* dh_rec;               // [B, H] (grad into carried h_t) or null
     int64_t ld_dh_rec;
@@ -62,29 +69,43 @@ struct BwdArgs {
     const float* ln_g; const float* lnc_g; const float* lnc_b;
     const float* xp; int64_t ld_xp;    // MOD: xh
     const float* R;  int64_t ld_R;     // MOD: R
-    const float* vec; int64_t vec_gs;  // MOD
+    const float* vec; int64_t vec_gs; int64_t vec_ld;  // MOD
+    const float* vec_bias;
     const float* reset;
     float keep; const int64_t* seed; uint32_t stream, step;
     float* dG; int64_t ld_dG;          // non-MOD: d(preact) [B, 4H]; MOD: dR = dg*ah
     void* dG_lp; int64_t ld_dG_lp; int dG_lp_kind;  // bf16 copy of dG for the next GEMM (1) or none (0)
     float* dxp; int64_t ld_dxp;        // MOD: dxh = dg*ax
-    float* dvec;                       // MOD: 12 blocks [B, H] (block stride vec_gs)
+    void* dvec; int dvec_kind;         // MOD: same layout as vec; 1 bf16, 2 fp32
     float* dlny;                       // LN: [B, 4H] grad wrt LN-all output (for gamma/beta)
     float* dlncy;                      // LN: [B, H]  grad wrt LN(c) output
     float* dinit_h; float* dinit_c;    // [B, H] accumulated on reset rows (or null)
 };
 
-template <int UPT, bool LN, bool MOD>
-__global__ __launch_bounds__(kThreads) void lstm_fwd_kernel(const FwdArgs a) {
-    __shared__ float lds[kWaves * 8];
+__device__ __forceinline__ float vec_at(const float* v, const float* vb, int64_t gs, int64_t ld, int k, int b, int u,
+                                        int H) {
+    float x = v[k * gs + (int64_t)b * ld + u];
+    if (vb) x += vb[k * H + u];
+    return x;
+}
+
+template <int NT, int UPT, bool LN, bool MOD>
+__global__ __launch_bounds__(NT) void lstm_fwd_kernel(const FwdArgs a) {
+    constexpr int NW = NT / 64;
+    __shared__ float lds[NW * 8];
     const int b = blockIdx.x, tid = threadIdx.x, H = a.H;
+    const int grp = a.grp_rows > 0 ? b / a.grp_rows : 0;
+    const float* ln_g = a.ln_g ? a.ln_g + grp * 4 * H : nullptr;
+    const float* ln_b = a.ln_b ? a.ln_b + grp * 4 * H : nullptr;
+    const float* lnc_g = a.lnc_g ? a.lnc_g + grp * H : nullptr;
+    const float* lnc_b = a.lnc_b ? a.lnc_b + grp * H : nullptr;
     const bool keep_on = a.keep < 1.0f;
     const uint32_t key = keep_on ? skr::hash_key(*a.seed, a.stream, a.step) : 0u;
     float g[UPT][4];
     bool act_u[UPT];
 #pragma unroll
     for (int k = 0; k < UPT; ++k) {
-        const int u = tid + k * kThreads;
+        const int u = tid + k * NT;
         act_u[k] = u < H;
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
@@ -93,9 +114,9 @@ __global__ __launch_bounds__(kThreads) void lstm_fwd_kernel(const FwdArgs a) {
                 const float xv = a.xp[b * a.ld_xp + q * H + u];
                 const float rv = a.R[b * a.ld_R + q * H + u];
                 if (MOD) {
-                    const int64_t o = (int64_t)b * H + u;
-                    v = xv * a.vec[q * a.vec_gs + o] + rv * a.vec[(4 + q) * a.vec_gs + o] +
-                        a.vec[(8 + q) * a.vec_gs + o] + a.bias[q * H + u];
+                    v = xv * vec_at(a.vec, a.vec_bias, a.vec_gs, a.vec_ld, q, b, u, H) +
+                        rv * vec_at(a.vec, a.vec_bias, a.vec_gs, a.vec_ld, 4 + q, b, u, H) +
+                        vec_at(a.vec, a.vec_bias, a.vec_gs, a.vec_ld, 8 + q, b, u, H) + a.bias[q * H + u];
                 } else {
                     v = xv + rv;
                 }
@@ -112,7 +133,7 @@ __global__ __launch_bounds__(kThreads) void lstm_fwd_kernel(const FwdArgs a) {
             for (int k = 0; k < UPT; ++k) s += g[k][q];
             mean[q] = s;
         }
-        skr::block_sum<4, kWaves>(mean, lds);
+        skr::block_sum<4, NW>(mean, lds);
         float var[4];
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
@@ -125,19 +146,19 @@ __global__ __launch_bounds__(kThreads) void lstm_fwd_kernel(const FwdArgs a) {
             }
             var[q] = s;
         }
-        skr::block_sum<4, kWaves>(var, lds);
+        skr::block_sum<4, NW>(var, lds);
         float rs[4];
 #pragma unroll
         for (int q = 0; q < 4; ++q) rs[q] = rsqrtf(var[q] / (float)H + kLnEps);
 #pragma unroll
         for (int k = 0; k < UPT; ++k) {
-            const int u = tid + k * kThreads;
+            const int u = tid + k * NT;
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
                 const float xh = (g[k][q] - mean[q]) * rs[q];
                 if (act_u[k]) {
                     a.xhat[(int64_t)b * 4 * H + q * H + u] = xh;
-                    g[k][q] = xh * a.ln_g[q * H + u] + a.ln_b[q * H + u];
+                    g[k][q] = xh * ln_g[q * H + u] + ln_b[q * H + u];
                 }
             }
         }
@@ -147,7 +168,7 @@ __global__ __launch_bounds__(kThreads) void lstm_fwd_kernel(const FwdArgs a) {
     float csum = 0.f;
 #pragma unroll
     for (int k = 0; k < UPT; ++k) {
-        const int u = tid + k * kThreads;
+        const int u = tid + k * NT;
         const int64_t ro = (int64_t)b * H + u;
         const float i = skr::sigmoidf_(g[k][0]);
         const float tj = tanhf(g[k][1]);
@@ -172,7 +193,7 @@ __global__ __launch_bounds__(kThreads) void lstm_fwd_kernel(const FwdArgs a) {
     float th[UPT];
     if (LN) {
         float s1[1] = {csum};
-        skr::block_sum<1, kWaves>(s1, lds);
+        skr::block_sum<1, NW>(s1, lds);
         const float mc = s1[0] / (float)H;
         float s2[1] = {0.f};
 #pragma unroll
@@ -180,17 +201,17 @@ __global__ __launch_bounds__(kThreads) void lstm_fwd_kernel(const FwdArgs a) {
             const float d = act_u[k] ? c[k] - mc : 0.f;
             s2[0] += d * d;
         }
-        skr::block_sum<1, kWaves>(s2, lds);
+        skr::block_sum<1, NW>(s2, lds);
         const float rc = rsqrtf(s2[0] / (float)H + kLnEps);
         if (tid == 0) a.rstd[b * 5 + 4] = rc;
 #pragma unroll
         for (int k = 0; k < UPT; ++k) {
-            const int u = tid + k * kThreads;
+            const int u = tid + k * NT;
             const float ch = (c[k] - mc) * rc;
             float t = 0.f;
             if (act_u[k]) {
                 a.chat[(int64_t)b * H + u] = ch;
-                t = tanhf(ch * a.lnc_g[u] + a.lnc_b[u]);
+                t = tanhf(ch * lnc_g[u] + lnc_b[u]);
             }
             th[k] = t;
         }
@@ -202,7 +223,7 @@ __global__ __launch_bounds__(kThreads) void lstm_fwd_kernel(const FwdArgs a) {
 #pragma unroll
     for (int k = 0; k < UPT; ++k) {
         if (!act_u[k]) continue;
-        const int u = tid + k * kThreads;
+        const int u = tid + k * NT;
         const int64_t ro = (int64_t)b * H + u;
         const float h = th[k] * o_[k];
         a.h_out[ro] = h;
@@ -215,10 +236,15 @@ __global__ __launch_bounds__(kThreads) void lstm_fwd_kernel(const FwdArgs a) {
     }
 }
 
-template <int UPT, bool LN, bool MOD>
-__global__ __launch_bounds__(kThreads) void lstm_bwd_kernel(const BwdArgs a) {
-    __shared__ float lds[kWaves * 8];
+template <int NT, int UPT, bool LN, bool MOD>
+__global__ __launch_bounds__(NT) void lstm_bwd_kernel(const BwdArgs a) {
+    constexpr int NW = NT / 64;
+    __shared__ float lds[NW * 8];
     const int b = blockIdx.x, tid = threadIdx.x, H = a.H;
+    const int grp = a.grp_rows > 0 ? b / a.grp_rows : 0;
+    const float* ln_g = a.ln_g ? a.ln_g + grp * 4 * H : nullptr;
+    const float* lnc_g = a.lnc_g ? a.lnc_g + grp * H : nullptr;
+    const float* lnc_b = a.lnc_b ? a.lnc_b + grp * H : nullptr;
     const bool keep_on = a.keep < 1.0f;
     const uint32_t key = keep_on ? skr::hash_key(*a.seed, a.stream, a.step) : 0u;
     const bool r = a.reset != nullptr && a.reset[b] != 0.f;
@@ -228,7 +254,7 @@ __global__ __launch_bounds__(kThreads) void lstm_bwd_kernel(const BwdArgs a) {
     // ---- output: h' = th * o ------------------------------------------------
 #pragma unroll
     for (int k = 0; k < UPT; ++k) {
-        const int u = tid + k * kThreads;
+        const int u = tid + k * NT;
         act_u[k] = u < H;
         const int64_t ro = (int64_t)b * H + u;
         float dcv = 0.f, dov = 0.f, dchv = 0.f, chv = 0.f;
@@ -245,7 +271,7 @@ __global__ __launch_bounds__(kThreads) void lstm_bwd_kernel(const BwdArgs a) {
             float t;
             if (LN) {
                 chv = a.chat[ro];
-                t = tanhf(chv * a.lnc_g[u] + a.lnc_b[u]);
+                t = tanhf(chv * lnc_g[u] + lnc_b[u]);
             } else {
                 t = tanhf(a.c_new[ro]);
             }
@@ -253,7 +279,7 @@ __global__ __launch_bounds__(kThreads) void lstm_bwd_kernel(const BwdArgs a) {
             const float dcn = dh * o * (1.f - t * t);
             if (LN) {
                 a.dlncy[ro] = dcn;
-                dchv = dcn * a.lnc_g[u];
+                dchv = dcn * lnc_g[u];
                 s1 += dchv;
                 s2 += dchv * chv;
             } else {
@@ -267,7 +293,7 @@ __global__ __launch_bounds__(kThreads) void lstm_bwd_kernel(const BwdArgs a) {
     }
     if (LN) {
         float s[2] = {s1, s2};
-        skr::block_sum<2, kWaves>(s, lds);
+        skr::block_sum<2, NW>(s, lds);
         const float m1 = s[0] / (float)H, m2 = s[1] / (float)H;
         const float rc = a.rstd[b * 5 + 4];
 #pragma unroll
@@ -277,7 +303,7 @@ __global__ __launch_bounds__(kThreads) void lstm_bwd_kernel(const BwdArgs a) {
     float dy[UPT][4];
 #pragma unroll
     for (int k = 0; k < UPT; ++k) {
-        const int u = tid + k * kThreads;
+        const int u = tid + k * NT;
         const int64_t ro = (int64_t)b * H + u;
         dy[k][0] = dy[k][1] = dy[k][2] = dy[k][3] = 0.f;
         if (!act_u[k]) continue;
@@ -301,7 +327,7 @@ __global__ __launch_bounds__(kThreads) void lstm_bwd_kernel(const BwdArgs a) {
         float xh[UPT][4];
 #pragma unroll
         for (int k = 0; k < UPT; ++k) {
-            const int u = tid + k * kThreads;
+            const int u = tid + k * NT;
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
                 float x = 0.f;
@@ -309,7 +335,7 @@ __global__ __launch_bounds__(kThreads) void lstm_bwd_kernel(const BwdArgs a) {
                     const int64_t gi = (int64_t)b * 4 * H + q * H + u;
                     x = a.xhat[gi];
                     a.dlny[gi] = dy[k][q];
-                    const float dg = dy[k][q] * a.ln_g[q * H + u];
+                    const float dg = dy[k][q] * ln_g[q * H + u];
                     dy[k][q] = dg;
                     acc[q] += dg;
                     acc[4 + q] += dg * x;
@@ -317,7 +343,7 @@ __global__ __launch_bounds__(kThreads) void lstm_bwd_kernel(const BwdArgs a) {
                 xh[k][q] = x;
             }
         }
-        skr::block_sum<8, kWaves>(acc, lds);
+        skr::block_sum<8, NW>(acc, lds);
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             const float rs = a.rstd[b * 5 + q];
@@ -330,20 +356,24 @@ __global__ __launch_bounds__(kThreads) void lstm_bwd_kernel(const BwdArgs a) {
 #pragma unroll
     for (int k = 0; k < UPT; ++k) {
         if (!act_u[k]) continue;
-        const int u = tid + k * kThreads;
+        const int u = tid + k * NT;
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             const float dg = dy[k][q];
             float dr = dg;
             if (MOD) {
-                const int64_t o = (int64_t)b * H + u;
                 const float xv = a.xp[b * a.ld_xp + q * H + u];
                 const float rv = a.R[b * a.ld_R + q * H + u];
-                a.dxp[b * a.ld_dxp + q * H + u] = dg * a.vec[q * a.vec_gs + o];
-                dr = dg * a.vec[(4 + q) * a.vec_gs + o];
-                a.dvec[q * a.vec_gs + o] = dg * xv;
-                a.dvec[(4 + q) * a.vec_gs + o] = dg * rv;
-                a.dvec[(8 + q) * a.vec_gs + o] = dg;
+                a.dxp[b * a.ld_dxp + q * H + u] = dg * vec_at(a.vec, a.vec_bias, a.vec_gs, a.vec_ld, q, b, u, H);
+                dr = dg * vec_at(a.vec, a.vec_bias, a.vec_gs, a.vec_ld, 4 + q, b, u, H);
+                const int64_t o0 = (int64_t)b * a.vec_ld + u;
+                const float d3[3] = {dg * xv, dg * rv, dg};
+#pragma unroll
+                for (int j = 0; j < 3; ++j) {
+                    const int64_t oi = (4 * j + q) * a.vec_gs + o0;
+                    if (a.dvec_kind == 1) ((__hip_bfloat16*)a.dvec)[oi] = skr::to_bf16(d3[j]);
+                    else ((float*)a.dvec)[oi] = d3[j];
+                }
             }
             a.dG[b * a.ld_dG + q * H + u] = dr;
             if (a.dG_lp_kind == 1) ((__hip_bfloat16*)a.dG_lp)[b * a.ld_dG_lp + q * H + u] = skr::to_bf16(dr);
@@ -351,46 +381,48 @@ __global__ __launch_bounds__(kThreads) void lstm_bwd_kernel(const BwdArgs a) {
     }
 }
 
-template <int UPT, bool LN, bool MOD>
-int launch_fwd(const FwdArgs& a, hipStream_t s) {
-    hipLaunchKernelGGL((lstm_fwd_kernel<UPT, LN, MOD>), dim3(a.B), dim3(kThreads), 0, s, a);
+template <int NT, int UPT>
+int launch(const FwdArgs& a, bool ln, bool mod, hipStream_t s) {
+    if (mod) hipLaunchKernelGGL((lstm_fwd_kernel<NT, UPT, true, true>), dim3(a.B), dim3(NT), 0, s, a);
+    else if (ln) hipLaunchKernelGGL((lstm_fwd_kernel<NT, UPT, true, false>), dim3(a.B), dim3(NT), 0, s, a);
+    else hipLaunchKernelGGL((lstm_fwd_kernel<NT, UPT, false, false>), dim3(a.B), dim3(NT), 0, s, a);
     return SKR_CHECK_LAUNCH();
 }
-template <int UPT, bool LN, bool MOD>
-int launch_bwd(const BwdArgs& a, hipStream_t s) {
-    hipLaunchKernelGGL((lstm_bwd_kernel<UPT, LN, MOD>), dim3(a.B), dim3(kThreads), 0, s, a);
+template <int NT, int UPT>
+int launch(const BwdArgs& a, bool ln, bool mod, hipStream_t s) {
+    if (mod) hipLaunchKernelGGL((lstm_bwd_kernel<NT, UPT, true, true>), dim3(a.B), dim3(NT), 0, s, a);
+    else if (ln) hipLaunchKernelGGL((lstm_bwd_kernel<NT, UPT, true, false>), dim3(a.B), dim3(NT), 0, s, a);
+    else hipLaunchKernelGGL((lstm_bwd_kernel<NT, UPT, false, false>), dim3(a.B), dim3(NT), 0, s, a);
     return SKR_CHECK_LAUNCH();
 }
 
-#define SKR_DISPATCH(FN, ARGS)                                                                \
-    do {                                                                                      \
-        const int upt = (H + kThreads - 1) / kThreads;                                        \
-        if (mod && !ln) return -3;                                                            \
-        if (upt <= 1) return ln ? (mod ? FN<1, true, true>(ARGS, s) : FN<1, true, false>(ARGS, s)) \
-                                : FN<1, false, false>(ARGS, s);                              \
-        if (upt <= 2) return ln ? (mod ? FN<2, true, true>(ARGS, s) : FN<2, true, false>(ARGS, s)) \
-                                : FN<2, false, false>(ARGS, s);                              \
-        if (upt <= 4) return ln ? (mod ? FN<4, true, true>(ARGS, s) : FN<4, true, false>(ARGS, s)) \
-                                : FN<4, false, false>(ARGS, s);                              \
-        if (upt <= 8) return ln ? (mod ? FN<8, true, true>(ARGS, s) : FN<8, true, false>(ARGS, s)) \
-                                : FN<8, false, false>(ARGS, s);                              \
-        return -2;                                                                            \
-    } while (0)
+// Workgroup shape from H: NT = next power of two >= H (64..1024), one unit
+// per thread; beyond 1024 units, 1024 threads with 2 or 4 units each.
+template <typename A>
+int dispatch(const A& a, bool ln, bool mod, hipStream_t s) {
+    if (mod && !ln) return -3;
+    if (a.B <= 0) return 0;
+    const int H = a.H;
+    if (H <= 64) return launch<64, 1>(a, ln, mod, s);
+    if (H <= 128) return launch<128, 1>(a, ln, mod, s);
+    if (H <= 256) return launch<256, 1>(a, ln, mod, s);
+    if (H <= 512) return launch<512, 1>(a, ln, mod, s);
+    if (H <= 1024) return launch<1024, 1>(a, ln, mod, s);
+    if (H <= 2048) return launch<1024, 2>(a, ln, mod, s);
+    if (H <= 4096) return launch<1024, 4>(a, ln, mod, s);
+    return -2;
+}
 
 }  // namespace
 
 // Host entry points: argument structs are passed by pointer from Python (ctypes
 // mirrors of FwdArgs / BwdArgs in sketch_rnn_amd/ops/_hipapi.py).
 SKR_API int skr_lstm_fwd_step(const FwdArgs* args, int ln, int mod, hipStream_t s) {
-    const FwdArgs& a = *args;
-    const int H = a.H;
-    SKR_DISPATCH(launch_fwd, a);
+    return dispatch(*args, ln != 0, mod != 0, s);
 }
 
 SKR_API int skr_lstm_bwd_step(const BwdArgs* args, int ln, int mod, hipStream_t s) {
-    const BwdArgs& a = *args;
-    const int H = a.H;
-    SKR_DISPATCH(launch_bwd, a);
+    return dispatch(*args, ln != 0, mod != 0, s);
 }
 
 SKR_API int skr_lstm_fwd_args_size() { return (int)sizeof(FwdArgs); }

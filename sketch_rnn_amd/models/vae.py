@@ -65,19 +65,19 @@ class Encoder(nn.Module):
         keep = cfg.recurrent_dropout_prob if (train and cfg.use_recurrent_dropout) else 1.0
         xr = reverse_padded(x, lengths)
         zeros = x.new_zeros(B, H)
-        hs = []
-        for p, xin, stream in ((self.fw, x, _S_ENC_FW), (self.bw, xr, _S_ENC_BW)):
+        xps, lns = [], []
+        for p, xin in ((self.fw, x), (self.bw, xr)):
             xp = (xin.reshape(T * B, 5) @ p.W_x).view(T, B, 4 * H)
             if isinstance(p, C.LNLSTMParams):
-                ln = (p.ln_gamma, p.ln_beta, p.lnc_gamma, p.lnc_beta)
+                lns.append((p.ln_gamma, p.ln_beta, p.lnc_gamma, p.lnc_beta))
             else:
                 xp = xp + p.bias
-                ln = None
-            out, _ = ops.lstm_sequence(xp, p.W_h, zeros, zeros, drop_keep=keep, drop_seed=seed,
-                                       drop_stream=stream, ln=ln)
-            idx = (lengths - 1).clamp(min=0).view(1, B, 1).expand(1, B, H)
-            hs.append(torch.gather(out, 0, idx).squeeze(0))
-        last_h = torch.cat(hs, -1)
+                lns.append(None)
+            xps.append(xp)
+        outs = ops.bilstm_sequence(xps[0], xps[1], self.fw.W_h, self.bw.W_h, zeros, zeros, drop_keep=keep,
+                                   drop_seed=seed, drop_stream=_S_ENC_FW, ln_f=lns[0], ln_b=lns[1])
+        idx = (lengths - 1).clamp(min=0).view(1, B, 1).expand(1, B, H)
+        last_h = torch.cat([torch.gather(o, 0, idx).squeeze(0) for o in outs], -1)
         mu = last_h @ self.mu_w + self.mu_b
         presig = last_h @ self.sig_w + self.sig_b
         return mu, presig

@@ -66,6 +66,23 @@ def lstm_sequence(xp, W_h, h0, c0, forget_bias: float = 1.0, reset=None, reset_h
                                drop_keep, drop_seed, drop_stream, ln)
 
 
+def bilstm_sequence(xp_f, xp_b, W_f, W_b, h0, c0, drop_keep: float = 1.0, drop_seed: int = 0,
+                    drop_stream: int = 0, ln_f=None, ln_b=None, forget_bias: float = 1.0):
+    """Two independent recurrences of equal shape (the encoder's forward and
+    backward directions). Returns the two output sequences. One dropout
+    stream covers both as ``2B`` rows (forward rows first)."""
+    if use_hip(xp_f):
+        from .recurrent import bilstm_sequence_hip
+        return bilstm_sequence_hip(xp_f, xp_b, W_f, W_b, h0, c0, drop_keep, drop_seed, (drop_stream, drop_stream),
+                                   ln_f, ln_b, forget_bias)
+    B = xp_f.shape[1]
+    of, _ = lstm_sequence_torch(xp_f, W_f, h0, c0, forget_bias, drop_keep=drop_keep, drop_seed=drop_seed,
+                                drop_stream=drop_stream, ln=ln_f, mask_rows=(2 * B, 0))
+    ob, _ = lstm_sequence_torch(xp_b, W_b, h0, c0, forget_bias, drop_keep=drop_keep, drop_seed=drop_seed,
+                                drop_stream=drop_stream, ln=ln_b, mask_rows=(2 * B, B))
+    return of, ob
+
+
 def hyper_sequence(p, x, h0, c0, hh0, hc0, forget_bias: float = 1.0, drop_keep: float = 1.0,
                    drop_seed: int = 0, drop_stream: int = 0, hyp_drop_keep: float = 1.0):
     if use_hip(x):

@@ -18,9 +18,11 @@ _i = C.c_int
 class LstmFwdArgs(C.Structure):
     _fields_ = [
         ("B", _i), ("H", _i),
+        ("grp_rows", _i),
         ("xp", _p), ("ld_xp", _i64),
         ("R", _p), ("ld_R", _i64),
-        ("vec", _p), ("vec_gs", _i64),
+        ("vec", _p), ("vec_gs", _i64), ("vec_ld", _i64),
+        ("vec_bias", _p),
         ("bias", _p),
         ("c_prev", _p),
         ("ln_g", _p), ("ln_b", _p), ("lnc_g", _p), ("lnc_b", _p),
@@ -38,6 +40,7 @@ class LstmFwdArgs(C.Structure):
 class LstmBwdArgs(C.Structure):
     _fields_ = [
         ("B", _i), ("H", _i),
+        ("grp_rows", _i),
         ("dh_out", _p),
         ("dh_rec", _p), ("ld_dh_rec", _i64),
         ("dc_rec", _p),
@@ -46,13 +49,14 @@ class LstmBwdArgs(C.Structure):
         ("ln_g", _p), ("lnc_g", _p), ("lnc_b", _p),
         ("xp", _p), ("ld_xp", _i64),
         ("R", _p), ("ld_R", _i64),
-        ("vec", _p), ("vec_gs", _i64),
+        ("vec", _p), ("vec_gs", _i64), ("vec_ld", _i64),
+        ("vec_bias", _p),
         ("reset", _p),
         ("keep", _f), ("seed", _p), ("stream", _u32), ("step", _u32),
         ("dG", _p), ("ld_dG", _i64),
         ("dG_lp", _p), ("ld_dG_lp", _i64), ("dG_lp_kind", _i),
         ("dxp", _p), ("ld_dxp", _i64),
-        ("dvec", _p),
+        ("dvec", _p), ("dvec_kind", _i),
         ("dlny", _p), ("dlncy", _p),
         ("dinit_h", _p), ("dinit_c", _p),
     ]
@@ -73,18 +77,10 @@ class HipLib:
         lib.skr_adam_step.restype = _i
         lib.skr_global_norm.argtypes = [_p, _i64, _p, _p, _p]
         lib.skr_global_norm.restype = _i
-        for name in ("skr_sample_step", "skr_decode_lstm_step"):
-            if hasattr(lib, name):
-                getattr(lib, name).restype = _i
         fs, bs = lib.skr_lstm_fwd_args_size(), lib.skr_lstm_bwd_args_size()
         if fs != C.sizeof(LstmFwdArgs) or bs != C.sizeof(LstmBwdArgs):
             raise RuntimeError("libskrnn_hip.so arg-struct layout mismatch: fwd %d vs %d, bwd %d vs %d"
                                % (fs, C.sizeof(LstmFwdArgs), bs, C.sizeof(LstmBwdArgs)))
-
-    @staticmethod
-    def check(rc: int, what: str):
-        if rc != 0:
-            raise RuntimeError("%s failed with code %d" % (what, rc))
 
 
 def bind(lib: C.CDLL) -> HipLib:

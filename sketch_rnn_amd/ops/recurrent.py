@@ -9,8 +9,16 @@ and leaves all weight gradients to single large GEMMs over the whole
 sequence after the scan. Launched from Python but designed to be captured
 whole into a HIP graph (no allocation depends on data, no host sync).
 
-Autograd boundaries are whole sequences (one ``Function`` per layer), so
-no per-step autograd nodes exist.
+* ``_LSTMSeq`` handles ``nd`` independent recurrences of the same shape in
+  one launch per step (``nd = 2``: both directions of the bidirectional
+  encoder as ``2B`` rows, one batched GEMM, per-direction LN parameters).
+* ``_HyperSeq`` folds the two-stage hyper-norm projections
+  ``vec_k = (hh @ W_z_k + b_z_k) @ W_a_k`` into ``vec = hh @ P + q`` with
+  ``P = [W_z_k W_a_k]_k`` built once per call, so each time step costs one
+  extra GEMM forward and one backward; all hyper-projection weight
+  gradients are reduced after the scan from the saved ``dvec`` stream.
+
+Autograd boundaries are whole sequences, so no per-step autograd nodes exist.
 """
 from __future__ import annotations
 
@@ -22,8 +30,6 @@ import torch
 from ..utils import native
 from . import gemm
 from ._hipapi import LstmBwdArgs, LstmFwdArgs
-
-_NULL = None
 
 
 def _ptr(t: Optional[torch.Tensor]):
@@ -53,43 +59,51 @@ class _Saved:
     """Plain holder for the big per-sequence buffers (kept off autograd)."""
 
 
+def _rec_mm(a: torch.Tensor, W: torch.Tensor, out: torch.Tensor, nd: int):
+    """``a [nd*B, K] @ W [nd, K, N] -> out [nd*B, N]`` (fp32 out)."""
+    if nd == 1:
+        return gemm.mm(a, W[0], out=out)
+    B = a.shape[0] // nd
+    return gemm.bmm(a.view(nd, B, -1), W, out=out.view(nd, B, -1))
+
+
 # =====================================================================================
-# LSTM / LayerNorm-LSTM sequence
+# LSTM / LayerNorm-LSTM sequence (nd groups)
 # =====================================================================================
 class _LSTMSeq(torch.autograd.Function):
     @staticmethod
     def forward(ctx, xp, W_h, h0, c0, reset_h, reset_c, ln_g, ln_b, lnc_g, lnc_b, reset, seed, meta):
-        forget_bias, keep, stream = meta
+        forget_bias, keep, stream, nd = meta
         lib = native.require_hip()
-        T, B, G = xp.shape
+        T, BB, G = xp.shape
         H = G // 4
         dev = xp.device
         f32 = torch.float32
         ln = ln_g is not None
         xp = xp.contiguous()
-        Wl = gemm.lp(W_h).contiguous()
+        Wl = gemm.lp(W_h.reshape(nd, H, G)).contiguous()
         ldt = Wl.dtype
-        A = torch.empty(T + 1, B, H, device=dev, dtype=ldt)   # GEMM operands: carried h
+        A = torch.empty(T + 1, BB, H, device=dev, dtype=ldt)   # GEMM operands: carried h
         A[0].copy_(h0)
-        CC = torch.empty(T + 1, B, H, device=dev, dtype=f32)  # carried c
+        CC = torch.empty(T + 1, BB, H, device=dev, dtype=f32)  # carried c
         CC[0].copy_(c0)
-        Hout = torch.empty(T, B, H, device=dev, dtype=f32)
-        Cout = torch.empty(T, B, H, device=dev, dtype=f32)
-        ACT = torch.empty(T, B, 4 * H, device=dev, dtype=f32)
-        XHAT = torch.empty(T, B, 4 * H, device=dev, dtype=f32) if ln else None
-        RSTD = torch.empty(T, B, 5, device=dev, dtype=f32) if ln else None
-        CHAT = torch.empty(T, B, H, device=dev, dtype=f32) if ln else None
-        HC = torch.empty(2, B, H, device=dev, dtype=f32)
-        R = torch.empty(B, 4 * H, device=dev, dtype=f32)
+        Hout = torch.empty(T, BB, H, device=dev, dtype=f32)
+        Cout = torch.empty(T, BB, H, device=dev, dtype=f32)
+        ACT = torch.empty(T, BB, G, device=dev, dtype=f32)
+        XHAT = torch.empty(T, BB, G, device=dev, dtype=f32) if ln else None
+        RSTD = torch.empty(T, BB, 5, device=dev, dtype=f32) if ln else None
+        CHAT = torch.empty(T, BB, H, device=dev, dtype=f32) if ln else None
+        HC = torch.empty(2, BB, H, device=dev, dtype=f32)
+        R = torch.empty(BB, G, device=dev, dtype=f32)
         rst = reset.contiguous().to(f32) if reset is not None else None
         rh = reset_h.contiguous() if reset_h is not None else None
         rc = reset_c.contiguous() if reset_c is not None else None
+        lnp = [t.contiguous() if t is not None else None for t in (ln_g, ln_b, lnc_g, lnc_b)]
         sd = _seed_tensor(seed, dev)
         a = LstmFwdArgs()
-        a.B, a.H = B, H
-        a.ld_xp, a.ld_R = 4 * H, 4 * H
-        a.vec, a.vec_gs, a.bias = None, 0, None
-        a.ln_g, a.ln_b, a.lnc_g, a.lnc_b = _ptr(ln_g), _ptr(ln_b), _ptr(lnc_g), _ptr(lnc_b)
+        a.B, a.H, a.grp_rows = BB, H, BB // nd if nd > 1 else 0
+        a.ld_xp, a.ld_R = G, G
+        a.ln_g, a.ln_b, a.lnc_g, a.lnc_b = (_ptr(t) for t in lnp)
         a.init_h, a.init_c = _ptr(rh), _ptr(rc)
         a.forget_bias, a.keep = float(forget_bias), float(keep)
         a.seed, a.stream = sd.data_ptr(), int(stream)
@@ -97,7 +111,7 @@ class _LSTMSeq(torch.autograd.Function):
         a.R = R.data_ptr()
         st = _stream()
         for t in range(T):
-            gemm.mm(A[t], Wl, out=R)
+            _rec_mm(A[t], Wl, R, nd)
             a.xp = xp[t].data_ptr()
             a.c_prev = CC[t].data_ptr()
             a.reset = _ptr(rst[t]) if rst is not None else None
@@ -113,40 +127,41 @@ class _LSTMSeq(torch.autograd.Function):
         cT = CC[T].clone()
         s = _Saved()
         s.Wl, s.A, s.CC, s.Cout, s.ACT, s.XHAT, s.RSTD, s.CHAT = Wl, A, CC, Cout, ACT, XHAT, RSTD, CHAT
-        s.reset, s.seed, s.meta = rst, sd, meta
-        s.ln_g, s.lnc_g, s.lnc_b = ln_g, lnc_g, lnc_b
-        s.has_reset_state = reset_h is not None
+        s.reset, s.seed, s.meta, s.lnp = rst, sd, meta, lnp
+        s.wshape = W_h.shape
         ctx.s = s
-        ctx.dims = (T, B, H)
+        ctx.dims = (T, BB, H)
         return Hout, hT, cT
 
     @staticmethod
     def backward(ctx, dHout, dhT, dcT):
         s = ctx.s
-        T, B, H = ctx.dims
-        forget_bias, keep, stream = s.meta
+        T, BB, H = ctx.dims
+        G = 4 * H
+        forget_bias, keep, stream, nd = s.meta
+        B = BB // nd
         lib = native.require_hip()
         dev = s.A.device
         f32 = torch.float32
-        ln = s.ln_g is not None
-        dG = torch.empty(T, B, 4 * H, device=dev, dtype=f32)
+        ln = s.lnp[0] is not None
+        dG = torch.empty(T, BB, G, device=dev, dtype=f32)
         lp_on = s.Wl.dtype == torch.bfloat16
-        dG_lp = torch.empty(T, B, 4 * H, device=dev, dtype=torch.bfloat16) if lp_on else None
-        dh_rec = dhT.contiguous().clone() if dhT is not None else torch.zeros(B, H, device=dev, dtype=f32)
-        dc_rec = dcT.contiguous().clone() if dcT is not None else torch.zeros(B, H, device=dev, dtype=f32)
+        dG_lp = torch.empty(T, BB, G, device=dev, dtype=torch.bfloat16) if lp_on else None
+        dh_rec = dhT.contiguous().clone() if dhT is not None else torch.zeros(BB, H, device=dev, dtype=f32)
+        dc_rec = dcT.contiguous().clone() if dcT is not None else torch.zeros(BB, H, device=dev, dtype=f32)
         dHout = dHout.contiguous() if dHout is not None else None
-        dinit_h = torch.zeros(B, H, device=dev, dtype=f32) if s.reset is not None else None
-        dinit_c = torch.zeros(B, H, device=dev, dtype=f32) if s.reset is not None else None
-        DLNY = torch.empty(T, B, 4 * H, device=dev, dtype=f32) if ln else None
-        DLNCY = torch.empty(T, B, H, device=dev, dtype=f32) if ln else None
-        WT = s.Wl.t()
+        dinit_h = torch.zeros(BB, H, device=dev, dtype=f32) if s.reset is not None else None
+        dinit_c = torch.zeros(BB, H, device=dev, dtype=f32) if s.reset is not None else None
+        DLNY = torch.empty(T, BB, G, device=dev, dtype=f32) if ln else None
+        DLNCY = torch.empty(T, BB, H, device=dev, dtype=f32) if ln else None
+        WT = s.Wl.transpose(1, 2)
         a = LstmBwdArgs()
-        a.B, a.H = B, H
+        a.B, a.H, a.grp_rows = BB, H, B if nd > 1 else 0
         a.ld_dh_rec = H
         a.dh_rec, a.dc_rec = dh_rec.data_ptr(), dc_rec.data_ptr()
-        a.ln_g, a.lnc_g, a.lnc_b = _ptr(s.ln_g), _ptr(s.lnc_g), _ptr(s.lnc_b)
+        a.ln_g, a.lnc_g, a.lnc_b = _ptr(s.lnp[0]), _ptr(s.lnp[2]), _ptr(s.lnp[3])
         a.keep, a.seed, a.stream = float(keep), s.seed.data_ptr(), int(stream)
-        a.ld_dG, a.ld_dG_lp, a.dG_lp_kind = 4 * H, 4 * H, 1 if lp_on else 0
+        a.ld_dG, a.ld_dG_lp, a.dG_lp_kind = G, G, 1 if lp_on else 0
         a.dinit_h, a.dinit_c = _ptr(dinit_h), _ptr(dinit_c)
         st = _stream()
         for t in range(T - 1, -1, -1):
@@ -160,18 +175,21 @@ class _LSTMSeq(torch.autograd.Function):
             a.dG = dG[t].data_ptr()
             a.dG_lp = dG_lp[t].data_ptr() if lp_on else None
             _check(lib.lib.skr_lstm_bwd_step(ctypes.byref(a), int(ln), 0, st), "lstm_bwd_step")
-            gemm.mm(dG_lp[t] if lp_on else dG[t], WT, out=dh_rec)
-        dGm = (dG_lp if lp_on else dG).view(T * B, 4 * H)
-        dW = gemm.mm(s.A[:T].reshape(T * B, H).t(), dGm)
+            _rec_mm(dG_lp[t] if lp_on else dG[t], WT, dh_rec, nd)
+        dGs = dG_lp if lp_on else dG
+        if nd == 1:
+            dW = gemm.mm(s.A[:T].reshape(T * BB, H).t(), dGs.view(T * BB, G)).view(s.wshape)
+        else:
+            An = s.A[:T].view(T, nd, B, H).permute(1, 0, 2, 3).reshape(nd, T * B, H)
+            dGn = dGs.view(T, nd, B, G).permute(1, 0, 2, 3).reshape(nd, T * B, G)
+            dW = gemm.bmm(An.transpose(1, 2), dGn).view(s.wshape)
         g_ln = [None] * 4
         if ln:
-            xh = s.XHAT.view(T * B, 4 * H)
-            dl = DLNY.view(T * B, 4 * H)
-            g_ln = [(dl * xh).sum(0), dl.sum(0),
-                    (DLNCY.view(T * B, H) * s.CHAT.view(T * B, H)).sum(0), DLNCY.view(T * B, H).sum(0)]
-        dh0, dc0 = dh_rec, dc_rec
+            def red(x, n):
+                return x.view(T, nd, B, n).sum((0, 2)).view(s.lnp[0].shape[:-1] + (n,))
+            g_ln = [red(DLNY * s.XHAT, G), red(DLNY, G), red(DLNCY * s.CHAT, H), red(DLNCY, H)]
         ctx.s = None
-        return (dG, dW, dh0, dc0, dinit_h, dinit_c, g_ln[0], g_ln[1], g_ln[2], g_ln[3], None, None, None)
+        return (dG, dW, dh_rec, dc_rec, dinit_h, dinit_c, g_ln[0], g_ln[1], g_ln[2], g_ln[3], None, None, None)
 
 
 def lstm_sequence_hip(xp, W_h, h0, c0, forget_bias=1.0, reset=None, reset_h=None, reset_c=None,
@@ -181,8 +199,27 @@ def lstm_sequence_hip(xp, W_h, h0, c0, forget_bias=1.0, reset=None, reset_h=None
     if reset is not None and reset_h is None:
         raise ValueError("reset requires reset_h / reset_c")
     Hout, hT, cT = _LSTMSeq.apply(xp, W_h, h0, c0, reset_h, reset_c, *ln, reset, drop_seed,
-                                  (float(forget_bias), float(drop_keep), int(drop_stream)))
+                                  (float(forget_bias), float(drop_keep), int(drop_stream), 1))
     return Hout, (hT, cT)
+
+
+def bilstm_sequence_hip(xp_f, xp_b, W_f, W_b, h0, c0, drop_keep=1.0, drop_seed=0, streams=(0, 0),
+                        ln_f=None, ln_b=None, forget_bias=1.0):
+    """Both encoder directions in one launch per step (2B rows). Each
+    direction keeps its own dropout stream via the row index (rows of the
+    backward direction are offset by B*H in the hash index)."""
+    B = xp_f.shape[1]
+    xp = torch.cat([xp_f, xp_b], 1)
+    W = torch.stack([W_f, W_b], 0)
+    h = torch.cat([h0, h0], 0)
+    c = torch.cat([c0, c0], 0)
+    if ln_f is not None:
+        ln = tuple(torch.stack([a, b], 0) for a, b in zip(ln_f, ln_b))
+    else:
+        ln = (None, None, None, None)
+    Hout, hT, cT = _LSTMSeq.apply(xp, W, h, c, None, None, *ln, None, drop_seed,
+                                  (float(forget_bias), float(drop_keep), int(streams[0]), 2))
+    return Hout[:, :B], Hout[:, B:]
 
 
 # =====================================================================================
@@ -200,7 +237,8 @@ class _HyperSeq(torch.autograd.Function):
         K, N = H + Hh, G + Gh
         dev = x.device
         f32 = torch.float32
-        x2 = x.reshape(T * B, IN).contiguous()
+        TB = T * B
+        x2 = x.reshape(TB, IN).contiguous()
         xl = gemm.lp(x2)
         XH = gemm.mm(xl, gemm.lp(W_x)).view(T, B, G)
         XHY = gemm.mm(xl, gemm.lp(hW_x[:IN])).view(T, B, Gh)
@@ -209,6 +247,11 @@ class _HyperSeq(torch.autograd.Function):
         Wcat[:H, :G].copy_(W_h)
         Wcat[:H, G:].copy_(hW_x[IN:])
         Wcat[H:, G:].copy_(hW_h)
+        # hyper-norm projections folded: vec = hh @ P + q
+        Wz3 = W_z.view(Hh, 12, E).permute(1, 0, 2)                 # [12, Hh, E]
+        P = torch.bmm(Wz3, W_a).permute(1, 0, 2).reshape(Hh, 12 * H)  # [Hh, 12H]
+        q = torch.bmm(b_z.view(12, 1, E), W_a).reshape(12, H).contiguous()
+        Pl = P.to(dt).contiguous()
         A = torch.empty(T + 1, B, K, device=dev, dtype=dt)
         A[0, :, :H].copy_(h0)
         A[0, :, H:].copy_(hh0)
@@ -229,16 +272,17 @@ class _HyperSeq(torch.autograd.Function):
         HXHAT = torch.empty(T, B, Gh, device=dev, dtype=f32)
         HRSTD = torch.empty(T, B, 5, device=dev, dtype=f32)
         HCHAT = torch.empty(T, B, Hh, device=dev, dtype=f32)
-        ZS = torch.empty(T, B, 12 * E, device=dev, dtype=f32)
-        VEC = torch.empty(T, 12, B, H, device=dev, dtype=f32)
+        VEC = torch.empty(T, B, 12 * H, device=dev, dtype=f32)
         HC = torch.empty(2, B, H, device=dev, dtype=f32)
         HHC = torch.empty(2, B, Hh, device=dev, dtype=f32)
         sd = _seed_tensor(seed, dev)
+        hln = [t.contiguous() for t in (hln_g, hln_b, hlnc_g, hlnc_b)]
+        mln = [t.contiguous() for t in (ln_g, ln_b, lnc_g, lnc_b)]
         # hyper cell args (LN-LSTM, no modulation)
         ah = LstmFwdArgs()
         ah.B, ah.H = B, Hh
         ah.ld_xp, ah.ld_R = Gh, N
-        ah.ln_g, ah.ln_b, ah.lnc_g, ah.lnc_b = hln_g.data_ptr(), hln_b.data_ptr(), hlnc_g.data_ptr(), hlnc_b.data_ptr()
+        ah.ln_g, ah.ln_b, ah.lnc_g, ah.lnc_b = (t.data_ptr() for t in hln)
         ah.forget_bias, ah.keep = float(forget_bias), float(hkeep)
         ah.seed, ah.stream = sd.data_ptr(), int(stream) + 1
         ah.ld_lp, ah.lp_kind = K, _lp_kind(A)
@@ -246,13 +290,11 @@ class _HyperSeq(torch.autograd.Function):
         am = LstmFwdArgs()
         am.B, am.H = B, H
         am.ld_xp, am.ld_R = G, N
-        am.vec_gs, am.bias = B * H, bias.data_ptr()
-        am.ln_g, am.ln_b, am.lnc_g, am.lnc_b = ln_g.data_ptr(), ln_b.data_ptr(), lnc_g.data_ptr(), lnc_b.data_ptr()
+        am.vec_gs, am.vec_ld, am.vec_bias, am.bias = H, 12 * H, q.data_ptr(), bias.contiguous().data_ptr()
+        am.ln_g, am.ln_b, am.lnc_g, am.lnc_b = (t.data_ptr() for t in mln)
         am.forget_bias, am.keep = float(forget_bias), float(keep)
         am.seed, am.stream = sd.data_ptr(), int(stream)
         am.ld_lp, am.lp_kind = K, _lp_kind(A)
-        Wz = W_z.contiguous()
-        Wa = W_a.contiguous()
         st = _stream()
         for t in range(T):
             gemm.mm(A[t], Wcat, out=RC[t])
@@ -262,8 +304,7 @@ class _HyperSeq(torch.autograd.Function):
             ah.xhat, ah.rstd, ah.chat = HXHAT[t].data_ptr(), HRSTD[t].data_ptr(), HCHAT[t].data_ptr()
             ah.h_carry, ah.h_lp, ah.c_carry = HHC[t % 2].data_ptr(), A[t + 1, :, H:].data_ptr(), HCC[t + 1].data_ptr()
             _check(lib.lib.skr_lstm_fwd_step(ctypes.byref(ah), 1, 0, st), "hyper_fwd_step")
-            torch.addmm(b_z, HH[t], Wz, out=ZS[t])
-            torch.bmm(ZS[t].view(B, 12, E).transpose(0, 1), Wa, out=VEC[t])
+            gemm.mm(A[t + 1, :, H:], Pl, out=VEC[t])
             am.xp, am.R, am.vec = XH[t].data_ptr(), RC[t, :, :G].data_ptr(), VEC[t].data_ptr()
             am.c_prev, am.step = CC[t].data_ptr(), t
             am.h_out, am.c_out, am.act = Hout[t].data_ptr(), Cout[t].data_ptr(), ACT[t].data_ptr()
@@ -273,10 +314,10 @@ class _HyperSeq(torch.autograd.Function):
         hT = HC[(T - 1) % 2].clone()
         hhT = HHC[(T - 1) % 2].clone()
         s = _Saved()
-        for k, v in dict(xl=xl, XH=XH, Wcat=Wcat, A=A, RC=RC, CC=CC, HCC=HCC, Cout=Cout, ACT=ACT, XHAT=XHAT,
-                         RSTD=RSTD, CHAT=CHAT, HH=HH, HCout=HCout, HACT=HACT, HXHAT=HXHAT, HRSTD=HRSTD,
-                         HCHAT=HCHAT, ZS=ZS, VEC=VEC, seed=sd, meta=meta, W_x=W_x, hW_x=hW_x, Wz=Wz, Wa=Wa,
-                         ln_g=ln_g, lnc_g=lnc_g, lnc_b=lnc_b, hln_g=hln_g, hlnc_g=hlnc_g, hlnc_b=hlnc_b).items():
+        for k, v in dict(xl=xl, XH=XH, Wcat=Wcat, Pl=Pl, q=q, A=A, RC=RC, CC=CC, HCC=HCC, Cout=Cout, ACT=ACT,
+                         XHAT=XHAT, RSTD=RSTD, CHAT=CHAT, HH=HH, HCout=HCout, HACT=HACT, HXHAT=HXHAT, HRSTD=HRSTD,
+                         HCHAT=HCHAT, VEC=VEC, seed=sd, meta=meta, W_x=W_x, hW_x=hW_x, W_z=W_z, b_z=b_z,
+                         W_a=W_a, mln=mln, hln=hln).items():
             setattr(s, k, v)
         ctx.s = s
         ctx.dims = (T, B, IN, H, Hh, E)
@@ -292,7 +333,9 @@ class _HyperSeq(torch.autograd.Function):
         f32 = torch.float32
         G, Gh = 4 * H, 4 * Hh
         K, N = H + Hh, G + Gh
+        TB = T * B
         lp_on = s.Wcat.dtype == torch.bfloat16
+        ldt = torch.bfloat16 if lp_on else f32
         dRC = torch.empty(T, B, N, device=dev, dtype=f32)
         dRC_lp = torch.empty(T, B, N, device=dev, dtype=torch.bfloat16) if lp_on else None
         dXH = torch.empty(T, B, G, device=dev, dtype=f32)
@@ -300,11 +343,7 @@ class _HyperSeq(torch.autograd.Function):
         DLNCY = torch.empty(T, B, H, device=dev, dtype=f32)
         HDLNY = torch.empty(T, B, Gh, device=dev, dtype=f32)
         HDLNCY = torch.empty(T, B, Hh, device=dev, dtype=f32)
-        dZS = torch.empty(T, B, 12 * E, device=dev, dtype=f32)
-        dvec = torch.empty(12, B, H, device=dev, dtype=f32)
-        dzs12 = torch.empty(12, B, E, device=dev, dtype=f32)
-        dWa = torch.zeros(12, E, H, device=dev, dtype=f32)
-        dbias = torch.zeros(4, H, device=dev, dtype=f32)
+        dVEC = torch.empty(T, B, 12 * H, device=dev, dtype=ldt)
         dhh_z = torch.empty(B, Hh, device=dev, dtype=f32)
         dA = torch.zeros(B, K, device=dev, dtype=f32)
         if dhT is not None:
@@ -315,21 +354,21 @@ class _HyperSeq(torch.autograd.Function):
         dhc_rec = dhcT.contiguous().clone() if dhcT is not None else torch.zeros(B, Hh, device=dev, dtype=f32)
         dHout = dHout.contiguous() if dHout is not None else None
         WcT = s.Wcat.t()
-        WzT = s.Wz.t()
-        WaT = s.Wa.transpose(1, 2)
+        PT = s.Pl.t()
         am = LstmBwdArgs()
         am.B, am.H = B, H
         am.dh_rec, am.ld_dh_rec, am.dc_rec = dA.data_ptr(), K, dc_rec.data_ptr()
-        am.ln_g, am.lnc_g, am.lnc_b = s.ln_g.data_ptr(), s.lnc_g.data_ptr(), s.lnc_b.data_ptr()
-        am.ld_xp, am.ld_R, am.vec_gs = G, N, B * H
+        am.ln_g, am.lnc_g, am.lnc_b = s.mln[0].data_ptr(), s.mln[2].data_ptr(), s.mln[3].data_ptr()
+        am.ld_xp, am.ld_R = G, N
+        am.vec_gs, am.vec_ld, am.vec_bias = H, 12 * H, s.q.data_ptr()
         am.keep, am.seed, am.stream = float(keep), s.seed.data_ptr(), int(stream)
         am.ld_dG, am.ld_dG_lp, am.dG_lp_kind = N, N, 1 if lp_on else 0
-        am.ld_dxp, am.dvec = G, dvec.data_ptr()
+        am.ld_dxp, am.dvec_kind = G, 1 if lp_on else 2
         ah = LstmBwdArgs()
         ah.B, ah.H = B, Hh
         ah.dh_out = dhh_z.data_ptr()
         ah.dh_rec, ah.ld_dh_rec, ah.dc_rec = dA[:, H:].data_ptr(), K, dhc_rec.data_ptr()
-        ah.ln_g, ah.lnc_g, ah.lnc_b = s.hln_g.data_ptr(), s.hlnc_g.data_ptr(), s.hlnc_b.data_ptr()
+        ah.ln_g, ah.lnc_g, ah.lnc_b = s.hln[0].data_ptr(), s.hln[2].data_ptr(), s.hln[3].data_ptr()
         ah.keep, ah.seed, ah.stream = float(hkeep), s.seed.data_ptr(), int(stream) + 1
         ah.ld_dG, ah.ld_dG_lp, ah.dG_lp_kind = N, N, 1 if lp_on else 0
         st = _stream()
@@ -341,15 +380,10 @@ class _HyperSeq(torch.autograd.Function):
             am.step = t
             am.dG = dRC[t, :, :G].data_ptr()
             am.dG_lp = dRC_lp[t, :, :G].data_ptr() if lp_on else None
-            am.dxp = dXH[t].data_ptr()
+            am.dxp, am.dvec = dXH[t].data_ptr(), dVEC[t].data_ptr()
             am.dlny, am.dlncy = DLNY[t].data_ptr(), DLNCY[t].data_ptr()
             _check(lib.lib.skr_lstm_bwd_step(ctypes.byref(am), 1, 1, st), "hyper_main_bwd_step")
-            # hyper-norm projections: vec = zs @ W_a (per block)
-            torch.bmm(dvec, WaT, out=dzs12)
-            dWa.baddbmm_(s.ZS[t].view(B, 12, E).permute(1, 2, 0), dvec)
-            dbias.add_(dvec[8:12].sum(1))
-            dZS[t].view(B, 12, E).copy_(dzs12.transpose(0, 1))
-            torch.mm(dZS[t], WzT, out=dhh_z)
+            gemm.mm(dVEC[t], PT, out=dhh_z)
             ah.act, ah.c_new, ah.c_prev = s.HACT[t].data_ptr(), s.HCout[t].data_ptr(), s.HCC[t].data_ptr()
             ah.xhat, ah.rstd, ah.chat = s.HXHAT[t].data_ptr(), s.HRSTD[t].data_ptr(), s.HCHAT[t].data_ptr()
             ah.step = t
@@ -358,7 +392,7 @@ class _HyperSeq(torch.autograd.Function):
             ah.dlny, ah.dlncy = HDLNY[t].data_ptr(), HDLNCY[t].data_ptr()
             _check(lib.lib.skr_lstm_bwd_step(ctypes.byref(ah), 1, 0, st), "hyper_bwd_step")
             gemm.mm(dRC_lp[t] if lp_on else dRC[t], WcT, out=dA)
-        TB = T * B
+        # ---- weight gradients: single large GEMMs over all T*B rows ----
         dRCm = (dRC_lp if lp_on else dRC).view(TB, N)
         dWcat = gemm.mm(s.A[:T].reshape(TB, K).t(), dRCm)
         dW_h = dWcat[:H, :G]
@@ -366,24 +400,32 @@ class _HyperSeq(torch.autograd.Function):
         dhW_x[IN:] = dWcat[:H, G:]
         dhW_h = dWcat[H:, G:]
         dXHY = dRC[:, :, G:].reshape(TB, Gh)
-        dXHm = dXH.view(TB, G)
-        dXHl, dXHYl = gemm.lp(dXHm), gemm.lp(dXHY)
+        dXHl, dXHYl = gemm.lp(dXH.view(TB, G)), gemm.lp(dXHY)
         dW_x = gemm.mm(s.xl.t(), dXHl)
         dhW_x[:IN] = gemm.mm(s.xl.t(), dXHYl)
         dx = gemm.mm(dXHl, gemm.lp(s.W_x).t())
         dx += gemm.mm(dXHYl, gemm.lp(s.hW_x[:IN]).t())
-        dZSm = dZS.view(TB, 12 * E)
-        dW_z = s.HH.view(TB, Hh).t() @ dZSm
-        db_z = dZSm.sum(0)
+        # hyper-norm projections: vec_k = zs_k @ W_a[k], zs = hh @ W_z + b_z
+        dV12 = dVEC.view(TB, 12, H).transpose(0, 1)                    # [12, TB, H] (strided)
+        Wal = gemm.lp(s.W_a)
+        dZS12 = gemm.bmm(dV12, Wal.transpose(1, 2))                    # [12, TB, E]
+        HHm = s.HH.view(TB, Hh)
+        ZS = torch.addmm(s.b_z, HHm, s.W_z)                            # [TB, 12E]
+        ZS12 = gemm.lp(ZS.view(TB, 12, E).transpose(0, 1))             # [12, TB, E]
+        dWa = gemm.bmm(ZS12.transpose(1, 2), dV12)                     # [12, E, H]
+        dZS = dZS12.transpose(0, 1).reshape(TB, 12 * E)
+        dW_z = HHm.t() @ dZS
+        db_z = dZS.sum(0)
+        dbias = torch.sum(dVEC.view(TB, 12, H)[:, 8:12], 0, dtype=f32).reshape(G)
+        red = lambda a, b_: (a * b_).sum(0)
         xh, dl = s.XHAT.view(TB, G), DLNY.view(TB, G)
-        g_ln = ((dl * xh).sum(0), dl.sum(0), (DLNCY.view(TB, H) * s.CHAT.view(TB, H)).sum(0),
-                DLNCY.view(TB, H).sum(0))
+        g_ln = (red(dl, xh), dl.sum(0), red(DLNCY.view(TB, H), s.CHAT.view(TB, H)), DLNCY.view(TB, H).sum(0))
         hxh, hdl = s.HXHAT.view(TB, Gh), HDLNY.view(TB, Gh)
-        g_hln = ((hdl * hxh).sum(0), hdl.sum(0), (HDLNCY.view(TB, Hh) * s.HCHAT.view(TB, Hh)).sum(0),
+        g_hln = (red(hdl, hxh), hdl.sum(0), red(HDLNCY.view(TB, Hh), s.HCHAT.view(TB, Hh)),
                  HDLNCY.view(TB, Hh).sum(0))
         dh0, dhh0 = dA[:, :H].contiguous(), dA[:, H:].contiguous()
         ctx.s = None
-        return (dx.view(T, B, IN), dh0, dc_rec, dhh0, dhc_rec, None, dW_x, dW_h, dbias.view(G), dhW_x, dhW_h,
+        return (dx.view(T, B, IN), dh0, dc_rec, dhh0, dhc_rec, None, dW_x, dW_h, dbias, dhW_x, dhW_h,
                 g_hln[0], g_hln[1], g_hln[2], g_hln[3], dW_z, db_z, dWa, g_ln[0], g_ln[1], g_ln[2], g_ln[3], None)
 
 

@@ -18,23 +18,27 @@ def lstm_sequence_torch(xp: torch.Tensor, W_h: torch.Tensor, h0: torch.Tensor, c
                         forget_bias: float = 1.0, reset: Optional[torch.Tensor] = None,
                         reset_h: Optional[torch.Tensor] = None, reset_c: Optional[torch.Tensor] = None,
                         drop_keep: float = 1.0, drop_seed: int = 0, drop_stream: int = 0,
-                        ln: Optional[Tuple[torch.Tensor, ...]] = None):
+                        ln: Optional[Tuple[torch.Tensor, ...]] = None, mask_rows: Optional[Tuple[int, int]] = None):
     """LSTM / LayerNorm-LSTM recurrence.
 
     ``reset[t, b] != 0`` replaces the state carried out of step ``t`` with
     ``(reset_h, reset_c)`` -- the reference's end-of-character reset
     (``model.py:82-92``). Outputs are the un-reset cell outputs.
     ``ln = (ln_gamma, ln_beta, lnc_gamma, lnc_beta)`` selects LayerNorm-LSTM.
+    ``mask_rows = (total, offset)``: this recurrence's rows are rows
+    ``offset .. offset+B`` of a ``total``-row dropout mask (bidirectional
+    encoder: both directions share one mask stream, as in the fused kernel).
     """
     T, B, G = xp.shape
     H = G // 4
     h, c = h0, c0
     outs = []
+    total, off = mask_rows if mask_rows is not None else (B, 0)
     for t in range(T):
         g = xp[t] + h @ W_h
         drop = None
         if drop_keep < 1.0:
-            drop = C.dropout_mask(drop_seed, drop_stream, t, (B, H), drop_keep, xp.device)
+            drop = C.dropout_mask(drop_seed, drop_stream, t, (total, H), drop_keep, xp.device)[off:off + B]
         if ln is None:
             h_new, c_new = C.lstm_pointwise(g, c, forget_bias, drop)
         else:

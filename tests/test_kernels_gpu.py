@@ -89,6 +89,35 @@ def test_lstm_sequence_matches_oracle(H, ln, reset, keep):
     _close(g_h, g_t, 1e-3, 1e-4, "grad")
 
 
+@pytest.mark.parametrize("H,ln,keep", [(64, False, 1.0), (512, False, 0.9), (96, True, 0.8)])
+def test_bilstm_sequence_matches_oracle(H, ln, keep):
+    torch.manual_seed(5)
+    T, B = 6, 4
+    xs = [torch.randn(T, B, 4 * H, device=DEV, requires_grad=True) for _ in range(2)]
+    Ws = [(torch.randn(H, 4 * H, device=DEV) / math.sqrt(H)).requires_grad_() for _ in range(2)]
+    h0 = torch.zeros(B, H, device=DEV)
+    lnp = []
+    if ln:
+        for _ in range(2):
+            lnp += [torch.randn(4 * H, device=DEV).mul(0.1).add(1).requires_grad_(),
+                    torch.randn(4 * H, device=DEV).mul(0.1).requires_grad_(),
+                    torch.randn(H, device=DEV).mul(0.1).add(1).requires_grad_(),
+                    torch.randn(H, device=DEV).mul(0.1).requires_grad_()]
+    seed = torch.tensor([3], device=DEV)
+
+    def fn(xf, xb, Wf, Wb, *lnp):
+        lf, lb = (tuple(lnp[:4]), tuple(lnp[4:])) if ln else (None, None)
+        of, ob = ops.bilstm_sequence(xf, xb, Wf, Wb, h0, h0, drop_keep=keep, drop_seed=seed, drop_stream=11,
+                                     ln_f=lf, ln_b=lb)
+        return [of, ob]
+
+    inputs = xs + Ws + lnp
+    o_h, g_h = _run("hip", fn, inputs)
+    o_t, g_t = _run("torch", fn, inputs)
+    _close(o_h, o_t, 1e-4, 1e-5, "out")
+    _close(g_h, g_t, 1e-3, 1e-4, "grad")
+
+
 def test_lstm_sequence_bf16_close():
     torch.manual_seed(1)
     T, B, H = 9, 8, 512
