@@ -37,6 +37,7 @@ struct FwdArgs {
     int grp_rows;                      // rows per parameter group (0: one group)
     const float* xp; int64_t ld_xp;    // [B, 4H]: x-projection (+bias unless MOD)
     const float* R;  int64_t ld_R;     // [B, 4H]: h_prev @ W_h (fp32)
+    int R_nslab; int64_t R_slab;       // R is the sum of R_nslab split-K partial slabs
     const float* vec; int64_t vec_gs; int64_t vec_ld;  // MOD: element (k,b,u) at k*gs + b*ld + u
     const float* vec_bias;             // MOD: [12, H] added to vec (or null)
     const float* bias;                 // MOD: [4H]
@@ -61,14 +62,17 @@ struct BwdArgs {
     int B, H;
     int grp_rows;
     const float* dh_out;               // [B, H] or null
+    int dho_nslab; int64_t dho_slab;
     const float* dh_rec;               // [B, H] (grad into carried h_t) or null
     int64_t ld_dh_rec;
+    int dhr_nslab; int64_t dhr_slab;
     float* dc_rec;                     // [B, H] in: grad into carried c_t; out: into carried c_{t-1}
     const float* act; const float* c_new; const float* c_prev;
     const float* xhat; const float* rstd; const float* chat;
     const float* ln_g; const float* lnc_g; const float* lnc_b;
     const float* xp; int64_t ld_xp;    // MOD: xh
     const float* R;  int64_t ld_R;     // MOD: R
+    int R_nslab; int64_t R_slab;
     const float* vec; int64_t vec_gs; int64_t vec_ld;  // MOD
     const float* vec_bias;
     const float* reset;
@@ -81,6 +85,13 @@ struct BwdArgs {
     float* dlncy;                      // LN: [B, H]  grad wrt LN(c) output
     float* dinit_h; float* dinit_c;    // [B, H] accumulated on reset rows (or null)
 };
+
+// Sum of n split-K partial slabs (n <= 1: a plain load).
+__device__ __forceinline__ float ld_slabs(const float* p, int64_t idx, int n, int64_t slab) {
+    float v = p[idx];
+    for (int s = 1; s < n; ++s) v += p[s * slab + idx];
+    return v;
+}
 
 __device__ __forceinline__ float vec_at(const float* v, const float* vb, int64_t gs, int64_t ld, int k, int b, int u,
                                         int H) {
@@ -112,7 +123,7 @@ __global__ __launch_bounds__(NT) void lstm_fwd_kernel(const FwdArgs a) {
             float v = 0.f;
             if (act_u[k]) {
                 const float xv = a.xp[b * a.ld_xp + q * H + u];
-                const float rv = a.R[b * a.ld_R + q * H + u];
+                const float rv = ld_slabs(a.R, b * a.ld_R + q * H + u, a.R_nslab, a.R_slab);
                 if (MOD) {
                     v = xv * vec_at(a.vec, a.vec_bias, a.vec_gs, a.vec_ld, q, b, u, H) +
                         rv * vec_at(a.vec, a.vec_bias, a.vec_gs, a.vec_ld, 4 + q, b, u, H) +
@@ -259,9 +270,9 @@ __global__ __launch_bounds__(NT) void lstm_bwd_kernel(const BwdArgs a) {
         const int64_t ro = (int64_t)b * H + u;
         float dcv = 0.f, dov = 0.f, dchv = 0.f, chv = 0.f;
         if (act_u[k]) {
-            const float dhc = a.dh_rec ? a.dh_rec[b * a.ld_dh_rec + u] : 0.f;
+            const float dhc = a.dh_rec ? ld_slabs(a.dh_rec, b * a.ld_dh_rec + u, a.dhr_nslab, a.dhr_slab) : 0.f;
             const float dcc = a.dc_rec[ro];
-            const float dh = (a.dh_out ? a.dh_out[ro] : 0.f) + (r ? 0.f : dhc);
+            const float dh = (a.dh_out ? ld_slabs(a.dh_out, ro, a.dho_nslab, a.dho_slab) : 0.f) + (r ? 0.f : dhc);
             dcv = r ? 0.f : dcc;
             if (r && a.dinit_h) {
                 a.dinit_h[ro] += dhc;
@@ -363,7 +374,7 @@ __global__ __launch_bounds__(NT) void lstm_bwd_kernel(const BwdArgs a) {
             float dr = dg;
             if (MOD) {
                 const float xv = a.xp[b * a.ld_xp + q * H + u];
-                const float rv = a.R[b * a.ld_R + q * H + u];
+                const float rv = ld_slabs(a.R, b * a.ld_R + q * H + u, a.R_nslab, a.R_slab);
                 a.dxp[b * a.ld_dxp + q * H + u] = dg * vec_at(a.vec, a.vec_bias, a.vec_gs, a.vec_ld, q, b, u, H);
                 dr = dg * vec_at(a.vec, a.vec_bias, a.vec_gs, a.vec_ld, 4 + q, b, u, H);
                 const int64_t o0 = (int64_t)b * a.vec_ld + u;

@@ -21,6 +21,7 @@ class LstmFwdArgs(C.Structure):
         ("grp_rows", _i),
         ("xp", _p), ("ld_xp", _i64),
         ("R", _p), ("ld_R", _i64),
+        ("R_nslab", _i), ("R_slab", _i64),
         ("vec", _p), ("vec_gs", _i64), ("vec_ld", _i64),
         ("vec_bias", _p),
         ("bias", _p),
@@ -42,13 +43,16 @@ class LstmBwdArgs(C.Structure):
         ("B", _i), ("H", _i),
         ("grp_rows", _i),
         ("dh_out", _p),
+        ("dho_nslab", _i), ("dho_slab", _i64),
         ("dh_rec", _p), ("ld_dh_rec", _i64),
+        ("dhr_nslab", _i), ("dhr_slab", _i64),
         ("dc_rec", _p),
         ("act", _p), ("c_new", _p), ("c_prev", _p),
         ("xhat", _p), ("rstd", _p), ("chat", _p),
         ("ln_g", _p), ("lnc_g", _p), ("lnc_b", _p),
         ("xp", _p), ("ld_xp", _i64),
         ("R", _p), ("ld_R", _i64),
+        ("R_nslab", _i), ("R_slab", _i64),
         ("vec", _p), ("vec_gs", _i64), ("vec_ld", _i64),
         ("vec_bias", _p),
         ("reset", _p),
@@ -77,6 +81,9 @@ class HipLib:
         lib.skr_adam_step.restype = _i
         lib.skr_global_norm.argtypes = [_p, _i64, _p, _p, _p]
         lib.skr_global_norm.restype = _i
+        lib.skr_skinny_gemm.argtypes = [_p, _i64, _i64, _p, _i64, _i64, _p, _i64, _i64, _i64, _i, _i, _i, _i, _i,
+                                        _p]
+        lib.skr_skinny_gemm.restype = _i
         fs, bs = lib.skr_lstm_fwd_args_size(), lib.skr_lstm_bwd_args_size()
         if fs != C.sizeof(LstmFwdArgs) or bs != C.sizeof(LstmBwdArgs):
             raise RuntimeError("libskrnn_hip.so arg-struct layout mismatch: fwd %d vs %d, bwd %d vs %d"

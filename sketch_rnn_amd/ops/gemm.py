@@ -45,6 +45,53 @@ def bmm(a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor] = None) ->
     return torch.bmm(a, b, out_dtype=torch.float32)
 
 
+_SPLITS = (1, 2, 3, 4, 6, 8, 12, 16, 24, 32)
+
+
+def plan_splits(M: int, N: int, K: int, batch: int = 1, dtype: torch.dtype = _BF16, max_splits: int = 32) -> int:
+    """Split-K factor for :func:`rec_gemm`: aim for 256-512 workgroups.
+    Returns 0 when the native skinny kernel cannot take the shape."""
+    if dtype != _BF16 or M > 128 or N % 64 or K % 64:
+        return 0
+    tiles = (N // 64) * batch
+    best = 1
+    for s in _SPLITS:
+        if s > max_splits or (K // 64) % s:
+            continue
+        if tiles * s > 512:
+            break
+        best = s
+        if tiles * s >= 256:
+            break
+    return best
+
+
+def rec_gemm(a: torch.Tensor, bt: torch.Tensor, out: torch.Tensor, splits: int, nd: int = 1) -> torch.Tensor:
+    """Per-step recurrent product with split-K partial slabs.
+
+    ``a [nd*M, K]`` (row stride may exceed K), ``bt [nd, N, K]`` (B^T, i.e.
+    K-contiguous), ``out [S, nd*M, N]`` fp32 with ``S = max(splits, 1)``:
+    ``sum_s out[s] = a @ bt^T``. ``splits == 0`` selects the library path
+    (one slab). The fused cell kernels sum the slabs while loading.
+    """
+    M = a.shape[0] // nd
+    N, K = bt.shape[-2], bt.shape[-1]
+    if splits <= 0 or not a.is_cuda:
+        if nd == 1:
+            mm(a, bt.reshape(N, K).t(), out=out[0])
+        else:
+            bmm(a.reshape(nd, M, K), bt.transpose(1, 2), out=out[0].view(nd, M, N))
+        return out
+    from ..utils import native
+    lib = native.require_hip()
+    rc = lib.lib.skr_skinny_gemm(a.data_ptr(), a.stride(0), M * a.stride(0), bt.data_ptr(), bt.stride(-2),
+                                 N * K if nd > 1 else 0, out.data_ptr(), N, out.stride(0), M * N, M, N, K, splits, nd,
+                                 torch.cuda.current_stream().cuda_stream)
+    if rc != 0:
+        raise RuntimeError("skr_skinny_gemm failed (%d) for M=%d N=%d K=%d S=%d" % (rc, M, N, K, splits))
+    return out
+
+
 class _Linear(torch.autograd.Function):
     """``x @ W + b`` in the compute precision with fp32 outputs/grads."""
 

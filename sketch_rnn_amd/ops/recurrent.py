@@ -59,13 +59,6 @@ class _Saved:
     """Plain holder for the big per-sequence buffers (kept off autograd)."""
 
 
-def _rec_mm(a: torch.Tensor, W: torch.Tensor, out: torch.Tensor, nd: int):
-    """``a [nd*B, K] @ W [nd, K, N] -> out [nd*B, N]`` (fp32 out)."""
-    if nd == 1:
-        return gemm.mm(a, W[0], out=out)
-    B = a.shape[0] // nd
-    return gemm.bmm(a.view(nd, B, -1), W, out=out.view(nd, B, -1))
-
 
 # =====================================================================================
 # LSTM / LayerNorm-LSTM sequence (nd groups)
@@ -81,8 +74,11 @@ class _LSTMSeq(torch.autograd.Function):
         f32 = torch.float32
         ln = ln_g is not None
         xp = xp.contiguous()
-        Wl = gemm.lp(W_h.reshape(nd, H, G)).contiguous()
+        Wl = gemm.lp(W_h.reshape(nd, H, G)).contiguous()   # B^T of the backward product dG @ W^T
+        WlT = Wl.transpose(1, 2).contiguous()              # B^T of the forward product h @ W
         ldt = Wl.dtype
+        Bg = BB // nd
+        S = gemm.plan_splits(Bg, G, H, nd, ldt)
         A = torch.empty(T + 1, BB, H, device=dev, dtype=ldt)   # GEMM operands: carried h
         A[0].copy_(h0)
         CC = torch.empty(T + 1, BB, H, device=dev, dtype=f32)  # carried c
@@ -94,7 +90,7 @@ class _LSTMSeq(torch.autograd.Function):
         RSTD = torch.empty(T, BB, 5, device=dev, dtype=f32) if ln else None
         CHAT = torch.empty(T, BB, H, device=dev, dtype=f32) if ln else None
         HC = torch.empty(2, BB, H, device=dev, dtype=f32)
-        R = torch.empty(BB, G, device=dev, dtype=f32)
+        R = torch.empty(max(S, 1), BB, G, device=dev, dtype=f32)
         rst = reset.contiguous().to(f32) if reset is not None else None
         rh = reset_h.contiguous() if reset_h is not None else None
         rc = reset_c.contiguous() if reset_c is not None else None
@@ -108,10 +104,10 @@ class _LSTMSeq(torch.autograd.Function):
         a.forget_bias, a.keep = float(forget_bias), float(keep)
         a.seed, a.stream = sd.data_ptr(), int(stream)
         a.ld_lp, a.lp_kind = H, _lp_kind(A)
-        a.R = R.data_ptr()
+        a.R, a.R_nslab, a.R_slab = R.data_ptr(), max(S, 1), BB * G
         st = _stream()
         for t in range(T):
-            _rec_mm(A[t], Wl, R, nd)
+            gemm.rec_gemm(A[t], WlT, R, S, nd)
             a.xp = xp[t].data_ptr()
             a.c_prev = CC[t].data_ptr()
             a.reset = _ptr(rst[t]) if rst is not None else None
@@ -147,18 +143,21 @@ class _LSTMSeq(torch.autograd.Function):
         dG = torch.empty(T, BB, G, device=dev, dtype=f32)
         lp_on = s.Wl.dtype == torch.bfloat16
         dG_lp = torch.empty(T, BB, G, device=dev, dtype=torch.bfloat16) if lp_on else None
-        dh_rec = dhT.contiguous().clone() if dhT is not None else torch.zeros(BB, H, device=dev, dtype=f32)
+        S = gemm.plan_splits(B, H, G, nd, s.Wl.dtype)
+        DH = torch.zeros(max(S, 1), BB, H, device=dev, dtype=f32)   # split-K slabs of dh into carried h
+        if dhT is not None:
+            DH[0].copy_(dhT)
         dc_rec = dcT.contiguous().clone() if dcT is not None else torch.zeros(BB, H, device=dev, dtype=f32)
         dHout = dHout.contiguous() if dHout is not None else None
         dinit_h = torch.zeros(BB, H, device=dev, dtype=f32) if s.reset is not None else None
         dinit_c = torch.zeros(BB, H, device=dev, dtype=f32) if s.reset is not None else None
         DLNY = torch.empty(T, BB, G, device=dev, dtype=f32) if ln else None
         DLNCY = torch.empty(T, BB, H, device=dev, dtype=f32) if ln else None
-        WT = s.Wl.transpose(1, 2)
         a = LstmBwdArgs()
         a.B, a.H, a.grp_rows = BB, H, B if nd > 1 else 0
-        a.ld_dh_rec = H
-        a.dh_rec, a.dc_rec = dh_rec.data_ptr(), dc_rec.data_ptr()
+        a.ld_dh_rec, a.dhr_nslab, a.dhr_slab = H, max(S, 1), BB * H
+        a.dho_nslab = 1
+        a.dh_rec, a.dc_rec = DH.data_ptr(), dc_rec.data_ptr()
         a.ln_g, a.lnc_g, a.lnc_b = _ptr(s.lnp[0]), _ptr(s.lnp[2]), _ptr(s.lnp[3])
         a.keep, a.seed, a.stream = float(keep), s.seed.data_ptr(), int(stream)
         a.ld_dG, a.ld_dG_lp, a.dG_lp_kind = G, G, 1 if lp_on else 0
@@ -175,7 +174,8 @@ class _LSTMSeq(torch.autograd.Function):
             a.dG = dG[t].data_ptr()
             a.dG_lp = dG_lp[t].data_ptr() if lp_on else None
             _check(lib.lib.skr_lstm_bwd_step(ctypes.byref(a), int(ln), 0, st), "lstm_bwd_step")
-            _rec_mm(dG_lp[t] if lp_on else dG[t], WT, dh_rec, nd)
+            gemm.rec_gemm(dG_lp[t] if lp_on else dG[t], s.Wl, DH, S, nd)
+        dh_rec = DH.sum(0) if DH.shape[0] > 1 else DH[0]
         dGs = dG_lp if lp_on else dG
         if nd == 1:
             dW = gemm.mm(s.A[:T].reshape(T * BB, H).t(), dGs.view(T * BB, G)).view(s.wshape)
@@ -251,11 +251,15 @@ class _HyperSeq(torch.autograd.Function):
         Wz3 = W_z.view(Hh, 12, E).permute(1, 0, 2)                 # [12, Hh, E]
         P = torch.bmm(Wz3, W_a).permute(1, 0, 2).reshape(Hh, 12 * H)  # [Hh, 12H]
         q = torch.bmm(b_z.view(12, 1, E), W_a).reshape(12, H).contiguous()
-        Pl = P.to(dt).contiguous()
+        Pl = P.to(dt).contiguous()             # B^T for the backward dvec @ P^T
+        PlT = Pl.t().contiguous()              # B^T for the forward  hh @ P
+        WcatT = Wcat.t().contiguous()
+        S_rc = gemm.plan_splits(B, N, K, 1, dt)
+        S_v = gemm.plan_splits(B, 12 * H, Hh, 1, dt, max_splits=1)
         A = torch.empty(T + 1, B, K, device=dev, dtype=dt)
         A[0, :, :H].copy_(h0)
         A[0, :, H:].copy_(hh0)
-        RC = torch.empty(T, B, N, device=dev, dtype=f32)
+        RC = torch.empty(T, max(S_rc, 1), B, N, device=dev, dtype=f32)
         CC = torch.empty(T + 1, B, H, device=dev, dtype=f32)
         CC[0].copy_(c0)
         HCC = torch.empty(T + 1, B, Hh, device=dev, dtype=f32)
@@ -282,6 +286,7 @@ class _HyperSeq(torch.autograd.Function):
         ah = LstmFwdArgs()
         ah.B, ah.H = B, Hh
         ah.ld_xp, ah.ld_R = Gh, N
+        ah.R_nslab, ah.R_slab = max(S_rc, 1), B * N
         ah.ln_g, ah.ln_b, ah.lnc_g, ah.lnc_b = (t.data_ptr() for t in hln)
         ah.forget_bias, ah.keep = float(forget_bias), float(hkeep)
         ah.seed, ah.stream = sd.data_ptr(), int(stream) + 1
@@ -290,22 +295,24 @@ class _HyperSeq(torch.autograd.Function):
         am = LstmFwdArgs()
         am.B, am.H = B, H
         am.ld_xp, am.ld_R = G, N
-        am.vec_gs, am.vec_ld, am.vec_bias, am.bias = H, 12 * H, q.data_ptr(), bias.contiguous().data_ptr()
+        am.R_nslab, am.R_slab = max(S_rc, 1), B * N
+        bias_c = bias.contiguous()
+        am.vec_gs, am.vec_ld, am.vec_bias, am.bias = H, 12 * H, q.data_ptr(), bias_c.data_ptr()
         am.ln_g, am.ln_b, am.lnc_g, am.lnc_b = (t.data_ptr() for t in mln)
         am.forget_bias, am.keep = float(forget_bias), float(keep)
         am.seed, am.stream = sd.data_ptr(), int(stream)
         am.ld_lp, am.lp_kind = K, _lp_kind(A)
         st = _stream()
         for t in range(T):
-            gemm.mm(A[t], Wcat, out=RC[t])
-            ah.xp, ah.R = XHY[t].data_ptr(), RC[t, :, G:].data_ptr()
+            gemm.rec_gemm(A[t], WcatT, RC[t], S_rc)
+            ah.xp, ah.R = XHY[t].data_ptr(), RC[t, 0, :, G:].data_ptr()
             ah.c_prev, ah.step = HCC[t].data_ptr(), t
             ah.h_out, ah.c_out, ah.act = HH[t].data_ptr(), HCout[t].data_ptr(), HACT[t].data_ptr()
             ah.xhat, ah.rstd, ah.chat = HXHAT[t].data_ptr(), HRSTD[t].data_ptr(), HCHAT[t].data_ptr()
             ah.h_carry, ah.h_lp, ah.c_carry = HHC[t % 2].data_ptr(), A[t + 1, :, H:].data_ptr(), HCC[t + 1].data_ptr()
             _check(lib.lib.skr_lstm_fwd_step(ctypes.byref(ah), 1, 0, st), "hyper_fwd_step")
-            gemm.mm(A[t + 1, :, H:], Pl, out=VEC[t])
-            am.xp, am.R, am.vec = XH[t].data_ptr(), RC[t, :, :G].data_ptr(), VEC[t].data_ptr()
+            gemm.rec_gemm(A[t + 1, :, H:], PlT, VEC[t].unsqueeze(0), S_v)
+            am.xp, am.R, am.vec = XH[t].data_ptr(), RC[t, 0, :, :G].data_ptr(), VEC[t].data_ptr()
             am.c_prev, am.step = CC[t].data_ptr(), t
             am.h_out, am.c_out, am.act = Hout[t].data_ptr(), Cout[t].data_ptr(), ACT[t].data_ptr()
             am.xhat, am.rstd, am.chat = XHAT[t].data_ptr(), RSTD[t].data_ptr(), CHAT[t].data_ptr()
@@ -314,7 +321,7 @@ class _HyperSeq(torch.autograd.Function):
         hT = HC[(T - 1) % 2].clone()
         hhT = HHC[(T - 1) % 2].clone()
         s = _Saved()
-        for k, v in dict(xl=xl, XH=XH, Wcat=Wcat, Pl=Pl, q=q, A=A, RC=RC, CC=CC, HCC=HCC, Cout=Cout, ACT=ACT,
+        for k, v in dict(xl=xl, XH=XH, Wcat=Wcat, Pl=Pl, q=q, bias_c=bias_c, S_rc=S_rc, A=A, RC=RC, CC=CC, HCC=HCC, Cout=Cout, ACT=ACT,
                          XHAT=XHAT, RSTD=RSTD, CHAT=CHAT, HH=HH, HCout=HCout, HACT=HACT, HXHAT=HXHAT, HRSTD=HRSTD,
                          HCHAT=HCHAT, VEC=VEC, seed=sd, meta=meta, W_x=W_x, hW_x=hW_x, W_z=W_z, b_z=b_z,
                          W_a=W_a, mln=mln, hln=hln).items():
@@ -344,30 +351,34 @@ class _HyperSeq(torch.autograd.Function):
         HDLNY = torch.empty(T, B, Gh, device=dev, dtype=f32)
         HDLNCY = torch.empty(T, B, Hh, device=dev, dtype=f32)
         dVEC = torch.empty(T, B, 12 * H, device=dev, dtype=ldt)
-        dhh_z = torch.empty(B, Hh, device=dev, dtype=f32)
-        dA = torch.zeros(B, K, device=dev, dtype=f32)
+        S_h = gemm.plan_splits(B, Hh, 12 * H, 1, ldt)
+        S_a = gemm.plan_splits(B, K, N, 1, ldt)
+        DHZ = torch.empty(max(S_h, 1), B, Hh, device=dev, dtype=f32)  # slabs of dhh from the vec path
+        DA = torch.zeros(max(S_a, 1), B, K, device=dev, dtype=f32)    # slabs of d[h | hh] carried
         if dhT is not None:
-            dA[:, :H].copy_(dhT)
+            DA[0, :, :H].copy_(dhT)
         if dhhT is not None:
-            dA[:, H:].copy_(dhhT)
+            DA[0, :, H:].copy_(dhhT)
         dc_rec = dcT.contiguous().clone() if dcT is not None else torch.zeros(B, H, device=dev, dtype=f32)
         dhc_rec = dhcT.contiguous().clone() if dhcT is not None else torch.zeros(B, Hh, device=dev, dtype=f32)
         dHout = dHout.contiguous() if dHout is not None else None
-        WcT = s.Wcat.t()
-        PT = s.Pl.t()
+        S_rc = max(s.S_rc, 1)
         am = LstmBwdArgs()
         am.B, am.H = B, H
-        am.dh_rec, am.ld_dh_rec, am.dc_rec = dA.data_ptr(), K, dc_rec.data_ptr()
+        am.dh_rec, am.ld_dh_rec, am.dc_rec = DA.data_ptr(), K, dc_rec.data_ptr()
+        am.dhr_nslab, am.dhr_slab, am.dho_nslab = max(S_a, 1), B * K, 1
         am.ln_g, am.lnc_g, am.lnc_b = s.mln[0].data_ptr(), s.mln[2].data_ptr(), s.mln[3].data_ptr()
         am.ld_xp, am.ld_R = G, N
+        am.R_nslab, am.R_slab = S_rc, B * N
         am.vec_gs, am.vec_ld, am.vec_bias = H, 12 * H, s.q.data_ptr()
         am.keep, am.seed, am.stream = float(keep), s.seed.data_ptr(), int(stream)
         am.ld_dG, am.ld_dG_lp, am.dG_lp_kind = N, N, 1 if lp_on else 0
         am.ld_dxp, am.dvec_kind = G, 1 if lp_on else 2
         ah = LstmBwdArgs()
         ah.B, ah.H = B, Hh
-        ah.dh_out = dhh_z.data_ptr()
-        ah.dh_rec, ah.ld_dh_rec, ah.dc_rec = dA[:, H:].data_ptr(), K, dhc_rec.data_ptr()
+        ah.dh_out, ah.dho_nslab, ah.dho_slab = DHZ.data_ptr(), max(S_h, 1), B * Hh
+        ah.dh_rec, ah.ld_dh_rec, ah.dc_rec = DA[0, :, H:].data_ptr(), K, dhc_rec.data_ptr()
+        ah.dhr_nslab, ah.dhr_slab = max(S_a, 1), B * K
         ah.ln_g, ah.lnc_g, ah.lnc_b = s.hln[0].data_ptr(), s.hln[2].data_ptr(), s.hln[3].data_ptr()
         ah.keep, ah.seed, ah.stream = float(hkeep), s.seed.data_ptr(), int(stream) + 1
         ah.ld_dG, ah.ld_dG_lp, ah.dG_lp_kind = N, N, 1 if lp_on else 0
@@ -376,14 +387,14 @@ class _HyperSeq(torch.autograd.Function):
             am.dh_out = dHout[t].data_ptr() if dHout is not None else None
             am.act, am.c_new, am.c_prev = s.ACT[t].data_ptr(), s.Cout[t].data_ptr(), s.CC[t].data_ptr()
             am.xhat, am.rstd, am.chat = s.XHAT[t].data_ptr(), s.RSTD[t].data_ptr(), s.CHAT[t].data_ptr()
-            am.xp, am.R, am.vec = s.XH[t].data_ptr(), s.RC[t, :, :G].data_ptr(), s.VEC[t].data_ptr()
+            am.xp, am.R, am.vec = s.XH[t].data_ptr(), s.RC[t, 0, :, :G].data_ptr(), s.VEC[t].data_ptr()
             am.step = t
             am.dG = dRC[t, :, :G].data_ptr()
             am.dG_lp = dRC_lp[t, :, :G].data_ptr() if lp_on else None
             am.dxp, am.dvec = dXH[t].data_ptr(), dVEC[t].data_ptr()
             am.dlny, am.dlncy = DLNY[t].data_ptr(), DLNCY[t].data_ptr()
             _check(lib.lib.skr_lstm_bwd_step(ctypes.byref(am), 1, 1, st), "hyper_main_bwd_step")
-            gemm.mm(dVEC[t], PT, out=dhh_z)
+            gemm.rec_gemm(dVEC[t], s.Pl, DHZ, S_h)
             ah.act, ah.c_new, ah.c_prev = s.HACT[t].data_ptr(), s.HCout[t].data_ptr(), s.HCC[t].data_ptr()
             ah.xhat, ah.rstd, ah.chat = s.HXHAT[t].data_ptr(), s.HRSTD[t].data_ptr(), s.HCHAT[t].data_ptr()
             ah.step = t
@@ -391,7 +402,8 @@ class _HyperSeq(torch.autograd.Function):
             ah.dG_lp = dRC_lp[t, :, G:].data_ptr() if lp_on else None
             ah.dlny, ah.dlncy = HDLNY[t].data_ptr(), HDLNCY[t].data_ptr()
             _check(lib.lib.skr_lstm_bwd_step(ctypes.byref(ah), 1, 0, st), "hyper_bwd_step")
-            gemm.mm(dRC_lp[t] if lp_on else dRC[t], WcT, out=dA)
+            gemm.rec_gemm(dRC_lp[t] if lp_on else dRC[t], s.Wcat, DA, S_a)
+        dA = DA.sum(0) if DA.shape[0] > 1 else DA[0]
         # ---- weight gradients: single large GEMMs over all T*B rows ----
         dRCm = (dRC_lp if lp_on else dRC).view(TB, N)
         dWcat = gemm.mm(s.A[:T].reshape(TB, K).t(), dRCm)

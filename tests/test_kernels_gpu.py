@@ -168,6 +168,24 @@ def test_hyper_sequence_matches_oracle(H, Hh, E, keep):
     _close(g_h, g_t, 2e-3, 2e-4, "grad")
 
 
+@pytest.mark.parametrize("M,N,K,nd", [(100, 9216, 2304, 1), (100, 2304, 9216, 1), (100, 256, 24576, 1),
+                                      (100, 24576, 256, 1), (7, 64, 64, 1), (128, 2048, 512, 2),
+                                      (100, 512, 2048, 2)])
+def test_skinny_gemm_matches_torch(M, N, K, nd):
+    from sketch_rnn_amd.ops import gemm
+    torch.manual_seed(6)
+    a = torch.randn(nd * M, K, device=DEV).to(torch.bfloat16)
+    bt = torch.randn(nd, N, K, device=DEV).to(torch.bfloat16)
+    S = gemm.plan_splits(M, N, K, nd)
+    assert S >= 1
+    out = torch.empty(S, nd * M, N, device=DEV)
+    gemm.rec_gemm(a, bt if nd > 1 else bt[0], out, S, nd)
+    ref = torch.bmm(a.float().view(nd, M, K), bt.float().transpose(1, 2)).reshape(nd * M, N)
+    got = out.sum(0)
+    err = (got - ref).abs().max().item()
+    assert err <= 1e-3 * ref.abs().max().item() + 1e-3, (S, err)
+
+
 @pytest.mark.parametrize("mode,M", [("reference", 24), ("magenta", 20), ("magenta", 5)])
 def test_mdn_loss_matches_oracle(mode, M):
     torch.manual_seed(3)
