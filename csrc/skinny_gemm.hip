@@ -17,8 +17,11 @@
 // C/D: col = l&15, row = 4(l>>4) + i.
 //
 // Block: 256 threads (4 waves); wave w owns rows 32w..32w+31 x all 64 cols
-// (2 x 4 accumulator tiles). K tile 64, double-buffered LDS with register
-// prefetch of the next tile; rows padded by 16 B against bank conflicts.
+// (2 x 4 accumulator tiles). K tile 64. Pipeline depth 3: tile kt in LDS
+// (double-buffered), tile kt+1 in staging registers, tile kt+2's global
+// loads issued before tile kt's MFMAs -- with only 16 MFMAs per wave per
+// tile, one tile of lookahead cannot cover the L2/MALL latency.
+// Rows padded by 16 B in LDS (conflict-free ds_read_b128 fragment reads).
 // gridDim.z batches independent problems (both encoder directions).
 #include "common.h"
 
@@ -38,37 +41,46 @@ __global__ __launch_bounds__(256) void skinny_gemm_nt_kernel(
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int n0 = blockIdx.x * BN;
     const int64_t k0 = (int64_t)blockIdx.y * kslice;
-    const int ntiles = kslice / BK;
+    const int n = kslice / BK;
     A += blockIdx.z * a_batch;
     Bt += blockIdx.z * b_batch;
     C += blockIdx.z * c_batch + blockIdx.y * c_slab;
 
-    uint4 ra[4], rb[2];
-    auto load = [&](int kt) {
-        const int64_t kb = k0 + (int64_t)kt * BK;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int c = tid + i * 256, row = c >> 3, kc = (c & 7) * 8;
-            ra[i] = row < M ? *(const uint4*)(A + row * lda + kb + kc) : make_uint4(0, 0, 0, 0);
-        }
-#pragma unroll
-        for (int i = 0; i < 2; ++i) {
-            const int c = tid + i * 256, col = c >> 3, kc = (c & 7) * 8;
-            rb[i] = *(const uint4*)(Bt + (int64_t)(n0 + col) * ldb + kb + kc);
-        }
-    };
-    auto store = [&](int buf) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int c = tid + i * 256, row = c >> 3, kc = (c & 7) * 8;
-            *(uint4*)(&As[buf][row * LDK + kc]) = ra[i];
-        }
-#pragma unroll
-        for (int i = 0; i < 2; ++i) {
-            const int c = tid + i * 256, col = c >> 3, kc = (c & 7) * 8;
-            *(uint4*)(&Bs[buf][col * LDK + kc]) = rb[i];
-        }
-    };
+    // Staging registers are named scalars, not an array: a private array
+    // captured by a lambda is promoted to LDS by the AMDGPU backend, which
+    // turns every prefetch into load -> wait -> LDS round trip.
+    // Thread t stages A rows t/8 + {0, 32, 64, 96} and B rows t/8 + {0, 32},
+    // 16 bytes each at k offset (t % 8) * 8 -- 128 contiguous bytes per row.
+    // Rows >= M re-read row M-1 (never stored): an unconditional load keeps
+    // hipcc from branching around it and draining vmcnt.
+    const int srow = tid >> 3, skc = (tid & 7) * 8;
+    const __hip_bfloat16* a0 = A + (int64_t)min(srow, M - 1) * lda + k0 + skc;
+    const __hip_bfloat16* a1 = A + (int64_t)min(srow + 32, M - 1) * lda + k0 + skc;
+    const __hip_bfloat16* a2 = A + (int64_t)min(srow + 64, M - 1) * lda + k0 + skc;
+    const __hip_bfloat16* a3 = A + (int64_t)min(srow + 96, M - 1) * lda + k0 + skc;
+    const __hip_bfloat16* b0 = Bt + (int64_t)(n0 + srow) * ldb + k0 + skc;
+    const __hip_bfloat16* b1 = Bt + (int64_t)(n0 + srow + 32) * ldb + k0 + skc;
+    uint4 xa0, xa1, xa2, xa3, xb0, xb1;  // register set X
+    uint4 ya0, ya1, ya2, ya3, yb0, yb1;  // register set Y
+#define SKR_LOAD(P, kt)                                  \
+    do {                                                 \
+        const int64_t ko = (int64_t)min(kt, n - 1) * BK; \
+        P##a0 = *(const uint4*)(a0 + ko);                \
+        P##a1 = *(const uint4*)(a1 + ko);                \
+        P##a2 = *(const uint4*)(a2 + ko);                \
+        P##a3 = *(const uint4*)(a3 + ko);                \
+        P##b0 = *(const uint4*)(b0 + ko);                \
+        P##b1 = *(const uint4*)(b1 + ko);                \
+    } while (0)
+#define SKR_STORE(P, buf)                                          \
+    do {                                                           \
+        *(uint4*)(&As[buf][srow * LDK + skc]) = P##a0;             \
+        *(uint4*)(&As[buf][(srow + 32) * LDK + skc]) = P##a1;      \
+        *(uint4*)(&As[buf][(srow + 64) * LDK + skc]) = P##a2;      \
+        *(uint4*)(&As[buf][(srow + 96) * LDK + skc]) = P##a3;      \
+        *(uint4*)(&Bs[buf][srow * LDK + skc]) = P##b0;             \
+        *(uint4*)(&Bs[buf][(srow + 32) * LDK + skc]) = P##b1;      \
+    } while (0)
 
     f32x4 acc[2][4];
 #pragma unroll
@@ -76,13 +88,8 @@ __global__ __launch_bounds__(256) void skinny_gemm_nt_kernel(
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-    load(0);
-    store(0);
-    __syncthreads();
     const int fr = lane & 15, fk = (lane >> 4) * 8;
-    for (int kt = 0; kt < ntiles; ++kt) {
-        const int buf = kt & 1;
-        if (kt + 1 < ntiles) load(kt + 1);
+    auto compute = [&](int buf) {
 #pragma unroll
         for (int ks = 0; ks < BK; ks += 32) {
             bf16x8 af[2], bfr[4];
@@ -97,9 +104,40 @@ __global__ __launch_bounds__(256) void skinny_gemm_nt_kernel(
                 for (int j = 0; j < 4; ++j)
                     acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
         }
-        if (kt + 1 < ntiles) store(buf ^ 1);
+    };
+
+    // prologue: tile 0 -> LDS[0], tile 1 -> Y (in flight)
+    SKR_LOAD(x, 0);
+    SKR_LOAD(y, 1);
+    SKR_STORE(x, 0);
+    __syncthreads();
+    // Each half-iteration: issue loads two tiles ahead into the free register
+    // set, MFMA the LDS tile, then write the one-ahead set into the other LDS
+    // buffer (its wait leaves the newest loads in flight), barrier.
+    // Loads past the last tile re-read it (min above): branch-free body.
+    // The asm clobber + sched_barrier pin the order: hipcc would otherwise
+    // hoist the LDS writes (and their vmcnt wait) above the MFMAs.
+    int kt = 0;
+    for (;;) {
+        SKR_LOAD(x, kt + 2);
+        __builtin_amdgcn_sched_barrier(0);
+        compute(kt & 1);
+        asm volatile("" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+        SKR_STORE(y, (kt + 1) & 1);
         __syncthreads();
+        if (++kt >= n) break;
+        SKR_LOAD(y, kt + 2);
+        __builtin_amdgcn_sched_barrier(0);
+        compute(kt & 1);
+        asm volatile("" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+        SKR_STORE(x, (kt + 1) & 1);
+        __syncthreads();
+        if (++kt >= n) break;
     }
+#undef SKR_LOAD
+#undef SKR_STORE
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll

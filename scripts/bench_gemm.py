@@ -1,0 +1,60 @@
+#!/usr/bin/env python3
+"""Microbenchmark: skinny split-K GEMM vs hipBLASLt on the recurrent shapes."""
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, __file__.rsplit("/scripts/", 1)[0])
+from sketch_rnn_amd.ops import gemm  # noqa: E402
+
+SHAPES = [  # (name, M, N, K, nd)
+    ("RC  fwd", 100, 9216, 2304, 1),
+    ("VEC fwd", 100, 24576, 256, 1),
+    ("dA  bwd", 100, 2304, 9216, 1),
+    ("dhh bwd", 100, 256, 24576, 1),
+    ("enc fwd", 100, 2048, 512, 2),
+    ("enc bwd", 100, 512, 2048, 2),
+]
+
+
+def timeit(fn, reps=200):
+    for _ in range(10):
+        fn()
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for _ in range(reps):
+            fn()
+    torch.cuda.synchronize()
+    t = time.perf_counter()
+    g.replay()
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t) / reps * 1e6
+
+
+def main():
+    dev = "cuda"
+    for name, M, N, K, nd in SHAPES:
+        a = torch.randn(nd * M, K, device=dev).to(torch.bfloat16)
+        bt = torch.randn(nd, N, K, device=dev).to(torch.bfloat16)
+        b = bt.transpose(1, 2).contiguous()
+        res = []
+        for S in sorted({gemm.plan_splits(M, N, K, nd), 1, 2, 4, 8, 16, 32}):
+            if S < 1 or (K // 64) % S:
+                continue
+            out = torch.empty(S, nd * M, N, device=dev)
+            us = timeit(lambda: gemm.rec_gemm(a, bt if nd > 1 else bt[0], out, S, nd))
+            res.append("S=%d %.1fus" % (S, us))
+        out1 = torch.empty(nd, M, N, device=dev)
+        if nd == 1:
+            us_lib = timeit(lambda: torch.mm(a, b[0], out_dtype=torch.float32, out=out1[0]))
+        else:
+            us_lib = timeit(lambda: torch.bmm(a.view(nd, M, K), b, out_dtype=torch.float32, out=out1))
+        flops = 2.0 * nd * M * N * K
+        print("%s M=%d N=%d K=%d nd=%d  hipBLASLt %.1fus | %s | plan S=%d | %.1f GFLOP" % (
+            name, M, N, K, nd, us_lib, " ".join(res), gemm.plan_splits(M, N, K, nd), flops / 1e9), flush=True)
+
+
+if __name__ == "__main__":
+    main()
