@@ -26,79 +26,11 @@
 //
 // Reference semantics: model.py:19-23 (BasicLSTMCell), model.py:82-92 (eoc
 // reset); LayerNorm-/Hyper-LSTM semantics: sketch_rnn_amd/models/cells.py.
-#include "common.h"
+#include "lstm_args.h"
 
 namespace {
 
-constexpr float kLnEps = 1e-3f;
-
-struct FwdArgs {
-    int B, H;
-    int grp_rows;                      // rows per parameter group (0: one group)
-    const float* xp; int64_t ld_xp;    // [B, 4H]: x-projection (+bias unless MOD)
-    const float* R;  int64_t ld_R;     // [B, 4H]: h_prev @ W_h (fp32)
-    int R_nslab; int64_t R_slab;       // R is the sum of R_nslab split-K partial slabs
-    const float* vec; int64_t vec_gs; int64_t vec_ld;  // MOD: element (k,b,u) at k*gs + b*ld + u
-    const float* vec_bias;             // MOD: [12, H] added to vec (or null)
-    const float* bias;                 // MOD: [4H]
-    const float* c_prev;               // [B, H]
-    const float* ln_g; const float* ln_b; const float* lnc_g; const float* lnc_b;
-    const float* reset;                // [B] or null
-    const float* init_h; const float* init_c;
-    float forget_bias, keep;
-    const int64_t* seed; uint32_t stream, step;
-    float* h_out;                      // [B, H]
-    float* c_out;                      // [B, H]
-    float* act;                        // [B, 4H] sig(i), tanh(j), sig(f+fb), sig(o)
-    float* xhat;                       // LN: [B, 4H]
-    float* rstd;                       // LN: [B, 5]
-    float* chat;                       // LN: [B, H]
-    float* h_carry;                    // [B, H]
-    void* h_lp; int64_t ld_lp; int lp_kind;  // 0: none, 1: bf16, 2: fp32
-    float* c_carry;                    // [B, H]
-};
-
-struct BwdArgs {
-    int B, H;
-    int grp_rows;
-    const float* dh_out;               // [B, H] or null
-    int dho_nslab; int64_t dho_slab;
-    const float* dh_rec;               // [B, H] (grad into carried h_t) or null
-    int64_t ld_dh_rec;
-    int dhr_nslab; int64_t dhr_slab;
-    float* dc_rec;                     // [B, H] in: grad into carried c_t; out: into carried c_{t-1}
-    const float* act; const float* c_new; const float* c_prev;
-    const float* xhat; const float* rstd; const float* chat;
-    const float* ln_g; const float* lnc_g; const float* lnc_b;
-    const float* xp; int64_t ld_xp;    // MOD: xh
-    const float* R;  int64_t ld_R;     // MOD: R
-    int R_nslab; int64_t R_slab;
-    const float* vec; int64_t vec_gs; int64_t vec_ld;  // MOD
-    const float* vec_bias;
-    const float* reset;
-    float keep; const int64_t* seed; uint32_t stream, step;
-    float* dG; int64_t ld_dG;          // non-MOD: d(preact) [B, 4H]; MOD: dR = dg*ah
-    void* dG_lp; int64_t ld_dG_lp; int dG_lp_kind;  // bf16 copy of dG for the next GEMM (1) or none (0)
-    float* dxp; int64_t ld_dxp;        // MOD: dxh = dg*ax
-    void* dvec; int dvec_kind;         // MOD: same layout as vec; 1 bf16, 2 fp32
-    float* dlny;                       // LN: [B, 4H] grad wrt LN-all output (for gamma/beta)
-    float* dlncy;                      // LN: [B, H]  grad wrt LN(c) output
-    float* dinit_h; float* dinit_c;    // [B, H] accumulated on reset rows (or null)
-};
-
-// Sum of n split-K partial slabs (n <= 1: a plain load).
-__device__ __forceinline__ float ld_slabs(const float* p, int64_t idx, int n, int64_t slab) {
-    float v = p[idx];
-    for (int s = 1; s < n; ++s) v += p[s * slab + idx];
-    return v;
-}
-
-__device__ __forceinline__ float vec_at(const float* v, const float* vb, int64_t gs, int64_t ld, int k, int b, int u,
-                                        int H) {
-    float x = v[k * gs + (int64_t)b * ld + u];
-    if (vb) x += vb[k * H + u];
-    return x;
-}
+using namespace skr;
 
 template <int NT, int UPT, bool LN, bool MOD>
 __global__ __launch_bounds__(NT) void lstm_fwd_kernel(const FwdArgs a) {
@@ -429,10 +361,12 @@ int dispatch(const A& a, bool ln, bool mod, hipStream_t s) {
 // Host entry points: argument structs are passed by pointer from Python (ctypes
 // mirrors of FwdArgs / BwdArgs in sketch_rnn_amd/ops/_hipapi.py).
 SKR_API int skr_lstm_fwd_step(const FwdArgs* args, int ln, int mod, hipStream_t s) {
+    if (args->cluster > 1) return skr::launch_cluster(*args, ln != 0, mod != 0, s);
     return dispatch(*args, ln != 0, mod != 0, s);
 }
 
 SKR_API int skr_lstm_bwd_step(const BwdArgs* args, int ln, int mod, hipStream_t s) {
+    if (args->cluster > 1) return skr::launch_cluster(*args, ln != 0, mod != 0, s);
     return dispatch(*args, ln != 0, mod != 0, s);
 }
 

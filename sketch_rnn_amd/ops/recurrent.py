@@ -59,6 +59,46 @@ class _Saved:
     """Plain holder for the big per-sequence buffers (kept off autograd)."""
 
 
+# ---- clustered cell kernels (csrc/lstm_cluster.hip) ---------------------------------
+CLUSTER_ENABLED = True
+_ERR_FLAGS = {}
+
+
+def cluster_error_flag(device) -> torch.Tensor:
+    """Device int32 flag set by a clustered kernel whose in-launch wait timed
+    out (results of that step are then invalid)."""
+    key = str(device)
+    if key not in _ERR_FLAGS:
+        _ERR_FLAGS[key] = torch.zeros(1, dtype=torch.int32, device=device)
+    return _ERR_FLAGS[key]
+
+
+def check_cluster_errors(device) -> None:
+    f = cluster_error_flag(device)
+    if int(f.item()) != 0:
+        f.zero_()
+        raise RuntimeError("clustered LSTM cell kernel: in-launch wait timed out (workgroups not co-resident)")
+
+
+class _ClusterSync:
+    """Per-sequence arrival counters / partial-stat scratch for one pass."""
+
+    def __init__(self, T: int, BB: int, H: int, device):
+        self.C = (H + 255) // 256
+        self.on = CLUSTER_ENABLED and 1 < self.C <= 16 and BB * self.C <= 1024
+        if self.on:
+            self.sync = torch.zeros(T, 2, BB, dtype=torch.int32, device=device)
+            self.part = torch.empty(2, BB, self.C, 8, dtype=torch.float32, device=device)
+            self.err = cluster_error_flag(device)
+
+    def set(self, args, t: int) -> None:
+        if self.on:
+            args.cluster, args.sync = self.C, self.sync[t].data_ptr()
+            args.part, args.err = self.part.data_ptr(), self.err.data_ptr()
+        else:
+            args.cluster = 0
+
+
 
 # =====================================================================================
 # LSTM / LayerNorm-LSTM sequence (nd groups)
@@ -105,8 +145,10 @@ class _LSTMSeq(torch.autograd.Function):
         a.seed, a.stream = sd.data_ptr(), int(stream)
         a.ld_lp, a.lp_kind = H, _lp_kind(A)
         a.R, a.R_nslab, a.R_slab = R.data_ptr(), max(S, 1), BB * G
+        cl = _ClusterSync(T, BB, H, dev)
         st = _stream()
         for t in range(T):
+            cl.set(a, t)
             gemm.rec_gemm(A[t], WlT, R, S, nd)
             a.xp = xp[t].data_ptr()
             a.c_prev = CC[t].data_ptr()
@@ -162,8 +204,10 @@ class _LSTMSeq(torch.autograd.Function):
         a.keep, a.seed, a.stream = float(keep), s.seed.data_ptr(), int(stream)
         a.ld_dG, a.ld_dG_lp, a.dG_lp_kind = G, G, 1 if lp_on else 0
         a.dinit_h, a.dinit_c = _ptr(dinit_h), _ptr(dinit_c)
+        cl = _ClusterSync(T, BB, H, dev)
         st = _stream()
         for t in range(T - 1, -1, -1):
+            cl.set(a, t)
             a.dh_out = dHout[t].data_ptr() if dHout is not None else None
             a.act, a.c_new, a.c_prev = s.ACT[t].data_ptr(), s.Cout[t].data_ptr(), s.CC[t].data_ptr()
             if ln:
@@ -302,8 +346,11 @@ class _HyperSeq(torch.autograd.Function):
         am.forget_bias, am.keep = float(forget_bias), float(keep)
         am.seed, am.stream = sd.data_ptr(), int(stream)
         am.ld_lp, am.lp_kind = K, _lp_kind(A)
+        clm, clh = _ClusterSync(T, B, H, dev), _ClusterSync(T, B, Hh, dev)
         st = _stream()
         for t in range(T):
+            clm.set(am, t)
+            clh.set(ah, t)
             gemm.rec_gemm(A[t], WcatT, RC[t], S_rc)
             ah.xp, ah.R = XHY[t].data_ptr(), RC[t, 0, :, G:].data_ptr()
             ah.c_prev, ah.step = HCC[t].data_ptr(), t
@@ -382,8 +429,11 @@ class _HyperSeq(torch.autograd.Function):
         ah.ln_g, ah.lnc_g, ah.lnc_b = s.hln[0].data_ptr(), s.hln[2].data_ptr(), s.hln[3].data_ptr()
         ah.keep, ah.seed, ah.stream = float(hkeep), s.seed.data_ptr(), int(stream) + 1
         ah.ld_dG, ah.ld_dG_lp, ah.dG_lp_kind = N, N, 1 if lp_on else 0
+        clm, clh = _ClusterSync(T, B, H, dev), _ClusterSync(T, B, Hh, dev)
         st = _stream()
         for t in range(T - 1, -1, -1):
+            clm.set(am, t)
+            clh.set(ah, t)
             am.dh_out = dHout[t].data_ptr() if dHout is not None else None
             am.act, am.c_new, am.c_prev = s.ACT[t].data_ptr(), s.Cout[t].data_ptr(), s.CC[t].data_ptr()
             am.xhat, am.rstd, am.chat = s.XHAT[t].data_ptr(), s.RSTD[t].data_ptr(), s.CHAT[t].data_ptr()

@@ -24,6 +24,9 @@ def _restore():
     yield
     ops.set_backend("auto")
     ops.set_compute_dtype("fp32")
+    from sketch_rnn_amd.ops.recurrent import check_cluster_errors
+    torch.cuda.synchronize()
+    check_cluster_errors(DEV)
 
 
 def _run(backend, fn, inputs):
@@ -58,7 +61,8 @@ def _close(a, b, rtol, atol, what):
 
 @pytest.mark.parametrize("H,ln,reset,keep", [(64, False, False, 1.0), (256, False, True, 1.0),
                                              (512, False, False, 0.9), (96, True, False, 1.0),
-                                             (300, True, True, 0.85), (2048, True, False, 1.0)])
+                                             (300, True, True, 0.85), (2048, True, False, 1.0),
+                                             (600, True, True, 0.9), (1100, False, True, 0.8)])
 def test_lstm_sequence_matches_oracle(H, ln, reset, keep):
     torch.manual_seed(0)
     T, B = 7, 5
