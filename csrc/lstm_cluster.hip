@@ -33,6 +33,11 @@ using namespace skr;
 constexpr int NT = 256, NW = NT / 64;
 constexpr int kMaxCluster = 16;          // H <= 4096
 constexpr unsigned kSpinLimit = 1u << 21;
+// Every arrival counter and every workgroup's partial slot owns a 128-byte
+// line: agent-scope atomics and sc1 traffic on a shared line serialise at the
+// memory side (CDNA4 guide, float-atomics contention row).
+constexpr int kSyncStride = 32;   // ints
+constexpr int kPartStride = 32;   // floats
 
 // Publish `nv` floats of this workgroup (LDS `mine`), wait for the row's C
 // workgroups, gather all C*nv values into LDS `all` ([C][nv]).
@@ -40,7 +45,7 @@ __device__ void cluster_allgather(float* part, int* cnt, int* err, int b, int c,
                                   float* all) {
     __syncthreads();
     if (threadIdx.x == 0) {
-        float* dst = part + ((int64_t)b * C + c) * 8;
+        float* dst = part + ((int64_t)b * C + c) * kPartStride;
         for (int i = 0; i < nv; ++i) __hip_atomic_store(dst + i, mine[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -56,7 +61,8 @@ __device__ void cluster_allgather(float* part, int* cnt, int* err, int b, int c,
     __syncthreads();
     for (int i = threadIdx.x; i < C * nv; i += NT) {
         const int cc = i / nv, k = i - cc * nv;
-        all[i] = __hip_atomic_load(part + ((int64_t)b * C + cc) * 8 + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        all[i] = __hip_atomic_load(part + ((int64_t)b * C + cc) * kPartStride + k, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
     }
     __syncthreads();
 }
@@ -128,7 +134,7 @@ __global__ __launch_bounds__(NT) void lstm_fwd_cluster(const FwdArgs a) {
                 mine[4 + q] = m2[q];
             }
         }
-        cluster_allgather(a.part, a.sync + b, a.err, b, c, C, mine, 8, all);
+        cluster_allgather(a.part, a.sync + b * kSyncStride, a.err, b, c, C, mine, 8, all);
         float rs[4];
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
@@ -170,7 +176,7 @@ __global__ __launch_bounds__(NT) void lstm_fwd_cluster(const FwdArgs a) {
             mine[0] = ml;
             mine[1] = s2[0];
         }
-        cluster_allgather(a.part + (int64_t)a.B * C * 8, a.sync + a.B + b, a.err, b, c, C, mine, 2, all);
+        cluster_allgather(a.part + (int64_t)a.B * C * kPartStride, a.sync + (a.B + b) * kSyncStride, a.err, b, c, C, mine, 2, all);
         float mean, var;
         chan_combine(all, C, 2, 0, H, mean, var);
         const float rc = rsqrtf(var + kLnEps);
@@ -246,7 +252,7 @@ __global__ __launch_bounds__(NT) void lstm_bwd_cluster(const BwdArgs a) {
             mine[0] = s[0];
             mine[1] = s[1];
         }
-        cluster_allgather(a.part, a.sync + b, a.err, b, c, C, mine, 2, all);
+        cluster_allgather(a.part, a.sync + b * kSyncStride, a.err, b, c, C, mine, 2, all);
         float t0 = 0.f, t1 = 0.f;
         for (int cc = 0; cc < C; ++cc) {
             t0 += all[cc * 2];
@@ -289,7 +295,7 @@ __global__ __launch_bounds__(NT) void lstm_bwd_cluster(const BwdArgs a) {
 #pragma unroll
             for (int k = 0; k < 8; ++k) mine[k] = acc[k];
         }
-        cluster_allgather(a.part + (int64_t)a.B * C * 8, a.sync + a.B + b, a.err, b, c, C, mine, 8, all);
+        cluster_allgather(a.part + (int64_t)a.B * C * kPartStride, a.sync + (a.B + b) * kSyncStride, a.err, b, c, C, mine, 8, all);
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             float t0 = 0.f, t1 = 0.f;

@@ -23,6 +23,7 @@ Autograd boundaries are whole sequences, so no per-step autograd nodes exist.
 from __future__ import annotations
 
 import ctypes
+import os
 from typing import Optional
 
 import torch
@@ -60,7 +61,7 @@ class _Saved:
 
 
 # ---- clustered cell kernels (csrc/lstm_cluster.hip) ---------------------------------
-CLUSTER_ENABLED = True
+CLUSTER_ENABLED = os.environ.get("SKR_CLUSTER", "1") != "0"
 _ERR_FLAGS = {}
 
 
@@ -87,8 +88,9 @@ class _ClusterSync:
         self.C = (H + 255) // 256
         self.on = CLUSTER_ENABLED and 1 < self.C <= 16 and BB * self.C <= 1024
         if self.on:
-            self.sync = torch.zeros(T, 2, BB, dtype=torch.int32, device=device)
-            self.part = torch.empty(2, BB, self.C, 8, dtype=torch.float32, device=device)
+            # one 128-byte line per counter / per workgroup slot (kSyncStride, kPartStride)
+            self.sync = torch.zeros(T, 2, BB, 32, dtype=torch.int32, device=device)
+            self.part = torch.empty(2, BB, self.C, 32, dtype=torch.float32, device=device)
             self.err = cluster_error_flag(device)
 
     def set(self, args, t: int) -> None:
