@@ -4,11 +4,11 @@
 // M = batch (<= 128), N in {256 .. 24576}, K in {256 .. 24576}. Library
 // kernels tile these for square problems and leave most of the 256 CUs idle
 // (e.g. [100 x 24576] x [24576 x 256] ran as 28 workgroups). This kernel
-// always covers all M rows in one 128-row tile, tiles N by 64 and splits K
-// over gridDim.y so that (N/64) * S ~ 1-2 workgroups per CU. Each split
-// writes its own fp32 partial slab; the CONSUMER (the fused cell kernel of
-// csrc/lstm_cell.hip) sums the S slabs while loading -- the reduction costs
-// no extra launch and no atomics, and the result is deterministic.
+// always covers all M rows in one 128-row tile, tiles N by BN (64 or 128)
+// and splits K over gridDim.y so that (N/BN) * S ~ 1-2 workgroups per CU.
+// Each split writes its own fp32 partial slab; the CONSUMER (the fused cell
+// kernels) sums the S slabs while loading -- the reduction costs no extra
+// launch and no atomics, and the result is deterministic.
 //
 // Both operands are K-contiguous ("NT"): A [M, K] row-major, Bt [N, K]
 // row-major (weights are kept in bf16 in both orientations), so MFMA
@@ -16,11 +16,11 @@
 // holds A[row l&15][k 8(l>>4) .. +7] and B[k 8(l>>4) .. +7][col l&15];
 // C/D: col = l&15, row = 4(l>>4) + i.
 //
-// Block: 256 threads (4 waves); wave w owns rows 32w..32w+31 x all 64 cols
-// (2 x 4 accumulator tiles). K tile 64. Pipeline depth 3: tile kt in LDS
+// Block: 256 threads (4 waves); wave w owns rows 32w..32w+31 x all BN cols
+// (2 x BN/16 accumulator tiles). K tile 64. Pipeline depth 3: tile kt in LDS
 // (double-buffered), tile kt+1 in staging registers, tile kt+2's global
-// loads issued before tile kt's MFMAs -- with only 16 MFMAs per wave per
-// tile, one tile of lookahead cannot cover the L2/MALL latency.
+// loads issued before tile kt's MFMAs -- with so few MFMAs per tile, one
+// tile of lookahead cannot cover the L2/MALL latency.
 // Rows padded by 16 B in LDS (conflict-free ds_read_b128 fragment reads).
 // gridDim.z batches independent problems (both encoder directions).
 #include "common.h"
@@ -30,12 +30,14 @@ namespace {
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
 typedef __attribute__((ext_vector_type(4))) float f32x4;
 
-constexpr int BM = 128, BN = 64, BK = 64, PAD = 8, LDK = BK + PAD;  // LDS row = 144 B
+constexpr int BM = 128, BK = 64, PAD = 8, LDK = BK + PAD;  // LDS row = 144 B
 
+template <int BN>
 __global__ __launch_bounds__(256) void skinny_gemm_nt_kernel(
     const __hip_bfloat16* __restrict__ A, int64_t lda, int64_t a_batch,
     const __hip_bfloat16* __restrict__ Bt, int64_t ldb, int64_t b_batch,
     float* __restrict__ C, int64_t ldc, int64_t c_slab, int64_t c_batch, int M, int kslice) {
+    constexpr int NJ = BN / 16;
     __shared__ __attribute__((aligned(16))) __hip_bfloat16 As[2][BM * LDK];
     __shared__ __attribute__((aligned(16))) __hip_bfloat16 Bs[2][BN * LDK];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -49,7 +51,7 @@ __global__ __launch_bounds__(256) void skinny_gemm_nt_kernel(
     // Staging registers are named scalars, not an array: a private array
     // captured by a lambda is promoted to LDS by the AMDGPU backend, which
     // turns every prefetch into load -> wait -> LDS round trip.
-    // Thread t stages A rows t/8 + {0, 32, 64, 96} and B rows t/8 + {0, 32},
+    // Thread t stages A rows t/8 + {0, 32, 64, 96} and B rows t/8 + 32j,
     // 16 bytes each at k offset (t % 8) * 8 -- 128 contiguous bytes per row.
     // Rows >= M re-read row M-1 (never stored): an unconditional load keeps
     // hipcc from branching around it and draining vmcnt.
@@ -59,18 +61,22 @@ __global__ __launch_bounds__(256) void skinny_gemm_nt_kernel(
     const __hip_bfloat16* a2 = A + (int64_t)min(srow + 64, M - 1) * lda + k0 + skc;
     const __hip_bfloat16* a3 = A + (int64_t)min(srow + 96, M - 1) * lda + k0 + skc;
     const __hip_bfloat16* b0 = Bt + (int64_t)(n0 + srow) * ldb + k0 + skc;
-    const __hip_bfloat16* b1 = Bt + (int64_t)(n0 + srow + 32) * ldb + k0 + skc;
-    uint4 xa0, xa1, xa2, xa3, xb0, xb1;  // register set X
-    uint4 ya0, ya1, ya2, ya3, yb0, yb1;  // register set Y
-#define SKR_LOAD(P, kt)                                  \
-    do {                                                 \
-        const int64_t ko = (int64_t)min(kt, n - 1) * BK; \
-        P##a0 = *(const uint4*)(a0 + ko);                \
-        P##a1 = *(const uint4*)(a1 + ko);                \
-        P##a2 = *(const uint4*)(a2 + ko);                \
-        P##a3 = *(const uint4*)(a3 + ko);                \
-        P##b0 = *(const uint4*)(b0 + ko);                \
-        P##b1 = *(const uint4*)(b1 + ko);                \
+    const int64_t bstep = 32 * ldb;
+    uint4 xa0, xa1, xa2, xa3, xb0, xb1, xb2, xb3;  // register set X
+    uint4 ya0, ya1, ya2, ya3, yb0, yb1, yb2, yb3;  // register set Y
+#define SKR_LOAD(P, kt)                                           \
+    do {                                                          \
+        const int64_t ko = (int64_t)min(kt, n - 1) * BK;          \
+        P##a0 = *(const uint4*)(a0 + ko);                         \
+        P##a1 = *(const uint4*)(a1 + ko);                         \
+        P##a2 = *(const uint4*)(a2 + ko);                         \
+        P##a3 = *(const uint4*)(a3 + ko);                         \
+        P##b0 = *(const uint4*)(b0 + ko);                         \
+        P##b1 = *(const uint4*)(b0 + bstep + ko);                 \
+        if constexpr (BN == 128) {                                \
+            P##b2 = *(const uint4*)(b0 + 2 * bstep + ko);         \
+            P##b3 = *(const uint4*)(b0 + 3 * bstep + ko);         \
+        }                                                         \
     } while (0)
 #define SKR_STORE(P, buf)                                          \
     do {                                                           \
@@ -80,28 +86,32 @@ __global__ __launch_bounds__(256) void skinny_gemm_nt_kernel(
         *(uint4*)(&As[buf][(srow + 96) * LDK + skc]) = P##a3;      \
         *(uint4*)(&Bs[buf][srow * LDK + skc]) = P##b0;             \
         *(uint4*)(&Bs[buf][(srow + 32) * LDK + skc]) = P##b1;      \
+        if constexpr (BN == 128) {                                 \
+            *(uint4*)(&Bs[buf][(srow + 64) * LDK + skc]) = P##b2;  \
+            *(uint4*)(&Bs[buf][(srow + 96) * LDK + skc]) = P##b3;  \
+        }                                                          \
     } while (0)
 
-    f32x4 acc[2][4];
+    f32x4 acc[2][NJ];
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
     const int fr = lane & 15, fk = (lane >> 4) * 8;
     auto compute = [&](int buf) {
 #pragma unroll
         for (int ks = 0; ks < BK; ks += 32) {
-            bf16x8 af[2], bfr[4];
+            bf16x8 af[2], bfr[NJ];
 #pragma unroll
             for (int i = 0; i < 2; ++i)
                 af[i] = *(const bf16x8*)(&As[buf][(32 * w + 16 * i + fr) * LDK + ks + fk]);
 #pragma unroll
-            for (int j = 0; j < 4; ++j) bfr[j] = *(const bf16x8*)(&Bs[buf][(16 * j + fr) * LDK + ks + fk]);
+            for (int j = 0; j < NJ; ++j) bfr[j] = *(const bf16x8*)(&Bs[buf][(16 * j + fr) * LDK + ks + fk]);
 #pragma unroll
             for (int i = 0; i < 2; ++i)
 #pragma unroll
-                for (int j = 0; j < 4; ++j)
+                for (int j = 0; j < NJ; ++j)
                     acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
         }
     };
@@ -141,7 +151,7 @@ __global__ __launch_bounds__(256) void skinny_gemm_nt_kernel(
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
+        for (int j = 0; j < NJ; ++j)
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
                 const int row = 32 * w + 16 * i + (lane >> 4) * 4 + e;
@@ -152,17 +162,22 @@ __global__ __launch_bounds__(256) void skinny_gemm_nt_kernel(
 }  // namespace
 
 // C[z][s] (slab s of batch z) = A[z][:, s*kslice:(s+1)*kslice] . Bt[z][:, same]^T
-// Requirements: M <= 128, N % 64 == 0, kslice % 64 == 0, splits * kslice == K,
-// 16-byte aligned rows (lda, ldb multiples of 8 elements).
+// bn: N tile (64 or 128; 0 = choose). Requirements: M <= 128, N % bn == 0,
+// kslice % 64 == 0, splits * kslice == K, 16-byte aligned rows.
 SKR_API int skr_skinny_gemm(const void* A, int64_t lda, int64_t a_batch, const void* Bt, int64_t ldb,
                             int64_t b_batch, float* C, int64_t ldc, int64_t c_slab, int64_t c_batch, int M, int N,
-                            int K, int splits, int batch, hipStream_t s) {
-    if (M < 1 || M > BM || N % BN != 0 || splits < 1 || K % splits != 0) return -2;
+                            int K, int splits, int batch, int bn, hipStream_t s) {
+    if (bn == 0) bn = (N % 128 == 0 && (N / 128) * splits * batch >= 192) ? 128 : 64;
+    if (M < 1 || M > BM || (bn != 64 && bn != 128) || N % bn != 0 || splits < 1 || K % splits != 0) return -2;
     const int kslice = K / splits;
     if (kslice % BK != 0 || lda % 8 != 0 || ldb % 8 != 0) return -3;
     if (((uintptr_t)A | (uintptr_t)Bt) & 15) return -4;
-    hipLaunchKernelGGL(skinny_gemm_nt_kernel, dim3(N / BN, splits, batch), dim3(256), 0, s,
-                       (const __hip_bfloat16*)A, lda, a_batch, (const __hip_bfloat16*)Bt, ldb, b_batch, C, ldc,
-                       c_slab, c_batch, M, kslice);
+    const dim3 grid(N / bn, splits, batch);
+    if (bn == 128)
+        hipLaunchKernelGGL(skinny_gemm_nt_kernel<128>, grid, dim3(256), 0, s, (const __hip_bfloat16*)A, lda, a_batch,
+                           (const __hip_bfloat16*)Bt, ldb, b_batch, C, ldc, c_slab, c_batch, M, kslice);
+    else
+        hipLaunchKernelGGL(skinny_gemm_nt_kernel<64>, grid, dim3(256), 0, s, (const __hip_bfloat16*)A, lda, a_batch,
+                           (const __hip_bfloat16*)Bt, ldb, b_batch, C, ldc, c_slab, c_batch, M, kslice);
     return SKR_CHECK_LAUNCH();
 }

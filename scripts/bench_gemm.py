@@ -40,12 +40,13 @@ def main():
         bt = torch.randn(nd, N, K, device=dev).to(torch.bfloat16)
         b = bt.transpose(1, 2).contiguous()
         res = []
-        for S in sorted({gemm.plan_splits(M, N, K, nd), 1, 2, 4, 8, 16, 32}):
-            if S < 1 or (K // 64) % S:
-                continue
-            out = torch.empty(S, nd * M, N, device=dev)
-            us = timeit(lambda: gemm.rec_gemm(a, bt if nd > 1 else bt[0], out, S, nd))
-            res.append("S=%d %.1fus" % (S, us))
+        for bn in (64, 128):
+            for S in sorted({gemm.plan_splits(M, N, K, nd), 1, 2, 4, 8, 16, 32}):
+                if S < 1 or (K // 64) % S or N % bn:
+                    continue
+                out = torch.empty(S, nd * M, N, device=dev)
+                us = timeit(lambda: gemm.rec_gemm(a, bt if nd > 1 else bt[0], out, S, nd, bn))
+                res.append("b%d/S%d %.1f" % (bn, S, us))
         out1 = torch.empty(nd, M, N, device=dev)
         if nd == 1:
             us_lib = timeit(lambda: torch.mm(a, b[0], out_dtype=torch.float32, out=out1[0]))

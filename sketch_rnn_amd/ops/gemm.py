@@ -66,7 +66,8 @@ def plan_splits(M: int, N: int, K: int, batch: int = 1, dtype: torch.dtype = _BF
     return best
 
 
-def rec_gemm(a: torch.Tensor, bt: torch.Tensor, out: torch.Tensor, splits: int, nd: int = 1) -> torch.Tensor:
+def rec_gemm(a: torch.Tensor, bt: torch.Tensor, out: torch.Tensor, splits: int, nd: int = 1,
+             bn: int = 0) -> torch.Tensor:
     """Per-step recurrent product with split-K partial slabs.
 
     ``a [nd*M, K]`` (row stride may exceed K), ``bt [nd, N, K]`` (B^T, i.e.
@@ -86,7 +87,7 @@ def rec_gemm(a: torch.Tensor, bt: torch.Tensor, out: torch.Tensor, splits: int, 
     lib = native.require_hip()
     rc = lib.lib.skr_skinny_gemm(a.data_ptr(), a.stride(0), M * a.stride(0), bt.data_ptr(), bt.stride(-2),
                                  N * K if nd > 1 else 0, out.data_ptr(), N, out.stride(0), M * N, M, N, K, splits, nd,
-                                 torch.cuda.current_stream().cuda_stream)
+                                 bn, torch.cuda.current_stream().cuda_stream)
     if rc != 0:
         raise RuntimeError("skr_skinny_gemm failed (%d) for M=%d N=%d K=%d S=%d" % (rc, M, N, K, splits))
     return out
