@@ -246,8 +246,11 @@ class Arc(_Segment):
         if not self.sweep:
             delta -= 360.0
         self.delta = delta
-        # out-of-range radii are scaled up (F.6.6); points use the corrected radii
-        self._rx, self._ry, self._rot = rx, ry, rot
+        # Out-of-range radii are scaled up (F.6.6) for the centre computation
+        # only; point() evaluates with the radii as given. This matches the
+        # reference's svg.path (path.py:199-272) and its regression vectors
+        # (test_paths.py TestPath.test_svg_specs), which depend on it.
+        self._rx, self._ry, self._rot = self.radius.real, self.radius.imag, rot
 
     def point(self, pos: float) -> complex:
         ang = math.radians(self.theta + self.delta * pos)

@@ -86,6 +86,7 @@ class HipLib:
         lib.skr_skinny_gemm.argtypes = [_p, _i64, _i64, _p, _i64, _i64, _p, _i64, _i64, _i64, _i, _i, _i, _i, _i,
                                         _i, _p]
         lib.skr_skinny_gemm.restype = _i
+        lib.skr_mdn_sample.restype = _i
         fs, bs = lib.skr_lstm_fwd_args_size(), lib.skr_lstm_bwd_args_size()
         if fs != C.sizeof(LstmFwdArgs) or bs != C.sizeof(LstmBwdArgs):
             raise RuntimeError("libskrnn_hip.so arg-struct layout mismatch: fwd %d vs %d, bwd %d vs %d"

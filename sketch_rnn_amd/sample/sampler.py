@@ -1,0 +1,247 @@
+"""Sketch generation.
+
+Host samplers (exact semantics, any device, one sketch at a time):
+
+* :func:`sample_reference` -- the reference's ``Model.sample``
+  (``model.py:187-264``): zero first input, mixture temperature applied from
+  step 2 on, inverse-CDF draws with the "-1 -> last component" rule, sigma
+  NOT temperature-scaled, optional early stop on ``eoc`` (the ``eoc`` row is
+  kept), offsets multiplied by ``data_scale``. The reference's pen-temperature
+  bug (``pi_pdf /= temp_pen``, ``model.py:230``) is reproduced by default;
+  ``fix_pen_temperature=True`` applies the temperature to the pen logits.
+* :func:`sample_vae` -- sketch-rnn VAE semantics: start token
+  ``[0, 0, 1, 0, 0]``, temperature on mixture and pen, sigma scaled by the
+  temperature, optional greedy mode, ``z`` from N(0, I) or given.
+
+Device sampler (:class:`GraphDecoder`): B sketches in parallel, the
+N-step decode loop (decoder step -> MDN head -> ``csrc/sampler.hip``, which
+writes the next input on device) captured once into a HIP graph and
+replayed; finished rows emit end-of-sketch padding. No host round trip per
+stroke (the reference does two ``sess.run`` transfers per stroke).
+"""
+from __future__ import annotations
+
+import random as _random
+from typing import List, Optional, Tuple
+
+import numpy as np
+import torch
+
+from ..models import mdn as M
+
+
+def _get_pi_idx(x: float, pdf: np.ndarray) -> int:
+    acc = 0.0
+    for i in range(pdf.size):
+        acc += pdf[i]
+        if acc >= x:
+            return i
+    return -1
+
+
+def _softmax_np(v):
+    v = np.asarray(v, dtype=np.float64)
+    v = v - v.max()
+    e = np.exp(v)
+    return e / e.sum()
+
+
+@torch.no_grad()
+def sample_reference(model, num: int = 300, temp_mixture: float = 1.0, temp_pen: float = 1.0,
+                     stop_if_eoc: bool = False, rng: Optional[np.random.RandomState] = None,
+                     py_rng: Optional[_random.Random] = None, fix_pen_temperature: bool = False,
+                     device=None):
+    """Reference ``Model.sample``. Returns ``(strokes [n, 5], mixture_params)``."""
+    rng = rng or np.random.RandomState()
+    py_rng = py_rng or _random.Random()
+    cfg = model.cfg
+    dev = device or next(model.parameters()).device
+    Mx = cfg.num_mixture
+    prev_x = torch.zeros(1, 5, device=dev)
+    state = model.zero_state(1, dev)
+    strokes = np.zeros((num, 5), dtype=np.float32)
+    params = []
+    for i in range(num):
+        z, next_state = model.step(prev_x, state)
+        pi, mu1, mu2, s1, s2, rho, _, pen_logits = (t[0].double().cpu().numpy() for t in M.mixture_coef(z, Mx))
+        pi_pdf = pi.copy()
+        if i > 1:
+            pi_pdf = np.log(pi_pdf) / temp_mixture
+            pi_pdf -= pi_pdf.max()
+            pi_pdf = np.exp(pi_pdf)
+        pi_pdf /= pi_pdf.sum()
+        idx = _get_pi_idx(py_rng.random(), pi_pdf)
+        pen = pen_logits.copy()
+        if i > 1:
+            if fix_pen_temperature:
+                pen = pen / temp_pen
+            else:
+                pi_pdf /= temp_pen  # reference bug: rescales pi, pen temperature has no effect
+        pen_pdf = _softmax_np(pen)
+        pen_idx = _get_pi_idx(py_rng.random(), pen_pdf)
+        eos, eoc, cont = (1, 0, 0) if pen_idx == 0 else (0, 1, 0) if pen_idx == 1 else (0, 0, 1)
+        cov = [[s1[idx] ** 2, rho[idx] * s1[idx] * s2[idx]], [rho[idx] * s1[idx] * s2[idx], s2[idx] ** 2]]
+        x1, x2 = rng.multivariate_normal([mu1[idx], mu2[idx]], cov, 1)[0]
+        strokes[i] = [x1, x2, eos, eoc, cont]
+        params.append([pi_pdf, mu1, mu2, s1, s2, rho, pen_pdf])
+        if stop_if_eoc and eoc == 1:
+            strokes = strokes[: i + 1]
+            break
+        prev_x = torch.tensor([[x1, x2, eos, eoc, cont]], dtype=torch.float32, device=dev)
+        state = next_state
+    strokes[:, 0:2] *= cfg.data_scale
+    return strokes, params
+
+
+def _adjust_temp(pdf: np.ndarray, temp: float) -> np.ndarray:
+    p = np.log(pdf) / temp
+    p -= p.max()
+    p = np.exp(p)
+    return p / p.sum()
+
+
+@torch.no_grad()
+def sample_vae(model, seq_len: int = 250, temperature: float = 1.0, greedy: bool = False,
+               z: Optional[torch.Tensor] = None, label: Optional[int] = None,
+               rng: Optional[np.random.RandomState] = None, py_rng: Optional[_random.Random] = None):
+    """One sketch from the VAE decoder. Returns ``(strokes5 [seq_len, 5], params)``
+    in the magenta layout (convert with ``data.strokes.to_normal_strokes``)."""
+    rng = rng or np.random.RandomState()
+    py_rng = py_rng or _random.Random()
+    cfg = model.cfg
+    dev = next(model.parameters()).device
+    if cfg.conditional and z is None:
+        z = torch.as_tensor(rng.randn(1, cfg.z_size), dtype=torch.float32, device=dev)
+    lab = torch.tensor([label], device=dev) if (label is not None and cfg.num_classes > 0) else None
+    zc = model.condition(z if cfg.conditional else None, lab, 1, dev)
+    state = model.initial_state(zc, 1, dev)
+    prev_x = torch.tensor([[0.0, 0.0, 1.0, 0.0, 0.0]], device=dev)
+    strokes = np.zeros((seq_len, 5), dtype=np.float32)
+    params = []
+    for i in range(seq_len):
+        zh, state = model.decode_step(prev_x, zc, state)
+        pi, mu1, mu2, s1, s2, rho, pen, _ = (t[0].double().cpu().numpy() for t in M.mixture_coef(zh, cfg.num_mixture))
+        if greedy:
+            idx, pidx = int(np.argmax(pi)), int(np.argmax(pen))
+            x1, x2 = mu1[idx], mu2[idx]
+        else:
+            idx = _get_pi_idx(py_rng.random(), _adjust_temp(pi, temperature))
+            pidx = _get_pi_idx(py_rng.random(), _adjust_temp(pen, temperature))
+            sa, sb = s1[idx] * temperature, s2[idx] * temperature
+            cov = [[sa * sa, rho[idx] * sa * sb], [rho[idx] * sa * sb, sb * sb]]
+            x1, x2 = rng.multivariate_normal([mu1[idx], mu2[idx]], cov, 1)[0]
+        row = [x1, x2, 0.0, 0.0, 0.0]
+        row[2 + pidx] = 1.0
+        strokes[i] = row
+        params.append([pi, mu1, mu2, s1, s2, rho, pen])
+        prev_x = torch.tensor([row], dtype=torch.float32, device=dev)
+    return strokes, params
+
+
+# =====================================================================================
+# device sampler + HIP graph decode
+# =====================================================================================
+def mdn_sample_device(zh: torch.Tensor, M_: int, mode: int, temp: float, greedy: bool, fix_pen: bool,
+                      seed: torch.Tensor, step: int, out_row: torch.Tensor, next_x: torch.Tensor,
+                      done: torch.Tensor, params: Optional[torch.Tensor] = None) -> None:
+    from ..utils import native
+    lib = native.require_hip()
+    import ctypes
+    rc = lib.lib.skr_mdn_sample(ctypes.c_void_p(zh.data_ptr()), ctypes.c_int64(zh.stride(0)), ctypes.c_int(zh.shape[0]),
+                                ctypes.c_int(M_), ctypes.c_int(mode), ctypes.c_float(temp), ctypes.c_int(int(greedy)),
+                                ctypes.c_int(int(fix_pen)), ctypes.c_void_p(seed.data_ptr()), ctypes.c_uint32(step),
+                                ctypes.c_void_p(out_row.data_ptr()), ctypes.c_int64(out_row.stride(0)),
+                                ctypes.c_void_p(next_x.data_ptr()), ctypes.c_int64(next_x.stride(0)),
+                                ctypes.c_void_p(done.data_ptr()),
+                                ctypes.c_void_p(params.data_ptr() if params is not None else 0),
+                                ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
+    if rc != 0:
+        raise RuntimeError("skr_mdn_sample failed (%d)" % rc)
+
+
+class GraphDecoder:
+    """Batched autoregressive decode captured in one HIP graph.
+
+    ``model`` is a :class:`~sketch_rnn_amd.models.reference.SketchRNN` (mode
+    ``reference``) or :class:`~sketch_rnn_amd.models.vae.SketchVAE` (mode
+    ``vae``). ``run()`` replays the graph and returns ``strokes [B, N, 5]``
+    (offsets in model units; reference mode multiplies by ``data_scale``)
+    plus the per-row number of valid steps.
+    """
+
+    def __init__(self, model, batch: int, steps: int, temperature: float = 1.0, greedy: bool = False,
+                 fix_pen_temperature: bool = False, use_graph: bool = True):
+        self.model = model
+        self.kind = "vae" if hasattr(model, "encoder") else "reference"
+        self.B, self.N = batch, steps
+        self.temp, self.greedy, self.fix_pen = float(temperature), bool(greedy), bool(fix_pen_temperature)
+        dev = next(model.parameters()).device
+        self.dev = dev
+        cfg = model.cfg
+        self.Mx = cfg.num_mixture
+        self.mode = 1 if self.kind == "vae" else 0
+        self.seed = torch.zeros(1, dtype=torch.int64, device=dev)
+        self.out = torch.zeros(batch, steps, 5, device=dev)
+        self.done = torch.zeros(batch, dtype=torch.int32, device=dev)
+        self.x0 = torch.zeros(batch, 5, device=dev)
+        if self.kind == "vae":
+            self.x0[:, 2] = 1.0
+            self.z = torch.zeros(batch, max(cfg.z_size, 1), device=dev)
+            self.labels = torch.zeros(batch, dtype=torch.int64, device=dev)
+        self.graph = None
+        self.use_graph = use_graph and dev.type == "cuda"
+
+    @torch.no_grad()
+    def _decode(self):
+        model, B = self.model, self.B
+        self.done.zero_()
+        x = self.x0.clone()
+        if self.kind == "vae":
+            cfg = model.cfg
+            lab = self.labels if cfg.num_classes > 0 else None
+            zc = model.condition(self.z if cfg.conditional else None, lab, B, self.dev)
+            state = model.initial_state(zc, B, self.dev)
+        else:
+            zc = None
+            state = model.zero_state(B, self.dev)
+        for t in range(self.N):
+            if self.kind == "vae":
+                zh, state = model.decode_step(x, zc, state)
+            else:
+                zh, state = model.step(x, state)
+            nx = torch.empty(B, 5, device=self.dev)
+            mdn_sample_device(zh.contiguous(), self.Mx, self.mode, self.temp, self.greedy, self.fix_pen, self.seed, t,
+                              self.out[:, t], nx, self.done)
+            x = nx
+
+    @torch.no_grad()
+    def run(self, seed: int = 0, z: Optional[torch.Tensor] = None, labels: Optional[torch.Tensor] = None):
+        if z is not None:
+            self.z.copy_(z)
+        elif self.kind == "vae":
+            g = torch.Generator(device=self.dev).manual_seed(int(seed))
+            self.z.copy_(torch.randn(self.z.shape, device=self.dev, generator=g))
+        if labels is not None:
+            self.labels.copy_(labels)
+        self.seed.fill_(int(seed))
+        if self.use_graph:
+            if self.graph is None:
+                s = torch.cuda.Stream()
+                s.wait_stream(torch.cuda.current_stream())
+                with torch.cuda.stream(s):
+                    self._decode()
+                torch.cuda.current_stream().wait_stream(s)
+                self.graph = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(self.graph):
+                    self._decode()
+            self.graph.replay()
+        else:
+            self._decode()
+        strokes = self.out.clone()
+        stop_col = 4 if self.kind == "vae" else 3
+        hits = strokes[:, :, stop_col] > 0
+        lengths = torch.where(hits.any(1), hits.float().argmax(1) + 1, torch.full_like(hits[:, 0], self.N,
+                                                                                      dtype=torch.long))
+        if self.kind == "reference":
+            strokes[:, :, 0:2] *= self.model.cfg.data_scale
+        return strokes, lengths
