@@ -67,6 +67,23 @@ class StrokeDataset:
             s[:, 0:2] /= scale_factor
         return scale_factor
 
+    # -- resume ----------------------------------------------------------------------
+    @staticmethod
+    def _rng_state(r: np.random.RandomState):
+        name, keys, pos, has_g, g = r.get_state()
+        return [name, keys.tolist(), int(pos), int(has_g), float(g)]
+
+    @staticmethod
+    def _set_rng(r: np.random.RandomState, st):
+        r.set_state((st[0], np.asarray(st[1], dtype=np.uint32), st[2], st[3], st[4]))
+
+    def state_dict(self) -> dict:
+        return {"rng": self._rng_state(self.rng), "aug_rng": self._rng_state(self.aug_rng)}
+
+    def load_state_dict(self, sd: dict) -> None:
+        self._set_rng(self.rng, sd["rng"])
+        self._set_rng(self.aug_rng, sd["aug_rng"])
+
     # -- batching ------------------------------------------------------------------
     def _from_indices(self, indices, augment: bool = True):
         batch, lens = [], []

@@ -129,6 +129,22 @@ class SketchLoader:
         self._perm = np.ascontiguousarray(perm, dtype=np.int64)
         self._cursor = _Cursor(len(self._perm))
 
+    def state_dict(self) -> dict:
+        """JSON-serialisable cursor + RNG state (exact resume mid-epoch)."""
+        name, keys, pos, has_g, g = self.rng.get_state()
+        return {"rng": [name, keys.tolist(), int(pos), int(has_g), float(g)], "index": self.index.tolist(),
+                "pointer": int(self._cursor.pointer), "epoch_finished": bool(self._cursor.epoch_finished)}
+
+    def load_state_dict(self, sd: dict) -> None:
+        name, keys, pos, has_g, g = sd["rng"]
+        self.rng.set_state((name, np.asarray(keys, dtype=np.uint32), pos, has_g, g))
+        self.index = np.asarray(sd["index"], dtype=np.int64)
+        perm = self.index[self.rank::self.world_size] if self.world_size > 1 else self.index
+        self._perm = np.ascontiguousarray(perm, dtype=np.int64)
+        self._cursor = _Cursor(len(self._perm))
+        self._cursor.pointer = int(sd["pointer"])
+        self._cursor.epoch_finished = bool(sd["epoch_finished"])
+
     def current_data(self) -> np.ndarray:
         return self.raw_data[self._perm[self._cursor.pointer]]
 

@@ -62,8 +62,10 @@ def mdn_loss_torch(z: torch.Tensor, target: torch.Tensor, M: int, mode: str = "m
                    stroke_importance: float = 200.0, is_training: bool = True,
                    clamp: float = 1e-20, eps: float = 1e-6) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
     """Returns ``(total, shape_term, pen_term)`` (each a mean over rows)."""
-    z = z.reshape(-1, z.shape[-1]).float()
-    target = target.reshape(-1, 5).float()
+    z = z.reshape(-1, z.shape[-1])
+    if z.dtype != torch.float64:
+        z = z.float()  # low-precision head outputs: the loss math runs in fp32
+    target = target.reshape(-1, 5).to(z.dtype)
     x1, x2, pen_t = target[:, 0], target[:, 1], target[:, 2:5]
     logS = log_mixture_density(z, x1, x2, M)
     ce = -(pen_t * torch.log_softmax(z[:, 0:3], -1)).sum(-1)

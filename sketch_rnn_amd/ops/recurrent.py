@@ -46,10 +46,19 @@ def _stream() -> int:
     return torch.cuda.current_stream().cuda_stream
 
 
+_SEED_CONST = {}
+
+
 def _seed_tensor(seed, device) -> torch.Tensor:
     if torch.is_tensor(seed):
         return seed.to(device=device, dtype=torch.int64).reshape(1)
-    return torch.tensor([int(seed)], dtype=torch.int64, device=device)
+    # constant seeds are cached on device: a host->device copy is not allowed
+    # while a HIP graph is being captured (eager warm-up creates the entry)
+    key = (str(device), int(seed))
+    t = _SEED_CONST.get(key)
+    if t is None:
+        t = _SEED_CONST[key] = torch.tensor([int(seed)], dtype=torch.int64, device=device)
+    return t
 
 
 def _lp_kind(t: torch.Tensor) -> int:

@@ -97,11 +97,15 @@ class GradReducer:
                 works.append(dist.all_reduce(b, op=dist.ReduceOp.SUM, async_op=True))
         if async_op:
             return works
+        self.wait(works)
+        return []
+
+    def wait(self, works) -> None:
+        """Complete an ``all_reduce(async_op=True)`` (and apply 1/world)."""
         for w in works:
             w.wait()
-        if self._premul is None:
+        if self.world > 1 and self._premul is None:
             self.grad.mul_(1.0 / self.world)
-        return []
 
 
 def average_scalars(d: Dict[str, float]) -> Dict[str, float]:

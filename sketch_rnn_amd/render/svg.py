@@ -76,8 +76,12 @@ def draw_stroke_color_array(data: Sequence, factor: float = 1, svg_filename: Opt
                             stroke_width: float = 1, block_size: float = 200, maxcol: int = 5,
                             color_mode: bool = True, rng: Optional[_random.Random] = None) -> Optional[SvgDoc]:
     num_char = len(data)
-    if num_char < 1:
-        return None
+    if num_char < 1:  # nothing accepted: still emit a (blank) canvas
+        doc = SvgDoc(block_size, block_size)
+        doc.rect(0, 0, block_size, block_size, "white")
+        if svg_filename:
+            doc.save(svg_filename)
+        return doc
     rng = rng or _random.Random()
     numrow = math.ceil(num_char / maxcol)
     w, h = block_size * min(num_char, maxcol), block_size * numrow

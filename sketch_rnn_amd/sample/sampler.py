@@ -21,6 +21,7 @@ stroke (the reference does two ``sess.run`` transfers per stroke).
 """
 from __future__ import annotations
 
+import math
 import random as _random
 from typing import List, Optional, Tuple
 
@@ -141,9 +142,67 @@ def sample_vae(model, seq_len: int = 250, temperature: float = 1.0, greedy: bool
 # =====================================================================================
 # device sampler + HIP graph decode
 # =====================================================================================
+_SAMPLE_STREAM = 0x5A3D
+
+
+def mdn_sample_torch(zh: torch.Tensor, M_: int, mode: int, temp: float, greedy: bool, fix_pen: bool,
+                     seed, step: int, out_row: torch.Tensor, next_x: torch.Tensor, done: torch.Tensor,
+                     params: Optional[torch.Tensor] = None) -> None:
+    """PyTorch transcription of ``csrc/sampler.hip`` (same hash random
+    numbers, same draws): the CPU path of :class:`GraphDecoder` and the
+    oracle the kernel is tested against."""
+    from ..models.cells import hash_uniform
+    B = zh.shape[0]
+    z = zh.float()
+    u = hash_uniform(seed, _SAMPLE_STREAM, step, (B, 4), device=z.device)
+    use_t = mode == 1 or step > 1
+    logits = z[:, 3:3 + M_] * ((1.0 / temp) if use_t else 1.0)
+    pi = torch.softmax(logits, -1)
+    ar = torch.arange(B, device=z.device)
+    if greedy:
+        idx = pi.argmax(-1)
+    else:
+        hit = torch.cumsum(pi, -1) >= u[:, 0:1]
+        idx = torch.where(hit.any(-1), hit.float().argmax(-1), torch.full_like(ar, M_ - 1))
+    pt = (1.0 / temp) if (mode == 1 or (fix_pen and step > 1)) else 1.0
+    pp = torch.softmax(z[:, 0:3] * pt, -1)
+    if greedy:
+        pidx = pp.argmax(-1)
+    else:
+        hit = torch.cumsum(pp, -1) >= u[:, 1:2]
+        pidx = torch.where(hit.any(-1), hit.float().argmax(-1), torch.full_like(ar, 2))
+    col = lambda k: z[ar, 3 + k * M_ + idx]  # noqa: E731
+    mu1, mu2, s1, s2, rho = col(1), col(2), torch.exp(col(3)), torch.exp(col(4)), torch.tanh(col(5))
+    if mode == 1:
+        s1, s2 = s1 * temp, s2 * temp
+    x1, x2 = mu1, mu2
+    if not greedy:
+        r = torch.sqrt(-2.0 * torch.log(torch.clamp(u[:, 2], min=1e-12)))
+        n1, n2 = r * torch.cos(2 * math.pi * u[:, 3]), r * torch.sin(2 * math.pi * u[:, 3])
+        x1 = mu1 + s1 * n1
+        x2 = mu2 + s2 * (rho * n1 + torch.sqrt(torch.clamp(1 - rho * rho, min=0.0)) * n2)
+    row = torch.zeros(B, 5, device=z.device)
+    row[:, 0], row[:, 1] = x1, x2
+    row[ar, 2 + pidx] = 1.0
+    stop_col = 4 if mode == 1 else 3
+    pad = torch.zeros(B, 5, device=z.device)
+    pad[:, stop_col] = 1.0
+    out_row.copy_(torch.where((done != 0).unsqueeze(-1), pad, row))
+    next_x.copy_(row)
+    done.copy_(torch.where(pidx + 2 == stop_col, torch.ones_like(done), done))
+    if params is not None:
+        params.copy_(torch.stack([idx.float(), pidx.float(), s1, s2], -1))
+
+
 def mdn_sample_device(zh: torch.Tensor, M_: int, mode: int, temp: float, greedy: bool, fix_pen: bool,
                       seed: torch.Tensor, step: int, out_row: torch.Tensor, next_x: torch.Tensor,
                       done: torch.Tensor, params: Optional[torch.Tensor] = None) -> None:
+    if zh.device.type != "cuda":
+        return mdn_sample_torch(zh, M_, mode, temp, greedy, fix_pen, seed, step, out_row, next_x, done, params)
+    assert zh.dtype == torch.float32 and zh.stride(1) == 1 and zh.shape[1] >= 3 + 6 * M_
+    assert out_row.dtype == torch.float32 and out_row.stride(-1) == 1 and out_row.shape[0] == zh.shape[0]
+    assert next_x.shape == (zh.shape[0], 5) and next_x.stride(-1) == 1
+    assert done.dtype == torch.int32 and done.numel() == zh.shape[0] and seed.dtype == torch.int64
     from ..utils import native
     lib = native.require_hip()
     import ctypes

@@ -63,6 +63,7 @@ class ReferenceTrainer:
         B = cfg.batch_size
         self.state = self.model.zero_state(B, self.device)
         self.seed = torch.zeros(1, dtype=torch.int64, device=self.device)
+        self._in_epoch = False
 
     # ---------------------------------------------------------------------------------
     def _step_fn(self, x, y, state_flat):
@@ -106,8 +107,9 @@ class ReferenceTrainer:
     # ---------------------------------------------------------------------------------
     def save(self):
         st = {"s%d" % i: t for i, t in enumerate(self._flatten(self.state))}
-        extra = {"epoch": self.epoch, "b_processed": self.b_processed,
-                 "pointer": int(self.loader.pointer), "rng": self.loader.rng.get_state()[1].tolist()[:4]}
+        extra = {"epoch": self.epoch, "in_epoch": self._in_epoch, "b_processed": self.b_processed,
+                 "seed": int(self.seed.item()),
+                 "loader": self.loader.state_dict()}
         path = ckpt.save_checkpoint(self.save_dir, self.b_processed, self.model, self.opt, self.cfg,
                                     extra=extra, state=st)
         self.log("model saved to {}".format(path))
@@ -120,9 +122,14 @@ class ReferenceTrainer:
         step, extra, st = ckpt.load_checkpoint(path, self.model, self.opt)
         self.b_processed = int(extra.get("b_processed", step))
         self.epoch = int(extra.get("epoch", 0))
+        self.seed.fill_(int(extra.get("seed", self.b_processed)))
         for i, t in enumerate(self._flatten(self.state)):
             if "s%d" % i in st:
                 t.copy_(st["s%d" % i])
+        if "loader" in extra:
+            # continue the interrupted epoch: same permutation, cursor, RNG and carried state
+            self.loader.load_state_dict(extra["loader"])
+            self._in_epoch = bool(extra.get("in_epoch", False))
         self.log("resumed from %s (epoch %d, batch %d)" % (path, self.epoch, self.b_processed))
         return True
 
@@ -130,19 +137,24 @@ class ReferenceTrainer:
         cfg, loader = self.cfg, self.loader
         num_epochs = cfg.num_epochs if num_epochs is None else num_epochs
         done = 0
-        for e in range(self.epoch, num_epochs):
-            self.epoch = e
+        while self.epoch < num_epochs:
+            e = self.epoch
             self.opt.set_lr(schedules.reference_lr(cfg, e))
-            loader.reset_index_pointer()
-            for s in self._flatten(self.state):
-                s.zero_()
-            while not loader.epoch_finished:
+            if not self._in_epoch:  # a resumed / interrupted epoch continues where it stopped
+                loader.reset_index_pointer()
+                for s in self._flatten(self.state):
+                    s.zero_()
+                self._in_epoch = True
+            while self._in_epoch:
                 t0 = time.time()
                 x, y = loader.next_batch()
                 out = self.train_step(_to_device(x, self.device), _to_device(y, self.device))
                 cost, shape, pen = (float(out[k]) for k in ("cost", "shape", "pen"))
                 dt = time.time() - t0
                 self.b_processed += 1
+                if loader.epoch_finished:
+                    self._in_epoch = False
+                    self.epoch += 1
                 self.log("{}/{} (epoch {} batch {}), cost = {:.2f} ({:.2f}+{:.4f}), time/batch = {:.2f}".format(
                     loader.pointer + e * loader.num_samples, num_epochs * loader.num_samples,
                     e, self.b_processed, cost, shape, pen, dt))
@@ -260,14 +272,25 @@ class VAETrainer:
     def save(self):
         if self.rank != 0:
             return None
-        return ckpt.save_checkpoint(self.save_dir, self.step, self.model, self.opt, self.cfg,
-                                    extra={"step": self.step})
+        extra = {"step": self.step, "seed": int(self.seed.item())}
+        if hasattr(self.train_set, "state_dict"):
+            extra["data"] = self.train_set.state_dict()
+        return ckpt.save_checkpoint(self.save_dir, self.step, self.model, self.opt, self.cfg, extra=extra)
 
     def resume(self) -> bool:
+        """Weights, Adam moments/step, schedules (a function of the step),
+        dropout seed and data RNG. With DP every rank loads the same file
+        (rank 0 wrote it); the per-rank augmentation RNG restarts from the
+        saved rank-0 stream offset by rank."""
         path = ckpt.latest_checkpoint(self.save_dir)
         if path is None:
             return False
-        self.step, _, _ = ckpt.load_checkpoint(path, self.model, self.opt)
+        self.step, extra, _ = ckpt.load_checkpoint(path, self.model, self.opt)
+        self.seed.fill_(int(extra.get("seed", self.step)))
+        if "data" in extra and hasattr(self.train_set, "load_state_dict"):
+            self.train_set.load_state_dict(extra["data"])
+            if self.rank:
+                self.train_set.aug_rng.seed((self.cfg.seed * 7919 + 1 + self.rank + self.step) % (2 ** 32))
         return True
 
     def train(self, num_steps: Optional[int] = None, eval_every: int = 0, log_every: int = 20):
