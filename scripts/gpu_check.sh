@@ -32,6 +32,9 @@ for s in "${steps[@]}"; do
         bench) run bench 600 python bench.py --steps 10 --warmup 2 ;;
         bench_fp32) run bench_fp32 600 python bench.py --steps 5 --warmup 2 --dtype fp32 ;;
         bench_small) run bench_small 600 python bench.py --steps 10 --warmup 2 --config vae_small ;;
+        bench_torch) run bench_torch 900 python bench.py --steps 3 --warmup 1 --backend torch --no-eval ;;
+        bench_torch_small) run bench_torch_small 600 python bench.py --steps 3 --warmup 1 --backend torch --no-eval --config vae_small ;;
+        bench_sample) run bench_sample 600 python scripts/bench_sample.py ;;
         prof) run prof 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --no-eval ;;
         *) echo "unknown step $s"; exit 2 ;;
     esac
