@@ -1,6 +1,5 @@
-// Argument blocks shared by the fused LSTM-family cell kernels
-// (csrc/lstm_cell.hip: one workgroup per row; csrc/lstm_cluster.hip: a row
-// split over a cluster of workgroups). Mirrored field for field by
+// Argument blocks of the fused LSTM-family cell kernels (csrc/lstm_cell.hip;
+// a row runs on `cluster` workgroups). Mirrored field for field by
 // sketch_rnn_amd/ops/_hipapi.py (size-checked at load).
 #pragma once
 #include "common.h"
@@ -16,7 +15,7 @@ struct FwdArgs {
     const float* R;  int64_t ld_R;     // [B, 4H]: h_prev @ W_h (fp32)
     int R_nslab; int64_t R_slab;       // R is the sum of R_nslab split-K partial slabs
     const float* vec; int64_t vec_gs; int64_t vec_ld;  // MOD: element (k,b,u) at k*gs + b*ld + u
-    const float* vec_bias;             // MOD: [12, H] added to vec (or null)
+    const float* vec_bias;             // MOD: [12, H] added to vec (required)
     const float* bias;                 // MOD: [4H]
     const float* c_prev;               // [B, H]
     const float* ln_g; const float* ln_b; const float* lnc_g; const float* lnc_b;
@@ -33,7 +32,7 @@ struct FwdArgs {
     float* h_carry;                    // [B, H]
     void* h_lp; int64_t ld_lp; int lp_kind;  // 0: none, 1: bf16, 2: fp32
     float* c_carry;                    // [B, H]
-    // cluster mode (csrc/lstm_cluster.hip): rows split over `cluster` workgroups
+    // rows split over `cluster` workgroups (LayerNorm statistics exchanged in-launch)
     int cluster;                       // <= 1: one workgroup per row
     int* sync;                         // [2][B] arrival counters for this step (zeroed per sequence)
     float* part;                       // [2][B][cluster][8] partial statistics
@@ -68,30 +67,6 @@ struct BwdArgs {
     float* dinit_h; float* dinit_c;    // [B, H] accumulated on reset rows (or null)
     int cluster; int* sync; float* part; int* err;
 };
-
-// Sum of n split-K partial slabs (n <= 1: a plain load); loads issued together.
-__device__ __forceinline__ float ld_slabs(const float* p, int64_t idx, int n, int64_t slab) {
-    float v = p[idx];
-    int s = 1;
-    for (; s + 3 < n; s += 4) {
-        const float a = p[s * slab + idx], b = p[(s + 1) * slab + idx];
-        const float c = p[(s + 2) * slab + idx], d = p[(s + 3) * slab + idx];
-        v += (a + b) + (c + d);
-    }
-    for (; s < n; ++s) v += p[s * slab + idx];
-    return v;
-}
-
-__device__ __forceinline__ float vec_at(const float* v, const float* vb, int64_t gs, int64_t ld, int k, int b, int u,
-                                        int H) {
-    float x = v[k * gs + (int64_t)b * ld + u];
-    if (vb) x += vb[k * H + u];
-    return x;
-}
-
-// csrc/lstm_cluster.hip
-int launch_cluster(const FwdArgs& a, bool ln, bool mod, hipStream_t s);
-int launch_cluster(const BwdArgs& a, bool ln, bool mod, hipStream_t s);
 
 __device__ __forceinline__ float dropout_mult(bool on, uint32_t key, int64_t idx, float keep) {
     if (!on) return 1.f;

@@ -1,0 +1,564 @@
+// Fused LSTM-family cell step (forward + backward) for gfx950.
+//
+// Everything between one step's recurrent GEMM and the next step's GEMM is
+// one launch:
+//
+//   g      = xp + R                              (plain / LN-LSTM)
+//          = xh*ax + R*ah + bh + bias            (HyperLSTM main cell, MOD;
+//                                                 a/b = vec + vec_bias per gate)
+//   y      = LN_all(g)*gamma + beta              (LN: per gate block over H)
+//   c'     = c*sig(y_f + fb) + sig(y_i)*tanh(y_j)*mask
+//   h'     = tanh(LN(c')*gc + bc)*sig(y_o)  |  tanh(c')*sig(y_o)
+//   carry  = reset[b] ? init : (h', c')          (reference eoc reset)
+//
+// plus the saves the backward needs and a bf16 copy of the carried h written
+// straight into the next GEMM's A operand (a column slice of a concatenated
+// [h | h_hyper] buffer, hence the explicit row stride). R is the sum of the
+// split-K partial slabs of csrc/skinny_gemm.hip, reduced here while loading.
+// The recurrent dropout mask is regenerated from a stateless hash of
+// (seed, stream, step, b*H + u) in both passes -- never stored. Rows can be
+// split into parameter groups (grp_rows): the two directions of the
+// bidirectional encoder run as 2B rows of one launch.
+//
+// Geometry: grid (C, B), 256 threads; workgroup c of row b owns the UPT*256
+// contiguous hidden units [c*UPT*256, (c+1)*UPT*256), every thread UPT units
+// (stride 256) x 4 gates. The step is latency-bound (B ~ 100 rows, a few
+// hundred KB per row), so the kernel is written for memory-level
+// parallelism: every global load of a thread is issued up front, from
+// clamped (never predicated) addresses, with the split-K slab count a
+// template parameter -- no branch or runtime loop sits between a load and
+// its first use, so one s_waitcnt covers them all. (A per-gate load -> use
+// chain costs one full memory round trip per dependency.)
+//
+// C > 1 (a row split over C workgroups) only matters with LayerNorm: the C
+// workgroups exchange partial (mean, M2) statistics inside the launch --
+// write-through (sc1) agent stores, vmcnt drain, one relaxed agent atomic
+// add on the row's arrival counter, one lane polls with s_sleep backoff
+// (bounded: a timeout sets *err for the host), sc1 loads, Chan's combine.
+// Counters are per (step, row, phase), each on its own 128-byte line, and
+// zeroed once per sequence. All B*C workgroups must be co-resident; the host
+// only picks C > 1 when that holds.
+//
+// Reference semantics: model.py:19-23 (BasicLSTMCell), model.py:82-92 (eoc
+// reset); LayerNorm-/Hyper-LSTM semantics: sketch_rnn_amd/models/cells.py.
+#include <type_traits>
+
+#include "lstm_args.h"
+
+namespace {
+
+using namespace skr;
+
+constexpr int NT = 256, NW = NT / 64;
+constexpr int kMaxCluster = 16;
+constexpr unsigned kSpinLimit = 1u << 21;
+constexpr int kSyncStride = 32;   // ints per arrival counter (128 B)
+constexpr int kPartStride = 32;   // floats per workgroup partial slot (128 B)
+
+// Sum of the NS split-K partial slabs at idx (NS > 0: compile-time count,
+// all loads independent); NS == 0: runtime count n, batches of 8 clamped loads.
+template <int NS>
+__device__ __forceinline__ float slab_sum(const float* p, int64_t idx, int n, int64_t slab) {
+    if constexpr (NS > 0) {
+        float v[NS];
+#pragma unroll
+        for (int s = 0; s < NS; ++s) v[s] = p[s * slab + idx];
+#pragma unroll
+        for (int w = 1; w < NS; w *= 2)
+#pragma unroll
+            for (int s = 0; s + w < NS; s += 2 * w) v[s] += v[s + w];
+        return v[0];
+    } else {
+        float v = 0.f;
+        for (int s0 = 0; s0 < n; s0 += 8) {
+            float t[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) t[k] = p[(int64_t)min(s0 + k, n - 1) * slab + idx];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) v += (s0 + k < n) ? t[k] : 0.f;
+        }
+        return v;
+    }
+}
+
+// Publish `nv` floats of this workgroup (LDS `mine`), wait for the row's C
+// workgroups, gather all C*nv values into LDS `all` ([C][nv]).
+__device__ void cluster_allgather(float* part, int* cnt, int* err, int b, int c, int C, const float* mine, int nv,
+                                  float* all) {
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        float* dst = part + ((int64_t)b * C + c) * kPartStride;
+        for (int i = 0; i < nv; ++i) __hip_atomic_store(dst + i, mine[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        unsigned spins = 0;
+        while (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < C) {
+            __builtin_amdgcn_s_sleep(1);
+            if (++spins > kSpinLimit) {
+                __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                break;
+            }
+        }
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < C * nv; i += NT) {
+        const int cc = i / nv, k = i - cc * nv;
+        all[i] = __hip_atomic_load(part + ((int64_t)b * C + cc) * kPartStride + k, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+}
+
+// Row mean / variance from per-workgroup (mean, M2) pairs (Chan et al.);
+// workgroup cc holds min(span, H - cc*span) of the row's H values.
+__device__ __forceinline__ void chan_combine(const float* all, int C, int nv, int q, int H, int span, float& mean,
+                                             float& var) {
+    float m = 0.f;
+    for (int cc = 0; cc < C; ++cc) m += (float)min(span, H - cc * span) * all[cc * nv + q];
+    m /= (float)H;
+    float m2 = 0.f;
+    for (int cc = 0; cc < C; ++cc) {
+        const float n = (float)min(span, H - cc * span);
+        const float d = all[cc * nv + q] - m;
+        m2 += all[cc * nv + (nv / 2) + q] + n * d * d;
+    }
+    mean = m;
+    var = m2 / (float)H;
+}
+
+// Row-wide sums of N per-thread values: block reduction, then (C > 1) the
+// in-launch exchange. `slot` selects the (counter, partial) pair of this phase.
+template <int N>
+__device__ __forceinline__ void row_sum(float (&v)[N], float* lds, float* mine, float* all, int slot,
+                                        int* sync_base, float* part_base, int* err, int B, int b, int c, int C) {
+    block_sum<N, NW>(v, lds);
+    if (C <= 1) return;
+    if (threadIdx.x == 0) {
+#pragma unroll
+        for (int i = 0; i < N; ++i) mine[i] = v[i];
+    }
+    cluster_allgather(part_base + (int64_t)slot * B * C * kPartStride, sync_base + (slot * B + b) * kSyncStride,
+                      err, b, c, C, mine, N, all);
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+        float s = 0.f;
+        for (int cc = 0; cc < C; ++cc) s += all[cc * N + i];
+        v[i] = s;
+    }
+}
+
+template <int UPT, int NS, bool LN, bool MOD>
+__global__ __launch_bounds__(NT) void cell_fwd(const FwdArgs a) {
+    __shared__ float lds[NW * 8];
+    __shared__ float mine[8];
+    __shared__ float all[kMaxCluster * 8];
+    const int c = blockIdx.x, b = blockIdx.y, C = gridDim.x, tid = threadIdx.x, H = a.H;
+    const int span = UPT * NT, base = c * span;
+    const int nloc = max(0, min(span, H - base));
+    const int grp = a.grp_rows > 0 ? b / a.grp_rows : 0;
+    const float* ln_g = LN ? a.ln_g + grp * 4 * H : nullptr;
+    const float* ln_b = LN ? a.ln_b + grp * 4 * H : nullptr;
+    const float* lnc_g = LN ? a.lnc_g + grp * H : nullptr;
+    const float* lnc_b = LN ? a.lnc_b + grp * H : nullptr;
+    const bool keep_on = a.keep < 1.0f;
+    const uint32_t key = keep_on ? hash_key(*a.seed, a.stream, a.step) : 0u;
+    const bool r = a.reset != nullptr && a.reset[b] != 0.f;
+
+    // ---- every load up front (clamped indices; results of u >= H discarded)
+    float g[UPT][4], cp[UPT], lg[UPT][4], lb[UPT][4], lcg[UPT], lcb[UPT];
+    bool on[UPT];
+#pragma unroll
+    for (int k = 0; k < UPT; ++k) {
+        const int u = base + k * NT + tid;
+        on[k] = u < H;
+        const int uc = min(u, H - 1);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const float xv = a.xp[b * a.ld_xp + q * H + uc];
+            const float rv = slab_sum<NS>(a.R, b * a.ld_R + q * H + uc, a.R_nslab, a.R_slab);
+            if (MOD) {
+                const int64_t vo = (int64_t)b * a.vec_ld + uc;
+                const float ax = a.vec[q * a.vec_gs + vo] + a.vec_bias[q * H + uc];
+                const float ah = a.vec[(4 + q) * a.vec_gs + vo] + a.vec_bias[(4 + q) * H + uc];
+                const float bh = a.vec[(8 + q) * a.vec_gs + vo] + a.vec_bias[(8 + q) * H + uc];
+                g[k][q] = xv * ax + rv * ah + bh + a.bias[q * H + uc];
+            } else {
+                g[k][q] = xv + rv;
+            }
+            if (LN) {
+                lg[k][q] = ln_g[q * H + uc];
+                lb[k][q] = ln_b[q * H + uc];
+            }
+        }
+        cp[k] = a.c_prev[(int64_t)b * H + uc];
+        if (LN) {
+            lcg[k] = lnc_g[uc];
+            lcb[k] = lnc_b[uc];
+        }
+    }
+    // ---- LayerNorm over each gate block of the row
+    if (LN) {
+        float s[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            s[q] = 0.f;
+#pragma unroll
+            for (int k = 0; k < UPT; ++k) s[q] += on[k] ? g[k][q] : 0.f;
+        }
+        block_sum<4, NW>(s, lds);
+        float ml[4], m2[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            ml[q] = s[q] / (float)max(nloc, 1);
+            m2[q] = 0.f;
+#pragma unroll
+            for (int k = 0; k < UPT; ++k) {
+                const float d = on[k] ? g[k][q] - ml[q] : 0.f;
+                m2[q] += d * d;
+            }
+        }
+        block_sum<4, NW>(m2, lds);
+        float mean[4], var[4];
+        if (C > 1) {
+            if (tid == 0) {
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    mine[q] = ml[q];
+                    mine[4 + q] = m2[q];
+                }
+            }
+            cluster_allgather(a.part, a.sync + b * kSyncStride, a.err, b, c, C, mine, 8, all);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) chan_combine(all, C, 8, q, H, span, mean[q], var[q]);
+        } else {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                mean[q] = ml[q];
+                var[q] = m2[q] / (float)H;
+            }
+        }
+        float rs[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) rs[q] = rsqrtf(var[q] + kLnEps);
+#pragma unroll
+        for (int k = 0; k < UPT; ++k) {
+            const int u = base + k * NT + tid;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const float xh = (g[k][q] - mean[q]) * rs[q];
+                if (on[k]) a.xhat[(int64_t)b * 4 * H + q * H + u] = xh;
+                g[k][q] = xh * lg[k][q] + lb[k][q];
+            }
+        }
+        if (c == 0 && tid < 4) a.rstd[b * 5 + tid] = rs[tid];
+    }
+    // ---- cell
+    float cn[UPT], og[UPT];
+#pragma unroll
+    for (int k = 0; k < UPT; ++k) {
+        const int u = base + k * NT + tid;
+        const int64_t ro = (int64_t)b * H + u;
+        const float i = sigmoidf_(g[k][0]);
+        const float tj = tanhf(g[k][1]);
+        const float f = sigmoidf_(g[k][2] + a.forget_bias);
+        const float o = sigmoidf_(g[k][3]);
+        const float m = dropout_mult(keep_on, key, ro, a.keep);
+        cn[k] = on[k] ? cp[k] * f + i * tj * m : 0.f;
+        og[k] = o;
+        if (on[k]) {
+            float* ap = a.act + (int64_t)b * 4 * H + u;
+            ap[0] = i;
+            ap[H] = tj;
+            ap[2 * H] = f;
+            ap[3 * H] = o;
+            a.c_out[ro] = cn[k];
+        }
+    }
+    float th[UPT];
+    if (LN) {
+        float s1[1] = {0.f};
+#pragma unroll
+        for (int k = 0; k < UPT; ++k) s1[0] += cn[k];
+        block_sum<1, NW>(s1, lds);
+        const float ml = s1[0] / (float)max(nloc, 1);
+        float s2[1] = {0.f};
+#pragma unroll
+        for (int k = 0; k < UPT; ++k) {
+            const float d = on[k] ? cn[k] - ml : 0.f;
+            s2[0] += d * d;
+        }
+        block_sum<1, NW>(s2, lds);
+        float mean, var;
+        if (C > 1) {
+            if (tid == 0) {
+                mine[0] = ml;
+                mine[1] = s2[0];
+            }
+            cluster_allgather(a.part + (int64_t)a.B * C * kPartStride, a.sync + (a.B + b) * kSyncStride, a.err, b,
+                              c, C, mine, 2, all);
+            chan_combine(all, C, 2, 0, H, span, mean, var);
+        } else {
+            mean = ml;
+            var = s2[0] / (float)H;
+        }
+        const float rc = rsqrtf(var + kLnEps);
+        if (c == 0 && tid == 0) a.rstd[b * 5 + 4] = rc;
+#pragma unroll
+        for (int k = 0; k < UPT; ++k) {
+            const int u = base + k * NT + tid;
+            const float ch = (cn[k] - mean) * rc;
+            if (on[k]) a.chat[(int64_t)b * H + u] = ch;
+            th[k] = tanhf(ch * lcg[k] + lcb[k]);
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < UPT; ++k) th[k] = tanhf(cn[k]);
+    }
+    // ---- outputs + carry (reference eoc reset)
+#pragma unroll
+    for (int k = 0; k < UPT; ++k) {
+        const int u = base + k * NT + tid;
+        if (!on[k]) continue;
+        const int64_t ro = (int64_t)b * H + u;
+        const float h = th[k] * og[k];
+        a.h_out[ro] = h;
+        const float hc = r ? a.init_h[ro] : h;
+        a.h_carry[ro] = hc;
+        a.c_carry[ro] = r ? a.init_c[ro] : cn[k];
+        if (a.lp_kind == 1) ((__hip_bfloat16*)a.h_lp)[b * a.ld_lp + u] = to_bf16(hc);
+        else if (a.lp_kind == 2) ((float*)a.h_lp)[b * a.ld_lp + u] = hc;
+    }
+}
+
+template <int UPT, int NS, bool LN, bool MOD>
+__global__ __launch_bounds__(NT) void cell_bwd(const BwdArgs a) {
+    __shared__ float lds[NW * 8];
+    __shared__ float mine[8];
+    __shared__ float all[kMaxCluster * 8];
+    const int c = blockIdx.x, b = blockIdx.y, C = gridDim.x, tid = threadIdx.x, H = a.H;
+    const int span = UPT * NT, base = c * span;
+    const int grp = a.grp_rows > 0 ? b / a.grp_rows : 0;
+    const float* ln_g = LN ? a.ln_g + grp * 4 * H : nullptr;
+    const float* lnc_g = LN ? a.lnc_g + grp * H : nullptr;
+    const float* lnc_b = LN ? a.lnc_b + grp * H : nullptr;
+    const bool keep_on = a.keep < 1.0f;
+    const uint32_t key = keep_on ? hash_key(*a.seed, a.stream, a.step) : 0u;
+    const bool r = a.reset != nullptr && a.reset[b] != 0.f;
+
+    // ---- every load up front
+    float dhc[UPT], dho[UPT], dcc[UPT], ac[UPT][4], cp[UPT], cx[UPT], lcg[UPT], lcb[UPT];
+    float xh[UPT][4], lg[UPT][4], xv[UPT][4], rv[UPT][4], ax[UPT][4], ah[UPT][4];
+    bool on[UPT];
+#pragma unroll
+    for (int k = 0; k < UPT; ++k) {
+        const int u = base + k * NT + tid;
+        on[k] = u < H;
+        const int uc = min(u, H - 1);
+        const int64_t ro = (int64_t)b * H + uc;
+        dhc[k] = a.dh_rec ? slab_sum<0>(a.dh_rec, b * a.ld_dh_rec + uc, a.dhr_nslab, a.dhr_slab) : 0.f;
+        dho[k] = a.dh_out ? slab_sum<0>(a.dh_out, ro, a.dho_nslab, a.dho_slab) : 0.f;
+        dcc[k] = a.dc_rec[ro];
+        cp[k] = a.c_prev[ro];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) ac[k][q] = a.act[(int64_t)b * 4 * H + q * H + uc];
+        if (LN) {
+            cx[k] = a.chat[ro];
+            lcg[k] = lnc_g[uc];
+            lcb[k] = lnc_b[uc];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                xh[k][q] = a.xhat[(int64_t)b * 4 * H + q * H + uc];
+                lg[k][q] = ln_g[q * H + uc];
+            }
+        } else {
+            cx[k] = a.c_new[ro];
+        }
+        if (MOD) {
+            const int64_t vo = (int64_t)b * a.vec_ld + uc;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                xv[k][q] = a.xp[b * a.ld_xp + q * H + uc];
+                rv[k][q] = slab_sum<NS>(a.R, b * a.ld_R + q * H + uc, a.R_nslab, a.R_slab);
+                ax[k][q] = a.vec[q * a.vec_gs + vo] + a.vec_bias[q * H + uc];
+                ah[k][q] = a.vec[(4 + q) * a.vec_gs + vo] + a.vec_bias[(4 + q) * H + uc];
+            }
+        }
+    }
+    // ---- output: h' = th * o
+    float dc[UPT], dout[UPT], dch[UPT];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int k = 0; k < UPT; ++k) {
+        const int u = base + k * NT + tid;
+        const int64_t ro = (int64_t)b * H + u;
+        const float dh = dho[k] + (r ? 0.f : dhc[k]);
+        dc[k] = r ? 0.f : dcc[k];
+        if (on[k] && r && a.dinit_h) {
+            a.dinit_h[ro] += dhc[k];
+            a.dinit_c[ro] += dcc[k];
+        }
+        const float o = ac[k][3];
+        const float t = LN ? tanhf(cx[k] * lcg[k] + lcb[k]) : tanhf(cx[k]);
+        dout[k] = dh * t;
+        const float dcn = dh * o * (1.f - t * t);
+        if (LN) {
+            if (on[k]) a.dlncy[ro] = dcn;
+            dch[k] = on[k] ? dcn * lcg[k] : 0.f;
+            s1 += dch[k];
+            s2 += dch[k] * cx[k];
+        } else {
+            dc[k] += dcn;
+        }
+    }
+    if (LN) {
+        float s[2] = {s1, s2};
+        row_sum<2>(s, lds, mine, all, 0, a.sync, a.part, a.err, a.B, b, c, C);
+        const float rc = a.rstd[b * 5 + 4];
+#pragma unroll
+        for (int k = 0; k < UPT; ++k) dc[k] += rc * (dch[k] - s[0] / (float)H - cx[k] * s[1] / (float)H);
+    }
+    // ---- cell: c' = c*f + i*tj*m
+    float dy[UPT][4];
+#pragma unroll
+    for (int k = 0; k < UPT; ++k) {
+        const int u = base + k * NT + tid;
+        const int64_t ro = (int64_t)b * H + u;
+        const float i = ac[k][0], tj = ac[k][1], f = ac[k][2], o = ac[k][3];
+        const float m = dropout_mult(keep_on, key, ro, a.keep);
+        dy[k][0] = dc[k] * tj * m * i * (1.f - i);
+        dy[k][1] = dc[k] * i * m * (1.f - tj * tj);
+        dy[k][2] = dc[k] * cp[k] * f * (1.f - f);
+        dy[k][3] = dout[k] * o * (1.f - o);
+        if (on[k]) a.dc_rec[ro] = dc[k] * f;
+    }
+    // ---- LayerNorm over each gate block
+    if (LN) {
+        float acc[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) acc[q] = 0.f;
+#pragma unroll
+        for (int k = 0; k < UPT; ++k) {
+            const int u = base + k * NT + tid;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                if (on[k]) a.dlny[(int64_t)b * 4 * H + q * H + u] = dy[k][q];
+                const float dg = on[k] ? dy[k][q] * lg[k][q] : 0.f;
+                dy[k][q] = dg;
+                acc[q] += dg;
+                acc[4 + q] += dg * xh[k][q];
+            }
+        }
+        row_sum<8>(acc, lds, mine, all, 1, a.sync, a.part, a.err, a.B, b, c, C);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const float rs = a.rstd[b * 5 + q];
+#pragma unroll
+            for (int k = 0; k < UPT; ++k)
+                dy[k][q] = rs * (dy[k][q] - acc[q] / (float)H - xh[k][q] * acc[4 + q] / (float)H);
+        }
+    }
+    // ---- outputs
+#pragma unroll
+    for (int k = 0; k < UPT; ++k) {
+        if (!on[k]) continue;
+        const int u = base + k * NT + tid;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const float dg = dy[k][q];
+            float dr = dg;
+            if (MOD) {
+                a.dxp[b * a.ld_dxp + q * H + u] = dg * ax[k][q];
+                dr = dg * ah[k][q];
+                const int64_t o0 = (int64_t)b * a.vec_ld + u;
+                const float d3[3] = {dg * xv[k][q], dg * rv[k][q], dg};
+#pragma unroll
+                for (int j = 0; j < 3; ++j) {
+                    const int64_t oi = (4 * j + q) * a.vec_gs + o0;
+                    if (a.dvec_kind == 1) ((__hip_bfloat16*)a.dvec)[oi] = to_bf16(d3[j]);
+                    else ((float*)a.dvec)[oi] = d3[j];
+                }
+            }
+            a.dG[b * a.ld_dG + q * H + u] = dr;
+            if (a.dG_lp_kind == 1) ((__hip_bfloat16*)a.dG_lp)[b * a.ld_dG_lp + q * H + u] = to_bf16(dr);
+        }
+    }
+}
+
+// ---- dispatch: (UPT, NS, LN, MOD) ------------------------------------------------------
+template <typename A>
+using KernelT = void (*)(const A);
+
+template <int UPT, int NS>
+KernelT<FwdArgs> pick_fwd(bool ln, bool mod) {
+    if (mod) return cell_fwd<UPT, NS, true, true>;
+    if (ln) return cell_fwd<UPT, NS, true, false>;
+    return cell_fwd<UPT, NS, false, false>;
+}
+template <int UPT, int NS>
+KernelT<BwdArgs> pick_bwd(bool ln, bool mod) {
+    if (mod) return cell_bwd<UPT, NS, true, true>;
+    if (ln) return cell_bwd<UPT, NS, true, false>;
+    return cell_bwd<UPT, NS, false, false>;
+}
+
+template <int UPT, typename A>
+KernelT<A> pick_ns(int ns, bool ln, bool mod) {
+    if constexpr (std::is_same<A, FwdArgs>::value) {
+        switch (ns) {
+            case 1: return pick_fwd<UPT, 1>(ln, mod);
+            case 2: return pick_fwd<UPT, 2>(ln, mod);
+            case 4: return pick_fwd<UPT, 4>(ln, mod);
+            case 8: return pick_fwd<UPT, 8>(ln, mod);
+            default: return pick_fwd<UPT, 0>(ln, mod);
+        }
+    } else {
+        // without MOD the backward never reads R
+        switch (mod ? ns : 1) {
+            case 1: return pick_bwd<UPT, 1>(ln, mod);
+            case 2: return pick_bwd<UPT, 2>(ln, mod);
+            case 4: return pick_bwd<UPT, 4>(ln, mod);
+            case 8: return pick_bwd<UPT, 8>(ln, mod);
+            default: return pick_bwd<UPT, 0>(ln, mod);
+        }
+    }
+}
+
+template <typename A>
+int launch(const A& a, bool ln, bool mod, hipStream_t s) {
+    if (mod && !ln) return -3;
+    if (a.B <= 0) return 0;
+    const int H = a.H;
+    const int C = a.cluster > 1 ? a.cluster : 1;
+    if (C > kMaxCluster) return -5;
+    if (C > 1 && ln && (a.sync == nullptr || a.part == nullptr || a.err == nullptr)) return -6;
+    const int per = (H + C - 1) / C;  // units per workgroup
+    int upt = (per + NT - 1) / NT;
+    upt = upt <= 1 ? 1 : upt <= 2 ? 2 : upt <= 4 ? 4 : upt <= 8 ? 8 : 0;
+    if (upt == 0) return -2;
+    if ((C - 1) * upt * NT >= H) return -7;  // an empty workgroup would never arrive
+    KernelT<A> k = nullptr;
+    switch (upt) {
+        case 1: k = pick_ns<1, A>(a.R_nslab, ln, mod); break;
+        case 2: k = pick_ns<2, A>(a.R_nslab, ln, mod); break;
+        case 4: k = pick_ns<4, A>(a.R_nslab, ln, mod); break;
+        default: k = pick_ns<8, A>(a.R_nslab, ln, mod); break;
+    }
+    hipLaunchKernelGGL(k, dim3(C, a.B), dim3(NT), 0, s, a);
+    return SKR_CHECK_LAUNCH();
+}
+
+}  // namespace
+
+// Host entry points: argument structs are passed by pointer from Python (ctypes
+// mirrors of FwdArgs / BwdArgs in sketch_rnn_amd/ops/_hipapi.py).
+// args->cluster = C workgroups per row (<= 1: one).
+SKR_API int skr_lstm_fwd_step(const FwdArgs* args, int ln, int mod, hipStream_t s) {
+    return launch(*args, ln != 0, mod != 0, s);
+}
+
+SKR_API int skr_lstm_bwd_step(const BwdArgs* args, int ln, int mod, hipStream_t s) {
+    return launch(*args, ln != 0, mod != 0, s);
+}
+
+SKR_API int skr_lstm_fwd_args_size() { return (int)sizeof(FwdArgs); }
+SKR_API int skr_lstm_bwd_args_size() { return (int)sizeof(BwdArgs); }

@@ -45,7 +45,7 @@ def bmm(a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor] = None) ->
     return torch.bmm(a, b, out_dtype=torch.float32)
 
 
-_SPLITS = (1, 2, 3, 4, 6, 8, 12, 16, 24, 32)
+_SPLITS = (1, 2, 4, 8, 16, 32)  # powers of two: the cell kernels sum <= 8 slabs unrolled
 
 
 def plan_splits(M: int, N: int, K: int, batch: int = 1, dtype: torch.dtype = _BF16, max_splits: int = 32) -> int:

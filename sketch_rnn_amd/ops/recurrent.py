@@ -1,7 +1,8 @@
 """Native recurrences on the GPU: per-step library GEMM + fused HIP cell kernel.
 
-Step ``t`` of a layer is two launches: ``R = h_{t-1} @ W_h`` (hipBLASLt,
-bf16/fp32 operands, fp32 out) and one fused cell kernel
+Step ``t`` of a layer is two launches: ``R = h_{t-1} @ W_h`` (the skinny
+split-K MFMA GEMM of ``csrc/skinny_gemm.hip``; hipBLASLt for fp32 operands)
+and one fused cell kernel
 (``csrc/lstm_cell.hip``) that adds the hoisted input projection, applies
 LayerNorm / hyper modulation / gates / dropout / eoc reset and writes the
 next GEMM's operand directly. The backward runs the mirror image in reverse
@@ -69,8 +70,11 @@ class _Saved:
     """Plain holder for the big per-sequence buffers (kept off autograd)."""
 
 
-# ---- clustered cell kernels (csrc/lstm_cluster.hip) ---------------------------------
+# ---- cell-kernel geometry (csrc/lstm_cell.hip) --------------------------------------
+# A row of H hidden units runs on C workgroups of 256 threads, CELL_UPT units
+# per thread (SKR_CELL_UPT, a power of two <= 8). SKR_CLUSTER=0 forces C = 1.
 CLUSTER_ENABLED = os.environ.get("SKR_CLUSTER", "1") != "0"
+CELL_UPT = int(os.environ.get("SKR_CELL_UPT", "1"))
 _ERR_FLAGS = {}
 
 
@@ -90,12 +94,28 @@ def check_cluster_errors(device) -> None:
         raise RuntimeError("clustered LSTM cell kernel: in-launch wait timed out (workgroups not co-resident)")
 
 
-class _ClusterSync:
-    """Per-sequence arrival counters / partial-stat scratch for one pass."""
+def cell_geometry(H: int, BB: int, ln: bool = True) -> int:
+    """Workgroups per row (C) for the fused cell kernels."""
+    if not CLUSTER_ENABLED:
+        C = 1
+    else:
+        upt = max(1, CELL_UPT)
+        C = min(-(-H // (256 * upt)), 16)
+        # LayerNorm rows spin-wait on each other: keep every workgroup co-resident
+        while ln and C > 1 and BB * C > 1024:
+            upt *= 2
+            C = -(-H // (256 * upt))
+    if -(-H // (256 * C)) > 8:
+        raise ValueError("cell kernels support at most 2048 hidden units per workgroup (H=%d, C=%d)" % (H, C))
+    return C
 
-    def __init__(self, T: int, BB: int, H: int, device):
-        self.C = (H + 255) // 256
-        self.on = CLUSTER_ENABLED and 1 < self.C <= 16 and BB * self.C <= 1024
+
+class _ClusterSync:
+    """Per-sequence geometry + arrival counters / partial-stat scratch for one pass."""
+
+    def __init__(self, T: int, BB: int, H: int, device, ln: bool = True):
+        self.C = cell_geometry(H, BB, ln)
+        self.on = ln and self.C > 1
         if self.on:
             # one 128-byte line per counter / per workgroup slot (kSyncStride, kPartStride)
             self.sync = torch.zeros(T, 2, BB, 32, dtype=torch.int32, device=device)
@@ -103,12 +123,12 @@ class _ClusterSync:
             self.err = cluster_error_flag(device)
 
     def set(self, args, t: int) -> None:
+        args.cluster = self.C
         if self.on:
-            args.cluster, args.sync = self.C, self.sync[t].data_ptr()
+            args.sync = self.sync[t].data_ptr()
             args.part, args.err = self.part.data_ptr(), self.err.data_ptr()
         else:
-            args.cluster = 0
-
+            args.sync, args.part, args.err = None, None, None
 
 
 # =====================================================================================
@@ -156,7 +176,7 @@ class _LSTMSeq(torch.autograd.Function):
         a.seed, a.stream = sd.data_ptr(), int(stream)
         a.ld_lp, a.lp_kind = H, _lp_kind(A)
         a.R, a.R_nslab, a.R_slab = R.data_ptr(), max(S, 1), BB * G
-        cl = _ClusterSync(T, BB, H, dev)
+        cl = _ClusterSync(T, BB, H, dev, ln)
         st = _stream()
         for t in range(T):
             cl.set(a, t)
@@ -215,7 +235,7 @@ class _LSTMSeq(torch.autograd.Function):
         a.keep, a.seed, a.stream = float(keep), s.seed.data_ptr(), int(stream)
         a.ld_dG, a.ld_dG_lp, a.dG_lp_kind = G, G, 1 if lp_on else 0
         a.dinit_h, a.dinit_c = _ptr(dinit_h), _ptr(dinit_c)
-        cl = _ClusterSync(T, BB, H, dev)
+        cl = _ClusterSync(T, BB, H, dev, ln)
         st = _stream()
         for t in range(T - 1, -1, -1):
             cl.set(a, t)
