@@ -47,6 +47,14 @@ __device__ __forceinline__ float wave_max(float v) {
     return v;
 }
 
+// Workgroup barrier for LDS hand-offs only: waits for this wave's LDS ops
+// (lgkmcnt) but, unlike __syncthreads(), not for its outstanding global loads
+// and stores (vmcnt) -- a __syncthreads() after a burst of global stores
+// stalls every wave until those stores retire.
+__device__ __forceinline__ void lds_barrier() {
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
 // Sums N values across a block of NW waves. `lds` must hold NW*N floats.
 template <int N, int NW>
 __device__ __forceinline__ void block_sum(float (&v)[N], float* lds) {
@@ -57,7 +65,7 @@ __device__ __forceinline__ void block_sum(float (&v)[N], float* lds) {
 #pragma unroll
         for (int i = 0; i < N; ++i) lds[w * N + i] = v[i];
     }
-    __syncthreads();
+    lds_barrier();
 #pragma unroll
     for (int i = 0; i < N; ++i) {
         float s = 0.f;
@@ -65,7 +73,7 @@ __device__ __forceinline__ void block_sum(float (&v)[N], float* lds) {
         for (int k = 0; k < NW; ++k) s += lds[k * N + i];
         v[i] = s;
     }
-    __syncthreads();
+    lds_barrier();
 }
 
 __device__ __forceinline__ __hip_bfloat16 to_bf16(float x) { return __float2bfloat16(x); }

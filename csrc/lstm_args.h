@@ -34,8 +34,7 @@ struct FwdArgs {
     float* c_carry;                    // [B, H]
     // rows split over `cluster` workgroups (LayerNorm statistics exchanged in-launch)
     int cluster;                       // <= 1: one workgroup per row
-    int* sync;                         // [2][B] arrival counters for this step (zeroed per sequence)
-    float* part;                       // [2][B][cluster][8] partial statistics
+    uint64_t* part;                    // [2][B][cluster][16] tagged partial statistics (zeroed per sequence)
     int* err;                          // set to 1 if a cluster wait timed out
 };
 
@@ -65,7 +64,7 @@ struct BwdArgs {
     float* dlny;                       // LN: [B, 4H] grad wrt LN-all output (for gamma/beta)
     float* dlncy;                      // LN: [B, H]  grad wrt LN(c) output
     float* dinit_h; float* dinit_c;    // [B, H] accumulated on reset rows (or null)
-    int cluster; int* sync; float* part; int* err;
+    int cluster; uint64_t* part; int* err;
 };
 
 __device__ __forceinline__ float dropout_mult(bool on, uint32_t key, int64_t idx, float keep) {

@@ -20,10 +20,11 @@
 // split into parameter groups (grp_rows): the two directions of the
 // bidirectional encoder run as 2B rows of one launch.
 //
-// Geometry: grid (C, B), 256 threads; workgroup c of row b owns the UPT*256
-// contiguous hidden units [c*UPT*256, (c+1)*UPT*256), every thread UPT units
-// (stride 256) x 4 gates. The step is latency-bound (B ~ 100 rows, a few
-// hundred KB per row), so the kernel is written for memory-level
+// Geometry: grid (C, B), NT threads (256, or 1024 for a whole wide row in one
+// workgroup); workgroup c of row b owns the UPT*NT contiguous hidden units
+// [c*UPT*NT, (c+1)*UPT*NT), every thread UPT units (stride NT) x 4 gates.
+// The step is latency-bound (B ~ 100 rows, a few hundred KB per row), so the
+// kernel is written for memory-level
 // parallelism: every global load of a thread is issued up front, from
 // clamped (never predicated) addresses, with the split-K slab count a
 // template parameter -- no branch or runtime loop sits between a load and
@@ -31,13 +32,17 @@
 // chain costs one full memory round trip per dependency.)
 //
 // C > 1 (a row split over C workgroups) only matters with LayerNorm: the C
-// workgroups exchange partial (mean, M2) statistics inside the launch --
-// write-through (sc1) agent stores, vmcnt drain, one relaxed agent atomic
-// add on the row's arrival counter, one lane polls with s_sleep backoff
-// (bounded: a timeout sets *err for the host), sc1 loads, Chan's combine.
-// Counters are per (step, row, phase), each on its own 128-byte line, and
-// zeroed once per sequence. All B*C workgroups must be co-resident; the host
-// only picks C > 1 when that holds.
+// workgroups exchange partial (mean, M2) statistics inside the launch as
+// data-tagged granules -- each value travels in one 8-byte word {value,
+// tag = step + 1}, written with a write-through (sc1, agent-scope) 64-bit
+// store; one wave per workgroup polls the row's C*nv words with sc1 loads
+// (s_sleep backoff, bounded: a timeout sets *err for the host) until every
+// tag is current, then Chan's formula combines them. No separate flag, no
+// vmcnt drain and no counter atomics: one store-to-visible hop per exchange
+// (CDNA4 guide: handoff-1to1 vs handoff-flag). Every slot owns its
+// workgroup's 128-byte line; the buffer is zeroed once per sequence and the
+// tags make slots of the previous step stale. All B*C workgroups must be
+// co-resident; the host only picks C > 1 when that holds.
 //
 // Reference semantics: model.py:19-23 (BasicLSTMCell), model.py:82-92 (eoc
 // reset); LayerNorm-/Hyper-LSTM semantics: sketch_rnn_amd/models/cells.py.
@@ -49,11 +54,9 @@ namespace {
 
 using namespace skr;
 
-constexpr int NT = 256, NW = NT / 64;
 constexpr int kMaxCluster = 16;
 constexpr unsigned kSpinLimit = 1u << 21;
-constexpr int kSyncStride = 32;   // ints per arrival counter (128 B)
-constexpr int kPartStride = 32;   // floats per workgroup partial slot (128 B)
+constexpr int kSlots = 16;        // 8-byte granules per workgroup slot (128 B)
 
 // Sum of the NS split-K partial slabs at idx (NS > 0: compile-time count,
 // all loads independent); NS == 0: runtime count n, batches of 8 clamped loads.
@@ -81,32 +84,34 @@ __device__ __forceinline__ float slab_sum(const float* p, int64_t idx, int n, in
     }
 }
 
-// Publish `nv` floats of this workgroup (LDS `mine`), wait for the row's C
-// workgroups, gather all C*nv values into LDS `all` ([C][nv]).
-__device__ void cluster_allgather(float* part, int* cnt, int* err, int b, int c, int C, const float* mine, int nv,
-                                  float* all) {
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        float* dst = part + ((int64_t)b * C + c) * kPartStride;
-        for (int i = 0; i < nv; ++i) __hip_atomic_store(dst + i, mine[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        unsigned spins = 0;
-        while (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < C) {
-            __builtin_amdgcn_s_sleep(1);
-            if (++spins > kSpinLimit) {
-                __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                break;
+// Publish `nv` floats of this workgroup (LDS `mine`) as tagged granules and
+// gather the row's C*nv values into LDS `all` ([C][nv]).
+__device__ void cluster_allgather(uint64_t* part, int* err, int b, int c, int C, const float* mine, int nv,
+                                  uint32_t tag, float* all) {
+    lds_barrier();
+    const int tid = threadIdx.x;
+    uint64_t* row = part + (int64_t)b * C * kSlots;
+    if (tid < nv) {
+        const uint64_t w = ((uint64_t)tag << 32) | __float_as_uint(mine[tid]);
+        __hip_atomic_store(row + c * kSlots + tid, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (tid < 64) {
+        for (int i = tid; i < C * nv; i += 64) {
+            const int cc = i / nv, k = i - cc * nv;
+            uint64_t w = __hip_atomic_load(row + cc * kSlots + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            unsigned spins = 0;
+            while ((uint32_t)(w >> 32) != tag) {
+                __builtin_amdgcn_s_sleep(1);
+                if (++spins > kSpinLimit) {
+                    __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    break;
+                }
+                w = __hip_atomic_load(row + cc * kSlots + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
+            all[i] = __uint_as_float((uint32_t)w);
         }
     }
-    __syncthreads();
-    for (int i = threadIdx.x; i < C * nv; i += NT) {
-        const int cc = i / nv, k = i - cc * nv;
-        all[i] = __hip_atomic_load(part + ((int64_t)b * C + cc) * kPartStride + k, __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
-    }
-    __syncthreads();
+    lds_barrier();
 }
 
 // Row mean / variance from per-workgroup (mean, M2) pairs (Chan et al.);
@@ -128,17 +133,16 @@ __device__ __forceinline__ void chan_combine(const float* all, int C, int nv, in
 
 // Row-wide sums of N per-thread values: block reduction, then (C > 1) the
 // in-launch exchange. `slot` selects the (counter, partial) pair of this phase.
-template <int N>
-__device__ __forceinline__ void row_sum(float (&v)[N], float* lds, float* mine, float* all, int slot,
-                                        int* sync_base, float* part_base, int* err, int B, int b, int c, int C) {
+template <int N, int NW>
+__device__ __forceinline__ void row_sum(float (&v)[N], float* lds, float* mine, float* all, uint64_t* part,
+                                        int* err, uint32_t tag, int b, int c, int C) {
     block_sum<N, NW>(v, lds);
     if (C <= 1) return;
     if (threadIdx.x == 0) {
 #pragma unroll
         for (int i = 0; i < N; ++i) mine[i] = v[i];
     }
-    cluster_allgather(part_base + (int64_t)slot * B * C * kPartStride, sync_base + (slot * B + b) * kSyncStride,
-                      err, b, c, C, mine, N, all);
+    cluster_allgather(part, err, b, c, C, mine, N, tag, all);
 #pragma unroll
     for (int i = 0; i < N; ++i) {
         float s = 0.f;
@@ -147,8 +151,9 @@ __device__ __forceinline__ void row_sum(float (&v)[N], float* lds, float* mine, 
     }
 }
 
-template <int UPT, int NS, bool LN, bool MOD>
+template <int NT, int UPT, int NS, bool LN, bool MOD>
 __global__ __launch_bounds__(NT) void cell_fwd(const FwdArgs a) {
+    constexpr int NW = NT / 64;
     __shared__ float lds[NW * 8];
     __shared__ float mine[8];
     __shared__ float all[kMaxCluster * 8];
@@ -227,7 +232,7 @@ __global__ __launch_bounds__(NT) void cell_fwd(const FwdArgs a) {
                     mine[4 + q] = m2[q];
                 }
             }
-            cluster_allgather(a.part, a.sync + b * kSyncStride, a.err, b, c, C, mine, 8, all);
+            cluster_allgather(a.part, a.err, b, c, C, mine, 8, a.step + 1, all);
 #pragma unroll
             for (int q = 0; q < 4; ++q) chan_combine(all, C, 8, q, H, span, mean[q], var[q]);
         } else {
@@ -294,8 +299,7 @@ __global__ __launch_bounds__(NT) void cell_fwd(const FwdArgs a) {
                 mine[0] = ml;
                 mine[1] = s2[0];
             }
-            cluster_allgather(a.part + (int64_t)a.B * C * kPartStride, a.sync + (a.B + b) * kSyncStride, a.err, b,
-                              c, C, mine, 2, all);
+            cluster_allgather(a.part + (int64_t)a.B * C * kSlots, a.err, b, c, C, mine, 2, a.step + 1, all);
             chan_combine(all, C, 2, 0, H, span, mean, var);
         } else {
             mean = ml;
@@ -330,8 +334,9 @@ __global__ __launch_bounds__(NT) void cell_fwd(const FwdArgs a) {
     }
 }
 
-template <int UPT, int NS, bool LN, bool MOD>
+template <int NT, int UPT, int NS, bool LN, bool MOD>
 __global__ __launch_bounds__(NT) void cell_bwd(const BwdArgs a) {
+    constexpr int NW = NT / 64;
     __shared__ float lds[NW * 8];
     __shared__ float mine[8];
     __shared__ float all[kMaxCluster * 8];
@@ -412,7 +417,7 @@ __global__ __launch_bounds__(NT) void cell_bwd(const BwdArgs a) {
     }
     if (LN) {
         float s[2] = {s1, s2};
-        row_sum<2>(s, lds, mine, all, 0, a.sync, a.part, a.err, a.B, b, c, C);
+        row_sum<2, NW>(s, lds, mine, all, a.part, a.err, a.step + 1, b, c, C);
         const float rc = a.rstd[b * 5 + 4];
 #pragma unroll
         for (int k = 0; k < UPT; ++k) dc[k] += rc * (dch[k] - s[0] / (float)H - cx[k] * s[1] / (float)H);
@@ -448,7 +453,7 @@ __global__ __launch_bounds__(NT) void cell_bwd(const BwdArgs a) {
                 acc[4 + q] += dg * xh[k][q];
             }
         }
-        row_sum<8>(acc, lds, mine, all, 1, a.sync, a.part, a.err, a.B, b, c, C);
+        row_sum<8, NW>(acc, lds, mine, all, a.part + (int64_t)a.B * C * kSlots, a.err, a.step + 1, b, c, C);
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             const float rs = a.rstd[b * 5 + q];
@@ -484,45 +489,39 @@ __global__ __launch_bounds__(NT) void cell_bwd(const BwdArgs a) {
     }
 }
 
-// ---- dispatch: (UPT, NS, LN, MOD) ------------------------------------------------------
+// ---- dispatch: (NT, UPT, NS, LN, MOD) ---------------------------------------------------
 template <typename A>
 using KernelT = void (*)(const A);
 
-template <int UPT, int NS>
-KernelT<FwdArgs> pick_fwd(bool ln, bool mod) {
-    if (mod) return cell_fwd<UPT, NS, true, true>;
-    if (ln) return cell_fwd<UPT, NS, true, false>;
-    return cell_fwd<UPT, NS, false, false>;
+template <int NT, int UPT, int NS>
+KernelT<FwdArgs> pick(bool ln, bool mod, const FwdArgs*) {
+    if (mod) return cell_fwd<NT, UPT, NS, true, true>;
+    if (ln) return cell_fwd<NT, UPT, NS, true, false>;
+    return cell_fwd<NT, UPT, NS, false, false>;
 }
-template <int UPT, int NS>
-KernelT<BwdArgs> pick_bwd(bool ln, bool mod) {
-    if (mod) return cell_bwd<UPT, NS, true, true>;
-    if (ln) return cell_bwd<UPT, NS, true, false>;
-    return cell_bwd<UPT, NS, false, false>;
+template <int NT, int UPT, int NS>
+KernelT<BwdArgs> pick(bool ln, bool mod, const BwdArgs*) {
+    if (mod) return cell_bwd<NT, UPT, NS, true, true>;
+    if (ln) return cell_bwd<NT, UPT, NS, true, false>;
+    return cell_bwd<NT, UPT, NS, false, false>;
 }
 
-template <int UPT, typename A>
-KernelT<A> pick_ns(int ns, bool ln, bool mod) {
-    if constexpr (std::is_same<A, FwdArgs>::value) {
-        switch (ns) {
-            case 1: return pick_fwd<UPT, 1>(ln, mod);
-            case 2: return pick_fwd<UPT, 2>(ln, mod);
-            case 4: return pick_fwd<UPT, 4>(ln, mod);
-            case 8: return pick_fwd<UPT, 8>(ln, mod);
-            default: return pick_fwd<UPT, 0>(ln, mod);
-        }
-    } else {
-        // without MOD the backward never reads R
-        switch (mod ? ns : 1) {
-            case 1: return pick_bwd<UPT, 1>(ln, mod);
-            case 2: return pick_bwd<UPT, 2>(ln, mod);
-            case 4: return pick_bwd<UPT, 4>(ln, mod);
-            case 8: return pick_bwd<UPT, 8>(ln, mod);
-            default: return pick_bwd<UPT, 0>(ln, mod);
-        }
+template <int NT, int UPT, typename A>
+KernelT<A> pick_ns(const A& a, bool ln, bool mod) {
+    // the backward reads R only with MOD
+    const int ns = (std::is_same<A, FwdArgs>::value || mod) ? a.R_nslab : 1;
+    switch (ns) {
+        case 1: return pick<NT, UPT, 1>(ln, mod, &a);
+        case 2: return pick<NT, UPT, 2>(ln, mod, &a);
+        case 4: return pick<NT, UPT, 4>(ln, mod, &a);
+        case 8: return pick<NT, UPT, 8>(ln, mod, &a);
+        default: return pick<NT, UPT, 0>(ln, mod, &a);
     }
 }
 
+// Geometry: C = args->cluster workgroups per row. C == 1 rows wider than 256
+// units run on 1024-thread workgroups (one row per CU, no exchange);
+// otherwise 256 threads with UPT units each.
 template <typename A>
 int launch(const A& a, bool ln, bool mod, hipStream_t s) {
     if (mod && !ln) return -3;
@@ -530,20 +529,25 @@ int launch(const A& a, bool ln, bool mod, hipStream_t s) {
     const int H = a.H;
     const int C = a.cluster > 1 ? a.cluster : 1;
     if (C > kMaxCluster) return -5;
-    if (C > 1 && ln && (a.sync == nullptr || a.part == nullptr || a.err == nullptr)) return -6;
+    if (C > 1 && ln && (a.part == nullptr || a.err == nullptr)) return -6;
     const int per = (H + C - 1) / C;  // units per workgroup
-    int upt = (per + NT - 1) / NT;
+    const int nt = (C == 1 && per > 256) ? 1024 : 256;
+    int upt = (per + nt - 1) / nt;
     upt = upt <= 1 ? 1 : upt <= 2 ? 2 : upt <= 4 ? 4 : upt <= 8 ? 8 : 0;
-    if (upt == 0) return -2;
-    if ((C - 1) * upt * NT >= H) return -7;  // an empty workgroup would never arrive
+    if (upt == 0 || (nt == 1024 && upt > 2)) return -2;
+    if ((C - 1) * upt * nt >= H) return -7;  // an empty workgroup would never arrive
     KernelT<A> k = nullptr;
-    switch (upt) {
-        case 1: k = pick_ns<1, A>(a.R_nslab, ln, mod); break;
-        case 2: k = pick_ns<2, A>(a.R_nslab, ln, mod); break;
-        case 4: k = pick_ns<4, A>(a.R_nslab, ln, mod); break;
-        default: k = pick_ns<8, A>(a.R_nslab, ln, mod); break;
+    if (nt == 1024) {
+        k = upt == 1 ? pick_ns<1024, 1>(a, ln, mod) : pick_ns<1024, 2>(a, ln, mod);
+    } else {
+        switch (upt) {
+            case 1: k = pick_ns<256, 1>(a, ln, mod); break;
+            case 2: k = pick_ns<256, 2>(a, ln, mod); break;
+            case 4: k = pick_ns<256, 4>(a, ln, mod); break;
+            default: k = pick_ns<256, 8>(a, ln, mod); break;
+        }
     }
-    hipLaunchKernelGGL(k, dim3(C, a.B), dim3(NT), 0, s, a);
+    hipLaunchKernelGGL(k, dim3(C, a.B), dim3(nt), 0, s, a);
     return SKR_CHECK_LAUNCH();
 }
 

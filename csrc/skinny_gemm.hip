@@ -135,7 +135,7 @@ __global__ __launch_bounds__(256) void skinny_gemm_nt_kernel(
         asm volatile("" ::: "memory");
         __builtin_amdgcn_sched_barrier(0);
         SKR_STORE(y, (kt + 1) & 1);
-        __syncthreads();
+        skr::lds_barrier();
         if (++kt >= n) break;
         SKR_LOAD(y, kt + 2);
         __builtin_amdgcn_sched_barrier(0);
@@ -143,7 +143,7 @@ __global__ __launch_bounds__(256) void skinny_gemm_nt_kernel(
         asm volatile("" ::: "memory");
         __builtin_amdgcn_sched_barrier(0);
         SKR_STORE(x, (kt + 1) & 1);
-        __syncthreads();
+        skr::lds_barrier();
         if (++kt >= n) break;
     }
 #undef SKR_LOAD

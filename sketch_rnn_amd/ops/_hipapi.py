@@ -35,7 +35,7 @@ class LstmFwdArgs(C.Structure):
         ("h_carry", _p),
         ("h_lp", _p), ("ld_lp", _i64), ("lp_kind", _i),
         ("c_carry", _p),
-        ("cluster", _i), ("sync", _p), ("part", _p), ("err", _p),
+        ("cluster", _i), ("part", _p), ("err", _p),
     ]
 
 
@@ -64,7 +64,7 @@ class LstmBwdArgs(C.Structure):
         ("dvec", _p), ("dvec_kind", _i),
         ("dlny", _p), ("dlncy", _p),
         ("dinit_h", _p), ("dinit_c", _p),
-        ("cluster", _i), ("sync", _p), ("part", _p), ("err", _p),
+        ("cluster", _i), ("part", _p), ("err", _p),
     ]
 
 

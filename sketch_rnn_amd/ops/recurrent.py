@@ -71,10 +71,12 @@ class _Saved:
 
 
 # ---- cell-kernel geometry (csrc/lstm_cell.hip) --------------------------------------
-# A row of H hidden units runs on C workgroups of 256 threads, CELL_UPT units
-# per thread (SKR_CELL_UPT, a power of two <= 8). SKR_CLUSTER=0 forces C = 1.
+# A row of H hidden units runs on C workgroups (C == 1 and H > 256: one
+# 1024-thread workgroup per row). Policy: 256-unit workgroups (measured
+# fastest at H = 2048 with LayerNorm, csrc/bench/cell_bench.hip, despite the
+# in-launch exchange). SKR_CELL_C overrides C; SKR_CLUSTER=0 forces C = 1.
 CLUSTER_ENABLED = os.environ.get("SKR_CLUSTER", "1") != "0"
-CELL_UPT = int(os.environ.get("SKR_CELL_UPT", "1"))
+CELL_C = int(os.environ.get("SKR_CELL_C", "0"))
 _ERR_FLAGS = {}
 
 
@@ -98,37 +100,37 @@ def cell_geometry(H: int, BB: int, ln: bool = True) -> int:
     """Workgroups per row (C) for the fused cell kernels."""
     if not CLUSTER_ENABLED:
         C = 1
+    elif CELL_C > 0:
+        C = CELL_C
     else:
-        upt = max(1, CELL_UPT)
-        C = min(-(-H // (256 * upt)), 16)
-        # LayerNorm rows spin-wait on each other: keep every workgroup co-resident
-        while ln and C > 1 and BB * C > 1024:
-            upt *= 2
-            C = -(-H // (256 * upt))
-    if -(-H // (256 * C)) > 8:
+        C = min(-(-H // 256), 16)
+    # LayerNorm rows spin-wait on each other: keep every workgroup co-resident
+    while ln and C > 1 and BB * C > 1024:
+        C //= 2
+    per = -(-H // C)
+    if (C == 1 and per > 2048) or (C > 1 and per > 2048):
         raise ValueError("cell kernels support at most 2048 hidden units per workgroup (H=%d, C=%d)" % (H, C))
     return C
 
 
 class _ClusterSync:
-    """Per-sequence geometry + arrival counters / partial-stat scratch for one pass."""
+    """Per-pass cell geometry + the tagged partial-statistics exchange buffer
+    (zeroed once per pass; tags = step + 1 make earlier steps' slots stale)."""
 
     def __init__(self, T: int, BB: int, H: int, device, ln: bool = True):
         self.C = cell_geometry(H, BB, ln)
         self.on = ln and self.C > 1
         if self.on:
-            # one 128-byte line per counter / per workgroup slot (kSyncStride, kPartStride)
-            self.sync = torch.zeros(T, 2, BB, 32, dtype=torch.int32, device=device)
-            self.part = torch.empty(2, BB, self.C, 32, dtype=torch.float32, device=device)
+            # [phase][row][workgroup][16 x 8-byte granules]: one 128-byte line per slot
+            self.part = torch.zeros(2, BB, self.C, 16, dtype=torch.int64, device=device)
             self.err = cluster_error_flag(device)
 
     def set(self, args, t: int) -> None:
         args.cluster = self.C
         if self.on:
-            args.sync = self.sync[t].data_ptr()
             args.part, args.err = self.part.data_ptr(), self.err.data_ptr()
         else:
-            args.sync, args.part, args.err = None, None, None
+            args.part, args.err = None, None
 
 
 # =====================================================================================
