@@ -159,6 +159,118 @@ __global__ __launch_bounds__(256) void skinny_gemm_nt_kernel(
             }
 }
 
+// ---------------------------------------------------------------------------
+// v2: LDS-DMA ring. Tiles move global -> LDS with global_load_lds_dwordx4
+// (no staging registers, no ds_write), NSTAGE buffers deep: NSTAGE-1 K-tiles
+// are in flight while one is multiplied. One counted `s_waitcnt vmcnt(N)`
+// plus a raw s_barrier per K-tile (a __syncthreads() would drain every
+// prefetch, CDNA4 guide "Pipelining across barriers"). LDS rows are 128 B
+// (BK = 64 bf16) with the 16-byte chunk index XOR-swizzled by (row >> 1) & 7
+// -- applied on the per-lane GLOBAL address, since an LDS-DMA wave writes
+// 1 KiB linearly -- so the 16 rows of a ds_read_b128 fragment read hit 16
+// distinct bank quads.
+constexpr int NSTAGE = 4;
+
+template <int BN>
+__global__ __launch_bounds__(256) void skinny_gemm_glds_kernel(
+    const __hip_bfloat16* __restrict__ A, int64_t lda, int64_t a_batch,
+    const __hip_bfloat16* __restrict__ Bt, int64_t ldb, int64_t b_batch,
+    float* __restrict__ C, int64_t ldc, int64_t c_slab, int64_t c_batch, int M, int kslice) {
+    constexpr int NJ = BN / 16;
+    constexpr int A_CH = BM / 8, B_CH = BN / 8;     // 1-KiB chunks (8 rows) per tile
+    constexpr int GPW = (A_CH + B_CH) / 4;          // glds per wave per tile
+    constexpr int TILE = (BM + BN) * BK;            // bf16 elements per stage
+    extern __shared__ __attribute__((aligned(16))) __hip_bfloat16 smem[];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int n0 = blockIdx.x * BN;
+    const int64_t k0 = (int64_t)blockIdx.y * kslice;
+    const int n = kslice / BK;
+    A += blockIdx.z * a_batch;
+    Bt += blockIdx.z * b_batch;
+    C += blockIdx.z * c_batch + blockIdx.y * c_slab;
+
+    // per-lane source rows / swizzled chunk (fixed across tiles)
+    const int r8 = lane >> 3, slot = lane & 7;
+    const __hip_bfloat16* asrc[A_CH / 4];
+    const __hip_bfloat16* bsrc[B_CH / 4];
+#pragma unroll
+    for (int i = 0; i < A_CH / 4; ++i) {
+        const int row = (w + 4 * i) * 8 + r8;
+        const int kc = slot ^ ((row >> 1) & 7);
+        asrc[i] = A + (int64_t)min(row, M - 1) * lda + k0 + kc * 8;
+    }
+#pragma unroll
+    for (int i = 0; i < B_CH / 4; ++i) {
+        const int row = (w + 4 * i) * 8 + r8;
+        const int kc = slot ^ ((row >> 1) & 7);
+        bsrc[i] = Bt + (int64_t)(n0 + row) * ldb + k0 + kc * 8;
+    }
+    auto issue = [&](int kt) {
+        __hip_bfloat16* st = smem + (kt % NSTAGE) * TILE;
+        const int64_t ko = (int64_t)kt * BK;
+#pragma unroll
+        for (int i = 0; i < A_CH / 4; ++i)
+            __builtin_amdgcn_global_load_lds((const void*)(asrc[i] + ko),
+                                             (__attribute__((address_space(3))) void*)(st + (w + 4 * i) * 512), 16, 0, 0);
+#pragma unroll
+        for (int i = 0; i < B_CH / 4; ++i)
+            __builtin_amdgcn_global_load_lds((const void*)(bsrc[i] + ko),
+                                             (__attribute__((address_space(3))) void*)(st + BM * BK + (w + 4 * i) * 512),
+                                             16, 0, 0);
+    };
+
+    f32x4 acc[2][NJ];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    const int fr = lane & 15, fq = lane >> 4;
+#pragma unroll
+    for (int p = 0; p < NSTAGE - 1; ++p)
+        if (p < n) issue(p);
+    for (int kt = 0; kt < n; ++kt) {
+        // tile kt landed (for this wave) once at most min(n-1-kt, NSTAGE-2) younger tiles are pending
+        const int ahead = min(n - 1 - kt, NSTAGE - 2);
+        if (ahead >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * GPW) : "memory");
+        else if (ahead == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GPW) : "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();  // ... and for every wave; buffer (kt-1) % NSTAGE is free
+        if (kt + NSTAGE - 1 < n) issue(kt + NSTAGE - 1);
+        const __hip_bfloat16* As = smem + (kt % NSTAGE) * TILE;
+        const __hip_bfloat16* Bs = As + BM * BK;
+#pragma unroll
+        for (int ks = 0; ks < BK; ks += 32) {
+            const int kc = ks / 8 + fq;
+            bf16x8 af[2], bfr[NJ];
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                const int row = 32 * w + 16 * i + fr;
+                af[i] = *(const bf16x8*)(&As[row * BK + ((kc ^ ((row >> 1) & 7)) * 8)]);
+            }
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) {
+                const int row = 16 * j + fr;
+                bfr[j] = *(const bf16x8*)(&Bs[row * BK + ((kc ^ ((row >> 1) & 7)) * 8)]);
+            }
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int j = 0; j < NJ; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int row = 32 * w + 16 * i + fq * 4 + e;
+                if (row < M) C[row * ldc + n0 + 16 * j + fr] = acc[i][j][e];
+            }
+}
+
 }  // namespace
 
 // C[z][s] (slab s of batch z) = A[z][:, s*kslice:(s+1)*kslice] . Bt[z][:, same]^T
@@ -179,5 +291,39 @@ SKR_API int skr_skinny_gemm(const void* A, int64_t lda, int64_t a_batch, const v
     else
         hipLaunchKernelGGL(skinny_gemm_nt_kernel<64>, grid, dim3(256), 0, s, (const __hip_bfloat16*)A, lda, a_batch,
                            (const __hip_bfloat16*)Bt, ldb, b_batch, C, ldc, c_slab, c_batch, M, kslice);
+    return SKR_CHECK_LAUNCH();
+}
+
+// Same contract as skr_skinny_gemm, LDS-DMA ring kernel (v2).
+SKR_API int skr_skinny_gemm_v2(const void* A, int64_t lda, int64_t a_batch, const void* Bt, int64_t ldb,
+                               int64_t b_batch, float* C, int64_t ldc, int64_t c_slab, int64_t c_batch, int M, int N,
+                               int K, int splits, int batch, int bn, hipStream_t s) {
+    // 128-wide N tiles once they still give >= 144 workgroups (measured, scripts/bench_gemm.py)
+    if (bn == 0) bn = (N % 128 == 0 && (N / 128) * splits * batch >= 144) ? 128 : 64;
+    if (M < 1 || M > BM || (bn != 64 && bn != 128) || N % bn != 0 || splits < 1 || K % splits != 0) return -2;
+    const int kslice = K / splits;
+    if (kslice % BK != 0 || lda % 8 != 0 || ldb % 8 != 0) return -3;
+    if (((uintptr_t)A | (uintptr_t)Bt) & 15) return -4;
+    const dim3 grid(N / bn, splits, batch);
+    const size_t lds = (size_t)NSTAGE * (BM + bn) * BK * 2;
+    if (bn == 128) {
+        static bool attr = false;
+        if (!attr) {
+            (void)hipFuncSetAttribute((const void*)skinny_gemm_glds_kernel<128>,
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+            attr = true;
+        }
+        hipLaunchKernelGGL(skinny_gemm_glds_kernel<128>, grid, dim3(256), lds, s, (const __hip_bfloat16*)A, lda,
+                           a_batch, (const __hip_bfloat16*)Bt, ldb, b_batch, C, ldc, c_slab, c_batch, M, kslice);
+    } else {
+        static bool attr = false;
+        if (!attr) {
+            (void)hipFuncSetAttribute((const void*)skinny_gemm_glds_kernel<64>,
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+            attr = true;
+        }
+        hipLaunchKernelGGL(skinny_gemm_glds_kernel<64>, grid, dim3(256), lds, s, (const __hip_bfloat16*)A, lda,
+                           a_batch, (const __hip_bfloat16*)Bt, ldb, b_batch, C, ldc, c_slab, c_batch, M, kslice);
+    }
     return SKR_CHECK_LAUNCH();
 }

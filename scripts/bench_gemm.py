@@ -40,12 +40,19 @@ def main():
         bt = torch.randn(nd, N, K, device=dev).to(torch.bfloat16)
         b = bt.transpose(1, 2).contiguous()
         res = []
-        for bn in (64, 128):
+        for algo in ("v1", "v2"):
+          gemm.GEMM_ALGO = algo
+          res.append(algo + ":")
+          for bn in (64, 128):
             for S in sorted({gemm.plan_splits(M, N, K, nd), 1, 2, 4, 8, 16, 32}):
                 if S < 1 or (K // 64) % S or N % bn:
                     continue
                 out = torch.empty(S, nd * M, N, device=dev)
                 us = timeit(lambda: gemm.rec_gemm(a, bt if nd > 1 else bt[0], out, S, nd, bn))
+                if algo == "v2" and bn == 64:
+                    ref = (a.float().view(nd, M, K) @ bt.float().transpose(1, 2)).reshape(nd * M, N)
+                    err = (out.sum(0) - ref).abs().max().item()
+                    assert err < 1e-2 * ref.abs().max().item() + 1e-3, (name, S, err)
                 res.append("b%d/S%d %.1f" % (bn, S, us))
         out1 = torch.empty(nd, M, N, device=dev)
         if nd == 1:

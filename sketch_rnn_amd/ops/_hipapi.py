@@ -83,9 +83,9 @@ class HipLib:
         lib.skr_adam_step.restype = _i
         lib.skr_global_norm.argtypes = [_p, _i64, _p, _p, _p]
         lib.skr_global_norm.restype = _i
-        lib.skr_skinny_gemm.argtypes = [_p, _i64, _i64, _p, _i64, _i64, _p, _i64, _i64, _i64, _i, _i, _i, _i, _i,
-                                        _i, _p]
-        lib.skr_skinny_gemm.restype = _i
+        for fn in (lib.skr_skinny_gemm, lib.skr_skinny_gemm_v2):
+            fn.argtypes = [_p, _i64, _i64, _p, _i64, _i64, _p, _i64, _i64, _i64, _i, _i, _i, _i, _i, _i, _p]
+            fn.restype = _i
         lib.skr_mdn_sample.restype = _i
         fs, bs = lib.skr_lstm_fwd_args_size(), lib.skr_lstm_bwd_args_size()
         if fs != C.sizeof(LstmFwdArgs) or bs != C.sizeof(LstmBwdArgs):

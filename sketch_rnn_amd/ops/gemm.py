@@ -8,6 +8,7 @@ bf16 -> fp32), so accumulation and everything downstream stay fp32.
 """
 from __future__ import annotations
 
+import os
 from typing import Optional
 
 import torch
@@ -44,6 +45,9 @@ def bmm(a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor] = None) ->
         return torch.bmm(a, b, out_dtype=torch.float32, out=out)
     return torch.bmm(a, b, out_dtype=torch.float32)
 
+
+# skinny GEMM kernel: "v2" = LDS-DMA ring (csrc/skinny_gemm.hip), "v1" = register-staged
+GEMM_ALGO = os.environ.get("SKR_GEMM", "v2")
 
 _SPLITS = (1, 2, 4, 8, 16, 32)  # powers of two: the cell kernels sum <= 8 slabs unrolled
 
@@ -85,7 +89,8 @@ def rec_gemm(a: torch.Tensor, bt: torch.Tensor, out: torch.Tensor, splits: int, 
         return out
     from ..utils import native
     lib = native.require_hip()
-    rc = lib.lib.skr_skinny_gemm(a.data_ptr(), a.stride(0), M * a.stride(0), bt.data_ptr(), bt.stride(-2),
+    fn = lib.lib.skr_skinny_gemm_v2 if GEMM_ALGO == "v2" else lib.lib.skr_skinny_gemm
+    rc = fn(a.data_ptr(), a.stride(0), M * a.stride(0), bt.data_ptr(), bt.stride(-2),
                                  N * K if nd > 1 else 0, out.data_ptr(), N, out.stride(0), M * N, M, N, K, splits, nd,
                                  bn, torch.cuda.current_stream().cuda_stream)
     if rc != 0:
