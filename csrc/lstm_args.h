@@ -46,6 +46,9 @@ struct BwdArgs {
     const float* dh_rec;               // [B, H] (grad into carried h_t) or null
     int64_t ld_dh_rec;
     int dhr_nslab; int64_t dhr_slab;
+    const float* dh_rec2;              // second split-K source of the carried-h grad (added) or null
+    int64_t ld_dh_rec2;
+    int dhr2_nslab; int64_t dhr2_slab;
     float* dc_rec;                     // [B, H] in: grad into carried c_t; out: into carried c_{t-1}
     const float* act; const float* c_new; const float* c_prev;
     const float* xhat; const float* rstd; const float* chat;

@@ -360,7 +360,8 @@ __global__ __launch_bounds__(NT) void cell_bwd(const BwdArgs a) {
         on[k] = u < H;
         const int uc = min(u, H - 1);
         const int64_t ro = (int64_t)b * H + uc;
-        dhc[k] = a.dh_rec ? slab_sum<0>(a.dh_rec, b * a.ld_dh_rec + uc, a.dhr_nslab, a.dhr_slab) : 0.f;
+        dhc[k] = (a.dh_rec ? slab_sum<0>(a.dh_rec, b * a.ld_dh_rec + uc, a.dhr_nslab, a.dhr_slab) : 0.f) +
+                 (a.dh_rec2 ? slab_sum<0>(a.dh_rec2, b * a.ld_dh_rec2 + uc, a.dhr2_nslab, a.dhr2_slab) : 0.f);
         dho[k] = a.dh_out ? slab_sum<0>(a.dh_out, ro, a.dho_nslab, a.dho_slab) : 0.f;
         dcc[k] = a.dc_rec[ro];
         cp[k] = a.c_prev[ro];

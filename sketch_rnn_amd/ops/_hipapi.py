@@ -47,6 +47,8 @@ class LstmBwdArgs(C.Structure):
         ("dho_nslab", _i), ("dho_slab", _i64),
         ("dh_rec", _p), ("ld_dh_rec", _i64),
         ("dhr_nslab", _i), ("dhr_slab", _i64),
+        ("dh_rec2", _p), ("ld_dh_rec2", _i64),
+        ("dhr2_nslab", _i), ("dhr2_slab", _i64),
         ("dc_rec", _p),
         ("act", _p), ("c_new", _p), ("c_prev", _p),
         ("xhat", _p), ("rstd", _p), ("chat", _p),

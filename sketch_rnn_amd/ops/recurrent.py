@@ -302,7 +302,49 @@ def bilstm_sequence_hip(xp_f, xp_b, W_f, W_b, h0, c0, drop_keep=1.0, drop_seed=0
 # =====================================================================================
 # HyperLSTM sequence
 # =====================================================================================
+_SIDE_STREAMS = {}
+# Concurrent branch on a second stream (SKR_TWO_STREAM=1). Off by default:
+# measured on MI355X, a cross-stream join inside a HIP graph costs 5-11 us
+# per step (rocprofv3 kernel trace), more than the overlap it buys.
+TWO_STREAM = os.environ.get("SKR_TWO_STREAM", "0") == "1"
+
+
+def _side_stream(device) -> "torch.cuda.Stream":
+    """The stream of a step's concurrent branch: an auxiliary stream per
+    device (created eagerly, so a later HIP-graph capture only records on
+    it), or the current stream when TWO_STREAM is off."""
+    if not TWO_STREAM:
+        return torch.cuda.current_stream(device)
+    key = str(device)
+    if key not in _SIDE_STREAMS:
+        _SIDE_STREAMS[key] = torch.cuda.Stream(device=device)
+    return _SIDE_STREAMS[key]
+
+
+def _join(waiter, other) -> None:
+    if waiter != other:
+        waiter.wait_stream(other)
+
+
 class _HyperSeq(torch.autograd.Function):
+    """HyperLSTM layer (LN main cell modulated by a LN hyper cell).
+
+    Per forward step the recurrent products are split by consumer so the
+    step's two dependency chains overlap on two streams:
+
+    * side stream: ``R_main = h_{t-1} @ W_h`` (the big one, N = 4H);
+    * main stream: ``R_hyp = [h_{t-1} | hh_{t-1}] @ [hW_x[IN:]; hW_h]`` ->
+      hyper cell -> ``vec = hh_t @ P`` (skinny GEMMs + fused cell kernel);
+    * join -> fused main cell (LN + modulation + gates + carry).
+
+    The backward mirrors it: after the main cell's backward, ``dh`` from the
+    main gates (``dR_main @ W_h^T``) runs on the side stream while the
+    ``dvec -> dhh`` product, the hyper cell's backward and
+    ``dR_hyp @ [hW_x[IN:]; hW_h]^T`` run on the main stream; the next main
+    cell sums both split-K slab sets while loading. Weight gradients are
+    single large GEMMs over all T*B rows after the scan.
+    """
+
     @staticmethod
     def forward(ctx, x, h0, c0, hh0, hc0, seed, W_x, W_h, bias, hW_x, hW_h, hln_g, hln_b, hlnc_g, hlnc_b,
                 W_z, b_z, W_a, ln_g, ln_b, lnc_g, lnc_b, meta):
@@ -311,7 +353,7 @@ class _HyperSeq(torch.autograd.Function):
         T, B, IN = x.shape
         H, Hh = W_h.shape[0], hW_h.shape[0]
         G, Gh = 4 * H, 4 * Hh
-        K, N = H + Hh, G + Gh
+        K = H + Hh
         dev = x.device
         f32 = torch.float32
         TB = T * B
@@ -320,23 +362,24 @@ class _HyperSeq(torch.autograd.Function):
         XH = gemm.mm(xl, gemm.lp(W_x)).view(T, B, G)
         XHY = gemm.mm(xl, gemm.lp(hW_x[:IN])).view(T, B, Gh)
         dt = gemm.lp_dtype()
-        Wcat = torch.zeros(K, N, device=dev, dtype=dt)
-        Wcat[:H, :G].copy_(W_h)
-        Wcat[:H, G:].copy_(hW_x[IN:])
-        Wcat[H:, G:].copy_(hW_h)
+        Whl = gemm.lp(W_h).contiguous()                            # [H, G]: B^T of dR_main @ W_h^T
+        WhT = Whl.t().contiguous()                                 # [G, H]: B^T of h @ W_h
+        Wyl = torch.cat([hW_x[IN:], hW_h], 0).to(dt).contiguous()  # [K, Gh]
+        WyT = Wyl.t().contiguous()                                 # [Gh, K]
         # hyper-norm projections folded: vec = hh @ P + q
         Wz3 = W_z.view(Hh, 12, E).permute(1, 0, 2)                 # [12, Hh, E]
         P = torch.bmm(Wz3, W_a).permute(1, 0, 2).reshape(Hh, 12 * H)  # [Hh, 12H]
         q = torch.bmm(b_z.view(12, 1, E), W_a).reshape(12, H).contiguous()
         Pl = P.to(dt).contiguous()             # B^T for the backward dvec @ P^T
         PlT = Pl.t().contiguous()              # B^T for the forward  hh @ P
-        WcatT = Wcat.t().contiguous()
-        S_rc = gemm.plan_splits(B, N, K, 1, dt)
+        S_m = gemm.plan_splits(B, G, H, 1, dt)
+        S_y = gemm.plan_splits(B, Gh, K, 1, dt)
         S_v = gemm.plan_splits(B, 12 * H, Hh, 1, dt, max_splits=1)
         A = torch.empty(T + 1, B, K, device=dev, dtype=dt)
         A[0, :, :H].copy_(h0)
         A[0, :, H:].copy_(hh0)
-        RC = torch.empty(T, max(S_rc, 1), B, N, device=dev, dtype=f32)
+        RM = torch.empty(T, max(S_m, 1), B, G, device=dev, dtype=f32)   # saved: the backward re-reads R_main
+        RY = torch.empty(max(S_y, 1), B, Gh, device=dev, dtype=f32)
         CC = torch.empty(T + 1, B, H, device=dev, dtype=f32)
         CC[0].copy_(c0)
         HCC = torch.empty(T + 1, B, Hh, device=dev, dtype=f32)
@@ -362,8 +405,8 @@ class _HyperSeq(torch.autograd.Function):
         # hyper cell args (LN-LSTM, no modulation)
         ah = LstmFwdArgs()
         ah.B, ah.H = B, Hh
-        ah.ld_xp, ah.ld_R = Gh, N
-        ah.R_nslab, ah.R_slab = max(S_rc, 1), B * N
+        ah.ld_xp, ah.ld_R = Gh, Gh
+        ah.R, ah.R_nslab, ah.R_slab = RY.data_ptr(), max(S_y, 1), B * Gh
         ah.ln_g, ah.ln_b, ah.lnc_g, ah.lnc_b = (t.data_ptr() for t in hln)
         ah.forget_bias, ah.keep = float(forget_bias), float(hkeep)
         ah.seed, ah.stream = sd.data_ptr(), int(stream) + 1
@@ -371,8 +414,8 @@ class _HyperSeq(torch.autograd.Function):
         # main cell args (LN + modulation)
         am = LstmFwdArgs()
         am.B, am.H = B, H
-        am.ld_xp, am.ld_R = G, N
-        am.R_nslab, am.R_slab = max(S_rc, 1), B * N
+        am.ld_xp, am.ld_R = G, G
+        am.R_nslab, am.R_slab = max(S_m, 1), B * G
         bias_c = bias.contiguous()
         am.vec_gs, am.vec_ld, am.vec_bias, am.bias = H, 12 * H, q.data_ptr(), bias_c.data_ptr()
         am.ln_g, am.ln_b, am.lnc_g, am.lnc_b = (t.data_ptr() for t in mln)
@@ -380,19 +423,23 @@ class _HyperSeq(torch.autograd.Function):
         am.seed, am.stream = sd.data_ptr(), int(stream)
         am.ld_lp, am.lp_kind = K, _lp_kind(A)
         clm, clh = _ClusterSync(T, B, H, dev), _ClusterSync(T, B, Hh, dev)
-        st = _stream()
+        main, side = torch.cuda.current_stream(), _side_stream(dev)
+        st = main.cuda_stream
         for t in range(T):
             clm.set(am, t)
             clh.set(ah, t)
-            gemm.rec_gemm(A[t], WcatT, RC[t], S_rc)
-            ah.xp, ah.R = XHY[t].data_ptr(), RC[t, 0, :, G:].data_ptr()
-            ah.c_prev, ah.step = HCC[t].data_ptr(), t
+            _join(side, main)                            # h_{t-1} written
+            with torch.cuda.stream(side):
+                gemm.rec_gemm(A[t, :, :H], WhT, RM[t], S_m)
+            gemm.rec_gemm(A[t], WyT, RY, S_y)
+            ah.xp, ah.c_prev, ah.step = XHY[t].data_ptr(), HCC[t].data_ptr(), t
             ah.h_out, ah.c_out, ah.act = HH[t].data_ptr(), HCout[t].data_ptr(), HACT[t].data_ptr()
             ah.xhat, ah.rstd, ah.chat = HXHAT[t].data_ptr(), HRSTD[t].data_ptr(), HCHAT[t].data_ptr()
             ah.h_carry, ah.h_lp, ah.c_carry = HHC[t % 2].data_ptr(), A[t + 1, :, H:].data_ptr(), HCC[t + 1].data_ptr()
             _check(lib.lib.skr_lstm_fwd_step(ctypes.byref(ah), 1, 0, st), "hyper_fwd_step")
             gemm.rec_gemm(A[t + 1, :, H:], PlT, VEC[t].unsqueeze(0), S_v)
-            am.xp, am.R, am.vec = XH[t].data_ptr(), RC[t, 0, :, :G].data_ptr(), VEC[t].data_ptr()
+            _join(main, side)                            # R_main(t) done
+            am.xp, am.R, am.vec = XH[t].data_ptr(), RM[t].data_ptr(), VEC[t].data_ptr()
             am.c_prev, am.step = CC[t].data_ptr(), t
             am.h_out, am.c_out, am.act = Hout[t].data_ptr(), Cout[t].data_ptr(), ACT[t].data_ptr()
             am.xhat, am.rstd, am.chat = XHAT[t].data_ptr(), RSTD[t].data_ptr(), CHAT[t].data_ptr()
@@ -401,10 +448,10 @@ class _HyperSeq(torch.autograd.Function):
         hT = HC[(T - 1) % 2].clone()
         hhT = HHC[(T - 1) % 2].clone()
         s = _Saved()
-        for k, v in dict(xl=xl, XH=XH, Wcat=Wcat, Pl=Pl, q=q, bias_c=bias_c, S_rc=S_rc, A=A, RC=RC, CC=CC, HCC=HCC, Cout=Cout, ACT=ACT,
-                         XHAT=XHAT, RSTD=RSTD, CHAT=CHAT, HH=HH, HCout=HCout, HACT=HACT, HXHAT=HXHAT, HRSTD=HRSTD,
-                         HCHAT=HCHAT, VEC=VEC, seed=sd, meta=meta, W_x=W_x, hW_x=hW_x, W_z=W_z, b_z=b_z,
-                         W_a=W_a, mln=mln, hln=hln).items():
+        for k, v in dict(xl=xl, XH=XH, Whl=Whl, Wyl=Wyl, Pl=Pl, q=q, bias_c=bias_c, S_m=S_m, A=A, RM=RM, CC=CC,
+                         HCC=HCC, Cout=Cout, ACT=ACT, XHAT=XHAT, RSTD=RSTD, CHAT=CHAT, HH=HH, HCout=HCout,
+                         HACT=HACT, HXHAT=HXHAT, HRSTD=HRSTD, HCHAT=HCHAT, VEC=VEC, seed=sd, meta=meta, W_x=W_x,
+                         hW_x=hW_x, W_z=W_z, b_z=b_z, W_a=W_a, mln=mln, hln=hln).items():
             setattr(s, k, v)
         ctx.s = s
         ctx.dims = (T, B, IN, H, Hh, E)
@@ -419,12 +466,14 @@ class _HyperSeq(torch.autograd.Function):
         dev = s.A.device
         f32 = torch.float32
         G, Gh = 4 * H, 4 * Hh
-        K, N = H + Hh, G + Gh
+        K = H + Hh
         TB = T * B
-        lp_on = s.Wcat.dtype == torch.bfloat16
+        lp_on = s.Whl.dtype == torch.bfloat16
         ldt = torch.bfloat16 if lp_on else f32
-        dRC = torch.empty(T, B, N, device=dev, dtype=f32)
-        dRC_lp = torch.empty(T, B, N, device=dev, dtype=torch.bfloat16) if lp_on else None
+        dRM = torch.empty(T, B, G, device=dev, dtype=f32)
+        dRY = torch.empty(T, B, Gh, device=dev, dtype=f32)
+        dRM_lp = torch.empty(T, B, G, device=dev, dtype=ldt) if lp_on else dRM
+        dRY_lp = torch.empty(T, B, Gh, device=dev, dtype=ldt) if lp_on else dRY
         dXH = torch.empty(T, B, G, device=dev, dtype=f32)
         DLNY = torch.empty(T, B, G, device=dev, dtype=f32)
         DLNCY = torch.empty(T, B, H, device=dev, dtype=f32)
@@ -432,70 +481,77 @@ class _HyperSeq(torch.autograd.Function):
         HDLNCY = torch.empty(T, B, Hh, device=dev, dtype=f32)
         dVEC = torch.empty(T, B, 12 * H, device=dev, dtype=ldt)
         S_h = gemm.plan_splits(B, Hh, 12 * H, 1, ldt)
-        S_a = gemm.plan_splits(B, K, N, 1, ldt)
-        DHZ = torch.empty(max(S_h, 1), B, Hh, device=dev, dtype=f32)  # slabs of dhh from the vec path
-        DA = torch.zeros(max(S_a, 1), B, K, device=dev, dtype=f32)    # slabs of d[h | hh] carried
+        S_am = gemm.plan_splits(B, H, G, 1, ldt)
+        S_ay = gemm.plan_splits(B, K, Gh, 1, ldt)
+        DHZ = torch.empty(max(S_h, 1), B, Hh, device=dev, dtype=f32)    # slabs of dhh from the vec path
+        DAM = torch.zeros(max(S_am, 1), B, H, device=dev, dtype=f32)    # slabs of dh from the main gates
+        DAY = torch.zeros(max(S_ay, 1), B, K, device=dev, dtype=f32)    # slabs of d[h | hh] from the hyper gates
         if dhT is not None:
-            DA[0, :, :H].copy_(dhT)
+            DAY[0, :, :H].copy_(dhT)
         if dhhT is not None:
-            DA[0, :, H:].copy_(dhhT)
+            DAY[0, :, H:].copy_(dhhT)
         dc_rec = dcT.contiguous().clone() if dcT is not None else torch.zeros(B, H, device=dev, dtype=f32)
         dhc_rec = dhcT.contiguous().clone() if dhcT is not None else torch.zeros(B, Hh, device=dev, dtype=f32)
         dHout = dHout.contiguous() if dHout is not None else None
-        S_rc = max(s.S_rc, 1)
         am = LstmBwdArgs()
         am.B, am.H = B, H
-        am.dh_rec, am.ld_dh_rec, am.dc_rec = DA.data_ptr(), K, dc_rec.data_ptr()
-        am.dhr_nslab, am.dhr_slab, am.dho_nslab = max(S_a, 1), B * K, 1
+        am.dh_rec, am.ld_dh_rec, am.dhr_nslab, am.dhr_slab = DAY.data_ptr(), K, max(S_ay, 1), B * K
+        am.dh_rec2, am.ld_dh_rec2, am.dhr2_nslab, am.dhr2_slab = DAM.data_ptr(), H, max(S_am, 1), B * H
+        am.dc_rec, am.dho_nslab = dc_rec.data_ptr(), 1
         am.ln_g, am.lnc_g, am.lnc_b = s.mln[0].data_ptr(), s.mln[2].data_ptr(), s.mln[3].data_ptr()
-        am.ld_xp, am.ld_R = G, N
-        am.R_nslab, am.R_slab = S_rc, B * N
+        am.ld_xp, am.ld_R = G, G
+        am.R_nslab, am.R_slab = max(s.S_m, 1), B * G
         am.vec_gs, am.vec_ld, am.vec_bias = H, 12 * H, s.q.data_ptr()
         am.keep, am.seed, am.stream = float(keep), s.seed.data_ptr(), int(stream)
-        am.ld_dG, am.ld_dG_lp, am.dG_lp_kind = N, N, 1 if lp_on else 0
+        am.ld_dG, am.ld_dG_lp, am.dG_lp_kind = G, G, 1 if lp_on else 0
         am.ld_dxp, am.dvec_kind = G, 1 if lp_on else 2
         ah = LstmBwdArgs()
         ah.B, ah.H = B, Hh
         ah.dh_out, ah.dho_nslab, ah.dho_slab = DHZ.data_ptr(), max(S_h, 1), B * Hh
-        ah.dh_rec, ah.ld_dh_rec, ah.dc_rec = DA[0, :, H:].data_ptr(), K, dhc_rec.data_ptr()
-        ah.dhr_nslab, ah.dhr_slab = max(S_a, 1), B * K
+        ah.dh_rec, ah.ld_dh_rec, ah.dc_rec = DAY[0, :, H:].data_ptr(), K, dhc_rec.data_ptr()
+        ah.dhr_nslab, ah.dhr_slab = max(S_ay, 1), B * K
         ah.ln_g, ah.lnc_g, ah.lnc_b = s.hln[0].data_ptr(), s.hln[2].data_ptr(), s.hln[3].data_ptr()
         ah.keep, ah.seed, ah.stream = float(hkeep), s.seed.data_ptr(), int(stream) + 1
-        ah.ld_dG, ah.ld_dG_lp, ah.dG_lp_kind = N, N, 1 if lp_on else 0
+        ah.ld_dG, ah.ld_dG_lp, ah.dG_lp_kind = Gh, Gh, 1 if lp_on else 0
         clm, clh = _ClusterSync(T, B, H, dev), _ClusterSync(T, B, Hh, dev)
-        st = _stream()
+        main, side = torch.cuda.current_stream(), _side_stream(dev)
+        st = main.cuda_stream
         for t in range(T - 1, -1, -1):
             clm.set(am, t)
             clh.set(ah, t)
             am.dh_out = dHout[t].data_ptr() if dHout is not None else None
             am.act, am.c_new, am.c_prev = s.ACT[t].data_ptr(), s.Cout[t].data_ptr(), s.CC[t].data_ptr()
             am.xhat, am.rstd, am.chat = s.XHAT[t].data_ptr(), s.RSTD[t].data_ptr(), s.CHAT[t].data_ptr()
-            am.xp, am.R, am.vec = s.XH[t].data_ptr(), s.RC[t, 0, :, :G].data_ptr(), s.VEC[t].data_ptr()
+            am.xp, am.R, am.vec = s.XH[t].data_ptr(), s.RM[t].data_ptr(), s.VEC[t].data_ptr()
             am.step = t
-            am.dG = dRC[t, :, :G].data_ptr()
-            am.dG_lp = dRC_lp[t, :, :G].data_ptr() if lp_on else None
+            am.dG = dRM[t].data_ptr()
+            am.dG_lp = dRM_lp[t].data_ptr() if lp_on else None
             am.dxp, am.dvec = dXH[t].data_ptr(), dVEC[t].data_ptr()
             am.dlny, am.dlncy = DLNY[t].data_ptr(), DLNCY[t].data_ptr()
             _check(lib.lib.skr_lstm_bwd_step(ctypes.byref(am), 1, 1, st), "hyper_main_bwd_step")
+            _join(side, main)                            # dR_main(t) written, DAM consumed
+            with torch.cuda.stream(side):
+                gemm.rec_gemm(dRM_lp[t], s.Whl, DAM, S_am)
             gemm.rec_gemm(dVEC[t], s.Pl, DHZ, S_h)
             ah.act, ah.c_new, ah.c_prev = s.HACT[t].data_ptr(), s.HCout[t].data_ptr(), s.HCC[t].data_ptr()
             ah.xhat, ah.rstd, ah.chat = s.HXHAT[t].data_ptr(), s.HRSTD[t].data_ptr(), s.HCHAT[t].data_ptr()
             ah.step = t
-            ah.dG = dRC[t, :, G:].data_ptr()
-            ah.dG_lp = dRC_lp[t, :, G:].data_ptr() if lp_on else None
+            ah.dG = dRY[t].data_ptr()
+            ah.dG_lp = dRY_lp[t].data_ptr() if lp_on else None
             ah.dlny, ah.dlncy = HDLNY[t].data_ptr(), HDLNCY[t].data_ptr()
             _check(lib.lib.skr_lstm_bwd_step(ctypes.byref(ah), 1, 0, st), "hyper_bwd_step")
-            gemm.rec_gemm(dRC_lp[t] if lp_on else dRC[t], s.Wcat, DA, S_a)
-        dA = DA.sum(0) if DA.shape[0] > 1 else DA[0]
+            gemm.rec_gemm(dRY_lp[t], s.Wyl, DAY, S_ay)
+            _join(main, side)                            # dh (main gates) for step t-1 ready
+        dh0 = DAY[:, :, :H].sum(0) + DAM.sum(0)
+        dhh0 = DAY[:, :, H:].sum(0)
         # ---- weight gradients: single large GEMMs over all T*B rows ----
-        dRCm = (dRC_lp if lp_on else dRC).view(TB, N)
-        dWcat = gemm.mm(s.A[:T].reshape(TB, K).t(), dRCm)
-        dW_h = dWcat[:H, :G]
+        A2 = s.A[:T].reshape(TB, K)
+        dW_h = gemm.mm(A2[:, :H].t(), dRM_lp.view(TB, G))
+        dW_y = gemm.mm(A2.t(), dRY_lp.view(TB, Gh))
         dhW_x = torch.empty_like(s.hW_x)
-        dhW_x[IN:] = dWcat[:H, G:]
-        dhW_h = dWcat[H:, G:]
-        dXHY = dRC[:, :, G:].reshape(TB, Gh)
-        dXHl, dXHYl = gemm.lp(dXH.view(TB, G)), gemm.lp(dXHY)
+        dhW_x[IN:] = dW_y[:H]
+        dhW_h = dW_y[H:]
+        dXHl, dXHYl = gemm.lp(dXH.view(TB, G)), gemm.lp(dRY.view(TB, Gh))
         dW_x = gemm.mm(s.xl.t(), dXHl)
         dhW_x[:IN] = gemm.mm(s.xl.t(), dXHYl)
         dx = gemm.mm(dXHl, gemm.lp(s.W_x).t())
@@ -518,7 +574,6 @@ class _HyperSeq(torch.autograd.Function):
         hxh, hdl = s.HXHAT.view(TB, Gh), HDLNY.view(TB, Gh)
         g_hln = (red(hdl, hxh), hdl.sum(0), red(HDLNCY.view(TB, Hh), s.HCHAT.view(TB, Hh)),
                  HDLNCY.view(TB, Hh).sum(0))
-        dh0, dhh0 = dA[:, :H].contiguous(), dA[:, H:].contiguous()
         ctx.s = None
         return (dx.view(T, B, IN), dh0, dc_rec, dhh0, dhc_rec, None, dW_x, dW_h, dbias, dhW_x, dhW_h,
                 g_hln[0], g_hln[1], g_hln[2], g_hln[3], dW_z, db_z, dWa, g_ln[0], g_ln[1], g_ln[2], g_ln[3], None)
