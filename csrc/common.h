@@ -78,6 +78,33 @@ __device__ __forceinline__ void block_sum(float (&v)[N], float* lds) {
 
 __device__ __forceinline__ __hip_bfloat16 to_bf16(float x) { return __float2bfloat16(x); }
 
+// Sum of the NS split-K partial slabs at idx (NS > 0: compile-time count,
+// all loads independent); NS == 0: runtime count n, batches of 8 clamped loads.
+template <int NS>
+__device__ __forceinline__ float slab_sum(const float* p, int64_t idx, int n, int64_t slab) {
+    if constexpr (NS > 0) {
+        float v[NS];
+#pragma unroll
+        for (int s = 0; s < NS; ++s) v[s] = p[s * slab + idx];
+#pragma unroll
+        for (int w = 1; w < NS; w *= 2)
+#pragma unroll
+            for (int s = 0; s + w < NS; s += 2 * w) v[s] += v[s + w];
+        return v[0];
+    } else {
+        float v = 0.f;
+        for (int s0 = 0; s0 < n; s0 += 8) {
+            float t[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) t[k] = p[(int64_t)min(s0 + k, n - 1) * slab + idx];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) v += (s0 + k < n) ? t[k] : 0.f;
+        }
+        return v;
+    }
+}
+
+
 }  // namespace skr
 
 #define SKR_CHECK_LAUNCH() (int)hipGetLastError()

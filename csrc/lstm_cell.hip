@@ -58,32 +58,6 @@ constexpr int kMaxCluster = 16;
 constexpr unsigned kSpinLimit = 1u << 21;
 constexpr int kSlots = 16;        // 8-byte granules per workgroup slot (128 B)
 
-// Sum of the NS split-K partial slabs at idx (NS > 0: compile-time count,
-// all loads independent); NS == 0: runtime count n, batches of 8 clamped loads.
-template <int NS>
-__device__ __forceinline__ float slab_sum(const float* p, int64_t idx, int n, int64_t slab) {
-    if constexpr (NS > 0) {
-        float v[NS];
-#pragma unroll
-        for (int s = 0; s < NS; ++s) v[s] = p[s * slab + idx];
-#pragma unroll
-        for (int w = 1; w < NS; w *= 2)
-#pragma unroll
-            for (int s = 0; s + w < NS; s += 2 * w) v[s] += v[s + w];
-        return v[0];
-    } else {
-        float v = 0.f;
-        for (int s0 = 0; s0 < n; s0 += 8) {
-            float t[8];
-#pragma unroll
-            for (int k = 0; k < 8; ++k) t[k] = p[(int64_t)min(s0 + k, n - 1) * slab + idx];
-#pragma unroll
-            for (int k = 0; k < 8; ++k) v += (s0 + k < n) ? t[k] : 0.f;
-        }
-        return v;
-    }
-}
-
 // Publish `nv` floats of this workgroup (LDS `mine`) as tagged granules and
 // gather the row's C*nv values into LDS `all` ([C][nv]).
 __device__ void cluster_allgather(uint64_t* part, int* err, int b, int c, int C, const float* mine, int nv,

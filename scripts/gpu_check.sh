@@ -35,6 +35,10 @@ for s in "${steps[@]}"; do
         bench_torch) run bench_torch 900 python bench.py --steps 3 --warmup 1 --backend torch --no-eval ;;
         bench_torch_small) run bench_torch_small 600 python bench.py --steps 3 --warmup 1 --backend torch --no-eval --config vae_small ;;
         bench_sample) run bench_sample 600 python scripts/bench_sample.py ;;
+        bench_ref) run bench_ref 600 python scripts/bench_reference.py ;;
+        bench_ref_bf16) run bench_ref_bf16 600 python scripts/bench_reference.py --dtype bf16 ;;
+        bench_ref_torch) run bench_ref_torch 600 python scripts/bench_reference.py --backend torch --steps 5 ;;
+        bench_ref_cudnn) run bench_ref_cudnn 600 python scripts/bench_reference.py --cudnn ;;
         prof) run prof 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --no-eval ;;
         *) echo "unknown step $s"; exit 2 ;;
     esac

@@ -94,10 +94,18 @@ def hyper_sequence(p, x, h0, c0, hh0, hc0, forget_bias: float = 1.0, drop_keep: 
 
 
 def gru_sequence(p, x, h0, reset=None, reset_h=None):
+    """TF GRUCell recurrence over ``x [T, B, in]`` -> ``(H [T, B, H], h_T)``."""
+    if use_hip(x):
+        from .recurrent_gru import gru_sequence_hip
+        return gru_sequence_hip(p, x, h0, reset, reset_h)
     return gru_sequence_torch(p, x, h0, reset, reset_h)
 
 
 def rnn_sequence(p, x, h0, reset=None, reset_h=None):
+    """tanh-RNN recurrence over ``x [T, B, in]`` -> ``(H [T, B, H], h_T)``."""
+    if use_hip(x):
+        from .recurrent_gru import rnn_sequence_hip
+        return rnn_sequence_hip(p, x, h0, reset, reset_h)
     return rnn_sequence_torch(p, x, h0, reset, reset_h)
 
 

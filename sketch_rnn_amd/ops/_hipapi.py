@@ -70,6 +70,43 @@ class LstmBwdArgs(C.Structure):
     ]
 
 
+class GruFwdArgs(C.Structure):
+    """Mirror of ``GruFwdArgs`` in csrc/gru_cell.hip."""
+    _fields_ = [
+        ("B", _i), ("H", _i),
+        ("xg", _p), ("ld_xg", _i64),
+        ("Rg", _p), ("ld_Rg", _i64), ("Rg_nslab", _i), ("Rg_slab", _i64),
+        ("xc", _p), ("ld_xc", _i64),
+        ("Rc", _p), ("ld_Rc", _i64), ("Rc_nslab", _i), ("Rc_slab", _i64),
+        ("h_prev", _p),
+        ("reset", _p), ("init_h", _p),
+        ("ru", _p),
+        ("rh_lp", _p), ("ld_rh", _i64), ("rh_kind", _i),
+        ("cand", _p),
+        ("h_out", _p),
+        ("h_carry", _p),
+        ("h_lp", _p), ("ld_lp", _i64), ("lp_kind", _i),
+    ]
+
+
+class GruBwdArgs(C.Structure):
+    """Mirror of ``GruBwdArgs`` in csrc/gru_cell.hip."""
+    _fields_ = [
+        ("B", _i), ("H", _i),
+        ("dh_out", _p),
+        ("dh_elem", _p),
+        ("dhg", _p), ("ld_dhg", _i64), ("dhg_nslab", _i), ("dhg_slab", _i64),
+        ("ru", _p), ("cand", _p), ("h_prev", _p),
+        ("reset", _p),
+        ("dinit_h", _p),
+        ("dh_tot", _p),
+        ("dpc", _p), ("dpc_lp", _p), ("dpc_kind", _i),
+        ("drh", _p), ("ld_drh", _i64), ("drh_nslab", _i), ("drh_slab", _i64),
+        ("dpg", _p), ("dpg_lp", _p), ("dpg_kind", _i),
+        ("dh_elem_out", _p),
+    ]
+
+
 class HipLib:
     def __init__(self, lib: C.CDLL):
         self.lib = lib
@@ -77,8 +114,6 @@ class HipLib:
         lib.skr_lstm_fwd_step.restype = _i
         lib.skr_lstm_bwd_step.argtypes = [C.POINTER(LstmBwdArgs), _i, _i, _p]
         lib.skr_lstm_bwd_step.restype = _i
-        lib.skr_lstm_fwd_args_size.restype = _i
-        lib.skr_lstm_bwd_args_size.restype = _i
         lib.skr_mdn_loss.argtypes = [_p, _i64, _p, _i64, _i64, _i, _i, _f, _i, _f, _p, _p, _p, _p]
         lib.skr_mdn_loss.restype = _i
         lib.skr_adam_step.argtypes = [_p, _p, _p, _p, _p, _p, _i64, _f, _f, _f, _i, _f, _p]
@@ -89,10 +124,17 @@ class HipLib:
             fn.argtypes = [_p, _i64, _i64, _p, _i64, _i64, _p, _i64, _i64, _i64, _i, _i, _i, _i, _i, _i, _p]
             fn.restype = _i
         lib.skr_mdn_sample.restype = _i
-        fs, bs = lib.skr_lstm_fwd_args_size(), lib.skr_lstm_bwd_args_size()
-        if fs != C.sizeof(LstmFwdArgs) or bs != C.sizeof(LstmBwdArgs):
-            raise RuntimeError("libskrnn_hip.so arg-struct layout mismatch: fwd %d vs %d, bwd %d vs %d"
-                               % (fs, C.sizeof(LstmFwdArgs), bs, C.sizeof(LstmBwdArgs)))
+        lib.skr_gru_fwd.argtypes = [C.POINTER(GruFwdArgs), _i, _p]
+        lib.skr_gru_fwd.restype = _i
+        lib.skr_gru_bwd.argtypes = [C.POINTER(GruBwdArgs), _i, _p]
+        lib.skr_gru_bwd.restype = _i
+        for name, cls in (("skr_lstm_fwd_args_size", LstmFwdArgs), ("skr_lstm_bwd_args_size", LstmBwdArgs),
+                          ("skr_gru_fwd_args_size", GruFwdArgs), ("skr_gru_bwd_args_size", GruBwdArgs)):
+            fn = getattr(lib, name)
+            fn.restype = _i
+            if fn() != C.sizeof(cls):
+                raise RuntimeError("libskrnn_hip.so arg-struct layout mismatch: %s %d vs %d"
+                                   % (cls.__name__, fn(), C.sizeof(cls)))
 
 
 def bind(lib: C.CDLL) -> HipLib:

@@ -1,0 +1,43 @@
+"""Native libraries load on the host (no GPU needed) and the ctypes mirrors of
+every kernel argument block match the compiled C++ layouts."""
+import ctypes
+import os
+import sys
+
+import pytest
+
+from sketch_rnn_amd.utils import native
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope="module")
+def hip():
+    if not os.path.exists(native.HIP_LIB):
+        sys.path.insert(0, os.path.join(ROOT, "scripts"))
+        import build_native
+        build_native.build_hip()
+    lib = native.hip_lib()
+    assert lib is not None
+    return lib
+
+
+def test_arg_struct_layouts(hip):
+    from sketch_rnn_amd.ops import _hipapi as api
+    for fn, cls in (("skr_lstm_fwd_args_size", api.LstmFwdArgs), ("skr_lstm_bwd_args_size", api.LstmBwdArgs),
+                    ("skr_gru_fwd_args_size", api.GruFwdArgs), ("skr_gru_bwd_args_size", api.GruBwdArgs)):
+        assert getattr(hip.lib, fn)() == ctypes.sizeof(cls), fn
+
+
+def test_exported_entry_points(hip):
+    for name in ("skr_lstm_fwd_step", "skr_lstm_bwd_step", "skr_gru_fwd", "skr_gru_bwd", "skr_skinny_gemm",
+                 "skr_skinny_gemm_v2", "skr_mdn_loss", "skr_adam_step", "skr_global_norm", "skr_mdn_sample"):
+        assert hasattr(hip.lib, name), name
+
+
+def test_host_packer_loads():
+    if native.host_lib() is None:
+        sys.path.insert(0, os.path.join(ROOT, "scripts"))
+        import build_native
+        build_native.build_host()
+    assert native.host_lib() is not None
