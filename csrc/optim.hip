@@ -4,7 +4,12 @@
 // contiguous fp32 buffers (sketch_rnn_amd/train/optim.py), padded to a
 // multiple of 64 elements, so one float4-vectorised launch updates every
 // tensor. Scalars live on the device so the step is graph-capturable:
-//   scal[0] = lr, scal[1] = t (incremented on device), scal[2] = |g|, scal[3] = clip scale
+//   scal[0] = lr, scal[1] = t (incremented on device), scal[2] = |g|, scal[3] = clip scale,
+//   scal[4] = 1 if this step was skipped, scal[5] = number of skipped steps
+// Failure detection: the global gradient norm is computed every step (all
+// clip modes); with nonfinite_policy = 1 a step whose norm is NaN/Inf is
+// skipped on the device (no update, t not advanced) and counted, so a
+// diverging batch never needs a host sync to be caught.
 // Adam is TF's (model.py:183): eps added to sqrt(v), bias corrections folded
 // into lr_t = lr * sqrt(1 - b2^t) / (1 - b1^t).
 #include "common.h"
@@ -27,21 +32,23 @@ __global__ __launch_bounds__(kBlock) void sumsq_partial_kernel(const float4* __r
 }
 
 __global__ void finalize_kernel(const double* __restrict__ partial, int nparts, float* __restrict__ scal,
-                                int clip_mode, float clip) {
+                                int clip_mode, float clip, int nonfinite_policy) {
     // single wave: deterministic order
     double s = 0.0;
     for (int i = threadIdx.x; i < nparts; i += 64) s += partial[i];
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
     if (threadIdx.x == 0) {
-        scal[1] += 1.0f;
-        if (clip_mode == 1) {
-            const float norm = (float)sqrt(s);
-            scal[2] = norm;
-            scal[3] = clip / fmaxf(norm, clip);
+        const float norm = (float)sqrt(s);
+        scal[2] = norm;
+        const bool skip = nonfinite_policy == 1 && !isfinite(norm);
+        scal[4] = skip ? 1.0f : 0.0f;
+        if (skip) {
+            scal[5] += 1.0f;
         } else {
-            scal[3] = 1.0f;
+            scal[1] += 1.0f;
         }
+        scal[3] = clip_mode == 1 ? clip / fmaxf(norm, clip) : 1.0f;
     }
 }
 
@@ -49,6 +56,7 @@ __global__ __launch_bounds__(kBlock) void adam_kernel(float4* __restrict__ p, co
                                                       float4* __restrict__ m, float4* __restrict__ v,
                                                       const float* __restrict__ scal, int64_t n4, float b1,
                                                       float b2, float eps, int clip_mode, float clip) {
+    if (scal[4] != 0.f) return;  // skipped (non-finite gradient)
     const float t = scal[1];
     const float lr_t = scal[0] * sqrtf(1.f - powf(b2, t)) / (1.f - powf(b1, t));
     const float sc = scal[3];
@@ -82,28 +90,28 @@ int grid_for(int64_t n4) {
 
 }  // namespace
 
-// clip_mode: 0 none, 1 global norm, 2 per-element value. `partial` must hold 2048 doubles.
+// clip_mode: 0 none, 1 global norm, 2 per-element value. nonfinite_policy: 0 apply (TF semantics),
+// 1 skip the step on a non-finite gradient norm. `partial` must hold 2048 doubles; scal 8 floats.
 SKR_API int skr_adam_step(float* p, const float* g, float* m, float* v, float* scal, double* partial, int64_t n,
-                          float b1, float b2, float eps, int clip_mode, float clip, hipStream_t s) {
+                          float b1, float b2, float eps, int clip_mode, float clip, int nonfinite_policy,
+                          hipStream_t s) {
     if (n % 4 != 0) return -2;
     const int64_t n4 = n / 4;
     const int grid = grid_for(n4);
-    if (clip_mode == 1) {
-        hipLaunchKernelGGL(sumsq_partial_kernel, dim3(grid), dim3(kBlock), 0, s, (const float4*)g, n4, partial);
-    }
-    hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(64), 0, s, partial, clip_mode == 1 ? grid : 0, scal,
-                       clip_mode, clip);
+    hipLaunchKernelGGL(sumsq_partial_kernel, dim3(grid), dim3(kBlock), 0, s, (const float4*)g, n4, partial);
+    hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(64), 0, s, partial, grid, scal, clip_mode, clip,
+                       nonfinite_policy);
     hipLaunchKernelGGL(adam_kernel, dim3(grid), dim3(kBlock), 0, s, (float4*)p, (const float4*)g, (float4*)m,
                        (float4*)v, (const float*)scal, n4, b1, b2, eps, clip_mode, clip);
     return SKR_CHECK_LAUNCH();
 }
 
-// standalone global norm (diagnostics): writes sqrt(sum g^2) to out[0]
+// standalone global norm (diagnostics): writes sqrt(sum g^2) to scal_tmp[2] (scal_tmp: 8 floats)
 SKR_API int skr_global_norm(const float* g, int64_t n, double* partial, float* scal_tmp, hipStream_t s) {
     if (n % 4 != 0) return -2;
     const int64_t n4 = n / 4;
     const int grid = grid_for(n4);
     hipLaunchKernelGGL(sumsq_partial_kernel, dim3(grid), dim3(kBlock), 0, s, (const float4*)g, n4, partial);
-    hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(64), 0, s, partial, grid, scal_tmp, 1, 1.0f);
+    hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(64), 0, s, partial, grid, scal_tmp, 1, 1.0f, 0);
     return SKR_CHECK_LAUNCH();
 }

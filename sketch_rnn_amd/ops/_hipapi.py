@@ -116,7 +116,7 @@ class HipLib:
         lib.skr_lstm_bwd_step.restype = _i
         lib.skr_mdn_loss.argtypes = [_p, _i64, _p, _i64, _i64, _i, _i, _f, _i, _f, _p, _p, _p, _p]
         lib.skr_mdn_loss.restype = _i
-        lib.skr_adam_step.argtypes = [_p, _p, _p, _p, _p, _p, _i64, _f, _f, _f, _i, _f, _p]
+        lib.skr_adam_step.argtypes = [_p, _p, _p, _p, _p, _p, _i64, _f, _f, _f, _i, _f, _i, _p]
         lib.skr_adam_step.restype = _i
         lib.skr_global_norm.argtypes = [_p, _i64, _p, _p, _p]
         lib.skr_global_norm.restype = _i

@@ -19,6 +19,12 @@ size, ``lr_t = lr * sqrt(1 - b2^t) / (1 - b1^t)``.
 Clipping modes:
 * ``"global_norm"`` -- ``tf.clip_by_global_norm`` (reference, ``model.py:182``);
 * ``"value"`` -- per-element ``clip_by_value`` (sketch-rnn VAE).
+
+Failure detection: the global gradient norm is computed every
+step; ``nonfinite="skip"`` drops a step whose gradient norm is NaN/Inf on the
+device (no parameter or moment update, ``t`` not advanced) and counts it in
+``scalars[5]`` -- no host sync per step. ``"apply"`` keeps TF semantics.
+Device scalars: ``[lr, t, grad_norm, clip_scale, skipped_now, skipped_total, -, -]``.
 """
 from __future__ import annotations
 
@@ -31,12 +37,15 @@ import torch
 class FlatAdam:
     def __init__(self, params: Iterable[torch.nn.Parameter], lr: float = 1e-3, betas=(0.9, 0.999),
                  eps: float = 1e-8, clip_mode: Optional[str] = None, clip: float = 0.0,
-                 align: int = 64):
+                 align: int = 64, nonfinite: str = "skip"):
         self.params: List[torch.nn.Parameter] = [p for p in params if p.requires_grad]
         self.b1, self.b2 = betas
         self.eps = eps
         self.clip_mode = clip_mode
         self.clip = float(clip)
+        if nonfinite not in ("skip", "apply"):
+            raise ValueError(nonfinite)
+        self.nonfinite = nonfinite
         dev = self.params[0].device
         # 256-byte aligned slots per tensor: vector loads never straddle tensors
         self.offsets, off = [], 0
@@ -53,8 +62,8 @@ class FlatAdam:
             self.flat[o:o + n].copy_(p.detach().reshape(-1))
             p.data = self.flat[o:o + n].view_as(p)
             p.grad = self.grad[o:o + n].view_as(p)
-        # device scalars: [lr, step, grad_norm, clip_scale]
-        self.scalars = torch.zeros(4, device=dev, dtype=torch.float32)
+        # device scalars: [lr, step, grad_norm, clip_scale, skipped_now, skipped_total, -, -]
+        self.scalars = torch.zeros(8, device=dev, dtype=torch.float32)
         self.set_lr(lr)
         self.step_count = 0
 
@@ -85,20 +94,33 @@ class FlatAdam:
     def _step_torch(self) -> None:
         g = self.grad
         sc = self.scalars
-        sc[1] += 1.0
+        norm = torch.sqrt((g.double() * g.double()).sum()).float()
+        sc[2] = norm
+        skip = (~torch.isfinite(norm)) & (self.nonfinite == "skip")
+        sc[4] = skip.float()
+        sc[5] += skip.float()
+        sc[1] += (~skip).float()
+        keep = (~skip).float()
         if self.clip_mode == "global_norm":
-            norm = torch.sqrt((g.double() * g.double()).sum()).float()
-            sc[2] = norm
             scale = self.clip / torch.clamp(norm, min=self.clip)
             sc[3] = scale
-            g = g * scale
-        elif self.clip_mode == "value":
-            g = g.clamp(-self.clip, self.clip)
-        t = sc[1]
-        lr_t = sc[0] * torch.sqrt(1.0 - self.b2 ** t) / (1.0 - self.b1 ** t)
-        self.m.mul_(self.b1).add_(g, alpha=1.0 - self.b1)
-        self.v.mul_(self.b2).addcmul_(g, g, value=1.0 - self.b2)
+            g = g * torch.where(skip, torch.zeros_like(scale), scale)
+        else:
+            sc[3] = 1.0
+            if self.clip_mode == "value":
+                g = g.clamp(-self.clip, self.clip)
+            g = torch.where(skip, torch.zeros_like(g), g)
+        t = torch.clamp(sc[1], min=1.0)
+        lr_t = sc[0] * torch.sqrt(1.0 - self.b2 ** t) / (1.0 - self.b1 ** t) * keep
+        b1 = 1.0 - (1.0 - self.b1) * keep
+        b2 = 1.0 - (1.0 - self.b2) * keep
+        self.m.mul_(b1).add_(g * (1.0 - b1))
+        self.v.mul_(b2).add_(g * g * (1.0 - b2))
         self.flat.sub_(lr_t * self.m / (torch.sqrt(self.v) + self.eps))
+
+    def skipped_steps(self) -> int:
+        """Steps dropped for a non-finite gradient (one host sync)."""
+        return int(self.scalars[5].item())
 
     # ---------------------------------------------------------------------------------
     def state_dict(self):

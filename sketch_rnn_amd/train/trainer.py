@@ -27,6 +27,7 @@ from ..config import RefConfig, VAEConfig
 from ..models.reference import SketchRNN
 from ..models.vae import SketchVAE
 from ..parallel import dp
+from ..utils.trace import GpuPhaseTimer, PhaseTimes, phase
 from . import schedules
 from .graph import GraphedStep
 from .optim import FlatAdam
@@ -51,8 +52,9 @@ class ReferenceTrainer:
         self.loader = loader
         self.device = torch.device(device)
         self.model = SketchRNN(cfg).to(self.device)
+        # TF semantics (a NaN step is applied; the divergence guard then stops the run, train.py:93-94)
         self.opt = FlatAdam(self.model.parameters(), lr=cfg.learning_rate, eps=cfg.adam_eps,
-                            clip_mode="global_norm", clip=cfg.grad_clip)
+                            clip_mode="global_norm", clip=cfg.grad_clip, nonfinite="apply")
         self.save_dir = os.path.join(save_root, cfg.dataset_name)
         self.log = log
         self.metrics_path = metrics_path
@@ -183,7 +185,7 @@ class VAETrainer:
     def __init__(self, cfg: VAEConfig, train_set, valid_set=None, test_set=None, device: str = "cpu",
                  save_dir: str = "save/vae", use_graph: Optional[bool] = None,
                  log: Callable[[str], None] = print, metrics_path: Optional[str] = None,
-                 compute_dtype: str = "fp32"):
+                 compute_dtype: str = "fp32", max_skipped: int = 100):
         self.cfg = cfg
         self.train_set, self.valid_set, self.test_set = train_set, valid_set, test_set
         self.device = torch.device(device)
@@ -191,8 +193,10 @@ class VAETrainer:
         self.model = SketchVAE(cfg).to(self.device)
         from .. import ops
         ops.set_compute_dtype(compute_dtype)
+        # a step with a non-finite gradient is dropped on the device and counted (FlatAdam)
         self.opt = FlatAdam(self.model.parameters(), lr=cfg.learning_rate, eps=cfg.adam_eps,
-                            clip_mode="value", clip=cfg.grad_clip)
+                            clip_mode="value", clip=cfg.grad_clip, nonfinite="skip")
+        self.max_skipped = max_skipped
         dp.broadcast_params(self.opt.flat)
         self.reducer = dp.GradReducer(self.opt.grad) if self.world > 1 else None
         self.save_dir = save_dir
@@ -203,6 +207,8 @@ class VAETrainer:
         self._graph = None
         self.seed = torch.zeros(1, dtype=torch.int64, device=self.device)
         self.kl_w = torch.zeros((), device=self.device)
+        self.host_times = PhaseTimes()            # data / step / eval / save wall time
+        self.gpu_times = GpuPhaseTimer(enabled=metrics_path is not None)
 
     def _fwd_bwd(self, strokes, lengths, labels):
         self.opt.zero_grad()
@@ -238,12 +244,16 @@ class VAETrainer:
                 else:
                     self._graph = GraphedStep(self._fwd_bwd, static, snapshot=snap)
                     self._graph_opt = GraphedStep(self._opt_step, {}, snapshot=snap)
-            out = self._graph(strokes=strokes, lengths=lengths, labels=labels)
+            with self.gpu_times.time("fwd_bwd" if self._graph_opt is not None else "step"):
+                out = self._graph(strokes=strokes, lengths=lengths, labels=labels)
             if self._graph_opt is not None:
-                self.reducer.all_reduce()
-                self._graph_opt()
+                with self.gpu_times.time("allreduce"):
+                    self.reducer.all_reduce()
+                with self.gpu_times.time("optimizer"):
+                    self._graph_opt()
         else:
-            out = self._step_fn(strokes, lengths, labels)
+            with self.gpu_times.time("step"):
+                out = self._step_fn(strokes, lengths, labels)
         self.seed.add_(1)
         self.step += 1
         return out
@@ -298,8 +308,10 @@ class VAETrainer:
         num_steps = cfg.num_steps if num_steps is None else num_steps
         t0 = time.time()
         while self.step < num_steps:
-            batch = self.batch_to_device(self.train_set.random_batch(self.rank, self.world))
-            out = self.train_step(*batch)
+            with phase("data", self.host_times):
+                batch = self.batch_to_device(self.train_set.random_batch(self.rank, self.world))
+            with phase("step", self.host_times):
+                out = self.train_step(*batch)
             if self.step % log_every == 0 or self.step == num_steps:
                 vals = {k: float(v) for k, v in out.items()}
                 dt = (time.time() - t0) / log_every
@@ -308,15 +320,26 @@ class VAETrainer:
                     self.log("step: %d, lr: %.6f, klw: %0.4f, cost: %.4f, recon: %.4f, kl: %.4f, time/step: %.4f" % (
                         self.step, self.opt.lr, schedules.kl_weight(cfg, self.step - 1), vals["cost"],
                         vals["r_cost"], vals["kl_cost"], dt))
+                    vals["grad_norm"] = float(self.opt.scalars[2])
                     if self.metrics_path:
+                        rec = dict(step=self.step, **vals, time=dt, lr=self.opt.lr,
+                                   kl_weight=schedules.kl_weight(cfg, self.step - 1),
+                                   strokes_per_s=self.world * cfg.batch_size * cfg.max_seq_len / max(dt, 1e-9),
+                                   skipped=self.opt.skipped_steps(),
+                                   host_ms=self.host_times.mean_ms(), gpu_ms=self.gpu_times.collect())
+                        self.host_times.reset()
                         with open(self.metrics_path, "a") as f:
-                            f.write(json.dumps(dict(step=self.step, **vals, time=dt)) + "\n")
-                if not math.isfinite(vals["cost"]):
-                    raise DivergenceError("non-finite cost at step %d" % self.step)
+                            f.write(json.dumps(rec) + "\n")
+                skipped = self.opt.skipped_steps()
+                if skipped > self.max_skipped:
+                    raise DivergenceError("%d steps with a non-finite gradient (last cost %r at step %d)"
+                                          % (skipped, vals["cost"], self.step))
             if eval_every and self.step % eval_every == 0 and self.valid_set is not None:
-                ev = self.evaluate(self.valid_set)
+                with phase("eval", self.host_times):
+                    ev = self.evaluate(self.valid_set)
                 if self.rank == 0:
                     self.log("valid: cost %.4f recon %.4f kl %.4f" % (ev["cost"], ev["r_cost"], ev["kl_cost"]))
             if cfg.save_every and self.step % cfg.save_every == 0:
-                self.save()
+                with phase("save", self.host_times):
+                    self.save()
         return self.save()

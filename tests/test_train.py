@@ -253,3 +253,48 @@ def test_cli_smoke(tmp_path):
     assert cvs.main(["--save_dir", root + "/v", "--out", root + "/v.svg", "--n", "2", "--mode", "interpolate",
                      "--device", "cpu"]) == 0
     assert os.path.exists(root + "/v.svg")
+
+
+def test_flat_adam_nonfinite_skip_and_apply():
+    ps = _params()
+    opt = FlatAdam(ps, lr=0.1, clip_mode="value", clip=1.0, nonfinite="skip")
+    for p in ps:
+        p.grad.fill_(0.5)
+    opt.step()
+    before = opt.flat.clone()
+    m0 = opt.m.clone()
+    ps[0].grad[0, 0] = float("nan")
+    opt.step()
+    assert torch.equal(opt.flat, before) and torch.equal(opt.m, m0)
+    assert int(opt.scalars[1]) == 1 and opt.skipped_steps() == 1 and int(opt.scalars[4]) == 1
+    ps[0].grad[0, 0] = 0.5
+    opt.step()
+    assert int(opt.scalars[1]) == 2 and int(opt.scalars[4]) == 0 and not torch.equal(opt.flat, before)
+    ps2 = _params()
+    opt2 = FlatAdam(ps2, lr=0.1, nonfinite="apply")
+    for p in ps2:
+        p.grad.fill_(0.5)
+    ps2[1].grad[0] = float("inf")
+    opt2.step()
+    assert opt2.skipped_steps() == 0 and not torch.isfinite(opt2.flat).all()
+
+
+def test_vae_metrics_jsonl_and_phases(tmp_path):
+    from sketch_rnn_amd.train.trainer import VAETrainer
+    from sketch_rnn_amd.utils.trace import PhaseTimes, phase
+    cfg = VAEConfig(enc_rnn_size=8, dec_rnn_size=16, z_size=4, num_mixture=2, max_seq_len=24, batch_size=4,
+                    save_every=0)
+    (train, valid, test), _ = _vae_sets(cfg, n=40)
+    m = str(tmp_path / "m.jsonl")
+    tr = VAETrainer(cfg, train, valid, test, save_dir=str(tmp_path / "v"), log=lambda s: None, metrics_path=m)
+    tr.train(num_steps=4, log_every=2)
+    recs = [json.loads(l) for l in open(m)]
+    assert [r["step"] for r in recs] == [2, 4]
+    for r in recs:
+        assert {"cost", "r_cost", "kl_cost", "grad_norm", "lr", "kl_weight", "strokes_per_s", "skipped",
+                "host_ms"} <= set(r)
+        assert "data" in r["host_ms"] and "step" in r["host_ms"] and r["skipped"] == 0
+    pt = PhaseTimes()
+    with phase("x", pt):
+        pass
+    assert pt.count["x"] == 1 and "x" in pt.mean_ms()
