@@ -271,6 +271,114 @@ __global__ __launch_bounds__(256) void skinny_gemm_glds_kernel(
             }
 }
 
+// ---------------------------------------------------------------------------
+// fp8 (OCP e4m3) variant of the v2 ring for inference-time recurrent
+// products: operands are bytes, a K-tile is 128 elements (the same 128-byte
+// LDS rows and swizzle as the bf16 kernel), v_mfma_f32_16x16x32_fp8_fp8
+// (lane l: 8 bytes of row l&15 at k 8(l>>4)). Epilogue applies the per-
+// output-column weight scale and the activation scale: C = acc * sa * sb[n].
+constexpr int BK8 = 128;
+
+template <int BN>
+__global__ __launch_bounds__(256) void skinny_gemm_fp8_kernel(
+    const uint8_t* __restrict__ A, int64_t lda, int64_t a_batch,
+    const uint8_t* __restrict__ Bt, int64_t ldb, int64_t b_batch, const float* __restrict__ b_scale,
+    int64_t bs_batch, float a_scale,
+    float* __restrict__ C, int64_t ldc, int64_t c_slab, int64_t c_batch, int M, int kslice) {
+    constexpr int NJ = BN / 16;
+    constexpr int A_CH = BM / 8, B_CH = BN / 8;      // 1-KiB chunks (8 rows x 128 B) per tile
+    constexpr int GPW = (A_CH + B_CH) / 4;
+    constexpr int TILE = (BM + BN) * BK8;            // bytes per stage
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem8[];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int n0 = blockIdx.x * BN;
+    const int64_t k0 = (int64_t)blockIdx.y * kslice;
+    const int n = kslice / BK8;
+    A += blockIdx.z * a_batch;
+    Bt += blockIdx.z * b_batch;
+    b_scale += blockIdx.z * bs_batch;
+    C += blockIdx.z * c_batch + blockIdx.y * c_slab;
+
+    const int r8 = lane >> 3, slot = lane & 7;
+    const uint8_t* asrc[A_CH / 4];
+    const uint8_t* bsrc[B_CH / 4];
+#pragma unroll
+    for (int i = 0; i < A_CH / 4; ++i) {
+        const int row = (w + 4 * i) * 8 + r8;
+        asrc[i] = A + (int64_t)min(row, M - 1) * lda + k0 + (slot ^ ((row >> 1) & 7)) * 16;
+    }
+#pragma unroll
+    for (int i = 0; i < B_CH / 4; ++i) {
+        const int row = (w + 4 * i) * 8 + r8;
+        bsrc[i] = Bt + (int64_t)(n0 + row) * ldb + k0 + (slot ^ ((row >> 1) & 7)) * 16;
+    }
+    auto issue = [&](int kt) {
+        uint8_t* st = smem8 + (kt % NSTAGE) * TILE;
+        const int64_t ko = (int64_t)kt * BK8;
+#pragma unroll
+        for (int i = 0; i < A_CH / 4; ++i)
+            __builtin_amdgcn_global_load_lds((const void*)(asrc[i] + ko),
+                                             (__attribute__((address_space(3))) void*)(st + (w + 4 * i) * 1024), 16, 0, 0);
+#pragma unroll
+        for (int i = 0; i < B_CH / 4; ++i)
+            __builtin_amdgcn_global_load_lds((const void*)(bsrc[i] + ko),
+                                             (__attribute__((address_space(3))) void*)(st + BM * BK8 + (w + 4 * i) * 1024),
+                                             16, 0, 0);
+    };
+
+    f32x4 acc[2][NJ];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    const int fr = lane & 15, fq = lane >> 4;
+#pragma unroll
+    for (int p = 0; p < NSTAGE - 1; ++p)
+        if (p < n) issue(p);
+    for (int kt = 0; kt < n; ++kt) {
+        const int ahead = min(n - 1 - kt, NSTAGE - 2);
+        if (ahead >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * GPW) : "memory");
+        else if (ahead == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GPW) : "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        if (kt + NSTAGE - 1 < n) issue(kt + NSTAGE - 1);
+        const uint8_t* As = smem8 + (kt % NSTAGE) * TILE;
+        const uint8_t* Bs = As + BM * BK8;
+#pragma unroll
+        for (int ks = 0; ks < BK8 / 32; ++ks) {
+            const int c16 = ks * 2 + (fq >> 1), half = (fq & 1) * 8;
+            long af[2], bfr[NJ];
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                const int row = 32 * w + 16 * i + fr;
+                af[i] = *(const long*)(&As[row * BK8 + ((c16 ^ ((row >> 1) & 7)) * 16) + half]);
+            }
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) {
+                const int row = 16 * j + fr;
+                bfr[j] = *(const long*)(&Bs[row * BK8 + ((c16 ^ ((row >> 1) & 7)) * 16) + half]);
+            }
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int j = 0; j < NJ; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(af[i], bfr[j], acc[i][j], 0, 0, 0);
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+        const float sc = a_scale * b_scale[n0 + 16 * j + fr];
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int row = 32 * w + 16 * i + fq * 4 + e;
+                if (row < M) C[row * ldc + n0 + 16 * j + fr] = acc[i][j][e] * sc;
+            }
+    }
+}
+
 }  // namespace
 
 // C[z][s] (slab s of batch z) = A[z][:, s*kslice:(s+1)*kslice] . Bt[z][:, same]^T
@@ -324,6 +432,43 @@ SKR_API int skr_skinny_gemm_v2(const void* A, int64_t lda, int64_t a_batch, cons
         }
         hipLaunchKernelGGL(skinny_gemm_glds_kernel<64>, grid, dim3(256), lds, s, (const __hip_bfloat16*)A, lda,
                            a_batch, (const __hip_bfloat16*)Bt, ldb, b_batch, C, ldc, c_slab, c_batch, M, kslice);
+    }
+    return SKR_CHECK_LAUNCH();
+}
+
+// fp8 e4m3 operands (bytes): C[z][s] = a_scale * b_scale[n] * A8[z][:, ks] . Bt8[z][:, ks]^T.
+// Requirements as skr_skinny_gemm_v2 with kslice % 128 == 0 and 16-byte aligned rows.
+SKR_API int skr_skinny_gemm_fp8(const void* A, int64_t lda, int64_t a_batch, const void* Bt, int64_t ldb,
+                                int64_t b_batch, const float* b_scale, int64_t bs_batch, float a_scale, float* C,
+                                int64_t ldc, int64_t c_slab, int64_t c_batch, int M, int N, int K, int splits,
+                                int batch, int bn, hipStream_t s) {
+    if (bn == 0) bn = (N % 128 == 0 && (N / 128) * splits * batch >= 144) ? 128 : 64;
+    if (M < 1 || M > BM || (bn != 64 && bn != 128) || N % bn != 0 || splits < 1 || K % splits != 0) return -2;
+    const int kslice = K / splits;
+    if (kslice % BK8 != 0 || lda % 16 != 0 || ldb % 16 != 0) return -3;
+    if (((uintptr_t)A | (uintptr_t)Bt) & 15) return -4;
+    const dim3 grid(N / bn, splits, batch);
+    const size_t lds = (size_t)NSTAGE * (BM + bn) * BK8;
+    if (bn == 128) {
+        static bool attr = false;
+        if (!attr) {
+            (void)hipFuncSetAttribute((const void*)skinny_gemm_fp8_kernel<128>,
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+            attr = true;
+        }
+        hipLaunchKernelGGL(skinny_gemm_fp8_kernel<128>, grid, dim3(256), lds, s, (const uint8_t*)A, lda, a_batch,
+                           (const uint8_t*)Bt, ldb, b_batch, b_scale, bs_batch, a_scale, C, ldc, c_slab, c_batch,
+                           M, kslice);
+    } else {
+        static bool attr = false;
+        if (!attr) {
+            (void)hipFuncSetAttribute((const void*)skinny_gemm_fp8_kernel<64>,
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+            attr = true;
+        }
+        hipLaunchKernelGGL(skinny_gemm_fp8_kernel<64>, grid, dim3(256), lds, s, (const uint8_t*)A, lda, a_batch,
+                           (const uint8_t*)Bt, ldb, b_batch, b_scale, bs_batch, a_scale, C, ldc, c_slab, c_batch,
+                           M, kslice);
     }
     return SKR_CHECK_LAUNCH();
 }

@@ -35,6 +35,9 @@ for s in "${steps[@]}"; do
         bench_torch) run bench_torch 900 python bench.py --steps 3 --warmup 1 --backend torch --no-eval ;;
         bench_torch_small) run bench_torch_small 600 python bench.py --steps 3 --warmup 1 --backend torch --no-eval --config vae_small ;;
         bench_sample) run bench_sample 600 python scripts/bench_sample.py ;;
+        bench_sample_fp8) run bench_sample_fp8 600 python scripts/bench_sample.py --dtype fp8 ;;
+        bench_sample_1k) run bench_sample_1k 600 python scripts/bench_sample.py --batch 1024 ;;
+        bench_sample_1k_fp8) run bench_sample_1k_fp8 600 python scripts/bench_sample.py --batch 1024 --dtype fp8 ;;
         bench_ref) run bench_ref 600 python scripts/bench_reference.py ;;
         bench_ref_bf16) run bench_ref_bf16 600 python scripts/bench_reference.py --dtype bf16 ;;
         bench_ref_torch) run bench_ref_torch 600 python scripts/bench_reference.py --backend torch --steps 5 ;;

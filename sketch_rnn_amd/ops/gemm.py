@@ -52,12 +52,21 @@ GEMM_ALGO = os.environ.get("SKR_GEMM", "v2")
 _SPLITS = (1, 2, 4, 8, 16, 32)  # powers of two: the cell kernels sum <= 8 slabs unrolled
 
 
+def row_blocks(M: int) -> int:
+    """128-row blocks the skinny kernels run for M rows (0: not supported):
+    M <= 128 in one block, or a multiple of 128 up to 1024 as a batch of blocks."""
+    if M <= 128:
+        return 1
+    return M // 128 if M % 128 == 0 and M <= 1024 else 0
+
+
 def plan_splits(M: int, N: int, K: int, batch: int = 1, dtype: torch.dtype = _BF16, max_splits: int = 32) -> int:
     """Split-K factor for :func:`rec_gemm`: aim for 256-512 workgroups.
     Returns 0 when the native skinny kernel cannot take the shape."""
-    if dtype != _BF16 or M > 128 or N % 64 or K % 64:
+    mb = row_blocks(M)
+    if dtype != _BF16 or mb == 0 or (mb > 1 and batch > 1) or N % 64 or K % 64:
         return 0
-    tiles = (N // 64) * batch
+    tiles = (N // 64) * batch * mb
     best = 1
     for s in _SPLITS:
         if s > max_splits or (K // 64) % s:
@@ -90,11 +99,86 @@ def rec_gemm(a: torch.Tensor, bt: torch.Tensor, out: torch.Tensor, splits: int, 
     from ..utils import native
     lib = native.require_hip()
     fn = lib.lib.skr_skinny_gemm_v2 if GEMM_ALGO == "v2" else lib.lib.skr_skinny_gemm
-    rc = fn(a.data_ptr(), a.stride(0), M * a.stride(0), bt.data_ptr(), bt.stride(-2),
-                                 N * K if nd > 1 else 0, out.data_ptr(), N, out.stride(0), M * N, M, N, K, splits, nd,
-                                 bn, torch.cuda.current_stream().cuda_stream)
+    if nd == 1 and M > 128:   # 128-row blocks as the kernel's batch dimension, sharing B
+        mb = row_blocks(M)
+        rc = fn(a.data_ptr(), a.stride(0), 128 * a.stride(0), bt.data_ptr(), bt.stride(-2), 0, out.data_ptr(), N,
+                out.stride(0), 128 * N, 128, N, K, splits, mb, bn, torch.cuda.current_stream().cuda_stream)
+    else:
+        rc = fn(a.data_ptr(), a.stride(0), M * a.stride(0), bt.data_ptr(), bt.stride(-2), N * K if nd > 1 else 0,
+                out.data_ptr(), N, out.stride(0), M * N, M, N, K, splits, nd, bn,
+                torch.cuda.current_stream().cuda_stream)
     if rc != 0:
         raise RuntimeError("skr_skinny_gemm failed (%d) for M=%d N=%d K=%d S=%d" % (rc, M, N, K, splits))
+    return out
+
+
+# ---- inference-time helpers ------------------------------------------------------------
+_WCACHE = {}
+
+
+def derived(W, tag: str, fn):
+    """``fn(W)`` cached while ``W`` (a tensor or a tuple of tensors) is
+    unchanged (same storage and version): for inference, so per-call weight
+    casts / transposes / quantisation run once instead of at every decode
+    step. Never use it inside a captured training step (in-graph updates do
+    not bump the version counter)."""
+    ws = W if isinstance(W, tuple) else (W,)
+    key = (tag,) + tuple((w.data_ptr(), w._version, tuple(w.shape), w.dtype) for w in ws)
+    v = _WCACHE.get(key)
+    if v is None:
+        if len(_WCACHE) > 512:
+            _WCACHE.clear()
+        v = _WCACHE[key] = fn(*ws)
+    return v
+
+
+FP8_MAX = 448.0           # OCP e4m3
+FP8_ACT_SCALE = 64.0      # csrc/common.h kFp8ActScale: activations are stored x64
+
+
+def quantize_fp8_rows(bt: torch.Tensor):
+    """``bt [N, K]`` (B^T) -> ``(q uint8 [N, K] OCP e4m3, scale fp32 [N])`` with
+    one scale per output column: ``bt ~= q * scale[:, None]``."""
+    b = bt.float()
+    scale = (b.abs().amax(1) / FP8_MAX).clamp_min(1e-12)
+    q = (b / scale[:, None]).to(torch.float8_e4m3fn).view(torch.uint8).contiguous()
+    return q, scale.contiguous()
+
+
+def plan_splits_fp8(M: int, N: int, K: int, batch: int = 1, max_splits: int = 32) -> int:
+    """Split-K factor for :func:`rec_gemm_fp8` (K-tiles of 128); 0 = unusable."""
+    mb = row_blocks(M)
+    if mb == 0 or N % 64 or K % 128:
+        return 0
+    tiles = (N // 64) * batch * mb
+    best = 1
+    for s in _SPLITS:
+        if s > max_splits or (K // 128) % s:
+            continue
+        if tiles * s > 512:
+            break
+        best = s
+        if tiles * s >= 256:
+            break
+    return best
+
+
+def rec_gemm_fp8(a8: torch.Tensor, bq, out: torch.Tensor, splits: int, bn: int = 0) -> torch.Tensor:
+    """``sum_s out[s] = (a8 / 64) @ (q * scale)^T`` with fp8 operands:
+    ``a8 [M, K]`` uint8 activations (x64), ``bq = quantize_fp8_rows(B^T)``."""
+    from ..utils import native
+    lib = native.require_hip()
+    q, scale = bq
+    M, K = a8.shape[0], a8.shape[1]
+    N = q.shape[0]
+    mb = row_blocks(M)
+    rows = M if mb == 1 else 128
+    rc = lib.lib.skr_skinny_gemm_fp8(a8.data_ptr(), a8.stride(0), 128 * a8.stride(0), q.data_ptr(), q.stride(0), 0,
+                                     scale.data_ptr(), 0, 1.0 / FP8_ACT_SCALE, out.data_ptr(), N, out.stride(0),
+                                     128 * N, rows, N, K, max(splits, 1), mb, bn,
+                                     torch.cuda.current_stream().cuda_stream)
+    if rc != 0:
+        raise RuntimeError("skr_skinny_gemm_fp8 failed (%d) for M=%d N=%d K=%d S=%d" % (rc, M, N, K, splits))
     return out
 
 

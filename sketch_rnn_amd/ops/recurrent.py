@@ -63,7 +63,23 @@ def _seed_tensor(seed, device) -> torch.Tensor:
 
 
 def _lp_kind(t: torch.Tensor) -> int:
+    """GEMM-operand encoding written by the cell kernels: 1 bf16, 2 fp32, 3 fp8 e4m3 (x64)."""
+    if t.dtype == torch.uint8:
+        return 3
     return 1 if t.dtype == torch.bfloat16 else 2
+
+
+def _fp8_ok(M: int, *nk) -> bool:
+    """fp8 recurrent GEMMs (inference only): compute dtype 'fp8' and every
+    (N, K) pair of the step tileable by the fp8 kernel."""
+    from . import get_compute_dtype
+    if get_compute_dtype() != "fp8":
+        return False
+    return all(gemm.plan_splits_fp8(M, n, k) > 0 for n, k in zip(nk[::2], nk[1::2]))
+
+
+def _to_fp8_act(h: torch.Tensor) -> torch.Tensor:
+    return (h.float() * gemm.FP8_ACT_SCALE).to(torch.float8_e4m3fn).view(torch.uint8)
 
 
 class _Saved:
@@ -147,13 +163,24 @@ class _LSTMSeq(torch.autograd.Function):
         f32 = torch.float32
         ln = ln_g is not None
         xp = xp.contiguous()
-        Wl = gemm.lp(W_h.reshape(nd, H, G)).contiguous()   # B^T of the backward product dG @ W^T
-        WlT = Wl.transpose(1, 2).contiguous()              # B^T of the forward product h @ W
-        ldt = Wl.dtype
         Bg = BB // nd
-        S = gemm.plan_splits(Bg, G, H, nd, ldt)
-        A = torch.empty(T + 1, BB, H, device=dev, dtype=ldt)   # GEMM operands: carried h
-        A[0].copy_(h0)
+        infer = not any(ctx.needs_input_grad)   # sampling / eval: weights are static, no backward
+        fp8 = infer and _fp8_ok(Bg, G, H) and nd == 1
+        ldt = gemm.lp_dtype()
+        if infer:
+            Wl = None
+            WlT = gemm.derived(W_h, "lstmT%s%d" % (ldt, nd),
+                               lambda W: gemm.lp(W.reshape(nd, H, G)).transpose(1, 2).contiguous())
+        else:
+            Wl = gemm.lp(W_h.reshape(nd, H, G)).contiguous()   # B^T of the backward product dG @ W^T
+            WlT = Wl.transpose(1, 2).contiguous()              # B^T of the forward product h @ W
+        if fp8:
+            WQ = gemm.derived(W_h, "lstm_fp8", lambda W: gemm.quantize_fp8_rows(W.reshape(H, G).t()))
+            S = gemm.plan_splits_fp8(Bg, G, H)
+        else:
+            S = gemm.plan_splits(Bg, G, H, nd, ldt)
+        A = torch.empty(T + 1, BB, H, device=dev, dtype=torch.uint8 if fp8 else ldt)   # GEMM operands: carried h
+        A[0].copy_(_to_fp8_act(h0) if fp8 else h0)
         CC = torch.empty(T + 1, BB, H, device=dev, dtype=f32)  # carried c
         CC[0].copy_(c0)
         Hout = torch.empty(T, BB, H, device=dev, dtype=f32)
@@ -182,7 +209,10 @@ class _LSTMSeq(torch.autograd.Function):
         st = _stream()
         for t in range(T):
             cl.set(a, t)
-            gemm.rec_gemm(A[t], WlT, R, S, nd)
+            if fp8:
+                gemm.rec_gemm_fp8(A[t], WQ, R, S)
+            else:
+                gemm.rec_gemm(A[t], WlT, R, S, nd)
             a.xp = xp[t].data_ptr()
             a.c_prev = CC[t].data_ptr()
             a.reset = _ptr(rst[t]) if rst is not None else None
@@ -362,22 +392,46 @@ class _HyperSeq(torch.autograd.Function):
         XH = gemm.mm(xl, gemm.lp(W_x)).view(T, B, G)
         XHY = gemm.mm(xl, gemm.lp(hW_x[:IN])).view(T, B, Gh)
         dt = gemm.lp_dtype()
-        Whl = gemm.lp(W_h).contiguous()                            # [H, G]: B^T of dR_main @ W_h^T
-        WhT = Whl.t().contiguous()                                 # [G, H]: B^T of h @ W_h
-        Wyl = torch.cat([hW_x[IN:], hW_h], 0).to(dt).contiguous()  # [K, Gh]
-        WyT = Wyl.t().contiguous()                                 # [Gh, K]
-        # hyper-norm projections folded: vec = hh @ P + q
-        Wz3 = W_z.view(Hh, 12, E).permute(1, 0, 2)                 # [12, Hh, E]
-        P = torch.bmm(Wz3, W_a).permute(1, 0, 2).reshape(Hh, 12 * H)  # [Hh, 12H]
-        q = torch.bmm(b_z.view(12, 1, E), W_a).reshape(12, H).contiguous()
-        Pl = P.to(dt).contiguous()             # B^T for the backward dvec @ P^T
-        PlT = Pl.t().contiguous()              # B^T for the forward  hh @ P
-        S_m = gemm.plan_splits(B, G, H, 1, dt)
-        S_y = gemm.plan_splits(B, Gh, K, 1, dt)
-        S_v = gemm.plan_splits(B, 12 * H, Hh, 1, dt, max_splits=1)
-        A = torch.empty(T + 1, B, K, device=dev, dtype=dt)
-        A[0, :, :H].copy_(h0)
-        A[0, :, H:].copy_(hh0)
+        infer = not any(ctx.needs_input_grad)   # sampling / eval: weights are static, no backward
+
+        def wy(hW_x, hW_h):                      # [K, Gh]: B^T of dR_hyp @ W_y^T
+            return torch.cat([hW_x[IN:], hW_h], 0).to(dt).contiguous()
+
+        def fold(W_z, b_z, W_a):                 # hyper-norm projections folded: vec = hh @ P + q
+            Wz3 = W_z.view(Hh, 12, E).permute(1, 0, 2)                      # [12, Hh, E]
+            P = torch.bmm(Wz3, W_a).permute(1, 0, 2).reshape(Hh, 12 * H)   # [Hh, 12H]
+            q = torch.bmm(b_z.view(12, 1, E), W_a).reshape(12, H).contiguous()
+            return P.to(dt).contiguous(), q
+
+        if infer:
+            Whl = Wyl = Pl = None
+            WhT = gemm.derived(W_h, "hypWhT%s" % dt, lambda W: gemm.lp(W).t().contiguous())
+            WyT = gemm.derived((hW_x, hW_h), "hypWyT%s" % dt, lambda a, b: wy(a, b).t().contiguous())
+            PlT, q = gemm.derived((W_z, b_z, W_a), "hypP%s" % dt,
+                                  lambda a, b, c: (lambda P, q: (P.t().contiguous(), q))(*fold(a, b, c)))
+        else:
+            Whl = gemm.lp(W_h).contiguous()      # [H, G]: B^T of dR_main @ W_h^T
+            WhT = Whl.t().contiguous()           # [G, H]: B^T of h @ W_h
+            Wyl = wy(hW_x, hW_h)
+            WyT = Wyl.t().contiguous()           # [Gh, K]
+            Pl, q = fold(W_z, b_z, W_a)          # B^T for the backward dvec @ P^T
+            PlT = Pl.t().contiguous()            # B^T for the forward  hh @ P
+        fp8 = infer and _fp8_ok(B, G, H, Gh, K, 12 * H, Hh)
+        if fp8:
+            WhT = gemm.derived(WhT, "q8", gemm.quantize_fp8_rows)
+            WyT = gemm.derived(WyT, "q8", gemm.quantize_fp8_rows)
+            PlT = gemm.derived(PlT, "q8", gemm.quantize_fp8_rows)
+            S_m, S_y = gemm.plan_splits_fp8(B, G, H), gemm.plan_splits_fp8(B, Gh, K)
+            S_v = gemm.plan_splits_fp8(B, 12 * H, Hh, max_splits=1)
+        else:
+            S_m = gemm.plan_splits(B, G, H, 1, dt)
+            S_y = gemm.plan_splits(B, Gh, K, 1, dt)
+            S_v = gemm.plan_splits(B, 12 * H, Hh, 1, dt, max_splits=1)
+        rgemm = (lambda a, b, out, S: gemm.rec_gemm_fp8(a, b, out, S)) if fp8 else \
+            (lambda a, b, out, S: gemm.rec_gemm(a, b, out, S))
+        A = torch.empty(T + 1, B, K, device=dev, dtype=torch.uint8 if fp8 else dt)
+        A[0, :, :H].copy_(_to_fp8_act(h0) if fp8 else h0)
+        A[0, :, H:].copy_(_to_fp8_act(hh0) if fp8 else hh0)
         RM = torch.empty(T, max(S_m, 1), B, G, device=dev, dtype=f32)   # saved: the backward re-reads R_main
         RY = torch.empty(max(S_y, 1), B, Gh, device=dev, dtype=f32)
         CC = torch.empty(T + 1, B, H, device=dev, dtype=f32)
@@ -430,14 +484,14 @@ class _HyperSeq(torch.autograd.Function):
             clh.set(ah, t)
             _join(side, main)                            # h_{t-1} written
             with torch.cuda.stream(side):
-                gemm.rec_gemm(A[t, :, :H], WhT, RM[t], S_m)
-            gemm.rec_gemm(A[t], WyT, RY, S_y)
+                rgemm(A[t, :, :H], WhT, RM[t], S_m)
+            rgemm(A[t], WyT, RY, S_y)
             ah.xp, ah.c_prev, ah.step = XHY[t].data_ptr(), HCC[t].data_ptr(), t
             ah.h_out, ah.c_out, ah.act = HH[t].data_ptr(), HCout[t].data_ptr(), HACT[t].data_ptr()
             ah.xhat, ah.rstd, ah.chat = HXHAT[t].data_ptr(), HRSTD[t].data_ptr(), HCHAT[t].data_ptr()
             ah.h_carry, ah.h_lp, ah.c_carry = HHC[t % 2].data_ptr(), A[t + 1, :, H:].data_ptr(), HCC[t + 1].data_ptr()
             _check(lib.lib.skr_lstm_fwd_step(ctypes.byref(ah), 1, 0, st), "hyper_fwd_step")
-            gemm.rec_gemm(A[t + 1, :, H:], PlT, VEC[t].unsqueeze(0), S_v)
+            rgemm(A[t + 1, :, H:], PlT, VEC[t].unsqueeze(0), S_v)
             _join(main, side)                            # R_main(t) done
             am.xp, am.R, am.vec = XH[t].data_ptr(), RM[t].data_ptr(), VEC[t].data_ptr()
             am.c_prev, am.step = CC[t].data_ptr(), t

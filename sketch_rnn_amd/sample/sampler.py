@@ -284,6 +284,11 @@ class GraphDecoder:
             self.labels.copy_(labels)
         self.seed.fill_(int(seed))
         if self.use_graph:
+            # the graph holds inference-cached weight copies (bf16 / fp8): re-capture after a weight update
+            sig = tuple(p._version for p in self.model.parameters())
+            if self.graph is not None and sig != self._sig:
+                self.graph = None
+            self._sig = sig
             if self.graph is None:
                 s = torch.cuda.Stream()
                 s.wait_stream(torch.cuda.current_stream())
