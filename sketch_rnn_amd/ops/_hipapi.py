@@ -127,6 +127,8 @@ class HipLib:
                                              _i, _i, _i, _i, _i, _i, _p]
         lib.skr_skinny_gemm_fp8.restype = _i
         lib.skr_mdn_sample.restype = _i
+        lib.skr_colsum.argtypes = [_p, _i, _p, _i64, _i64, _i64, _i64, _i, _i, _p, _p, _p]
+        lib.skr_colsum.restype = _i
         lib.skr_gru_fwd.argtypes = [C.POINTER(GruFwdArgs), _i, _p]
         lib.skr_gru_fwd.restype = _i
         lib.skr_gru_bwd.argtypes = [C.POINTER(GruBwdArgs), _i, _p]

@@ -32,6 +32,7 @@ import torch
 from ..utils import native
 from . import gemm
 from ._hipapi import LstmBwdArgs, LstmFwdArgs
+from .reduce import colsum
 
 
 def _ptr(t: Optional[torch.Tensor]):
@@ -292,9 +293,11 @@ class _LSTMSeq(torch.autograd.Function):
             dW = gemm.bmm(An.transpose(1, 2), dGn).view(s.wshape)
         g_ln = [None] * 4
         if ln:
-            def red(x, n):
-                return x.view(T, nd, B, n).sum((0, 2)).view(s.lnp[0].shape[:-1] + (n,))
-            g_ln = [red(DLNY * s.XHAT, G), red(DLNY, G), red(DLNCY * s.CHAT, H), red(DLNCY, H)]
+            def red(x, y, n):   # per direction group: rows (t, b) of the [T, nd, B, n] stream
+                parts = [colsum(x.view(T, nd, B, n)[:, g], y.view(T, nd, B, n)[:, g]) for g in range(nd)]
+                shape = s.lnp[0].shape[:-1] + (n,)
+                return torch.stack([p[0] for p in parts]).view(shape), torch.stack([p[1] for p in parts]).view(shape)
+            g_ln = list(red(DLNY, s.XHAT, G) + red(DLNCY, s.CHAT, H))
         ctx.s = None
         return (dG, dW, dh_rec, dc_rec, dinit_h, dinit_c, g_ln[0], g_ln[1], g_ln[2], g_ln[3], None, None, None)
 
@@ -621,13 +624,9 @@ class _HyperSeq(torch.autograd.Function):
         dZS = dZS12.transpose(0, 1).reshape(TB, 12 * E)
         dW_z = HHm.t() @ dZS
         db_z = dZS.sum(0)
-        dbias = torch.sum(dVEC.view(TB, 12, H)[:, 8:12], 0, dtype=f32).reshape(G)
-        red = lambda a, b_: (a * b_).sum(0)
-        xh, dl = s.XHAT.view(TB, G), DLNY.view(TB, G)
-        g_ln = (red(dl, xh), dl.sum(0), red(DLNCY.view(TB, H), s.CHAT.view(TB, H)), DLNCY.view(TB, H).sum(0))
-        hxh, hdl = s.HXHAT.view(TB, Gh), HDLNY.view(TB, Gh)
-        g_hln = (red(hdl, hxh), hdl.sum(0), red(HDLNCY.view(TB, Hh), s.HCHAT.view(TB, Hh)),
-                 HDLNCY.view(TB, Hh).sum(0))
+        _, dbias = colsum(dVEC.view(TB, 12 * H)[:, 8 * H:])          # shift-vector grads = bias grads
+        g_ln = colsum(DLNY.view(TB, G), s.XHAT.view(TB, G)) + colsum(DLNCY.view(TB, H), s.CHAT.view(TB, H))
+        g_hln = colsum(HDLNY.view(TB, Gh), s.HXHAT.view(TB, Gh)) + colsum(HDLNCY.view(TB, Hh), s.HCHAT.view(TB, Hh))
         ctx.s = None
         return (dx.view(T, B, IN), dh0, dc_rec, dhh0, dhc_rec, None, dW_x, dW_h, dbias, dhW_x, dhW_h,
                 g_hln[0], g_hln[1], g_hln[2], g_hln[3], dW_z, db_z, dWa, g_ln[0], g_ln[1], g_ln[2], g_ln[3], None)

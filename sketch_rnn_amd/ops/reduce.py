@@ -1,0 +1,40 @@
+"""Column reductions for sequence parameter gradients (``csrc/reduce.hip``).
+
+``colsum(x, y)`` returns ``(sum_rows(x * y), sum_rows(x))`` for ``x, y``
+shaped ``[R1, R2, C]`` (any strides with a contiguous last dim) -- the
+LayerNorm gamma/beta and bias gradients of the recurrent layers, computed in
+one pass over the saved ``[T*B, C]`` streams. PyTorch fallback on the CPU.
+"""
+from __future__ import annotations
+
+from typing import Optional, Tuple
+
+import torch
+
+
+def colsum(x: torch.Tensor, y: Optional[torch.Tensor] = None, splits: int = 32
+           ) -> Tuple[Optional[torch.Tensor], torch.Tensor]:
+    if x.dim() == 2:
+        x = x.unsqueeze(0)
+        y = y.unsqueeze(0) if y is not None else None
+    assert x.dim() == 3 and x.stride(-1) == 1
+    from . import use_hip
+    if not use_hip(x):
+        xf = x.float()
+        sxy = (xf * y.float()).sum((0, 1)) if y is not None else None
+        return sxy, xf.sum((0, 1))
+    from ..utils import native
+    lib = native.require_hip()
+    R1, R2, C = x.shape
+    if y is not None:
+        assert y.dtype == torch.float32 and y.shape == x.shape and y.stride() == x.stride()
+    RS = max(1, min(splits, (R1 * R2) // 64))
+    part = torch.empty(2, RS, C, device=x.device, dtype=torch.float32)
+    kind = 1 if x.dtype == torch.bfloat16 else 2
+    assert x.dtype in (torch.bfloat16, torch.float32)
+    rc = lib.lib.skr_colsum(x.data_ptr(), kind, y.data_ptr() if y is not None else None, R1, x.stride(0), R2,
+                            x.stride(1), C, RS, part[0].data_ptr(), part[1].data_ptr(),
+                            torch.cuda.current_stream().cuda_stream)
+    if rc != 0:
+        raise RuntimeError("skr_colsum failed (%d)" % rc)
+    return (part[0].sum(0) if y is not None else None), part[1].sum(0)

@@ -347,3 +347,21 @@ def test_fp8_inference_decode_close_to_bf16(dec_model):
     finally:
         ops.set_compute_dtype("fp32")
         ops.set_backend("auto")
+
+
+@pytest.mark.parametrize("shape,xdt,with_y", [((250, 100, 512), torch.float32, True), ((3, 7, 300), torch.bfloat16, False),
+                                              ((250, 2, 100, 64), torch.float32, True)])
+def test_colsum_matches_torch(shape, xdt, with_y):
+    from sketch_rnn_amd.ops.reduce import colsum
+    torch.manual_seed(2)
+    x = torch.randn(*shape, device=DEV).to(xdt)
+    y = torch.randn(*shape, device=DEV) if with_y else None
+    if len(shape) == 4:   # per-group reduction over a [T, nd, B, C] view
+        xv, yv = x[:, 1], y[:, 1]
+    else:
+        xv, yv = x, y
+    sxy, sx = colsum(xv, yv)
+    ref_x = xv.float().sum((0, 1))
+    assert torch.allclose(sx, ref_x, rtol=1e-4, atol=1e-3)
+    if with_y:
+        assert torch.allclose(sxy, (xv.float() * yv).sum((0, 1)), rtol=1e-4, atol=1e-3)
