@@ -121,6 +121,8 @@ def load_checkpoint(path: str, model: torch.nn.Module, optimizer=None, strict: b
         for k, v in own.items():
             if k in sd:
                 v.copy_(sd[k].to(v.dtype))
+    from ..ops import gemm
+    gemm.invalidate_derived()
     if optimizer is not None and "optim/m" in t:
         osd = {k[len("optim/"):]: v.to(optimizer.m.device) for k, v in t.items() if k.startswith("optim/")}
         osd["step_count"] = int(meta.get("optim_step_count", "0"))

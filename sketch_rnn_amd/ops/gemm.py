@@ -114,14 +114,23 @@ def rec_gemm(a: torch.Tensor, bt: torch.Tensor, out: torch.Tensor, splits: int, 
 
 # ---- inference-time helpers ------------------------------------------------------------
 _WCACHE = {}
+WEIGHTS_EPOCH = [0]
+
+
+def invalidate_derived() -> None:
+    """Drop cached inference weight copies. Called by every code path that
+    changes parameters without bumping their version counters -- optimizer
+    steps replayed from a HIP graph, checkpoint loads."""
+    _WCACHE.clear()
+    WEIGHTS_EPOCH[0] += 1
 
 
 def derived(W, tag: str, fn):
     """``fn(W)`` cached while ``W`` (a tensor or a tuple of tensors) is
     unchanged (same storage and version): for inference, so per-call weight
     casts / transposes / quantisation run once instead of at every decode
-    step. Never use it inside a captured training step (in-graph updates do
-    not bump the version counter)."""
+    step. Parameter updates replayed from a HIP graph do not bump version
+    counters: the trainers call :func:`invalidate_derived` every step."""
     ws = W if isinstance(W, tuple) else (W,)
     key = (tag,) + tuple((w.data_ptr(), w._version, tuple(w.shape), w.dtype) for w in ws)
     v = _WCACHE.get(key)
@@ -217,5 +226,11 @@ def linear(x: torch.Tensor, W: torch.Tensor, b: Optional[torch.Tensor] = None) -
         y = x.reshape(-1, x.shape[-1]) @ W
         if b is not None:
             y = y + b
+        return y.view(*x.shape[:-1], W.shape[1])
+    if not (torch.is_grad_enabled() and (x.requires_grad or W.requires_grad)):
+        # inference: the low-precision weight copy is made once, not per call
+        y = mm(lp(x.reshape(-1, x.shape[-1])), derived(W, "lp%s" % lp_dtype(), lp))
+        if b is not None:
+            y.add_(b)
         return y.view(*x.shape[:-1], W.shape[1])
     return _Linear.apply(x, W, b)

@@ -79,6 +79,14 @@ def _fp8_ok(M: int, *nk) -> bool:
     return all(gemm.plan_splits_fp8(M, n, k) > 0 for n, k in zip(nk[::2], nk[1::2]))
 
 
+def _inference(*ts) -> bool:
+    """True when no backward will run (grad mode off or nothing requires
+    grad): weights are then static, so derived copies are cached and fp8
+    GEMMs are allowed. Evaluated outside the autograd Function, whose
+    forward always runs with grad mode off."""
+    return not (torch.is_grad_enabled() and any(t is not None and t.requires_grad for t in ts))
+
+
 def _to_fp8_act(h: torch.Tensor) -> torch.Tensor:
     return (h.float() * gemm.FP8_ACT_SCALE).to(torch.float8_e4m3fn).view(torch.uint8)
 
@@ -156,7 +164,7 @@ class _ClusterSync:
 class _LSTMSeq(torch.autograd.Function):
     @staticmethod
     def forward(ctx, xp, W_h, h0, c0, reset_h, reset_c, ln_g, ln_b, lnc_g, lnc_b, reset, seed, meta):
-        forget_bias, keep, stream, nd = meta
+        forget_bias, keep, stream, nd, infer = meta   # infer: no autograd graph is being built
         lib = native.require_hip()
         T, BB, G = xp.shape
         H = G // 4
@@ -165,7 +173,6 @@ class _LSTMSeq(torch.autograd.Function):
         ln = ln_g is not None
         xp = xp.contiguous()
         Bg = BB // nd
-        infer = not any(ctx.needs_input_grad)   # sampling / eval: weights are static, no backward
         fp8 = infer and _fp8_ok(Bg, G, H) and nd == 1
         ldt = gemm.lp_dtype()
         if infer:
@@ -240,7 +247,7 @@ class _LSTMSeq(torch.autograd.Function):
         s = ctx.s
         T, BB, H = ctx.dims
         G = 4 * H
-        forget_bias, keep, stream, nd = s.meta
+        forget_bias, keep, stream, nd, _ = s.meta
         B = BB // nd
         lib = native.require_hip()
         dev = s.A.device
@@ -309,7 +316,8 @@ def lstm_sequence_hip(xp, W_h, h0, c0, forget_bias=1.0, reset=None, reset_h=None
     if reset is not None and reset_h is None:
         raise ValueError("reset requires reset_h / reset_c")
     Hout, hT, cT = _LSTMSeq.apply(xp, W_h, h0, c0, reset_h, reset_c, *ln, reset, drop_seed,
-                                  (float(forget_bias), float(drop_keep), int(drop_stream), 1))
+                                  (float(forget_bias), float(drop_keep), int(drop_stream), 1,
+                                   _inference(xp, W_h, h0, c0)))
     return Hout, (hT, cT)
 
 
@@ -328,7 +336,8 @@ def bilstm_sequence_hip(xp_f, xp_b, W_f, W_b, h0, c0, drop_keep=1.0, drop_seed=0
     else:
         ln = (None, None, None, None)
     Hout, hT, cT = _LSTMSeq.apply(xp, W, h, c, None, None, *ln, None, drop_seed,
-                                  (float(forget_bias), float(drop_keep), int(streams[0]), 2))
+                                  (float(forget_bias), float(drop_keep), int(streams[0]), 2,
+                                   _inference(xp, W, h, c)))
     return Hout[:, :B], Hout[:, B:]
 
 
@@ -381,7 +390,7 @@ class _HyperSeq(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, h0, c0, hh0, hc0, seed, W_x, W_h, bias, hW_x, hW_h, hln_g, hln_b, hlnc_g, hlnc_b,
                 W_z, b_z, W_a, ln_g, ln_b, lnc_g, lnc_b, meta):
-        forget_bias, keep, hkeep, stream, E = meta
+        forget_bias, keep, hkeep, stream, E, infer = meta   # infer: no autograd graph is being built
         lib = native.require_hip()
         T, B, IN = x.shape
         H, Hh = W_h.shape[0], hW_h.shape[0]
@@ -392,10 +401,14 @@ class _HyperSeq(torch.autograd.Function):
         TB = T * B
         x2 = x.reshape(TB, IN).contiguous()
         xl = gemm.lp(x2)
-        XH = gemm.mm(xl, gemm.lp(W_x)).view(T, B, G)
-        XHY = gemm.mm(xl, gemm.lp(hW_x[:IN])).view(T, B, Gh)
+        if infer:
+            XH = gemm.mm(xl, gemm.derived(W_x, "lp%s" % gemm.lp_dtype(), gemm.lp)).view(T, B, G)
+            XHY = gemm.mm(xl, gemm.derived(hW_x, "lpx%d%s" % (IN, gemm.lp_dtype()),
+                                           lambda W: gemm.lp(W[:IN]).contiguous())).view(T, B, Gh)
+        else:
+            XH = gemm.mm(xl, gemm.lp(W_x)).view(T, B, G)
+            XHY = gemm.mm(xl, gemm.lp(hW_x[:IN])).view(T, B, Gh)
         dt = gemm.lp_dtype()
-        infer = not any(ctx.needs_input_grad)   # sampling / eval: weights are static, no backward
 
         def wy(hW_x, hW_h):                      # [K, Gh]: B^T of dR_hyp @ W_y^T
             return torch.cat([hW_x[IN:], hW_h], 0).to(dt).contiguous()
@@ -518,7 +531,7 @@ class _HyperSeq(torch.autograd.Function):
     def backward(ctx, dHout, dhT, dcT, dhhT, dhcT):
         s = ctx.s
         T, B, IN, H, Hh, E = ctx.dims
-        forget_bias, keep, hkeep, stream, _ = s.meta
+        forget_bias, keep, hkeep, stream, _, _ = s.meta
         lib = native.require_hip()
         dev = s.A.device
         f32 = torch.float32
@@ -639,6 +652,7 @@ def hyper_sequence_hip(p, x, h0, c0, hh0, hc0, forget_bias=1.0, drop_keep=1.0, d
     outs = _HyperSeq.apply(x, h0, c0, hh0, hc0, drop_seed, p.W_x, p.W_h, p.bias, p.hyp_W_x, p.hyp_W_h,
                            p.hyp_ln_gamma, p.hyp_ln_beta, p.hyp_lnc_gamma, p.hyp_lnc_beta, p.W_z, p.b_z, p.W_a,
                            p.ln_gamma, p.ln_beta, p.lnc_gamma, p.lnc_beta,
-                           (float(forget_bias), float(drop_keep), float(hyp_drop_keep), int(drop_stream), p.embed))
+                           (float(forget_bias), float(drop_keep), float(hyp_drop_keep), int(drop_stream), p.embed,
+                            _inference(x, h0, p.W_h, p.W_x)))
     Hout, hT, cT, hhT, hcT = outs
     return Hout, (hT, cT, hhT, hcT)

@@ -285,7 +285,8 @@ class GraphDecoder:
         self.seed.fill_(int(seed))
         if self.use_graph:
             # the graph holds inference-cached weight copies (bf16 / fp8): re-capture after a weight update
-            sig = tuple(p._version for p in self.model.parameters())
+            from ..ops import gemm
+            sig = (gemm.WEIGHTS_EPOCH[0],) + tuple(p._version for p in self.model.parameters())
             if self.graph is not None and sig != self._sig:
                 self.graph = None
             self._sig = sig

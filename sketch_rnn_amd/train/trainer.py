@@ -26,6 +26,7 @@ from ..ckpt import checkpoint as ckpt
 from ..config import RefConfig, VAEConfig
 from ..models.reference import SketchRNN
 from ..models.vae import SketchVAE
+from ..ops import gemm
 from ..parallel import dp
 from ..utils.trace import GpuPhaseTimer, PhaseTimes, phase
 from . import schedules
@@ -91,6 +92,7 @@ class ReferenceTrainer:
         return list(flat)
 
     def train_step(self, x: torch.Tensor, y: torch.Tensor) -> Dict[str, torch.Tensor]:
+        gemm.invalidate_derived()   # weights change in place (possibly inside a graph replay)
         state_flat = self._flatten(self.state)
         if self.use_graph:
             if self._graph is None:
@@ -232,6 +234,7 @@ class VAETrainer:
         """One optimisation step. On the GPU the forward+backward is one
         captured HIP graph; with DP the bucketed RCCL all-reduce runs between
         it and a second graph holding the fused clip+Adam update."""
+        gemm.invalidate_derived()   # weights change in place (possibly inside a graph replay)
         self.opt.set_lr(schedules.vae_lr(self.cfg, self.step))
         self.kl_w.fill_(schedules.kl_weight(self.cfg, self.step))
         if self.use_graph:

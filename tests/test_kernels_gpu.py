@@ -365,3 +365,27 @@ def test_colsum_matches_torch(shape, xdt, with_y):
     assert torch.allclose(sx, ref_x, rtol=1e-4, atol=1e-3)
     if with_y:
         assert torch.allclose(sxy, (xv.float() * yv).sum((0, 1)), rtol=1e-4, atol=1e-3)
+
+
+def test_inference_weight_cache_tracks_graph_training():
+    """Inference paths cache low-precision weight copies; parameters updated by
+    HIP-graph replays (no version bump) must invalidate them."""
+    from sketch_rnn_amd.cli.vae_train import make_datasets
+    from sketch_rnn_amd.config import VAEConfig
+    from sketch_rnn_amd.train.trainer import VAETrainer
+    cfg = VAEConfig(enc_rnn_size=64, dec_rnn_size=256, z_size=16, num_mixture=5, max_seq_len=40, batch_size=16,
+                    dec_model="hyper", hyper_num_units=64, hyper_embedding_size=8, save_every=0)
+    (tr_set, va, te), _ = make_datasets(cfg, None, 200)
+    tr = VAETrainer(cfg, tr_set, va, te, device=DEV, save_dir="/tmp/skr_cache_test", log=lambda s: None,
+                    compute_dtype="bf16", use_graph=True)
+    e0 = tr.evaluate(te, max_batches=2)
+    for _ in range(3):
+        tr.train_step(*tr.batch_to_device(tr_set.random_batch()))
+    e1 = tr.evaluate(te, max_batches=2)
+    ops.set_backend("torch")
+    try:
+        e_ref = tr.evaluate(te, max_batches=2)   # oracle path: no caches at all
+    finally:
+        ops.set_backend("auto")
+    assert e1["cost"] != e0["cost"]
+    assert abs(e1["cost"] - e_ref["cost"]) < 0.05 * abs(e_ref["cost"]) + 0.02, (e1, e_ref)
