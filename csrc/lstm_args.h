@@ -62,7 +62,7 @@ struct BwdArgs {
     float keep; const int64_t* seed; uint32_t stream, step;
     float* dG; int64_t ld_dG;          // non-MOD: d(preact) [B, 4H]; MOD: dR = dg*ah
     void* dG_lp; int64_t ld_dG_lp; int dG_lp_kind;  // bf16 copy of dG for the next GEMM (1) or none (0)
-    float* dxp; int64_t ld_dxp;        // MOD: dxh = dg*ax
+    void* dxp; int64_t ld_dxp; int dxp_kind;  // MOD: dxh = dg*ax (1 bf16, 2 fp32)
     void* dvec; int dvec_kind;         // MOD: same layout as vec; 1 bf16, 2 fp32
     float* dlny;                       // LN: [B, 4H] grad wrt LN-all output (for gamma/beta)
     float* dlncy;                      // LN: [B, H]  grad wrt LN(c) output

@@ -448,7 +448,8 @@ __global__ __launch_bounds__(NT) void cell_bwd(const BwdArgs a) {
             const float dg = dy[k][q];
             float dr = dg;
             if (MOD) {
-                a.dxp[b * a.ld_dxp + q * H + u] = dg * ax[k][q];
+                if (a.dxp_kind == 1) ((__hip_bfloat16*)a.dxp)[b * a.ld_dxp + q * H + u] = to_bf16(dg * ax[k][q]);
+                else ((float*)a.dxp)[b * a.ld_dxp + q * H + u] = dg * ax[k][q];
                 dr = dg * ah[k][q];
                 const int64_t o0 = (int64_t)b * a.vec_ld + u;
                 const float d3[3] = {dg * xv[k][q], dg * rv[k][q], dg};

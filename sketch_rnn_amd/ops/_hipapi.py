@@ -62,7 +62,7 @@ class LstmBwdArgs(C.Structure):
         ("keep", _f), ("seed", _p), ("stream", _u32), ("step", _u32),
         ("dG", _p), ("ld_dG", _i64),
         ("dG_lp", _p), ("ld_dG_lp", _i64), ("dG_lp_kind", _i),
-        ("dxp", _p), ("ld_dxp", _i64),
+        ("dxp", _p), ("ld_dxp", _i64), ("dxp_kind", _i),
         ("dvec", _p), ("dvec_kind", _i),
         ("dlny", _p), ("dlncy", _p),
         ("dinit_h", _p), ("dinit_c", _p),

@@ -544,7 +544,7 @@ class _HyperSeq(torch.autograd.Function):
         dRY = torch.empty(T, B, Gh, device=dev, dtype=f32)
         dRM_lp = torch.empty(T, B, G, device=dev, dtype=ldt) if lp_on else dRM
         dRY_lp = torch.empty(T, B, Gh, device=dev, dtype=ldt) if lp_on else dRY
-        dXH = torch.empty(T, B, G, device=dev, dtype=f32)
+        dXH = torch.empty(T, B, G, device=dev, dtype=ldt)   # only a GEMM operand downstream
         DLNY = torch.empty(T, B, G, device=dev, dtype=f32)
         DLNCY = torch.empty(T, B, H, device=dev, dtype=f32)
         HDLNY = torch.empty(T, B, Gh, device=dev, dtype=f32)
@@ -574,7 +574,7 @@ class _HyperSeq(torch.autograd.Function):
         am.vec_gs, am.vec_ld, am.vec_bias = H, 12 * H, s.q.data_ptr()
         am.keep, am.seed, am.stream = float(keep), s.seed.data_ptr(), int(stream)
         am.ld_dG, am.ld_dG_lp, am.dG_lp_kind = G, G, 1 if lp_on else 0
-        am.ld_dxp, am.dvec_kind = G, 1 if lp_on else 2
+        am.ld_dxp, am.dxp_kind, am.dvec_kind = G, 1 if lp_on else 2, 1 if lp_on else 2
         ah = LstmBwdArgs()
         ah.B, ah.H = B, Hh
         ah.dh_out, ah.dho_nslab, ah.dho_slab = DHZ.data_ptr(), max(S_h, 1), B * Hh
@@ -621,7 +621,7 @@ class _HyperSeq(torch.autograd.Function):
         dhW_x = torch.empty_like(s.hW_x)
         dhW_x[IN:] = dW_y[:H]
         dhW_h = dW_y[H:]
-        dXHl, dXHYl = gemm.lp(dXH.view(TB, G)), gemm.lp(dRY.view(TB, Gh))
+        dXHl, dXHYl = gemm.lp(dXH.view(TB, G)), gemm.lp(dRY_lp.view(TB, Gh))
         dW_x = gemm.mm(s.xl.t(), dXHl)
         dhW_x[:IN] = gemm.mm(s.xl.t(), dXHYl)
         dx = gemm.mm(dXHl, gemm.lp(s.W_x).t())
