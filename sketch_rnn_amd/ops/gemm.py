@@ -133,11 +133,15 @@ def derived(W, tag: str, fn):
     counters: the trainers call :func:`invalidate_derived` every step."""
     ws = W if isinstance(W, tuple) else (W,)
     key = (tag,) + tuple((w.data_ptr(), w._version, tuple(w.shape), w.dtype) for w in ws)
-    v = _WCACHE.get(key)
-    if v is None:
-        if len(_WCACHE) > 512:
-            _WCACHE.clear()
-        v = _WCACHE[key] = fn(*ws)
+    hit = _WCACHE.get(key)
+    # the entry holds its source tensors: a freed-and-reallocated tensor at the
+    # same address (fresh version counter) is a different object -> miss
+    if hit is not None and all(a is b for a, b in zip(hit[0], ws)):
+        return hit[1]
+    if len(_WCACHE) > 512:
+        _WCACHE.clear()
+    v = fn(*ws)
+    _WCACHE[key] = (ws, v)
     return v
 
 

@@ -175,10 +175,9 @@ class _LSTMSeq(torch.autograd.Function):
         Bg = BB // nd
         fp8 = infer and _fp8_ok(Bg, G, H) and nd == 1
         ldt = gemm.lp_dtype()
-        if infer:
+        if infer and nd == 1:   # (nd > 1: W_h is a per-call stack of the directions -- nothing to cache)
             Wl = None
-            WlT = gemm.derived(W_h, "lstmT%s%d" % (ldt, nd),
-                               lambda W: gemm.lp(W.reshape(nd, H, G)).transpose(1, 2).contiguous())
+            WlT = gemm.derived(W_h, "lstmT%s" % ldt, lambda W: gemm.lp(W).t().contiguous())
         else:
             Wl = gemm.lp(W_h.reshape(nd, H, G)).contiguous()   # B^T of the backward product dG @ W^T
             WlT = Wl.transpose(1, 2).contiguous()              # B^T of the forward product h @ W
