@@ -38,6 +38,8 @@ def main():
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-eval", action="store_true")
     ap.add_argument("--sketches", type=int, default=2000)
+    ap.add_argument("--dist-backend", default=None, help="override (default: nccl = RCCL on GPUs); "
+                    "'gloo' rehearses the multi-rank path with several ranks on one GPU")
     args = ap.parse_args()
 
     import torch
@@ -50,11 +52,12 @@ def main():
 
     world_env = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    device = "cuda:%d" % local_rank if torch.cuda.is_available() else "cpu"
+    ndev = torch.cuda.device_count()
+    device = "cuda:%d" % (local_rank % max(ndev, 1)) if torch.cuda.is_available() else "cpu"
     if device.startswith("cuda"):
-        torch.cuda.set_device(local_rank)
+        torch.cuda.set_device(torch.device(device))
     if world_env > 1:
-        dp.init_from_env(device=device)
+        dp.init_from_env(backend=args.dist_backend, device=device)
     world, rank = dp.world_size(), dp.rank()
     ops.set_backend(args.backend)
 

@@ -10,8 +10,7 @@ Design for MI355X / xGMI:
   gradients becomes 4 ring all-reduces -- large enough to be link-bandwidth
   bound on the 7 xGMI links, small enough that the first bucket's
   reduction overlaps the remaining backward when issued from a hook;
-* the average (1/world) is folded into the all-reduce via ``PREMUL_SUM``
-  when available, otherwise a single in-place scale of the arena;
+* the average (1/world) is one in-place scale of the arena after the sums;
 * scalars for logging (recon / KL / pen) are averaged with one all-reduce;
   schedules (lr, KL weight) are pure functions of the step and need none;
 * :func:`broadcast_params` makes rank 0's initial weights authoritative.
@@ -52,6 +51,8 @@ def init_from_env(backend: Optional[str] = None, device: Optional[str] = None) -
         lr = int(os.environ.get("LOCAL_RANK", "0"))
         torch.cuda.set_device(lr)
         kw["device_id"] = torch.device("cuda", lr)
+    elif device is not None and device.startswith("cuda"):
+        torch.cuda.set_device(torch.device(device))
     dist.init_process_group(backend=backend, **kw)
     return True
 
@@ -79,22 +80,15 @@ class GradReducer:
         per = (per + 63) // 64 * 64
         self.buckets: List[torch.Tensor] = [grad[i:i + per] for i in range(0, n, per)]
         self.world = world_size()
-        self._premul = None
-        if is_dist() and dist.get_backend() == "nccl" and hasattr(dist, "_make_nccl_premul_sum"):
-            try:
-                self._premul = dist._make_nccl_premul_sum(1.0 / self.world)
-            except Exception:
-                self._premul = None
 
     def all_reduce(self, async_op: bool = False):
+        """Sum every bucket across ranks (all in flight at once), then one
+        in-place 1/world scale of the arena. Plain SUM is used rather than a
+        pre-multiplied sum so the call pattern is the same on every RCCL
+        version."""
         if self.world <= 1:
             return []
-        works = []
-        for b in self.buckets:
-            if self._premul is not None:
-                works.append(dist.all_reduce(b, op=self._premul, async_op=True))
-            else:
-                works.append(dist.all_reduce(b, op=dist.ReduceOp.SUM, async_op=True))
+        works = [dist.all_reduce(b, op=dist.ReduceOp.SUM, async_op=True) for b in self.buckets]
         if async_op:
             return works
         self.wait(works)
@@ -104,7 +98,7 @@ class GradReducer:
         """Complete an ``all_reduce(async_op=True)`` (and apply 1/world)."""
         for w in works:
             w.wait()
-        if self.world > 1 and self._premul is None:
+        if self.world > 1:
             self.grad.mul_(1.0 / self.world)
 
 
