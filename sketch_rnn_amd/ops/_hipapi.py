@@ -107,6 +107,24 @@ class GruBwdArgs(C.Structure):
     ]
 
 
+class FusedFwdArgs(C.Structure):
+    """Mirror of ``FusedFwdArgs`` in csrc/lstm_fused.hip."""
+    _fields_ = [
+        ("B", _i), ("H", _i), ("nd", _i),
+        ("A", _p), ("lda", _i64),
+        ("WT", _p), ("w_gs", _i64),
+        ("xp", _p), ("ld_xp", _i64),
+        ("c_prev", _p),
+        ("reset", _p),
+        ("init_h", _p), ("init_c", _p),
+        ("forget_bias", _f), ("keep", _f),
+        ("seed", _p), ("stream", _u32), ("step", _u32),
+        ("h_out", _p), ("c_out", _p), ("act", _p),
+        ("h_carry", _p), ("c_carry", _p),
+        ("h_next", _p), ("ld_next", _i64),
+    ]
+
+
 class HipLib:
     def __init__(self, lib: C.CDLL):
         self.lib = lib
@@ -133,8 +151,11 @@ class HipLib:
         lib.skr_gru_fwd.restype = _i
         lib.skr_gru_bwd.argtypes = [C.POINTER(GruBwdArgs), _i, _p]
         lib.skr_gru_bwd.restype = _i
+        lib.skr_lstm_fused_fwd.argtypes = [C.POINTER(FusedFwdArgs), _p]
+        lib.skr_lstm_fused_fwd.restype = _i
         for name, cls in (("skr_lstm_fwd_args_size", LstmFwdArgs), ("skr_lstm_bwd_args_size", LstmBwdArgs),
-                          ("skr_gru_fwd_args_size", GruFwdArgs), ("skr_gru_bwd_args_size", GruBwdArgs)):
+                          ("skr_gru_fwd_args_size", GruFwdArgs), ("skr_gru_bwd_args_size", GruBwdArgs),
+                          ("skr_lstm_fused_fwd_args_size", FusedFwdArgs)):
             fn = getattr(lib, name)
             fn.restype = _i
             if fn() != C.sizeof(cls):

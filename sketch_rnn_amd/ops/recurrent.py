@@ -31,7 +31,7 @@ import torch
 
 from ..utils import native
 from . import gemm
-from ._hipapi import LstmBwdArgs, LstmFwdArgs
+from ._hipapi import FusedFwdArgs, LstmBwdArgs, LstmFwdArgs
 from .reduce import colsum
 
 
@@ -158,6 +158,16 @@ class _ClusterSync:
             args.part, args.err = None, None
 
 
+# ---- fused GEMM + cell forward step (csrc/lstm_fused.hip) ---------------------------
+# Plain LSTM (no LayerNorm) layers with H in {256, 512} and bf16 operands run
+# each forward step as ONE launch. SKR_FUSED=0 keeps the GEMM + cell pair.
+FUSED_ENABLED = os.environ.get("SKR_FUSED", "1") != "0"
+
+
+def _fused_ok(H: int, ln: bool, fp8: bool, ldt) -> bool:
+    return FUSED_ENABLED and not ln and not fp8 and ldt == torch.bfloat16 and H in (256, 512)
+
+
 # =====================================================================================
 # LSTM / LayerNorm-LSTM sequence (nd groups)
 # =====================================================================================
@@ -212,9 +222,27 @@ class _LSTMSeq(torch.autograd.Function):
         a.seed, a.stream = sd.data_ptr(), int(stream)
         a.ld_lp, a.lp_kind = H, _lp_kind(A)
         a.R, a.R_nslab, a.R_slab = R.data_ptr(), max(S, 1), BB * G
-        cl = _ClusterSync(T, BB, H, dev, ln)
         st = _stream()
-        for t in range(T):
+        if _fused_ok(H, ln, fp8, ldt):
+            f = FusedFwdArgs()
+            f.B, f.H, f.nd = Bg, H, nd
+            f.lda, f.ld_xp, f.ld_next = H, G, H
+            f.WT, f.w_gs = WlT.data_ptr(), (G * H if nd > 1 else 0)
+            f.init_h, f.init_c = _ptr(rh), _ptr(rc)
+            f.forget_bias, f.keep = float(forget_bias), float(keep)
+            f.seed, f.stream = sd.data_ptr(), int(stream)
+            for t in range(T):
+                f.A, f.xp, f.c_prev = A[t].data_ptr(), xp[t].data_ptr(), CC[t].data_ptr()
+                f.reset = _ptr(rst[t]) if rst is not None else None
+                f.step = t
+                f.h_out, f.c_out, f.act = Hout[t].data_ptr(), Cout[t].data_ptr(), ACT[t].data_ptr()
+                f.h_carry, f.c_carry, f.h_next = HC[t % 2].data_ptr(), CC[t + 1].data_ptr(), A[t + 1].data_ptr()
+                _check(lib.lib.skr_lstm_fused_fwd(ctypes.byref(f), st), "lstm_fused_fwd")
+            T_loop = 0
+        else:
+            T_loop = T
+        cl = _ClusterSync(T, BB, H, dev, ln)
+        for t in range(T_loop):
             cl.set(a, t)
             if fp8:
                 gemm.rec_gemm_fp8(A[t], WQ, R, S)

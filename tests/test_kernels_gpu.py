@@ -142,6 +142,51 @@ def test_lstm_sequence_bf16_close():
     _close(g_h, g_t, 5e-2, 5e-2, "grad")
 
 
+@pytest.mark.parametrize("H,nd,B,reset,keep", [(512, 2, 100, False, 0.9), (256, 1, 37, True, 0.8),
+                                               (512, 1, 70, True, 1.0), (256, 2, 5, False, 1.0)])
+def test_fused_lstm_step_matches_unfused(H, nd, B, reset, keep):
+    """csrc/lstm_fused.hip (GEMM + cell in one launch, bf16 operands) vs the
+    split GEMM + cell path and the fp32 oracle."""
+    from sketch_rnn_amd.ops import recurrent
+    torch.manual_seed(2)
+    T = 8
+    xs = [torch.randn(T, B, 4 * H, device=DEV, requires_grad=True) for _ in range(nd)]
+    Ws = [(torch.randn(H, 4 * H, device=DEV) / math.sqrt(H)).requires_grad_() for _ in range(nd)]
+    h0 = (torch.randn(B, H, device=DEV) * 0.5).requires_grad_()
+    c0 = (torch.randn(B, H, device=DEV) * 0.5).requires_grad_()
+    rst = (torch.rand(T, B, device=DEV) < 0.3).float() if reset else None
+    seed = torch.tensor([23], device=DEV)
+
+    if nd == 1:
+        def fn(xp, W, h0, c0):
+            out, (hT, cT) = ops.lstm_sequence(xp, W, h0, c0, reset=rst, reset_h=h0 if reset else None,
+                                              reset_c=c0 if reset else None, drop_keep=keep, drop_seed=seed,
+                                              drop_stream=5)
+            return [out, hT, cT]
+        inputs = xs + Ws + [h0, c0]
+    else:
+        def fn(xf, xb, Wf, Wb):
+            return list(ops.bilstm_sequence(xf, xb, Wf, Wb, torch.zeros(B, H, device=DEV),
+                                            torch.zeros(B, H, device=DEV), drop_keep=keep, drop_seed=seed,
+                                            drop_stream=11))
+        inputs = xs + Ws
+    saved = recurrent.FUSED_ENABLED
+    try:
+        ops.set_compute_dtype("bf16")
+        recurrent.FUSED_ENABLED = True
+        o_f, g_f = _run("hip", fn, inputs)
+        recurrent.FUSED_ENABLED = False
+        o_u, g_u = _run("hip", fn, inputs)
+    finally:
+        recurrent.FUSED_ENABLED = saved
+    ops.set_compute_dtype("fp32")
+    o_t, g_t = _run("torch", fn, inputs)
+    _close(o_f, o_u, 1e-2, 1e-2, "fused vs unfused out")
+    _close(g_f, g_u, 2e-2, 2e-2, "fused vs unfused grad")
+    _close(o_f, o_t, 3e-2, 3e-2, "fused vs oracle out")
+    _close(g_f, g_t, 5e-2, 5e-2, "fused vs oracle grad")
+
+
 @pytest.mark.parametrize("H,Hh,E,keep", [(64, 32, 4, 1.0), (256, 64, 8, 0.9), (2048, 256, 32, 1.0)])
 def test_hyper_sequence_matches_oracle(H, Hh, E, keep):
     torch.manual_seed(2)
