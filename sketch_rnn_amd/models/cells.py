@@ -70,6 +70,16 @@ def hash_uniform(seed, stream: int, step: int, shape, device=None) -> torch.Tens
     return ((h >> 8).to(torch.float32) * (1.0 / 16777216.0)).view(*shape)
 
 
+def hash_normal(seed, stream: int, step: int, shape, device=None) -> torch.Tensor:
+    """N(0, 1) per element (Box-Muller over two hash_uniform streams): the
+    VAE's reparameterisation noise, a pure function of (seed, stream, step)
+    like the dropout masks -- independent of any process-global RNG state,
+    so a step replays identically (HIP graphs, resume, two fresh runs)."""
+    u1 = 1.0 - hash_uniform(seed, stream, step, shape, device)        # (0, 1]
+    u2 = hash_uniform(seed, stream + 0x3C6EF372, step, shape, device)
+    return torch.sqrt(-2.0 * torch.log(u1)) * torch.cos((2.0 * math.pi) * u2)
+
+
 def dropout_mask(seed: int, stream: int, step: int, shape, keep: float, device=None) -> torch.Tensor:
     """Inverted-dropout multiplier: ``1/keep`` where kept, else 0."""
     u = hash_uniform(seed, stream, step, shape, device)

@@ -29,7 +29,7 @@ from ..ops import gemm
 from . import cells as C
 
 # dropout hash streams
-_S_ENC_FW, _S_ENC_BW, _S_DEC, _S_IN, _S_OUT = 11, 13, 17, 23, 29
+_S_ENC_FW, _S_ENC_BW, _S_DEC, _S_IN, _S_OUT, _S_EPS = 11, 13, 17, 23, 29, 31
 
 
 def _gaussian(shape, std, gen):
@@ -196,7 +196,7 @@ class SketchVAE(nn.Module):
             mu, presig = self.encode(strokes, lengths, train, seed)
             sigma = torch.exp(presig / 2.0)
             if eps is None:
-                eps = torch.randn(B, cfg.z_size, device=dev)
+                eps = C.hash_normal(seed, _S_EPS, 0, (B, cfg.z_size), dev)
             z = mu + sigma * eps
             kl_raw = -0.5 * torch.mean(1 + presig - mu * mu - torch.exp(presig))
             kl = torch.clamp(kl_raw, min=cfg.kl_tolerance)

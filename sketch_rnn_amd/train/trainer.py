@@ -207,7 +207,9 @@ class VAETrainer:
         self.step = 0
         self.use_graph = (self.device.type == "cuda") if use_graph is None else use_graph
         self._graph = None
-        self.seed = torch.zeros(1, dtype=torch.int64, device=self.device)
+        # noise seed (dropout masks, reparameterisation eps): rank r uses
+        # r, r + world, r + 2*world, ... so ranks draw independent noise
+        self.seed = torch.full((1,), self.rank, dtype=torch.int64, device=self.device)
         self.kl_w = torch.zeros((), device=self.device)
         self.host_times = PhaseTimes()            # data / step / eval / save wall time
         self.gpu_times = GpuPhaseTimer(enabled=metrics_path is not None)
@@ -257,7 +259,7 @@ class VAETrainer:
         else:
             with self.gpu_times.time("step"):
                 out = self._step_fn(strokes, lengths, labels)
-        self.seed.add_(1)
+        self.seed.add_(self.world)
         self.step += 1
         return out
 
@@ -299,7 +301,7 @@ class VAETrainer:
         if path is None:
             return False
         self.step, extra, _ = ckpt.load_checkpoint(path, self.model, self.opt)
-        self.seed.fill_(int(extra.get("seed", self.step)))
+        self.seed.fill_(int(extra.get("seed", self.step * self.world)) + self.rank)   # saved by rank 0
         if "data" in extra and hasattr(self.train_set, "load_state_dict"):
             self.train_set.load_state_dict(extra["data"])
             if self.rank:

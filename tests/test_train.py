@@ -298,3 +298,18 @@ def test_vae_metrics_jsonl_and_phases(tmp_path):
     with phase("x", pt):
         pass
     assert pt.count["x"] == 1 and "x" in pt.mean_ms()
+
+
+def test_vae_training_reproducible_across_fresh_trainers(tmp_path):
+    """Noise (dropout, reparameterisation eps) is keyed by (seed, step), not a
+    process-global RNG: two fresh trainers in one process train identically."""
+    from sketch_rnn_amd.train.trainer import VAETrainer
+    cfg = VAEConfig(enc_rnn_size=16, dec_rnn_size=32, z_size=8, num_mixture=3, max_seq_len=30, batch_size=4,
+                    dec_model="lstm", save_every=0)
+    runs = []
+    for k in range(2):
+        (train, valid, test), _ = _vae_sets(cfg)
+        tr = VAETrainer(cfg, train, valid, test, save_dir=str(tmp_path / str(k)), log=lambda s: None)
+        runs.append([float(tr.train_step(*tr.batch_to_device(train.random_batch()))["cost"]) for _ in range(3)])
+        torch.randn(5)   # perturb the global RNG between runs
+    assert runs[0] == runs[1]
