@@ -41,6 +41,24 @@ struct FusedFwdArgs {
     __hip_bfloat16* h_next; int64_t ld_next;
 };
 
+// Backward step t: dh_rec = dG_{t+1} @ W_h^T (K = 4H) fused with the cell
+// backward of step t. Operands are read straight from L2 into MFMA fragments
+// (no LDS staging: K is split over the 4 waves and each wave streams only
+// its quarter); the 4 partial tiles are summed in LDS by the epilogue.
+struct FusedBwdArgs {
+    int B, H, nd;
+    const __hip_bfloat16* dG_next; int64_t ld_dgn;  // bf16 dG of step t+1 [nd*B, 4H], null at t = T-1
+    const __hip_bfloat16* W; int64_t w_gs;          // W_h per group [H, 4H], group stride w_gs
+    const float* dh_extra;                          // [nd*B, H] added to dh_rec (dh_T at t = T-1) or null
+    const float* dh_out;                            // [nd*B, H] or null
+    float* dc_rec;                                  // [nd*B, H] in: dc from step t+1, out: dc into step t-1
+    const float* act; const float* c_new; const float* c_prev;
+    const float* reset;
+    float keep; const int64_t* seed; uint32_t stream, step;
+    float* dG; __hip_bfloat16* dG_lp;               // [nd*B, 4H]
+    float* dinit_h; float* dinit_c;                 // [nd*B, H] accumulated on reset rows (or null)
+};
+
 namespace {
 
 using namespace skr;
@@ -150,6 +168,99 @@ __global__ __launch_bounds__(256) void lstm_fused_fwd(const FusedFwdArgs a) {
 }
 
 template <int H>
+__global__ __launch_bounds__(256) void lstm_fused_bwd(const FusedBwdArgs a) {
+    constexpr int K = 4 * H, KW = K / 4;   // K per wave
+    __shared__ float red[4][RB][UB + 1];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int grp = blockIdx.z, rb = blockIdx.y * RB, u0 = blockIdx.x * UB;
+    const int B = a.B;
+    const int64_t row0 = (int64_t)grp * B;
+    const bool keep_on = a.keep < 1.0f;
+    const uint32_t key = keep_on ? hash_key(*a.seed, a.stream, a.step) : 0u;
+
+    // ---- epilogue inputs first (2 (row, unit) pairs per thread)
+    float ac[2][4], cx[2], cp[2], dcc[2], dho[2], dhx[2];
+    int br[2], uu[2];
+    bool on[2], rs[2];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        const int p = tid + 256 * k, r = p / UB;
+        uu[k] = p % UB;
+        on[k] = rb + r < B;
+        br[k] = (int)row0 + min(rb + r, B - 1);
+        const int64_t ro = (int64_t)br[k] * H + u0 + uu[k];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) ac[k][q] = a.act[(int64_t)br[k] * K + q * H + u0 + uu[k]];
+        cx[k] = a.c_new[ro];
+        cp[k] = a.c_prev[ro];
+        dcc[k] = a.dc_rec[ro];
+        dho[k] = a.dh_out ? a.dh_out[ro] : 0.f;
+        dhx[k] = a.dh_extra ? a.dh_extra[ro] : 0.f;
+        rs[k] = a.reset != nullptr && a.reset[br[k]] != 0.f;
+    }
+
+    // ---- dh_rec tile [32 rows x 16 units], this wave's K quarter
+    const int fr = lane & 15, fq = lane >> 4;
+    f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+    if (a.dG_next != nullptr) {
+        const __hip_bfloat16* wp = a.W + grp * a.w_gs + (int64_t)(u0 + fr) * K + w * KW + fq * 8;
+        const __hip_bfloat16* ap0 = a.dG_next + (row0 + min(rb + fr, B - 1)) * a.ld_dgn + w * KW + fq * 8;
+        const __hip_bfloat16* ap1 = a.dG_next + (row0 + min(rb + 16 + fr, B - 1)) * a.ld_dgn + w * KW + fq * 8;
+#pragma unroll 8
+        for (int ks = 0; ks < KW / 32; ++ks) {
+            const bf16x8 bfr = *(const bf16x8*)(wp + ks * 32);
+            const bf16x8 a0 = *(const bf16x8*)(ap0 + ks * 32);
+            const bf16x8 a1 = *(const bf16x8*)(ap1 + ks * 32);
+            acc[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, bfr, acc[0], 0, 0, 0);
+            acc[1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, bfr, acc[1], 0, 0, 0);
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) red[w][16 * i + fq * 4 + e][fr] = acc[i][e];
+    __syncthreads();
+
+    // ---- cell backward (plain LSTM path of csrc/lstm_cell.hip cell_bwd)
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        if (!on[k]) continue;
+        const int p = tid + 256 * k, r = p / UB;
+        const int b = br[k], u = u0 + uu[k];
+        const int64_t ro = (int64_t)b * H + u;
+        const float dhc = red[0][r][uu[k]] + red[1][r][uu[k]] + red[2][r][uu[k]] + red[3][r][uu[k]] + dhx[k];
+        const float dh = dho[k] + (rs[k] ? 0.f : dhc);
+        float dc = rs[k] ? 0.f : dcc[k];
+        if (rs[k] && a.dinit_h) {
+            a.dinit_h[ro] += dhc;
+            a.dinit_c[ro] += dcc[k];
+        }
+        const float i = ac[k][0], tj = ac[k][1], f = ac[k][2], o = ac[k][3];
+        const float t = tanhf(cx[k]);
+        const float dout = dh * t;
+        dc += dh * o * (1.f - t * t);
+        const float m = dropout_mult(keep_on, key, ro, a.keep);
+        float dy[4];
+        dy[0] = dc * tj * m * i * (1.f - i);
+        dy[1] = dc * i * m * (1.f - tj * tj);
+        dy[2] = dc * cp[k] * f * (1.f - f);
+        dy[3] = dout * o * (1.f - o);
+        a.dc_rec[ro] = dc * f;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            a.dG[(int64_t)b * K + q * H + u] = dy[q];
+            a.dG_lp[(int64_t)b * K + q * H + u] = to_bf16(dy[q]);
+        }
+    }
+}
+
+template <int H>
+int launch_bwd(const FusedBwdArgs& a, hipStream_t s) {
+    hipLaunchKernelGGL(lstm_fused_bwd<H>, dim3(H / UB, (a.B + RB - 1) / RB, a.nd), dim3(256), 0, s, a);
+    return SKR_CHECK_LAUNCH();
+}
+
+template <int H>
 int launch(const FusedFwdArgs& a, hipStream_t s) {
     const size_t lds = (size_t)(RB + 4 * UB) * H * 2 + 4 * RB * UB * 4;
     static bool attr = false;
@@ -174,4 +285,15 @@ SKR_API int skr_lstm_fused_fwd(const FusedFwdArgs* a, hipStream_t s) {
     }
 }
 
+SKR_API int skr_lstm_fused_bwd(const FusedBwdArgs* a, hipStream_t s) {
+    if (a->B <= 0) return 0;
+    if ((a->dG_next && (a->ld_dgn % 8)) || (((uintptr_t)a->dG_next | (uintptr_t)a->W) & 15)) return -3;
+    switch (a->H) {
+        case 256: return launch_bwd<256>(*a, s);
+        case 512: return launch_bwd<512>(*a, s);
+        default: return -2;
+    }
+}
+
 SKR_API int skr_lstm_fused_fwd_args_size() { return (int)sizeof(FusedFwdArgs); }
+SKR_API int skr_lstm_fused_bwd_args_size() { return (int)sizeof(FusedBwdArgs); }

@@ -125,6 +125,23 @@ class FusedFwdArgs(C.Structure):
     ]
 
 
+class FusedBwdArgs(C.Structure):
+    """Mirror of ``FusedBwdArgs`` in csrc/lstm_fused.hip."""
+    _fields_ = [
+        ("B", _i), ("H", _i), ("nd", _i),
+        ("dG_next", _p), ("ld_dgn", _i64),
+        ("W", _p), ("w_gs", _i64),
+        ("dh_extra", _p),
+        ("dh_out", _p),
+        ("dc_rec", _p),
+        ("act", _p), ("c_new", _p), ("c_prev", _p),
+        ("reset", _p),
+        ("keep", _f), ("seed", _p), ("stream", _u32), ("step", _u32),
+        ("dG", _p), ("dG_lp", _p),
+        ("dinit_h", _p), ("dinit_c", _p),
+    ]
+
+
 class HipLib:
     def __init__(self, lib: C.CDLL):
         self.lib = lib
@@ -153,9 +170,12 @@ class HipLib:
         lib.skr_gru_bwd.restype = _i
         lib.skr_lstm_fused_fwd.argtypes = [C.POINTER(FusedFwdArgs), _p]
         lib.skr_lstm_fused_fwd.restype = _i
+        lib.skr_lstm_fused_bwd.argtypes = [C.POINTER(FusedBwdArgs), _p]
+        lib.skr_lstm_fused_bwd.restype = _i
         for name, cls in (("skr_lstm_fwd_args_size", LstmFwdArgs), ("skr_lstm_bwd_args_size", LstmBwdArgs),
                           ("skr_gru_fwd_args_size", GruFwdArgs), ("skr_gru_bwd_args_size", GruBwdArgs),
-                          ("skr_lstm_fused_fwd_args_size", FusedFwdArgs)):
+                          ("skr_lstm_fused_fwd_args_size", FusedFwdArgs),
+                          ("skr_lstm_fused_bwd_args_size", FusedBwdArgs)):
             fn = getattr(lib, name)
             fn.restype = _i
             if fn() != C.sizeof(cls):

@@ -31,7 +31,7 @@ import torch
 
 from ..utils import native
 from . import gemm
-from ._hipapi import FusedFwdArgs, LstmBwdArgs, LstmFwdArgs
+from ._hipapi import FusedBwdArgs, FusedFwdArgs, LstmBwdArgs, LstmFwdArgs
 from .reduce import colsum
 
 
@@ -302,9 +302,32 @@ class _LSTMSeq(torch.autograd.Function):
         a.keep, a.seed, a.stream = float(keep), s.seed.data_ptr(), int(stream)
         a.ld_dG, a.ld_dG_lp, a.dG_lp_kind = G, G, 1 if lp_on else 0
         a.dinit_h, a.dinit_c = _ptr(dinit_h), _ptr(dinit_c)
-        cl = _ClusterSync(T, BB, H, dev, ln)
         st = _stream()
-        for t in range(T - 1, -1, -1):
+        if lp_on and _fused_ok(H, ln, False, s.Wl.dtype):
+            # one launch per step: dh_rec = dG_{t+1} @ W^T fused with the cell backward
+            f = FusedBwdArgs()
+            f.B, f.H, f.nd = B, H, nd
+            f.ld_dgn, f.W, f.w_gs = G, s.Wl.data_ptr(), H * G
+            f.dc_rec = dc_rec.data_ptr()
+            f.keep, f.seed, f.stream = float(keep), s.seed.data_ptr(), int(stream)
+            f.dinit_h, f.dinit_c = _ptr(dinit_h), _ptr(dinit_c)
+            dhT_c = dhT.contiguous() if dhT is not None else None
+            for t in range(T - 1, -1, -1):
+                f.dG_next = dG_lp[t + 1].data_ptr() if t < T - 1 else None
+                f.dh_extra = _ptr(dhT_c) if t == T - 1 else None
+                f.dh_out = dHout[t].data_ptr() if dHout is not None else None
+                f.act, f.c_new, f.c_prev = s.ACT[t].data_ptr(), s.Cout[t].data_ptr(), s.CC[t].data_ptr()
+                f.reset = _ptr(s.reset[t]) if s.reset is not None else None
+                f.step = t
+                f.dG, f.dG_lp = dG[t].data_ptr(), dG_lp[t].data_ptr()
+                _check(lib.lib.skr_lstm_fused_bwd(ctypes.byref(f), st), "lstm_fused_bwd")
+            if T > 0:
+                gemm.rec_gemm(dG_lp[0], s.Wl, DH, S, nd)    # dh into the initial state
+            T_loop = 0
+        else:
+            T_loop = T
+        cl = _ClusterSync(T, BB, H, dev, ln)
+        for t in range(T_loop - 1, -1, -1):
             cl.set(a, t)
             a.dh_out = dHout[t].data_ptr() if dHout is not None else None
             a.act, a.c_new, a.c_prev = s.ACT[t].data_ptr(), s.Cout[t].data_ptr(), s.CC[t].data_ptr()
