@@ -171,23 +171,20 @@ __global__ __launch_bounds__(256) void skinny_gemm_nt_kernel(
 // distinct bank quads.
 constexpr int NSTAGE = 4;
 
+// One [M<=128, BN] output tile over K range [k0, k0 + kslice) of
+// C = A . Bt^T (C points at this split's slab). Shared by the single-problem
+// and the grouped launch.
 template <int BN>
-__global__ __launch_bounds__(256) void skinny_gemm_glds_kernel(
-    const __hip_bfloat16* __restrict__ A, int64_t lda, int64_t a_batch,
-    const __hip_bfloat16* __restrict__ Bt, int64_t ldb, int64_t b_batch,
-    float* __restrict__ C, int64_t ldc, int64_t c_slab, int64_t c_batch, int M, int kslice) {
+__device__ __forceinline__ void glds_tile(const __hip_bfloat16* __restrict__ A, int64_t lda,
+                                          const __hip_bfloat16* __restrict__ Bt, int64_t ldb,
+                                          float* __restrict__ C, int64_t ldc, int M, int n0, int64_t k0, int kslice,
+                                          __hip_bfloat16* smem) {
     constexpr int NJ = BN / 16;
     constexpr int A_CH = BM / 8, B_CH = BN / 8;     // 1-KiB chunks (8 rows) per tile
     constexpr int GPW = (A_CH + B_CH) / 4;          // glds per wave per tile
     constexpr int TILE = (BM + BN) * BK;            // bf16 elements per stage
-    extern __shared__ __attribute__((aligned(16))) __hip_bfloat16 smem[];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const int n0 = blockIdx.x * BN;
-    const int64_t k0 = (int64_t)blockIdx.y * kslice;
     const int n = kslice / BK;
-    A += blockIdx.z * a_batch;
-    Bt += blockIdx.z * b_batch;
-    C += blockIdx.z * c_batch + blockIdx.y * c_slab;
 
     // per-lane source rows / swizzled chunk (fixed across tiles)
     const int r8 = lane >> 3, slot = lane & 7;
@@ -269,6 +266,58 @@ __global__ __launch_bounds__(256) void skinny_gemm_glds_kernel(
                 const int row = 32 * w + 16 * i + fq * 4 + e;
                 if (row < M) C[row * ldc + n0 + 16 * j + fr] = acc[i][j][e];
             }
+}
+
+template <int BN>
+__global__ __launch_bounds__(256) void skinny_gemm_glds_kernel(
+    const __hip_bfloat16* __restrict__ A, int64_t lda, int64_t a_batch,
+    const __hip_bfloat16* __restrict__ Bt, int64_t ldb, int64_t b_batch,
+    float* __restrict__ C, int64_t ldc, int64_t c_slab, int64_t c_batch, int M, int kslice) {
+    extern __shared__ __attribute__((aligned(16))) __hip_bfloat16 smem[];
+    glds_tile<BN>(A + blockIdx.z * a_batch, lda, Bt + blockIdx.z * b_batch, ldb,
+                  C + blockIdx.z * c_batch + blockIdx.y * c_slab, ldc, M, blockIdx.x * BN,
+                  (int64_t)blockIdx.y * kslice, kslice, smem);
+}
+
+// Grouped launch: up to kMaxGroup independent products (different operands,
+// shapes and split factors, same N-tile width) in ONE launch. The per-step
+// products of a recurrence that do not depend on each other (HyperLSTM:
+// h @ W_h for the main gates and [h | hh] @ W_y for the hyper gates; in the
+// backward dR_main @ W_h^T and dvec @ P^T) then share one kernel boundary
+// and fill the chip together instead of each leaving most CUs idle.
+// Workgroup id -> (problem, split, N tile) through the prefix sums `start`.
+}  // namespace
+
+struct GemmProblem {
+    const void* A; int64_t lda;
+    const void* Bt; int64_t ldb;
+    float* C; int64_t ldc; int64_t c_slab;
+    int M, N, K, splits;
+};
+
+namespace {
+
+constexpr int kMaxGroup = 4;
+struct GemmGroup {
+    GemmProblem p[kMaxGroup];
+    int start[kMaxGroup + 1];
+    int n;
+};
+
+template <int BN>
+__global__ __launch_bounds__(256) void skinny_gemm_group_kernel(const GemmGroup g) {
+    extern __shared__ __attribute__((aligned(16))) __hip_bfloat16 smem[];
+    const int id = blockIdx.x;
+    int q = 0;
+#pragma unroll
+    for (int i = 1; i < kMaxGroup; ++i) q += (i < g.n && id >= g.start[i]) ? 1 : 0;
+    const GemmProblem& p = g.p[q];
+    const int local = id - g.start[q];
+    const int ntiles = p.N / BN;
+    const int split = local / ntiles, nt = local - split * ntiles;
+    const int kslice = p.K / p.splits;
+    glds_tile<BN>((const __hip_bfloat16*)p.A, p.lda, (const __hip_bfloat16*)p.Bt, p.ldb, p.C + split * p.c_slab, p.ldc,
+                  p.M, nt * BN, (int64_t)split * kslice, kslice, smem);
 }
 
 // ---------------------------------------------------------------------------
@@ -435,6 +484,47 @@ SKR_API int skr_skinny_gemm_v2(const void* A, int64_t lda, int64_t a_batch, cons
     }
     return SKR_CHECK_LAUNCH();
 }
+
+// Grouped bf16 products (see skinny_gemm_group_kernel): each problem as
+// skr_skinny_gemm_v2 with batch 1; all use N tiles of `bn` (0: 64).
+SKR_API int skr_skinny_gemm_group(const GemmProblem* probs, int n, int bn, hipStream_t s) {
+    if (n < 1 || n > kMaxGroup) return -2;
+    if (bn == 0) bn = 64;
+    if (bn != 64 && bn != 128) return -2;
+    GemmGroup g{};
+    g.n = n;
+    g.start[0] = 0;
+    for (int i = 0; i < n; ++i) {
+        const GemmProblem& p = probs[i];
+        if (p.M < 1 || p.M > BM || p.N % bn != 0 || p.splits < 1 || p.K % p.splits != 0) return -2;
+        if ((p.K / p.splits) % BK != 0 || p.lda % 8 != 0 || p.ldb % 8 != 0) return -3;
+        if (((uintptr_t)p.A | (uintptr_t)p.Bt) & 15) return -4;
+        g.p[i] = p;
+        g.start[i + 1] = g.start[i] + (p.N / bn) * p.splits;
+    }
+    for (int i = n + 1; i <= kMaxGroup; ++i) g.start[i] = g.start[n];
+    const size_t lds = (size_t)NSTAGE * (BM + bn) * BK * 2;
+    if (bn == 128) {
+        static bool attr = false;
+        if (!attr) {
+            (void)hipFuncSetAttribute((const void*)skinny_gemm_group_kernel<128>,
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+            attr = true;
+        }
+        hipLaunchKernelGGL(skinny_gemm_group_kernel<128>, dim3(g.start[n]), dim3(256), lds, s, g);
+    } else {
+        static bool attr = false;
+        if (!attr) {
+            (void)hipFuncSetAttribute((const void*)skinny_gemm_group_kernel<64>,
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+            attr = true;
+        }
+        hipLaunchKernelGGL(skinny_gemm_group_kernel<64>, dim3(g.start[n]), dim3(256), lds, s, g);
+    }
+    return SKR_CHECK_LAUNCH();
+}
+
+SKR_API int skr_gemm_problem_size() { return (int)sizeof(GemmProblem); }
 
 // fp8 e4m3 operands (bytes): C[z][s] = a_scale * b_scale[n] * A8[z][:, ks] . Bt8[z][:, ks]^T.
 // Requirements as skr_skinny_gemm_v2 with kslice % 128 == 0 and 16-byte aligned rows.

@@ -8,13 +8,15 @@ import torch
 sys.path.insert(0, __file__.rsplit("/scripts/", 1)[0])
 from sketch_rnn_amd.ops import gemm  # noqa: E402
 
-SHAPES = [  # (name, M, N, K, nd)
-    ("RC  fwd", 100, 9216, 2304, 1),
-    ("VEC fwd", 100, 24576, 256, 1),
-    ("dA  bwd", 100, 2304, 9216, 1),
-    ("dhh bwd", 100, 256, 24576, 1),
-    ("enc fwd", 100, 2048, 512, 2),
-    ("enc bwd", 100, 512, 2048, 2),
+SHAPES = [  # (name, M, N, K, nd): the per-step products of the vae_large step
+    ("R_main fwd", 100, 8192, 2048, 1),
+    ("R_hyp  fwd", 100, 1024, 2304, 1),
+    ("VEC    fwd", 100, 24576, 256, 1),
+    ("DAM    bwd", 100, 2048, 8192, 1),
+    ("DHZ    bwd", 100, 256, 24576, 1),
+    ("DAY    bwd", 100, 2304, 1024, 1),
+    ("enc    fwd", 100, 2048, 512, 2),
+    ("enc    bwd", 100, 512, 2048, 2),
 ]
 
 

@@ -142,6 +142,16 @@ class FusedBwdArgs(C.Structure):
     ]
 
 
+class GemmProblem(C.Structure):
+    """Mirror of ``GemmProblem`` in csrc/skinny_gemm.hip."""
+    _fields_ = [
+        ("A", _p), ("lda", _i64),
+        ("Bt", _p), ("ldb", _i64),
+        ("C", _p), ("ldc", _i64), ("c_slab", _i64),
+        ("M", _i), ("N", _i), ("K", _i), ("splits", _i),
+    ]
+
+
 class HipLib:
     def __init__(self, lib: C.CDLL):
         self.lib = lib
@@ -168,6 +178,8 @@ class HipLib:
         lib.skr_gru_fwd.restype = _i
         lib.skr_gru_bwd.argtypes = [C.POINTER(GruBwdArgs), _i, _p]
         lib.skr_gru_bwd.restype = _i
+        lib.skr_skinny_gemm_group.argtypes = [C.POINTER(GemmProblem), _i, _i, _p]
+        lib.skr_skinny_gemm_group.restype = _i
         lib.skr_lstm_fused_fwd.argtypes = [C.POINTER(FusedFwdArgs), _p]
         lib.skr_lstm_fused_fwd.restype = _i
         lib.skr_lstm_fused_bwd.argtypes = [C.POINTER(FusedBwdArgs), _p]
@@ -175,7 +187,8 @@ class HipLib:
         for name, cls in (("skr_lstm_fwd_args_size", LstmFwdArgs), ("skr_lstm_bwd_args_size", LstmBwdArgs),
                           ("skr_gru_fwd_args_size", GruFwdArgs), ("skr_gru_bwd_args_size", GruBwdArgs),
                           ("skr_lstm_fused_fwd_args_size", FusedFwdArgs),
-                          ("skr_lstm_fused_bwd_args_size", FusedBwdArgs)):
+                          ("skr_lstm_fused_bwd_args_size", FusedBwdArgs),
+                          ("skr_gemm_problem_size", GemmProblem)):
             fn = getattr(lib, name)
             fn.restype = _i
             if fn() != C.sizeof(cls):

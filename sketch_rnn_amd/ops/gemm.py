@@ -112,6 +112,34 @@ def rec_gemm(a: torch.Tensor, bt: torch.Tensor, out: torch.Tensor, splits: int, 
     return out
 
 
+GROUPED = os.environ.get("SKR_GEMM_GROUP", "1") != "0"   # SKR_GEMM_GROUP=0: independent per-step products as separate launches
+
+
+def rec_gemm_group(jobs) -> None:
+    """Several independent :func:`rec_gemm` products ``(a, bt, out, splits)``
+    (nd = 1, M <= 128, bf16, splits >= 1) in ONE grouped launch
+    (csrc/skinny_gemm.hip ``skr_skinny_gemm_group``); falls back to one
+    launch per product when a job does not qualify."""
+    ok = GROUPED and GEMM_ALGO == "v2" and 1 <= len(jobs) <= 4 and all(
+        a.is_cuda and a.dtype == _BF16 and s >= 1 and a.shape[0] <= 128 for a, _, _, s in jobs)
+    if not ok:
+        for a, bt, out, s in jobs:
+            rec_gemm(a, bt, out, s)
+        return
+    from ..utils import native
+    from ._hipapi import GemmProblem
+    lib = native.require_hip()
+    probs = (GemmProblem * len(jobs))()
+    for p, (a, bt, out, s) in zip(probs, jobs):
+        N, K = bt.shape[-2], bt.shape[-1]
+        p.A, p.lda, p.Bt, p.ldb = a.data_ptr(), a.stride(0), bt.data_ptr(), bt.stride(-2)
+        p.C, p.ldc, p.c_slab = out.data_ptr(), N, out.stride(0)
+        p.M, p.N, p.K, p.splits = a.shape[0], N, K, s
+    rc = lib.lib.skr_skinny_gemm_group(probs, len(jobs), 0, torch.cuda.current_stream().cuda_stream)
+    if rc != 0:
+        raise RuntimeError("skr_skinny_gemm_group failed (%d)" % rc)
+
+
 # ---- inference-time helpers ------------------------------------------------------------
 _WCACHE = {}
 WEIGHTS_EPOCH = [0]

@@ -545,13 +545,17 @@ class _HyperSeq(torch.autograd.Function):
         clm, clh = _ClusterSync(T, B, H, dev), _ClusterSync(T, B, Hh, dev)
         main, side = torch.cuda.current_stream(), _side_stream(dev)
         st = main.cuda_stream
+        group = not fp8 and not TWO_STREAM and gemm.GROUPED and S_m >= 1 and S_y >= 1 and dt == torch.bfloat16
         for t in range(T):
             clm.set(am, t)
             clh.set(ah, t)
-            _join(side, main)                            # h_{t-1} written
-            with torch.cuda.stream(side):
-                rgemm(A[t, :, :H], WhT, RM[t], S_m)
-            rgemm(A[t], WyT, RY, S_y)
+            if group:   # R_main and R_hyp in one launch
+                gemm.rec_gemm_group([(A[t, :, :H], WhT, RM[t], S_m), (A[t], WyT, RY, S_y)])
+            else:
+                _join(side, main)                        # h_{t-1} written
+                with torch.cuda.stream(side):
+                    rgemm(A[t, :, :H], WhT, RM[t], S_m)
+                rgemm(A[t], WyT, RY, S_y)
             ah.xp, ah.c_prev, ah.step = XHY[t].data_ptr(), HCC[t].data_ptr(), t
             ah.h_out, ah.c_out, ah.act = HH[t].data_ptr(), HCout[t].data_ptr(), HACT[t].data_ptr()
             ah.xhat, ah.rstd, ah.chat = HXHAT[t].data_ptr(), HRSTD[t].data_ptr(), HCHAT[t].data_ptr()
@@ -636,6 +640,7 @@ class _HyperSeq(torch.autograd.Function):
         clm, clh = _ClusterSync(T, B, H, dev), _ClusterSync(T, B, Hh, dev)
         main, side = torch.cuda.current_stream(), _side_stream(dev)
         st = main.cuda_stream
+        group = lp_on and not TWO_STREAM and gemm.GROUPED and S_am >= 1 and S_h >= 1
         for t in range(T - 1, -1, -1):
             clm.set(am, t)
             clh.set(ah, t)
@@ -649,10 +654,13 @@ class _HyperSeq(torch.autograd.Function):
             am.dxp, am.dvec = dXH[t].data_ptr(), dVEC[t].data_ptr()
             am.dlny, am.dlncy = DLNY[t].data_ptr(), DLNCY[t].data_ptr()
             _check(lib.lib.skr_lstm_bwd_step(ctypes.byref(am), 1, 1, st), "hyper_main_bwd_step")
-            _join(side, main)                            # dR_main(t) written, DAM consumed
-            with torch.cuda.stream(side):
-                gemm.rec_gemm(dRM_lp[t], s.Whl, DAM, S_am)
-            gemm.rec_gemm(dVEC[t], s.Pl, DHZ, S_h)
+            if group:   # dR_main @ W_h^T and dvec @ P^T in one launch
+                gemm.rec_gemm_group([(dRM_lp[t], s.Whl, DAM, S_am), (dVEC[t], s.Pl, DHZ, S_h)])
+            else:
+                _join(side, main)                        # dR_main(t) written, DAM consumed
+                with torch.cuda.stream(side):
+                    gemm.rec_gemm(dRM_lp[t], s.Whl, DAM, S_am)
+                gemm.rec_gemm(dVEC[t], s.Pl, DHZ, S_h)
             ah.act, ah.c_new, ah.c_prev = s.HACT[t].data_ptr(), s.HCout[t].data_ptr(), s.HCC[t].data_ptr()
             ah.xhat, ah.rstd, ah.chat = s.HXHAT[t].data_ptr(), s.HRSTD[t].data_ptr(), s.HCHAT[t].data_ptr()
             ah.step = t

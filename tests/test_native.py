@@ -27,14 +27,16 @@ def test_arg_struct_layouts(hip):
     for fn, cls in (("skr_lstm_fwd_args_size", api.LstmFwdArgs), ("skr_lstm_bwd_args_size", api.LstmBwdArgs),
                     ("skr_gru_fwd_args_size", api.GruFwdArgs), ("skr_gru_bwd_args_size", api.GruBwdArgs),
                     ("skr_lstm_fused_fwd_args_size", api.FusedFwdArgs),
-                    ("skr_lstm_fused_bwd_args_size", api.FusedBwdArgs)):
+                    ("skr_lstm_fused_bwd_args_size", api.FusedBwdArgs),
+                    ("skr_gemm_problem_size", api.GemmProblem)):
         assert getattr(hip.lib, fn)() == ctypes.sizeof(cls), fn
 
 
 def test_exported_entry_points(hip):
     for name in ("skr_lstm_fwd_step", "skr_lstm_bwd_step", "skr_gru_fwd", "skr_gru_bwd", "skr_skinny_gemm",
                  "skr_skinny_gemm_v2", "skr_skinny_gemm_fp8", "skr_mdn_loss", "skr_adam_step", "skr_global_norm", "skr_mdn_sample",
-                 "skr_lstm_fused_fwd", "skr_lstm_fused_bwd", "skr_colsum"):
+                 "skr_lstm_fused_fwd", "skr_lstm_fused_bwd", "skr_colsum",
+                 "skr_skinny_gemm_group"):
         assert hasattr(hip.lib, name), name
 
 
