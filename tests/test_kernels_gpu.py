@@ -217,6 +217,35 @@ def test_hyper_sequence_matches_oracle(H, Hh, E, keep):
     _close(g_h, g_t, 2e-3, 2e-4, "grad")
 
 
+@pytest.mark.parametrize("H,Hh,E", [(2048, 256, 32), (512, 64, 8)])
+def test_hyper_grouped_gemm_path_bitwise(H, Hh, E):
+    """bf16 HyperLSTM with the grouped per-step GEMM launches equals the
+    one-launch-per-product path bit for bit (same tiles, same sums)."""
+    from sketch_rnn_amd.ops import gemm
+    torch.manual_seed(3)
+    T, B, IN = 4, 100, 13
+    p = C.HyperLSTMParams(IN, H, Hh, E).to(DEV)
+    x = torch.randn(T, B, IN, device=DEV, requires_grad=True)
+    st = [torch.zeros(B, n, device=DEV) for n in (H, H, Hh, Hh)]
+    w = torch.randn(T, B, H, device=DEV)
+    saved = gemm.GROUPED
+    res = []
+    try:
+        ops.set_compute_dtype("bf16")
+        ops.set_backend("hip")
+        for grouped in (True, False):
+            gemm.GROUPED = grouped
+            p.zero_grad()
+            xg = x.detach().clone().requires_grad_()
+            out, _ = ops.hyper_sequence(p, xg, *st, drop_keep=0.9, drop_seed=3, drop_stream=9)
+            (out * w).sum().backward()
+            res.append([out.detach(), xg.grad] + [q.grad.clone() for q in p.parameters()])
+    finally:
+        gemm.GROUPED = saved
+    for a, b in zip(*res):
+        assert torch.equal(a, b)
+
+
 @pytest.mark.parametrize("M,N,K,nd", [(100, 9216, 2304, 1), (100, 2304, 9216, 1), (100, 256, 24576, 1),
                                       (100, 24576, 256, 1), (7, 64, 64, 1), (128, 2048, 512, 2),
                                       (100, 512, 2048, 2), (256, 8192, 2048, 1), (512, 1024, 256, 1)])
