@@ -174,7 +174,17 @@ constexpr int NSTAGE = 4;
 // One [M<=128, BN] output tile over K range [k0, k0 + kslice) of
 // C = A . Bt^T (C points at this split's slab). Shared by the single-problem
 // and the grouped launch.
-template <int BN>
+template <int GPW, int NS>
+__device__ __forceinline__ void wait_ahead(int ahead) {
+    // tile kt landed (for this wave) once at most `ahead` younger tiles are pending
+    if constexpr (NS - 2 >= 4) if (ahead >= 4) { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * GPW) : "memory"); return; }
+    if constexpr (NS - 2 >= 3) if (ahead == 3) { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * GPW) : "memory"); return; }
+    if constexpr (NS - 2 >= 2) if (ahead == 2) { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * GPW) : "memory"); return; }
+    if (ahead == 1) { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GPW) : "memory"); return; }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+template <int BN, int NS>
 __device__ __forceinline__ void glds_tile(const __hip_bfloat16* __restrict__ A, int64_t lda,
                                           const __hip_bfloat16* __restrict__ Bt, int64_t ldb,
                                           float* __restrict__ C, int64_t ldc, int M, int n0, int64_t k0, int kslice,
@@ -194,7 +204,9 @@ __device__ __forceinline__ void glds_tile(const __hip_bfloat16* __restrict__ A, 
     for (int i = 0; i < A_CH / 4; ++i) {
         const int row = (w + 4 * i) * 8 + r8;
         const int kc = slot ^ ((row >> 1) & 7);
-        asrc[i] = A + (int64_t)min(row, M - 1) * lda + k0 + kc * 8;
+        // rows past M: every lane of the chunk reads the same 16 bytes (one
+        // line instead of 1 KiB; the wave's glds count stays uniform)
+        asrc[i] = row < M ? A + (int64_t)row * lda + k0 + kc * 8 : A + (int64_t)(M - 1) * lda + k0;
     }
 #pragma unroll
     for (int i = 0; i < B_CH / 4; ++i) {
@@ -203,7 +215,7 @@ __device__ __forceinline__ void glds_tile(const __hip_bfloat16* __restrict__ A, 
         bsrc[i] = Bt + (int64_t)(n0 + row) * ldb + k0 + kc * 8;
     }
     auto issue = [&](int kt) {
-        __hip_bfloat16* st = smem + (kt % NSTAGE) * TILE;
+        __hip_bfloat16* st = smem + (kt % NS) * TILE;
         const int64_t ko = (int64_t)kt * BK;
 #pragma unroll
         for (int i = 0; i < A_CH / 4; ++i)
@@ -224,17 +236,13 @@ __device__ __forceinline__ void glds_tile(const __hip_bfloat16* __restrict__ A, 
 
     const int fr = lane & 15, fq = lane >> 4;
 #pragma unroll
-    for (int p = 0; p < NSTAGE - 1; ++p)
+    for (int p = 0; p < NS - 1; ++p)
         if (p < n) issue(p);
     for (int kt = 0; kt < n; ++kt) {
-        // tile kt landed (for this wave) once at most min(n-1-kt, NSTAGE-2) younger tiles are pending
-        const int ahead = min(n - 1 - kt, NSTAGE - 2);
-        if (ahead >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * GPW) : "memory");
-        else if (ahead == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GPW) : "memory");
-        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();  // ... and for every wave; buffer (kt-1) % NSTAGE is free
-        if (kt + NSTAGE - 1 < n) issue(kt + NSTAGE - 1);
-        const __hip_bfloat16* As = smem + (kt % NSTAGE) * TILE;
+        wait_ahead<GPW, NS>(min(n - 1 - kt, NS - 2));
+        __builtin_amdgcn_s_barrier();  // ... and for every wave; buffer (kt-1) % NS is free
+        if (kt + NS - 1 < n) issue(kt + NS - 1);
+        const __hip_bfloat16* As = smem + (kt % NS) * TILE;
         const __hip_bfloat16* Bs = As + BM * BK;
 #pragma unroll
         for (int ks = 0; ks < BK; ks += 32) {
@@ -268,13 +276,13 @@ __device__ __forceinline__ void glds_tile(const __hip_bfloat16* __restrict__ A, 
             }
 }
 
-template <int BN>
+template <int BN, int NS>
 __global__ __launch_bounds__(256) void skinny_gemm_glds_kernel(
     const __hip_bfloat16* __restrict__ A, int64_t lda, int64_t a_batch,
     const __hip_bfloat16* __restrict__ Bt, int64_t ldb, int64_t b_batch,
     float* __restrict__ C, int64_t ldc, int64_t c_slab, int64_t c_batch, int M, int kslice) {
     extern __shared__ __attribute__((aligned(16))) __hip_bfloat16 smem[];
-    glds_tile<BN>(A + blockIdx.z * a_batch, lda, Bt + blockIdx.z * b_batch, ldb,
+    glds_tile<BN, NS>(A + blockIdx.z * a_batch, lda, Bt + blockIdx.z * b_batch, ldb,
                   C + blockIdx.z * c_batch + blockIdx.y * c_slab, ldc, M, blockIdx.x * BN,
                   (int64_t)blockIdx.y * kslice, kslice, smem);
 }
@@ -304,7 +312,7 @@ struct GemmGroup {
     int n;
 };
 
-template <int BN>
+template <int BN, int NS>
 __global__ __launch_bounds__(256) void skinny_gemm_group_kernel(const GemmGroup g) {
     extern __shared__ __attribute__((aligned(16))) __hip_bfloat16 smem[];
     const int id = blockIdx.x;
@@ -316,7 +324,7 @@ __global__ __launch_bounds__(256) void skinny_gemm_group_kernel(const GemmGroup 
     const int ntiles = p.N / BN;
     const int split = local / ntiles, nt = local - split * ntiles;
     const int kslice = p.K / p.splits;
-    glds_tile<BN>((const __hip_bfloat16*)p.A, p.lda, (const __hip_bfloat16*)p.Bt, p.ldb, p.C + split * p.c_slab, p.ldc,
+    glds_tile<BN, NS>((const __hip_bfloat16*)p.A, p.lda, (const __hip_bfloat16*)p.Bt, p.ldb, p.C + split * p.c_slab, p.ldc,
                   p.M, nt * BN, (int64_t)split * kslice, kslice, smem);
 }
 
@@ -451,6 +459,49 @@ SKR_API int skr_skinny_gemm(const void* A, int64_t lda, int64_t a_batch, const v
     return SKR_CHECK_LAUNCH();
 }
 
+// Ring depth of the v2 / grouped kernels (stages of (BM + BN) x 128 B):
+// 3, 4 or 6 (6 only with BN = 64: 144 KiB). skr_gemm_set_nstage() tunes it
+// (scripts/bench_gemm.py sweeps it).
+static int g_nstage = 4;
+
+SKR_API int skr_gemm_set_nstage(int ns) {
+    if (ns != 3 && ns != 4 && ns != 6) return -2;
+    g_nstage = ns;
+    return 0;
+}
+
+namespace {
+
+template <typename K>
+void set_lds_attr(K k, size_t lds) {
+    // per instantiation, once (a HIP graph capture must not see the call twice)
+    static bool done = false;
+    if (!done) {
+        (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        done = true;
+    }
+}
+
+template <int BN, int NS>
+int launch_v2(dim3 grid, hipStream_t s, const void* A, int64_t lda, int64_t a_batch, const void* Bt, int64_t ldb,
+              int64_t b_batch, float* C, int64_t ldc, int64_t c_slab, int64_t c_batch, int M, int kslice) {
+    const size_t lds = (size_t)NS * (BM + BN) * BK * 2;
+    set_lds_attr(skinny_gemm_glds_kernel<BN, NS>, lds);
+    hipLaunchKernelGGL((skinny_gemm_glds_kernel<BN, NS>), grid, dim3(256), lds, s, (const __hip_bfloat16*)A, lda,
+                       a_batch, (const __hip_bfloat16*)Bt, ldb, b_batch, C, ldc, c_slab, c_batch, M, kslice);
+    return SKR_CHECK_LAUNCH();
+}
+
+template <int BN, int NS>
+int launch_group(const GemmGroup& g, hipStream_t s) {
+    const size_t lds = (size_t)NS * (BM + BN) * BK * 2;
+    set_lds_attr(skinny_gemm_group_kernel<BN, NS>, lds);
+    hipLaunchKernelGGL((skinny_gemm_group_kernel<BN, NS>), dim3(g.start[g.n]), dim3(256), lds, s, g);
+    return SKR_CHECK_LAUNCH();
+}
+
+}  // namespace
+
 // Same contract as skr_skinny_gemm, LDS-DMA ring kernel (v2).
 SKR_API int skr_skinny_gemm_v2(const void* A, int64_t lda, int64_t a_batch, const void* Bt, int64_t ldb,
                                int64_t b_batch, float* C, int64_t ldc, int64_t c_slab, int64_t c_batch, int M, int N,
@@ -462,27 +513,10 @@ SKR_API int skr_skinny_gemm_v2(const void* A, int64_t lda, int64_t a_batch, cons
     if (kslice % BK != 0 || lda % 8 != 0 || ldb % 8 != 0) return -3;
     if (((uintptr_t)A | (uintptr_t)Bt) & 15) return -4;
     const dim3 grid(N / bn, splits, batch);
-    const size_t lds = (size_t)NSTAGE * (BM + bn) * BK * 2;
-    if (bn == 128) {
-        static bool attr = false;
-        if (!attr) {
-            (void)hipFuncSetAttribute((const void*)skinny_gemm_glds_kernel<128>,
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-            attr = true;
-        }
-        hipLaunchKernelGGL(skinny_gemm_glds_kernel<128>, grid, dim3(256), lds, s, (const __hip_bfloat16*)A, lda,
-                           a_batch, (const __hip_bfloat16*)Bt, ldb, b_batch, C, ldc, c_slab, c_batch, M, kslice);
-    } else {
-        static bool attr = false;
-        if (!attr) {
-            (void)hipFuncSetAttribute((const void*)skinny_gemm_glds_kernel<64>,
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-            attr = true;
-        }
-        hipLaunchKernelGGL(skinny_gemm_glds_kernel<64>, grid, dim3(256), lds, s, (const __hip_bfloat16*)A, lda,
-                           a_batch, (const __hip_bfloat16*)Bt, ldb, b_batch, C, ldc, c_slab, c_batch, M, kslice);
-    }
-    return SKR_CHECK_LAUNCH();
+#define SKR_V2(BN_, NS_) launch_v2<BN_, NS_>(grid, s, A, lda, a_batch, Bt, ldb, b_batch, C, ldc, c_slab, c_batch, M, kslice)
+    if (bn == 128) return g_nstage == 3 ? SKR_V2(128, 3) : SKR_V2(128, 4);
+    return g_nstage == 3 ? SKR_V2(64, 3) : g_nstage == 6 ? SKR_V2(64, 6) : SKR_V2(64, 4);
+#undef SKR_V2
 }
 
 // Grouped bf16 products (see skinny_gemm_group_kernel): each problem as
@@ -503,25 +537,9 @@ SKR_API int skr_skinny_gemm_group(const GemmProblem* probs, int n, int bn, hipSt
         g.start[i + 1] = g.start[i] + (p.N / bn) * p.splits;
     }
     for (int i = n + 1; i <= kMaxGroup; ++i) g.start[i] = g.start[n];
-    const size_t lds = (size_t)NSTAGE * (BM + bn) * BK * 2;
-    if (bn == 128) {
-        static bool attr = false;
-        if (!attr) {
-            (void)hipFuncSetAttribute((const void*)skinny_gemm_group_kernel<128>,
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-            attr = true;
-        }
-        hipLaunchKernelGGL(skinny_gemm_group_kernel<128>, dim3(g.start[n]), dim3(256), lds, s, g);
-    } else {
-        static bool attr = false;
-        if (!attr) {
-            (void)hipFuncSetAttribute((const void*)skinny_gemm_group_kernel<64>,
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-            attr = true;
-        }
-        hipLaunchKernelGGL(skinny_gemm_group_kernel<64>, dim3(g.start[n]), dim3(256), lds, s, g);
-    }
-    return SKR_CHECK_LAUNCH();
+    if (bn == 128) return g_nstage == 3 ? launch_group<128, 3>(g, s) : launch_group<128, 4>(g, s);
+    return g_nstage == 3 ? launch_group<64, 3>(g, s) : g_nstage == 6 ? launch_group<64, 6>(g, s)
+                                                                    : launch_group<64, 4>(g, s);
 }
 
 SKR_API int skr_gemm_problem_size() { return (int)sizeof(GemmProblem); }

@@ -178,6 +178,8 @@ class HipLib:
         lib.skr_gru_fwd.restype = _i
         lib.skr_gru_bwd.argtypes = [C.POINTER(GruBwdArgs), _i, _p]
         lib.skr_gru_bwd.restype = _i
+        lib.skr_gemm_set_nstage.argtypes = [_i]
+        lib.skr_gemm_set_nstage.restype = _i
         lib.skr_skinny_gemm_group.argtypes = [C.POINTER(GemmProblem), _i, _i, _p]
         lib.skr_skinny_gemm_group.restype = _i
         lib.skr_lstm_fused_fwd.argtypes = [C.POINTER(FusedFwdArgs), _p]
