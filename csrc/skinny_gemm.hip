@@ -462,7 +462,7 @@ SKR_API int skr_skinny_gemm(const void* A, int64_t lda, int64_t a_batch, const v
 // Ring depth of the v2 / grouped kernels (stages of (BM + BN) x 128 B):
 // 3, 4 or 6 (6 only with BN = 64: 144 KiB). skr_gemm_set_nstage() tunes it
 // (scripts/bench_gemm.py sweeps it).
-static int g_nstage = 4;
+static int g_nstage = 3;   // measured best: 2 workgroups per CU fit (72 KiB at BN = 64)
 
 SKR_API int skr_gemm_set_nstage(int ns) {
     if (ns != 3 && ns != 4 && ns != 6) return -2;

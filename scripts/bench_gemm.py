@@ -77,7 +77,7 @@ def main():
             lib.skr_gemm_set_nstage(ns)
             res.append("n%d %.1f" % (ns, timeit(lambda: gemm.rec_gemm_group(jobs))))
         print("group %s: %s" % (gname, " ".join(res)), flush=True)
-    lib.skr_gemm_set_nstage(4)
+    lib.skr_gemm_set_nstage(3)
 
 
 if __name__ == "__main__":
