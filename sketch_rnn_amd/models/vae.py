@@ -27,6 +27,7 @@ from .. import ops
 from ..config import VAEConfig
 from ..ops import gemm
 from . import cells as C
+from ..ops.inproj import bilstm_input_proj
 
 # dropout hash streams
 _S_ENC_FW, _S_ENC_BW, _S_DEC, _S_IN, _S_OUT, _S_EPS = 11, 13, 17, 23, 29, 31
@@ -63,19 +64,15 @@ class Encoder(nn.Module):
         T, B, _ = x.shape
         H = cfg.enc_rnn_size
         keep = cfg.recurrent_dropout_prob if (train and cfg.use_recurrent_dropout) else 1.0
-        xr = reverse_padded(x, lengths)
         zeros = x.new_zeros(B, H)
-        xps, lns = [], []
-        for p, xin in ((self.fw, x), (self.bw, xr)):
-            xp = (xin.reshape(T * B, 5) @ p.W_x).view(T, B, 4 * H)
-            if isinstance(p, C.LNLSTMParams):
-                lns.append((p.ln_gamma, p.ln_beta, p.lnc_gamma, p.lnc_beta))
-            else:
-                xp = xp + p.bias
-                lns.append(None)
-            xps.append(xp)
-        outs = ops.bilstm_sequence(xps[0], xps[1], self.fw.W_h, self.bw.W_h, zeros, zeros, drop_keep=keep,
-                                   drop_seed=seed, drop_stream=_S_ENC_FW, ln_f=lns[0], ln_b=lns[1])
+        ln = isinstance(self.fw, C.LNLSTMParams)
+        lns = [(p.ln_gamma, p.ln_beta, p.lnc_gamma, p.lnc_beta) if ln else None for p in (self.fw, self.bw)]
+        # both directions' projections in one [T, 2B, 4H] tensor (the backward
+        # direction reads each sketch reversed within its length)
+        xp = bilstm_input_proj(x, lengths, self.fw.W_x, self.bw.W_x, None if ln else self.fw.bias,
+                               None if ln else self.bw.bias)
+        outs = ops.bilstm_sequence_packed(xp, self.fw.W_h, self.bw.W_h, zeros, zeros, drop_keep=keep,
+                                          drop_seed=seed, drop_stream=_S_ENC_FW, ln_f=lns[0], ln_b=lns[1])
         idx = (lengths - 1).clamp(min=0).view(1, B, 1).expand(1, B, H)
         last_h = torch.cat([torch.gather(o, 0, idx).squeeze(0) for o in outs], -1)
         mu = last_h @ self.mu_w + self.mu_b

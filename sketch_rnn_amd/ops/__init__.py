@@ -83,6 +83,20 @@ def bilstm_sequence(xp_f, xp_b, W_f, W_b, h0, c0, drop_keep: float = 1.0, drop_s
     return of, ob
 
 
+def bilstm_sequence_packed(xp, W_f, W_b, h0, c0, drop_keep: float = 1.0, drop_seed: int = 0,
+                           drop_stream: int = 0, ln_f=None, ln_b=None, forget_bias: float = 1.0):
+    """:func:`bilstm_sequence` with both directions' input projections packed
+    as ``xp [T, 2B, 4H]`` (forward rows first), e.g. from
+    :func:`.inproj.bilstm_input_proj`."""
+    if use_hip(xp):
+        from .recurrent import bilstm_sequence_packed_hip
+        return bilstm_sequence_packed_hip(xp, W_f, W_b, h0, c0, drop_keep, drop_seed, (drop_stream, drop_stream),
+                                          ln_f, ln_b, forget_bias)
+    B = xp.shape[1] // 2
+    return bilstm_sequence(xp[:, :B], xp[:, B:], W_f, W_b, h0, c0, drop_keep, drop_seed, drop_stream, ln_f, ln_b,
+                           forget_bias)
+
+
 def hyper_sequence(p, x, h0, c0, hh0, hc0, forget_bias: float = 1.0, drop_keep: float = 1.0,
                    drop_seed: int = 0, drop_stream: int = 0, hyp_drop_keep: float = 1.0):
     if use_hip(x):

@@ -376,8 +376,15 @@ def bilstm_sequence_hip(xp_f, xp_b, W_f, W_b, h0, c0, drop_keep=1.0, drop_seed=0
     """Both encoder directions in one launch per step (2B rows). Each
     direction keeps its own dropout stream via the row index (rows of the
     backward direction are offset by B*H in the hash index)."""
-    B = xp_f.shape[1]
-    xp = torch.cat([xp_f, xp_b], 1)
+    return bilstm_sequence_packed_hip(torch.cat([xp_f, xp_b], 1), W_f, W_b, h0, c0, drop_keep, drop_seed, streams,
+                                      ln_f, ln_b, forget_bias)
+
+
+def bilstm_sequence_packed_hip(xp, W_f, W_b, h0, c0, drop_keep=1.0, drop_seed=0, streams=(0, 0),
+                               ln_f=None, ln_b=None, forget_bias=1.0):
+    """As :func:`bilstm_sequence_hip` with the input projections already in
+    the ``[T, 2B, 4H]`` layout (forward-direction rows first; ops/inproj.py)."""
+    B = xp.shape[1] // 2
     W = torch.stack([W_f, W_b], 0)
     h = torch.cat([h0, h0], 0)
     c = torch.cat([c0, c0], 0)

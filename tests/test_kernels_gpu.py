@@ -264,6 +264,29 @@ def test_skinny_gemm_matches_torch(M, N, K, nd):
     assert err <= 1e-3 * ref.abs().max().item() + 1e-3, (S, err)
 
 
+@pytest.mark.parametrize("with_bias", [True, False])
+def test_bilstm_input_proj_matches_torch(with_bias):
+    """csrc/inproj.hip: both encoder directions' K=5 projections (reversed
+    backward direction) and their weight / bias gradients."""
+    from sketch_rnn_amd.ops.inproj import _BiInProj, bilstm_input_proj_torch
+    torch.manual_seed(6)
+    T, B, IN, G = 37, 13, 5, 768
+    x = torch.randn(T, B, IN, device=DEV)
+    lengths = torch.randint(1, T + 1, (B,), device=DEV)
+    params = [torch.randn(IN, G, device=DEV, requires_grad=True) for _ in range(2)]
+    params += [torch.randn(G, device=DEV, requires_grad=True) for _ in range(2)] if with_bias else [None, None]
+    w = torch.randn(T, 2 * B, G, device=DEV)
+    outs, grads = [], []
+    for fn in (lambda *a: _BiInProj.apply(x, lengths, *a), lambda *a: bilstm_input_proj_torch(x, lengths, *a)):
+        ps = [p.detach().clone().requires_grad_() if p is not None else None for p in params]
+        y = fn(*ps)
+        (y * w).sum().backward()
+        outs.append(y.detach())
+        grads.append([p.grad for p in ps if p is not None])
+    _close([outs[0]], [outs[1]], 1e-5, 1e-5, "xp")
+    _close(grads[0], grads[1], 1e-4, 1e-3, "grad")
+
+
 def test_grouped_skinny_gemm_matches_torch():
     """Independent products in one grouped launch (csrc/skinny_gemm.hip)."""
     from sketch_rnn_amd.ops import gemm
