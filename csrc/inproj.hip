@@ -111,3 +111,105 @@ SKR_API int skr_inproj_bwd(const float* x, const int64_t* len, const float* dxp,
         default: return -2;
     }
 }
+
+// ---------------------------------------------------------------------------
+// Decoder input projection with a per-sequence broadcast part: the decoder
+// input is [stroke-5 | z] with z constant over time, so
+//
+//   xp[t, b, g] = zw[b, g] + sum_{i<IN} x[t, b, i] * W[i, g]
+//
+// with zw = z @ W_z (+ bias) computed once per sequence ([B, G], a tiny
+// GEMM) instead of a K = 5 + |z| product over all T*B rows. Backward, one
+// read of dxp (fp32 or bf16):
+//   S[b, g] = sum_t dxp[t, b, g]                    (-> dz, dW_z, dbias)
+//   P[b, i, g] = sum_t x[t, b, i] dxp[t, b, g]     (-> dW[:IN] = sum_b P)
+namespace {
+
+template <int IN>
+__global__ __launch_bounds__(256) void bproj_fwd(const float* __restrict__ x, const float* __restrict__ W,
+                                                 const float* __restrict__ zw, float* __restrict__ xp, int T, int B,
+                                                 int G, int tpb) {
+    const int g = blockIdx.x * 256 + threadIdx.x;
+    const int b = blockIdx.y;
+    if (g >= G) return;
+    float w[IN];
+#pragma unroll
+    for (int i = 0; i < IN; ++i) w[i] = W[(int64_t)i * G + g];
+    const float z0 = zw ? zw[(int64_t)b * G + g] : 0.f;
+    const int t0 = blockIdx.z * tpb, t1 = min(T, t0 + tpb);
+#pragma unroll 4
+    for (int t = t0; t < t1; ++t) {
+        const float* xr = x + ((int64_t)t * B + b) * IN;
+        float acc = z0;
+#pragma unroll
+        for (int i = 0; i < IN; ++i) acc += xr[i] * w[i];
+        __builtin_nontemporal_store(acc, xp + ((int64_t)t * B + b) * G + g);
+    }
+}
+
+template <int IN, bool BF16>
+__global__ __launch_bounds__(256) void bproj_bwd(const float* __restrict__ x, const void* __restrict__ dxp,
+                                                 int64_t ld, float* __restrict__ S, float* __restrict__ P, int T,
+                                                 int B, int G) {
+    const int g = blockIdx.x * 256 + threadIdx.x;
+    const int b = blockIdx.y;
+    if (g >= G) return;
+    float acc[IN + 1];
+#pragma unroll
+    for (int i = 0; i <= IN; ++i) acc[i] = 0.f;
+#pragma unroll 4
+    for (int t = 0; t < T; ++t) {
+        const int64_t o = ((int64_t)t * B + b) * ld + g;
+        const float dv = BF16 ? __bfloat162float(((const __hip_bfloat16*)dxp)[o]) : ((const float*)dxp)[o];
+        const float* xr = x + ((int64_t)t * B + b) * IN;
+#pragma unroll
+        for (int i = 0; i < IN; ++i) acc[i] += xr[i] * dv;
+        acc[IN] += dv;
+    }
+    S[(int64_t)b * G + g] = acc[IN];
+#pragma unroll
+    for (int i = 0; i < IN; ++i) P[((int64_t)b * IN + i) * G + g] = acc[i];
+}
+
+template <int IN>
+int bproj_launch_fwd(const float* x, const float* W, const float* zw, float* xp, int T, int B, int G, hipStream_t s) {
+    const int tz = (T + 31) / 32;   // time slices: >= 256 workgroups at B ~ 100
+    hipLaunchKernelGGL(bproj_fwd<IN>, dim3((G + 255) / 256, B, tz), dim3(256), 0, s, x, W, zw, xp, T, B, G,
+                       (T + tz - 1) / tz);
+    return SKR_CHECK_LAUNCH();
+}
+
+template <int IN>
+int bproj_launch_bwd(const float* x, const void* dxp, int kind, int64_t ld, float* S, float* P, int T, int B, int G,
+                     hipStream_t s) {
+    const dim3 grid((G + 255) / 256, B);
+    if (kind == 1)
+        hipLaunchKernelGGL((bproj_bwd<IN, true>), grid, dim3(256), 0, s, x, dxp, ld, S, P, T, B, G);
+    else
+        hipLaunchKernelGGL((bproj_bwd<IN, false>), grid, dim3(256), 0, s, x, dxp, ld, S, P, T, B, G);
+    return SKR_CHECK_LAUNCH();
+}
+
+}  // namespace
+
+// x [T, B, IN] fp32, W [IN, G] fp32 (the stroke rows), zw [B, G] fp32 or null -> xp [T, B, G] fp32.
+SKR_API int skr_bproj_fwd(const float* x, const float* W, const float* zw, float* xp, int T, int B, int IN, int G,
+                          hipStream_t s) {
+    if (T <= 0 || B <= 0 || G <= 0) return 0;
+    switch (IN) {
+        case 3: return bproj_launch_fwd<3>(x, W, zw, xp, T, B, G, s);
+        case 5: return bproj_launch_fwd<5>(x, W, zw, xp, T, B, G, s);
+        default: return -2;
+    }
+}
+
+// dxp [T, B, *] (row stride ld; kind 1 bf16, 2 fp32) -> S [B, G], P [B, IN, G].
+SKR_API int skr_bproj_bwd(const float* x, const void* dxp, int kind, int64_t ld, float* S, float* P, int T, int B,
+                          int IN, int G, hipStream_t s) {
+    if (T <= 0 || B <= 0 || G <= 0) return -2;
+    switch (IN) {
+        case 3: return bproj_launch_bwd<3>(x, dxp, kind, ld, S, P, T, B, G, s);
+        case 5: return bproj_launch_bwd<5>(x, dxp, kind, ld, S, P, T, B, G, s);
+        default: return -2;
+    }
+}

@@ -27,7 +27,7 @@ from .. import ops
 from ..config import VAEConfig
 from ..ops import gemm
 from . import cells as C
-from ..ops.inproj import bilstm_input_proj
+from ..ops.inproj import bilstm_input_proj, stroke_input_proj
 
 # dropout hash streams
 _S_ENC_FW, _S_ENC_BW, _S_DEC, _S_IN, _S_OUT, _S_EPS = 11, 13, 17, 23, 29, 31
@@ -150,26 +150,23 @@ class SketchVAE(nn.Module):
         """``x [T, B, 5]`` time-major -> ``(outputs [T, B, H], final_state)``."""
         cfg = self.cfg
         T, B, _ = x.shape
-        H = cfg.dec_rnn_size
-        if zc is not None:
-            x = torch.cat([x, zc.unsqueeze(0).expand(T, B, zc.shape[-1])], -1)
-        if train and cfg.use_input_dropout:
+        if train and cfg.use_input_dropout:   # the mask covers z too: no per-sequence factoring
+            if zc is not None:
+                x = torch.cat([x, zc.unsqueeze(0).expand(T, B, zc.shape[-1])], -1)
+                zc = None
             x = x * C.dropout_mask(seed, _S_IN, 0, x.shape, cfg.input_dropout_prob, x.device)
+        # otherwise z stays separate: its projection is computed once per sequence
         keep = cfg.recurrent_dropout_prob if (train and cfg.use_recurrent_dropout) else 1.0
         p = self.dec
         if cfg.dec_model == "hyper":
             h0, c0, hh0, hc0 = state
             hkeep = cfg.recurrent_dropout_prob if (train and cfg.hyper_use_recurrent_dropout) else 1.0
             out, final = ops.hyper_sequence(p, x, h0, c0, hh0, hc0, drop_keep=keep, drop_seed=seed,
-                                            drop_stream=_S_DEC, hyp_drop_keep=hkeep)
+                                            drop_stream=_S_DEC, hyp_drop_keep=hkeep, zc=zc)
         else:
             h0, c0 = state
-            xp = gemm.linear(x, p.W_x)
-            if cfg.dec_model == "layer_norm":
-                ln = (p.ln_gamma, p.ln_beta, p.lnc_gamma, p.lnc_beta)
-            else:
-                xp = xp + p.bias
-                ln = None
+            ln = (p.ln_gamma, p.ln_beta, p.lnc_gamma, p.lnc_beta) if cfg.dec_model == "layer_norm" else None
+            xp = stroke_input_proj(x, zc, p.W_x, None if ln else p.bias)
             out, final = ops.lstm_sequence(xp, p.W_h, h0, c0, drop_keep=keep, drop_seed=seed,
                                            drop_stream=_S_DEC, ln=ln)
         if train and cfg.use_output_dropout:

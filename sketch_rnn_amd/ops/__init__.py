@@ -98,11 +98,15 @@ def bilstm_sequence_packed(xp, W_f, W_b, h0, c0, drop_keep: float = 1.0, drop_se
 
 
 def hyper_sequence(p, x, h0, c0, hh0, hc0, forget_bias: float = 1.0, drop_keep: float = 1.0,
-                   drop_seed: int = 0, drop_stream: int = 0, hyp_drop_keep: float = 1.0):
+                   drop_seed: int = 0, drop_stream: int = 0, hyp_drop_keep: float = 1.0, zc=None):
+    """HyperLSTM over the input ``[x | zc broadcast over time]`` (``zc``
+    optional: a per-sequence input whose projection is computed once)."""
     if use_hip(x):
         from .recurrent import hyper_sequence_hip
         return hyper_sequence_hip(p, x, h0, c0, hh0, hc0, forget_bias, drop_keep, drop_seed,
-                                  drop_stream, hyp_drop_keep)
+                                  drop_stream, hyp_drop_keep, zc)
+    if zc is not None:
+        x = torch.cat([x, zc.unsqueeze(0).expand(x.shape[0], x.shape[1], zc.shape[-1])], -1)
     return hyper_sequence_torch(p, x, h0, c0, hh0, hc0, forget_bias, drop_keep, drop_seed,
                                 drop_stream, hyp_drop_keep)
 

@@ -176,6 +176,10 @@ class HipLib:
         lib.skr_inproj_fwd.restype = _i
         lib.skr_inproj_bwd.argtypes = [_p, _p, _p, _p, _i, _i, _i, _i, _i, _p]
         lib.skr_inproj_bwd.restype = _i
+        lib.skr_bproj_fwd.argtypes = [_p, _p, _p, _p, _i, _i, _i, _i, _p]
+        lib.skr_bproj_fwd.restype = _i
+        lib.skr_bproj_bwd.argtypes = [_p, _p, _i, _i64, _p, _p, _i, _i, _i, _i, _p]
+        lib.skr_bproj_bwd.restype = _i
         lib.skr_colsum.argtypes = [_p, _i, _p, _i64, _i64, _i64, _i64, _i, _i, _p, _p, _p]
         lib.skr_colsum.restype = _i
         lib.skr_gru_fwd.argtypes = [C.POINTER(GruFwdArgs), _i, _p]

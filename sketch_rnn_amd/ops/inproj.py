@@ -82,3 +82,80 @@ def bilstm_input_proj(x, lengths, W_f, W_b, b_f=None, b_b=None):
         if use_hip(x):
             return _BiInProj.apply(x, lengths, W_f, W_b, b_f, b_b)
     return bilstm_input_proj_torch(x, lengths, W_f, W_b, b_f, b_b)
+
+
+# ---- decoder: [stroke-5 | z] inputs with z broadcast over time ------------------------
+def bproj_ok(x) -> bool:
+    return x.is_cuda and x.shape[-1] in (3, 5)
+
+
+def bproj_fwd(x, W, zw=None):
+    """``xp[t, b] = x[t, b] @ W + zw[b]`` (csrc/inproj.hip ``skr_bproj_fwd``)."""
+    lib = native.require_hip()
+    T, B, IN = x.shape
+    G = W.shape[1]
+    x = x.contiguous().float()
+    W = W.contiguous().float()
+    zw = zw.contiguous().float() if zw is not None else None
+    xp = torch.empty(T, B, G, device=x.device, dtype=torch.float32)
+    rc = lib.lib.skr_bproj_fwd(x.data_ptr(), W.data_ptr(), None if zw is None else zw.data_ptr(), xp.data_ptr(),
+                               T, B, IN, G, torch.cuda.current_stream().cuda_stream)
+    if rc != 0:
+        raise RuntimeError("skr_bproj_fwd failed (%d)" % rc)
+    return xp
+
+
+def bproj_reduce(x, dxp):
+    """One read of ``dxp [T, B, G]`` (fp32 or bf16, rows may be strided):
+    ``S[b] = sum_t dxp[t, b]`` and ``P = sum_{t,b} x[t, b]^T dxp[t, b]`` ([IN, G])."""
+    lib = native.require_hip()
+    T, B, IN = x.shape
+    G = dxp.shape[-1]
+    assert dxp.stride(-1) == 1 and dxp.stride(0) == B * dxp.stride(1)
+    kind = 1 if dxp.dtype == torch.bfloat16 else 2
+    if kind == 2 and dxp.dtype != torch.float32:
+        dxp = dxp.float().contiguous()
+    S = torch.empty(B, G, device=x.device, dtype=torch.float32)
+    P = torch.empty(B, IN, G, device=x.device, dtype=torch.float32)
+    rc = lib.lib.skr_bproj_bwd(x.contiguous().data_ptr(), dxp.data_ptr(), kind, dxp.stride(1), S.data_ptr(),
+                               P.data_ptr(), T, B, IN, G, torch.cuda.current_stream().cuda_stream)
+    if rc != 0:
+        raise RuntimeError("skr_bproj_bwd failed (%d)" % rc)
+    return S, P.sum(0)
+
+
+class _BProj(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, zc, W, bias):
+        IN = x.shape[-1]
+        zw = None
+        if zc is not None:
+            zw = zc @ W[IN:]
+        if bias is not None:
+            zw = bias.expand(x.shape[1], -1) if zw is None else zw + bias
+        ctx.save_for_backward(x, zc, W)
+        ctx.has_bias = bias is not None
+        return bproj_fwd(x, W[:IN], zw)
+
+    @staticmethod
+    def backward(ctx, dxp):
+        x, zc, W = ctx.saved_tensors
+        IN = x.shape[-1]
+        S, P = bproj_reduce(x, dxp.contiguous())
+        dW = P if zc is None else torch.cat([P, zc.t() @ S], 0)
+        dzc = S @ W[IN:].t() if zc is not None and ctx.needs_input_grad[1] else None
+        db = S.sum(0) if ctx.has_bias else None
+        return None, dzc, dW, db
+
+
+def stroke_input_proj(x, zc, W, bias=None):
+    """``[x | zc broadcast over T] @ W + bias`` -> ``[T, B, G]`` fp32 with the
+    z part computed once per sequence (x: data, no gradient)."""
+    from . import use_hip
+    if bproj_ok(x) and not x.requires_grad and use_hip(x):
+        return _BProj.apply(x, zc, W, bias)
+    T, B, _ = x.shape
+    xin = x if zc is None else torch.cat([x, zc.unsqueeze(0).expand(T, B, zc.shape[-1])], -1)
+    from . import gemm
+    xp = gemm.linear(xin, W)
+    return xp + bias if bias is not None else xp

@@ -32,6 +32,7 @@ import torch
 from ..utils import native
 from . import gemm
 from ._hipapi import FusedBwdArgs, FusedFwdArgs, LstmBwdArgs, LstmFwdArgs
+from .inproj import bproj_fwd, bproj_ok, bproj_reduce
 from .reduce import colsum
 
 
@@ -445,26 +446,34 @@ class _HyperSeq(torch.autograd.Function):
     """
 
     @staticmethod
-    def forward(ctx, x, h0, c0, hh0, hc0, seed, W_x, W_h, bias, hW_x, hW_h, hln_g, hln_b, hlnc_g, hlnc_b,
+    def forward(ctx, x, zc, h0, c0, hh0, hc0, seed, W_x, W_h, bias, hW_x, hW_h, hln_g, hln_b, hlnc_g, hlnc_b,
                 W_z, b_z, W_a, ln_g, ln_b, lnc_g, lnc_b, meta):
         forget_bias, keep, hkeep, stream, E, infer = meta   # infer: no autograd graph is being built
         lib = native.require_hip()
-        T, B, IN = x.shape
+        T, B, IX = x.shape                      # input = [x | zc broadcast over T]
+        IN = W_x.shape[0]
         H, Hh = W_h.shape[0], hW_h.shape[0]
         G, Gh = 4 * H, 4 * Hh
         K = H + Hh
         dev = x.device
         f32 = torch.float32
         TB = T * B
-        x2 = x.reshape(TB, IN).contiguous()
-        xl = gemm.lp(x2)
-        if infer:
-            XH = gemm.mm(xl, gemm.derived(W_x, "lp%s" % gemm.lp_dtype(), gemm.lp)).view(T, B, G)
-            XHY = gemm.mm(xl, gemm.derived(hW_x, "lpx%d%s" % (IN, gemm.lp_dtype()),
-                                           lambda W: gemm.lp(W[:IN]).contiguous())).view(T, B, Gh)
+        bp = bproj_ok(x) and not x.requires_grad
+        xl = None
+        if bp:   # stroke rows per position, z rows once per sequence (csrc/inproj.hip)
+            XH = bproj_fwd(x, W_x[:IX], zc @ W_x[IX:] if zc is not None else None)
+            XHY = bproj_fwd(x, hW_x[:IX], zc @ hW_x[IX:IN] if zc is not None else None)
         else:
-            XH = gemm.mm(xl, gemm.lp(W_x)).view(T, B, G)
-            XHY = gemm.mm(xl, gemm.lp(hW_x[:IN])).view(T, B, Gh)
+            if zc is not None:
+                x = torch.cat([x, zc.unsqueeze(0).expand(T, B, zc.shape[-1])], -1)
+            xl = gemm.lp(x.reshape(TB, IN).contiguous())
+            if infer:
+                XH = gemm.mm(xl, gemm.derived(W_x, "lp%s" % gemm.lp_dtype(), gemm.lp)).view(T, B, G)
+                XHY = gemm.mm(xl, gemm.derived(hW_x, "lpx%d%s" % (IN, gemm.lp_dtype()),
+                                               lambda W: gemm.lp(W[:IN]).contiguous())).view(T, B, Gh)
+            else:
+                XH = gemm.mm(xl, gemm.lp(W_x)).view(T, B, G)
+                XHY = gemm.mm(xl, gemm.lp(hW_x[:IN])).view(T, B, Gh)
         dt = gemm.lp_dtype()
 
         def wy(hW_x, hW_h):                      # [K, Gh]: B^T of dR_hyp @ W_y^T
@@ -579,19 +588,19 @@ class _HyperSeq(torch.autograd.Function):
         hT = HC[(T - 1) % 2].clone()
         hhT = HHC[(T - 1) % 2].clone()
         s = _Saved()
-        for k, v in dict(xl=xl, XH=XH, Whl=Whl, Wyl=Wyl, Pl=Pl, q=q, bias_c=bias_c, S_m=S_m, A=A, RM=RM, CC=CC,
+        for k, v in dict(xl=xl, x=x, zc=zc, bp=bp, XH=XH, Whl=Whl, Wyl=Wyl, Pl=Pl, q=q, bias_c=bias_c, S_m=S_m, A=A, RM=RM, CC=CC,
                          HCC=HCC, Cout=Cout, ACT=ACT, XHAT=XHAT, RSTD=RSTD, CHAT=CHAT, HH=HH, HCout=HCout,
                          HACT=HACT, HXHAT=HXHAT, HRSTD=HRSTD, HCHAT=HCHAT, VEC=VEC, seed=sd, meta=meta, W_x=W_x,
                          hW_x=hW_x, W_z=W_z, b_z=b_z, W_a=W_a, mln=mln, hln=hln).items():
             setattr(s, k, v)
         ctx.s = s
-        ctx.dims = (T, B, IN, H, Hh, E)
+        ctx.dims = (T, B, IX, IN, H, Hh, E)
         return Hout, hT, CC[T].clone(), hhT, HCC[T].clone()
 
     @staticmethod
     def backward(ctx, dHout, dhT, dcT, dhhT, dhcT):
         s = ctx.s
-        T, B, IN, H, Hh, E = ctx.dims
+        T, B, IX, IN, H, Hh, E = ctx.dims
         forget_bias, keep, hkeep, stream, _, _ = s.meta
         lib = native.require_hip()
         dev = s.A.device
@@ -686,11 +695,28 @@ class _HyperSeq(torch.autograd.Function):
         dhW_x = torch.empty_like(s.hW_x)
         dhW_x[IN:] = dW_y[:H]
         dhW_h = dW_y[H:]
-        dXHl, dXHYl = gemm.lp(dXH.view(TB, G)), gemm.lp(dRY_lp.view(TB, Gh))
-        dW_x = gemm.mm(s.xl.t(), dXHl)
-        dhW_x[:IN] = gemm.mm(s.xl.t(), dXHYl)
-        dx = gemm.mm(dXHl, gemm.lp(s.W_x).t())
-        dx += gemm.mm(dXHYl, gemm.lp(s.hW_x[:IN]).t())
+        dx = dzc = None
+        if s.bp:   # input-side gradients from one read of dXH / dR_hyp each
+            S_m, P_m = bproj_reduce(s.x, dXH)
+            S_y, P_y = bproj_reduce(s.x, dRY_lp)
+            if s.zc is not None:
+                dW_x = torch.cat([P_m, s.zc.t() @ S_m], 0)
+                dhW_x[:IN] = torch.cat([P_y, s.zc.t() @ S_y], 0)
+                dzc = S_m @ s.W_x[IX:].t() + S_y @ s.hW_x[IX:IN].t()
+            else:
+                dW_x = P_m
+                dhW_x[:IN] = P_y
+        else:
+            dXHl, dXHYl = gemm.lp(dXH.view(TB, G)), gemm.lp(dRY_lp.view(TB, Gh))
+            dW_x = gemm.mm(s.xl.t(), dXHl)
+            dhW_x[:IN] = gemm.mm(s.xl.t(), dXHYl)
+            dxf = gemm.mm(dXHl, gemm.lp(s.W_x).t())
+            dxf += gemm.mm(dXHYl, gemm.lp(s.hW_x[:IN]).t())
+            dxf = dxf.view(T, B, IN)
+            if s.zc is not None:
+                dx, dzc = dxf[..., :IX], dxf[..., IX:].sum(0)
+            else:
+                dx = dxf
         # hyper-norm projections: vec_k = zs_k @ W_a[k], zs = hh @ W_z + b_z
         dV12 = dVEC.view(TB, 12, H).transpose(0, 1)                    # [12, TB, H] (strided)
         Wal = gemm.lp(s.W_a)
@@ -706,18 +732,18 @@ class _HyperSeq(torch.autograd.Function):
         g_ln = colsum(DLNY.view(TB, G), s.XHAT.view(TB, G)) + colsum(DLNCY.view(TB, H), s.CHAT.view(TB, H))
         g_hln = colsum(HDLNY.view(TB, Gh), s.HXHAT.view(TB, Gh)) + colsum(HDLNCY.view(TB, Hh), s.HCHAT.view(TB, Hh))
         ctx.s = None
-        return (dx.view(T, B, IN), dh0, dc_rec, dhh0, dhc_rec, None, dW_x, dW_h, dbias, dhW_x, dhW_h,
+        return (dx, dzc, dh0, dc_rec, dhh0, dhc_rec, None, dW_x, dW_h, dbias, dhW_x, dhW_h,
                 g_hln[0], g_hln[1], g_hln[2], g_hln[3], dW_z, db_z, dWa, g_ln[0], g_ln[1], g_ln[2], g_ln[3], None)
 
 
 def hyper_sequence_hip(p, x, h0, c0, hh0, hc0, forget_bias=1.0, drop_keep=1.0, drop_seed=0, drop_stream=0,
-                       hyp_drop_keep=1.0):
+                       hyp_drop_keep=1.0, zc=None):
     if not p.use_layer_norm:
         raise NotImplementedError("HIP HyperLSTM path requires use_layer_norm=True")
-    outs = _HyperSeq.apply(x, h0, c0, hh0, hc0, drop_seed, p.W_x, p.W_h, p.bias, p.hyp_W_x, p.hyp_W_h,
+    outs = _HyperSeq.apply(x, zc, h0, c0, hh0, hc0, drop_seed, p.W_x, p.W_h, p.bias, p.hyp_W_x, p.hyp_W_h,
                            p.hyp_ln_gamma, p.hyp_ln_beta, p.hyp_lnc_gamma, p.hyp_lnc_beta, p.W_z, p.b_z, p.W_a,
                            p.ln_gamma, p.ln_beta, p.lnc_gamma, p.lnc_beta,
                            (float(forget_bias), float(drop_keep), float(hyp_drop_keep), int(drop_stream), p.embed,
-                            _inference(x, h0, p.W_h, p.W_x)))
+                            _inference(x, zc, h0, p.W_h, p.W_x)))
     Hout, hT, cT, hhT, hcT = outs
     return Hout, (hT, cT, hhT, hcT)

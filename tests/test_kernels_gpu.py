@@ -287,6 +287,54 @@ def test_bilstm_input_proj_matches_torch(with_bias):
     _close(grads[0], grads[1], 1e-4, 1e-3, "grad")
 
 
+@pytest.mark.parametrize("with_z,with_bias", [(True, True), (False, True), (True, False)])
+def test_stroke_input_proj_matches_torch(with_z, with_bias):
+    """csrc/inproj.hip bproj: [x | z broadcast] @ W + b with the z part once
+    per sequence, and its W / bias / z gradients from one read of dxp."""
+    from sketch_rnn_amd.ops.inproj import stroke_input_proj
+    torch.manual_seed(8)
+    T, B, IN, Z, G = 29, 11, 5, 16, 512
+    x = torch.randn(T, B, IN, device=DEV)
+    zc = torch.randn(B, Z, device=DEV, requires_grad=True) if with_z else None
+    W = torch.randn(IN + (Z if with_z else 0), G, device=DEV, requires_grad=True)
+    b = torch.randn(G, device=DEV, requires_grad=True) if with_bias else None
+    w = torch.randn(T, B, G, device=DEV)
+    res = []
+    for backend in ("hip", "torch"):
+        ops.set_backend(backend)
+        ins = [t.detach().clone().requires_grad_() if t is not None else None for t in (zc, W, b)]
+        y = stroke_input_proj(x, ins[0], ins[1], ins[2])
+        (y * w).sum().backward()
+        res.append([y.detach()] + [t.grad for t in ins if t is not None])
+    _close(res[0][:1], res[1][:1], 1e-5, 1e-5, "xp")
+    _close(res[0][1:], res[1][1:], 1e-4, 1e-3, "grad")
+
+
+def test_hyper_sequence_with_broadcast_z_matches_oracle():
+    """HyperLSTM with a stroke-5 input + per-sequence z (bproj path) vs the
+    oracle on the concatenated input."""
+    torch.manual_seed(9)
+    T, B, IX, Z, H, Hh, E = 6, 5, 5, 12, 256, 64, 8
+    p = C.HyperLSTMParams(IX + Z, H, Hh, E).to(DEV)
+    with torch.no_grad():
+        for prm in p.parameters():
+            prm.add_(torch.randn_like(prm) * 0.05)
+    x = torch.randn(T, B, IX, device=DEV)
+    zc = torch.randn(B, Z, device=DEV, requires_grad=True)
+    st = [torch.randn(B, n, device=DEV).mul(0.3) for n in (H, H, Hh, Hh)]
+    w = torch.randn(T, B, H, device=DEV)
+    res = []
+    for backend in ("hip", "torch"):
+        ops.set_backend(backend)
+        p.zero_grad()
+        z = zc.detach().clone().requires_grad_()
+        out, _ = ops.hyper_sequence(p, x, *st, drop_keep=0.9, drop_seed=4, drop_stream=9, zc=z)
+        (out * w).sum().backward()
+        res.append([out.detach(), z.grad] + [q.grad.clone() for q in p.parameters()])
+    _close(res[0][:1], res[1][:1], 2e-4, 2e-5, "out")
+    _close(res[0][1:], res[1][1:], 2e-3, 2e-4, "grad")
+
+
 def test_grouped_skinny_gemm_matches_torch():
     """Independent products in one grouped launch (csrc/skinny_gemm.hip)."""
     from sketch_rnn_amd.ops import gemm
