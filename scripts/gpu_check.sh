@@ -30,6 +30,7 @@ for s in "${steps[@]}"; do
         pytest) run pytest_gpu 900 python -m pytest tests -m gpu -q --maxfail=10 ;;
         pytest_sel) run pytest_sel 600 python -m pytest tests -m gpu -q --maxfail=10 -k "${PYTEST_K:-fused}" ;;
         bench_nofused) SKR_FUSED=0 run bench_nofused 600 python bench.py --steps 10 --warmup 2 ;;
+        bench_wgrad) run bench_wgrad 600 python scripts/bench_wgrad.py ;;
         bench_gemm) run bench_gemm 600 python scripts/bench_gemm.py ;;
         smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
         bench) run bench 600 python bench.py --steps 10 --warmup 2 ;;

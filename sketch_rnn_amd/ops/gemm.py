@@ -249,7 +249,8 @@ class _Linear(torch.autograd.Function):
         if ctx.needs_input_grad[1]:
             dW = mm(xl.t(), dyl)
         if ctx.has_b and ctx.needs_input_grad[2]:
-            db = dy2.sum(0)
+            from .reduce import colsum
+            db = colsum(dy2)[1]   # torch's dim-0 sum is ~0.35 ms on [25000, 123]
         return dx, dW, db
 
 

@@ -12,8 +12,11 @@ from typing import Optional, Tuple
 import torch
 
 
-def colsum(x: torch.Tensor, y: Optional[torch.Tensor] = None, splits: int = 32
+def colsum(x: torch.Tensor, y: Optional[torch.Tensor] = None, splits: Optional[int] = None
            ) -> Tuple[Optional[torch.Tensor], torch.Tensor]:
+    """``splits``: row slices (workgroups per 256 columns); default fills
+    ~1024 workgroups, so narrow outputs (a head bias: 123 columns) still
+    spread over the chip."""
     if x.dim() == 2:
         x = x.unsqueeze(0)
         y = y.unsqueeze(0) if y is not None else None
@@ -28,7 +31,9 @@ def colsum(x: torch.Tensor, y: Optional[torch.Tensor] = None, splits: int = 32
     R1, R2, C = x.shape
     if y is not None:
         assert y.dtype == torch.float32 and y.shape == x.shape and y.stride() == x.stride()
-    RS = max(1, min(splits, (R1 * R2) // 64))
+    if splits is None:
+        splits = -(-1024 // -(-C // 256))
+    RS = max(1, min(splits, (R1 * R2) // 16))
     part = torch.empty(2, RS, C, device=x.device, dtype=torch.float32)
     kind = 1 if x.dtype == torch.bfloat16 else 2
     assert x.dtype in (torch.bfloat16, torch.float32)
