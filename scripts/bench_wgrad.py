@@ -28,7 +28,14 @@ def main():
     out = torch.empty(2048, 8192, device=dev)
     outT = torch.empty(8192, 2048, device=dev)
     fl = 2 * TB * 2048 * 8192
+    def splitk(a, b, S):   # a [K, M], b [K, N] -> sum_s a_s^T b_s via one bmm
+        K = a.shape[0]
+        return torch.bmm(a.view(S, K // S, -1).transpose(1, 2), b.view(S, K // S, -1),
+                         out_dtype=torch.float32).sum(0)
+
     for name, fn in [
+        ("dW_h  splitK2", lambda: splitk(A2c, dRM, 2)),
+        ("dW_h  splitK5", lambda: splitk(A2c, dRM, 5)),
         ("dW_h  A^T@B strided A", lambda: torch.mm(A2[:, :2048].t(), dRM, out_dtype=torch.float32, out=out)),
         ("dW_h  A^T@B contig A", lambda: torch.mm(A2c.t(), dRM, out_dtype=torch.float32, out=out)),
         ("dW_h^T B^T@A", lambda: torch.mm(dRM.t(), A2[:, :2048], out_dtype=torch.float32, out=outT)),
@@ -55,6 +62,12 @@ def main():
         ("enc dW 2x mm (contig)", lambda: [torch.mm(An[d].t(), dGn[d], out_dtype=torch.float32, out=o1[d])
                                             for d in range(2)]),
         ("enc dW bmm^T", lambda: torch.bmm(dGn.transpose(1, 2), An, out_dtype=torch.float32)),
+        ("enc dW splitK5", lambda: torch.bmm(An.view(10, 5000, 512).transpose(1, 2), dGn.view(10, 5000, 2048),
+                                             out_dtype=torch.float32).view(2, 5, 512, 2048).sum(1)),
+        ("enc dW splitK10", lambda: torch.bmm(An.view(20, 2500, 512).transpose(1, 2), dGn.view(20, 2500, 2048),
+                                              out_dtype=torch.float32).view(2, 10, 512, 2048).sum(1)),
+        ("enc dW splitK25", lambda: torch.bmm(An.view(50, 1000, 512).transpose(1, 2), dGn.view(50, 1000, 2048),
+                                              out_dtype=torch.float32).view(2, 25, 512, 2048).sum(1)),
     ]:
         us = timeit(fn)
         print("%-26s %8.1f us  %6.1f TFLOP/s" % (name, us, fl / us / 1e6), flush=True)
@@ -65,6 +78,8 @@ def main():
     for name, fn in [
         ("dP HH1^T@dVEC (M=264)", lambda: torch.mm(HH.t(), dV, out_dtype=torch.float32)),
         ("dP^T dVEC^T@HH1", lambda: torch.mm(dV.t(), HH, out_dtype=torch.float32)),
+        ("dP splitK5", lambda: splitk(HH, dV, 5)),
+        ("dP splitK10", lambda: splitk(HH, dV, 10)),
     ]:
         us = timeit(fn)
         print("%-26s %8.1f us  %6.1f TFLOP/s" % (name, us, fl / us / 1e6), flush=True)

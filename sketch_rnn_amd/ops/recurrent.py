@@ -344,11 +344,11 @@ class _LSTMSeq(torch.autograd.Function):
         dh_rec = DH.sum(0) if DH.shape[0] > 1 else DH[0]
         dGs = dG_lp if lp_on else dG
         if nd == 1:
-            dW = gemm.mm(s.A[:T].reshape(T * BB, H).t(), dGs.view(T * BB, G)).view(s.wshape)
+            dW = gemm.wgrad(s.A[:T].reshape(T * BB, H), dGs.view(T * BB, G)).view(s.wshape)
         else:
             An = s.A[:T].view(T, nd, B, H).permute(1, 0, 2, 3).reshape(nd, T * B, H)
             dGn = dGs.view(T, nd, B, G).permute(1, 0, 2, 3).reshape(nd, T * B, G)
-            dW = gemm.bmm(An.transpose(1, 2), dGn).view(s.wshape)
+            dW = gemm.wgrad(An, dGn).view(s.wshape)
         g_ln = [None] * 4
         if ln:
             def red(x, y, n):   # per direction group: rows (t, b) of the [T, nd, B, n] stream
@@ -690,8 +690,8 @@ class _HyperSeq(torch.autograd.Function):
         dhh0 = DAY[:, :, H:].sum(0)
         # ---- weight gradients: single large GEMMs over all T*B rows ----
         A2 = s.A[:T].reshape(TB, K)
-        dW_h = gemm.mm(A2[:, :H].t(), dRM_lp.view(TB, G))
-        dW_y = gemm.mm(A2.t(), dRY_lp.view(TB, Gh))
+        dW_h = gemm.wgrad(A2[:, :H], dRM_lp.view(TB, G))
+        dW_y = gemm.wgrad(A2, dRY_lp.view(TB, Gh))
         dhW_x = torch.empty_like(s.hW_x)
         dhW_x[IN:] = dW_y[:H]
         dhW_h = dW_y[H:]
@@ -708,8 +708,8 @@ class _HyperSeq(torch.autograd.Function):
                 dhW_x[:IN] = P_y
         else:
             dXHl, dXHYl = gemm.lp(dXH.view(TB, G)), gemm.lp(dRY_lp.view(TB, Gh))
-            dW_x = gemm.mm(s.xl.t(), dXHl)
-            dhW_x[:IN] = gemm.mm(s.xl.t(), dXHYl)
+            dW_x = gemm.wgrad(s.xl, dXHl)
+            dhW_x[:IN] = gemm.wgrad(s.xl, dXHYl)
             dxf = gemm.mm(dXHl, gemm.lp(s.W_x).t())
             dxf += gemm.mm(dXHYl, gemm.lp(s.hW_x[:IN]).t())
             dxf = dxf.view(T, B, IN)
@@ -717,18 +717,20 @@ class _HyperSeq(torch.autograd.Function):
                 dx, dzc = dxf[..., :IX], dxf[..., IX:].sum(0)
             else:
                 dx = dxf
-        # hyper-norm projections: vec_k = zs_k @ W_a[k], zs = hh @ W_z + b_z
-        dV12 = dVEC.view(TB, 12, H).transpose(0, 1)                    # [12, TB, H] (strided)
-        Wal = gemm.lp(s.W_a)
-        dZS12 = gemm.bmm(dV12, Wal.transpose(1, 2))                    # [12, TB, E]
-        HHm = s.HH.view(TB, Hh)
-        ZS = torch.addmm(s.b_z, HHm, s.W_z)                            # [TB, 12E]
-        ZS12 = gemm.lp(ZS.view(TB, 12, E).transpose(0, 1))             # [12, TB, E]
-        dWa = gemm.bmm(ZS12.transpose(1, 2), dV12)                     # [12, E, H]
-        dZS = dZS12.transpose(0, 1).reshape(TB, 12 * E)
-        dW_z = HHm.t() @ dZS
-        db_z = dZS.sum(0)
-        _, dbias = colsum(dVEC.view(TB, 12 * H)[:, 8 * H:])          # shift-vector grads = bias grads
+        # hyper-norm projections, vec_k = (hh @ W_z_k + b_z_k) @ W_a_k: ONE long-K
+        # GEMM dP = [hh | 1]^T @ dvec gives dP_k = hh^T dvec_k and (ones row) the
+        # column sums of dvec; the per-k factors are then tiny batched products
+        HH1 = torch.zeros(TB, Hh + 8, device=dev, dtype=ldt)
+        HH1[:, :Hh] = s.HH.view(TB, Hh)
+        HH1[:, Hh] = 1.0
+        dP1 = gemm.wgrad(HH1, dVEC.view(TB, 12 * H))                   # [Hh + 8, 12H] fp32
+        dP = dP1[:Hh].view(Hh, 12, H).transpose(0, 1)                  # [12, Hh, H]
+        sV = dP1[Hh].view(12, H)                                       # column sums of dvec
+        Wz3 = s.W_z.view(Hh, 12, E).transpose(0, 1)                    # [12, Hh, E]
+        dW_z = torch.bmm(dP, s.W_a.transpose(1, 2)).transpose(0, 1).reshape(Hh, 12 * E)
+        dWa = torch.bmm(Wz3.transpose(1, 2), dP) + s.b_z.view(12, E, 1) * sV.view(12, 1, H)
+        db_z = torch.bmm(sV.view(12, 1, H), s.W_a.transpose(1, 2)).reshape(12 * E)
+        dbias = sV[8:].reshape(4 * H)                                  # shift-vector grads = bias grads
         g_ln = colsum(DLNY.view(TB, G), s.XHAT.view(TB, G)) + colsum(DLNCY.view(TB, H), s.CHAT.view(TB, H))
         g_hln = colsum(HDLNY.view(TB, Gh), s.HXHAT.view(TB, Gh)) + colsum(HDLNCY.view(TB, Hh), s.HCHAT.view(TB, Hh))
         ctx.s = None

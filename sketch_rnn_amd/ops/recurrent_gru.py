@@ -116,10 +116,10 @@ class _GRUSeq(torch.autograd.Function):
             cur = 1 - cur
         dh0 = DE[cur] + DHG.sum(0)
         dpg2, dpc2 = DPG_lp.view(TB, 2 * H), DPC_lp.view(TB, H)
-        dW_gh = gemm.mm(HL[:T].reshape(TB, H).t(), dpg2)
-        dW_ch = gemm.mm(RH.reshape(TB, H).t(), dpc2)
-        dW_gx = gemm.mm(xl.t(), dpg2)
-        dW_cx = gemm.mm(xl.t(), dpc2)
+        dW_gh = gemm.wgrad(HL[:T].reshape(TB, H), dpg2)
+        dW_ch = gemm.wgrad(RH.reshape(TB, H), dpc2)
+        dW_gx = gemm.wgrad(xl, dpg2)
+        dW_cx = gemm.wgrad(xl, dpc2)
         db_g, db_c = DPG.view(TB, 2 * H).sum(0), DPC.view(TB, H).sum(0)
         dx = gemm.mm(dpg2, gemm.lp(W_gx).t()) + gemm.mm(dpc2, gemm.lp(W_cx).t())
         return (dx.view(T, B, -1), dh0, None, dinit, dW_gx, dW_gh, db_g, dW_cx, dW_ch, db_c)
