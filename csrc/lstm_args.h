@@ -14,7 +14,7 @@ struct FwdArgs {
     const float* xp; int64_t ld_xp;    // [B, 4H]: x-projection (+bias unless MOD)
     const float* R;  int64_t ld_R;     // [B, 4H]: h_prev @ W_h (fp32)
     int R_nslab; int64_t R_slab;       // R is the sum of R_nslab split-K partial slabs
-    const float* vec; int64_t vec_gs; int64_t vec_ld;  // MOD: element (k,b,u) at k*gs + b*ld + u
+    const void* vec; int64_t vec_gs; int64_t vec_ld;   // MOD: element (k,b,u) at k*gs + b*ld + u (mod 1 fp32, 2 bf16)
     const float* vec_bias;             // MOD: [12, H] added to vec (required)
     const float* bias;                 // MOD: [4H]
     const float* c_prev;               // [B, H]
@@ -56,7 +56,7 @@ struct BwdArgs {
     const float* xp; int64_t ld_xp;    // MOD: xh
     const float* R;  int64_t ld_R;     // MOD: R
     int R_nslab; int64_t R_slab;
-    const float* vec; int64_t vec_gs; int64_t vec_ld;  // MOD
+    const void* vec; int64_t vec_gs; int64_t vec_ld;   // MOD (mod 1 fp32, 2 bf16)
     const float* vec_bias;
     const float* reset;
     float keep; const int64_t* seed; uint32_t stream, step;
@@ -69,6 +69,13 @@ struct BwdArgs {
     float* dinit_h; float* dinit_c;    // [B, H] accumulated on reset rows (or null)
     int cluster; uint64_t* part; int* err;
 };
+
+// hyper modulation vectors: MOD 1 fp32, MOD 2 bf16
+template <int MOD>
+__device__ __forceinline__ float ldvec(const void* v, int64_t i) {
+    if constexpr (MOD == 2) return __bfloat162float(((const __hip_bfloat16*)v)[i]);
+    else return ((const float*)v)[i];
+}
 
 __device__ __forceinline__ float dropout_mult(bool on, uint32_t key, int64_t idx, float keep) {
     if (!on) return 1.f;

@@ -125,7 +125,7 @@ __device__ __forceinline__ void row_sum(float (&v)[N], float* lds, float* mine, 
     }
 }
 
-template <int NT, int UPT, int NS, bool LN, bool MOD>
+template <int NT, int UPT, int NS, bool LN, int MOD>
 __global__ __launch_bounds__(NT) void cell_fwd(const FwdArgs a) {
     constexpr int NW = NT / 64;
     __shared__ float lds[NW * 8];
@@ -157,9 +157,9 @@ __global__ __launch_bounds__(NT) void cell_fwd(const FwdArgs a) {
             const float rv = slab_sum<NS>(a.R, b * a.ld_R + q * H + uc, a.R_nslab, a.R_slab);
             if (MOD) {
                 const int64_t vo = (int64_t)b * a.vec_ld + uc;
-                const float ax = a.vec[q * a.vec_gs + vo] + a.vec_bias[q * H + uc];
-                const float ah = a.vec[(4 + q) * a.vec_gs + vo] + a.vec_bias[(4 + q) * H + uc];
-                const float bh = a.vec[(8 + q) * a.vec_gs + vo] + a.vec_bias[(8 + q) * H + uc];
+                const float ax = ldvec<MOD>(a.vec, q * a.vec_gs + vo) + a.vec_bias[q * H + uc];
+                const float ah = ldvec<MOD>(a.vec, (4 + q) * a.vec_gs + vo) + a.vec_bias[(4 + q) * H + uc];
+                const float bh = ldvec<MOD>(a.vec, (8 + q) * a.vec_gs + vo) + a.vec_bias[(8 + q) * H + uc];
                 g[k][q] = xv * ax + rv * ah + bh + a.bias[q * H + uc];
             } else {
                 g[k][q] = xv + rv;
@@ -309,7 +309,7 @@ __global__ __launch_bounds__(NT) void cell_fwd(const FwdArgs a) {
     }
 }
 
-template <int NT, int UPT, int NS, bool LN, bool MOD>
+template <int NT, int UPT, int NS, bool LN, int MOD>
 __global__ __launch_bounds__(NT) void cell_bwd(const BwdArgs a) {
     constexpr int NW = NT / 64;
     __shared__ float lds[NW * 8];
@@ -360,8 +360,8 @@ __global__ __launch_bounds__(NT) void cell_bwd(const BwdArgs a) {
             for (int q = 0; q < 4; ++q) {
                 xv[k][q] = a.xp[b * a.ld_xp + q * H + uc];
                 rv[k][q] = slab_sum<NS>(a.R, b * a.ld_R + q * H + uc, a.R_nslab, a.R_slab);
-                ax[k][q] = a.vec[q * a.vec_gs + vo] + a.vec_bias[q * H + uc];
-                ah[k][q] = a.vec[(4 + q) * a.vec_gs + vo] + a.vec_bias[(4 + q) * H + uc];
+                ax[k][q] = ldvec<MOD>(a.vec, q * a.vec_gs + vo) + a.vec_bias[q * H + uc];
+                ah[k][q] = ldvec<MOD>(a.vec, (4 + q) * a.vec_gs + vo) + a.vec_bias[(4 + q) * H + uc];
             }
         }
     }
@@ -471,20 +471,22 @@ template <typename A>
 using KernelT = void (*)(const A);
 
 template <int NT, int UPT, int NS>
-KernelT<FwdArgs> pick(bool ln, bool mod, const FwdArgs*) {
-    if (mod) return cell_fwd<NT, UPT, NS, true, true>;
-    if (ln) return cell_fwd<NT, UPT, NS, true, false>;
-    return cell_fwd<NT, UPT, NS, false, false>;
+KernelT<FwdArgs> pick(bool ln, int mod, const FwdArgs*) {
+    if (mod == 2) return cell_fwd<NT, UPT, NS, true, 2>;
+    if (mod) return cell_fwd<NT, UPT, NS, true, 1>;
+    if (ln) return cell_fwd<NT, UPT, NS, true, 0>;
+    return cell_fwd<NT, UPT, NS, false, 0>;
 }
 template <int NT, int UPT, int NS>
-KernelT<BwdArgs> pick(bool ln, bool mod, const BwdArgs*) {
-    if (mod) return cell_bwd<NT, UPT, NS, true, true>;
-    if (ln) return cell_bwd<NT, UPT, NS, true, false>;
-    return cell_bwd<NT, UPT, NS, false, false>;
+KernelT<BwdArgs> pick(bool ln, int mod, const BwdArgs*) {
+    if (mod == 2) return cell_bwd<NT, UPT, NS, true, 2>;
+    if (mod) return cell_bwd<NT, UPT, NS, true, 1>;
+    if (ln) return cell_bwd<NT, UPT, NS, true, 0>;
+    return cell_bwd<NT, UPT, NS, false, 0>;
 }
 
 template <int NT, int UPT, typename A>
-KernelT<A> pick_ns(const A& a, bool ln, bool mod) {
+KernelT<A> pick_ns(const A& a, bool ln, int mod) {
     // the backward reads R only with MOD
     const int ns = (std::is_same<A, FwdArgs>::value || mod) ? a.R_nslab : 1;
     switch (ns) {
@@ -500,7 +502,7 @@ KernelT<A> pick_ns(const A& a, bool ln, bool mod) {
 // units run on 1024-thread workgroups (one row per CU, no exchange);
 // otherwise 256 threads with UPT units each.
 template <typename A>
-int launch(const A& a, bool ln, bool mod, hipStream_t s) {
+int launch(const A& a, bool ln, int mod, hipStream_t s) {
     if (mod && !ln) return -3;
     if (a.B <= 0) return 0;
     const int H = a.H;
@@ -534,11 +536,11 @@ int launch(const A& a, bool ln, bool mod, hipStream_t s) {
 // mirrors of FwdArgs / BwdArgs in sketch_rnn_amd/ops/_hipapi.py).
 // args->cluster = C workgroups per row (<= 1: one).
 SKR_API int skr_lstm_fwd_step(const FwdArgs* args, int ln, int mod, hipStream_t s) {
-    return launch(*args, ln != 0, mod != 0, s);
+    return launch(*args, ln != 0, mod, s);   // mod: 0 none, 1 fp32 vec, 2 bf16 vec
 }
 
 SKR_API int skr_lstm_bwd_step(const BwdArgs* args, int ln, int mod, hipStream_t s) {
-    return launch(*args, ln != 0, mod != 0, s);
+    return launch(*args, ln != 0, mod, s);   // mod: 0 none, 1 fp32 vec, 2 bf16 vec
 }
 
 SKR_API int skr_lstm_fwd_args_size() { return (int)sizeof(FwdArgs); }

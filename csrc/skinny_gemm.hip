@@ -184,10 +184,10 @@ __device__ __forceinline__ void wait_ahead(int ahead) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
-template <int BN, int NS>
+template <int BN, int NS, bool CBF16 = false>
 __device__ __forceinline__ void glds_tile(const __hip_bfloat16* __restrict__ A, int64_t lda,
                                           const __hip_bfloat16* __restrict__ Bt, int64_t ldb,
-                                          float* __restrict__ C, int64_t ldc, int M, int n0, int64_t k0, int kslice,
+                                          void* __restrict__ Cv, int64_t ldc, int M, int n0, int64_t k0, int kslice,
                                           __hip_bfloat16* smem) {
     constexpr int NJ = BN / 16;
     constexpr int A_CH = BM / 8, B_CH = BN / 8;     // 1-KiB chunks (8 rows) per tile
@@ -272,18 +272,22 @@ __device__ __forceinline__ void glds_tile(const __hip_bfloat16* __restrict__ A, 
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
                 const int row = 32 * w + 16 * i + fq * 4 + e;
-                if (row < M) C[row * ldc + n0 + 16 * j + fr] = acc[i][j][e];
+                if (row < M) {
+                    if constexpr (CBF16) ((__hip_bfloat16*)Cv)[row * ldc + n0 + 16 * j + fr] = skr::to_bf16(acc[i][j][e]);
+                    else ((float*)Cv)[row * ldc + n0 + 16 * j + fr] = acc[i][j][e];
+                }
             }
 }
 
-template <int BN, int NS>
+template <int BN, int NS, bool CBF16 = false>
 __global__ __launch_bounds__(256) void skinny_gemm_glds_kernel(
     const __hip_bfloat16* __restrict__ A, int64_t lda, int64_t a_batch,
     const __hip_bfloat16* __restrict__ Bt, int64_t ldb, int64_t b_batch,
-    float* __restrict__ C, int64_t ldc, int64_t c_slab, int64_t c_batch, int M, int kslice) {
+    void* __restrict__ C, int64_t ldc, int64_t c_slab, int64_t c_batch, int M, int kslice) {
     extern __shared__ __attribute__((aligned(16))) __hip_bfloat16 smem[];
-    glds_tile<BN, NS>(A + blockIdx.z * a_batch, lda, Bt + blockIdx.z * b_batch, ldb,
-                  C + blockIdx.z * c_batch + blockIdx.y * c_slab, ldc, M, blockIdx.x * BN,
+    const int64_t co = blockIdx.z * c_batch + blockIdx.y * c_slab;
+    glds_tile<BN, NS, CBF16>(A + blockIdx.z * a_batch, lda, Bt + blockIdx.z * b_batch, ldb,
+                  CBF16 ? (void*)((__hip_bfloat16*)C + co) : (void*)((float*)C + co), ldc, M, blockIdx.x * BN,
                   (int64_t)blockIdx.y * kslice, kslice, smem);
 }
 
@@ -482,13 +486,13 @@ void set_lds_attr(K k, size_t lds) {
     }
 }
 
-template <int BN, int NS>
+template <int BN, int NS, bool CBF16 = false>
 int launch_v2(dim3 grid, hipStream_t s, const void* A, int64_t lda, int64_t a_batch, const void* Bt, int64_t ldb,
-              int64_t b_batch, float* C, int64_t ldc, int64_t c_slab, int64_t c_batch, int M, int kslice) {
+              int64_t b_batch, void* C, int64_t ldc, int64_t c_slab, int64_t c_batch, int M, int kslice) {
     const size_t lds = (size_t)NS * (BM + BN) * BK * 2;
-    set_lds_attr(skinny_gemm_glds_kernel<BN, NS>, lds);
-    hipLaunchKernelGGL((skinny_gemm_glds_kernel<BN, NS>), grid, dim3(256), lds, s, (const __hip_bfloat16*)A, lda,
-                       a_batch, (const __hip_bfloat16*)Bt, ldb, b_batch, C, ldc, c_slab, c_batch, M, kslice);
+    set_lds_attr(skinny_gemm_glds_kernel<BN, NS, CBF16>, lds);
+    hipLaunchKernelGGL((skinny_gemm_glds_kernel<BN, NS, CBF16>), grid, dim3(256), lds, s, (const __hip_bfloat16*)A,
+                       lda, a_batch, (const __hip_bfloat16*)Bt, ldb, b_batch, C, ldc, c_slab, c_batch, M, kslice);
     return SKR_CHECK_LAUNCH();
 }
 
@@ -517,6 +521,18 @@ SKR_API int skr_skinny_gemm_v2(const void* A, int64_t lda, int64_t a_batch, cons
     if (bn == 128) return g_nstage == 3 ? SKR_V2(128, 3) : SKR_V2(128, 4);
     return g_nstage == 3 ? SKR_V2(64, 3) : g_nstage == 6 ? SKR_V2(64, 6) : SKR_V2(64, 4);
 #undef SKR_V2
+}
+
+// As skr_skinny_gemm_v2 with a bf16 output (one slab: splits == 1), for
+// products consumed only as bf16 (the HyperLSTM modulation vectors).
+SKR_API int skr_skinny_gemm_v2_bf16out(const void* A, int64_t lda, int64_t a_batch, const void* Bt, int64_t ldb,
+                                       int64_t b_batch, void* C, int64_t ldc, int64_t c_batch, int M, int N, int K,
+                                       int batch, hipStream_t s) {
+    if (M < 1 || M > BM || N % 64 != 0 || K % BK != 0 || lda % 8 != 0 || ldb % 8 != 0) return -2;
+    if (((uintptr_t)A | (uintptr_t)Bt) & 15) return -4;
+    const dim3 grid(N / 64, 1, batch);
+    return g_nstage == 3 ? launch_v2<64, 3, true>(grid, s, A, lda, a_batch, Bt, ldb, b_batch, C, ldc, 0, c_batch, M, K)
+                         : launch_v2<64, 4, true>(grid, s, A, lda, a_batch, Bt, ldb, b_batch, C, ldc, 0, c_batch, M, K);
 }
 
 // Grouped bf16 products (see skinny_gemm_group_kernel): each problem as

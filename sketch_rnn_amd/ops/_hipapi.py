@@ -186,6 +186,9 @@ class HipLib:
         lib.skr_gru_fwd.restype = _i
         lib.skr_gru_bwd.argtypes = [C.POINTER(GruBwdArgs), _i, _p]
         lib.skr_gru_bwd.restype = _i
+        lib.skr_skinny_gemm_v2_bf16out.argtypes = [_p, _i64, _i64, _p, _i64, _i64, _p, _i64, _i64, _i, _i, _i, _i,
+                                                    _p]
+        lib.skr_skinny_gemm_v2_bf16out.restype = _i
         lib.skr_gemm_set_nstage.argtypes = [_i]
         lib.skr_gemm_set_nstage.restype = _i
         lib.skr_skinny_gemm_group.argtypes = [C.POINTER(GemmProblem), _i, _i, _p]

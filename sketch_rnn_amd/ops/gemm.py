@@ -141,6 +141,22 @@ def rec_gemm(a: torch.Tensor, bt: torch.Tensor, out: torch.Tensor, splits: int, 
     return out
 
 
+def rec_gemm_bf16out(a: torch.Tensor, bt: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
+    """``out [M, N] (bf16) = a @ bt^T`` in one slab (no split-K): for products
+    read only as bf16 downstream (csrc/skinny_gemm.hip ``skr_skinny_gemm_v2_bf16out``)."""
+    from ..utils import native
+    lib = native.require_hip()
+    M, K = a.shape
+    N = bt.shape[-2]
+    assert out.dtype == _BF16 and out.shape[-1] == N and M <= 128
+    rc = lib.lib.skr_skinny_gemm_v2_bf16out(a.data_ptr(), a.stride(0), 0, bt.data_ptr(), bt.stride(-2), 0,
+                                            out.data_ptr(), out.stride(-2), 0, M, N, K, 1,
+                                            torch.cuda.current_stream().cuda_stream)
+    if rc != 0:
+        raise RuntimeError("skr_skinny_gemm_v2_bf16out failed (%d) for M=%d N=%d K=%d" % (rc, M, N, K))
+    return out
+
+
 GROUPED = os.environ.get("SKR_GEMM_GROUP", "1") != "0"   # SKR_GEMM_GROUP=0: independent per-step products as separate launches
 
 

@@ -532,7 +532,10 @@ class _HyperSeq(torch.autograd.Function):
         HXHAT = torch.empty(T, B, Gh, device=dev, dtype=f32)
         HRSTD = torch.empty(T, B, 5, device=dev, dtype=f32)
         HCHAT = torch.empty(T, B, Hh, device=dev, dtype=f32)
-        VEC = torch.empty(T, B, 12 * H, device=dev, dtype=f32)
+        # modulation vectors in bf16 when the GEMMs are bf16 (read only by the main cells)
+        vbf = not fp8 and dt == torch.bfloat16 and B <= 128 and S_v == 1
+        VEC = torch.empty(T, B, 12 * H, device=dev, dtype=torch.bfloat16 if vbf else f32)
+        mod = 2 if vbf else 1
         HC = torch.empty(2, B, H, device=dev, dtype=f32)
         HHC = torch.empty(2, B, Hh, device=dev, dtype=f32)
         sd = _seed_tensor(seed, dev)
@@ -577,14 +580,17 @@ class _HyperSeq(torch.autograd.Function):
             ah.xhat, ah.rstd, ah.chat = HXHAT[t].data_ptr(), HRSTD[t].data_ptr(), HCHAT[t].data_ptr()
             ah.h_carry, ah.h_lp, ah.c_carry = HHC[t % 2].data_ptr(), A[t + 1, :, H:].data_ptr(), HCC[t + 1].data_ptr()
             _check(lib.lib.skr_lstm_fwd_step(ctypes.byref(ah), 1, 0, st), "hyper_fwd_step")
-            rgemm(A[t + 1, :, H:], PlT, VEC[t].unsqueeze(0), S_v)
+            if vbf:
+                gemm.rec_gemm_bf16out(A[t + 1, :, H:], PlT, VEC[t])
+            else:
+                rgemm(A[t + 1, :, H:], PlT, VEC[t].unsqueeze(0), S_v)
             _join(main, side)                            # R_main(t) done
             am.xp, am.R, am.vec = XH[t].data_ptr(), RM[t].data_ptr(), VEC[t].data_ptr()
             am.c_prev, am.step = CC[t].data_ptr(), t
             am.h_out, am.c_out, am.act = Hout[t].data_ptr(), Cout[t].data_ptr(), ACT[t].data_ptr()
             am.xhat, am.rstd, am.chat = XHAT[t].data_ptr(), RSTD[t].data_ptr(), CHAT[t].data_ptr()
             am.h_carry, am.h_lp, am.c_carry = HC[t % 2].data_ptr(), A[t + 1, :, :H].data_ptr(), CC[t + 1].data_ptr()
-            _check(lib.lib.skr_lstm_fwd_step(ctypes.byref(am), 1, 1, st), "hyper_main_fwd_step")
+            _check(lib.lib.skr_lstm_fwd_step(ctypes.byref(am), 1, mod, st), "hyper_main_fwd_step")
         hT = HC[(T - 1) % 2].clone()
         hhT = HHC[(T - 1) % 2].clone()
         s = _Saved()
@@ -669,7 +675,8 @@ class _HyperSeq(torch.autograd.Function):
             am.dG_lp = dRM_lp[t].data_ptr() if lp_on else None
             am.dxp, am.dvec = dXH[t].data_ptr(), dVEC[t].data_ptr()
             am.dlny, am.dlncy = DLNY[t].data_ptr(), DLNCY[t].data_ptr()
-            _check(lib.lib.skr_lstm_bwd_step(ctypes.byref(am), 1, 1, st), "hyper_main_bwd_step")
+            _check(lib.lib.skr_lstm_bwd_step(ctypes.byref(am), 1, 2 if s.VEC.dtype == torch.bfloat16 else 1, st),
+                   "hyper_main_bwd_step")
             if group:   # dR_main @ W_h^T and dvec @ P^T in one launch
                 gemm.rec_gemm_group([(dRM_lp[t], s.Whl, DAM, S_am), (dVEC[t], s.Pl, DHZ, S_h)])
             else:

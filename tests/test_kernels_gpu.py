@@ -217,6 +217,32 @@ def test_hyper_sequence_matches_oracle(H, Hh, E, keep):
     _close(g_h, g_t, 2e-3, 2e-4, "grad")
 
 
+def test_hyper_sequence_bf16_close():
+    """bf16 HyperLSTM (grouped GEMMs, bf16 modulation vectors) against the
+    fp32 oracle at bf16 tolerances."""
+    torch.manual_seed(12)
+    T, B, IN, H, Hh, E = 6, 100, 5, 512, 64, 8
+    p = C.HyperLSTMParams(IN + 16, H, Hh, E).to(DEV)
+    with torch.no_grad():
+        for prm in p.parameters():
+            prm.add_(torch.randn_like(prm) * 0.05)
+    x = torch.randn(T, B, IN, device=DEV)
+    zc = torch.randn(B, 16, device=DEV, requires_grad=True)
+    st = [torch.zeros(B, n, device=DEV) for n in (H, H, Hh, Hh)]
+    w = torch.randn(T, B, H, device=DEV)
+    res = []
+    for backend, dt in (("hip", "bf16"), ("torch", "fp32")):
+        ops.set_backend(backend)
+        ops.set_compute_dtype(dt)
+        p.zero_grad()
+        z = zc.detach().clone().requires_grad_()
+        out, _ = ops.hyper_sequence(p, x, *st, drop_keep=0.9, drop_seed=4, drop_stream=9, zc=z)
+        (out * w).sum().backward()
+        res.append([out.detach(), z.grad] + [q.grad.clone() for q in p.parameters()])
+    _close(res[0][:1], res[1][:1], 3e-2, 3e-2, "out")
+    _close(res[0][1:], res[1][1:], 6e-2, 6e-2, "grad")
+
+
 @pytest.mark.parametrize("H,Hh,E", [(2048, 256, 32), (512, 64, 8)])
 def test_hyper_grouped_gemm_path_bitwise(H, Hh, E):
     """bf16 HyperLSTM with the grouped per-step GEMM launches equals the
