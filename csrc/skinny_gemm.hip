@@ -510,8 +510,9 @@ int launch_group(const GemmGroup& g, hipStream_t s) {
 SKR_API int skr_skinny_gemm_v2(const void* A, int64_t lda, int64_t a_batch, const void* Bt, int64_t ldb,
                                int64_t b_batch, float* C, int64_t ldc, int64_t c_slab, int64_t c_batch, int M, int N,
                                int K, int splits, int batch, int bn, hipStream_t s) {
-    // 128-wide N tiles once they still give >= 144 workgroups (measured, scripts/bench_gemm.py)
-    if (bn == 0) bn = (N % 128 == 0 && (N / 128) * splits * batch >= 144) ? 128 : 64;
+    // 64-wide N tiles: with the 3-deep ring two workgroups share a CU and
+    // 64 beat 128 on every recurrent shape (scripts/bench_gemm.py)
+    if (bn == 0) bn = (g_nstage == 3) ? 64 : ((N % 128 == 0 && (N / 128) * splits * batch >= 144) ? 128 : 64);
     if (M < 1 || M > BM || (bn != 64 && bn != 128) || N % bn != 0 || splits < 1 || K % splits != 0) return -2;
     const int kslice = K / splits;
     if (kslice % BK != 0 || lda % 8 != 0 || ldb % 8 != 0) return -3;
