@@ -17,6 +17,7 @@ Design for MI355X / xGMI:
 """
 from __future__ import annotations
 
+import datetime
 import os
 from typing import Dict, List, Optional
 
@@ -46,7 +47,11 @@ def init_from_env(backend: Optional[str] = None, device: Optional[str] = None) -
     if backend is None:
         backend = "nccl" if (device or "").startswith("cuda") else "gloo"
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-    kw = {}
+    # failure detection: a collective that does not complete
+    # within the timeout aborts the communicator (RCCL watchdog) instead of
+    # hanging every rank; SKR_DIST_TIMEOUT seconds, default 600
+    os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
+    kw = {"timeout": datetime.timedelta(seconds=float(os.environ.get("SKR_DIST_TIMEOUT", "600")))}
     if backend == "nccl":
         lr = int(os.environ.get("LOCAL_RANK", "0"))
         torch.cuda.set_device(lr)

@@ -46,3 +46,24 @@ def test_host_packer_loads():
         import build_native
         build_native.build_host()
     assert native.host_lib() is not None
+
+
+def test_host_packer_under_asan_ubsan(tmp_path):
+    """the host runtime built with AddressSanitizer +
+    UndefinedBehaviorSanitizer and driven over random corpora in its own
+    process (host code only -- no GPU sanitizers on this pool)."""
+    import shutil
+    import subprocess
+    gxx = shutil.which("g++")
+    if gxx is None:
+        pytest.skip("no g++")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    exe = str(tmp_path / "packer_sanitize")
+    subprocess.check_call([gxx, "-std=c++17", "-O1", "-g", "-fno-omit-frame-pointer",
+                           "-fsanitize=address,undefined", "-fno-sanitize-recover=all",
+                           os.path.join(root, "csrc", "host", "tests", "packer_sanitize.cpp"),
+                           os.path.join(root, "csrc", "host", "packer.cpp"), "-o", exe])
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=0", UBSAN_OPTIONS="print_stacktrace=1")
+    r = subprocess.run([exe], capture_output=True, text=True, env=env, timeout=300)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    assert "0 failures" in r.stdout
