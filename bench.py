@@ -37,6 +37,7 @@ def main():
     ap.add_argument("--backend", default="auto", choices=["auto", "hip", "torch"])
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-eval", action="store_true")
+    ap.add_argument("--trace", action="store_true", help="print every step's cost to stderr (syncs each step)")
     ap.add_argument("--sketches", type=int, default=2000)
     ap.add_argument("--dist-backend", default=None, help="override (default: nccl = RCCL on GPUs); "
                     "'gloo' rehearses the multi-rank path with several ranks on one GPU")
@@ -82,13 +83,17 @@ def main():
     batches = [batch() for _ in range(4)]
     sync = torch.cuda.synchronize if device.startswith("cuda") else (lambda: None)
     for i in range(args.warmup):
-        trainer.train_step(*batches[i % len(batches)])
+        out = trainer.train_step(*batches[i % len(batches)])
+        if args.trace:
+            print("warmup %d cost %.6f" % (i, float(out["cost"])), file=sys.stderr)
     sync()
     dp.barrier()
     sync()
     t0 = time.perf_counter()
     for i in range(args.steps):
         out = trainer.train_step(*batches[i % len(batches)])
+        if args.trace:
+            print("step %d cost %.6f" % (i, float(out["cost"])), file=sys.stderr)
     sync()
     dp.barrier()
     sync()

@@ -68,6 +68,9 @@ struct BwdArgs {
     float* dlncy;                      // LN: [B, H]  grad wrt LN(c) output
     float* dinit_h; float* dinit_c;    // [B, H] accumulated on reset rows (or null)
     int cluster; uint64_t* part; int* err;
+    // LN: the gate activations are recomputed from xhat (the forward does not
+    // store them): act = sig/tanh(xhat * ln_g + ln_b (+ forget_bias on f))
+    const float* ln_b; float forget_bias;
 };
 
 // hyper modulation vectors: MOD 1 fp32, MOD 2 bf16

@@ -11,7 +11,10 @@
 //   h'     = tanh(LN(c')*gc + bc)*sig(y_o)  |  tanh(c')*sig(y_o)
 //   carry  = reset[b] ? init : (h', c')          (reference eoc reset)
 //
-// plus the saves the backward needs and a bf16 copy of the carried h written
+// plus the saves the backward needs (LN layers: xhat / rstd / chat only; the
+// backward recomputes sig/tanh of the gates from xhat instead of re-reading a
+// stored [B, 4H] activation tensor; none at inference) and a bf16 copy of the
+// carried h written
 // straight into the next GEMM's A operand (a column slice of a concatenated
 // [h | h_hyper] buffer, hence the explicit row stride). R is the sum of the
 // split-K partial slabs of csrc/skinny_gemm.hip, reduced here while loading.
@@ -142,6 +145,10 @@ __global__ __launch_bounds__(NT) void cell_fwd(const FwdArgs a) {
     const bool keep_on = a.keep < 1.0f;
     const uint32_t key = keep_on ? hash_key(*a.seed, a.stream, a.step) : 0u;
     const bool r = a.reset != nullptr && a.reset[b] != 0.f;
+    // saves for the backward (null pointers at inference): LN layers save
+    // xhat / rstd / chat only -- the backward recomputes the gate activations
+    // from xhat -- plain layers save act
+    const bool save = LN ? a.xhat != nullptr : a.act != nullptr;
 
     // ---- every load up front (clamped indices; results of u >= H discarded)
     float g[UPT][4], cp[UPT], lg[UPT][4], lb[UPT][4], lcg[UPT], lcb[UPT];
@@ -225,11 +232,11 @@ __global__ __launch_bounds__(NT) void cell_fwd(const FwdArgs a) {
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
                 const float xh = (g[k][q] - mean[q]) * rs[q];
-                if (on[k]) a.xhat[(int64_t)b * 4 * H + q * H + u] = xh;
+                if (save && on[k]) a.xhat[(int64_t)b * 4 * H + q * H + u] = xh;
                 g[k][q] = xh * lg[k][q] + lb[k][q];
             }
         }
-        if (c == 0 && tid < 4) a.rstd[b * 5 + tid] = rs[tid];
+        if (save && c == 0 && tid < 4) a.rstd[b * 5 + tid] = rs[tid];
     }
     // ---- cell
     float cn[UPT], og[UPT];
@@ -244,14 +251,14 @@ __global__ __launch_bounds__(NT) void cell_fwd(const FwdArgs a) {
         const float m = dropout_mult(keep_on, key, ro, a.keep);
         cn[k] = on[k] ? cp[k] * f + i * tj * m : 0.f;
         og[k] = o;
-        if (on[k]) {
+        if (!LN && save && on[k]) {
             float* ap = a.act + (int64_t)b * 4 * H + u;
             ap[0] = i;
             ap[H] = tj;
             ap[2 * H] = f;
             ap[3 * H] = o;
-            a.c_out[ro] = cn[k];
         }
+        if (a.c_out != nullptr && on[k]) a.c_out[ro] = cn[k];
     }
     float th[UPT];
     if (LN) {
@@ -280,12 +287,12 @@ __global__ __launch_bounds__(NT) void cell_fwd(const FwdArgs a) {
             var = s2[0] / (float)H;
         }
         const float rc = rsqrtf(var + kLnEps);
-        if (c == 0 && tid == 0) a.rstd[b * 5 + 4] = rc;
+        if (save && c == 0 && tid == 0) a.rstd[b * 5 + 4] = rc;
 #pragma unroll
         for (int k = 0; k < UPT; ++k) {
             const int u = base + k * NT + tid;
             const float ch = (cn[k] - mean) * rc;
-            if (on[k]) a.chat[(int64_t)b * H + u] = ch;
+            if (save && on[k]) a.chat[(int64_t)b * H + u] = ch;
             th[k] = tanhf(ch * lcg[k] + lcb[k]);
         }
     } else {
@@ -301,7 +308,7 @@ __global__ __launch_bounds__(NT) void cell_fwd(const FwdArgs a) {
         const float h = th[k] * og[k];
         a.h_out[ro] = h;
         const float hc = r ? a.init_h[ro] : h;
-        a.h_carry[ro] = hc;
+        if (a.h_carry != nullptr) a.h_carry[ro] = hc;   // (== h_out without resets: callers skip it)
         a.c_carry[ro] = r ? a.init_c[ro] : cn[k];
         if (a.lp_kind == 1) ((__hip_bfloat16*)a.h_lp)[b * a.ld_lp + u] = to_bf16(hc);
         else if (a.lp_kind == 2) ((float*)a.h_lp)[b * a.ld_lp + u] = hc;
@@ -319,6 +326,7 @@ __global__ __launch_bounds__(NT) void cell_bwd(const BwdArgs a) {
     const int span = UPT * NT, base = c * span;
     const int grp = a.grp_rows > 0 ? b / a.grp_rows : 0;
     const float* ln_g = LN ? a.ln_g + grp * 4 * H : nullptr;
+    const float* ln_b = LN ? a.ln_b + grp * 4 * H : nullptr;
     const float* lnc_g = LN ? a.lnc_g + grp * H : nullptr;
     const float* lnc_b = LN ? a.lnc_b + grp * H : nullptr;
     const bool keep_on = a.keep < 1.0f;
@@ -327,7 +335,7 @@ __global__ __launch_bounds__(NT) void cell_bwd(const BwdArgs a) {
 
     // ---- every load up front
     float dhc[UPT], dho[UPT], dcc[UPT], ac[UPT][4], cp[UPT], cx[UPT], lcg[UPT], lcb[UPT];
-    float xh[UPT][4], lg[UPT][4], xv[UPT][4], rv[UPT][4], ax[UPT][4], ah[UPT][4];
+    float xh[UPT][4], lg[UPT][4], lb[UPT][4], xv[UPT][4], rv[UPT][4], ax[UPT][4], ah[UPT][4];
     bool on[UPT];
 #pragma unroll
     for (int k = 0; k < UPT; ++k) {
@@ -340,8 +348,6 @@ __global__ __launch_bounds__(NT) void cell_bwd(const BwdArgs a) {
         dho[k] = a.dh_out ? slab_sum<0>(a.dh_out, ro, a.dho_nslab, a.dho_slab) : 0.f;
         dcc[k] = a.dc_rec[ro];
         cp[k] = a.c_prev[ro];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) ac[k][q] = a.act[(int64_t)b * 4 * H + q * H + uc];
         if (LN) {
             cx[k] = a.chat[ro];
             lcg[k] = lnc_g[uc];
@@ -350,8 +356,11 @@ __global__ __launch_bounds__(NT) void cell_bwd(const BwdArgs a) {
             for (int q = 0; q < 4; ++q) {
                 xh[k][q] = a.xhat[(int64_t)b * 4 * H + q * H + uc];
                 lg[k][q] = ln_g[q * H + uc];
+                lb[k][q] = ln_b[q * H + uc];
             }
         } else {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) ac[k][q] = a.act[(int64_t)b * 4 * H + q * H + uc];
             cx[k] = a.c_new[ro];
         }
         if (MOD) {
@@ -363,6 +372,16 @@ __global__ __launch_bounds__(NT) void cell_bwd(const BwdArgs a) {
                 ax[k][q] = ldvec<MOD>(a.vec, q * a.vec_gs + vo) + a.vec_bias[q * H + uc];
                 ah[k][q] = ldvec<MOD>(a.vec, (4 + q) * a.vec_gs + vo) + a.vec_bias[(4 + q) * H + uc];
             }
+        }
+    }
+    // ---- LN: gate activations from the saved xhat (same expressions as the forward)
+    if (LN) {
+#pragma unroll
+        for (int k = 0; k < UPT; ++k) {
+            ac[k][0] = sigmoidf_(xh[k][0] * lg[k][0] + lb[k][0]);
+            ac[k][1] = tanhf(xh[k][1] * lg[k][1] + lb[k][1]);
+            ac[k][2] = sigmoidf_(xh[k][2] * lg[k][2] + lb[k][2] + a.forget_bias);
+            ac[k][3] = sigmoidf_(xh[k][3] * lg[k][3] + lb[k][3]);
         }
     }
     // ---- output: h' = th * o
@@ -460,7 +479,7 @@ __global__ __launch_bounds__(NT) void cell_bwd(const BwdArgs a) {
                     else ((float*)a.dvec)[oi] = d3[j];
                 }
             }
-            a.dG[b * a.ld_dG + q * H + u] = dr;
+            if (a.dG != nullptr) a.dG[b * a.ld_dG + q * H + u] = dr;   // (null: only the bf16 copy is read)
             if (a.dG_lp_kind == 1) ((__hip_bfloat16*)a.dG_lp)[b * a.ld_dG_lp + q * H + u] = to_bf16(dr);
         }
     }

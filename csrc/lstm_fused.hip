@@ -161,7 +161,7 @@ __global__ __launch_bounds__(256) void lstm_fused_fwd(const FusedFwdArgs a) {
         a.h_out[ro] = h;
         const bool rs = a.reset != nullptr && a.reset[b] != 0.f;
         const float hc = rs ? a.init_h[ro] : h;
-        a.h_carry[ro] = hc;
+        if (a.h_carry != nullptr) a.h_carry[ro] = hc;   // (== h_out without resets: callers skip it)
         a.c_carry[ro] = rs ? a.init_c[ro] : cn;
         a.h_next[(int64_t)b * a.ld_next + u] = to_bf16(hc);
     }

@@ -35,6 +35,18 @@ def main():
         if d >= min_us:
             print("%8.1f us  t=%8.0f  %s" % (d, ts, n[:100]))
     print("step span %.2f ms; non-loop kernels %.2f ms" % (span / 1e3, other / 1e3))
+    # per-kernel totals inside the step (duration = start-to-end, which under
+    # graph replay includes the kernel-boundary gap to the previous launch)
+    agg = {}
+    for r in seq:
+        n = r["Kernel_Name"][:110]
+        d = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
+        a = agg.setdefault(n, [0, 0.0])
+        a[0] += 1
+        a[1] += d
+    print("\nper kernel (last step):")
+    for n, (c, d) in sorted(agg.items(), key=lambda kv: -kv[1][1])[:25]:
+        print("%9.1f us %5d x %7.2f us  %s" % (d, c, d / c, n))
 
 
 if __name__ == "__main__":

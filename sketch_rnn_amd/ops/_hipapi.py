@@ -67,6 +67,7 @@ class LstmBwdArgs(C.Structure):
         ("dlny", _p), ("dlncy", _p),
         ("dinit_h", _p), ("dinit_c", _p),
         ("cluster", _i), ("part", _p), ("err", _p),
+        ("ln_b", _p), ("forget_bias", _f),
     ]
 
 

@@ -202,14 +202,20 @@ class _LSTMSeq(torch.autograd.Function):
         CC = torch.empty(T + 1, BB, H, device=dev, dtype=f32)  # carried c
         CC[0].copy_(c0)
         Hout = torch.empty(T, BB, H, device=dev, dtype=f32)
-        Cout = torch.empty(T, BB, H, device=dev, dtype=f32)
-        ACT = torch.empty(T, BB, G, device=dev, dtype=f32)
-        XHAT = torch.empty(T, BB, G, device=dev, dtype=f32) if ln else None
-        RSTD = torch.empty(T, BB, 5, device=dev, dtype=f32) if ln else None
-        CHAT = torch.empty(T, BB, H, device=dev, dtype=f32) if ln else None
-        HC = torch.empty(2, BB, H, device=dev, dtype=f32)
-        R = torch.empty(max(S, 1), BB, G, device=dev, dtype=f32)
+        fused = _fused_ok(H, ln, fp8, ldt)
+        # saves for the backward: LN layers keep xhat / rstd / chat (the kernel
+        # recomputes the gate activations from xhat); plain layers keep act and
+        # c'. Nothing is saved at inference (the fused kernel always writes them).
+        keep_plain = not ln and (fused or not infer)
+        Cout = torch.empty(T, BB, H, device=dev, dtype=f32) if keep_plain else None
+        ACT = torch.empty(T, BB, G, device=dev, dtype=f32) if keep_plain else None
+        XHAT = torch.empty(T, BB, G, device=dev, dtype=f32) if ln and not infer else None
+        RSTD = torch.empty(T, BB, 5, device=dev, dtype=f32) if ln and not infer else None
+        CHAT = torch.empty(T, BB, H, device=dev, dtype=f32) if ln and not infer else None
         rst = reset.contiguous().to(f32) if reset is not None else None
+        # carried h differs from h' only on reset rows: without resets hT = h'_{T-1}
+        HC = torch.empty(2, BB, H, device=dev, dtype=f32) if rst is not None else None
+        R = torch.empty(max(S, 1), BB, G, device=dev, dtype=f32)
         rh = reset_h.contiguous() if reset_h is not None else None
         rc = reset_c.contiguous() if reset_c is not None else None
         lnp = [t.contiguous() if t is not None else None for t in (ln_g, ln_b, lnc_g, lnc_b)]
@@ -224,7 +230,7 @@ class _LSTMSeq(torch.autograd.Function):
         a.ld_lp, a.lp_kind = H, _lp_kind(A)
         a.R, a.R_nslab, a.R_slab = R.data_ptr(), max(S, 1), BB * G
         st = _stream()
-        if _fused_ok(H, ln, fp8, ldt):
+        if fused:
             f = FusedFwdArgs()
             f.B, f.H, f.nd = Bg, H, nd
             f.lda, f.ld_xp, f.ld_next = H, G, H
@@ -237,7 +243,8 @@ class _LSTMSeq(torch.autograd.Function):
                 f.reset = _ptr(rst[t]) if rst is not None else None
                 f.step = t
                 f.h_out, f.c_out, f.act = Hout[t].data_ptr(), Cout[t].data_ptr(), ACT[t].data_ptr()
-                f.h_carry, f.c_carry, f.h_next = HC[t % 2].data_ptr(), CC[t + 1].data_ptr(), A[t + 1].data_ptr()
+                f.h_carry = HC[t % 2].data_ptr() if HC is not None else None
+                f.c_carry, f.h_next = CC[t + 1].data_ptr(), A[t + 1].data_ptr()
                 _check(lib.lib.skr_lstm_fused_fwd(ctypes.byref(f), st), "lstm_fused_fwd")
             T_loop = 0
         else:
@@ -253,14 +260,19 @@ class _LSTMSeq(torch.autograd.Function):
             a.c_prev = CC[t].data_ptr()
             a.reset = _ptr(rst[t]) if rst is not None else None
             a.step = t
-            a.h_out, a.c_out, a.act = Hout[t].data_ptr(), Cout[t].data_ptr(), ACT[t].data_ptr()
-            if ln:
+            a.h_out = Hout[t].data_ptr()
+            a.c_out = _ptr(Cout[t] if Cout is not None else None)
+            a.act = _ptr(ACT[t] if ACT is not None else None)
+            if XHAT is not None:
                 a.xhat, a.rstd, a.chat = XHAT[t].data_ptr(), RSTD[t].data_ptr(), CHAT[t].data_ptr()
-            a.h_carry = HC[t % 2].data_ptr()
+            a.h_carry = HC[t % 2].data_ptr() if HC is not None else None
             a.h_lp = A[t + 1].data_ptr()
             a.c_carry = CC[t + 1].data_ptr()
             _check(lib.lib.skr_lstm_fwd_step(ctypes.byref(a), int(ln), 0, st), "lstm_fwd_step")
-        hT = HC[(T - 1) % 2].clone() if T > 0 else h0.clone()
+        if T == 0:
+            hT = h0.clone()
+        else:
+            hT = HC[(T - 1) % 2].clone() if HC is not None else Hout[T - 1].clone()
         cT = CC[T].clone()
         s = _Saved()
         s.Wl, s.A, s.CC, s.Cout, s.ACT, s.XHAT, s.RSTD, s.CHAT = Wl, A, CC, Cout, ACT, XHAT, RSTD, CHAT
@@ -300,6 +312,7 @@ class _LSTMSeq(torch.autograd.Function):
         a.dho_nslab = 1
         a.dh_rec, a.dc_rec = DH.data_ptr(), dc_rec.data_ptr()
         a.ln_g, a.lnc_g, a.lnc_b = _ptr(s.lnp[0]), _ptr(s.lnp[2]), _ptr(s.lnp[3])
+        a.ln_b, a.forget_bias = _ptr(s.lnp[1]), float(forget_bias)
         a.keep, a.seed, a.stream = float(keep), s.seed.data_ptr(), int(stream)
         a.ld_dG, a.ld_dG_lp, a.dG_lp_kind = G, G, 1 if lp_on else 0
         a.dinit_h, a.dinit_c = _ptr(dinit_h), _ptr(dinit_c)
@@ -331,8 +344,10 @@ class _LSTMSeq(torch.autograd.Function):
         for t in range(T_loop - 1, -1, -1):
             cl.set(a, t)
             a.dh_out = dHout[t].data_ptr() if dHout is not None else None
-            a.act, a.c_new, a.c_prev = s.ACT[t].data_ptr(), s.Cout[t].data_ptr(), s.CC[t].data_ptr()
-            if ln:
+            a.c_prev = s.CC[t].data_ptr()
+            if not ln:
+                a.act, a.c_new = s.ACT[t].data_ptr(), s.Cout[t].data_ptr()
+            else:
                 a.xhat, a.rstd, a.chat = s.XHAT[t].data_ptr(), s.RSTD[t].data_ptr(), s.CHAT[t].data_ptr()
                 a.dlny, a.dlncy = DLNY[t].data_ptr(), DLNCY[t].data_ptr()
             a.reset = _ptr(s.reset[t]) if s.reset is not None else None
@@ -521,23 +536,16 @@ class _HyperSeq(torch.autograd.Function):
         HCC = torch.empty(T + 1, B, Hh, device=dev, dtype=f32)
         HCC[0].copy_(hc0)
         Hout = torch.empty(T, B, H, device=dev, dtype=f32)
-        Cout = torch.empty(T, B, H, device=dev, dtype=f32)
-        ACT = torch.empty(T, B, G, device=dev, dtype=f32)
-        XHAT = torch.empty(T, B, G, device=dev, dtype=f32)
-        RSTD = torch.empty(T, B, 5, device=dev, dtype=f32)
-        CHAT = torch.empty(T, B, H, device=dev, dtype=f32)
         HH = torch.empty(T, B, Hh, device=dev, dtype=f32)
-        HCout = torch.empty(T, B, Hh, device=dev, dtype=f32)
-        HACT = torch.empty(T, B, Gh, device=dev, dtype=f32)
-        HXHAT = torch.empty(T, B, Gh, device=dev, dtype=f32)
-        HRSTD = torch.empty(T, B, 5, device=dev, dtype=f32)
-        HCHAT = torch.empty(T, B, Hh, device=dev, dtype=f32)
+        # saves for the backward (both cells are LayerNorm cells: xhat / rstd /
+        # chat; the kernels recompute the gate activations); none at inference
+        sv = (lambda *shape: None) if infer else (lambda *shape: torch.empty(*shape, device=dev, dtype=f32))
+        XHAT, RSTD, CHAT = sv(T, B, G), sv(T, B, 5), sv(T, B, H)
+        HXHAT, HRSTD, HCHAT = sv(T, B, Gh), sv(T, B, 5), sv(T, B, Hh)
         # modulation vectors in bf16 when the GEMMs are bf16 (read only by the main cells)
         vbf = not fp8 and dt == torch.bfloat16 and B <= 128 and S_v == 1
         VEC = torch.empty(T, B, 12 * H, device=dev, dtype=torch.bfloat16 if vbf else f32)
         mod = 2 if vbf else 1
-        HC = torch.empty(2, B, H, device=dev, dtype=f32)
-        HHC = torch.empty(2, B, Hh, device=dev, dtype=f32)
         sd = _seed_tensor(seed, dev)
         hln = [t.contiguous() for t in (hln_g, hln_b, hlnc_g, hlnc_b)]
         mln = [t.contiguous() for t in (ln_g, ln_b, lnc_g, lnc_b)]
@@ -576,9 +584,10 @@ class _HyperSeq(torch.autograd.Function):
                     rgemm(A[t, :, :H], WhT, RM[t], S_m)
                 rgemm(A[t], WyT, RY, S_y)
             ah.xp, ah.c_prev, ah.step = XHY[t].data_ptr(), HCC[t].data_ptr(), t
-            ah.h_out, ah.c_out, ah.act = HH[t].data_ptr(), HCout[t].data_ptr(), HACT[t].data_ptr()
-            ah.xhat, ah.rstd, ah.chat = HXHAT[t].data_ptr(), HRSTD[t].data_ptr(), HCHAT[t].data_ptr()
-            ah.h_carry, ah.h_lp, ah.c_carry = HHC[t % 2].data_ptr(), A[t + 1, :, H:].data_ptr(), HCC[t + 1].data_ptr()
+            ah.h_out = HH[t].data_ptr()
+            if not infer:
+                ah.xhat, ah.rstd, ah.chat = HXHAT[t].data_ptr(), HRSTD[t].data_ptr(), HCHAT[t].data_ptr()
+            ah.h_lp, ah.c_carry = A[t + 1, :, H:].data_ptr(), HCC[t + 1].data_ptr()
             _check(lib.lib.skr_lstm_fwd_step(ctypes.byref(ah), 1, 0, st), "hyper_fwd_step")
             if vbf:
                 gemm.rec_gemm_bf16out(A[t + 1, :, H:], PlT, VEC[t])
@@ -587,16 +596,17 @@ class _HyperSeq(torch.autograd.Function):
             _join(main, side)                            # R_main(t) done
             am.xp, am.R, am.vec = XH[t].data_ptr(), RM[t].data_ptr(), VEC[t].data_ptr()
             am.c_prev, am.step = CC[t].data_ptr(), t
-            am.h_out, am.c_out, am.act = Hout[t].data_ptr(), Cout[t].data_ptr(), ACT[t].data_ptr()
-            am.xhat, am.rstd, am.chat = XHAT[t].data_ptr(), RSTD[t].data_ptr(), CHAT[t].data_ptr()
-            am.h_carry, am.h_lp, am.c_carry = HC[t % 2].data_ptr(), A[t + 1, :, :H].data_ptr(), CC[t + 1].data_ptr()
+            am.h_out = Hout[t].data_ptr()
+            if not infer:
+                am.xhat, am.rstd, am.chat = XHAT[t].data_ptr(), RSTD[t].data_ptr(), CHAT[t].data_ptr()
+            am.h_lp, am.c_carry = A[t + 1, :, :H].data_ptr(), CC[t + 1].data_ptr()
             _check(lib.lib.skr_lstm_fwd_step(ctypes.byref(am), 1, mod, st), "hyper_main_fwd_step")
-        hT = HC[(T - 1) % 2].clone()
-        hhT = HHC[(T - 1) % 2].clone()
+        hT = Hout[T - 1].clone()    # no resets: the carried h is h'
+        hhT = HH[T - 1].clone()
         s = _Saved()
         for k, v in dict(xl=xl, x=x, zc=zc, bp=bp, XH=XH, Whl=Whl, Wyl=Wyl, Pl=Pl, q=q, bias_c=bias_c, S_m=S_m, A=A, RM=RM, CC=CC,
-                         HCC=HCC, Cout=Cout, ACT=ACT, XHAT=XHAT, RSTD=RSTD, CHAT=CHAT, HH=HH, HCout=HCout,
-                         HACT=HACT, HXHAT=HXHAT, HRSTD=HRSTD, HCHAT=HCHAT, VEC=VEC, seed=sd, meta=meta, W_x=W_x,
+                         HCC=HCC, XHAT=XHAT, RSTD=RSTD, CHAT=CHAT, HH=HH,
+                         HXHAT=HXHAT, HRSTD=HRSTD, HCHAT=HCHAT, VEC=VEC, seed=sd, meta=meta, W_x=W_x,
                          hW_x=hW_x, W_z=W_z, b_z=b_z, W_a=W_a, mln=mln, hln=hln).items():
             setattr(s, k, v)
         ctx.s = s
@@ -616,8 +626,10 @@ class _HyperSeq(torch.autograd.Function):
         TB = T * B
         lp_on = s.Whl.dtype == torch.bfloat16
         ldt = torch.bfloat16 if lp_on else f32
-        dRM = torch.empty(T, B, G, device=dev, dtype=f32)
-        dRY = torch.empty(T, B, Gh, device=dev, dtype=f32)
+        # d(recurrent pre-activations): only GEMM operands downstream, so with
+        # bf16 operands the cell kernels write the bf16 copy alone
+        dRM = None if lp_on else torch.empty(T, B, G, device=dev, dtype=f32)
+        dRY = None if lp_on else torch.empty(T, B, Gh, device=dev, dtype=f32)
         dRM_lp = torch.empty(T, B, G, device=dev, dtype=ldt) if lp_on else dRM
         dRY_lp = torch.empty(T, B, Gh, device=dev, dtype=ldt) if lp_on else dRY
         dXH = torch.empty(T, B, G, device=dev, dtype=ldt)   # only a GEMM operand downstream
@@ -645,6 +657,7 @@ class _HyperSeq(torch.autograd.Function):
         am.dh_rec2, am.ld_dh_rec2, am.dhr2_nslab, am.dhr2_slab = DAM.data_ptr(), H, max(S_am, 1), B * H
         am.dc_rec, am.dho_nslab = dc_rec.data_ptr(), 1
         am.ln_g, am.lnc_g, am.lnc_b = s.mln[0].data_ptr(), s.mln[2].data_ptr(), s.mln[3].data_ptr()
+        am.ln_b, am.forget_bias = s.mln[1].data_ptr(), float(forget_bias)
         am.ld_xp, am.ld_R = G, G
         am.R_nslab, am.R_slab = max(s.S_m, 1), B * G
         am.vec_gs, am.vec_ld, am.vec_bias = H, 12 * H, s.q.data_ptr()
@@ -657,6 +670,7 @@ class _HyperSeq(torch.autograd.Function):
         ah.dh_rec, ah.ld_dh_rec, ah.dc_rec = DAY[0, :, H:].data_ptr(), K, dhc_rec.data_ptr()
         ah.dhr_nslab, ah.dhr_slab = max(S_ay, 1), B * K
         ah.ln_g, ah.lnc_g, ah.lnc_b = s.hln[0].data_ptr(), s.hln[2].data_ptr(), s.hln[3].data_ptr()
+        ah.ln_b, ah.forget_bias = s.hln[1].data_ptr(), float(forget_bias)
         ah.keep, ah.seed, ah.stream = float(hkeep), s.seed.data_ptr(), int(stream) + 1
         ah.ld_dG, ah.ld_dG_lp, ah.dG_lp_kind = Gh, Gh, 1 if lp_on else 0
         clm, clh = _ClusterSync(T, B, H, dev), _ClusterSync(T, B, Hh, dev)
@@ -667,11 +681,11 @@ class _HyperSeq(torch.autograd.Function):
             clm.set(am, t)
             clh.set(ah, t)
             am.dh_out = dHout[t].data_ptr() if dHout is not None else None
-            am.act, am.c_new, am.c_prev = s.ACT[t].data_ptr(), s.Cout[t].data_ptr(), s.CC[t].data_ptr()
+            am.c_prev = s.CC[t].data_ptr()
             am.xhat, am.rstd, am.chat = s.XHAT[t].data_ptr(), s.RSTD[t].data_ptr(), s.CHAT[t].data_ptr()
             am.xp, am.R, am.vec = s.XH[t].data_ptr(), s.RM[t].data_ptr(), s.VEC[t].data_ptr()
             am.step = t
-            am.dG = dRM[t].data_ptr()
+            am.dG = None if lp_on else dRM[t].data_ptr()
             am.dG_lp = dRM_lp[t].data_ptr() if lp_on else None
             am.dxp, am.dvec = dXH[t].data_ptr(), dVEC[t].data_ptr()
             am.dlny, am.dlncy = DLNY[t].data_ptr(), DLNCY[t].data_ptr()
@@ -684,10 +698,10 @@ class _HyperSeq(torch.autograd.Function):
                 with torch.cuda.stream(side):
                     gemm.rec_gemm(dRM_lp[t], s.Whl, DAM, S_am)
                 gemm.rec_gemm(dVEC[t], s.Pl, DHZ, S_h)
-            ah.act, ah.c_new, ah.c_prev = s.HACT[t].data_ptr(), s.HCout[t].data_ptr(), s.HCC[t].data_ptr()
+            ah.c_prev = s.HCC[t].data_ptr()
             ah.xhat, ah.rstd, ah.chat = s.HXHAT[t].data_ptr(), s.HRSTD[t].data_ptr(), s.HCHAT[t].data_ptr()
             ah.step = t
-            ah.dG = dRY[t].data_ptr()
+            ah.dG = None if lp_on else dRY[t].data_ptr()
             ah.dG_lp = dRY_lp[t].data_ptr() if lp_on else None
             ah.dlny, ah.dlncy = HDLNY[t].data_ptr(), HDLNCY[t].data_ptr()
             _check(lib.lib.skr_lstm_bwd_step(ctypes.byref(ah), 1, 0, st), "hyper_bwd_step")
