@@ -31,7 +31,7 @@ static float* dalloc(size_t n, float v = 0.01f) {
 struct Cfg {
     const char* name;
     int B, H, C, NS;
-    bool ln, mod;
+    bool ln, mod;   // mod: bf16 modulation vectors (the HyperLSTM main cell)
 };
 
 static double run_fwd(const Cfg& c, int steps) {
@@ -56,7 +56,7 @@ static double run_fwd(const Cfg& c, int steps) {
     a.part = part; a.err = err;
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
-    for (int t = 0; t < 5; ++t) { a.step = t; if (skr_lstm_fwd_step(&a, c.ln, c.mod, 0)) { fprintf(stderr, "launch failed\n"); exit(1); } }
+    for (int t = 0; t < 5; ++t) { a.step = t; if (skr_lstm_fwd_step(&a, c.ln, c.mod ? 2 : 0, 0)) { fprintf(stderr, "launch failed\n"); exit(1); } }
     CK(hipDeviceSynchronize());
     // capture the launches in a graph: times kernels + graph boundaries, not host launch cost
     hipStream_t st;
@@ -65,12 +65,64 @@ static double run_fwd(const Cfg& c, int steps) {
     hipGraphExec_t ge;
     CK(hipMemset(part, 0, (size_t)2 * B * c.C * 128));
     CK(hipStreamBeginCapture(st, hipStreamCaptureModeGlobal));
-    for (int t = 0; t < steps; ++t) { a.step = 5 + t; skr_lstm_fwd_step(&a, c.ln, c.mod, st); }
+    for (int t = 0; t < steps; ++t) { a.step = 5 + t; skr_lstm_fwd_step(&a, c.ln, c.mod ? 2 : 0, st); }
     CK(hipStreamEndCapture(st, &g));
     CK(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
     CK(hipGraphLaunch(ge, st));
     CK(hipStreamSynchronize(st));
     CK(hipMemset(part, 0, (size_t)2 * B * c.C * 128));
+    CK(hipEventRecord(e0, st));
+    CK(hipGraphLaunch(ge, st));
+    CK(hipEventRecord(e1, st));
+    CK(hipEventSynchronize(e1));
+    float ms; CK(hipEventElapsedTime(&ms, e0, e1));
+    int herr; CK(hipMemcpy(&herr, err, 4, hipMemcpyDeviceToHost));
+    if (herr) fprintf(stderr, "cluster wait timeout!\n");
+    return 1000.0 * ms / steps;
+}
+
+static double run_bwd(const Cfg& c, int steps) {
+    const int B = c.B, H = c.H, G = 4 * H;
+    skr::BwdArgs a{};
+    a.B = B; a.H = H; a.grp_rows = 0;
+    a.dh_out = dalloc((size_t)B * H); a.dho_nslab = 1; a.dho_slab = (int64_t)B * H;
+    a.dh_rec = dalloc((size_t)2 * B * H); a.ld_dh_rec = H; a.dhr_nslab = 2; a.dhr_slab = (int64_t)B * H;
+    a.dc_rec = dalloc((size_t)B * H);
+    a.act = dalloc((size_t)B * G); a.c_new = dalloc((size_t)B * H); a.c_prev = dalloc((size_t)B * H);
+    a.xhat = dalloc((size_t)B * G); a.rstd = dalloc((size_t)B * 5, 1.f); a.chat = dalloc((size_t)B * H);
+    a.ln_g = dalloc(G, 1.f); a.ln_b = dalloc(G); a.lnc_g = dalloc(H, 1.f); a.lnc_b = dalloc(H);
+    a.forget_bias = 1.f;
+    a.xp = dalloc((size_t)B * G); a.ld_xp = G;
+    a.R = dalloc((size_t)c.NS * B * G); a.ld_R = G; a.R_nslab = c.NS; a.R_slab = (int64_t)B * G;
+    a.vec = dalloc((size_t)B * 12 * H); a.vec_gs = H; a.vec_ld = 12 * H; a.vec_bias = dalloc(12 * H);
+    a.keep = 0.9f;
+    int64_t* seed; CK(hipMalloc(&seed, 8)); CK(hipMemset(seed, 0, 8)); a.seed = seed; a.stream = 3;
+    a.dG = nullptr; a.ld_dG = G;
+    a.dG_lp = dalloc((size_t)B * G); a.ld_dG_lp = G; a.dG_lp_kind = 1;
+    a.dxp = dalloc((size_t)B * G); a.ld_dxp = G; a.dxp_kind = 1;
+    a.dvec = dalloc((size_t)B * 12 * H); a.dvec_kind = 1;
+    a.dlny = dalloc((size_t)B * G); a.dlncy = dalloc((size_t)B * H);
+    a.cluster = c.C;
+    uint64_t* part; CK(hipMalloc(&part, (size_t)2 * B * c.C * 16 * 8)); CK(hipMemset(part, 0, (size_t)2 * B * c.C * 128));
+    int* err; CK(hipMalloc(&err, 4)); CK(hipMemset(err, 0, 4));
+    a.part = part; a.err = err;
+    const int mod = c.mod ? 2 : 0;
+    for (int t = 0; t < 5; ++t) { a.step = t; if (skr_lstm_bwd_step(&a, c.ln, mod, 0)) { fprintf(stderr, "launch failed\n"); exit(1); } }
+    CK(hipDeviceSynchronize());
+    hipStream_t st;
+    CK(hipStreamCreate(&st));
+    hipGraph_t g;
+    hipGraphExec_t ge;
+    CK(hipMemset(part, 0, (size_t)2 * B * c.C * 128));
+    CK(hipStreamBeginCapture(st, hipStreamCaptureModeGlobal));
+    for (int t = 0; t < steps; ++t) { a.step = 5 + t; skr_lstm_bwd_step(&a, c.ln, mod, st); }
+    CK(hipStreamEndCapture(st, &g));
+    CK(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
+    CK(hipGraphLaunch(ge, st));
+    CK(hipStreamSynchronize(st));
+    CK(hipMemset(part, 0, (size_t)2 * B * c.C * 128));
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
     CK(hipEventRecord(e0, st));
     CK(hipGraphLaunch(ge, st));
     CK(hipEventRecord(e1, st));
@@ -100,6 +152,8 @@ int main(int argc, char** argv) {
         {"encoder     H512  C2 NS4 (2B)  ", 200, 512, 2, 4, false, false},
         {"tiny        H64   C1 NS1 B8    ", 8, 64, 1, 1, false, false},
     };
-    for (const Cfg& c : cfgs) printf("%-36s %8.2f us/launch\n", c.name, run_fwd(c, steps));
+    for (const Cfg& c : cfgs) printf("fwd %-36s %8.2f us/launch\n", c.name, run_fwd(c, steps));
+    for (const Cfg& c : cfgs)
+        if (c.ln) printf("bwd %-36s %8.2f us/launch\n", c.name, run_bwd(c, steps));
     return 0;
 }
