@@ -29,6 +29,11 @@ for s in "${steps[@]}"; do
     case $s in
         pytest) run pytest_gpu 900 python -m pytest tests -m gpu -q --maxfail=10 ;;
         pytest_sel) run pytest_sel 600 python -m pytest tests -m gpu -q --maxfail=10 -k "${PYTEST_K:-fused}" ;;
+        bench_stride1) SKR_WGRAD_CU_STRIDE=1 run bench_stride1 600 python bench.py --steps 10 --warmup 2 ;;
+        bench_stride2) SKR_WGRAD_CU_STRIDE=2 run bench_stride2 600 python bench.py --steps 10 --warmup 2 ;;
+        bench_stride8) SKR_WGRAD_CU_STRIDE=8 run bench_stride8 600 python bench.py --steps 10 --warmup 2 ;;
+        bench_noov) SKR_WGRAD_OVERLAP=0 run bench_noov 600 python bench.py --steps 10 --warmup 2 ;;
+        bench_ch50) SKR_WGRAD_CHUNK=50 run bench_ch50 600 python bench.py --steps 10 --warmup 2 ;;
         bench_nofused) SKR_FUSED=0 run bench_nofused 600 python bench.py --steps 10 --warmup 2 ;;
         bench_wgrad) run bench_wgrad 600 python scripts/bench_wgrad.py ;;
         bench_gemm) run bench_gemm 600 python scripts/bench_gemm.py ;;

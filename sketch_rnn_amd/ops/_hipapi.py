@@ -198,6 +198,10 @@ class HipLib:
         lib.skr_lstm_fused_fwd.restype = _i
         lib.skr_lstm_fused_bwd.argtypes = [C.POINTER(FusedBwdArgs), _p]
         lib.skr_lstm_fused_bwd.restype = _i
+        lib.skr_stream_create_cumask.argtypes = [_i, _i, _i, C.POINTER(_p)]
+        lib.skr_stream_create_cumask.restype = _i
+        lib.skr_stream_destroy.argtypes = [_p]
+        lib.skr_stream_destroy.restype = _i
         for name, cls in (("skr_lstm_fwd_args_size", LstmFwdArgs), ("skr_lstm_bwd_args_size", LstmBwdArgs),
                           ("skr_gru_fwd_args_size", GruFwdArgs), ("skr_gru_bwd_args_size", GruBwdArgs),
                           ("skr_lstm_fused_fwd_args_size", FusedFwdArgs),

@@ -7,7 +7,8 @@ and one fused cell kernel
 LayerNorm / hyper modulation / gates / dropout / eoc reset and writes the
 next GEMM's operand directly. The backward runs the mirror image in reverse
 and leaves all weight gradients to single large GEMMs over the whole
-sequence after the scan. Launched from Python but designed to be captured
+sequence after the scan (optionally chunked onto an auxiliary stream during
+the scan: ``_ChunkedWgrad``, off by default -- see WGRAD_OVERLAP). Launched from Python but designed to be captured
 whole into a HIP graph (no allocation depends on data, no host sync).
 
 * ``_LSTMSeq`` handles ``nd`` independent recurrences of the same shape in
@@ -441,6 +442,86 @@ def _join(waiter, other) -> None:
         waiter.wait_stream(other)
 
 
+# Weight gradients overlapped with the backward scan (SKR_WGRAD_OVERLAP=1):
+# every WGRAD_CHUNK reverse steps the products over the rows just finished
+# go to an auxiliary stream while the scan continues; the last chunk runs on
+# the main stream after one join. SKR_WGRAD_CU_STRIDE = s > 1 confines the
+# auxiliary stream to every s-th CU (csrc/streams.hip); 1 = unrestricted.
+# OFF by default -- measured on MI355X (vae_large, bench.py, 10 steps):
+# no overlap 30.8 ms/step; overlap on an unrestricted stream 35.3 ms; on a
+# 64-CU (stride 4) or 32-CU (stride 8) masked stream 112-114 ms. The scan's
+# LayerNorm cell kernels spin-wait on co-resident peer workgroups, and
+# long-running GEMM workgroups delay those peers' dispatch, so every step of
+# the scan stretches by far more than the hidden GEMM time.
+WGRAD_OVERLAP = os.environ.get("SKR_WGRAD_OVERLAP", "0") == "1"
+WGRAD_CHUNK = int(os.environ.get("SKR_WGRAD_CHUNK", "25"))
+WGRAD_CU_STRIDE = int(os.environ.get("SKR_WGRAD_CU_STRIDE", "1"))
+_WGRAD_STREAMS = {}
+
+
+def _wgrad_stream(device):
+    """The auxiliary weight-gradient stream of ``device`` (created once,
+    before any graph capture records on it), or None when overlap is off."""
+    if not WGRAD_OVERLAP or device.type != "cuda":
+        return None
+    key = str(device)
+    if key not in _WGRAD_STREAMS:
+        if WGRAD_CU_STRIDE > 1:
+            lib = native.require_hip()
+            n_cu = torch.cuda.get_device_properties(device).multi_processor_count
+            h = ctypes.c_void_p()
+            rc = lib.lib.skr_stream_create_cumask(n_cu, 0, WGRAD_CU_STRIDE, ctypes.byref(h))
+            if rc != 0:
+                raise RuntimeError("skr_stream_create_cumask failed (%d)" % rc)
+            _WGRAD_STREAMS[key] = torch.cuda.ExternalStream(h.value, device=device)
+        else:
+            _WGRAD_STREAMS[key] = torch.cuda.Stream(device=device)
+    return _WGRAD_STREAMS[key]
+
+
+class _ChunkedWgrad:
+    """Accumulates ``sum_t f(rows of steps [t0, t1))`` for a list of
+    row-separable gradient products while a reverse scan runs.
+
+    ``work(t0, t1)`` returns the chunk's partial results (new fp32 tensors
+    of the shapes in ``shapes``). They are accumulated into buffers
+    allocated up front on the main stream (the first chunk copies), so no
+    tensor allocated on the auxiliary stream outlives its chunk.
+    ``step_done(t)`` is called after reverse step ``t``; ``finish()`` joins
+    the auxiliary stream and runs the last chunk on the main stream,
+    returning the totals. Without an auxiliary stream the whole range is one
+    chunk at ``finish()``."""
+
+    def __init__(self, T: int, work, shapes, device, stream, chunk: int):
+        self.T, self.work, self.stream, self.chunk = T, work, stream, max(1, chunk)
+        self.hi = T
+        self.acc = None
+        if stream is not None:
+            self.acc = [torch.empty(s, device=device, dtype=torch.float32) for s in shapes]
+
+    def step_done(self, t: int) -> None:
+        if self.stream is None or t <= 0 or self.hi - t < self.chunk:
+            return
+        first = self.hi == self.T
+        self.stream.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(self.stream):
+            for a, p in zip(self.acc, self.work(t, self.hi)):
+                a.copy_(p) if first else a.add_(p)
+        self.hi = t
+
+    def finish(self):
+        if self.stream is not None and self.hi < self.T:
+            torch.cuda.current_stream().wait_stream(self.stream)
+        if self.hi > 0:
+            parts = self.work(0, self.hi)
+            if self.hi == self.T:
+                self.acc = parts
+            else:
+                for a, p in zip(self.acc, parts):
+                    a.add_(p)
+        return self.acc
+
+
 class _HyperSeq(torch.autograd.Function):
     """HyperLSTM layer (LN main cell modulated by a LN hyper cell).
 
@@ -677,6 +758,27 @@ class _HyperSeq(torch.autograd.Function):
         main, side = torch.cuda.current_stream(), _side_stream(dev)
         st = main.cuda_stream
         group = lp_on and not TWO_STREAM and gemm.GROUPED and S_am >= 1 and S_h >= 1
+        # weight / LayerNorm-parameter gradients: row-separable products over
+        # the T*B saved rows, accumulated chunk by chunk on the auxiliary
+        # stream while the scan continues (see _ChunkedWgrad)
+        A2 = s.A[:T].reshape(TB, K)
+        # hyper-norm projections, vec_k = (hh @ W_z_k + b_z_k) @ W_a_k: ONE long-K
+        # GEMM dP = [hh | 1]^T @ dvec gives dP_k = hh^T dvec_k and (ones row) the
+        # column sums of dvec; the per-k factors are then tiny batched products
+        HH1 = torch.zeros(TB, Hh + 8, device=dev, dtype=ldt)
+        HH1[:, :Hh] = s.HH.view(TB, Hh)
+        HH1[:, Hh] = 1.0
+        dRMf, dRYf, dVECf = dRM_lp.view(TB, G), dRY_lp.view(TB, Gh), dVEC.view(TB, 12 * H)
+
+        def wwork(t0, t1):
+            r = slice(t0 * B, t1 * B)
+            out = [gemm.wgrad(A2[r, :H], dRMf[r]), gemm.wgrad(A2[r], dRYf[r]), gemm.wgrad(HH1[r], dVECf[r])]
+            for dy, xh, n in ((DLNY, s.XHAT, G), (DLNCY, s.CHAT, H), (HDLNY, s.HXHAT, Gh), (HDLNCY, s.HCHAT, Hh)):
+                out += list(colsum(dy[t0:t1].view(-1, n), xh[t0:t1].view(-1, n)))
+            return out
+
+        wg = _ChunkedWgrad(T, wwork, [(H, G), (K, Gh), (Hh + 8, 12 * H), (G,), (G,), (H,), (H,), (Gh,), (Gh,),
+                                      (Hh,), (Hh,)], dev, _wgrad_stream(dev), WGRAD_CHUNK)
         for t in range(T - 1, -1, -1):
             clm.set(am, t)
             clh.set(ah, t)
@@ -707,12 +809,11 @@ class _HyperSeq(torch.autograd.Function):
             _check(lib.lib.skr_lstm_bwd_step(ctypes.byref(ah), 1, 0, st), "hyper_bwd_step")
             gemm.rec_gemm(dRY_lp[t], s.Wyl, DAY, S_ay)
             _join(main, side)                            # dh (main gates) for step t-1 ready
+            wg.step_done(t)
         dh0 = DAY[:, :, :H].sum(0) + DAM.sum(0)
         dhh0 = DAY[:, :, H:].sum(0)
-        # ---- weight gradients: single large GEMMs over all T*B rows ----
-        A2 = s.A[:T].reshape(TB, K)
-        dW_h = gemm.wgrad(A2[:, :H], dRM_lp.view(TB, G))
-        dW_y = gemm.wgrad(A2, dRY_lp.view(TB, Gh))
+        dW_h, dW_y, dP1, *cs = wg.finish()
+        g_ln, g_hln = cs[:4], cs[4:]
         dhW_x = torch.empty_like(s.hW_x)
         dhW_x[IN:] = dW_y[:H]
         dhW_h = dW_y[H:]
@@ -738,13 +839,6 @@ class _HyperSeq(torch.autograd.Function):
                 dx, dzc = dxf[..., :IX], dxf[..., IX:].sum(0)
             else:
                 dx = dxf
-        # hyper-norm projections, vec_k = (hh @ W_z_k + b_z_k) @ W_a_k: ONE long-K
-        # GEMM dP = [hh | 1]^T @ dvec gives dP_k = hh^T dvec_k and (ones row) the
-        # column sums of dvec; the per-k factors are then tiny batched products
-        HH1 = torch.zeros(TB, Hh + 8, device=dev, dtype=ldt)
-        HH1[:, :Hh] = s.HH.view(TB, Hh)
-        HH1[:, Hh] = 1.0
-        dP1 = gemm.wgrad(HH1, dVEC.view(TB, 12 * H))                   # [Hh + 8, 12H] fp32
         dP = dP1[:Hh].view(Hh, 12, H).transpose(0, 1)                  # [12, Hh, H]
         sV = dP1[Hh].view(12, H)                                       # column sums of dvec
         Wz3 = s.W_z.view(Hh, 12, E).transpose(0, 1)                    # [12, Hh, E]
@@ -752,8 +846,6 @@ class _HyperSeq(torch.autograd.Function):
         dWa = torch.bmm(Wz3.transpose(1, 2), dP) + s.b_z.view(12, E, 1) * sV.view(12, 1, H)
         db_z = torch.bmm(sV.view(12, 1, H), s.W_a.transpose(1, 2)).reshape(12 * E)
         dbias = sV[8:].reshape(4 * H)                                  # shift-vector grads = bias grads
-        g_ln = colsum(DLNY.view(TB, G), s.XHAT.view(TB, G)) + colsum(DLNCY.view(TB, H), s.CHAT.view(TB, H))
-        g_hln = colsum(HDLNY.view(TB, Gh), s.HXHAT.view(TB, Gh)) + colsum(HDLNCY.view(TB, Hh), s.HCHAT.view(TB, Hh))
         ctx.s = None
         return (dx, dzc, dh0, dc_rec, dhh0, dhc_rec, None, dW_x, dW_h, dbias, dhW_x, dhW_h,
                 g_hln[0], g_hln[1], g_hln[2], g_hln[3], dW_z, db_z, dWa, g_ln[0], g_ln[1], g_ln[2], g_ln[3], None)

@@ -37,7 +37,12 @@ class GraphedStep:
         torch.cuda.current_stream().wait_stream(side)
         torch.cuda.synchronize()
         self.graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.graph):
+        # With an RCCL process group its watchdog thread polls collective
+        # events concurrently; "thread_local" capture only restricts the
+        # capturing thread, so those polls cannot invalidate the capture.
+        import torch.distributed as dist
+        mode = "thread_local" if dist.is_available() and dist.is_initialized() else "global"
+        with torch.cuda.graph(self.graph, capture_error_mode=mode):
             self.outputs = fn(**self.static)
         torch.cuda.synchronize()
         with torch.no_grad():

@@ -272,6 +272,45 @@ def test_hyper_grouped_gemm_path_bitwise(H, Hh, E):
         assert torch.equal(a, b)
 
 
+@pytest.mark.parametrize("dt,cu_stride", [("fp32", 4), ("bf16", 4), ("bf16", 1)])
+def test_hyper_chunked_wgrad_overlap(dt, cu_stride):
+    """Weight / LN-parameter gradients accumulated in chunks on the
+    auxiliary (optionally CU-masked) stream while the backward scan runs
+    equal the one-shot reduction after the scan (same products, different
+    summation order), with and without HIP-graph capture."""
+    from sketch_rnn_amd.ops import recurrent
+    torch.manual_seed(4)
+    T, B, IN, H, Hh, E = 9, 100, 13, 512, 64, 8
+    p = C.HyperLSTMParams(IN, H, Hh, E).to(DEV)
+    with torch.no_grad():
+        for prm in p.parameters():
+            prm.add_(torch.randn_like(prm) * 0.05)
+    x = torch.randn(T, B, IN, device=DEV)
+    st = [torch.zeros(B, n, device=DEV) for n in (H, H, Hh, Hh)]
+    w = torch.randn(T, B, H, device=DEV)
+    saved = (recurrent.WGRAD_OVERLAP, recurrent.WGRAD_CHUNK, recurrent.WGRAD_CU_STRIDE)
+    res = []
+    try:
+        ops.set_backend("hip")
+        ops.set_compute_dtype(dt)
+        recurrent.WGRAD_CU_STRIDE = cu_stride
+        recurrent._WGRAD_STREAMS.clear()
+        for on in (False, True):
+            recurrent.WGRAD_OVERLAP, recurrent.WGRAD_CHUNK = on, 2
+            p.zero_grad()
+            xg = x.detach().clone().requires_grad_()
+            out, _ = ops.hyper_sequence(p, xg, *st, drop_keep=0.9, drop_seed=3, drop_stream=9)
+            (out * w).sum().backward()
+            res.append([xg.grad] + [q.grad.clone() for q in p.parameters()])
+        torch.cuda.synchronize()
+    finally:
+        recurrent.WGRAD_OVERLAP, recurrent.WGRAD_CHUNK, recurrent.WGRAD_CU_STRIDE = saved
+        recurrent._WGRAD_STREAMS.clear()
+    for (n, _), a, b in zip([("x", None)] + list(p.named_parameters()), *res):
+        err = (a - b).abs().max().item()
+        assert err <= 1e-5 * max(b.abs().max().item(), 1.0), (n, err)
+
+
 @pytest.mark.parametrize("M,N,K,nd", [(100, 9216, 2304, 1), (100, 2304, 9216, 1), (100, 256, 24576, 1),
                                       (100, 24576, 256, 1), (7, 64, 64, 1), (128, 2048, 512, 2),
                                       (100, 512, 2048, 2), (256, 8192, 2048, 1), (512, 1024, 256, 1)])
