@@ -35,12 +35,12 @@
 // chain costs one full memory round trip per dependency.)
 //
 // C > 1 (a row split over C workgroups) only matters with LayerNorm: the C
-// workgroups exchange partial (mean, M2) statistics inside the launch as
-// data-tagged granules -- each value travels in one 8-byte word {value,
+// workgroups exchange partial (sum, sum of squares) statistics inside the
+// launch as data-tagged granules -- each value travels in one 8-byte word {value,
 // tag = step + 1}, written with a write-through (sc1, agent-scope) 64-bit
 // store; one wave per workgroup polls the row's C*nv words with sc1 loads
 // (s_sleep backoff, bounded: a timeout sets *err for the host) until every
-// tag is current, then Chan's formula combines them. No separate flag, no
+// tag is current, then sums them. No separate flag, no
 // vmcnt drain and no counter atomics: one store-to-visible hop per exchange
 // (CDNA4 guide: handoff-1to1 vs handoff-flag). Every slot owns its
 // workgroup's 128-byte line; the buffer is zeroed once per sequence and the
@@ -91,23 +91,6 @@ __device__ void cluster_allgather(uint64_t* part, int* err, int b, int c, int C,
     lds_barrier();
 }
 
-// Row mean / variance from per-workgroup (mean, M2) pairs (Chan et al.);
-// workgroup cc holds min(span, H - cc*span) of the row's H values.
-__device__ __forceinline__ void chan_combine(const float* all, int C, int nv, int q, int H, int span, float& mean,
-                                             float& var) {
-    float m = 0.f;
-    for (int cc = 0; cc < C; ++cc) m += (float)min(span, H - cc * span) * all[cc * nv + q];
-    m /= (float)H;
-    float m2 = 0.f;
-    for (int cc = 0; cc < C; ++cc) {
-        const float n = (float)min(span, H - cc * span);
-        const float d = all[cc * nv + q] - m;
-        m2 += all[cc * nv + (nv / 2) + q] + n * d * d;
-    }
-    mean = m;
-    var = m2 / (float)H;
-}
-
 // Row-wide sums of N per-thread values: block reduction, then (C > 1) the
 // in-launch exchange. `slot` selects the (counter, partial) pair of this phase.
 template <int N, int NW>
@@ -136,7 +119,6 @@ __global__ __launch_bounds__(NT) void cell_fwd(const FwdArgs a) {
     __shared__ float all[kMaxCluster * 8];
     const int c = blockIdx.x, b = blockIdx.y, C = gridDim.x, tid = threadIdx.x, H = a.H;
     const int span = UPT * NT, base = c * span;
-    const int nloc = max(0, min(span, H - base));
     const int grp = a.grp_rows > 0 ? b / a.grp_rows : 0;
     const float* ln_g = LN ? a.ln_g + grp * 4 * H : nullptr;
     const float* ln_b = LN ? a.ln_b + grp * 4 * H : nullptr;
@@ -182,46 +164,27 @@ __global__ __launch_bounds__(NT) void cell_fwd(const FwdArgs a) {
             lcb[k] = lnc_b[uc];
         }
     }
-    // ---- LayerNorm over each gate block of the row
+    // ---- LayerNorm over each gate block of the row: sums and sums of
+    // squares in ONE row reduction (var = E[g^2] - mean^2 in fp32, clamped)
     if (LN) {
-        float s[4];
+        float s[8];
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             s[q] = 0.f;
-#pragma unroll
-            for (int k = 0; k < UPT; ++k) s[q] += on[k] ? g[k][q] : 0.f;
-        }
-        block_sum<4, NW>(s, lds);
-        float ml[4], m2[4];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            ml[q] = s[q] / (float)max(nloc, 1);
-            m2[q] = 0.f;
+            s[4 + q] = 0.f;
 #pragma unroll
             for (int k = 0; k < UPT; ++k) {
-                const float d = on[k] ? g[k][q] - ml[q] : 0.f;
-                m2[q] += d * d;
+                const float v = on[k] ? g[k][q] : 0.f;
+                s[q] += v;
+                s[4 + q] += v * v;
             }
         }
-        block_sum<4, NW>(m2, lds);
+        row_sum<8, NW>(s, lds, mine, all, a.part, a.err, a.step + 1, b, c, C);
         float mean[4], var[4];
-        if (C > 1) {
-            if (tid == 0) {
 #pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    mine[q] = ml[q];
-                    mine[4 + q] = m2[q];
-                }
-            }
-            cluster_allgather(a.part, a.err, b, c, C, mine, 8, a.step + 1, all);
-#pragma unroll
-            for (int q = 0; q < 4; ++q) chan_combine(all, C, 8, q, H, span, mean[q], var[q]);
-        } else {
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                mean[q] = ml[q];
-                var[q] = m2[q] / (float)H;
-            }
+        for (int q = 0; q < 4; ++q) {
+            mean[q] = s[q] / (float)H;
+            var[q] = fmaxf(s[4 + q] / (float)H - mean[q] * mean[q], 0.f);
         }
         float rs[4];
 #pragma unroll
@@ -262,30 +225,15 @@ __global__ __launch_bounds__(NT) void cell_fwd(const FwdArgs a) {
     }
     float th[UPT];
     if (LN) {
-        float s1[1] = {0.f};
-#pragma unroll
-        for (int k = 0; k < UPT; ++k) s1[0] += cn[k];
-        block_sum<1, NW>(s1, lds);
-        const float ml = s1[0] / (float)max(nloc, 1);
-        float s2[1] = {0.f};
+        float s2[2] = {0.f, 0.f};
 #pragma unroll
         for (int k = 0; k < UPT; ++k) {
-            const float d = on[k] ? cn[k] - ml : 0.f;
-            s2[0] += d * d;
+            s2[0] += cn[k];          // cn == 0 for units past H
+            s2[1] += cn[k] * cn[k];
         }
-        block_sum<1, NW>(s2, lds);
-        float mean, var;
-        if (C > 1) {
-            if (tid == 0) {
-                mine[0] = ml;
-                mine[1] = s2[0];
-            }
-            cluster_allgather(a.part + (int64_t)a.B * C * kSlots, a.err, b, c, C, mine, 2, a.step + 1, all);
-            chan_combine(all, C, 2, 0, H, span, mean, var);
-        } else {
-            mean = ml;
-            var = s2[0] / (float)H;
-        }
+        row_sum<2, NW>(s2, lds, mine, all, a.part + (int64_t)a.B * C * kSlots, a.err, a.step + 1, b, c, C);
+        const float mean = s2[0] / (float)H;
+        const float var = fmaxf(s2[1] / (float)H - mean * mean, 0.f);
         const float rc = rsqrtf(var + kLnEps);
         if (save && c == 0 && tid == 0) a.rstd[b * 5 + 4] = rc;
 #pragma unroll

@@ -34,6 +34,7 @@ for s in "${steps[@]}"; do
         bench_stride8) SKR_WGRAD_CU_STRIDE=8 run bench_stride8 600 python bench.py --steps 10 --warmup 2 ;;
         bench_noov) SKR_WGRAD_OVERLAP=0 run bench_noov 600 python bench.py --steps 10 --warmup 2 ;;
         bench_ch50) SKR_WGRAD_CHUNK=50 run bench_ch50 600 python bench.py --steps 10 --warmup 2 ;;
+        bench_env) run "bench_${BENCH_TAG:-env}" 600 python bench.py --steps 10 --warmup 2 ;;
         bench_nofused) SKR_FUSED=0 run bench_nofused 600 python bench.py --steps 10 --warmup 2 ;;
         bench_wgrad) run bench_wgrad 600 python scripts/bench_wgrad.py ;;
         bench_gemm) run bench_gemm 600 python scripts/bench_gemm.py ;;

@@ -522,6 +522,13 @@ class _ChunkedWgrad:
         return self.acc
 
 
+def _split_override(var: str, planned: int, K: int) -> int:
+    """Split-K factor of a per-step HyperLSTM product: the planned one, or
+    ``$var`` (tuning sweeps) when it divides K into whole 64-wide K tiles."""
+    v = int(os.environ.get(var, "0"))
+    return v if v > 0 and planned > 0 and K % (64 * v) == 0 else planned
+
+
 class _HyperSeq(torch.autograd.Function):
     """HyperLSTM layer (LN main cell modulated by a LN hyper cell).
 
@@ -602,8 +609,8 @@ class _HyperSeq(torch.autograd.Function):
             S_m, S_y = gemm.plan_splits_fp8(B, G, H), gemm.plan_splits_fp8(B, Gh, K)
             S_v = gemm.plan_splits_fp8(B, 12 * H, Hh, max_splits=1)
         else:
-            S_m = gemm.plan_splits(B, G, H, 1, dt)
-            S_y = gemm.plan_splits(B, Gh, K, 1, dt)
+            S_m = _split_override("SKR_HYP_SM", gemm.plan_splits(B, G, H, 1, dt), H)
+            S_y = _split_override("SKR_HYP_SY", gemm.plan_splits(B, Gh, K, 1, dt), K)
             S_v = gemm.plan_splits(B, 12 * H, Hh, 1, dt, max_splits=1)
         rgemm = (lambda a, b, out, S: gemm.rec_gemm_fp8(a, b, out, S)) if fp8 else \
             (lambda a, b, out, S: gemm.rec_gemm(a, b, out, S))
@@ -719,9 +726,9 @@ class _HyperSeq(torch.autograd.Function):
         HDLNY = torch.empty(T, B, Gh, device=dev, dtype=f32)
         HDLNCY = torch.empty(T, B, Hh, device=dev, dtype=f32)
         dVEC = torch.empty(T, B, 12 * H, device=dev, dtype=ldt)
-        S_h = gemm.plan_splits(B, Hh, 12 * H, 1, ldt)
-        S_am = gemm.plan_splits(B, H, G, 1, ldt)
-        S_ay = gemm.plan_splits(B, K, Gh, 1, ldt)
+        S_h = _split_override("SKR_HYP_SH", gemm.plan_splits(B, Hh, 12 * H, 1, ldt), 12 * H)
+        S_am = _split_override("SKR_HYP_SAM", gemm.plan_splits(B, H, G, 1, ldt), G)
+        S_ay = _split_override("SKR_HYP_SAY", gemm.plan_splits(B, K, Gh, 1, ldt), Gh)
         DHZ = torch.empty(max(S_h, 1), B, Hh, device=dev, dtype=f32)    # slabs of dhh from the vec path
         DAM = torch.zeros(max(S_am, 1), B, H, device=dev, dtype=f32)    # slabs of dh from the main gates
         DAY = torch.zeros(max(S_ay, 1), B, K, device=dev, dtype=f32)    # slabs of d[h | hh] from the hyper gates

@@ -29,6 +29,7 @@ import numpy as np
 import torch
 
 from ..models import mdn as M
+from ..train.graph import capture
 
 
 def _get_pi_idx(x: float, pdf: np.ndarray) -> int:
@@ -297,7 +298,7 @@ class GraphDecoder:
                     self._decode()
                 torch.cuda.current_stream().wait_stream(s)
                 self.graph = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(self.graph):
+                with capture(self.graph):
                     self._decode()
             self.graph.replay()
         else:

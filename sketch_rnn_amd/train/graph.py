@@ -18,9 +18,34 @@ scalars) and restores it after capture.
 """
 from __future__ import annotations
 
+import contextlib
+import gc
 from typing import Callable, Dict, Optional
 
 import torch
+
+
+@contextlib.contextmanager
+def capture(graph: "torch.cuda.CUDAGraph"):
+    """``torch.cuda.graph`` with Python's cyclic GC held off for the
+    duration of the capture. A collection triggered by an allocation inside
+    the captured region could run the destructor of an unreachable object
+    that owns HIP resources (an earlier ``CUDAGraph``, an event), and such
+    HIP calls are illegal while a stream is capturing -- the process aborts.
+    Garbage is collected before the capture instead. Under an initialised
+    process group the capture mode is "thread_local": the RCCL watchdog
+    thread polls collective events concurrently and must not invalidate it."""
+    import torch.distributed as dist
+    mode = "thread_local" if dist.is_available() and dist.is_initialized() else "global"
+    gc.collect()
+    enabled = gc.isenabled()
+    gc.disable()
+    try:
+        with torch.cuda.graph(graph, capture_error_mode=mode):
+            yield
+    finally:
+        if enabled:
+            gc.enable()
 
 
 class GraphedStep:
@@ -37,12 +62,7 @@ class GraphedStep:
         torch.cuda.current_stream().wait_stream(side)
         torch.cuda.synchronize()
         self.graph = torch.cuda.CUDAGraph()
-        # With an RCCL process group its watchdog thread polls collective
-        # events concurrently; "thread_local" capture only restricts the
-        # capturing thread, so those polls cannot invalidate the capture.
-        import torch.distributed as dist
-        mode = "thread_local" if dist.is_available() and dist.is_initialized() else "global"
-        with torch.cuda.graph(self.graph, capture_error_mode=mode):
+        with capture(self.graph):
             self.outputs = fn(**self.static)
         torch.cuda.synchronize()
         with torch.no_grad():
