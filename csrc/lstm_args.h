@@ -36,6 +36,7 @@ struct FwdArgs {
     int cluster;                       // <= 1: one workgroup per row
     uint64_t* part;                    // [2][B][cluster][16] tagged partial statistics (zeroed per sequence)
     int* err;                          // set to 1 if a cluster wait timed out
+    __hip_bfloat16* r_lp;              // MOD: bf16 copy of the summed R ([B, ld_R]) for the backward, or null
 };
 
 struct BwdArgs {
@@ -71,6 +72,7 @@ struct BwdArgs {
     // LN: the gate activations are recomputed from xhat (the forward does not
     // store them): act = sig/tanh(xhat * ln_g + ln_b (+ forget_bias on f))
     const float* ln_b; float forget_bias;
+    const __hip_bfloat16* r_lp;        // MOD: R from the forward's bf16 copy (stride ld_R) instead of the slabs
 };
 
 // hyper modulation vectors: MOD 1 fp32, MOD 2 bf16

@@ -134,6 +134,7 @@ __global__ __launch_bounds__(NT) void cell_fwd(const FwdArgs a) {
 
     // ---- every load up front (clamped indices; results of u >= H discarded)
     float g[UPT][4], cp[UPT], lg[UPT][4], lb[UPT][4], lcg[UPT], lcb[UPT];
+    float rsv[UPT][4];   // MOD: summed R (saved in bf16 for the backward when r_lp is set)
     bool on[UPT];
 #pragma unroll
     for (int k = 0; k < UPT; ++k) {
@@ -150,6 +151,7 @@ __global__ __launch_bounds__(NT) void cell_fwd(const FwdArgs a) {
                 const float ah = ldvec<MOD>(a.vec, (4 + q) * a.vec_gs + vo) + a.vec_bias[(4 + q) * H + uc];
                 const float bh = ldvec<MOD>(a.vec, (8 + q) * a.vec_gs + vo) + a.vec_bias[(8 + q) * H + uc];
                 g[k][q] = xv * ax + rv * ah + bh + a.bias[q * H + uc];
+                rsv[k][q] = rv;
             } else {
                 g[k][q] = xv + rv;
             }
@@ -222,6 +224,10 @@ __global__ __launch_bounds__(NT) void cell_fwd(const FwdArgs a) {
             ap[3 * H] = o;
         }
         if (a.c_out != nullptr && on[k]) a.c_out[ro] = cn[k];
+        if (MOD && a.r_lp != nullptr && on[k]) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) a.r_lp[b * a.ld_R + q * H + u] = to_bf16(rsv[k][q]);
+        }
     }
     float th[UPT];
     if (LN) {
@@ -316,7 +322,8 @@ __global__ __launch_bounds__(NT) void cell_bwd(const BwdArgs a) {
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
                 xv[k][q] = a.xp[b * a.ld_xp + q * H + uc];
-                rv[k][q] = slab_sum<NS>(a.R, b * a.ld_R + q * H + uc, a.R_nslab, a.R_slab);
+                rv[k][q] = a.r_lp != nullptr ? __bfloat162float(a.r_lp[b * a.ld_R + q * H + uc])
+                                             : slab_sum<NS>(a.R, b * a.ld_R + q * H + uc, a.R_nslab, a.R_slab);
                 ax[k][q] = ldvec<MOD>(a.vec, q * a.vec_gs + vo) + a.vec_bias[q * H + uc];
                 ah[k][q] = ldvec<MOD>(a.vec, (4 + q) * a.vec_gs + vo) + a.vec_bias[(4 + q) * H + uc];
             }

@@ -36,6 +36,7 @@ class LstmFwdArgs(C.Structure):
         ("h_lp", _p), ("ld_lp", _i64), ("lp_kind", _i),
         ("c_carry", _p),
         ("cluster", _i), ("part", _p), ("err", _p),
+        ("r_lp", _p),
     ]
 
 
@@ -68,6 +69,7 @@ class LstmBwdArgs(C.Structure):
         ("dinit_h", _p), ("dinit_c", _p),
         ("cluster", _i), ("part", _p), ("err", _p),
         ("ln_b", _p), ("forget_bias", _f),
+        ("r_lp", _p),
     ]
 
 

@@ -617,7 +617,15 @@ class _HyperSeq(torch.autograd.Function):
         A = torch.empty(T + 1, B, K, device=dev, dtype=torch.uint8 if fp8 else dt)
         A[0, :, :H].copy_(_to_fp8_act(h0) if fp8 else h0)
         A[0, :, H:].copy_(_to_fp8_act(hh0) if fp8 else hh0)
-        RM = torch.empty(T, max(S_m, 1), B, G, device=dev, dtype=f32)   # saved: the backward re-reads R_main
+        # R_main: the backward re-reads it (the hyper-modulation gradient
+        # dg * R). With bf16 modulation vectors the main cell saves a bf16 copy
+        # of the summed R, so the GEMM's fp32 split-K slabs live in ONE buffer
+        # reused by every step (cache-resident) instead of T saved slab sets;
+        # at inference nothing is saved either
+        vbf = not fp8 and dt == torch.bfloat16 and B <= 128 and S_v == 1
+        RLP = torch.empty(T, B, G, device=dev, dtype=torch.bfloat16) if (vbf and not infer) else None
+        RM = torch.empty(T if (RLP is None and not infer) else 1, max(S_m, 1), B, G, device=dev, dtype=f32)
+        rmi = (lambda t: t) if RM.shape[0] == T else (lambda t: 0)
         RY = torch.empty(max(S_y, 1), B, Gh, device=dev, dtype=f32)
         CC = torch.empty(T + 1, B, H, device=dev, dtype=f32)
         CC[0].copy_(c0)
@@ -631,7 +639,6 @@ class _HyperSeq(torch.autograd.Function):
         XHAT, RSTD, CHAT = sv(T, B, G), sv(T, B, 5), sv(T, B, H)
         HXHAT, HRSTD, HCHAT = sv(T, B, Gh), sv(T, B, 5), sv(T, B, Hh)
         # modulation vectors in bf16 when the GEMMs are bf16 (read only by the main cells)
-        vbf = not fp8 and dt == torch.bfloat16 and B <= 128 and S_v == 1
         VEC = torch.empty(T, B, 12 * H, device=dev, dtype=torch.bfloat16 if vbf else f32)
         mod = 2 if vbf else 1
         sd = _seed_tensor(seed, dev)
@@ -665,11 +672,11 @@ class _HyperSeq(torch.autograd.Function):
             clm.set(am, t)
             clh.set(ah, t)
             if group:   # R_main and R_hyp in one launch
-                gemm.rec_gemm_group([(A[t, :, :H], WhT, RM[t], S_m), (A[t], WyT, RY, S_y)])
+                gemm.rec_gemm_group([(A[t, :, :H], WhT, RM[rmi(t)], S_m), (A[t], WyT, RY, S_y)])
             else:
                 _join(side, main)                        # h_{t-1} written
                 with torch.cuda.stream(side):
-                    rgemm(A[t, :, :H], WhT, RM[t], S_m)
+                    rgemm(A[t, :, :H], WhT, RM[rmi(t)], S_m)
                 rgemm(A[t], WyT, RY, S_y)
             ah.xp, ah.c_prev, ah.step = XHY[t].data_ptr(), HCC[t].data_ptr(), t
             ah.h_out = HH[t].data_ptr()
@@ -682,7 +689,8 @@ class _HyperSeq(torch.autograd.Function):
             else:
                 rgemm(A[t + 1, :, H:], PlT, VEC[t].unsqueeze(0), S_v)
             _join(main, side)                            # R_main(t) done
-            am.xp, am.R, am.vec = XH[t].data_ptr(), RM[t].data_ptr(), VEC[t].data_ptr()
+            am.xp, am.R, am.vec = XH[t].data_ptr(), RM[rmi(t)].data_ptr(), VEC[t].data_ptr()
+            am.r_lp = RLP[t].data_ptr() if RLP is not None else None
             am.c_prev, am.step = CC[t].data_ptr(), t
             am.h_out = Hout[t].data_ptr()
             if not infer:
@@ -692,7 +700,7 @@ class _HyperSeq(torch.autograd.Function):
         hT = Hout[T - 1].clone()    # no resets: the carried h is h'
         hhT = HH[T - 1].clone()
         s = _Saved()
-        for k, v in dict(xl=xl, x=x, zc=zc, bp=bp, XH=XH, Whl=Whl, Wyl=Wyl, Pl=Pl, q=q, bias_c=bias_c, S_m=S_m, A=A, RM=RM, CC=CC,
+        for k, v in dict(xl=xl, x=x, zc=zc, bp=bp, XH=XH, Whl=Whl, Wyl=Wyl, Pl=Pl, q=q, bias_c=bias_c, S_m=S_m, A=A, RM=RM, RLP=RLP, CC=CC,
                          HCC=HCC, XHAT=XHAT, RSTD=RSTD, CHAT=CHAT, HH=HH,
                          HXHAT=HXHAT, HRSTD=HRSTD, HCHAT=HCHAT, VEC=VEC, seed=sd, meta=meta, W_x=W_x,
                          hW_x=hW_x, W_z=W_z, b_z=b_z, W_a=W_a, mln=mln, hln=hln).items():
@@ -792,7 +800,11 @@ class _HyperSeq(torch.autograd.Function):
             am.dh_out = dHout[t].data_ptr() if dHout is not None else None
             am.c_prev = s.CC[t].data_ptr()
             am.xhat, am.rstd, am.chat = s.XHAT[t].data_ptr(), s.RSTD[t].data_ptr(), s.CHAT[t].data_ptr()
-            am.xp, am.R, am.vec = s.XH[t].data_ptr(), s.RM[t].data_ptr(), s.VEC[t].data_ptr()
+            am.xp, am.vec = s.XH[t].data_ptr(), s.VEC[t].data_ptr()
+            if s.RLP is not None:
+                am.R, am.r_lp = None, s.RLP[t].data_ptr()
+            else:
+                am.R, am.r_lp = s.RM[t].data_ptr(), None
             am.step = t
             am.dG = None if lp_on else dRM[t].data_ptr()
             am.dG_lp = dRM_lp[t].data_ptr() if lp_on else None
