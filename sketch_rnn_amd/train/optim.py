@@ -72,8 +72,34 @@ class FlatAdam:
         self.lr = float(lr)
         self.scalars[0].fill_(self.lr)
 
-    def zero_grad(self) -> None:
-        self.grad.zero_()
+    def zero_grad(self, set_to_none: bool = False) -> None:
+        """``set_to_none``: unbind ``p.grad`` so autograd hands over the
+        gradient tensors it produces instead of adding each into a zeroed
+        arena view (one fill + one add launch per parameter); follow the
+        backward with :meth:`gather_grads`."""
+        if set_to_none:
+            for p in self.params:
+                p.grad = None
+        else:
+            self.grad.zero_()
+
+    def gather_grads(self) -> None:
+        """After ``zero_grad(set_to_none=True)`` + backward: copy the
+        produced gradients into the arena with one multi-tensor copy, zero
+        the slots of parameters that received none, and rebind ``p.grad`` to
+        the arena views. Capture-safe (fixed pointer lists)."""
+        dst, src = [], []
+        for p, o in zip(self.params, self.offsets):
+            view = self.grad[o:o + p.numel()].view_as(p)
+            g = p.grad
+            if g is None:
+                view.zero_()
+            elif g.data_ptr() != view.data_ptr():
+                dst.append(view)
+                src.append(g)
+            p.grad = view
+        if dst:
+            torch._foreach_copy_(dst, src)
 
     def named_slices(self):
         for p, o in zip(self.params, self.offsets):

@@ -71,9 +71,10 @@ class ReferenceTrainer:
     # ---------------------------------------------------------------------------------
     def _step_fn(self, x, y, state_flat):
         state = self._unflatten(state_flat)
-        self.opt.zero_grad()
+        self.opt.zero_grad(set_to_none=True)
         cost, shape, pen, final = self.model.loss(x, y, state, train=True, drop_seed=self.seed)
         cost.backward()
+        self.opt.gather_grads()
         self.opt.step()
         with torch.no_grad():
             for dst, src in zip(state_flat, self._flatten(final)):
@@ -215,10 +216,11 @@ class VAETrainer:
         self.gpu_times = GpuPhaseTimer(enabled=metrics_path is not None)
 
     def _fwd_bwd(self, strokes, lengths, labels):
-        self.opt.zero_grad()
+        self.opt.zero_grad(set_to_none=True)
         out = self.model.loss(strokes, lengths, labels if self.cfg.num_classes > 0 else None,
                               kl_weight=self.kl_w, train=True, seed=self.seed)
         out["cost"].backward()
+        self.opt.gather_grads()
         return {k: v.detach() for k, v in out.items()}
 
     def _opt_step(self):

@@ -66,6 +66,35 @@ def test_flat_adam_params_are_arena_views():
     assert float(opt.grad.abs().sum()) == 0.0
 
 
+def test_flat_adam_gather_grads_equals_accumulation():
+    """zero_grad(set_to_none) + backward + gather_grads fills the arena
+    exactly like accumulating into zeroed arena views; parameters without a
+    gradient get zeroed slots (stale values from the previous step are
+    cleared) and p.grad is rebound to the arena."""
+    torch.manual_seed(0)
+    ps = [torch.nn.Parameter(torch.randn(5, 3)), torch.nn.Parameter(torch.randn(3)),
+          torch.nn.Parameter(torch.randn(4))]
+    x = torch.randn(7, 5)
+
+    def loss():
+        return ((x @ ps[0] + ps[1]) ** 2).sum()    # ps[2] unused
+
+    opt = FlatAdam(ps, lr=0.1)
+    opt.zero_grad()
+    loss().backward()
+    ref = opt.grad.clone()
+    opt.grad.fill_(9.0)                              # stale contents
+    opt.zero_grad(set_to_none=True)
+    assert all(p.grad is None for p in ps)
+    loss().backward()
+    opt.gather_grads()
+    o = opt.offsets
+    for i, p in enumerate(ps):
+        assert p.grad.data_ptr() == opt.grad[o[i]:].data_ptr()
+        assert torch.equal(opt.grad[o[i]:o[i] + p.numel()], ref[o[i]:o[i] + p.numel()])
+    assert float(opt.grad[o[2]:o[2] + 4].abs().sum()) == 0.0
+
+
 def test_schedules():
     rc = RefConfig()
     assert schedules.reference_lr(rc, 0) == 0.005
