@@ -179,7 +179,12 @@ class SketchVAE(nn.Module):
     # -- training objective -------------------------------------------------------------
     def loss(self, strokes: torch.Tensor, lengths: torch.Tensor, labels: Optional[torch.Tensor] = None,
              kl_weight: float = 1.0, train: bool = True, seed: int = 0,
-             eps: Optional[torch.Tensor] = None) -> Dict[str, torch.Tensor]:
+             eps: Optional[torch.Tensor] = None, split_encoder: bool = False) -> Dict[str, torch.Tensor]:
+        """``split_encoder``: cut the autograd graph at the encoder outputs
+        (``mu``, ``presig``); ``cost.backward()`` then stops there and the
+        result carries ``"_enc": ((mu, presig), (mu_cut, presig_cut))`` so the
+        caller runs the encoder's backward as a separate phase
+        (``torch.autograd.backward(enc, [t.grad for t in cut])``)."""
         cfg = self.cfg
         B = strokes.shape[0]
         Nmax = strokes.shape[1] - 1
@@ -188,6 +193,10 @@ class SketchVAE(nn.Module):
         kl = strokes.new_zeros(())
         if cfg.conditional:
             mu, presig = self.encode(strokes, lengths, train, seed)
+            if split_encoder:
+                enc = (mu, presig)
+                mu, presig = mu.detach().requires_grad_(), presig.detach().requires_grad_()
+                enc_cut = (enc, (mu, presig))
             sigma = torch.exp(presig / 2.0)
             if eps is None:
                 eps = C.hash_normal(seed, _S_EPS, 0, (B, cfg.z_size), dev)
@@ -203,7 +212,10 @@ class SketchVAE(nn.Module):
         r_cost, shape, pen = ops.mdn_loss(zout, target, cfg.num_mixture, mode="magenta",
                                           is_training=cfg.is_training)
         cost = r_cost + kl * kl_weight
-        return {"cost": cost, "r_cost": r_cost, "kl_cost": kl, "shape_cost": shape, "pen_cost": pen}
+        out = {"cost": cost, "r_cost": r_cost, "kl_cost": kl, "shape_cost": shape, "pen_cost": pen}
+        if split_encoder and cfg.conditional:
+            out["_enc"] = enc_cut
+        return out
 
     # -- sampling helpers --------------------------------------------------------------------
     @torch.no_grad()

@@ -76,15 +76,29 @@ def barrier() -> None:
 
 
 class GradReducer:
-    """Bucketed average of a flat gradient arena across ranks."""
+    """Bucketed average of a flat gradient arena across ranks.
 
-    def __init__(self, grad: torch.Tensor, bucket_mb: float = 32.0):
+    ``split``: arena offset separating gradients that are final early in the
+    backward from those produced last (the VAE encoder); each part gets its
+    own buckets so the first part's reduction can run while the rest of the
+    backward computes (:meth:`start` per part, one :meth:`wait`)."""
+
+    def __init__(self, grad: torch.Tensor, bucket_mb: float = 32.0, split: Optional[int] = None):
         self.grad = grad
         n = grad.numel()
         per = max(1, int(bucket_mb * 1024 * 1024 // 4))
         per = (per + 63) // 64 * 64
-        self.buckets: List[torch.Tensor] = [grad[i:i + per] for i in range(0, n, per)]
+        bounds = [0, n] if not split or split >= n else [0, split, n]
+        self.parts: List[List[torch.Tensor]] = [
+            [grad[i:min(i + per, hi)] for i in range(lo, hi, per)] for lo, hi in zip(bounds, bounds[1:])]
+        self.buckets: List[torch.Tensor] = [b for part in self.parts for b in part]
         self.world = world_size()
+
+    def start(self, part: int):
+        """Issue the SUM all-reduces of one part's buckets (async)."""
+        if self.world <= 1:
+            return []
+        return [dist.all_reduce(b, op=dist.ReduceOp.SUM, async_op=True) for b in self.parts[part]]
 
     def all_reduce(self, async_op: bool = False):
         """Sum every bucket across ranks (all in flight at once), then one
@@ -93,14 +107,14 @@ class GradReducer:
         version."""
         if self.world <= 1:
             return []
-        works = [dist.all_reduce(b, op=dist.ReduceOp.SUM, async_op=True) for b in self.buckets]
+        works = [w for i in range(len(self.parts)) for w in self.start(i)]
         if async_op:
             return works
         self.wait(works)
         return []
 
     def wait(self, works) -> None:
-        """Complete an ``all_reduce(async_op=True)`` (and apply 1/world)."""
+        """Complete issued all-reduces (and apply 1/world to the arena)."""
         for w in works:
             w.wait()
         if self.world > 1:

@@ -26,7 +26,7 @@ import torch
 
 
 @contextlib.contextmanager
-def capture(graph: "torch.cuda.CUDAGraph"):
+def capture(graph: "torch.cuda.CUDAGraph", pool=None):
     """``torch.cuda.graph`` with Python's cyclic GC held off for the
     duration of the capture. A collection triggered by an allocation inside
     the captured region could run the destructor of an unreachable object
@@ -41,7 +41,7 @@ def capture(graph: "torch.cuda.CUDAGraph"):
     enabled = gc.isenabled()
     gc.disable()
     try:
-        with torch.cuda.graph(graph, capture_error_mode=mode):
+        with torch.cuda.graph(graph, pool=pool, capture_error_mode=mode):
             yield
     finally:
         if enabled:
@@ -76,3 +76,54 @@ class GraphedStep:
                 dst.copy_(v, non_blocking=True)
         self.graph.replay()
         return self.outputs
+
+
+class GraphedPhases:
+    """A step split into consecutive phases, each captured in its own HIP
+    graph (one shared memory pool, replayed in capture order), so that host
+    work -- the RCCL collectives of data parallelism -- can be issued
+    between them while the next phase runs.
+
+    ``phases[0]`` takes the static inputs; later phases take no arguments
+    and communicate through state they keep themselves (e.g. the encoder
+    outputs and their gradients stashed by phase 0 for phase 1). Warm-up
+    runs every phase in order; the optimizer arena is snapshotted and
+    restored around warm-up + capture exactly as in :class:`GraphedStep`.
+    """
+
+    def __init__(self, phases, static_inputs: Dict[str, torch.Tensor], warmup: int = 2,
+                 snapshot: Optional[list] = None):
+        self.phases = list(phases)
+        self.static = static_inputs
+        saved = [t.detach().clone() for t in (snapshot or [])]
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            for _ in range(max(1, warmup)):
+                self.phases[0](**self.static)
+                for fn in self.phases[1:]:
+                    fn()
+        torch.cuda.current_stream().wait_stream(side)
+        torch.cuda.synchronize()
+        self.graphs = []
+        self.outputs = []
+        pool = None
+        for i, fn in enumerate(self.phases):
+            g = torch.cuda.CUDAGraph()
+            with capture(g, pool=pool):
+                self.outputs.append(fn(**self.static) if i == 0 else fn())
+            pool = g.pool() if pool is None else pool
+            self.graphs.append(g)
+        torch.cuda.synchronize()
+        with torch.no_grad():
+            for t, s in zip(snapshot or [], saved):
+                t.copy_(s)
+
+    def replay(self, i: int, **inputs):
+        if i == 0:
+            for k, v in inputs.items():
+                dst = self.static[k]
+                if v.data_ptr() != dst.data_ptr():
+                    dst.copy_(v, non_blocking=True)
+        self.graphs[i].replay()
+        return self.outputs[i]

@@ -53,6 +53,7 @@ class FlatAdam:
             self.offsets.append(off)
             off += (p.numel() + align - 1) // align * align
         self.numel = off
+        self.offset_of = {id(p): o for p, o in zip(self.params, self.offsets)}
         self.flat = torch.zeros(off, device=dev, dtype=torch.float32)
         self.grad = torch.zeros(off, device=dev, dtype=torch.float32)
         self.m = torch.zeros(off, device=dev, dtype=torch.float32)
@@ -83,13 +84,17 @@ class FlatAdam:
         else:
             self.grad.zero_()
 
-    def gather_grads(self) -> None:
+    def gather_grads(self, params=None) -> None:
         """After ``zero_grad(set_to_none=True)`` + backward: copy the
         produced gradients into the arena with one multi-tensor copy, zero
         the slots of parameters that received none, and rebind ``p.grad`` to
-        the arena views. Capture-safe (fixed pointer lists)."""
+        the arena views. Capture-safe (fixed pointer lists). ``params``: only
+        these parameters (a backward split into phases gathers per phase)."""
+        sel = None if params is None else {id(p) for p in params}
         dst, src = [], []
         for p, o in zip(self.params, self.offsets):
+            if sel is not None and id(p) not in sel:
+                continue
             view = self.grad[o:o + p.numel()].view_as(p)
             g = p.grad
             if g is None:

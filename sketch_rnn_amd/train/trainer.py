@@ -30,7 +30,7 @@ from ..ops import gemm
 from ..parallel import dp
 from ..utils.trace import GpuPhaseTimer, PhaseTimes, phase
 from . import schedules
-from .graph import GraphedStep
+from .graph import GraphedPhases, GraphedStep
 from .optim import FlatAdam
 
 
@@ -196,12 +196,23 @@ class VAETrainer:
         self.model = SketchVAE(cfg).to(self.device)
         from .. import ops
         ops.set_compute_dtype(compute_dtype)
+        # arena order: parameters whose gradients are final once the decoder /
+        # head backward is done, then the encoder's (computed last); with DP
+        # the first part's all-reduce overlaps the encoder backward
+        enc = self.model.encoder
+        enc_ids = {id(p) for p in enc.parameters()} if enc is not None else set()
+        self._early = [p for p in self.model.parameters() if id(p) not in enc_ids]
+        self._late = [p for p in self.model.parameters() if id(p) in enc_ids]
         # a step with a non-finite gradient is dropped on the device and counted (FlatAdam)
-        self.opt = FlatAdam(self.model.parameters(), lr=cfg.learning_rate, eps=cfg.adam_eps,
+        self.opt = FlatAdam(self._early + self._late, lr=cfg.learning_rate, eps=cfg.adam_eps,
                             clip_mode="value", clip=cfg.grad_clip, nonfinite="skip")
         self.max_skipped = max_skipped
         dp.broadcast_params(self.opt.flat)
-        self.reducer = dp.GradReducer(self.opt.grad) if self.world > 1 else None
+        late = [p for p in self._late if p.requires_grad]
+        self.overlap = (self.world > 1 and bool(late) and os.environ.get("SKR_DP_OVERLAP", "1") != "0")
+        split = self.opt.offset_of[id(late[0])] if self.overlap else None
+        self.reducer = dp.GradReducer(self.opt.grad, split=split) if self.world > 1 else None
+        self._enc_pending = None
         self.save_dir = save_dir
         self.log = log
         self.metrics_path = metrics_path
@@ -227,6 +238,25 @@ class VAETrainer:
         self.opt.step()
         return {}
 
+    # two-phase backward (DP overlap): phase A = forward + backward down to
+    # the encoder outputs, phase B = the encoder backward
+    def _fwd_bwd_a(self, strokes, lengths, labels):
+        self.opt.zero_grad(set_to_none=True)
+        out = self.model.loss(strokes, lengths, labels if self.cfg.num_classes > 0 else None,
+                              kl_weight=self.kl_w, train=True, seed=self.seed, split_encoder=True)
+        enc, cut = out.pop("_enc")
+        out["cost"].backward()
+        self.opt.gather_grads(self._early)
+        self._enc_pending = (enc, [t.grad for t in cut])
+        return {k: v.detach() for k, v in out.items()}
+
+    def _bwd_b(self):
+        enc, grads = self._enc_pending
+        self._enc_pending = None
+        torch.autograd.backward(list(enc), grads)
+        self.opt.gather_grads(self._late)
+        return {}
+
     def _step_fn(self, strokes, lengths, labels):
         out = self._fwd_bwd(strokes, lengths, labels)
         if self.reducer is not None:
@@ -236,12 +266,17 @@ class VAETrainer:
 
     def train_step(self, strokes, lengths, labels):
         """One optimisation step. On the GPU the forward+backward is one
-        captured HIP graph; with DP the bucketed RCCL all-reduce runs between
-        it and a second graph holding the fused clip+Adam update."""
+        captured HIP graph; with DP (and an encoder) the step runs as three
+        graphs with the bucketed RCCL all-reduces issued between them, the
+        decoder/head part overlapping the encoder backward
+        (:meth:`_train_step_overlap`; ``SKR_DP_OVERLAP=0``: one all-reduce
+        between the forward+backward graph and the clip+Adam graph).""" 
         gemm.invalidate_derived()   # weights change in place (possibly inside a graph replay)
         self.opt.set_lr(schedules.vae_lr(self.cfg, self.step))
         self.kl_w.fill_(schedules.kl_weight(self.cfg, self.step))
-        if self.use_graph:
+        if self.overlap:
+            out = self._train_step_overlap(strokes, lengths, labels)
+        elif self.use_graph:
             if self._graph is None:
                 static = {"strokes": strokes.clone(), "lengths": lengths.clone(), "labels": labels.clone()}
                 snap = [self.opt.flat, self.opt.m, self.opt.v, self.opt.scalars]
@@ -263,6 +298,33 @@ class VAETrainer:
                 out = self._step_fn(strokes, lengths, labels)
         self.seed.add_(self.world)
         self.step += 1
+        return out
+
+    def _train_step_overlap(self, strokes, lengths, labels):
+        """DP step with the decoder/head gradient all-reduce in flight while
+        the encoder backward runs: [phase A] -> all-reduce(part 0, async)
+        -> [phase B] -> all-reduce(part 1, async) -> wait -> [clip + Adam].
+        On the GPU each bracketed phase is a captured HIP graph."""
+        if self.use_graph:
+            if self._graph is None:
+                static = {"strokes": strokes.clone(), "lengths": lengths.clone(), "labels": labels.clone()}
+                snap = [self.opt.flat, self.opt.m, self.opt.v, self.opt.scalars]
+                self._graph = GraphedPhases([self._fwd_bwd_a, self._bwd_b, self._opt_step], static, snapshot=snap)
+            with self.gpu_times.time("fwd_bwd"):
+                out = self._graph.replay(0, strokes=strokes, lengths=lengths, labels=labels)
+                w0 = self.reducer.start(0)
+                self._graph.replay(1)
+            with self.gpu_times.time("allreduce"):
+                self.reducer.wait(w0 + self.reducer.start(1))
+            with self.gpu_times.time("optimizer"):
+                self._graph.replay(2)
+            return out
+        with self.gpu_times.time("step"):
+            out = self._fwd_bwd_a(strokes, lengths, labels)
+            w0 = self.reducer.start(0)
+            self._bwd_b()
+            self.reducer.wait(w0 + self.reducer.start(1))
+            self.opt.step()
         return out
 
     def batch_to_device(self, batch):

@@ -101,3 +101,36 @@ def test_dp_vae_trainer_ranks_stay_in_sync(tmp_path):
     v = [torch.load(tmp_path / ("v%d.pt" % k), weights_only=True) for k in range(2)]
     assert torch.equal(v[0]["flat"], v[1]["flat"])
     assert v[0]["ev"] == v[1]["ev"]
+
+
+def _vae_overlap_worker(rank, world, port, out_dir):
+    """Same training run with the two-phase overlapped step (decoder/head
+    all-reduce in flight during the encoder backward) and with the plain
+    step: the updates must agree bit for bit."""
+    dp = _init(rank, world, port)
+    from sketch_rnn_amd.cli.vae_train import make_datasets
+    from sketch_rnn_amd.config import VAEConfig
+    from sketch_rnn_amd.train.trainer import VAETrainer
+    res = {}
+    for mode in ("1", "0"):
+        os.environ["SKR_DP_OVERLAP"] = mode
+        cfg = VAEConfig(enc_rnn_size=8, dec_rnn_size=16, z_size=4, num_mixture=2, max_seq_len=24, batch_size=4,
+                        save_every=0, seed=rank, num_classes=3)
+        (tr_set, va, te), _ = make_datasets(cfg, None, 40, rank=rank)
+        tr = VAETrainer(cfg, tr_set, va, te, save_dir=os.path.join(out_dir, "o" + mode), log=lambda s: None)
+        assert tr.overlap == (mode == "1")
+        if tr.overlap:
+            assert len(tr.reducer.parts) == 2
+        tr.train(num_steps=3, log_every=1)
+        res[mode] = tr.opt.flat.clone()
+    os.environ.pop("SKR_DP_OVERLAP")
+    torch.save(res, os.path.join(out_dir, "o%d.pt" % rank))
+    dp.barrier()
+    torch.distributed.destroy_process_group()
+
+
+def test_dp_overlapped_step_matches_plain_step(tmp_path):
+    _spawn(_vae_overlap_worker, tmp_path)
+    o = [torch.load(tmp_path / ("o%d.pt" % k), weights_only=True) for k in range(2)]
+    assert torch.equal(o[0]["1"], o[0]["0"])
+    assert torch.equal(o[0]["1"], o[1]["1"])
