@@ -54,6 +54,8 @@ for s in "${steps[@]}"; do
         bench_ref_cudnn) run bench_ref_cudnn 600 python scripts/bench_reference.py --cudnn ;;
         prof) run prof 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --no-eval ;;
         dp_rehearsal) run dp_rehearsal 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 --steps 3 --warmup 2 --dist-backend gloo --config vae_small ;;
+        dp_rehearsal_noov) SKR_DP_OVERLAP=0 run dp_rehearsal_noov 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29518 bench.py --gpus 2 --steps 3 --warmup 2 --dist-backend gloo --config vae_small ;;
+        dp_rehearsal_nograph) run dp_rehearsal_nograph 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29519 bench.py --gpus 2 --steps 3 --warmup 2 --dist-backend gloo --config vae_small --no-graph ;;
         prof_sample) run prof_sample 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_sample -o run --output-format csv -- python scripts/bench_sample.py --reps 1 --host-steps 2 ;;
         *) echo "unknown step $s"; exit 2 ;;
     esac

@@ -33,6 +33,10 @@ def rank() -> int:
     return dist.get_rank() if is_dist() else 0
 
 
+def backend() -> Optional[str]:
+    return dist.get_backend() if is_dist() else None
+
+
 def world_size() -> int:
     return dist.get_world_size() if is_dist() else 1
 

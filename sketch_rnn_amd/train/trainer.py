@@ -209,7 +209,15 @@ class VAETrainer:
         self.max_skipped = max_skipped
         dp.broadcast_params(self.opt.flat)
         late = [p for p in self._late if p.requires_grad]
-        self.overlap = (self.world > 1 and bool(late) and os.environ.get("SKR_DP_OVERLAP", "1") != "0")
+        # SKR_DP_OVERLAP: "1" on, "0" off, default on for RCCL only. gloo's
+        # CUDA collectives stage through host threads that block on stream
+        # syncs: the overlapped step measured 4.1 s/step against 20 ms for the
+        # plain step (2 ranks on one GPU, vae_small; 41 ms with a device sync
+        # between phases), so gloo keeps the plain step unless forced.
+        ov = os.environ.get("SKR_DP_OVERLAP", "auto")
+        if ov == "auto":
+            ov = "1" if (self.world > 1 and dp.backend() == "nccl") or self.device.type == "cpu" else "0"
+        self.overlap = self.world > 1 and bool(late) and ov == "1"
         split = self.opt.offset_of[id(late[0])] if self.overlap else None
         self.reducer = dp.GradReducer(self.opt.grad, split=split) if self.world > 1 else None
         self._enc_pending = None
@@ -310,6 +318,27 @@ class VAETrainer:
                 static = {"strokes": strokes.clone(), "lengths": lengths.clone(), "labels": labels.clone()}
                 snap = [self.opt.flat, self.opt.m, self.opt.v, self.opt.scalars]
                 self._graph = GraphedPhases([self._fwd_bwd_a, self._bwd_b, self._opt_step], static, snapshot=snap)
+            if os.environ.get("SKR_TRACE_PHASES"):
+                import sys
+                ts = [time.perf_counter()]
+
+                def mark():
+                    torch.cuda.synchronize()
+                    ts.append(time.perf_counter())
+                out = self._graph.replay(0, strokes=strokes, lengths=lengths, labels=labels)
+                mark()
+                w0 = self.reducer.start(0)
+                mark()
+                self._graph.replay(1)
+                mark()
+                w1 = self.reducer.start(1)
+                mark()
+                self.reducer.wait(w0 + w1)
+                mark()
+                self._graph.replay(2)
+                mark()
+                print("phases ms:", ["%.2f" % (1e3 * (b - a)) for a, b in zip(ts, ts[1:])], file=sys.stderr)
+                return out
             with self.gpu_times.time("fwd_bwd"):
                 out = self._graph.replay(0, strokes=strokes, lengths=lengths, labels=labels)
                 w0 = self.reducer.start(0)
