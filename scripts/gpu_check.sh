@@ -41,6 +41,8 @@ for s in "${steps[@]}"; do
         smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
         bench) run bench 600 python bench.py --steps 10 --warmup 2 ;;
         bench_fp32) run bench_fp32 600 python bench.py --steps 5 --warmup 2 --dtype fp32 ;;
+        bench_classcond) run bench_classcond 600 python bench.py --steps 10 --warmup 2 --config vae_classcond ;;
+        bench_layernorm) run bench_layernorm 600 python bench.py --steps 10 --warmup 2 --config vae_layernorm ;;
         bench_small) run bench_small 600 python bench.py --steps 10 --warmup 2 --config vae_small ;;
         bench_torch) run bench_torch 900 python bench.py --steps 3 --warmup 1 --backend torch --no-eval ;;
         bench_torch_small) run bench_torch_small 600 python bench.py --steps 3 --warmup 1 --backend torch --no-eval --config vae_small ;;
