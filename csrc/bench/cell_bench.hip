@@ -32,6 +32,7 @@ struct Cfg {
     const char* name;
     int B, H, C, NS;
     bool ln, mod;   // mod: bf16 modulation vectors (the HyperLSTM main cell)
+    int dhr = 2, dhr2 = 0, dho = 1;   // backward dh split-K slab counts (dh_rec, dh_rec2, dh_out)
 };
 
 static double run_fwd(const Cfg& c, int steps) {
@@ -85,8 +86,12 @@ static double run_bwd(const Cfg& c, int steps) {
     const int B = c.B, H = c.H, G = 4 * H;
     skr::BwdArgs a{};
     a.B = B; a.H = H; a.grp_rows = 0;
-    a.dh_out = dalloc((size_t)B * H); a.dho_nslab = 1; a.dho_slab = (int64_t)B * H;
-    a.dh_rec = dalloc((size_t)2 * B * H); a.ld_dh_rec = H; a.dhr_nslab = 2; a.dhr_slab = (int64_t)B * H;
+    a.dh_out = dalloc((size_t)c.dho * B * H); a.dho_nslab = c.dho; a.dho_slab = (int64_t)B * H;
+    a.dh_rec = dalloc((size_t)c.dhr * B * H); a.ld_dh_rec = H; a.dhr_nslab = c.dhr; a.dhr_slab = (int64_t)B * H;
+    if (c.dhr2 > 0) {
+        a.dh_rec2 = dalloc((size_t)c.dhr2 * B * H); a.ld_dh_rec2 = H; a.dhr2_nslab = c.dhr2;
+        a.dhr2_slab = (int64_t)B * H;
+    }
     a.dc_rec = dalloc((size_t)B * H);
     a.act = dalloc((size_t)B * G); a.c_new = dalloc((size_t)B * H); a.c_prev = dalloc((size_t)B * H);
     a.xhat = dalloc((size_t)B * G); a.rstd = dalloc((size_t)B * 5, 1.f); a.chat = dalloc((size_t)B * H);
@@ -151,6 +156,9 @@ int main(int argc, char** argv) {
         {"hyper plain H256  C1 NS1       ", 100, 256, 1, 1, false, false},
         {"encoder     H512  C2 NS4 (2B)  ", 200, 512, 2, 4, false, false},
         {"tiny        H64   C1 NS1 B8    ", 8, 64, 1, 1, false, false},
+        // vae_large backward slab counts: main cell dh 8 + 8 slabs, hyper cell dh_out 32 + dh_rec 8
+        {"main hyper  H2048 C8 dh 8+8      ", 100, 2048, 8, 2, true, true, 8, 8, 1},
+        {"hyper cell  H256  C1 dh 8, out 32", 100, 256, 1, 1, true, false, 8, 0, 32},
     };
     for (const Cfg& c : cfgs) printf("fwd %-36s %8.2f us/launch\n", c.name, run_fwd(c, steps));
     for (const Cfg& c : cfgs)

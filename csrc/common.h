@@ -129,6 +129,33 @@ __device__ __forceinline__ float slab_sum(const float* p, int64_t idx, int n, in
 }
 
 
+// Split-K slab loads with a compile-time ceiling D on the runtime count n
+// (1 <= n <= D): all D loads are issued back to back from clamped addresses
+// (slabs past n re-read slab n-1: same line, no extra memory traffic), so a
+// kernel can start several such sums before its first wait; slab_fold sums
+// the first n. A null source contributes zeros without any load.
+template <int D>
+__device__ __forceinline__ void slab_load(const float* p, int64_t idx, int n, int64_t slab, float (&t)[D]) {
+    if (p == nullptr) {
+#pragma unroll
+        for (int s = 0; s < D; ++s) t[s] = 0.f;
+        return;
+    }
+#pragma unroll
+    for (int s = 0; s < D; ++s) t[s] = p[(int64_t)min(s, n - 1) * slab + idx];
+}
+
+template <int D>
+__device__ __forceinline__ float slab_fold(float (&t)[D], int n) {
+#pragma unroll
+    for (int s = 1; s < D; ++s) t[s] = s < n ? t[s] : 0.f;
+#pragma unroll
+    for (int w = 1; w < D; w *= 2)
+#pragma unroll
+        for (int s = 0; s + w < D; s += 2 * w) t[s] += t[s + w];
+    return t[0];
+}
+
 }  // namespace skr
 
 #define SKR_CHECK_LAUNCH() (int)hipGetLastError()

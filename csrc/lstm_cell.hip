@@ -58,6 +58,7 @@ namespace {
 using namespace skr;
 
 constexpr int kMaxCluster = 16;
+constexpr int kRecSlabs = 8;      // ceiling of the unrolled dh_rec / dh_rec2 slab loads
 constexpr unsigned kSpinLimit = 1u << 21;
 constexpr int kSlots = 16;        // 8-byte granules per workgroup slot (128 B)
 
@@ -270,7 +271,10 @@ __global__ __launch_bounds__(NT) void cell_fwd(const FwdArgs a) {
     }
 }
 
-template <int NT, int UPT, int NS, bool LN, int MOD>
+// DHS > 0: the dh split-K sources are loaded up front with compile-time
+// ceilings (slab_load) -- DHS slabs for dh_out, kRecSlabs for dh_rec /
+// dh_rec2; 0: runtime-count loops (any count).
+template <int NT, int UPT, int NS, bool LN, int MOD, int DHS = 0>
 __global__ __launch_bounds__(NT) void cell_bwd(const BwdArgs a) {
     constexpr int NW = NT / 64;
     __shared__ float lds[NW * 8];
@@ -290,6 +294,8 @@ __global__ __launch_bounds__(NT) void cell_bwd(const BwdArgs a) {
     // ---- every load up front
     float dhc[UPT], dho[UPT], dcc[UPT], ac[UPT][4], cp[UPT], cx[UPT], lcg[UPT], lcb[UPT];
     float xh[UPT][4], lg[UPT][4], lb[UPT][4], xv[UPT][4], rv[UPT][4], ax[UPT][4], ah[UPT][4];
+    constexpr int D = DHS > 0 ? DHS : 1, DR = DHS > 0 ? kRecSlabs : 1;
+    float t1[UPT][DR], t2[UPT][DR], t3[UPT][D];   // DHS > 0: raw dh slab loads, folded after all loads
     bool on[UPT];
 #pragma unroll
     for (int k = 0; k < UPT; ++k) {
@@ -297,9 +303,15 @@ __global__ __launch_bounds__(NT) void cell_bwd(const BwdArgs a) {
         on[k] = u < H;
         const int uc = min(u, H - 1);
         const int64_t ro = (int64_t)b * H + uc;
-        dhc[k] = (a.dh_rec ? slab_sum<0>(a.dh_rec, b * a.ld_dh_rec + uc, a.dhr_nslab, a.dhr_slab) : 0.f) +
-                 (a.dh_rec2 ? slab_sum<0>(a.dh_rec2, b * a.ld_dh_rec2 + uc, a.dhr2_nslab, a.dhr2_slab) : 0.f);
-        dho[k] = a.dh_out ? slab_sum<0>(a.dh_out, ro, a.dho_nslab, a.dho_slab) : 0.f;
+        if constexpr (DHS > 0) {
+            slab_load<DR>(a.dh_rec, b * a.ld_dh_rec + uc, a.dhr_nslab, a.dhr_slab, t1[k]);
+            slab_load<DR>(a.dh_rec2, b * a.ld_dh_rec2 + uc, a.dhr2_nslab, a.dhr2_slab, t2[k]);
+            slab_load<D>(a.dh_out, ro, a.dho_nslab, a.dho_slab, t3[k]);
+        } else {
+            dhc[k] = (a.dh_rec ? slab_sum<0>(a.dh_rec, b * a.ld_dh_rec + uc, a.dhr_nslab, a.dhr_slab) : 0.f) +
+                     (a.dh_rec2 ? slab_sum<0>(a.dh_rec2, b * a.ld_dh_rec2 + uc, a.dhr2_nslab, a.dhr2_slab) : 0.f);
+            dho[k] = a.dh_out ? slab_sum<0>(a.dh_out, ro, a.dho_nslab, a.dho_slab) : 0.f;
+        }
         dcc[k] = a.dc_rec[ro];
         cp[k] = a.c_prev[ro];
         if (LN) {
@@ -327,6 +339,13 @@ __global__ __launch_bounds__(NT) void cell_bwd(const BwdArgs a) {
                 ax[k][q] = ldvec<MOD>(a.vec, q * a.vec_gs + vo) + a.vec_bias[q * H + uc];
                 ah[k][q] = ldvec<MOD>(a.vec, (4 + q) * a.vec_gs + vo) + a.vec_bias[(4 + q) * H + uc];
             }
+        }
+    }
+    if constexpr (DHS > 0) {
+#pragma unroll
+        for (int k = 0; k < UPT; ++k) {
+            dhc[k] = slab_fold<DR>(t1[k], a.dhr_nslab) + slab_fold<DR>(t2[k], a.dhr2_nslab);
+            dho[k] = slab_fold<D>(t3[k], a.dho_nslab);
         }
     }
     // ---- LN: gate activations from the saved xhat (same expressions as the forward)
@@ -451,8 +470,34 @@ KernelT<FwdArgs> pick(bool ln, int mod, const FwdArgs*) {
     if (ln) return cell_fwd<NT, UPT, NS, true, 0>;
     return cell_fwd<NT, UPT, NS, false, 0>;
 }
+// dh_out slab ceiling of a backward step for the unrolled loads: 1, 8, 32,
+// or 0 (runtime loops) when a source does not fit the ceilings
+inline int dh_ceiling(const BwdArgs& a) {
+    if ((a.dh_rec && (a.dhr_nslab < 1 || a.dhr_nslab > kRecSlabs)) ||
+        (a.dh_rec2 && (a.dhr2_nslab < 1 || a.dhr2_nslab > kRecSlabs)))
+        return 0;
+    const int n = a.dh_out ? a.dho_nslab : 1;
+    return n == 1 ? 1 : (n >= 2 && n <= 8) ? 8 : (n > 8 && n <= 32) ? 32 : 0;
+}
+
+template <int NT, int UPT, int NS, int MOD>
+KernelT<BwdArgs> pick_dh(int d) {
+    switch (d) {
+        case 1: return cell_bwd<NT, UPT, NS, true, MOD, 1>;
+        case 8: return cell_bwd<NT, UPT, NS, true, MOD, 8>;
+        case 32: return cell_bwd<NT, UPT, NS, true, MOD, 32>;
+        default: return cell_bwd<NT, UPT, NS, true, MOD, 0>;
+    }
+}
+
 template <int NT, int UPT, int NS>
-KernelT<BwdArgs> pick(bool ln, int mod, const BwdArgs*) {
+KernelT<BwdArgs> pick(bool ln, int mod, const BwdArgs* a) {
+    // hot LayerNorm shapes (HyperLSTM main / hyper cells, LN-LSTM layers):
+    // dh slab loads unrolled to compile-time ceilings
+    if constexpr (NT == 256 && UPT == 1 && (NS == 1 || NS == 2)) {
+        if (ln && mod == 2) return pick_dh<NT, UPT, NS, 2>(dh_ceiling(*a));
+        if (ln && mod == 0) return pick_dh<NT, UPT, NS, 0>(dh_ceiling(*a));
+    }
     if (mod == 2) return cell_bwd<NT, UPT, NS, true, 2>;
     if (mod) return cell_bwd<NT, UPT, NS, true, 1>;
     if (ln) return cell_bwd<NT, UPT, NS, true, 0>;
