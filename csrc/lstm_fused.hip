@@ -17,6 +17,8 @@
 // forget bias, stateless dropout on tanh(j) keyed (seed, stream, step,
 // row*H + u), eoc reset of the carried state, bf16 copy of the carried h for
 // the next step. Grid (H/16, ceil(B/32), nd).
+#include <cstdlib>
+
 #include "lstm_args.h"
 
 namespace {
@@ -43,8 +45,8 @@ struct FusedFwdArgs {
 
 // Backward step t: dh_rec = dG_{t+1} @ W_h^T (K = 4H) fused with the cell
 // backward of step t. Operands are read straight from L2 into MFMA fragments
-// (no LDS staging: K is split over the 4 waves and each wave streams only
-// its quarter); the 4 partial tiles are summed in LDS by the epilogue.
+// (no LDS staging: K is split over the NW waves and each wave streams only
+// its slice); the NW partial tiles are summed in LDS by the epilogue.
 struct FusedBwdArgs {
     int B, H, nd;
     const __hip_bfloat16* dG_next; int64_t ld_dgn;  // bf16 dG of step t+1 [nd*B, 4H], null at t = T-1
@@ -167,10 +169,15 @@ __global__ __launch_bounds__(256) void lstm_fused_fwd(const FusedFwdArgs a) {
     }
 }
 
-template <int H>
-__global__ __launch_bounds__(256) void lstm_fused_bwd(const FusedBwdArgs a) {
-    constexpr int K = 4 * H, KW = K / 4;   // K per wave
-    __shared__ float red[4][RB][UB + 1];
+// NW waves split K = 4H (each streams K/NW straight from L2 into MFMA
+// fragments, loop fully unrolled so all of a wave's loads are in flight
+// before its first MFMA); the NW partial tiles meet in LDS; each of the
+// 64*NW threads finishes 512/(64*NW) (row, unit) pairs.
+template <int H, int NW>
+__global__ __launch_bounds__(64 * NW) void lstm_fused_bwd(const FusedBwdArgs a) {
+    constexpr int K = 4 * H, KW = K / NW;   // K per wave
+    constexpr int NTH = 64 * NW, P = RB * UB / NTH;
+    __shared__ float red[NW][RB][UB + 1];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int grp = blockIdx.z, rb = blockIdx.y * RB, u0 = blockIdx.x * UB;
     const int B = a.B;
@@ -178,13 +185,13 @@ __global__ __launch_bounds__(256) void lstm_fused_bwd(const FusedBwdArgs a) {
     const bool keep_on = a.keep < 1.0f;
     const uint32_t key = keep_on ? hash_key(*a.seed, a.stream, a.step) : 0u;
 
-    // ---- epilogue inputs first (2 (row, unit) pairs per thread)
-    float ac[2][4], cx[2], cp[2], dcc[2], dho[2], dhx[2];
-    int br[2], uu[2];
-    bool on[2], rs[2];
+    // ---- epilogue inputs first (P (row, unit) pairs per thread)
+    float ac[P][4], cx[P], cp[P], dcc[P], dho[P], dhx[P];
+    int br[P], uu[P];
+    bool on[P], rs[P];
 #pragma unroll
-    for (int k = 0; k < 2; ++k) {
-        const int p = tid + 256 * k, r = p / UB;
+    for (int k = 0; k < P; ++k) {
+        const int p = tid + NTH * k, r = p / UB;
         uu[k] = p % UB;
         on[k] = rb + r < B;
         br[k] = (int)row0 + min(rb + r, B - 1);
@@ -199,20 +206,25 @@ __global__ __launch_bounds__(256) void lstm_fused_bwd(const FusedBwdArgs a) {
         rs[k] = a.reset != nullptr && a.reset[br[k]] != 0.f;
     }
 
-    // ---- dh_rec tile [32 rows x 16 units], this wave's K quarter
+    // ---- dh_rec tile [32 rows x 16 units], this wave's K slice
     const int fr = lane & 15, fq = lane >> 4;
     f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
     if (a.dG_next != nullptr) {
         const __hip_bfloat16* wp = a.W + grp * a.w_gs + (int64_t)(u0 + fr) * K + w * KW + fq * 8;
         const __hip_bfloat16* ap0 = a.dG_next + (row0 + min(rb + fr, B - 1)) * a.ld_dgn + w * KW + fq * 8;
         const __hip_bfloat16* ap1 = a.dG_next + (row0 + min(rb + 16 + fr, B - 1)) * a.ld_dgn + w * KW + fq * 8;
-#pragma unroll 8
-        for (int ks = 0; ks < KW / 32; ++ks) {
-            const bf16x8 bfr = *(const bf16x8*)(wp + ks * 32);
-            const bf16x8 a0 = *(const bf16x8*)(ap0 + ks * 32);
-            const bf16x8 a1 = *(const bf16x8*)(ap1 + ks * 32);
-            acc[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, bfr, acc[0], 0, 0, 0);
-            acc[1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, bfr, acc[1], 0, 0, 0);
+        constexpr int NK = KW / 32;
+        bf16x8 bfr[NK], a0[NK], a1[NK];
+#pragma unroll
+        for (int ks = 0; ks < NK; ++ks) {
+            bfr[ks] = *(const bf16x8*)(wp + ks * 32);
+            a0[ks] = *(const bf16x8*)(ap0 + ks * 32);
+            a1[ks] = *(const bf16x8*)(ap1 + ks * 32);
+        }
+#pragma unroll
+        for (int ks = 0; ks < NK; ++ks) {
+            acc[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0[ks], bfr[ks], acc[0], 0, 0, 0);
+            acc[1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1[ks], bfr[ks], acc[1], 0, 0, 0);
         }
     }
 #pragma unroll
@@ -223,12 +235,14 @@ __global__ __launch_bounds__(256) void lstm_fused_bwd(const FusedBwdArgs a) {
 
     // ---- cell backward (plain LSTM path of csrc/lstm_cell.hip cell_bwd)
 #pragma unroll
-    for (int k = 0; k < 2; ++k) {
+    for (int k = 0; k < P; ++k) {
         if (!on[k]) continue;
-        const int p = tid + 256 * k, r = p / UB;
+        const int p = tid + NTH * k, r = p / UB;
         const int b = br[k], u = u0 + uu[k];
         const int64_t ro = (int64_t)b * H + u;
-        const float dhc = red[0][r][uu[k]] + red[1][r][uu[k]] + red[2][r][uu[k]] + red[3][r][uu[k]] + dhx[k];
+        float dhc = dhx[k];
+#pragma unroll
+        for (int v = 0; v < NW; ++v) dhc += red[v][r][uu[k]];
         const float dh = dho[k] + (rs[k] ? 0.f : dhc);
         float dc = rs[k] ? 0.f : dcc[k];
         if (rs[k] && a.dinit_h) {
@@ -254,9 +268,21 @@ __global__ __launch_bounds__(256) void lstm_fused_bwd(const FusedBwdArgs a) {
     }
 }
 
+// SKR_FUSED_BWD_WAVES: 4 or 8 waves per workgroup (default 8)
+inline int bwd_waves() {
+    static int nw = -1;
+    if (nw < 0) {
+        const char* e = getenv("SKR_FUSED_BWD_WAVES");
+        nw = (e != nullptr && atoi(e) == 4) ? 4 : 8;
+    }
+    return nw;
+}
+
 template <int H>
 int launch_bwd(const FusedBwdArgs& a, hipStream_t s) {
-    hipLaunchKernelGGL(lstm_fused_bwd<H>, dim3(H / UB, (a.B + RB - 1) / RB, a.nd), dim3(256), 0, s, a);
+    const dim3 grid(H / UB, (a.B + RB - 1) / RB, a.nd);
+    if (bwd_waves() == 4) hipLaunchKernelGGL((lstm_fused_bwd<H, 4>), grid, dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((lstm_fused_bwd<H, 8>), grid, dim3(512), 0, s, a);
     return SKR_CHECK_LAUNCH();
 }
 
