@@ -23,6 +23,8 @@
 // tile of lookahead cannot cover the L2/MALL latency.
 // Rows padded by 16 B in LDS (conflict-free ds_read_b128 fragment reads).
 // gridDim.z batches independent problems (both encoder directions).
+#include <cstdlib>
+
 #include "common.h"
 
 namespace {
@@ -279,6 +281,127 @@ __device__ __forceinline__ void glds_tile(const __hip_bfloat16* __restrict__ A, 
             }
 }
 
+// v3 ("A in registers"): the B (weight) tiles alone go through the LDS-DMA
+// ring, NSB stages deep (8 KiB per stage at BN = 64, so 7 tiles of weights
+// are in flight per workgroup instead of 2), while each wave loads its own
+// 32 rows of the small, L2-resident A operand straight into MFMA fragment
+// registers, NSB tiles deep as well (a register ring indexed by the
+// unrolled slot). Per tile and lane: 4 A loads + B_CH/4 glds, in that
+// order; the counted wait covers both.
+template <int LPT, int AHEAD>
+__device__ __forceinline__ void wait_tiles_ra(int ahead) {
+    if constexpr (AHEAD >= 6) if (ahead >= 6) { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(6 * LPT) : "memory"); return; }
+    if constexpr (AHEAD >= 5) if (ahead == 5) { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(5 * LPT) : "memory"); return; }
+    if constexpr (AHEAD >= 4) if (ahead == 4) { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * LPT) : "memory"); return; }
+    if constexpr (AHEAD >= 3) if (ahead == 3) { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * LPT) : "memory"); return; }
+    if constexpr (AHEAD >= 2) if (ahead == 2) { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * LPT) : "memory"); return; }
+    if (ahead == 1) { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(LPT) : "memory"); return; }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+template <int BN, int NSB, bool CBF16 = false>
+__device__ __forceinline__ void glds_tile_ra(const __hip_bfloat16* __restrict__ A, int64_t lda,
+                                             const __hip_bfloat16* __restrict__ Bt, int64_t ldb,
+                                             void* __restrict__ Cv, int64_t ldc, int M, int n0, int64_t k0,
+                                             int kslice, __hip_bfloat16* smem) {
+    constexpr int NJ = BN / 16;
+    constexpr int B_CH = BN / 8;                    // 1-KiB chunks (8 rows) per B tile
+    constexpr int GPW = B_CH / 4;                   // glds per wave per tile
+    constexpr int LPT = 4 + GPW;                    // vector-memory ops per lane per tile
+    constexpr int TILE = BN * BK;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int n = kslice / BK;
+    const int fr = lane & 15, fq = lane >> 4;
+    const int r8 = lane >> 3, slot8 = lane & 7;
+    const __hip_bfloat16* bsrc[GPW];
+#pragma unroll
+    for (int i = 0; i < GPW; ++i) {
+        const int row = (w + 4 * i) * 8 + r8;
+        const int kc = slot8 ^ ((row >> 1) & 7);
+        bsrc[i] = Bt + (int64_t)(n0 + row) * ldb + k0 + kc * 8;
+    }
+    // A fragment rows of this wave (rows past M re-read row M-1; never stored)
+    const __hip_bfloat16* asrc0 = A + (int64_t)min(32 * w + fr, M - 1) * lda + k0 + fq * 8;
+    const __hip_bfloat16* asrc1 = A + (int64_t)min(32 * w + 16 + fr, M - 1) * lda + k0 + fq * 8;
+    bf16x8 ar[NSB][2][2];   // [slot][row tile][k step]
+
+#define SKR_RA_ISSUE(KT, SL)                                                                                   \
+    do {                                                                                                      \
+        const int64_t ko_ = (int64_t)(KT) * BK;                                                               \
+        ar[SL][0][0] = *(const bf16x8*)(asrc0 + ko_);                                                         \
+        ar[SL][0][1] = *(const bf16x8*)(asrc0 + ko_ + 32);                                                    \
+        ar[SL][1][0] = *(const bf16x8*)(asrc1 + ko_);                                                         \
+        ar[SL][1][1] = *(const bf16x8*)(asrc1 + ko_ + 32);                                                    \
+        __hip_bfloat16* st_ = smem + (SL) * TILE;                                                             \
+        _Pragma("unroll") for (int i_ = 0; i_ < GPW; ++i_)                                                    \
+            __builtin_amdgcn_global_load_lds((const void*)(bsrc[i_] + ko_),                                   \
+                                             (__attribute__((address_space(3))) void*)(st_ + (w + 4 * i_) * 512), \
+                                             16, 0, 0);                                                       \
+    } while (0)
+
+    f32x4 acc[2][NJ];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+#pragma unroll
+    for (int p = 0; p < NSB - 1; ++p)
+        if (p < n) SKR_RA_ISSUE(p, p);
+    for (int kt0 = 0; kt0 < n; kt0 += NSB) {
+#pragma unroll
+        for (int j = 0; j < NSB; ++j) {
+            const int kt = kt0 + j;
+            if (kt < n) {
+                wait_tiles_ra<LPT, NSB - 2>(min(n - 1 - kt, NSB - 2));
+                __builtin_amdgcn_s_barrier();   // every wave's B chunks of tile kt landed; slot (kt-1) free
+                if (kt + NSB - 1 < n) SKR_RA_ISSUE(kt + NSB - 1, (j + NSB - 1) % NSB);
+                const __hip_bfloat16* Bs = smem + j * TILE;
+#pragma unroll
+                for (int ks = 0; ks < 2; ++ks) {
+                    const int kc = ks * 4 + fq;
+                    bf16x8 bfr[NJ];
+#pragma unroll
+                    for (int jj = 0; jj < NJ; ++jj) {
+                        const int row = 16 * jj + fr;
+                        bfr[jj] = *(const bf16x8*)(&Bs[row * BK + ((kc ^ ((row >> 1) & 7)) * 8)]);
+                    }
+#pragma unroll
+                    for (int i = 0; i < 2; ++i)
+#pragma unroll
+                        for (int jj = 0; jj < NJ; ++jj)
+                            acc[i][jj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ar[j][i][ks], bfr[jj], acc[i][jj], 0, 0, 0);
+                }
+            }
+        }
+    }
+#undef SKR_RA_ISSUE
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int row = 32 * w + 16 * i + fq * 4 + e;
+                if (row < M) {
+                    if constexpr (CBF16) ((__hip_bfloat16*)Cv)[row * ldc + n0 + 16 * j + fr] = skr::to_bf16(acc[i][j][e]);
+                    else ((float*)Cv)[row * ldc + n0 + 16 * j + fr] = acc[i][j][e];
+                }
+            }
+}
+
+template <int BN, int NSB, bool CBF16 = false>
+__global__ __launch_bounds__(256) void skinny_gemm_ra_kernel(
+    const __hip_bfloat16* __restrict__ A, int64_t lda, int64_t a_batch,
+    const __hip_bfloat16* __restrict__ Bt, int64_t ldb, int64_t b_batch,
+    void* __restrict__ C, int64_t ldc, int64_t c_slab, int64_t c_batch, int M, int kslice) {
+    extern __shared__ __attribute__((aligned(16))) __hip_bfloat16 smem[];
+    const int64_t co = blockIdx.z * c_batch + blockIdx.y * c_slab;
+    glds_tile_ra<BN, NSB, CBF16>(A + blockIdx.z * a_batch, lda, Bt + blockIdx.z * b_batch, ldb,
+                                 CBF16 ? (void*)((__hip_bfloat16*)C + co) : (void*)((float*)C + co), ldc, M,
+                                 blockIdx.x * BN, (int64_t)blockIdx.y * kslice, kslice, smem);
+}
+
 template <int BN, int NS, bool CBF16 = false>
 __global__ __launch_bounds__(256) void skinny_gemm_glds_kernel(
     const __hip_bfloat16* __restrict__ A, int64_t lda, int64_t a_batch,
@@ -330,6 +453,22 @@ __global__ __launch_bounds__(256) void skinny_gemm_group_kernel(const GemmGroup 
     const int kslice = p.K / p.splits;
     glds_tile<BN, NS>((const __hip_bfloat16*)p.A, p.lda, (const __hip_bfloat16*)p.Bt, p.ldb, p.C + split * p.c_slab, p.ldc,
                   p.M, nt * BN, (int64_t)split * kslice, kslice, smem);
+}
+
+template <int BN, int NSB>
+__global__ __launch_bounds__(256) void skinny_gemm_group_ra_kernel(const GemmGroup g) {
+    extern __shared__ __attribute__((aligned(16))) __hip_bfloat16 smem[];
+    const int id = blockIdx.x;
+    int q = 0;
+#pragma unroll
+    for (int i = 1; i < kMaxGroup; ++i) q += (i < g.n && id >= g.start[i]) ? 1 : 0;
+    const GemmProblem& p = g.p[q];
+    const int local = id - g.start[q];
+    const int ntiles = p.N / BN;
+    const int split = local / ntiles, nt = local - split * ntiles;
+    const int kslice = p.K / p.splits;
+    glds_tile_ra<BN, NSB>((const __hip_bfloat16*)p.A, p.lda, (const __hip_bfloat16*)p.Bt, p.ldb, p.C + split * p.c_slab,
+                          p.ldc, p.M, nt * BN, (int64_t)split * kslice, kslice, smem);
 }
 
 // ---------------------------------------------------------------------------
@@ -467,6 +606,18 @@ SKR_API int skr_skinny_gemm(const void* A, int64_t lda, int64_t a_batch, const v
 // 3, 4 or 6 (6 only with BN = 64: 144 KiB). skr_gemm_set_nstage() tunes it
 // (scripts/bench_gemm.py sweeps it).
 static int g_nstage = 3;   // measured best: 2 workgroups per CU fit (72 KiB at BN = 64)
+// v3 (A operand in registers, B-only LDS ring of kRaStages): SKR_GEMM_AREG=1.
+// Off by default -- measured on MI355X: vae_large 32.5 ms/step against
+// 29.6 with the v2 ring (numerics identical to the tolerance of the tests).
+static const int kRaStages = 8;
+static int g_areg = -1;
+static bool areg_on() {
+    if (g_areg < 0) {
+        const char* e = getenv("SKR_GEMM_AREG");
+        g_areg = (e != nullptr && atoi(e) == 1) ? 1 : 0;
+    }
+    return g_areg == 1;
+}
 
 SKR_API int skr_gemm_set_nstage(int ns) {
     if (ns != 3 && ns != 4 && ns != 6) return -2;
@@ -489,6 +640,14 @@ void set_lds_attr(K k, size_t lds) {
 template <int BN, int NS, bool CBF16 = false>
 int launch_v2(dim3 grid, hipStream_t s, const void* A, int64_t lda, int64_t a_batch, const void* Bt, int64_t ldb,
               int64_t b_batch, void* C, int64_t ldc, int64_t c_slab, int64_t c_batch, int M, int kslice) {
+    if (BN == 64 && areg_on()) {   // (v3 is instantiated for 64-wide tiles only)
+        const size_t lds_ra = (size_t)kRaStages * BN * BK * 2;
+        set_lds_attr(skinny_gemm_ra_kernel<BN, kRaStages, CBF16>, lds_ra);
+        hipLaunchKernelGGL((skinny_gemm_ra_kernel<BN, kRaStages, CBF16>), grid, dim3(256), lds_ra, s,
+                           (const __hip_bfloat16*)A, lda, a_batch, (const __hip_bfloat16*)Bt, ldb, b_batch, C, ldc,
+                           c_slab, c_batch, M, kslice);
+        return SKR_CHECK_LAUNCH();
+    }
     const size_t lds = (size_t)NS * (BM + BN) * BK * 2;
     set_lds_attr(skinny_gemm_glds_kernel<BN, NS, CBF16>, lds);
     hipLaunchKernelGGL((skinny_gemm_glds_kernel<BN, NS, CBF16>), grid, dim3(256), lds, s, (const __hip_bfloat16*)A,
@@ -498,6 +657,12 @@ int launch_v2(dim3 grid, hipStream_t s, const void* A, int64_t lda, int64_t a_ba
 
 template <int BN, int NS>
 int launch_group(const GemmGroup& g, hipStream_t s) {
+    if (BN == 64 && areg_on()) {   // (v3 is instantiated for 64-wide tiles only)
+        const size_t lds_ra = (size_t)kRaStages * BN * BK * 2;
+        set_lds_attr(skinny_gemm_group_ra_kernel<BN, kRaStages>, lds_ra);
+        hipLaunchKernelGGL((skinny_gemm_group_ra_kernel<BN, kRaStages>), dim3(g.start[g.n]), dim3(256), lds_ra, s, g);
+        return SKR_CHECK_LAUNCH();
+    }
     const size_t lds = (size_t)NS * (BM + BN) * BK * 2;
     set_lds_attr(skinny_gemm_group_kernel<BN, NS>, lds);
     hipLaunchKernelGGL((skinny_gemm_group_kernel<BN, NS>), dim3(g.start[g.n]), dim3(256), lds, s, g);
