@@ -25,6 +25,7 @@ import torch
 import torch.nn as nn
 
 from .. import ops
+from ..ops import gemm
 from ..config import RefConfig
 from . import cells as C
 
@@ -90,7 +91,10 @@ class SketchRNN(nn.Module):
         out = inp.reshape(T * B, -1)
         if train and cfg.keep_prob < 1.0:
             out = out * C.dropout_mask(drop_seed, 7, 0, out.shape, cfg.keep_prob, out.device)
-        z = torch.addmm(self.output_b, out, self.output_w)
+        # head through ops.gemm.linear (as the VAE head, vae.py:177): bf16 operands
+        # in bf16 mode and the bias gradient as one column-sum kernel (torch's
+        # dim-0 sum was 0.31 ms/step, profiles/r1_ref_config_kernel_summary.txt)
+        z = gemm.linear(out, self.output_w, self.output_b)
         return z, final
 
     def loss(self, x: torch.Tensor, y: torch.Tensor, state=None, train: bool = True, drop_seed: int = 0):
