@@ -10,9 +10,20 @@ step (encoder + decoder forward, backward, all-reduce, clip + Adam) over all
 250 decoder positions (the pen-state loss covers every position in training
 mode, so all B*Nmax positions are training targets).
 
-Usage: ``python bench.py --gpus N --steps K --warmup W``; for N > 1 launch
-with ``torch.distributed.run`` (one rank per GPU, RCCL). Rank 0 prints one
-JSON line; ``value`` = global_batch * Nmax * K / max-over-ranks(seconds).
+Usage: ``python bench.py --gpus N --steps K --warmup W``. For N > 1 the job
+runs one rank per GPU over RCCL: either the caller launches it under
+``torch.distributed.run`` (WORLD_SIZE set), or this script starts that
+launcher itself as a child process before anything touches the GPU and exits
+with its code. Rank 0 prints one JSON line:
+
+* ``value`` -- valid (non-padding) stroke points processed per second by the
+  whole job: sum of the sketch lengths of the K timed global batches divided
+  by the max-over-ranks wall time (strokes/s = sum of valid
+  steps / wall time);
+* ``positions_per_s`` -- all ``global_batch * Nmax`` decoder positions per
+  second (the Magenta recipe trains the pen-state loss on every padded
+  position too, so these are loss targets; round 1 reported this number as
+  ``value``).
 """
 from __future__ import annotations
 
@@ -23,6 +34,28 @@ import sys
 import time
 
 import numpy as np
+
+
+def _free_port() -> int:
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _launch_ranks(n: int) -> int:
+    """Start ``n`` ranks (one per GPU) under torch.distributed.run as a child
+    process and return its exit code. Runs before this process touches the
+    GPU (device_count() does not initialise it on this image)."""
+    import subprocess
+    import torch
+    ndev = torch.cuda.device_count()
+    if ndev < n:
+        print("bench.py: --gpus %d requested but only %d device(s) visible" % (n, ndev), file=sys.stderr)
+        return 2
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n),
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
 
 
 def main():
@@ -43,6 +76,9 @@ def main():
                     "'gloo' rehearses the multi-rank path with several ranks on one GPU")
     args = ap.parse_args()
 
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return _launch_ranks(args.gpus)
+
     import torch
     from sketch_rnn_amd import ops
     from sketch_rnn_amd.config import PRESETS
@@ -60,6 +96,9 @@ def main():
     if world_env > 1:
         dp.init_from_env(backend=args.dist_backend, device=device)
     world, rank = dp.world_size(), dp.rank()
+    if world != args.gpus and rank == 0:
+        print("bench.py: --gpus %d but WORLD_SIZE=%d; reporting the real rank count" % (args.gpus, world),
+              file=sys.stderr)
     ops.set_backend(args.backend)
 
     cfg = PRESETS[args.config].replace(batch_size=args.batch, max_seq_len=args.seq_len, save_every=0)
@@ -81,6 +120,8 @@ def main():
         return trainer.batch_to_device(train.random_batch(rank, world))
 
     batches = [batch() for _ in range(4)]
+    # valid stroke points per global batch (every rank draws the same count of rows)
+    valid = [float(dp.sum_scalar(float(b[1].sum()))) for b in batches]
     sync = torch.cuda.synchronize if device.startswith("cuda") else (lambda: None)
     for i in range(args.warmup):
         out = trainer.train_step(*batches[i % len(batches)])
@@ -105,8 +146,8 @@ def main():
         ev = trainer.evaluate(test, max_batches=1)
         recon = ev["r_cost"]
     global_batch = args.batch * world
-    strokes_per_step = global_batch * args.seq_len
-    value = strokes_per_step * args.steps / elapsed
+    positions_per_s = global_batch * args.seq_len * args.steps / elapsed
+    value = sum(valid[i % len(valid)] for i in range(args.steps)) / elapsed
     if rank == 0:
         rec = {
             "metric": "train strokes/sec (whole node) + test recon NLL, enc512/dec2048 QuickDraw",
@@ -131,6 +172,8 @@ def main():
                 "backend": ops.get_backend(),
                 "hip_graph": bool(trainer.use_graph),
             },
+            "positions_per_s": round(positions_per_s, 1),
+            "valid_fraction": round(value / positions_per_s, 4),
             "train_cost": round(cost, 4),
             "test_recon_nll": None if recon is None else round(recon, 4),
         }

@@ -517,6 +517,29 @@ KernelT<A> pick_ns(const A& a, bool ln, int mod) {
     }
 }
 
+// Workgroups of kernel k (nt threads) that can be resident on the whole
+// device at once: occupancy API x CU count, at most 4 per CU. Cached per
+// kernel (queried on the first, eager, launch -- before any graph capture).
+inline int64_t coresident_capacity(const void* k, int nt) {
+    static const void* keys[64];
+    static int64_t vals[64];
+    static int n = 0;
+    for (int i = 0; i < n; ++i)
+        if (keys[i] == k) return vals[i];
+    int dev = 0, cus = 0, per = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k, nt, 0) != hipSuccess)
+        return 0;
+    const int64_t cap = (int64_t)cus * (per < 4 ? per : 4);
+    if (n < 64) {
+        keys[n] = k;
+        vals[n] = cap;
+        ++n;
+    }
+    return cap;
+}
+
 // Geometry: C = args->cluster workgroups per row. C == 1 rows wider than 256
 // units run on 1024-thread workgroups (one row per CU, no exchange);
 // otherwise 256 threads with UPT units each.
@@ -545,6 +568,12 @@ int launch(const A& a, bool ln, int mod, hipStream_t s) {
             default: k = pick_ns<256, 8>(a, ln, mod); break;
         }
     }
+    // Rows split over C > 1 workgroups spin-wait on each other: every one of
+    // the B*C workgroups must be resident at once. Checked against the
+    // occupancy API (capped at 4 per CU, below the API's answer near the
+    // SGPR edges where it reads one block high) -- a grid that could strand
+    // a workgroup is refused instead of spinning into the timeout.
+    if (C > 1 && ln && (int64_t)a.B * C > coresident_capacity((const void*)k, nt)) return -8;
     hipLaunchKernelGGL(k, dim3(C, a.B), dim3(nt), 0, s, a);
     return SKR_CHECK_LAUNCH();
 }

@@ -8,7 +8,10 @@
 //
 // Grid (ceil(C/256), RS): thread = one column, block row RS_idx owns a slice
 // of the R1*R2 rows; per-slice partial sums go to part[RS][C] (fp32),
-// summed by the caller (RS <= 64: a tiny deterministic second pass).
+// summed by a deterministic second pass. RS is chosen by the caller
+// (ops/reduce.py): about 1024 / ceil(C/256) slices, capped at R/16 rows per
+// slice -- e.g. the [30000, 123] MDN-head bias gradient runs RS = 1024
+// slices of ~30 rows.
 #include "common.h"
 
 namespace {

@@ -6,7 +6,11 @@
   ``csrc/*.hip``, linked against the HIP runtime by soname with an rpath to
   PyTorch's ``lib/`` so the process uses a single runtime.
 
-Incremental: a target is rebuilt only when a source or header is newer.
+Incremental by CONTENT, not mtime: every object and library carries a
+``.sha256`` stamp of its sources, headers, compiler flags and toolchain; a
+target is rebuilt whenever the stamp does not match the current tree, so a
+library that travelled with a snapshot is never mistaken for a build of
+different sources. ``--force`` rebuilds everything.
 Usage: ``python scripts/build_native.py [--force] [--only host|hip] [-j N]``
 """
 from __future__ import annotations
@@ -26,11 +30,29 @@ BUILD = os.path.join(ROOT, "build", "obj")
 ARCH = os.environ.get("SKR_OFFLOAD_ARCH", "gfx950")
 
 
-def _newer(target, deps):
-    if not os.path.exists(target):
+def _digest(files, cmd):
+    import hashlib
+    h = hashlib.sha256()
+    h.update(" ".join(cmd).encode())
+    for f in sorted(files):
+        h.update(os.path.basename(f).encode())
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()
+
+
+def _stale(target, files, cmd):
+    """True unless ``target`` exists with a stamp matching ``files`` + ``cmd``."""
+    stamp = target + ".sha256"
+    if not os.path.exists(target) or not os.path.exists(stamp):
         return True
-    t = os.path.getmtime(target)
-    return any(os.path.getmtime(d) > t for d in deps)
+    with open(stamp) as f:
+        return f.read().strip() != _digest(files, cmd)
+
+
+def _stamp(target, files, cmd):
+    with open(target + ".sha256", "w") as f:
+        f.write(_digest(files, cmd) + "\n")
 
 
 def _run(cmd):
@@ -51,11 +73,13 @@ def build_host(force=False):
     srcs = sorted(glob.glob(os.path.join(CSRC, "host", "*.cpp")))
     hdrs = sorted(glob.glob(os.path.join(CSRC, "host", "*.h")))
     target = os.path.join(OUT, "libskrnn_host.so")
-    if not force and not _newer(target, srcs + hdrs):
+    cmd = ["g++", "-O3", "-std=c++17", "-fPIC", "-shared", "-Wall", "-o", target] + srcs + ["-lpthread"]
+    if not force and not _stale(target, srcs + hdrs, cmd):
         print("host lib up to date")
         return target
     os.makedirs(OUT, exist_ok=True)
-    _run(["g++", "-O3", "-std=c++17", "-fPIC", "-shared", "-Wall", "-o", target] + srcs + ["-lpthread"])
+    _run(cmd)
+    _stamp(target, srcs + hdrs, cmd)
     return target
 
 
@@ -68,24 +92,40 @@ def build_hip(force=False, jobs=8):
     os.makedirs(OUT, exist_ok=True)
     flags = ["-O3", "-std=c++17", "-fPIC", "--offload-arch=" + ARCH, "-Wall", "-Wno-unused-function",
              "-munsafe-fp-atomics", "-I" + CSRC]
+    tool = [_toolchain_id(hipcc)]
     objs, jobs_list = [], []
     for s in srcs:
         o = os.path.join(BUILD, os.path.basename(s) + ".o")
         objs.append(o)
-        if force or _newer(o, [s] + hdrs):
-            jobs_list.append([hipcc] + flags + ["-c", s, "-o", o])
+        cmd = [hipcc] + flags + ["-c", s, "-o", o]
+        if force or _stale(o, [s] + hdrs, cmd + tool):
+            jobs_list.append((cmd, o, [s] + hdrs))
+
+    def compile_one(job):
+        cmd, o, deps = job
+        _run(cmd)
+        _stamp(o, deps, cmd + tool)
+
     if jobs_list:
         with ThreadPoolExecutor(max_workers=max(1, min(jobs, len(jobs_list)))) as ex:
-            list(ex.map(_run, jobs_list))
-    if force or jobs_list or _newer(target, objs):
-        link = [hipcc, "-shared", "-fPIC", "--offload-arch=" + ARCH, "-o", target] + objs
-        tl = torch_lib_dir()
-        if tl:
-            link += ["-Wl,-rpath," + tl]
+            list(ex.map(compile_one, jobs_list))
+    link = [hipcc, "-shared", "-fPIC", "--offload-arch=" + ARCH, "-o", target] + objs
+    tl = torch_lib_dir()
+    if tl:
+        link += ["-Wl,-rpath," + tl]
+    if force or jobs_list or _stale(target, objs, link):
         _run(link)
+        _stamp(target, objs, link)
     else:
         print("hip lib up to date")
     return target
+
+
+def _toolchain_id(hipcc):
+    try:
+        return subprocess.check_output([hipcc, "--version"], stderr=subprocess.STDOUT, text=True).strip()
+    except Exception:
+        return "unknown"
 
 
 def main():

@@ -27,7 +27,7 @@ run() {  # name, limit, cmd...
 
 for s in "${steps[@]}"; do
     case $s in
-        pytest) run pytest_gpu 900 python -m pytest tests -m gpu -q --maxfail=10 ;;
+        pytest) run pytest_gpu 900 python -u -m pytest tests -m gpu -q --maxfail=10 --timeout 300 --timeout-method thread ;;
         pytest_sel) run pytest_sel 600 python -m pytest tests -m gpu -q --maxfail=10 -k "${PYTEST_K:-fused}" ;;
         bench_stride1) SKR_WGRAD_CU_STRIDE=1 run bench_stride1 600 python bench.py --steps 10 --warmup 2 ;;
         bench_stride2) SKR_WGRAD_CU_STRIDE=2 run bench_stride2 600 python bench.py --steps 10 --warmup 2 ;;

@@ -77,7 +77,10 @@ class SketchRNN(nn.Module):
         for l, p in enumerate(self.layers):
             if cfg.model == "lstm":
                 h0, c0 = state[l]
-                xp = torch.addmm(p.bias, inp.reshape(T * B, -1), p.W_x).view(T, B, -1)
+                if l == 0:   # K = 5: a trivial fp32 product
+                    xp = torch.addmm(p.bias, inp.reshape(T * B, -1), p.W_x).view(T, B, -1)
+                else:        # hoisted layer-l input projection in the compute precision (bf16 MFMA)
+                    xp = gemm.linear(inp.reshape(T * B, -1), p.W_x, p.bias).view(T, B, -1)
                 out, (hT, cT) = ops.lstm_sequence(xp, p.W_h, h0, c0, forget_bias=1.0, reset=reset,
                                                   reset_h=h0, reset_c=c0)
                 final.append((hT, cT))

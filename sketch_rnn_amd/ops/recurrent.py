@@ -123,6 +123,21 @@ def check_cluster_errors(device) -> None:
         raise RuntimeError("clustered LSTM cell kernel: in-launch wait timed out (workgroups not co-resident)")
 
 
+_CAPACITY = {}
+
+
+def _coresident_capacity() -> int:
+    """Workgroups the LN cell kernels may keep resident at once: 4 per CU
+    (the launcher re-checks each kernel against the occupancy API and
+    refuses a grid that could strand a spinning workgroup)."""
+    if not torch.cuda.is_available():
+        return 1024
+    d = torch.cuda.current_device()
+    if d not in _CAPACITY:
+        _CAPACITY[d] = 4 * torch.cuda.get_device_properties(d).multi_processor_count
+    return _CAPACITY[d]
+
+
 def cell_geometry(H: int, BB: int, ln: bool = True) -> int:
     """Workgroups per row (C) for the fused cell kernels."""
     if not CLUSTER_ENABLED:
@@ -132,7 +147,7 @@ def cell_geometry(H: int, BB: int, ln: bool = True) -> int:
     else:
         C = min(-(-H // 256), 16)
     # LayerNorm rows spin-wait on each other: keep every workgroup co-resident
-    while ln and C > 1 and BB * C > 1024:
+    while ln and C > 1 and BB * C > _coresident_capacity():
         C //= 2
     per = -(-H // C)
     if (C == 1 and per > 2048) or (C > 1 and per > 2048):

@@ -38,8 +38,23 @@ class DivergenceError(RuntimeError):
     pass
 
 
+def check_device_faults() -> None:
+    """Raise when a kernel reported a fault through a device flag since the
+    last check: the clustered LayerNorm cell kernels set it when an in-launch
+    wait on a peer workgroup timed out (that step's outputs are invalid).
+    Costs one tiny device read; trainers call it at every log interval."""
+    from ..ops import recurrent
+    for f in list(recurrent._ERR_FLAGS.values()):
+        if int(f.item()) != 0:
+            f.zero_()
+            raise DivergenceError("LayerNorm cell kernel: in-launch exchange with a peer workgroup timed out "
+                                  "(workgroups not co-resident); the step's results are invalid")
+
+
 def _to_device(a, device, dtype=torch.float32):
-    return torch.as_tensor(np.ascontiguousarray(a)).to(device=device, dtype=dtype, non_blocking=True)
+    if not torch.is_tensor(a):
+        a = torch.as_tensor(np.ascontiguousarray(a))
+    return a.to(device=device, dtype=dtype, non_blocking=True)
 
 
 # =====================================================================================
@@ -166,6 +181,7 @@ class ReferenceTrainer:
                 self._metrics({"step": self.b_processed, "epoch": e, "cost": cost, "shape": shape,
                                "pen": pen, "time": dt, "lr": self.opt.lr,
                                "strokes_per_s": cfg.batch_size * cfg.seq_length / max(dt, 1e-9)})
+                check_device_faults()
                 if not (cost < cfg.divergence_bound):  # NaN fails this too (train.py:93-94)
                     raise DivergenceError("training diverged: cost=%r" % cost)
                 if self.b_processed % cfg.save_every == 0 and self.b_processed > 0:
@@ -188,7 +204,8 @@ class VAETrainer:
     def __init__(self, cfg: VAEConfig, train_set, valid_set=None, test_set=None, device: str = "cpu",
                  save_dir: str = "save/vae", use_graph: Optional[bool] = None,
                  log: Callable[[str], None] = print, metrics_path: Optional[str] = None,
-                 compute_dtype: str = "fp32", max_skipped: int = 100):
+                 compute_dtype: str = "fp32", max_skipped: int = 100, dp_wire_dtype: Optional[str] = None,
+                 force_reducer: bool = False):
         self.cfg = cfg
         self.train_set, self.valid_set, self.test_set = train_set, valid_set, test_set
         self.device = torch.device(device)
@@ -217,9 +234,14 @@ class VAETrainer:
         ov = os.environ.get("SKR_DP_OVERLAP", "auto")
         if ov == "auto":
             ov = "1" if (self.world > 1 and dp.backend() == "nccl") or self.device.type == "cpu" else "0"
-        self.overlap = self.world > 1 and bool(late) and ov == "1"
+        # force_reducer: run the collectives even at world size 1 (RCCL path check on one GPU)
+        reduce_on = self.world > 1 or (force_reducer and dp.is_dist())
+        self.overlap = reduce_on and bool(late) and ov == "1"
         split = self.opt.offset_of[id(late[0])] if self.overlap else None
-        self.reducer = dp.GradReducer(self.opt.grad, split=split) if self.world > 1 else None
+        # SKR_DP_WIRE=bf16: gradients cross the xGMI ring in bf16 (half the bytes)
+        wire = dp_wire_dtype or os.environ.get("SKR_DP_WIRE", "fp32")
+        self.reducer = dp.GradReducer(self.opt.grad, split=split, wire_dtype=wire,
+                                      force=force_reducer) if reduce_on else None
         self._enc_pending = None
         self.save_dir = save_dir
         self.log = log
@@ -381,7 +403,10 @@ class VAETrainer:
         if self.rank != 0:
             return None
         extra = {"step": self.step, "seed": int(self.seed.item())}
-        if hasattr(self.train_set, "state_dict"):
+        pf = getattr(self, "_prefetch", None)
+        if pf is not None and pf.consumed_state is not None:
+            extra["data"] = pf.consumed_state     # batches still queued are regenerated on resume
+        elif hasattr(self.train_set, "state_dict"):
             extra["data"] = self.train_set.state_dict()
         return ckpt.save_checkpoint(self.save_dir, self.step, self.model, self.opt, self.cfg, extra=extra)
 
@@ -401,16 +426,36 @@ class VAETrainer:
                 self.train_set.aug_rng.seed((self.cfg.seed * 7919 + 1 + self.rank + self.step) % (2 ** 32))
         return True
 
-    def train(self, num_steps: Optional[int] = None, eval_every: int = 0, log_every: int = 20):
+    def train(self, num_steps: Optional[int] = None, eval_every: int = 0, log_every: int = 20,
+              prefetch: bool = True):
+        """Step loop. ``prefetch``: batches are built ``2`` ahead on a
+        background thread into pinned host memory (:mod:`..data.prefetch`);
+        the same batches in the same order as without it."""
+        from ..data.prefetch import Prefetcher
+        self._prefetch = None
+        if prefetch:
+            self._prefetch = Prefetcher(lambda: self.train_set.random_batch(self.rank, self.world),
+                                        getattr(self.train_set, "state_dict", None))
+        try:
+            return self._train_loop(num_steps, eval_every, log_every)
+        finally:
+            if self._prefetch is not None:
+                self._prefetch.close()
+                self._prefetch = None
+
+    def _train_loop(self, num_steps, eval_every, log_every):
         cfg = self.cfg
         num_steps = cfg.num_steps if num_steps is None else num_steps
+        pf = self._prefetch
         t0 = time.time()
         while self.step < num_steps:
             with phase("data", self.host_times):
-                batch = self.batch_to_device(self.train_set.random_batch(self.rank, self.world))
+                raw = pf.get() if pf is not None else self.train_set.random_batch(self.rank, self.world)
+                batch = self.batch_to_device(raw)
             with phase("step", self.host_times):
                 out = self.train_step(*batch)
             if self.step % log_every == 0 or self.step == num_steps:
+                check_device_faults()
                 vals = {k: float(v) for k, v in out.items()}
                 dt = (time.time() - t0) / log_every
                 t0 = time.time()

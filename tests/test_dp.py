@@ -134,3 +134,54 @@ def test_dp_overlapped_step_matches_plain_step(tmp_path):
     o = [torch.load(tmp_path / ("o%d.pt" % k), weights_only=True) for k in range(2)]
     assert torch.equal(o[0]["1"], o[0]["0"])
     assert torch.equal(o[0]["1"], o[1]["1"])
+
+
+def _wire_worker(rank, world, port, out_dir):
+    """bf16-on-the-wire gradient averaging vs the fp32 reduction of the same
+    per-rank gradients."""
+    dp = _init(rank, world, port)
+    g = torch.Generator().manual_seed(100 + rank)
+    base = torch.randn(10000, generator=g) * (1.0 + rank)
+    res = {}
+    for wire in ("fp32", "bf16"):
+        grad = base.clone()
+        red = dp.GradReducer(grad, bucket_mb=0.01, split=3000, wire_dtype=wire)
+        assert len(red.parts) == 2 and len(red.buckets) > 2
+        w0 = red.start(0)
+        red.wait(w0 + red.start(1))
+        res[wire] = grad
+    torch.save(res, os.path.join(out_dir, "w%d.pt" % rank))
+    dp.barrier()
+    torch.distributed.destroy_process_group()
+
+
+def test_dp_bf16_wire_matches_fp32(tmp_path):
+    _spawn(_wire_worker, tmp_path)
+    w = [torch.load(tmp_path / ("w%d.pt" % k), weights_only=True) for k in range(2)]
+    ref = sum(torch.randn(10000, generator=torch.Generator().manual_seed(100 + r)) * (1.0 + r) for r in range(2)) / 2
+    assert torch.allclose(w[0]["fp32"], ref, atol=1e-6)
+    assert torch.equal(w[0]["bf16"], w[1]["bf16"])                       # every rank holds the same average
+    err = (w[0]["bf16"] - ref).abs() / ref.abs().clamp_min(1e-3)
+    assert float(err.median()) < 4e-3 and float((w[0]["bf16"] - ref).abs().max()) < 0.05
+
+
+def test_bench_multi_rank_cpu(tmp_path):
+    """bench.py's multi-rank path (torch.distributed.run, gloo on CPU): one
+    JSON line from rank 0 with n_gpus = world and the whole-job valid-stroke
+    count."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(root, "bench.py"),
+           "--gpus", "2", "--steps", "2", "--warmup", "1", "--config", "plumbing", "--batch", "4",
+           "--seq-len", "24", "--sketches", "60", "--dtype", "fp32", "--backend", "torch", "--no-eval"]
+    env = dict(os.environ, OMP_NUM_THREADS="1", CUDA_VISIBLE_DEVICES="")
+    p = subprocess.run(cmd, cwd=str(tmp_path), env=env, capture_output=True, text=True, timeout=600)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout
+    rec = json.loads(lines[0])
+    assert rec["n_gpus"] == 2 and rec["config"]["global_batch"] == 8 and rec["config"]["parallelism"] == "dp2"
+    assert 0 < rec["value"] <= rec["positions_per_s"] and 0 < rec["valid_fraction"] <= 1

@@ -521,6 +521,36 @@ def test_reference_model_train_step_hip(model):
     assert all(math.isfinite(c) for c in costs), costs
 
 
+def test_reference_model_bf16_grads_match_fp32():
+    """Reference model in bf16 mode (layer-1 input projection and MDN head
+    through bf16 MFMA GEMMs, head bias gradient by the column-sum kernel)
+    against the same model in fp32: every parameter gradient within bf16
+    tolerance."""
+    from sketch_rnn_amd.config import RefConfig
+    from sketch_rnn_amd.models.reference import SketchRNN
+    cfg = RefConfig(rnn_size=256, num_mixture=24, batch_size=32, seq_length=60, keep_prob=1.0)
+    m = SketchRNN(cfg, seed=3).to(DEV)
+    g = torch.Generator().manual_seed(5)
+    x = torch.randn(32, 60, 5, generator=g) * 0.5
+    y = torch.randn(32, 60, 5, generator=g) * 0.5
+    pen = torch.randint(0, 3, (2, 32, 60), generator=g)
+    for t, p in ((x, pen[0]), (y, pen[1])):
+        t[..., 2:] = torch.nn.functional.one_hot(p, 3).float()
+    x, y = x.to(DEV), y.to(DEV)
+    grads = {}
+    for dt in ("fp32", "bf16"):
+        ops.set_backend("hip")
+        ops.set_compute_dtype(dt)
+        m.zero_grad(set_to_none=True)
+        cost = m.loss(x, y, None, train=False)[0]
+        cost.backward()
+        grads[dt] = {n: p.grad.detach().clone() for n, p in m.named_parameters()}
+    for n, ref in grads["fp32"].items():
+        got = grads["bf16"][n]
+        rel = float((got - ref).norm() / ref.norm().clamp_min(1e-12))
+        assert rel < 3e-2, (n, rel)
+
+
 @pytest.mark.parametrize("M,N,K", [(100, 8192, 2048), (64, 1024, 2304), (100, 24576, 256), (17, 512, 640),
                                    (256, 2048, 512)])
 def test_fp8_skinny_gemm(M, N, K):
@@ -584,7 +614,8 @@ def test_fp8_inference_decode_close_to_bf16(dec_model):
 
 
 @pytest.mark.parametrize("shape,xdt,with_y", [((250, 100, 512), torch.float32, True), ((3, 7, 300), torch.bfloat16, False),
-                                              ((250, 2, 100, 64), torch.float32, True)])
+                                              ((250, 2, 100, 64), torch.float32, True),
+                                              ((30000, 123), torch.float32, False)])   # the MDN head bias shape
 def test_colsum_matches_torch(shape, xdt, with_y):
     from sketch_rnn_amd.ops.reduce import colsum
     torch.manual_seed(2)
@@ -595,10 +626,11 @@ def test_colsum_matches_torch(shape, xdt, with_y):
     else:
         xv, yv = x, y
     sxy, sx = colsum(xv, yv)
-    ref_x = xv.float().sum((0, 1))
+    dims = tuple(range(xv.dim() - 1))
+    ref_x = xv.float().sum(dims)
     assert torch.allclose(sx, ref_x, rtol=1e-4, atol=1e-3)
     if with_y:
-        assert torch.allclose(sxy, (xv.float() * yv).sum((0, 1)), rtol=1e-4, atol=1e-3)
+        assert torch.allclose(sxy, (xv.float() * yv).sum(dims), rtol=1e-4, atol=1e-3)
 
 
 def test_inference_weight_cache_tracks_graph_training():

@@ -81,3 +81,56 @@ def test_phased_step_equals_single_graph_step(graph):
     cp, wp = torch.stack(costs), tr.opt.flat.detach().clone()
     assert torch.allclose(cp, cs, rtol=1e-6, atol=1e-6), (cp, cs)
     assert torch.allclose(wp, ws, rtol=1e-5, atol=1e-6), (wp - ws).abs().max()
+
+
+def _rccl_child(rank, out_path, port):
+    """World-size-1 RCCL process group: the trainer's reducer is forced on, so
+    every step really issues the bucketed all-reduces (fp32 and bf16 on the
+    wire) through RCCL, in the phased (overlapped) and the plain DP step."""
+    import os
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    res = {}
+    try:
+        for wire in ("fp32", "bf16"):
+            for ov in ("1", "0"):
+                os.environ["SKR_DP_OVERLAP"] = ov
+                from sketch_rnn_amd.cli.vae_train import make_datasets
+                from sketch_rnn_amd.train.trainer import VAETrainer
+                cfg = _CFGS["hyper"]
+                (train, valid, test), _ = make_datasets(cfg, None, 64)
+                tr = VAETrainer(cfg, train, valid, test, device="cuda", save_dir="/tmp/skr_gpu_test", use_graph=True,
+                                log=lambda s: None, compute_dtype="bf16", dp_wire_dtype=wire, force_reducer=True)
+                assert tr.reducer is not None and tr.reducer.active and tr.overlap == (ov == "1")
+                costs = []
+                for _ in range(3):
+                    out = tr.train_step(*tr.batch_to_device(train.random_batch()))
+                    costs.append(out["cost"].detach().clone())
+                torch.cuda.synchronize()
+                res[wire + ov] = (torch.stack(costs).cpu(), tr.opt.flat.detach().cpu())
+    finally:
+        dist.destroy_process_group()
+    torch.save(res, out_path)
+
+
+def test_rccl_world1_reducer_matches_single_graph(tmp_path):
+    import socket
+    import torch.multiprocessing as mp
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    out = str(tmp_path / "rccl.pt")
+    mp.start_processes(_rccl_child, args=(out, port), nprocs=1, join=True, start_method="spawn")
+    res = torch.load(out, weights_only=True)
+    cs, ws = _run(_CFGS["hyper"], graph=True, steps=3)
+    cs, ws = cs.cpu(), ws.cpu()
+    for key in ("fp321", "fp320"):
+        c, w = res[key]
+        assert torch.allclose(c, cs, rtol=1e-6, atol=1e-6), (key, c, cs)
+        assert torch.allclose(w, ws, rtol=1e-5, atol=1e-6), (key, (w - ws).abs().max())
+    for key in ("bf161", "bf160"):   # gradients rounded to bf16 on the wire
+        c, w = res[key]
+        assert torch.allclose(c, cs, rtol=2e-3, atol=2e-3), (key, c, cs)
+        assert (w - ws).abs().max() < 1e-3, (key, (w - ws).abs().max())
