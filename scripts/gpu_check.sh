@@ -28,7 +28,8 @@ run() {  # name, limit, cmd...
 for s in "${steps[@]}"; do
     case $s in
         pytest) run pytest_gpu 900 python -u -m pytest tests -m gpu -q --maxfail=10 --timeout 300 --timeout-method thread ;;
-        pytest_sel) run pytest_sel 600 python -m pytest tests -m gpu -q --maxfail=10 -k "${PYTEST_K:-fused}" ;;
+        pytest_sel) run pytest_sel 600 python -u -m pytest tests -m gpu -v -x --timeout 240 --timeout-method thread -k "${PYTEST_K:-fused}" ;;
+        pytest_file) run pytest_file 600 python -u -m pytest "${PYTEST_FILE:-tests/test_persist_gpu.py}" -m gpu -v -x --timeout 240 --timeout-method thread ;;
         bench_stride1) SKR_WGRAD_CU_STRIDE=1 run bench_stride1 600 python bench.py --steps 10 --warmup 2 ;;
         bench_stride2) SKR_WGRAD_CU_STRIDE=2 run bench_stride2 600 python bench.py --steps 10 --warmup 2 ;;
         bench_stride8) SKR_WGRAD_CU_STRIDE=8 run bench_stride8 600 python bench.py --steps 10 --warmup 2 ;;

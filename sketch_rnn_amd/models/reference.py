@@ -25,7 +25,7 @@ import torch
 import torch.nn as nn
 
 from .. import ops
-from ..ops import gemm
+from ..ops import gemm, persist
 from ..config import RefConfig
 from . import cells as C
 
@@ -74,6 +74,18 @@ class SketchRNN(nn.Module):
         reset = (xt[:, :, 3] > 0).to(torch.float32) if reset_on_eoc else None
         inp = xt
         final = []
+        L = len(self.layers)
+        if cfg.model == "lstm" and L <= 2 and ops.use_hip(x) and persist.persist_ok(cfg.rnn_size, 1, L):
+            # the whole stack as ONE persistent launch (csrc/lstm_persist.hip):
+            # layer 1's input projection runs inside the recurrence, so the
+            # two layers advance as a wavefront
+            p0 = self.layers[0]
+            xp0 = torch.addmm(p0.bias, xt.reshape(T * B, -1), p0.W_x).view(T, B, -1)
+            out, final = persist.lstm_stack(
+                xp0, [p.W_h for p in self.layers], [s[0] for s in state], [s[1] for s in state],
+                W_in1=self.layers[1].W_x if L == 2 else None, b1=self.layers[1].bias if L == 2 else None,
+                reset=reset)
+            return self._head(out.reshape(T * B, -1), train, drop_seed), final
         for l, p in enumerate(self.layers):
             if cfg.model == "lstm":
                 h0, c0 = state[l]
@@ -91,14 +103,16 @@ class SketchRNN(nn.Module):
                 out, hT = ops.rnn_sequence(p, inp, state[l], reset=reset, reset_h=state[l])
                 final.append(hT)
             inp = out
-        out = inp.reshape(T * B, -1)
+        return self._head(inp.reshape(T * B, -1), train, drop_seed), final
+
+    def _head(self, out: torch.Tensor, train: bool, drop_seed) -> torch.Tensor:
+        cfg = self.cfg
         if train and cfg.keep_prob < 1.0:
             out = out * C.dropout_mask(drop_seed, 7, 0, out.shape, cfg.keep_prob, out.device)
         # head through ops.gemm.linear (as the VAE head, vae.py:177): bf16 operands
         # in bf16 mode and the bias gradient as one column-sum kernel (torch's
         # dim-0 sum was 0.31 ms/step, profiles/r1_ref_config_kernel_summary.txt)
-        z = gemm.linear(out, self.output_w, self.output_b)
-        return z, final
+        return gemm.linear(out, self.output_w, self.output_b)
 
     def loss(self, x: torch.Tensor, y: torch.Tensor, state=None, train: bool = True, drop_seed: int = 0):
         """Reference cost: ``(cost, cost_shape, cost_pen, final_state)``."""

@@ -145,6 +145,58 @@ class FusedBwdArgs(C.Structure):
     ]
 
 
+class PFwdLayer(C.Structure):
+    """Mirror of ``PFwdLayer`` in csrc/lstm_persist.hip."""
+    _fields_ = [
+        ("WT", _p), ("w_gs", _i64),
+        ("kin", _i),
+        ("xp", _p), ("xp_ts", _i64), ("xp_ld", _i64),
+        ("c0", _p),
+        ("init_h", _p), ("init_c", _p),
+        ("hlp", _p), ("hup", _p), ("h_out", _p), ("c_out", _p), ("c_carry", _p), ("act", _p),
+        ("hT", _p), ("cT", _p),
+        ("keep", _f), ("stream", _u32),
+    ]
+
+
+class PFwdArgs(C.Structure):
+    _fields_ = [
+        ("T", _i), ("B", _i), ("nd", _i), ("L", _i), ("H", _i), ("nrb", _i),
+        ("ly", PFwdLayer * 2),
+        ("reset", _p),
+        ("forget_bias", _f),
+        ("seed", _p),
+        ("flags", _p),
+        ("err", _p),
+    ]
+
+
+class PBwdLayer(C.Structure):
+    """Mirror of ``PBwdLayer`` in csrc/lstm_persist.hip."""
+    _fields_ = [
+        ("Wr", _p), ("wr_gs", _i64),
+        ("Wu", _p),
+        ("dh_out", _p),
+        ("dhT", _p), ("dcT", _p),
+        ("act", _p), ("c_out", _p), ("c_carry", _p), ("c0", _p),
+        ("dg_lp", _p), ("dg", _p),
+        ("dh0", _p), ("dc0", _p),
+        ("dinit_h", _p), ("dinit_c", _p),
+        ("keep", _f), ("stream", _u32),
+    ]
+
+
+class PBwdArgs(C.Structure):
+    _fields_ = [
+        ("T", _i), ("B", _i), ("nd", _i), ("L", _i), ("H", _i), ("nrb", _i),
+        ("ly", PBwdLayer * 2),
+        ("reset", _p),
+        ("seed", _p),
+        ("flags", _p),
+        ("err", _p),
+    ]
+
+
 class GemmProblem(C.Structure):
     """Mirror of ``GemmProblem`` in csrc/skinny_gemm.hip."""
     _fields_ = [
@@ -200,6 +252,10 @@ class HipLib:
         lib.skr_lstm_fused_fwd.restype = _i
         lib.skr_lstm_fused_bwd.argtypes = [C.POINTER(FusedBwdArgs), _p]
         lib.skr_lstm_fused_bwd.restype = _i
+        lib.skr_lstm_persist_fwd.argtypes = [C.POINTER(PFwdArgs), _p]
+        lib.skr_lstm_persist_fwd.restype = _i
+        lib.skr_lstm_persist_bwd.argtypes = [C.POINTER(PBwdArgs), _p]
+        lib.skr_lstm_persist_bwd.restype = _i
         lib.skr_stream_create_cumask.argtypes = [_i, _i, _i, C.POINTER(_p)]
         lib.skr_stream_create_cumask.restype = _i
         lib.skr_stream_destroy.argtypes = [_p]
@@ -208,6 +264,8 @@ class HipLib:
                           ("skr_gru_fwd_args_size", GruFwdArgs), ("skr_gru_bwd_args_size", GruBwdArgs),
                           ("skr_lstm_fused_fwd_args_size", FusedFwdArgs),
                           ("skr_lstm_fused_bwd_args_size", FusedBwdArgs),
+                          ("skr_lstm_persist_fwd_args_size", PFwdArgs),
+                          ("skr_lstm_persist_bwd_args_size", PBwdArgs),
                           ("skr_gemm_problem_size", GemmProblem)):
             fn = getattr(lib, name)
             fn.restype = _i

@@ -1,0 +1,218 @@
+"""Persistent LSTM sequences on the GPU (``csrc/lstm_persist.hip``).
+
+One kernel launch runs a whole sequence -- forward, and one more the whole
+reverse-time backward -- for
+
+* a stack of up to two plain-LSTM layers (the reference decoder-only model,
+  ``model.py:14-30``: the layer-1 input projection ``h0_t @ W_x1`` is
+  computed inside the recurrence, so the two layers run as a wavefront:
+  layer 1 step t overlaps layer 0 step t+1), or
+* two independent recurrences of one layer (the VAE's bidirectional
+  encoder),
+
+with bf16 MFMA operands and fp32 cell state, the reference's eoc state reset
+and the stateless recurrent-dropout hash. Weight gradients are formed after
+the scan as single long-K products over every saved step (``gemm.wgrad``).
+
+Dispatch: :func:`persist_ok` is the eligibility test (bf16 compute dtype,
+H in {256, 512}, no LayerNorm); ``SKR_PERSIST=0`` disables the path (the
+per-step fused kernels of :mod:`.recurrent` run instead).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import List, Optional, Sequence, Tuple
+
+import torch
+
+from ..utils import native
+from . import gemm
+from ._hipapi import PBwdArgs, PFwdArgs
+from .reduce import colsum
+
+PERSIST_ENABLED = os.environ.get("SKR_PERSIST", "1") != "0"
+_ROWS = 32          # rows per workgroup row block (kMTW = 2 sixteen-row tiles)
+
+
+def persist_ok(H: int, nd: int = 1, L: int = 1, ln: bool = False) -> bool:
+    if not PERSIST_ENABLED or ln or gemm.lp_dtype() != torch.bfloat16:
+        return False
+    if L == 2:
+        return nd == 1 and H == 256
+    return L == 1 and nd in (1, 2) and H in (256, 512)
+
+
+def _ptr(t: Optional[torch.Tensor]):
+    return None if t is None else t.data_ptr()
+
+
+def _check(rc: int, what: str) -> None:
+    if rc != 0:
+        raise RuntimeError("%s: launch failed (code %d)" % (what, rc))
+
+
+class _Saved:
+    pass
+
+
+class _PersistLSTM(torch.autograd.Function):
+    """Inputs: ``xp0 [T, nd*B, 4H]`` (layer-0 input projection + bias),
+    ``W_in1 [H, 4H]`` / ``b1 [4H]`` (layer 1's input weights, L = 2),
+    ``W_h0 [nd, H, 4H]`` (or ``[H, 4H]``), ``W_h1``, initial states
+    ``[nd*B, H]`` per layer (also the eoc-reset targets), ``reset [T, nd*B]``.
+    Outputs: the top layer's ``h [T, nd*B, H]`` and every layer's final
+    carried ``(h, c)``."""
+
+    @staticmethod
+    def forward(ctx, xp0, W_in1, b1, W_h0, W_h1, h0a, c0a, h0b, c0b, reset, seed, meta):
+        L, nd, keep, stream, fb = meta
+        from .recurrent import _seed_tensor, cluster_error_flag
+        lib = native.require_hip()
+        T, NB, G = xp0.shape
+        H, B = G // 4, NB // nd
+        dev, bf, f32 = xp0.device, torch.bfloat16, torch.float32
+        nrb = -(-B // _ROWS)
+        xp0 = xp0.contiguous()
+        Wh = [W_h0] + ([W_h1] if L == 2 else [])
+        h0s = [h0a.contiguous()] + ([h0b.contiguous()] if L == 2 else [])
+        c0s = [c0a.contiguous()] + ([c0b.contiguous()] if L == 2 else [])
+        Wl = [gemm.lp(W).reshape(-1, H, G).contiguous() for W in Wh]          # [nd, H, 4H] (backward B^T)
+        WT = [Wl[0].transpose(1, 2).contiguous()]                              # [nd, 4H, H]
+        Wu = None
+        if L == 2:
+            Wu = gemm.lp(W_in1).contiguous()                                    # [H, 4H]
+            WT.append(torch.cat([Wu, Wl[1][0]], 0).t().contiguous())           # [4H, 2H]: [W_in | W_h] per column
+        rst = reset.contiguous().to(f32) if reset is not None else None
+        sd = _seed_tensor(seed, dev)
+        b1c = b1.contiguous().to(f32) if L == 2 else None
+        a = PFwdArgs()
+        a.T, a.B, a.nd, a.L, a.H, a.nrb = T, B, nd, L, H, nrb
+        a.reset, a.forget_bias, a.seed = _ptr(rst), float(fb), sd.data_ptr()
+        flags = torch.empty(L * nd * nrb * 64, dtype=torch.int32, device=dev)
+        a.flags, a.err = flags.data_ptr(), cluster_error_flag(dev).data_ptr()
+        s = _Saved()
+        s.hlp, s.hup, s.c_out, s.c_carry, s.act = [], [], [], [], []
+        outs = []
+        for l in range(L):
+            ly = a.ly[l]
+            hlp = torch.empty(T + 1, NB, H, dtype=bf, device=dev)
+            hlp[0].copy_(h0s[l])
+            hup = torch.empty(T, NB, H, dtype=bf, device=dev) if (l < L - 1 and rst is not None) else None
+            h_out = torch.empty(T, NB, H, dtype=f32, device=dev) if l == L - 1 else None
+            c_out = torch.empty(T, NB, H, dtype=f32, device=dev)
+            c_carry = torch.empty(T + 1, NB, H, dtype=f32, device=dev) if rst is not None else None
+            act = torch.empty(T, NB, G, dtype=f32, device=dev)
+            hT = torch.empty(NB, H, dtype=f32, device=dev)
+            cT = torch.empty(NB, H, dtype=f32, device=dev)
+            ly.WT, ly.w_gs, ly.kin = WT[l].data_ptr(), (G * H if (l == 0 and nd > 1) else 0), (0 if l == 0 else H)
+            if l == 0:
+                ly.xp, ly.xp_ts, ly.xp_ld = xp0.data_ptr(), NB * G, G
+            else:
+                ly.xp, ly.xp_ts, ly.xp_ld = b1c.data_ptr(), 0, 0
+            ly.c0 = c0s[l].data_ptr()
+            ly.init_h, ly.init_c = (h0s[l].data_ptr(), c0s[l].data_ptr()) if rst is not None else (None, None)
+            ly.hlp, ly.hup, ly.h_out, ly.c_out = hlp.data_ptr(), _ptr(hup), _ptr(h_out), c_out.data_ptr()
+            ly.c_carry, ly.act, ly.hT, ly.cT = _ptr(c_carry), act.data_ptr(), hT.data_ptr(), cT.data_ptr()
+            ly.keep, ly.stream = float(keep), int(stream) + l
+            s.hlp.append(hlp)
+            s.hup.append(hup)
+            s.c_out.append(c_out)
+            s.c_carry.append(c_carry)
+            s.act.append(act)
+            if l == L - 1:
+                top = h_out
+            outs += [hT, cT]
+        _check(lib.lib.skr_lstm_persist_fwd(ctypes.byref(a), torch.cuda.current_stream().cuda_stream),
+               "lstm_persist_fwd")
+        s.Wl, s.Wu, s.c0s, s.rst, s.seed, s.meta = Wl, Wu, c0s, rst, sd, meta
+        s.shapes = [W.shape for W in Wh]
+        s.keep_flags = flags
+        ctx.s = s
+        ctx.dims = (T, B, H, nrb)
+        return (top, *outs)
+
+    @staticmethod
+    def backward(ctx, dtop, *dfinal):
+        s = ctx.s
+        T, B, H, nrb = ctx.dims
+        L, nd, keep, stream, fb = s.meta
+        from .recurrent import cluster_error_flag
+        lib = native.require_hip()
+        NB, G = nd * B, 4 * H
+        dev, bf, f32 = s.hlp[0].device, torch.bfloat16, torch.float32
+        b = PBwdArgs()
+        b.T, b.B, b.nd, b.L, b.H, b.nrb = T, B, nd, L, H, nrb
+        b.reset, b.seed = _ptr(s.rst), s.seed.data_ptr()
+        flags = torch.empty(L * nd * nrb * 64, dtype=torch.int32, device=dev)
+        b.flags, b.err = flags.data_ptr(), cluster_error_flag(dev).data_ptr()
+        dtop = dtop.contiguous() if dtop is not None else None
+        dg_lp, dg, dh0, dc0, dih, dic, keep_alive = [], [], [], [], [], [], []
+        for l in range(L):
+            ly = b.ly[l]
+            ly.Wr, ly.wr_gs = s.Wl[l].data_ptr(), (H * G if nd > 1 else 0)
+            ly.Wu = s.Wu.data_ptr() if (L == 2 and l == 0) else None
+            ly.dh_out = _ptr(dtop) if l == L - 1 else None
+            dhT, dcT = dfinal[2 * l], dfinal[2 * l + 1]
+            dhT = dhT.contiguous() if dhT is not None else None
+            dcT = dcT.contiguous() if dcT is not None else None
+            keep_alive += [dhT, dcT]
+            ly.dhT, ly.dcT = _ptr(dhT), _ptr(dcT)
+            ly.act, ly.c_out, ly.c_carry, ly.c0 = (s.act[l].data_ptr(), s.c_out[l].data_ptr(), _ptr(s.c_carry[l]),
+                                                   s.c0s[l].data_ptr())
+            gl = torch.empty(T, NB, G, dtype=bf, device=dev)
+            gf = torch.empty(T, NB, G, dtype=f32, device=dev)
+            h0g = torch.empty(NB, H, dtype=f32, device=dev)
+            c0g = torch.empty(NB, H, dtype=f32, device=dev)
+            ihg = torch.empty(NB, H, dtype=f32, device=dev) if s.rst is not None else None
+            icg = torch.empty(NB, H, dtype=f32, device=dev) if s.rst is not None else None
+            ly.dg_lp, ly.dg, ly.dh0, ly.dc0 = gl.data_ptr(), gf.data_ptr(), h0g.data_ptr(), c0g.data_ptr()
+            ly.dinit_h, ly.dinit_c = _ptr(ihg), _ptr(icg)
+            ly.keep, ly.stream = float(keep), int(stream) + l
+            dg_lp.append(gl)
+            dg.append(gf)
+            dh0.append(h0g)
+            dc0.append(c0g)
+            dih.append(ihg)
+            dic.append(icg)
+        _check(lib.lib.skr_lstm_persist_bwd(ctypes.byref(b), torch.cuda.current_stream().cuda_stream),
+               "lstm_persist_bwd")
+        # weight gradients: one long-K product per matrix over all T*B rows
+        dWh = []
+        for l in range(L):
+            A = s.hlp[l][:T]
+            if nd == 1:
+                dW = gemm.wgrad(A.reshape(T * NB, H), dg_lp[l].view(T * NB, G))
+            else:
+                An = A.view(T, nd, B, H).permute(1, 0, 2, 3).reshape(nd, T * B, H)
+                Gn = dg_lp[l].view(T, nd, B, G).permute(1, 0, 2, 3).reshape(nd, T * B, G)
+                dW = gemm.wgrad(An, Gn)
+            dWh.append(dW.reshape(s.shapes[l]))
+        dWin1 = db1 = None
+        if L == 2:
+            src = s.hup[0] if s.hup[0] is not None else s.hlp[0][1:]
+            dWin1 = gemm.wgrad(src.reshape(T * NB, H), dg_lp[1].view(T * NB, G))
+            db1 = colsum(dg[1].view(T * NB, G))[1]
+        # the eoc-reset targets are the initial states themselves
+        dh0t = [dh0[l] + dih[l] if dih[l] is not None else dh0[l] for l in range(L)]
+        dc0t = [dc0[l] + dic[l] if dic[l] is not None else dc0[l] for l in range(L)]
+        ctx.s = None
+        return (dg[0], dWin1, db1, dWh[0], dWh[1] if L == 2 else None,
+                dh0t[0], dc0t[0], dh0t[1] if L == 2 else None, dc0t[1] if L == 2 else None,
+                None, None, None)
+
+
+def lstm_stack(xp0: torch.Tensor, W_h: Sequence[torch.Tensor], h0: Sequence[torch.Tensor],
+               c0: Sequence[torch.Tensor], W_in1: Optional[torch.Tensor] = None, b1: Optional[torch.Tensor] = None,
+               reset: Optional[torch.Tensor] = None, nd: int = 1, drop_keep: float = 1.0, drop_seed=0,
+               drop_stream: int = 0, forget_bias: float = 1.0) -> Tuple[torch.Tensor, List[Tuple]]:
+    """Run ``len(W_h)`` (1 or 2) stacked LSTM layers over ``xp0`` in one
+    persistent launch. Returns the top layer's outputs ``[T, nd*B, H]`` and
+    the final carried ``(h, c)`` of every layer."""
+    L = len(W_h)
+    meta = (L, nd, float(drop_keep), int(drop_stream), float(forget_bias))
+    if L == 2:
+        outs = _PersistLSTM.apply(xp0, W_in1, b1, W_h[0], W_h[1], h0[0], c0[0], h0[1], c0[1], reset, drop_seed, meta)
+        return outs[0], [(outs[1], outs[2]), (outs[3], outs[4])]
+    outs = _PersistLSTM.apply(xp0, None, None, W_h[0], None, h0[0], c0[0], None, None, reset, drop_seed, meta)
+    return outs[0], [(outs[1], outs[2])]

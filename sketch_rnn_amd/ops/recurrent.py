@@ -420,6 +420,12 @@ def bilstm_sequence_packed_hip(xp, W_f, W_b, h0, c0, drop_keep=1.0, drop_seed=0,
     W = torch.stack([W_f, W_b], 0)
     h = torch.cat([h0, h0], 0)
     c = torch.cat([c0, c0], 0)
+    from . import persist
+    if persist.persist_ok(W_f.shape[0], 2, 1, ln=ln_f is not None):
+        # both directions, every step, one persistent launch (csrc/lstm_persist.hip)
+        Hout, _ = persist.lstm_stack(xp, [W], [h], [c], nd=2, drop_keep=drop_keep, drop_seed=drop_seed,
+                                     drop_stream=streams[0], forget_bias=forget_bias)
+        return Hout[:, :B], Hout[:, B:]
     if ln_f is not None:
         ln = tuple(torch.stack([a, b], 0) for a, b in zip(ln_f, ln_b))
     else:

@@ -1,0 +1,117 @@
+"""Persistent LSTM sequence kernels (csrc/lstm_persist.hip) against the fp32
+PyTorch oracle: forward outputs, final states and every gradient (inputs,
+weights, initial state), bf16 tolerances.
+
+* the reference decoder-only 2-layer stack (one launch for both layers, eoc
+  state reset to the batch-initial state, model.py:66-95);
+* the bidirectional encoder (two directions in one launch, recurrent
+  dropout from the shared stateless hash).
+"""
+import pytest
+import torch
+
+from sketch_rnn_amd import ops
+from sketch_rnn_amd.ops import persist
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+@pytest.fixture(autouse=True)
+def _restore():
+    yield
+    ops.set_backend("auto")
+    ops.set_compute_dtype("fp32")
+    persist.PERSIST_ENABLED = True
+    from sketch_rnn_amd.ops.recurrent import check_cluster_errors
+    torch.cuda.synchronize()
+    check_cluster_errors(DEV)
+
+
+def _rel(a, b):
+    return float((a.float() - b.float()).norm() / b.float().norm().clamp_min(1e-12))
+
+
+def _ref_run(m, x, state, backend, dtype):
+    ops.set_backend(backend)
+    ops.set_compute_dtype(dtype)
+    m.zero_grad(set_to_none=True)
+    st = [(h.detach().clone().requires_grad_(), c.detach().clone().requires_grad_()) for h, c in state]
+    z, final = m.forward(x, st, train=False)
+    g = torch.Generator(device=DEV).manual_seed(11)
+    rz = torch.randn(z.shape, device=DEV, generator=g)
+    rf = [torch.randn(s.shape, device=DEV, generator=g) for f in final for s in f]
+    loss = (z * rz).sum() + sum((s * r).sum() for s, r in zip([s for f in final for s in f], rf))
+    loss.backward()
+    grads = {n: p.grad.detach().clone() for n, p in m.named_parameters()}
+    for l, (h, c) in enumerate(st):
+        grads["h0_%d" % l], grads["c0_%d" % l] = h.grad.clone(), c.grad.clone()
+    return z.detach(), [s.detach() for f in final for s in f], grads
+
+
+@pytest.mark.parametrize("B,T,with_reset", [(100, 40, True), (37, 17, False), (64, 5, True)])
+def test_persistent_reference_stack_matches_oracle(B, T, with_reset):
+    from sketch_rnn_amd.config import RefConfig
+    from sketch_rnn_amd.models.reference import SketchRNN
+    cfg = RefConfig(rnn_size=256, num_layers=2, num_mixture=4, keep_prob=1.0)
+    m = SketchRNN(cfg, seed=1).to(DEV)
+    g = torch.Generator().manual_seed(B + T)
+    x = torch.randn(B, T, 5, generator=g) * 0.6
+    pen = torch.randint(0, 3, (B, T), generator=g)
+    x[..., 2:] = torch.nn.functional.one_hot(pen, 3).float()
+    if not with_reset:
+        x[..., 3] = 0.0
+        x[..., 2] = torch.maximum(x[..., 2], 1.0 - x[..., 4])
+    x = x.to(DEV)
+    state = [(0.3 * torch.randn(B, 256, generator=g), 0.5 * torch.randn(B, 256, generator=g)) for _ in range(2)]
+    state = [(h.to(DEV), c.to(DEV)) for h, c in state]
+    z_ref, f_ref, g_ref = _ref_run(m, x, state, "torch", "fp32")
+    z, f, gr = _ref_run(m, x, state, "hip", "bf16")
+    assert _rel(z, z_ref) < 2e-2, _rel(z, z_ref)
+    for a, b in zip(f, f_ref):
+        assert _rel(a, b) < 2e-2, _rel(a, b)
+    for n, ref in g_ref.items():
+        assert _rel(gr[n], ref) < 4e-2, (n, _rel(gr[n], ref))
+
+
+def test_persistent_bilstm_matches_oracle():
+    torch.manual_seed(3)
+    T, B, H = 30, 100, 512
+    xp = (torch.randn(T, 2 * B, 4 * H, device=DEV) * 0.5).requires_grad_()
+    W_f = (torch.randn(H, 4 * H, device=DEV) / H ** 0.5).requires_grad_()
+    W_b = (torch.randn(H, 4 * H, device=DEV) / H ** 0.5).requires_grad_()
+    h0 = (0.2 * torch.randn(B, H, device=DEV)).requires_grad_()
+    c0 = (0.2 * torch.randn(B, H, device=DEV)).requires_grad_()
+    R = [torch.randn(T, B, H, device=DEV) for _ in range(2)]
+    res = {}
+    for backend, dt in (("torch", "fp32"), ("hip", "bf16")):
+        ops.set_backend(backend)
+        ops.set_compute_dtype(dt)
+        for t in (xp, W_f, W_b, h0, c0):
+            t.grad = None
+        of, ob = ops.bilstm_sequence_packed(xp, W_f, W_b, h0, c0, drop_keep=0.9, drop_seed=5, drop_stream=2)
+        ((of * R[0]).sum() + (ob * R[1]).sum()).backward()
+        res[backend] = [of.detach(), ob.detach()] + [t.grad.clone() for t in (xp, W_f, W_b, h0, c0)]
+    names = ["out_f", "out_b", "xp", "W_f", "W_b", "h0", "c0"]
+    for n, a, b in zip(names, res["hip"], res["torch"]):
+        assert _rel(a, b) < 4e-2, (n, _rel(a, b))
+
+
+def test_persistent_matches_per_step_kernels():
+    """Same model, persistent launch vs the per-step fused kernels (both
+    bf16): outputs agree to bf16 rounding of the operands."""
+    from sketch_rnn_amd.config import RefConfig
+    from sketch_rnn_amd.models.reference import SketchRNN
+    cfg = RefConfig(rnn_size=256, num_layers=2, num_mixture=4, keep_prob=1.0)
+    m = SketchRNN(cfg, seed=2).to(DEV)
+    g = torch.Generator().manual_seed(0)
+    x = torch.randn(100, 60, 5, generator=g)
+    x[..., 2:] = torch.nn.functional.one_hot(torch.randint(0, 3, (100, 60), generator=g), 3).float()
+    x = x.to(DEV)
+    state = [(torch.zeros(100, 256, device=DEV), torch.zeros(100, 256, device=DEV)) for _ in range(2)]
+    z1, f1, g1 = _ref_run(m, x, state, "hip", "bf16")
+    persist.PERSIST_ENABLED = False
+    z2, f2, g2 = _ref_run(m, x, state, "hip", "bf16")
+    assert _rel(z1, z2) < 1e-2
+    for n in g1:
+        assert _rel(g1[n], g2[n]) < 3e-2, (n, _rel(g1[n], g2[n]))

@@ -133,4 +133,7 @@ def test_rccl_world1_reducer_matches_single_graph(tmp_path):
     for key in ("bf161", "bf160"):   # gradients rounded to bf16 on the wire
         c, w = res[key]
         assert torch.allclose(c, cs, rtol=2e-3, atol=2e-3), (key, c, cs)
-        assert (w - ws).abs().max() < 1e-3, (key, (w - ws).abs().max())
+        # Adam normalises each update to ~lr: bf16 rounding of a near-zero
+        # gradient can move that element by up to ~lr per step (3 steps, lr 1e-3)
+        assert (w - ws).abs().max() < 3e-3, (key, (w - ws).abs().max())
+        assert (w - ws).abs().mean() < 1e-4, (key, (w - ws).abs().mean())
