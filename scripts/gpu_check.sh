@@ -59,6 +59,7 @@ for s in "${steps[@]}"; do
         dp_rehearsal) run dp_rehearsal 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 --steps 3 --warmup 2 --dist-backend gloo --config vae_small ;;
         dp_rehearsal_noov) SKR_DP_OVERLAP=0 run dp_rehearsal_noov 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29518 bench.py --gpus 2 --steps 3 --warmup 2 --dist-backend gloo --config vae_small ;;
         dp_rehearsal_nograph) run dp_rehearsal_nograph 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29519 bench.py --gpus 2 --steps 3 --warmup 2 --dist-backend gloo --config vae_small --no-graph ;;
+        prof_ref) run prof_ref 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_ref -o run --output-format csv -- python scripts/bench_reference.py --dtype bf16 --steps 5 --warmup 2 ;;
         prof_sample) run prof_sample 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_sample -o run --output-format csv -- python scripts/bench_sample.py --reps 1 --host-steps 2 ;;
         *) echo "unknown step $s"; exit 2 ;;
     esac

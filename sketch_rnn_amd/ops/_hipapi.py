@@ -256,6 +256,8 @@ class HipLib:
         lib.skr_lstm_persist_fwd.restype = _i
         lib.skr_lstm_persist_bwd.argtypes = [C.POINTER(PBwdArgs), _p]
         lib.skr_lstm_persist_bwd.restype = _i
+        lib.skr_hyper_vec_fwd.argtypes = [_p, _i64, _p, _p, _p, _i64, _i64, _i, _i, _i, _p]
+        lib.skr_hyper_vec_fwd.restype = _i
         lib.skr_stream_create_cumask.argtypes = [_i, _i, _i, C.POINTER(_p)]
         lib.skr_stream_create_cumask.restype = _i
         lib.skr_stream_destroy.argtypes = [_p]

@@ -440,6 +440,12 @@ def bilstm_sequence_packed_hip(xp, W_f, W_b, h0, c0, drop_keep=1.0, drop_seed=0,
 # HyperLSTM sequence
 # =====================================================================================
 _SIDE_STREAMS = {}
+# Unfolded modulation vectors (csrc/hyper_vec.hip, SKR_UNFOLD_VEC=1): reads
+# 1.7 MB of weights per step instead of the folded P (12.6 MB) but measured
+# 7.2 us/step against 6.6 us for the folded skinny GEMM on MI355X (vae_large,
+# rocprofv3 kernel trace): the step is bound by the 4.9 MB bf16 vec write and
+# launch latency, not by the weight stream. Off by default.
+UNFOLD_VEC = os.environ.get("SKR_UNFOLD_VEC", "0") == "1"
 # Concurrent branch on a second stream (SKR_TWO_STREAM=1). Off by default:
 # measured on MI355X, a cross-stream join inside a HIP graph costs 5-11 us
 # per step (rocprofv3 kernel trace), more than the overlap it buys.
@@ -644,6 +650,16 @@ class _HyperSeq(torch.autograd.Function):
         # reused by every step (cache-resident) instead of T saved slab sets;
         # at inference nothing is saved either
         vbf = not fp8 and dt == torch.bfloat16 and B <= 128 and S_v == 1
+        # unfolded modulation vectors (csrc/hyper_vec.hip): per step W_z + W_a
+        # (1.7 MB) instead of the folded P (12H x Hh); E = 32 embeddings
+        unfold = vbf and UNFOLD_VEC and E == 32 and Hh in (64, 128, 256, 512) and H % 64 == 0
+        if unfold:
+            if infer:
+                WzT = gemm.derived(W_z, "hvWzT", lambda W: W.to(dt).t().contiguous())
+                WaT = gemm.derived(W_a, "hvWaT", lambda W: W.to(dt).transpose(1, 2).contiguous())
+            else:
+                WzT = W_z.to(dt).t().contiguous()                     # [12E, Hh]
+                WaT = W_a.to(dt).transpose(1, 2).contiguous()         # [12, H, E]
         RLP = torch.empty(T, B, G, device=dev, dtype=torch.bfloat16) if (vbf and not infer) else None
         RM = torch.empty(T if (RLP is None and not infer) else 1, max(S_m, 1), B, G, device=dev, dtype=f32)
         rmi = (lambda t: t) if RM.shape[0] == T else (lambda t: 0)
@@ -705,7 +721,10 @@ class _HyperSeq(torch.autograd.Function):
                 ah.xhat, ah.rstd, ah.chat = HXHAT[t].data_ptr(), HRSTD[t].data_ptr(), HCHAT[t].data_ptr()
             ah.h_lp, ah.c_carry = A[t + 1, :, H:].data_ptr(), HCC[t + 1].data_ptr()
             _check(lib.lib.skr_lstm_fwd_step(ctypes.byref(ah), 1, 0, st), "hyper_fwd_step")
-            if vbf:
+            if unfold:
+                _check(lib.lib.skr_hyper_vec_fwd(A[t + 1, :, H:].data_ptr(), K, WzT.data_ptr(), WaT.data_ptr(),
+                                                 VEC[t].data_ptr(), H, 12 * H, B, H, Hh, st), "hyper_vec_fwd")
+            elif vbf:
                 gemm.rec_gemm_bf16out(A[t + 1, :, H:], PlT, VEC[t])
             else:
                 rgemm(A[t + 1, :, H:], PlT, VEC[t].unsqueeze(0), S_v)

@@ -24,6 +24,8 @@ def _restore():
     yield
     ops.set_backend("auto")
     ops.set_compute_dtype("fp32")
+    from sketch_rnn_amd.ops import recurrent
+    recurrent.UNFOLD_VEC = False
     from sketch_rnn_amd.ops.recurrent import check_cluster_errors
     torch.cuda.synchronize()
     check_cluster_errors(DEV)
@@ -217,11 +219,15 @@ def test_hyper_sequence_matches_oracle(H, Hh, E, keep):
     _close(g_h, g_t, 2e-3, 2e-4, "grad")
 
 
-def test_hyper_sequence_bf16_close():
-    """bf16 HyperLSTM (grouped GEMMs, bf16 modulation vectors) against the
-    fp32 oracle at bf16 tolerances."""
+@pytest.mark.parametrize("H,Hh,E,unfold", [(512, 64, 8, True), (2048, 256, 32, True), (2048, 256, 32, False)])
+def test_hyper_sequence_bf16_close(H, Hh, E, unfold):
+    """bf16 HyperLSTM (grouped GEMMs, bf16 modulation vectors; E = 32: the
+    unfolded modulation-vector kernel csrc/hyper_vec.hip, or the folded
+    P GEMM) against the fp32 oracle at bf16 tolerances."""
+    from sketch_rnn_amd.ops import recurrent
+    recurrent.UNFOLD_VEC = unfold
     torch.manual_seed(12)
-    T, B, IN, H, Hh, E = 6, 100, 5, 512, 64, 8
+    T, B, IN = 6, 100, 5
     p = C.HyperLSTMParams(IN + 16, H, Hh, E).to(DEV)
     with torch.no_grad():
         for prm in p.parameters():
@@ -239,6 +245,7 @@ def test_hyper_sequence_bf16_close():
         out, _ = ops.hyper_sequence(p, x, *st, drop_keep=0.9, drop_seed=4, drop_stream=9, zc=z)
         (out * w).sum().backward()
         res.append([out.detach(), z.grad] + [q.grad.clone() for q in p.parameters()])
+    recurrent.UNFOLD_VEC = False
     _close(res[0][:1], res[1][:1], 3e-2, 3e-2, "out")
     _close(res[0][1:], res[1][1:], 6e-2, 6e-2, "grad")
 
