@@ -586,6 +586,11 @@ inline size_t bwd_lds(int H, int L) {
     return (size_t)(L > 1 ? 2 : 1) * 16 * 4 * H * 2 + (size_t)(8 / kMTW) * kMTW * 2 * 64 * 16 + (size_t)kMTW * 1024 * 2;
 }
 
+__global__ void zero_flags(uint32_t* f, int n) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i < n) f[i] = 0u;
+}
+
 // all workgroups of a launch must be co-resident (they wait on each other)
 inline bool fits(const void* k, size_t lds, int grid) {
     int dev = 0, cus = 0, per = 0;
@@ -610,8 +615,14 @@ int launch_persist(KF kern, const A& a, size_t lds, hipStream_t s) {
             if (p == nullptr) { p = (const void*)kern; break; }
     }
     if (!fits((const void*)kern, lds, grid)) return -8;
-    const size_t fbytes = (size_t)a.L * a.nd * a.nrb * kFlagStride * 4;
-    if (hipMemsetAsync(a.flags, 0, fbytes, s) != hipSuccess) return -10;
+    // Zero the flag words with a kernel, not hipMemsetAsync: on MI355X with
+    // torch's HIP 7.0 runtime a memset node captured into a HIP graph is not
+    // ordered before the next kernel node on replay -- replays 2.. of a
+    // captured persistent launch saw the previous replay's epochs and read
+    // hand-off buffers before they were written (tests/test_persist_gpu.py::
+    // test_persistent_graph_replay_matches_eager, with poisoned buffers).
+    const int nflags = a.L * a.nd * a.nrb * kFlagStride;
+    hipLaunchKernelGGL(zero_flags, dim3((nflags + 255) / 256), dim3(256), 0, s, a.flags, nflags);
     hipLaunchKernelGGL(kern, dim3(grid), dim3(NTHR), lds, s, a);
     return SKR_CHECK_LAUNCH();
 }

@@ -32,6 +32,9 @@ from ._hipapi import PBwdArgs, PFwdArgs
 from .reduce import colsum
 
 PERSIST_ENABLED = os.environ.get("SKR_PERSIST", "1") != "0"
+# debug: fill every handed-off buffer with NaN before the launch, so a read
+# that overtakes its hand-off shows up as a NaN instead of a stale value
+POISON = os.environ.get("SKR_PERSIST_POISON", "0") == "1"
 _ROWS = 32          # rows per workgroup row block (kMTW = 2 sixteen-row tiles)
 
 
@@ -89,7 +92,7 @@ class _PersistLSTM(torch.autograd.Function):
         a = PFwdArgs()
         a.T, a.B, a.nd, a.L, a.H, a.nrb = T, B, nd, L, H, nrb
         a.reset, a.forget_bias, a.seed = _ptr(rst), float(fb), sd.data_ptr()
-        flags = torch.empty(L * nd * nrb * 64, dtype=torch.int32, device=dev)
+        flags = torch.empty(L * nd * nrb * 64, dtype=torch.int32, device=dev)   # zeroed by the launcher
         a.flags, a.err = flags.data_ptr(), cluster_error_flag(dev).data_ptr()
         s = _Saved()
         s.hlp, s.hup, s.c_out, s.c_carry, s.act = [], [], [], [], []
@@ -97,6 +100,8 @@ class _PersistLSTM(torch.autograd.Function):
         for l in range(L):
             ly = a.ly[l]
             hlp = torch.empty(T + 1, NB, H, dtype=bf, device=dev)
+            if POISON:
+                hlp.fill_(float("nan"))
             hlp[0].copy_(h0s[l])
             hup = torch.empty(T, NB, H, dtype=bf, device=dev) if (l < L - 1 and rst is not None) else None
             h_out = torch.empty(T, NB, H, dtype=f32, device=dev) if l == L - 1 else None
@@ -144,7 +149,7 @@ class _PersistLSTM(torch.autograd.Function):
         b = PBwdArgs()
         b.T, b.B, b.nd, b.L, b.H, b.nrb = T, B, nd, L, H, nrb
         b.reset, b.seed = _ptr(s.rst), s.seed.data_ptr()
-        flags = torch.empty(L * nd * nrb * 64, dtype=torch.int32, device=dev)
+        flags = torch.empty(L * nd * nrb * 64, dtype=torch.int32, device=dev)   # zeroed by the launcher
         b.flags, b.err = flags.data_ptr(), cluster_error_flag(dev).data_ptr()
         dtop = dtop.contiguous() if dtop is not None else None
         dg_lp, dg, dh0, dc0, dih, dic, keep_alive = [], [], [], [], [], [], []
@@ -161,6 +166,8 @@ class _PersistLSTM(torch.autograd.Function):
             ly.act, ly.c_out, ly.c_carry, ly.c0 = (s.act[l].data_ptr(), s.c_out[l].data_ptr(), _ptr(s.c_carry[l]),
                                                    s.c0s[l].data_ptr())
             gl = torch.empty(T, NB, G, dtype=bf, device=dev)
+            if POISON:
+                gl.fill_(float("nan"))
             gf = torch.empty(T, NB, G, dtype=f32, device=dev)
             h0g = torch.empty(NB, H, dtype=f32, device=dev)
             c0g = torch.empty(NB, H, dtype=f32, device=dev)

@@ -115,3 +115,45 @@ def test_persistent_matches_per_step_kernels():
     assert _rel(z1, z2) < 1e-2
     for n in g1:
         assert _rel(g1[n], g2[n]) < 3e-2, (n, _rel(g1[n], g2[n]))
+
+
+def test_persistent_graph_replay_matches_eager():
+    """The persistent launch captured in a HIP graph and replayed with new
+    inputs equals the eager launch bitwise. The hand-off buffers are filled
+    with NaN before every launch (persist.POISON), so a consumer that reads a
+    step before its producer published it -- e.g. because the per-launch flag
+    reset was not ordered before the kernel on replay -- shows up as NaN."""
+    from sketch_rnn_amd.train.graph import capture
+    ops.set_backend("hip")
+    ops.set_compute_dtype("bf16")
+    persist.POISON = True
+    try:
+        torch.manual_seed(3)
+        T, B, H = 60, 16, 256
+        xp = torch.randn(T, 2 * B, 4 * H, device=DEV) * 0.5
+        W_f, W_b = (torch.randn(H, 4 * H, device=DEV) / H ** 0.5 for _ in range(2))
+        h0, c0 = (0.2 * torch.randn(B, H, device=DEV) for _ in range(2))
+
+        def fwd():
+            return ops.bilstm_sequence_packed(xp, W_f, W_b, h0, c0, drop_keep=0.9, drop_seed=5, drop_stream=2)
+
+        with torch.no_grad():
+            side = torch.cuda.Stream()
+            side.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(side):
+                fwd()
+            torch.cuda.current_stream().wait_stream(side)
+            torch.cuda.synchronize()
+            g = torch.cuda.CUDAGraph()
+            with capture(g):
+                outs = fwd()
+            for it in range(6):
+                xp.copy_(torch.randn_like(xp) * 0.5)
+                g.replay()
+                got = [o.clone() for o in outs]
+                ref = fwd()
+                torch.cuda.synchronize()
+                for a, b in zip(got, ref):
+                    assert torch.equal(a, b), (it, float((a - b).abs().max()))
+    finally:
+        persist.POISON = False
