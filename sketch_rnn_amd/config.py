@@ -155,4 +155,5 @@ PRESETS: Dict[str, VAEConfig] = {
     "vae_large": VAEConfig(enc_rnn_size=512, dec_rnn_size=2048, dec_model="hyper"),
     "vae_classcond": VAEConfig(enc_rnn_size=512, dec_rnn_size=2048, dec_model="hyper", num_classes=345),
     "vae_layernorm": VAEConfig(enc_rnn_size=256, dec_rnn_size=512, dec_model="layer_norm"),
+    "vae_layernorm_large": VAEConfig(enc_rnn_size=512, dec_rnn_size=2048, dec_model="layer_norm"),
 }

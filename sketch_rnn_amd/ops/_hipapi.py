@@ -197,6 +197,24 @@ class PBwdArgs(C.Structure):
     ]
 
 
+class WFwdArgs(C.Structure):
+    """Mirror of ``WFwdArgs`` in csrc/lstm_wide.hip (wide persistent LN-LSTM)."""
+    _fields_ = [
+        ("T", _i), ("B", _i), ("H", _i),
+        ("WT", _p),
+        ("xp", _p), ("xp_ts", _i64), ("xp_ld", _i64),
+        ("c0", _p),
+        ("ln_g", _p), ("ln_b", _p), ("lnc_g", _p), ("lnc_b", _p),
+        ("forget_bias", _f), ("keep", _f),
+        ("seed", _p), ("stream", _u32),
+        ("hlp", _p), ("ldh", _i64),
+        ("gbuf", _p), ("h_out", _p), ("cc", _p),
+        ("xhat", _p), ("rstd", _p), ("chat", _p),
+        ("flags", _p), ("err", _p),
+        ("trace", _p),
+    ]
+
+
 class GemmProblem(C.Structure):
     """Mirror of ``GemmProblem`` in csrc/skinny_gemm.hip."""
     _fields_ = [
@@ -256,6 +274,10 @@ class HipLib:
         lib.skr_lstm_persist_fwd.restype = _i
         lib.skr_lstm_persist_bwd.argtypes = [C.POINTER(PBwdArgs), _p]
         lib.skr_lstm_persist_bwd.restype = _i
+        lib.skr_lstm_wide_fwd.argtypes = [C.POINTER(WFwdArgs), _p]
+        lib.skr_lstm_wide_fwd.restype = _i
+        lib.skr_lstm_wide_flag_words.argtypes = [_i, _i]
+        lib.skr_lstm_wide_flag_words.restype = _i
         lib.skr_hyper_vec_fwd.argtypes = [_p, _i64, _p, _p, _p, _i64, _i64, _i, _i, _i, _p]
         lib.skr_hyper_vec_fwd.restype = _i
         lib.skr_stream_create_cumask.argtypes = [_i, _i, _i, C.POINTER(_p)]
@@ -268,6 +290,7 @@ class HipLib:
                           ("skr_lstm_fused_bwd_args_size", FusedBwdArgs),
                           ("skr_lstm_persist_fwd_args_size", PFwdArgs),
                           ("skr_lstm_persist_bwd_args_size", PBwdArgs),
+                          ("skr_lstm_wide_fwd_args_size", WFwdArgs),
                           ("skr_gemm_problem_size", GemmProblem)):
             fn = getattr(lib, name)
             fn.restype = _i

@@ -185,6 +185,73 @@ def _fused_ok(H: int, ln: bool, fp8: bool, ldt) -> bool:
     return FUSED_ENABLED and not ln and not fp8 and ldt == torch.bfloat16 and H in (256, 512)
 
 
+# ---- wide persistent LayerNorm-LSTM forward (csrc/lstm_wide.hip) ---------------------
+# A LayerNorm layer with H in {1024, 2048}, bf16 operands, one
+# direction, no eoc resets and at most min(128, H/8) rows can run its whole
+# forward recurrence as ONE launch: W_h stays in LDS across all CUs, two
+# in-launch hand-offs per step (gate tiles to row owners, h rows back). The
+# backward consumes the same saves as the per-step kernels. OPT-IN
+# (SKR_WIDE=1): measured slower than the per-step chain on MI355X (27 vs ~20
+# us per step at H = 2048, B = 100; csrc/lstm_wide.hip, STATUS).
+WIDE_ENABLED = os.environ.get("SKR_WIDE", "0") == "1"
+WIDE_TRACE = os.environ.get("SKR_WIDE_TRACE", "0") == "1"
+WIDE_TRACES = []
+
+
+def _wide_ok(H, BB, nd, ln, fp8, ldt, reset, xp) -> bool:
+    return (WIDE_ENABLED and xp.is_cuda and nd == 1 and ln and not fp8 and ldt == torch.bfloat16
+            and reset is None and xp.shape[0] > 0 and H % 1024 == 0 and 1024 <= H <= 2048
+            and 1 <= BB <= min(128, H // 8))
+
+
+def _wide_forward(ctx, xp, W_h, Wl, WlT, h0, c0, ln_g, ln_b, lnc_g, lnc_b, seed, meta):
+    from ._hipapi import WFwdArgs
+    forget_bias, keep, stream, nd, infer = meta
+    lib = native.require_hip()
+    T, B, G = xp.shape
+    H = G // 4
+    dev, f32, bf = xp.device, torch.float32, torch.bfloat16
+    A = torch.empty(T + 1, B, H, device=dev, dtype=bf)
+    A[0].copy_(h0)
+    CC = torch.empty(T + 1, B, H, device=dev, dtype=f32)
+    CC[0].copy_(c0)
+    Hout = torch.empty(T, B, H, device=dev, dtype=f32)
+    gbuf = torch.empty(T, B, 2, G, device=dev, dtype=f32)   # per-K-half partial gate rows
+    flags = torch.empty(lib.lib.skr_lstm_wide_flag_words(H, B), device=dev, dtype=torch.int32)
+    XHAT = None if infer else torch.empty(T, B, G, device=dev, dtype=f32)
+    RSTD = None if infer else torch.empty(T, B, 5, device=dev, dtype=f32)
+    CHAT = None if infer else torch.empty(T, B, H, device=dev, dtype=f32)
+    lnp = [t.contiguous() for t in (ln_g, ln_b, lnc_g, lnc_b)]
+    sd = _seed_tensor(seed, dev)
+    c0c = c0.contiguous()
+    a = WFwdArgs()
+    a.T, a.B, a.H = T, B, H
+    a.WT = WlT.data_ptr()
+    a.xp, a.xp_ts, a.xp_ld = xp.data_ptr(), B * G, G
+    a.c0 = c0c.data_ptr()
+    a.ln_g, a.ln_b, a.lnc_g, a.lnc_b = (t.data_ptr() for t in lnp)
+    a.forget_bias, a.keep = float(forget_bias), float(keep)
+    a.seed, a.stream = sd.data_ptr(), int(stream)
+    a.hlp, a.ldh = A.data_ptr(), H
+    a.gbuf, a.h_out, a.cc = gbuf.data_ptr(), Hout.data_ptr(), CC.data_ptr()
+    a.xhat, a.rstd, a.chat = _ptr(XHAT), _ptr(RSTD), _ptr(CHAT)
+    a.flags, a.err = flags.data_ptr(), cluster_error_flag(dev).data_ptr()
+    trace = None
+    if WIDE_TRACE:   # diagnostic: per-step s_memtime stamps of every wave (scripts/wide_trace.py)
+        trace = torch.zeros(T, H // 8, 16, 4, device=dev, dtype=torch.int64)
+        a.trace = trace.data_ptr()
+        WIDE_TRACES.append(trace)
+    _check(lib.lib.skr_lstm_wide_fwd(ctypes.byref(a), _stream()), "lstm_wide_fwd")
+    s = _Saved()
+    s.Wl, s.A, s.CC, s.Cout, s.ACT, s.XHAT, s.RSTD, s.CHAT = Wl, A, CC, None, None, XHAT, RSTD, CHAT
+    s.reset, s.seed, s.meta, s.lnp = None, sd, meta, lnp
+    s.wshape = W_h.shape
+    s.keep_alive = (gbuf, flags, c0c)
+    ctx.s = s
+    ctx.dims = (T, B, H)
+    return Hout, Hout[T - 1].clone(), CC[T].clone()
+
+
 # =====================================================================================
 # LSTM / LayerNorm-LSTM sequence (nd groups)
 # =====================================================================================
@@ -208,6 +275,8 @@ class _LSTMSeq(torch.autograd.Function):
         else:
             Wl = gemm.lp(W_h.reshape(nd, H, G)).contiguous()   # B^T of the backward product dG @ W^T
             WlT = Wl.transpose(1, 2).contiguous()              # B^T of the forward product h @ W
+        if _wide_ok(H, BB, nd, ln, fp8, ldt, reset, xp):
+            return _wide_forward(ctx, xp, W_h, Wl, WlT, h0, c0, ln_g, ln_b, lnc_g, lnc_b, seed, meta)
         if fp8:
             WQ = gemm.derived(W_h, "lstm_fp8", lambda W: gemm.quantize_fp8_rows(W.reshape(H, G).t()))
             S = gemm.plan_splits_fp8(Bg, G, H)
