@@ -66,6 +66,12 @@ class SketchRNN(nn.Module):
                 drop_seed: int = 0, reset_on_eoc: bool = True):
         """``x [B, T, 5]`` (reference layout). Returns ``(z [T*B, NOUT], final_state)``
         with rows in time-major order."""
+        out, final = self.features(x, state, reset_on_eoc)
+        return self._head(out, train, drop_seed), final
+
+    def features(self, x: torch.Tensor, state: Optional[List] = None, reset_on_eoc: bool = True):
+        """Top-layer outputs ``[T*B, H]`` (time-major rows, before the output
+        dropout) and the final state."""
         cfg = self.cfg
         B, T, _ = x.shape
         if state is None:
@@ -85,7 +91,7 @@ class SketchRNN(nn.Module):
                 xp0, [p.W_h for p in self.layers], [s[0] for s in state], [s[1] for s in state],
                 W_in1=self.layers[1].W_x if L == 2 else None, b1=self.layers[1].bias if L == 2 else None,
                 reset=reset)
-            return self._head(out.reshape(T * B, -1), train, drop_seed), final
+            return out.reshape(T * B, -1), final
         for l, p in enumerate(self.layers):
             if cfg.model == "lstm":
                 h0, c0 = state[l]
@@ -103,7 +109,7 @@ class SketchRNN(nn.Module):
                 out, hT = ops.rnn_sequence(p, inp, state[l], reset=reset, reset_h=state[l])
                 final.append(hT)
             inp = out
-        return self._head(inp.reshape(T * B, -1), train, drop_seed), final
+        return inp.reshape(T * B, -1), final
 
     def _head(self, out: torch.Tensor, train: bool, drop_seed) -> torch.Tensor:
         cfg = self.cfg
@@ -116,11 +122,15 @@ class SketchRNN(nn.Module):
 
     def loss(self, x: torch.Tensor, y: torch.Tensor, state=None, train: bool = True, drop_seed: int = 0):
         """Reference cost: ``(cost, cost_shape, cost_pen, final_state)``."""
-        z, final = self.forward(x, state, train=train, drop_seed=drop_seed)
+        out, final = self.features(x, state)
         tgt = y.transpose(0, 1).reshape(-1, 5)
-        cost, shape, pen = ops.mdn_loss(z, tgt, self.cfg.num_mixture, mode="reference",
-                                        stroke_importance=self.cfg.stroke_importance_factor,
-                                        clamp=self.cfg.loss_clamp)
+        # output dropout (model.py:29-30) + head (model.py:98-99) + loss (model.py:124-178):
+        # one fused kernel on the GPU (ops.mdn_head_loss)
+        keep = self.cfg.keep_prob if (train and self.cfg.keep_prob < 1.0) else 1.0
+        cost, shape, pen = ops.mdn_head_loss(out, self.output_w, self.output_b, tgt, self.cfg.num_mixture,
+                                             mode="reference", stroke_importance=self.cfg.stroke_importance_factor,
+                                             clamp=self.cfg.loss_clamp, drop_keep=keep, drop_seed=drop_seed,
+                                             drop_stream=7)
         return cost, shape, pen, final
 
     # -- single step (sampling) --------------------------------------------------------

@@ -146,8 +146,11 @@ class SketchVAE(nn.Module):
         return (h, c, hh, hc)
 
     # -- decoder ---------------------------------------------------------------------
-    def decode(self, x: torch.Tensor, zc: Optional[torch.Tensor], state, train: bool, seed: int):
-        """``x [T, B, 5]`` time-major -> ``(outputs [T, B, H], final_state)``."""
+    def decode(self, x: torch.Tensor, zc: Optional[torch.Tensor], state, train: bool, seed: int,
+               out_dropout: bool = True):
+        """``x [T, B, 5]`` time-major -> ``(outputs [T, B, H], final_state)``.
+        ``out_dropout=False``: the caller applies the output dropout itself
+        (the fused MDN head masks its input in-kernel)."""
         cfg = self.cfg
         T, B, _ = x.shape
         if train and cfg.use_input_dropout:   # the mask covers z too: no per-sequence factoring
@@ -169,7 +172,7 @@ class SketchVAE(nn.Module):
             xp = stroke_input_proj(x, zc, p.W_x, None if ln else p.bias)
             out, final = ops.lstm_sequence(xp, p.W_h, h0, c0, drop_keep=keep, drop_seed=seed,
                                            drop_stream=_S_DEC, ln=ln)
-        if train and cfg.use_output_dropout:
+        if train and cfg.use_output_dropout and out_dropout:
             out = out * C.dropout_mask(seed, _S_OUT, 0, out.shape, cfg.output_dropout_prob, out.device)
         return out, final
 
@@ -206,11 +209,13 @@ class SketchVAE(nn.Module):
         zc = self.condition(z, labels, B, dev)
         state = self.initial_state(zc, B, dev)
         x_in = strokes[:, :Nmax].transpose(0, 1)
-        out, _ = self.decode(x_in, zc, state, train, seed)
-        zout = self.head(out)
+        out, _ = self.decode(x_in, zc, state, train, seed, out_dropout=False)
         target = strokes[:, 1:].transpose(0, 1).reshape(-1, 5)
-        r_cost, shape, pen = ops.mdn_loss(zout, target, cfg.num_mixture, mode="magenta",
-                                          is_training=cfg.is_training)
+        # head + loss (fused on the GPU: projection, MDN loss and dL/dz in one kernel)
+        keep = cfg.output_dropout_prob if (train and cfg.use_output_dropout) else 1.0
+        r_cost, shape, pen = ops.mdn_head_loss(out.reshape(-1, out.shape[-1]), self.output_w, self.output_b, target,
+                                               cfg.num_mixture, mode="magenta", is_training=cfg.is_training,
+                                               drop_keep=keep, drop_seed=seed, drop_stream=_S_OUT)
         cost = r_cost + kl * kl_weight
         out = {"cost": cost, "r_cost": r_cost, "kl_cost": kl, "shape_cost": shape, "pen_cost": pen}
         if split_encoder and cfg.conditional:

@@ -135,3 +135,26 @@ def mdn_loss(z, target, M: int, mode: str = "magenta", stroke_importance: float 
         return mdn_loss_hip(z, target, M, mode, stroke_importance, is_training, clamp, eps)
     from ..models.mdn import mdn_loss_torch
     return mdn_loss_torch(z, target, M, mode, stroke_importance, is_training, clamp, eps)
+
+
+def mdn_head_loss(x, W, b, target, M: int, mode: str = "magenta", stroke_importance: float = 200.0,
+                  is_training: bool = True, clamp: float = 1e-20, eps: float = 1e-6,
+                  drop_keep: float = 1.0, drop_seed=0, drop_stream: int = 0):
+    """MDN loss of the head ``z = dropout(x) @ W + b`` (``x [..., Hd]``).
+
+    bf16 HIP training: ONE kernel computes the projection on MFMA, the loss
+    and dL/dz (csrc/mdn_head.hip; z never reaches HBM) and the backward runs
+    hand-written MFMA kernels. Otherwise: dropout, ``gemm.linear`` and
+    :func:`mdn_loss` (identical math, reference model.py:98-178)."""
+    from .mdn_hip import head_fused_ok
+    if head_fused_ok(x, W, M) and torch.is_grad_enabled():
+        from .mdn_hip import mdn_head_loss_hip
+        return mdn_head_loss_hip(x, W, b, target, M, mode, stroke_importance, is_training, clamp, eps,
+                                 drop_keep, drop_seed, drop_stream)
+    from . import gemm
+    from ..models.cells import dropout_mask
+    x2 = x.reshape(-1, x.shape[-1])
+    if drop_keep < 1.0:
+        x2 = x2 * dropout_mask(drop_seed, drop_stream, 0, x2.shape, drop_keep, x2.device)
+    z = gemm.linear(x2, W, b)
+    return mdn_loss(z, target, M, mode, stroke_importance, is_training, clamp, eps)

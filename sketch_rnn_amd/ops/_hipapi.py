@@ -215,6 +215,36 @@ class WFwdArgs(C.Structure):
     ]
 
 
+class HeadFwd(C.Structure):
+    """Mirror of ``HeadFwd`` in csrc/mdn_head.hip (fused MDN head forward)."""
+    _fields_ = [
+        ("X", _p), ("ldx", _i64), ("N", _i64), ("Hd", _i),
+        ("Wt", _p), ("bias", _p), ("tgt", _p), ("ldt", _i64),
+        ("M", _i), ("NOUT", _i), ("NOUTP", _i), ("mode", _i), ("mask_pen", _i),
+        ("F", _f), ("log_floor", _f), ("inv_n", _f),
+        ("keep", _f), ("seed", _p), ("stream", _u32),
+        ("dz", _p), ("part", _p),
+    ]
+
+
+class HeadDx(C.Structure):
+    _fields_ = [
+        ("dz", _p), ("N", _i64), ("NOUTP", _i),
+        ("Wb", _p), ("Hd", _i),
+        ("scale", _p), ("keep", _f), ("seed", _p), ("stream", _u32),
+        ("dX", _p), ("lddx", _i64),
+    ]
+
+
+class HeadDw(C.Structure):
+    _fields_ = [
+        ("X", _p), ("ldx", _i64), ("N", _i64), ("Hd", _i),
+        ("dz", _p), ("NOUTP", _i),
+        ("scale", _p), ("keep", _f), ("seed", _p), ("stream", _u32),
+        ("slab", _p), ("rows_per", _i64),
+    ]
+
+
 class GemmProblem(C.Structure):
     """Mirror of ``GemmProblem`` in csrc/skinny_gemm.hip."""
     _fields_ = [
@@ -274,6 +304,14 @@ class HipLib:
         lib.skr_lstm_persist_fwd.restype = _i
         lib.skr_lstm_persist_bwd.argtypes = [C.POINTER(PBwdArgs), _p]
         lib.skr_lstm_persist_bwd.restype = _i
+        lib.skr_mdn_head_fwd.argtypes = [C.POINTER(HeadFwd), _p, _p]
+        lib.skr_mdn_head_fwd.restype = _i
+        lib.skr_mdn_head_nblocks.argtypes = [_i64]
+        lib.skr_mdn_head_nblocks.restype = _i
+        lib.skr_mdn_head_dx.argtypes = [C.POINTER(HeadDx), _p]
+        lib.skr_mdn_head_dx.restype = _i
+        lib.skr_mdn_head_dw.argtypes = [C.POINTER(HeadDw), _i, _i, _p, _p, _p]
+        lib.skr_mdn_head_dw.restype = _i
         lib.skr_lstm_wide_fwd.argtypes = [C.POINTER(WFwdArgs), _p]
         lib.skr_lstm_wide_fwd.restype = _i
         lib.skr_lstm_wide_flag_words.argtypes = [_i, _i]
@@ -291,6 +329,9 @@ class HipLib:
                           ("skr_lstm_persist_fwd_args_size", PFwdArgs),
                           ("skr_lstm_persist_bwd_args_size", PBwdArgs),
                           ("skr_lstm_wide_fwd_args_size", WFwdArgs),
+                          ("skr_mdn_head_fwd_args_size", HeadFwd),
+                          ("skr_mdn_head_dx_args_size", HeadDx),
+                          ("skr_mdn_head_dw_args_size", HeadDw),
                           ("skr_gemm_problem_size", GemmProblem)):
             fn = getattr(lib, name)
             fn.restype = _i

@@ -3,6 +3,7 @@ per-row loss terms and dL/dz; backward only rescales the pen / mixture
 column groups by the incoming gradients."""
 from __future__ import annotations
 
+import ctypes as C
 import math
 
 import torch
@@ -50,3 +51,115 @@ def mdn_loss_hip(z, target, M, mode="magenta", stroke_importance=200.0, is_train
     if mode == "reference":
         return _MDNLoss.apply(z, target, M, 0, stroke_importance, 0, math.log(clamp))
     return _MDNLoss.apply(z, target, M, 1, 0.0, 0 if is_training else 1, math.log(eps))
+
+
+# ---------------------------------------------------------------------------------
+# fused head: projection + loss + dz in one kernel (csrc/mdn_head.hip)
+# ---------------------------------------------------------------------------------
+def head_fused_ok(x: torch.Tensor, W: torch.Tensor, M: int) -> bool:
+    """The fused MDN head applies to bf16 HIP training on the GPU with M <= 24
+    mixtures and a decoder width that is a multiple of 128."""
+    from . import gemm, use_hip
+    return (FUSED_HEAD and x.is_cuda and use_hip(x) and gemm.lp_dtype() == torch.bfloat16 and 1 <= M <= 24
+            and W.shape[0] % 128 == 0 and W.shape[1] == 3 + 6 * M)
+
+
+FUSED_HEAD = __import__("os").environ.get("SKR_FUSED_HEAD", "1") != "0"
+
+
+def _noutp(nout: int) -> int:
+    return (nout + 31) // 32 * 32
+
+
+class _MDNHead(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, X, W, b, target, seed, meta):
+        from ._hipapi import HeadDx, HeadDw, HeadFwd  # noqa: F401 (bound in native)
+        M, mode, F, mask_pen, log_floor, keep, stream = meta
+        lib = native.require_hip()
+        Hd, NOUT = W.shape
+        NOUTP = _noutp(NOUT)
+        X2 = X.reshape(-1, Hd).contiguous().float()
+        N = X2.shape[0]
+        dev = X2.device
+        tgt = target.reshape(-1, 5).contiguous().float()
+        Wt = torch.zeros(NOUTP, Hd, device=dev, dtype=torch.bfloat16)
+        Wt[:NOUT] = W.t()
+        bias = b.contiguous().float()
+        nb = lib.lib.skr_mdn_head_nblocks(N)
+        part = torch.empty(2 * nb, device=dev, dtype=torch.float32)
+        out3 = torch.empty(3, device=dev, dtype=torch.float32)
+        need = any(ctx.needs_input_grad[:3])
+        dz = torch.empty(N, NOUTP, device=dev, dtype=torch.bfloat16) if need else None
+        from .recurrent import _seed_tensor
+        sd = _seed_tensor(seed, dev)
+        a = HeadFwd()
+        a.X, a.ldx, a.N, a.Hd = X2.data_ptr(), X2.stride(0), N, Hd
+        a.Wt, a.bias, a.tgt, a.ldt = Wt.data_ptr(), bias.data_ptr(), tgt.data_ptr(), tgt.stride(0)
+        a.M, a.NOUT, a.NOUTP, a.mode, a.mask_pen = M, NOUT, NOUTP, mode, mask_pen
+        a.F, a.log_floor, a.inv_n = float(F), float(log_floor), 1.0 / max(N, 1)
+        a.keep, a.seed, a.stream = float(keep), sd.data_ptr(), int(stream)
+        a.dz, a.part = (dz.data_ptr() if dz is not None else None), part.data_ptr()
+        rc = lib.lib.skr_mdn_head_fwd(C.byref(a), out3.data_ptr(), _stream())
+        if rc != 0:
+            raise RuntimeError("skr_mdn_head_fwd failed (%d)" % rc)
+        ctx.save_for_backward(X2, W)
+        ctx.dz, ctx.sd, ctx.meta, ctx.xshape, ctx.keep_alive = dz, sd, meta, X.shape, (Wt, tgt, bias, part)
+        return out3[0], out3[1], out3[2]
+
+    @staticmethod
+    def backward(ctx, g_total, g_shape, g_pen):
+        from ._hipapi import HeadDw, HeadDx
+        X2, W = ctx.saved_tensors
+        M, mode, F, mask_pen, log_floor, keep, stream = ctx.meta
+        lib = native.require_hip()
+        dz, sd = ctx.dz, ctx.sd
+        ctx.dz = ctx.keep_alive = None
+        N, Hd = X2.shape
+        NOUT = W.shape[1]
+        NOUTP = dz.shape[1]
+        dev = X2.device
+        z0 = torch.zeros((), device=dev)
+        gt = g_total if g_total is not None else z0
+        scale = torch.stack([gt + (g_pen if g_pen is not None else z0),
+                             gt + (g_shape if g_shape is not None else z0)]).float().contiguous()
+        dX = dW = db = None
+        if ctx.needs_input_grad[0]:
+            Wb = torch.zeros(Hd, NOUTP, device=dev, dtype=torch.bfloat16)
+            Wb[:, :NOUT] = W
+            dX = torch.empty(N, Hd, device=dev, dtype=torch.float32)
+            a = HeadDx()
+            a.dz, a.N, a.NOUTP, a.Wb, a.Hd = dz.data_ptr(), N, NOUTP, Wb.data_ptr(), Hd
+            a.scale, a.keep, a.seed, a.stream = scale.data_ptr(), float(keep), sd.data_ptr(), int(stream)
+            a.dX, a.lddx = dX.data_ptr(), Hd
+            rc = lib.lib.skr_mdn_head_dx(C.byref(a), _stream())
+            if rc != 0:
+                raise RuntimeError("skr_mdn_head_dx failed (%d)" % rc)
+            dX = dX.view(ctx.xshape)
+        if ctx.needs_input_grad[1] or ctx.needs_input_grad[2]:
+            S = 16
+            rows_per = (-(-N // S) + 31) // 32 * 32
+            S = -(-N // rows_per)
+            slab = torch.empty(S, Hd + 64, NOUTP, device=dev, dtype=torch.float32)
+            dW = torch.empty(Hd, NOUT, device=dev, dtype=torch.float32)
+            db = torch.empty(NOUT, device=dev, dtype=torch.float32)
+            a = HeadDw()
+            a.X, a.ldx, a.N, a.Hd = X2.data_ptr(), X2.stride(0), N, Hd
+            a.dz, a.NOUTP = dz.data_ptr(), NOUTP
+            a.scale, a.keep, a.seed, a.stream = scale.data_ptr(), float(keep), sd.data_ptr(), int(stream)
+            a.slab, a.rows_per = slab.data_ptr(), rows_per
+            rc = lib.lib.skr_mdn_head_dw(C.byref(a), S, NOUT, dW.data_ptr(), db.data_ptr(), _stream())
+            if rc != 0:
+                raise RuntimeError("skr_mdn_head_dw failed (%d)" % rc)
+        return dX, dW, db, None, None, None
+
+
+def mdn_head_loss_hip(x, W, b, target, M, mode="magenta", stroke_importance=200.0, is_training=True,
+                      clamp=1e-20, eps=1e-6, drop_keep=1.0, drop_seed=0, drop_stream=0):
+    """``(total, shape, pen)`` of the MDN loss of ``z = drop(x) @ W + b`` with
+    the projection, loss and dL/dz fused (``x [..., Hd]`` fp32)."""
+    if mode == "reference":
+        meta = (M, 0, float(stroke_importance), 0, math.log(clamp), float(drop_keep), int(drop_stream))
+    else:
+        meta = (M, 1, 0.0, 0 if is_training else 1, math.log(eps), float(drop_keep), int(drop_stream))
+    return _MDNHead.apply(x, W, b, target, drop_seed, meta)
