@@ -1,0 +1,95 @@
+// In-launch hand-off primitives shared by the persistent kernels
+// (csrc/lstm_persist.hip, csrc/decode_ref.hip).
+//
+// Protocol (CDNA4 guide, Guideline 16, first row of the measured hand-offs
+// table): the producer stores its payload write-through (buffer_store ...
+// sc1), every storing wave drains (s_waitcnt vmcnt(0)), a workgroup barrier,
+// then ONE lane stores the workgroup's epoch into its flag word with an sc1
+// store. A consumer wave polls the flag words it depends on with sc1 loads
+// (one lane per flag, bounded spin with s_sleep) and then reads the payload
+// with sc1 buffer loads only. A timed-out wait sets *err (the host raises)
+// and poisons the launch so every other wait returns at once: the grid
+// always drains.
+#pragma once
+#include "common.h"
+
+namespace skr {
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int kSc1 = 16;                  // buffer cache-policy bits: sc1 (device scope, write-through)
+constexpr unsigned kHandoffSpinLimit = 1u << 22;
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* p, int64_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, (int)(bytes > 0x7fffffff ? 0x7fffffff : bytes),
+                                             0x00020000);
+}
+__device__ __forceinline__ bf16x8 ld_sc1(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+    return __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, kSc1));
+}
+__device__ __forceinline__ float ld_sc1_f32(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, kSc1));
+}
+__device__ __forceinline__ void st_sc1(__amdgpu_buffer_rsrc_t r, uint32_t off, u32x4 v) {
+    __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, kSc1);
+}
+__device__ __forceinline__ void st_sc1_f32(__amdgpu_buffer_rsrc_t r, uint32_t off, float v) {
+    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), r, off, 0, kSc1);
+}
+
+// One wave waits until every flag of `flags[0..n)` (n <= 64) is >= epoch
+// (lane i polls flag i with sc1 loads). Bounded; on a timeout (or when
+// another wait of this launch already timed out) sets/observes *err and
+// returns false.
+__device__ inline bool wait_flags(const uint32_t* flags, int n, uint32_t epoch, int* err) {
+    const int lane = threadIdx.x & 63;
+    const uint32_t* f = flags + (lane < n ? lane : 0);
+    for (unsigned spins = 0;; ++spins) {
+        const uint32_t v = __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (__all(lane >= n || v >= epoch)) break;
+        if ((spins & 255) == 255) {
+            const int e = __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (e != 0) return false;
+            if (spins > kHandoffSpinLimit) {
+                if (lane == 0) __hip_atomic_store(err, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                return false;
+            }
+        }
+        __builtin_amdgcn_s_sleep(1);
+    }
+    // compiler barrier: the payload loads may not move above the poll
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    return true;
+}
+
+// Publish: every storing wave already issued its sc1 payload stores.
+__device__ __forceinline__ void publish(uint32_t* flag, uint32_t epoch) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_store(flag, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Flag words are zeroed by a kernel, not hipMemsetAsync: on MI355X with
+// torch's HIP 7.0 runtime a memset node captured into a HIP graph is not
+// ordered before the next kernel node on replay (see csrc/lstm_persist.hip).
+namespace {
+__global__ void zero_flags(uint32_t* f, int n) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i < n) f[i] = 0u;
+}
+}  // namespace
+
+// All workgroups of a persistent launch must be co-resident (they wait on
+// each other): check the grid against the occupancy API.
+inline bool grid_fits(const void* k, int threads, size_t lds, int grid, int max_per_cu = 2) {
+    int dev = 0, cus = 0, per = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k, threads, lds) != hipSuccess)
+        return false;
+    return per >= 1 && grid <= cus * (per < max_per_cu ? per : max_per_cu);
+}
+
+}  // namespace skr

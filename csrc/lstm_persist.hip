@@ -46,20 +46,15 @@
 // model.py:66-95 (static unroll with the eoc state reset: the carried state
 // of a row whose input has eoc set is replaced by the batch-initial state);
 // recurrent dropout on tanh(j) keyed like csrc/lstm_cell.hip.
+#include "handoff.h"
 #include "lstm_args.h"
 
 namespace {
 
 using namespace skr;
 
-typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
-typedef __attribute__((ext_vector_type(4))) float f32x4;
-typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-
 constexpr int U = 16;               // hidden units per workgroup
 constexpr int NTHR = 512;           // 8 waves
-constexpr int kSc1 = 16;            // buffer cache-policy bits: sc1 (device scope, write-through)
-constexpr unsigned kSpinLimit = 1u << 22;
 constexpr int kFlagStride = 64;     // u32 flag words per (layer, group, row block)
 
 }  // namespace
@@ -113,48 +108,6 @@ struct PBwdArgs {
 };
 
 namespace {
-
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* p, int64_t bytes) {
-    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, (int)(bytes > 0x7fffffff ? 0x7fffffff : bytes),
-                                             0x00020000);
-}
-__device__ __forceinline__ bf16x8 ld_sc1(__amdgpu_buffer_rsrc_t r, uint32_t off) {
-    return __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, kSc1));
-}
-__device__ __forceinline__ void st_sc1(__amdgpu_buffer_rsrc_t r, uint32_t off, u32x4 v) {
-    __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, kSc1);
-}
-
-// One wave waits until every flag of `flags[0..n)` is >= epoch (lane i polls
-// flag i with sc1 loads). Bounded; on a timeout (or when another wait of this
-// launch already timed out) sets/observes *err and returns false.
-__device__ bool wait_flags(const uint32_t* flags, int n, uint32_t epoch, int* err) {
-    const int lane = threadIdx.x & 63;
-    const uint32_t* f = flags + (lane < n ? lane : 0);
-    for (unsigned spins = 0;; ++spins) {
-        const uint32_t v = __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (__all(lane >= n || v >= epoch)) break;
-        if ((spins & 255) == 255) {
-            const int e = __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (e != 0) return false;
-            if (spins > kSpinLimit) {
-                if (lane == 0) __hip_atomic_store(err, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                return false;
-            }
-        }
-        __builtin_amdgcn_s_sleep(1);
-    }
-    // compiler barrier: the payload loads may not move above the poll
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    return true;
-}
-
-// Publish: every storing wave already issued its sc1 payload stores.
-__device__ __forceinline__ void publish(uint32_t* flag, uint32_t epoch) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0) __hip_atomic_store(flag, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
 
 // Stage nrows x K of a row-major bf16 matrix into LDS with the 16-byte
 // chunks of LDS row r XOR-swizzled by (r & 15) (conflict-free ds_read_b128 of
@@ -586,21 +539,6 @@ inline size_t bwd_lds(int H, int L) {
     return (size_t)(L > 1 ? 2 : 1) * 16 * 4 * H * 2 + (size_t)(8 / kMTW) * kMTW * 2 * 64 * 16 + (size_t)kMTW * 1024 * 2;
 }
 
-__global__ void zero_flags(uint32_t* f, int n) {
-    const int i = blockIdx.x * 256 + threadIdx.x;
-    if (i < n) f[i] = 0u;
-}
-
-// all workgroups of a launch must be co-resident (they wait on each other)
-inline bool fits(const void* k, size_t lds, int grid) {
-    int dev = 0, cus = 0, per = 0;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k, NTHR, lds) != hipSuccess)
-        return false;
-    return per >= 1 && grid <= cus * (per < 2 ? per : 2);
-}
-
 template <typename A, typename KF>
 int launch_persist(KF kern, const A& a, size_t lds, hipStream_t s) {
     const int NW = a.H / U;
@@ -614,7 +552,7 @@ int launch_persist(KF kern, const A& a, size_t lds, hipStream_t s) {
         for (auto& p : attr_done)
             if (p == nullptr) { p = (const void*)kern; break; }
     }
-    if (!fits((const void*)kern, lds, grid)) return -8;
+    if (!grid_fits((const void*)kern, NTHR, lds, grid)) return -8;
     // Zero the flag words with a kernel, not hipMemsetAsync: on MI355X with
     // torch's HIP 7.0 runtime a memset node captured into a HIP graph is not
     // ordered before the next kernel node on replay -- replays 2.. of a

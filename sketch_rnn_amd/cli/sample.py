@@ -6,9 +6,12 @@ the non-executing pickle reader) and the latest checkpoint, then generates
 in ``[4, 22]``, at least one ``eoc``, bounding box within
 ``[0, 0.8] * picture_size``) and writes a colour SVG grid.
 
-``--device_sampler`` draws candidates in parallel batches with the
-HIP-graph decoder (``sample.sampler.GraphDecoder``) instead of the
-one-stroke-at-a-time host loop.
+``--device_sampler`` draws candidates in parallel batches on the GPU
+instead of the one-stroke-at-a-time host loop: with the fused whole-sketch
+decoder (``sample.fused.FusedRefDecoder``, one kernel launch per batch)
+when the model is eligible (2 x 256 LSTM class), otherwise with the
+HIP-graph decoder (``sample.sampler.GraphDecoder``; ``--graph_decoder``
+forces it).
 """
 from __future__ import annotations
 
@@ -38,6 +41,8 @@ def build_parser():
     p.add_argument("--device", type=str, default=None)
     p.add_argument("--seed", type=int, default=None)
     p.add_argument("--device_sampler", action="store_true")
+    p.add_argument("--graph_decoder", action="store_true",
+                   help="with --device_sampler: per-stroke HIP-graph decoder instead of the fused one-launch decoder")
     p.add_argument("--batch", type=int, default=64, help="candidates per device-sampler replay")
     p.add_argument("--max_attempts", type=int, default=100000)
     p.add_argument("--fix_pen_temperature", action="store_true")
@@ -89,7 +94,13 @@ def main(argv=None) -> int:
     py_rng = random.Random(a.seed)
     accepted, attempts = [], 0
     if a.device_sampler and device.startswith("cuda"):
-        dec = GraphDecoder(model, a.batch, a.sample_length, a.temperature, fix_pen_temperature=a.fix_pen_temperature)
+        from ..sample.fused import FusedRefDecoder, fused_decode_ok
+        if fused_decode_ok(model) and not a.graph_decoder:   # one launch per batch (csrc/decode_ref.hip)
+            dec = FusedRefDecoder(model, a.batch, a.sample_length, a.temperature,
+                                  fix_pen_temperature=a.fix_pen_temperature)
+        else:
+            dec = GraphDecoder(model, a.batch, a.sample_length, a.temperature,
+                               fix_pen_temperature=a.fix_pen_temperature)
         while len(accepted) < a.num_picture and attempts < a.max_attempts:
             strokes, lengths = dec.run(seed=rng.randint(1 << 30))
             s_np, l_np = strokes.cpu().numpy(), lengths.cpu().numpy()

@@ -245,6 +245,26 @@ class HeadDw(C.Structure):
     ]
 
 
+class DecLayer(C.Structure):
+    """Mirror of ``DecLayer`` in csrc/decode_ref.hip (fused whole-sketch decoder)."""
+    _fields_ = [
+        ("WT", _p), ("bias", _p), ("h0", _p), ("c0", _p),
+        ("hbuf", _p), ("hup", _p), ("hT", _p), ("cT", _p),
+    ]
+
+
+class DecArgs(C.Structure):
+    _fields_ = [
+        ("N", _i), ("B", _i), ("L", _i), ("H", _i), ("mtw", _i), ("nrb", _i), ("M", _i), ("nout", _i),
+        ("noutp", _i), ("mode", _i), ("greedy", _i), ("fix_pen", _i), ("forced", _i), ("row0", _i),
+        ("temp", _f), ("forget_bias", _f),
+        ("ly", DecLayer * 2),
+        ("Wx0", _p), ("WoT", _p), ("bo", _p),
+        ("xin", _p), ("out", _p), ("done", _p), ("zout", _p),
+        ("seed", _p), ("flags", _p), ("err", _p),
+    ]
+
+
 class GemmProblem(C.Structure):
     """Mirror of ``GemmProblem`` in csrc/skinny_gemm.hip."""
     _fields_ = [
@@ -318,6 +338,8 @@ class HipLib:
         lib.skr_lstm_wide_flag_words.restype = _i
         lib.skr_hyper_vec_fwd.argtypes = [_p, _i64, _p, _p, _p, _i64, _i64, _i, _i, _i, _p]
         lib.skr_hyper_vec_fwd.restype = _i
+        lib.skr_decode_ref.argtypes = [C.POINTER(DecArgs), _p]
+        lib.skr_decode_ref.restype = _i
         lib.skr_stream_create_cumask.argtypes = [_i, _i, _i, C.POINTER(_p)]
         lib.skr_stream_create_cumask.restype = _i
         lib.skr_stream_destroy.argtypes = [_p]
@@ -332,6 +354,7 @@ class HipLib:
                           ("skr_mdn_head_fwd_args_size", HeadFwd),
                           ("skr_mdn_head_dx_args_size", HeadDx),
                           ("skr_mdn_head_dw_args_size", HeadDw),
+                          ("skr_decode_ref_args_size", DecArgs),
                           ("skr_gemm_problem_size", GemmProblem)):
             fn = getattr(lib, name)
             fn.restype = _i
