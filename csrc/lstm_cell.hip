@@ -168,7 +168,10 @@ __global__ __launch_bounds__(NT) void cell_fwd(const FwdArgs a) {
         }
     }
     // ---- LayerNorm over each gate block of the row: sums and sums of
-    // squares in ONE row reduction (var = E[g^2] - mean^2 in fp32, clamped)
+    // squares in ONE row reduction (var = E[g^2] - mean^2 in fp32, clamped).
+    // The saves (xhat, bf16 R, c') are stored only after the second
+    // exchange: stores queued on a CU delay its in-launch hand-offs.
+    float xs[UPT][4];   // xhat (LN)
     if (LN) {
         float s[8];
 #pragma unroll
@@ -194,12 +197,10 @@ __global__ __launch_bounds__(NT) void cell_fwd(const FwdArgs a) {
         for (int q = 0; q < 4; ++q) rs[q] = rsqrtf(var[q] + kLnEps);
 #pragma unroll
         for (int k = 0; k < UPT; ++k) {
-            const int u = base + k * NT + tid;
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
-                const float xh = (g[k][q] - mean[q]) * rs[q];
-                if (save && on[k]) a.xhat[(int64_t)b * 4 * H + q * H + u] = xh;
-                g[k][q] = xh * lg[k][q] + lb[k][q];
+                xs[k][q] = (g[k][q] - mean[q]) * rs[q];
+                g[k][q] = xs[k][q] * lg[k][q] + lb[k][q];
             }
         }
         if (save && c == 0 && tid < 4) a.rstd[b * 5 + tid] = rs[tid];
@@ -224,10 +225,8 @@ __global__ __launch_bounds__(NT) void cell_fwd(const FwdArgs a) {
             ap[2 * H] = f;
             ap[3 * H] = o;
         }
-        if (a.c_out != nullptr && on[k]) a.c_out[ro] = cn[k];
-        if (MOD && a.r_lp != nullptr && on[k]) {
-#pragma unroll
-            for (int q = 0; q < 4; ++q) a.r_lp[b * a.ld_R + q * H + u] = to_bf16(rsv[k][q]);
+        if (!LN) {
+            if (a.c_out != nullptr && on[k]) a.c_out[ro] = cn[k];
         }
     }
     float th[UPT];
@@ -246,9 +245,20 @@ __global__ __launch_bounds__(NT) void cell_fwd(const FwdArgs a) {
 #pragma unroll
         for (int k = 0; k < UPT; ++k) {
             const int u = base + k * NT + tid;
+            const int64_t ro = (int64_t)b * H + u;
             const float ch = (cn[k] - mean) * rc;
-            if (save && on[k]) a.chat[(int64_t)b * H + u] = ch;
             th[k] = tanhf(ch * lcg[k] + lcb[k]);
+            if (!on[k]) continue;
+            if (save) {
+                a.chat[ro] = ch;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) a.xhat[(int64_t)b * 4 * H + q * H + u] = xs[k][q];
+            }
+            if (a.c_out != nullptr) a.c_out[ro] = cn[k];
+            if (MOD && a.r_lp != nullptr) {
+#pragma unroll
+                for (int q = 0; q < 4; ++q) a.r_lp[b * a.ld_R + q * H + u] = to_bf16(rsv[k][q]);
+            }
         }
     } else {
 #pragma unroll
@@ -359,7 +369,9 @@ __global__ __launch_bounds__(NT) void cell_bwd(const BwdArgs a) {
         }
     }
     // ---- output: h' = th * o
-    float dc[UPT], dout[UPT], dch[UPT];
+    // (the LN-path saves dlncy / dc_rec / dlny are stored after the last
+    // exchange: stores queued on a CU delay its in-launch hand-offs)
+    float dc[UPT], dout[UPT], dch[UPT], dlc[UPT], dcr[UPT];
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
     for (int k = 0; k < UPT; ++k) {
@@ -376,7 +388,7 @@ __global__ __launch_bounds__(NT) void cell_bwd(const BwdArgs a) {
         dout[k] = dh * t;
         const float dcn = dh * o * (1.f - t * t);
         if (LN) {
-            if (on[k]) a.dlncy[ro] = dcn;
+            dlc[k] = dcn;
             dch[k] = on[k] ? dcn * lcg[k] : 0.f;
             s1 += dch[k];
             s2 += dch[k] * cx[k];
@@ -403,19 +415,19 @@ __global__ __launch_bounds__(NT) void cell_bwd(const BwdArgs a) {
         dy[k][1] = dc[k] * i * m * (1.f - tj * tj);
         dy[k][2] = dc[k] * cp[k] * f * (1.f - f);
         dy[k][3] = dout[k] * o * (1.f - o);
-        if (on[k]) a.dc_rec[ro] = dc[k] * f;
+        dcr[k] = dc[k] * f;
+        if (!LN && on[k]) a.dc_rec[ro] = dcr[k];
     }
     // ---- LayerNorm over each gate block
     if (LN) {
-        float acc[8];
+        float acc[8], dly[UPT][4];
 #pragma unroll
         for (int q = 0; q < 8; ++q) acc[q] = 0.f;
 #pragma unroll
         for (int k = 0; k < UPT; ++k) {
-            const int u = base + k * NT + tid;
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
-                if (on[k]) a.dlny[(int64_t)b * 4 * H + q * H + u] = dy[k][q];
+                dly[k][q] = dy[k][q];
                 const float dg = on[k] ? dy[k][q] * lg[k][q] : 0.f;
                 dy[k][q] = dg;
                 acc[q] += dg;
@@ -423,6 +435,16 @@ __global__ __launch_bounds__(NT) void cell_bwd(const BwdArgs a) {
             }
         }
         row_sum<8, NW>(acc, lds, mine, all, a.part + (int64_t)a.B * C * kSlots, a.err, a.step + 1, b, c, C);
+#pragma unroll
+        for (int k = 0; k < UPT; ++k) {
+            if (!on[k]) continue;
+            const int u = base + k * NT + tid;
+            const int64_t ro = (int64_t)b * H + u;
+            a.dlncy[ro] = dlc[k];
+            a.dc_rec[ro] = dcr[k];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) a.dlny[(int64_t)b * 4 * H + q * H + u] = dly[k][q];
+        }
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             const float rs = a.rstd[b * 5 + q];
