@@ -49,7 +49,48 @@ __global__ __launch_bounds__(64) void mdn_sample_kernel(const float* __restrict_
     }
 }
 
+// Same, with z given as the sum of `nslab` split-K partial slabs of a head
+// GEMM without bias (csrc/skinny_gemm.hip, z = h @ W_out in slabs) plus the
+// bias: the wave first folds its row into LDS, then samples from there.
+__global__ __launch_bounds__(64) void mdn_sample_slabs_kernel(const float* __restrict__ zs, int64_t ldz, int nslab,
+                                                              int64_t slab, const float* __restrict__ bias, int nout,
+                                                              int M, int mode, float temp, int greedy, int fix_pen,
+                                                              const int64_t* seed, uint32_t step, int row0,
+                                                              float* __restrict__ out_row, int64_t ld_out,
+                                                              float* __restrict__ next_x, int64_t ld_next,
+                                                              int* __restrict__ done) {
+    __shared__ float zrow[256];
+    const int b = blockIdx.x, lane = threadIdx.x;
+    for (int c = lane; c < nout; c += 64) {
+        float v = bias[c];
+        for (int s = 0; s < nslab; ++s) v += zs[s * slab + (int64_t)b * ldz + c];
+        zrow[c] = v;
+    }
+    __syncthreads();
+    const uint32_t key = skr::hash_key(*seed, 0x5A3Du, step);
+    const skr::MdnDraw d = skr::mdn_sample_wave(zrow, M, mode, temp, greedy, fix_pen, key, (uint32_t)(row0 + b), step);
+    if (lane != 0) return;
+    const int stop_col = mode == 1 ? 4 : 3;  // p3 | eoc
+    float* o = out_row + b * ld_out;
+    const bool was_done = done[b] != 0;
+    for (int k = 0; k < 5; ++k) o[k] = was_done ? (k == stop_col ? 1.f : 0.f) : d.row[k];
+    float* nx = next_x + b * ld_next;
+    for (int k = 0; k < 5; ++k) nx[k] = d.row[k];
+    if (d.pidx + 2 == stop_col) done[b] = 1;
+}
+
 }  // namespace
+
+SKR_API int skr_mdn_sample_slabs(const float* zs, int64_t ldz, int nslab, int64_t slab, const float* bias, int B,
+                                 int M, int mode, float temp, int greedy, int fix_pen, const int64_t* seed,
+                                 uint32_t step, int row0, float* out_row, int64_t ld_out, float* next_x,
+                                 int64_t ld_next, int* done, hipStream_t s) {
+    if (M < 1 || M > 32 || nslab < 1) return -2;
+    if (B <= 0) return 0;
+    hipLaunchKernelGGL(mdn_sample_slabs_kernel, dim3(B), dim3(64), 0, s, zs, ldz, nslab, slab, bias, 3 + 6 * M, M,
+                       mode, temp, greedy, fix_pen, seed, step, row0, out_row, ld_out, next_x, ld_next, done);
+    return SKR_CHECK_LAUNCH();
+}
 
 SKR_API int skr_mdn_sample(const float* z, int64_t ldz, int B, int M, int mode, float temp, int greedy, int fix_pen,
                            const int64_t* seed, uint32_t step, float* out_row, int64_t ld_out, float* next_x,

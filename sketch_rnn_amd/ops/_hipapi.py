@@ -295,6 +295,9 @@ class HipLib:
                                              _i, _i, _i, _i, _i, _i, _p]
         lib.skr_skinny_gemm_fp8.restype = _i
         lib.skr_mdn_sample.restype = _i
+        lib.skr_mdn_sample_slabs.argtypes = [_p, _i64, _i, _i64, _p, _i, _i, _i, _f, _i, _i, _p, _u32, _i, _p, _i64,
+                                             _p, _i64, _p, _p]
+        lib.skr_mdn_sample_slabs.restype = _i
         lib.skr_inproj_fwd.argtypes = [_p, _p, _p, _p, _p, _i, _i, _i, _i, _p]
         lib.skr_inproj_fwd.restype = _i
         lib.skr_inproj_bwd.argtypes = [_p, _p, _p, _p, _i, _i, _i, _i, _i, _p]

@@ -1,0 +1,185 @@
+"""Lean per-stroke HyperLSTM decode step for :class:`~.sampler.GraphDecoder`
+(reference per-stroke step ``model.py:213-249``).
+
+The generic path (``SketchVAE.decode_step``) runs a whole T = 1 sequence per
+stroke: per-call state copies into the operand buffers, zero fills, the
+``z`` projections, a library head GEMM -- 20+ launches, ~60 % of them glue
+(rocprofv3: 0.169 ms per step at B = 256, 28 us of it ``copyBuffer``). Here
+the decoder state lives in place for the whole decode, the per-sketch
+constants (``z`` projections) are computed once, and a stroke is exactly
+seven kernels, all hand-written:
+
+1. ``bproj``: ``[x | z] @ [W_x; hW_x]`` for the main and hyper gates at once
+   (stroke rows only; the z rows are a per-sketch constant);
+2. grouped skinny MFMA GEMM: ``h @ W_h`` and ``[h | hh] @ W_y``;
+3. hyper LayerNorm cell (writes ``hh`` in bf16 straight into the operand
+   buffer, ``c`` in place);
+4. modulation vectors ``hh @ P`` (bf16 out);
+5. main LayerNorm + modulation cell (``h`` into the operand buffer);
+6. head ``h @ W_out`` as a skinny split-K GEMM on the bf16 ``h`` operand;
+7. device sampler folding the head's split-K slabs + bias, writing the next
+   input.
+
+Rows are processed in chunks of at most 128 (one MFMA row tile).
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+
+from ..ops import gemm
+from ..ops._hipapi import LstmFwdArgs
+from ..ops.recurrent import _ClusterSync, _seed_tensor
+from ..utils import native
+
+
+def hyper_step_ok(model, B: int) -> bool:
+    cfg = model.cfg
+    if cfg.dec_model != "hyper" or not torch.cuda.is_available():
+        return False
+    if next(model.parameters()).device.type != "cuda" or gemm.lp_dtype() != torch.bfloat16:
+        return False
+    from ..ops import get_compute_dtype
+    if get_compute_dtype() != "bf16" or not model.dec.use_layer_norm:
+        return False
+    H, Hh = cfg.dec_rnn_size, cfg.hyper_num_units
+    return B <= 128 and H % 64 == 0 and Hh % 64 == 0 and cfg.num_mixture <= 32
+
+
+class HyperStepDecoder:
+    """In-place decoder state of B <= 128 rows + the per-step launch sequence."""
+
+    def __init__(self, model, B: int, device):
+        self.lib = native.require_hip().lib
+        cfg, p = model.cfg, model.dec
+        self.model, self.B, self.dev = model, B, device
+        H, Hh = cfg.dec_rnn_size, cfg.hyper_num_units
+        G, Gh, K = 4 * H, 4 * Hh, H + Hh
+        self.H, self.Hh, self.G, self.Gh, self.K = H, Hh, G, Gh, K
+        self.M = cfg.num_mixture
+        self.nout = 3 + 6 * self.M
+        self.E = p.embed
+        bf, f32 = torch.bfloat16, torch.float32
+        self.S_m = gemm.plan_splits(B, G, H, 1, bf)
+        self.S_y = gemm.plan_splits(B, Gh, K, 1, bf)
+        self.S_o = gemm.plan_splits(B, 128, H, 1, bf)
+        assert min(self.S_m, self.S_y, self.S_o) >= 1
+        # state / operand buffers (resident for the whole decode)
+        self.A = torch.zeros(B, K, dtype=bf, device=device)          # [h | hh] bf16 GEMM operand
+        self.CC = torch.zeros(B, H, dtype=f32, device=device)
+        self.HCC = torch.zeros(B, Hh, dtype=f32, device=device)
+        self.Hout = torch.empty(B, H, dtype=f32, device=device)
+        self.HH = torch.empty(B, Hh, dtype=f32, device=device)
+        self.RM = torch.empty(self.S_m, B, G, dtype=f32, device=device)
+        self.RY = torch.empty(self.S_y, B, Gh, dtype=f32, device=device)
+        self.VEC = torch.empty(B, 12 * H, dtype=bf, device=device)
+        self.XP = torch.empty(B, G + Gh, dtype=f32, device=device)   # [main | hyper] stroke projections
+        self.ZP = torch.zeros(B, G + Gh, dtype=f32, device=device)   # per-sketch z projections
+        self.ZS = torch.empty(self.S_o, B, 128, dtype=f32, device=device)
+        self.clm = _ClusterSync(1, B, H, device)
+        self.clh = _ClusterSync(1, B, Hh, device)
+        self.sd = _seed_tensor(0, device)
+
+    # -- weights (cached per weight version, like the inference path of _HyperSeq) -----
+    def _weights(self):
+        m, p = self.model, self.model.dec
+        H, Hh, E, dt = self.H, self.Hh, self.E, torch.bfloat16
+        IN = p.W_x.shape[0]
+
+        def fold(W_z, b_z, W_a):
+            Wz3 = W_z.view(Hh, 12, E).permute(1, 0, 2)
+            P = torch.bmm(Wz3, W_a).permute(1, 0, 2).reshape(Hh, 12 * H)
+            q = torch.bmm(b_z.view(12, 1, E), W_a).reshape(12, H).contiguous()
+            return P.t().to(dt).contiguous(), q
+
+        def wy(a, b):
+            return torch.cat([a[IN:], b], 0).to(dt).t().contiguous()
+
+        def wout(W):
+            Wt = torch.zeros(128, H, dtype=dt, device=W.device)
+            Wt[: W.shape[1]] = W.t().to(dt)
+            return Wt
+
+        return dict(
+            WhT=gemm.derived(p.W_h, "hypWhT%s" % dt, lambda W: W.to(dt).t().contiguous()),
+            WyT=gemm.derived((p.hyp_W_x, p.hyp_W_h), "hypWyT%s" % dt, wy),
+            PQ=gemm.derived((p.W_z, p.b_z, p.W_a), "hypP%s" % dt, fold),
+            W5=gemm.derived((p.W_x, p.hyp_W_x), "stepW5",
+                            lambda a, b: torch.cat([a[:5], b[:5]], 1).float().contiguous()),
+            WoT=gemm.derived(m.output_w, "stepWoT", wout),
+            bo=m.output_b.detach().float().contiguous(),
+        )
+
+    @torch.no_grad()
+    def begin(self, zc, state) -> None:
+        """Load the initial state and the per-sketch z projections."""
+        p = self.model.dec
+        H = self.H
+        h0, c0, hh0, hc0 = state
+        self.A[:, :H].copy_(h0)
+        self.A[:, H:].copy_(hh0)
+        self.CC.copy_(c0)
+        self.HCC.copy_(hc0)
+        if zc is not None:
+            IN = p.W_x.shape[0]
+            torch.mm(zc, torch.cat([p.W_x[5:], p.hyp_W_x[5:IN]], 1), out=self.ZP)
+        else:
+            self.ZP.zero_()
+        for cl in (self.clm, self.clh):
+            if cl.on:
+                cl.part.zero_()
+
+    def _cell_args(self, t: int):
+        p, w = self.model.dec, self._w
+        B, H, Hh, G, Gh, K = self.B, self.H, self.Hh, self.G, self.Gh, self.K
+        lnh = [t_.contiguous() for t_ in (p.hyp_ln_gamma, p.hyp_ln_beta, p.hyp_lnc_gamma, p.hyp_lnc_beta)]
+        lnm = [t_.contiguous() for t_ in (p.ln_gamma, p.ln_beta, p.lnc_gamma, p.lnc_beta)]
+        self._keep = lnh + lnm
+        ah = LstmFwdArgs()
+        ah.B, ah.H = B, Hh
+        ah.xp, ah.ld_xp = self.XP[:, G:].data_ptr(), G + Gh
+        ah.R, ah.ld_R, ah.R_nslab, ah.R_slab = self.RY.data_ptr(), Gh, self.S_y, B * Gh
+        ah.ln_g, ah.ln_b, ah.lnc_g, ah.lnc_b = (x.data_ptr() for x in lnh)
+        ah.forget_bias, ah.keep = 1.0, 1.0
+        ah.seed, ah.stream, ah.step = self.sd.data_ptr(), 1, t
+        ah.c_prev, ah.c_carry, ah.h_out = self.HCC.data_ptr(), self.HCC.data_ptr(), self.HH.data_ptr()
+        ah.h_lp, ah.ld_lp, ah.lp_kind = self.A[:, H:].data_ptr(), K, 1
+        self.clh.set(ah, t)
+        am = LstmFwdArgs()
+        am.B, am.H = B, H
+        am.xp, am.ld_xp = self.XP.data_ptr(), G + Gh
+        am.R, am.ld_R, am.R_nslab, am.R_slab = self.RM.data_ptr(), G, self.S_m, B * G
+        PlT, q = w["PQ"]
+        am.vec, am.vec_gs, am.vec_ld, am.vec_bias = self.VEC.data_ptr(), H, 12 * H, q.data_ptr()
+        am.bias = p.bias.data_ptr()
+        am.ln_g, am.ln_b, am.lnc_g, am.lnc_b = (x.data_ptr() for x in lnm)
+        am.forget_bias, am.keep = 1.0, 1.0
+        am.seed, am.stream, am.step = self.sd.data_ptr(), 0, t
+        am.c_prev, am.c_carry, am.h_out = self.CC.data_ptr(), self.CC.data_ptr(), self.Hout.data_ptr()
+        am.h_lp, am.ld_lp, am.lp_kind = self.A.data_ptr(), K, 1
+        self.clm.set(am, t)
+        return ah, am
+
+    @torch.no_grad()
+    def step(self, x: torch.Tensor, t: int, sample) -> None:
+        """One stroke: ``x [B, 5]`` (fp32, contiguous) -> decoder step -> head
+        slabs -> ``sample(zs, ldz, nslab, slab, bias)`` (the caller's sampler)."""
+        if t == 0:
+            self._w = self._weights()
+        w = self._w
+        B, H, G, Gh = self.B, self.H, self.G, self.Gh
+        st = torch.cuda.current_stream().cuda_stream
+        rc = self.lib.skr_bproj_fwd(x.data_ptr(), w["W5"].data_ptr(), self.ZP.data_ptr(), self.XP.data_ptr(),
+                                    1, B, 5, G + Gh, st)
+        if rc != 0:
+            raise RuntimeError("skr_bproj_fwd failed (%d)" % rc)
+        gemm.rec_gemm_group([(self.A[:, :H], w["WhT"], self.RM, self.S_m), (self.A, w["WyT"], self.RY, self.S_y)])
+        ah, am = self._cell_args(t)
+        if self.lib.skr_lstm_fwd_step(ctypes.byref(ah), 1, 0, st) != 0:
+            raise RuntimeError("hyper cell step failed")
+        gemm.rec_gemm_bf16out(self.A[:, H:], w["PQ"][0], self.VEC)
+        if self.lib.skr_lstm_fwd_step(ctypes.byref(am), 1, 2, st) != 0:
+            raise RuntimeError("main cell step failed")
+        gemm.rec_gemm(self.A[:, :H], w["WoT"], self.ZS, self.S_o)
+        sample(self.ZS, 128, self.S_o, B * 128, w["bo"])

@@ -80,3 +80,42 @@ def test_graph_decoder_vae(dec_model):
             assert torch.all(sa[r, la[r]:, 4] == 1)
     finally:
         ops.set_backend("auto")
+
+
+@pytest.mark.parametrize("B", [16, 100])
+def test_hyper_step_decoder_matches_decode_step(B):
+    """The lean in-place HyperLSTM step (sample/hyper_step.py) against the
+    generic T = 1 sequence path (SketchVAE.decode_step) on the same inputs:
+    head outputs within bf16 tolerances over several strokes."""
+    from sketch_rnn_amd.sample.hyper_step import HyperStepDecoder, hyper_step_ok
+    native.require_hip()
+    ops.set_backend("hip")
+    ops.set_compute_dtype("bf16")
+    try:
+        cfg = VAEConfig(enc_rnn_size=64, dec_rnn_size=512, z_size=32, dec_model="hyper", hyper_num_units=128,
+                        hyper_embedding_size=16, num_classes=0, max_seq_len=16)
+        m = SketchVAE(cfg, seed=1).to(DEV).eval()
+        assert hyper_step_ok(m, B)
+        g = torch.Generator(device=DEV).manual_seed(3)
+        z = torch.randn(B, cfg.z_size, device=DEV, generator=g)
+        zc = m.condition(z, None, B, DEV)
+        state = m.initial_state(zc, B, DEV)
+        st = HyperStepDecoder(m, B, torch.device(DEV))
+        st.begin(zc, state)
+        for t in range(6):
+            x = torch.zeros(B, 5, device=DEV)
+            x[:, :2] = torch.randn(B, 2, device=DEV, generator=g) * 0.5
+            x[:, 2] = 1.0
+            got = {}
+
+            def sample(zs, ldz, nslab, slab, bias):
+                got["z"] = zs[:, :, : cfg.n_out].sum(0) + bias
+
+            st.step(x, t, sample)
+            ref, state = m.decode_step(x, zc, state)
+            torch.cuda.synchronize()
+            rel = float((got["z"] - ref).norm() / ref.norm())
+            assert rel < 2e-2, (t, rel)
+    finally:
+        ops.set_backend("auto")
+        ops.set_compute_dtype("fp32")
