@@ -51,22 +51,39 @@ __global__ __launch_bounds__(64) void mdn_sample_kernel(const float* __restrict_
 
 // Same, with z given as the sum of `nslab` split-K partial slabs of a head
 // GEMM without bias (csrc/skinny_gemm.hip, z = h @ W_out in slabs) plus the
-// bias: the wave first folds its row into LDS, then samples from there.
-__global__ __launch_bounds__(64) void mdn_sample_slabs_kernel(const float* __restrict__ zs, int64_t ldz, int nslab,
-                                                              int64_t slab, const float* __restrict__ bias, int nout,
-                                                              int M, int mode, float temp, int greedy, int fix_pen,
-                                                              const int64_t* seed, uint32_t step, int row0,
-                                                              float* __restrict__ out_row, int64_t ld_out,
-                                                              float* __restrict__ next_x, int64_t ld_next,
-                                                              int* __restrict__ done) {
+// bias. One 256-thread workgroup per row: wave w folds the slabs s = w mod 4
+// of every column with independent (unrolled, clamped) loads, the four
+// partial rows meet in LDS, then wave 0 samples.
+__global__ __launch_bounds__(256) void mdn_sample_slabs_kernel(const float* __restrict__ zs, int64_t ldz, int nslab,
+                                                               int64_t slab, const float* __restrict__ bias, int nout,
+                                                               int M, int mode, float temp, int greedy, int fix_pen,
+                                                               const int64_t* seed, uint32_t step, int row0,
+                                                               float* __restrict__ out_row, int64_t ld_out,
+                                                               float* __restrict__ next_x, int64_t ld_next,
+                                                               int* __restrict__ done) {
+    constexpr int kU = 8;                  // slabs per unrolled batch (per wave)
+    __shared__ float part[4][256];
     __shared__ float zrow[256];
-    const int b = blockIdx.x, lane = threadIdx.x;
-    for (int c = lane; c < nout; c += 64) {
-        float v = bias[c];
-        for (int s = 0; s < nslab; ++s) v += zs[s * slab + (int64_t)b * ldz + c];
-        zrow[c] = v;
+    const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const float* zb = zs + (int64_t)b * ldz;
+#pragma unroll
+    for (int cc = 0; cc < 4; ++cc) {
+        const int c = lane + 64 * cc;
+        if (c >= nout) break;
+        float v = 0.f;
+        for (int s0 = w; s0 < nslab; s0 += 4 * kU) {
+            float t[kU];
+#pragma unroll
+            for (int k = 0; k < kU; ++k) t[k] = zb[(int64_t)min(s0 + 4 * k, nslab - 1) * slab + c];
+#pragma unroll
+            for (int k = 0; k < kU; ++k) v += (s0 + 4 * k < nslab) ? t[k] : 0.f;
+        }
+        part[w][c] = v;
     }
     __syncthreads();
+    if (tid < nout) zrow[tid] = bias[tid] + ((part[0][tid] + part[1][tid]) + (part[2][tid] + part[3][tid]));
+    __syncthreads();
+    if (w != 0) return;
     const uint32_t key = skr::hash_key(*seed, 0x5A3Du, step);
     const skr::MdnDraw d = skr::mdn_sample_wave(zrow, M, mode, temp, greedy, fix_pen, key, (uint32_t)(row0 + b), step);
     if (lane != 0) return;
@@ -87,7 +104,7 @@ SKR_API int skr_mdn_sample_slabs(const float* zs, int64_t ldz, int nslab, int64_
                                  int64_t ld_next, int* done, hipStream_t s) {
     if (M < 1 || M > 32 || nslab < 1) return -2;
     if (B <= 0) return 0;
-    hipLaunchKernelGGL(mdn_sample_slabs_kernel, dim3(B), dim3(64), 0, s, zs, ldz, nslab, slab, bias, 3 + 6 * M, M,
+    hipLaunchKernelGGL(mdn_sample_slabs_kernel, dim3(B), dim3(256), 0, s, zs, ldz, nslab, slab, bias, 3 + 6 * M, M,
                        mode, temp, greedy, fix_pen, seed, step, row0, out_row, ld_out, next_x, ld_next, done);
     return SKR_CHECK_LAUNCH();
 }

@@ -57,16 +57,19 @@ def main():
         lstm.flatten_parameters()
         state = None
 
+        amp = a.dtype == "bf16"   # bf16 comparator: MIOpen LSTM + head under autocast, fp32 master weights
+
         def step(x, y):
             nonlocal state
             opt.zero_grad()
-            out, st = lstm(x, state)
-            out = torch.nn.functional.dropout(out, 1 - cfg.keep_prob)
-            z = head(out.reshape(-1, cfg.rnn_size))
-            cost = mdn_loss_torch(z, y.reshape(-1, 5), cfg.num_mixture, mode="reference")[0]
+            with torch.autocast("cuda", dtype=torch.bfloat16, enabled=amp):
+                out, st = lstm(x, state)
+                out = torch.nn.functional.dropout(out, 1 - cfg.keep_prob)
+                z = head(out.reshape(-1, cfg.rnn_size))
+            cost = mdn_loss_torch(z.float(), y.reshape(-1, 5), cfg.num_mixture, mode="reference")[0]
             cost.backward()
             opt.step()
-            state = tuple(s.detach() for s in st)
+            state = tuple(s.detach().float() for s in st)
             return cost
     else:
         tr = ReferenceTrainer(cfg, loader, device=dev, log=lambda s: None)
