@@ -275,6 +275,17 @@ class GemmProblem(C.Structure):
     ]
 
 
+class GemmProblem8(C.Structure):
+    """Mirror of ``GemmProblem8`` in csrc/skinny_gemm.hip (fp8 v2 products)."""
+    _fields_ = [
+        ("A", _p), ("lda", _i64),
+        ("Bt", _p), ("ldb", _i64),
+        ("b_scale", _p), ("a_scale", _f),
+        ("C", _p), ("ldc", _i64), ("c_slab", _i64),
+        ("M", _i), ("N", _i), ("K", _i), ("splits", _i),
+    ]
+
+
 class HipLib:
     def __init__(self, lib: C.CDLL):
         self.lib = lib
@@ -341,6 +352,10 @@ class HipLib:
         lib.skr_lstm_wide_flag_words.restype = _i
         lib.skr_hyper_vec_fwd.argtypes = [_p, _i64, _p, _p, _p, _i64, _i64, _i, _i, _i, _p]
         lib.skr_hyper_vec_fwd.restype = _i
+        lib.skr_skinny_gemm_fp8_v2.argtypes = [C.POINTER(GemmProblem8), _i, _p]
+        lib.skr_skinny_gemm_fp8_v2.restype = _i
+        lib.skr_skinny_gemm_group_fp8.argtypes = [C.POINTER(GemmProblem8), _i, _p]
+        lib.skr_skinny_gemm_group_fp8.restype = _i
         lib.skr_decode_ref.argtypes = [C.POINTER(DecArgs), _p]
         lib.skr_decode_ref.restype = _i
         lib.skr_stream_create_cumask.argtypes = [_i, _i, _i, C.POINTER(_p)]
@@ -358,7 +373,8 @@ class HipLib:
                           ("skr_mdn_head_dx_args_size", HeadDx),
                           ("skr_mdn_head_dw_args_size", HeadDw),
                           ("skr_decode_ref_args_size", DecArgs),
-                          ("skr_gemm_problem_size", GemmProblem)):
+                          ("skr_gemm_problem_size", GemmProblem),
+                          ("skr_gemm_problem8_size", GemmProblem8)):
             fn = getattr(lib, name)
             fn.restype = _i
             if fn() != C.sizeof(cls):

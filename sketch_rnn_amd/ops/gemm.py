@@ -268,6 +268,41 @@ def rec_gemm_fp8(a8: torch.Tensor, bq, out: torch.Tensor, splits: int, bn: int =
     return out
 
 
+def _problem8(p, a8, bq, out, splits):
+    q, scale = bq
+    p.A, p.lda, p.Bt, p.ldb = a8.data_ptr(), a8.stride(0), q.data_ptr(), q.stride(0)
+    p.b_scale, p.a_scale = scale.data_ptr(), 1.0 / FP8_ACT_SCALE
+    p.C, p.ldc, p.c_slab = out.data_ptr(), out.stride(-2), out.stride(0) if out.dim() == 3 else 0
+    p.M, p.N, p.K, p.splits = a8.shape[0], q.shape[0], a8.shape[1], max(splits, 1)
+
+
+def rec_gemm_fp8_v2(a8: torch.Tensor, bq, out: torch.Tensor, splits: int) -> torch.Tensor:
+    """fp8 v2 ring (csrc/skinny_gemm.hip ``skr_skinny_gemm_fp8_v2``, M <= 128):
+    ``out [S, M, N]`` fp32 slabs, or ``out [M, N]`` bf16 (one slab)."""
+    from ..utils import native
+    from ._hipapi import GemmProblem8
+    lib = native.require_hip()
+    p = GemmProblem8()
+    _problem8(p, a8, bq, out, splits)
+    rc = lib.lib.skr_skinny_gemm_fp8_v2(p, int(out.dtype == _BF16), torch.cuda.current_stream().cuda_stream)
+    if rc != 0:
+        raise RuntimeError("skr_skinny_gemm_fp8_v2 failed (%d)" % rc)
+    return out
+
+
+def rec_gemm_fp8_group(jobs) -> None:
+    """Independent fp8 products ``(a8, bq, out [S, M, N] fp32, splits)`` in one launch."""
+    from ..utils import native
+    from ._hipapi import GemmProblem8
+    lib = native.require_hip()
+    probs = (GemmProblem8 * len(jobs))()
+    for p, (a8, bq, out, s) in zip(probs, jobs):
+        _problem8(p, a8, bq, out, s)
+    rc = lib.lib.skr_skinny_gemm_group_fp8(probs, len(jobs), torch.cuda.current_stream().cuda_stream)
+    if rc != 0:
+        raise RuntimeError("skr_skinny_gemm_group_fp8 failed (%d)" % rc)
+
+
 class _Linear(torch.autograd.Function):
     """``x @ W + b`` in the compute precision with fp32 outputs/grads."""
 

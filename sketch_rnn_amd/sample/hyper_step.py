@@ -21,6 +21,11 @@ seven kernels, all hand-written:
    input.
 
 Rows are processed in chunks of at most 128 (one MFMA row tile).
+
+Compute dtype ``fp8`` (BASELINE config 5): the four GEMMs run on OCP e4m3
+operands (``v_mfma_f32_16x16x32_fp8_fp8``, per-output-column weight scales;
+the cells write the bf16-free operand buffer as e4m3 x 64 -- |h| <= 1, so a
+static scale maps it onto [-64, 64] with subnormals down to ~3e-5).
 """
 from __future__ import annotations
 
@@ -41,7 +46,7 @@ def hyper_step_ok(model, B: int) -> bool:
     if next(model.parameters()).device.type != "cuda" or gemm.lp_dtype() != torch.bfloat16:
         return False
     from ..ops import get_compute_dtype
-    if get_compute_dtype() != "bf16" or not model.dec.use_layer_norm:
+    if get_compute_dtype() not in ("bf16", "fp8") or not model.dec.use_layer_norm:
         return False
     H, Hh = cfg.dec_rnn_size, cfg.hyper_num_units
     return B <= 128 and H % 64 == 0 and Hh % 64 == 0 and cfg.num_mixture <= 32
@@ -61,12 +66,19 @@ class HyperStepDecoder:
         self.nout = 3 + 6 * self.M
         self.E = p.embed
         bf, f32 = torch.bfloat16, torch.float32
-        self.S_m = gemm.plan_splits(B, G, H, 1, bf)
-        self.S_y = gemm.plan_splits(B, Gh, K, 1, bf)
-        self.S_o = gemm.plan_splits(B, 128, H, 1, bf)
+        from ..ops import get_compute_dtype
+        self.fp8 = get_compute_dtype() == "fp8"
+        if self.fp8:
+            self.S_m = gemm.plan_splits_fp8(B, G, H)
+            self.S_y = gemm.plan_splits_fp8(B, Gh, K)
+            self.S_o = gemm.plan_splits_fp8(B, 128, H)
+        else:
+            self.S_m = gemm.plan_splits(B, G, H, 1, bf)
+            self.S_y = gemm.plan_splits(B, Gh, K, 1, bf)
+            self.S_o = gemm.plan_splits(B, 128, H, 1, bf)
         assert min(self.S_m, self.S_y, self.S_o) >= 1
         # state / operand buffers (resident for the whole decode)
-        self.A = torch.zeros(B, K, dtype=bf, device=device)          # [h | hh] bf16 GEMM operand
+        self.A = torch.zeros(B, K, dtype=torch.uint8 if self.fp8 else bf, device=device)   # [h | hh] GEMM operand
         self.CC = torch.zeros(B, H, dtype=f32, device=device)
         self.HCC = torch.zeros(B, Hh, dtype=f32, device=device)
         self.Hout = torch.empty(B, H, dtype=f32, device=device)
@@ -101,7 +113,7 @@ class HyperStepDecoder:
             Wt[: W.shape[1]] = W.t().to(dt)
             return Wt
 
-        return dict(
+        w = dict(
             WhT=gemm.derived(p.W_h, "hypWhT%s" % dt, lambda W: W.to(dt).t().contiguous()),
             WyT=gemm.derived((p.hyp_W_x, p.hyp_W_h), "hypWyT%s" % dt, wy),
             PQ=gemm.derived((p.W_z, p.b_z, p.W_a), "hypP%s" % dt, fold),
@@ -110,6 +122,12 @@ class HyperStepDecoder:
             WoT=gemm.derived(m.output_w, "stepWoT", wout),
             bo=m.output_b.detach().float().contiguous(),
         )
+        if self.fp8:   # per-output-column e4m3 weights
+            w["WhT"] = gemm.derived(w["WhT"], "q8", gemm.quantize_fp8_rows)
+            w["WyT"] = gemm.derived(w["WyT"], "q8", gemm.quantize_fp8_rows)
+            w["PQ"] = (gemm.derived(w["PQ"][0], "q8", gemm.quantize_fp8_rows), w["PQ"][1])
+            w["WoT"] = gemm.derived(w["WoT"], "q8", gemm.quantize_fp8_rows)
+        return w
 
     @torch.no_grad()
     def begin(self, zc, state) -> None:
@@ -117,8 +135,13 @@ class HyperStepDecoder:
         p = self.model.dec
         H = self.H
         h0, c0, hh0, hc0 = state
-        self.A[:, :H].copy_(h0)
-        self.A[:, H:].copy_(hh0)
+        if self.fp8:
+            from ..ops.recurrent import _to_fp8_act
+            self.A[:, :H].copy_(_to_fp8_act(h0))
+            self.A[:, H:].copy_(_to_fp8_act(hh0))
+        else:
+            self.A[:, :H].copy_(h0)
+            self.A[:, H:].copy_(hh0)
         self.CC.copy_(c0)
         self.HCC.copy_(hc0)
         if zc is not None:
@@ -144,7 +167,8 @@ class HyperStepDecoder:
         ah.forget_bias, ah.keep = 1.0, 1.0
         ah.seed, ah.stream, ah.step = self.sd.data_ptr(), 1, t
         ah.c_prev, ah.c_carry, ah.h_out = self.HCC.data_ptr(), self.HCC.data_ptr(), self.HH.data_ptr()
-        ah.h_lp, ah.ld_lp, ah.lp_kind = self.A[:, H:].data_ptr(), K, 1
+        lpk = 3 if self.fp8 else 1
+        ah.h_lp, ah.ld_lp, ah.lp_kind = self.A[:, H:].data_ptr(), K, lpk
         self.clh.set(ah, t)
         am = LstmFwdArgs()
         am.B, am.H = B, H
@@ -157,7 +181,7 @@ class HyperStepDecoder:
         am.forget_bias, am.keep = 1.0, 1.0
         am.seed, am.stream, am.step = self.sd.data_ptr(), 0, t
         am.c_prev, am.c_carry, am.h_out = self.CC.data_ptr(), self.CC.data_ptr(), self.Hout.data_ptr()
-        am.h_lp, am.ld_lp, am.lp_kind = self.A.data_ptr(), K, 1
+        am.h_lp, am.ld_lp, am.lp_kind = self.A.data_ptr(), K, lpk
         self.clm.set(am, t)
         return ah, am
 
@@ -174,12 +198,15 @@ class HyperStepDecoder:
                                     1, B, 5, G + Gh, st)
         if rc != 0:
             raise RuntimeError("skr_bproj_fwd failed (%d)" % rc)
-        gemm.rec_gemm_group([(self.A[:, :H], w["WhT"], self.RM, self.S_m), (self.A, w["WyT"], self.RY, self.S_y)])
+        f8 = self.fp8
+        jobs = [(self.A[:, :H], w["WhT"], self.RM, self.S_m), (self.A, w["WyT"], self.RY, self.S_y)]
+        (gemm.rec_gemm_fp8_group if f8 else gemm.rec_gemm_group)(jobs)
         ah, am = self._cell_args(t)
         if self.lib.skr_lstm_fwd_step(ctypes.byref(ah), 1, 0, st) != 0:
             raise RuntimeError("hyper cell step failed")
-        gemm.rec_gemm_bf16out(self.A[:, H:], w["PQ"][0], self.VEC)
+        (gemm.rec_gemm_fp8_v2(self.A[:, H:], w["PQ"][0], self.VEC, 1) if f8 else
+         gemm.rec_gemm_bf16out(self.A[:, H:], w["PQ"][0], self.VEC))
         if self.lib.skr_lstm_fwd_step(ctypes.byref(am), 1, 2, st) != 0:
             raise RuntimeError("main cell step failed")
-        gemm.rec_gemm(self.A[:, :H], w["WoT"], self.ZS, self.S_o)
+        (gemm.rec_gemm_fp8_v2 if f8 else gemm.rec_gemm)(self.A[:, :H], w["WoT"], self.ZS, self.S_o)
         sample(self.ZS, 128, self.S_o, B * 128, w["bo"])
