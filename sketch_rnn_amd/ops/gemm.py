@@ -268,6 +268,42 @@ def rec_gemm_fp8(a8: torch.Tensor, bq, out: torch.Tensor, splits: int, bn: int =
     return out
 
 
+def cast_transpose(W: torch.Tensor, plain: Optional[torch.Tensor] = None, trans: Optional[torch.Tensor] = None,
+                   want_plain: bool = True, want_trans: bool = True):
+    """fp32 ``W [..., R, C]`` -> bf16 ``W`` and bf16 ``W^T [..., C, R]`` in one
+    pass (csrc/convert.hip). ``plain`` / ``trans`` may be given (views into
+    larger buffers: row-strided, e.g. a column slice of a concatenated B^T);
+    returns ``(plain, trans)``. CPU tensors / fp32 compute: torch ops."""
+    R, C = W.shape[-2], W.shape[-1]
+    nb = W.numel() // (R * C) if W.numel() else 0
+    lead = W.shape[:-2]
+    if plain is None and want_plain:
+        plain = torch.empty(*lead, R, C, dtype=_BF16, device=W.device)
+    if trans is None and want_trans:
+        trans = torch.empty(*lead, C, R, dtype=_BF16, device=W.device)
+    Wc = W.detach()
+    sb = lambda t: (t.stride(-3) if t.dim() >= 3 else 0) if t is not None else 0   # noqa: E731
+    # the kernel's vector loads / stores need rows (and batches) in multiples of 4 elements
+    vec_ok = all(t is None or (t.stride(-1) == 1 and t.stride(-2) % 4 == 0 and sb(t) % 4 == 0
+                               and t.data_ptr() % (16 if t is Wc else 8) == 0) for t in (Wc, plain, trans))
+    if not Wc.is_cuda or Wc.dtype != torch.float32 or not vec_ok:
+        if plain is not None:
+            plain.copy_(Wc)
+        if trans is not None:
+            trans.copy_(Wc.transpose(-1, -2))
+        return plain, trans
+    from ..utils import native
+    lib = native.require_hip()
+    rc = lib.lib.skr_cast_transpose_bf16(
+        Wc.data_ptr(), Wc.stride(-2), sb(Wc), R, C, max(nb, 1),
+        plain.data_ptr() if plain is not None else None, plain.stride(-2) if plain is not None else 0, sb(plain),
+        trans.data_ptr() if trans is not None else None, trans.stride(-2) if trans is not None else 0, sb(trans),
+        torch.cuda.current_stream().cuda_stream)
+    if rc != 0:
+        raise RuntimeError("skr_cast_transpose_bf16 failed (%d) for %s" % (rc, tuple(W.shape)))
+    return plain, trans
+
+
 def _problem8(p, a8, bq, out, splits):
     q, scale = bq
     p.A, p.lda, p.Bt, p.ldb = a8.data_ptr(), a8.stride(0), q.data_ptr(), q.stride(0)

@@ -80,12 +80,16 @@ class _PersistLSTM(torch.autograd.Function):
         Wh = [W_h0] + ([W_h1] if L == 2 else [])
         h0s = [h0a.contiguous()] + ([h0b.contiguous()] if L == 2 else [])
         c0s = [c0a.contiguous()] + ([c0b.contiguous()] if L == 2 else [])
-        Wl = [gemm.lp(W).reshape(-1, H, G).contiguous() for W in Wh]          # [nd, H, 4H] (backward B^T)
-        WT = [Wl[0].transpose(1, 2).contiguous()]                              # [nd, 4H, H]
+        # bf16 operands in both layouts, one pass per weight (csrc/convert.hip)
+        Wl0, WT0 = gemm.cast_transpose(W_h0.reshape(-1, H, G))                 # [nd, H, 4H] (backward B^T), [nd, 4H, H]
+        Wl, WT = [Wl0], [WT0]
         Wu = None
         if L == 2:
-            Wu = gemm.lp(W_in1).contiguous()                                    # [H, 4H]
-            WT.append(torch.cat([Wu, Wl[1][0]], 0).t().contiguous())           # [4H, 2H]: [W_in | W_h] per column
+            WT1 = torch.empty(G, 2 * H, dtype=bf, device=dev)                  # [4H, 2H]: [W_in | W_h] per column
+            Wu, _ = gemm.cast_transpose(W_in1, trans=WT1[:, :H])               # [H, 4H]
+            Wl1, _ = gemm.cast_transpose(W_h1, trans=WT1[:, H:])
+            Wl.append(Wl1.reshape(1, H, G))
+            WT.append(WT1)
         rst = reset.contiguous().to(f32) if reset is not None else None
         sd = _seed_tensor(seed, dev)
         b1c = b1.contiguous().to(f32) if L == 2 else None

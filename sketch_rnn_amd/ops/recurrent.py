@@ -690,6 +690,17 @@ class _HyperSeq(torch.autograd.Function):
             WyT = gemm.derived((hW_x, hW_h), "hypWyT%s" % dt, lambda a, b: wy(a, b).t().contiguous())
             PlT, q = gemm.derived((W_z, b_z, W_a), "hypP%s" % dt,
                                   lambda a, b, c: (lambda P, q: (P.t().contiguous(), q))(*fold(a, b, c)))
+        elif dt == torch.bfloat16 and W_h.is_cuda:
+            # both bf16 layouts of each weight in one pass (csrc/convert.hip)
+            Whl, WhT = gemm.cast_transpose(W_h)  # [H, G]: B^T of dR_main @ W_h^T; [G, H]: B^T of h @ W_h
+            Wyl = torch.empty(K, Gh, dtype=dt, device=dev)
+            WyT = torch.empty(Gh, K, dtype=dt, device=dev)
+            gemm.cast_transpose(hW_x[IN:], Wyl[:H], WyT[:, :H])
+            gemm.cast_transpose(hW_h, Wyl[H:], WyT[:, H:])
+            Wz3 = W_z.view(Hh, 12, E).permute(1, 0, 2)
+            Pf = torch.bmm(Wz3, W_a).permute(1, 0, 2).reshape(Hh, 12 * H)
+            q = torch.bmm(b_z.view(12, 1, E), W_a).reshape(12, H).contiguous()
+            Pl, PlT = gemm.cast_transpose(Pf)    # B^T for the backward dvec @ P^T / the forward hh @ P
         else:
             Whl = gemm.lp(W_h).contiguous()      # [H, G]: B^T of dR_main @ W_h^T
             WhT = Whl.t().contiguous()           # [G, H]: B^T of h @ W_h

@@ -662,3 +662,23 @@ def test_inference_weight_cache_tracks_graph_training():
         ops.set_backend("auto")
     assert e1["cost"] != e0["cost"]
     assert abs(e1["cost"] - e_ref["cost"]) < 0.05 * abs(e_ref["cost"]) + 0.02, (e1, e_ref)
+
+
+@pytest.mark.parametrize("shape", [(2048, 8192), (2, 512, 2048), (133, 1000), (37, 61)])
+def test_cast_transpose_matches_torch(shape):
+    """csrc/convert.hip: both bf16 layouts bit-equal to torch's cast / transpose,
+    including ragged edges and strided destinations."""
+    from sketch_rnn_amd.ops import gemm
+    torch.manual_seed(1)
+    W = torch.randn(*shape, device=DEV)
+    plain, trans = gemm.cast_transpose(W)
+    torch.cuda.synchronize()
+    assert torch.equal(plain, W.to(torch.bfloat16))
+    assert torch.equal(trans, W.to(torch.bfloat16).transpose(-1, -2))
+    if len(shape) == 2 and shape[1] % 4 == 0 and shape[0] % 4 == 0:
+        R, C = shape
+        big = torch.zeros(C, R + 64, dtype=torch.bfloat16, device=DEV)
+        gemm.cast_transpose(W, trans=big[:, 64:], want_plain=False)
+        torch.cuda.synchronize()
+        assert torch.equal(big[:, 64:], W.to(torch.bfloat16).t())
+        assert torch.count_nonzero(big[:, :64]) == 0
