@@ -75,6 +75,19 @@ def hash_normal(seed, stream: int, step: int, shape, device=None) -> torch.Tenso
     VAE's reparameterisation noise, a pure function of (seed, stream, step)
     like the dropout masks -- independent of any process-global RNG state,
     so a step replays identically (HIP graphs, resume, two fresh runs)."""
+    if torch.is_tensor(seed) and seed.is_cuda and seed.dtype == torch.int64:
+        from ..utils import native
+        lib = native.hip_lib()
+        if lib is not None:   # one kernel (csrc/noise.hip) instead of ~40 int64 torch ops
+            n = 1
+            for s_ in shape:
+                n *= s_
+            out = torch.empty(*shape, device=seed.device, dtype=torch.float32)
+            rc = lib.lib.skr_hash_normal(seed.data_ptr(), stream & _M32, step & _M32, out.data_ptr(), n,
+                                         torch.cuda.current_stream(seed.device).cuda_stream)
+            if rc != 0:
+                raise RuntimeError("skr_hash_normal failed (%d)" % rc)
+            return out
     u1 = 1.0 - hash_uniform(seed, stream, step, shape, device)        # (0, 1]
     u2 = hash_uniform(seed, stream + 0x3C6EF372, step, shape, device)
     return torch.sqrt(-2.0 * torch.log(u1)) * torch.cos((2.0 * math.pi) * u2)

@@ -358,6 +358,8 @@ class HipLib:
         lib.skr_skinny_gemm_group_fp8.restype = _i
         lib.skr_cast_transpose_bf16.argtypes = [_p, _i64, _i64, _i, _i, _i, _p, _i64, _i64, _p, _i64, _i64, _p]
         lib.skr_cast_transpose_bf16.restype = _i
+        lib.skr_hash_normal.argtypes = [_p, _u32, _u32, _p, _i64, _p]
+        lib.skr_hash_normal.restype = _i
         lib.skr_decode_ref.argtypes = [C.POINTER(DecArgs), _p]
         lib.skr_decode_ref.restype = _i
         lib.skr_stream_create_cumask.argtypes = [_i, _i, _i, C.POINTER(_p)]

@@ -682,3 +682,15 @@ def test_cast_transpose_matches_torch(shape):
         torch.cuda.synchronize()
         assert torch.equal(big[:, 64:], W.to(torch.bfloat16).t())
         assert torch.count_nonzero(big[:, :64]) == 0
+
+
+def test_hash_normal_kernel_matches_torch_emulation():
+    """csrc/noise.hip (device-seed path of models.cells.hash_normal) against the
+    int64 torch emulation of the same hash streams."""
+    from sketch_rnn_amd.models import cells as C
+    seed = torch.tensor([12345], dtype=torch.int64, device=DEV)
+    k = C.hash_normal(seed, 0x5E, 3, (100, 128))
+    t = C.hash_normal(12345, 0x5E, 3, (100, 128), device=DEV)
+    torch.cuda.synchronize()
+    assert torch.allclose(k, t, rtol=1e-5, atol=1e-5)
+    assert abs(float(k.mean())) < 0.05 and abs(float(k.std()) - 1.0) < 0.05
