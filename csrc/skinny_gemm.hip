@@ -690,6 +690,113 @@ __global__ __launch_bounds__(256) void skinny_gemm_fp8v2_kernel(const uint8_t* _
                                  blockIdx.x * BN, (int64_t)blockIdx.y * kslice, kslice, smem8);
 }
 
+// fp32 operands (fp32 parity runs): the same LDS-DMA ring with K-tiles of
+// 32 floats (128-byte LDS rows, same chunk swizzle), v_mfma_f32_16x16x4_f32.
+// An MFMA consumes one k per lane group, so a lane reads a float4 of its row
+// (chunk fq or fq + 4 of the tile) and feeds its four elements to four
+// MFMAs: MFMA (g, j) covers k = 16g + 4fq + j -- a permutation of the
+// tile's 32 k shared by A and B, so every product term is summed once.
+constexpr int BKF = 32;
+
+template <int BN, int NS>
+__device__ __forceinline__ void glds_tile_f32(const float* __restrict__ A, int64_t lda, const float* __restrict__ Bt,
+                                              int64_t ldb, float* __restrict__ C, int64_t ldc, int M, int n0,
+                                              int64_t k0, int kslice, float* smem) {
+    constexpr int NJ = BN / 16;
+    constexpr int A_CH = BM / 8, B_CH = BN / 8;     // 1-KiB chunks (8 rows x 128 B) per tile
+    constexpr int GPW = (A_CH + B_CH) / 4;
+    constexpr int TILE = (BM + BN) * BKF;           // floats per stage
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int n = kslice / BKF;
+    const int r8 = lane >> 3, slot = lane & 7;
+    const float* asrc[A_CH / 4];
+    const float* bsrc[B_CH / 4];
+#pragma unroll
+    for (int i = 0; i < A_CH / 4; ++i) {
+        const int row = (w + 4 * i) * 8 + r8;
+        const int kc = slot ^ ((row >> 1) & 7);
+        asrc[i] = row < M ? A + (int64_t)row * lda + k0 + kc * 4 : A + (int64_t)(M - 1) * lda + k0;
+    }
+#pragma unroll
+    for (int i = 0; i < B_CH / 4; ++i) {
+        const int row = (w + 4 * i) * 8 + r8;
+        const int kc = slot ^ ((row >> 1) & 7);
+        bsrc[i] = Bt + (int64_t)(n0 + row) * ldb + k0 + kc * 4;
+    }
+    auto issue = [&](int kt) {
+        float* st = smem + (kt % NS) * TILE;
+        const int64_t ko = (int64_t)kt * BKF;
+#pragma unroll
+        for (int i = 0; i < A_CH / 4; ++i)
+            __builtin_amdgcn_global_load_lds((const void*)(asrc[i] + ko),
+                                             (__attribute__((address_space(3))) void*)(st + (w + 4 * i) * 256), 16, 0, 0);
+#pragma unroll
+        for (int i = 0; i < B_CH / 4; ++i)
+            __builtin_amdgcn_global_load_lds((const void*)(bsrc[i] + ko),
+                                             (__attribute__((address_space(3))) void*)(st + BM * BKF + (w + 4 * i) * 256),
+                                             16, 0, 0);
+    };
+    f32x4 acc[2][NJ];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const int fr = lane & 15, fq = lane >> 4;
+#pragma unroll
+    for (int p = 0; p < NS - 1; ++p)
+        if (p < n) issue(p);
+    for (int kt = 0; kt < n; ++kt) {
+        wait_ahead<GPW, NS>(min(n - 1 - kt, NS - 2));
+        __builtin_amdgcn_s_barrier();
+        if (kt + NS - 1 < n) issue(kt + NS - 1);
+        const float* As = smem + (kt % NS) * TILE;
+        const float* Bs = As + BM * BKF;
+#pragma unroll
+        for (int g = 0; g < 2; ++g) {
+            const int kc = fq + 4 * g;
+            f32x4 af[2], bfr[NJ];
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                const int row = 32 * w + 16 * i + fr;
+                af[i] = *(const f32x4*)(&As[row * BKF + ((kc ^ ((row >> 1) & 7)) * 4)]);
+            }
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) {
+                const int row = 16 * j + fr;
+                bfr[j] = *(const f32x4*)(&Bs[row * BKF + ((kc ^ ((row >> 1) & 7)) * 4)]);
+            }
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+#pragma unroll
+                for (int i = 0; i < 2; ++i)
+#pragma unroll
+                    for (int j = 0; j < NJ; ++j)
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i][e], bfr[j][e], acc[i][j], 0, 0, 0);
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int row = 32 * w + 16 * i + fq * 4 + e;
+                if (row < M) C[row * ldc + n0 + 16 * j + fr] = acc[i][j][e];
+            }
+}
+
+template <int BN, int NS>
+__global__ __launch_bounds__(256) void skinny_gemm_f32_kernel(const float* __restrict__ A, int64_t lda,
+                                                              int64_t a_batch, const float* __restrict__ Bt,
+                                                              int64_t ldb, int64_t b_batch, float* __restrict__ C,
+                                                              int64_t ldc, int64_t c_slab, int64_t c_batch, int M,
+                                                              int kslice) {
+    extern __shared__ __attribute__((aligned(16))) float smemf[];
+    glds_tile_f32<BN, NS>(A + blockIdx.z * a_batch, lda, Bt + blockIdx.z * b_batch, ldb,
+                          C + blockIdx.z * c_batch + blockIdx.y * c_slab, ldc, M, blockIdx.x * BN,
+                          (int64_t)blockIdx.y * kslice, kslice, smemf);
+}
+
 }  // namespace
 
 // C[z][s] (slab s of batch z) = A[z][:, s*kslice:(s+1)*kslice] . Bt[z][:, same]^T
@@ -833,6 +940,23 @@ SKR_API int skr_skinny_gemm_group(const GemmProblem* probs, int n, int bn, hipSt
     if (bn == 128) return g_nstage == 3 ? launch_group<128, 3>(g, s) : launch_group<128, 4>(g, s);
     return g_nstage == 3 ? launch_group<64, 3>(g, s) : g_nstage == 6 ? launch_group<64, 6>(g, s)
                                                                     : launch_group<64, 4>(g, s);
+}
+
+// fp32 operands: same contract as skr_skinny_gemm_v2 with kslice % 32 == 0
+// (64-wide N tiles, 3-deep ring of (128 + 64) x 128 B stages).
+SKR_API int skr_skinny_gemm_f32(const void* A, int64_t lda, int64_t a_batch, const void* Bt, int64_t ldb,
+                                int64_t b_batch, float* C, int64_t ldc, int64_t c_slab, int64_t c_batch, int M, int N,
+                                int K, int splits, int batch, hipStream_t s) {
+    if (M < 1 || M > BM || N % 64 != 0 || splits < 1 || K % splits != 0) return -2;
+    const int kslice = K / splits;
+    if (kslice % BKF != 0 || lda % 4 != 0 || ldb % 4 != 0) return -3;
+    if (((uintptr_t)A | (uintptr_t)Bt) & 15) return -4;
+    const dim3 grid(N / 64, splits, batch);
+    const size_t lds = (size_t)3 * (BM + 64) * BKF * 4;
+    set_lds_attr(skinny_gemm_f32_kernel<64, 3>, lds);
+    hipLaunchKernelGGL((skinny_gemm_f32_kernel<64, 3>), grid, dim3(256), lds, s, (const float*)A, lda, a_batch,
+                       (const float*)Bt, ldb, b_batch, C, ldc, c_slab, c_batch, M, kslice);
+    return SKR_CHECK_LAUNCH();
 }
 
 SKR_API int skr_gemm_problem_size() { return (int)sizeof(GemmProblem); }

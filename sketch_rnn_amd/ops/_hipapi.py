@@ -302,6 +302,9 @@ class HipLib:
         for fn in (lib.skr_skinny_gemm, lib.skr_skinny_gemm_v2):
             fn.argtypes = [_p, _i64, _i64, _p, _i64, _i64, _p, _i64, _i64, _i64, _i, _i, _i, _i, _i, _i, _p]
             fn.restype = _i
+        lib.skr_skinny_gemm_f32.argtypes = [_p, _i64, _i64, _p, _i64, _i64, _p, _i64, _i64, _i64, _i, _i, _i, _i, _i,
+                                             _p]
+        lib.skr_skinny_gemm_f32.restype = _i
         lib.skr_skinny_gemm_fp8.argtypes = [_p, _i64, _i64, _p, _i64, _i64, _p, _i64, _f, _p, _i64, _i64, _i64,
                                              _i, _i, _i, _i, _i, _i, _p]
         lib.skr_skinny_gemm_fp8.restype = _i

@@ -89,16 +89,24 @@ def row_blocks(M: int) -> int:
     return M // 128 if M % 128 == 0 and M <= 1024 else 0
 
 
+# fp32 operands (fp32 parity runs) through the fp32 MFMA skinny kernel
+# (csrc/skinny_gemm.hip skr_skinny_gemm_f32); SKR_GEMM_F32=0: library GEMMs.
+F32_GEMM = os.environ.get("SKR_GEMM_F32", "1") != "0"
+
+
 def plan_splits(M: int, N: int, K: int, batch: int = 1, dtype: torch.dtype = _BF16, max_splits: int = 32) -> int:
     """Split-K factor for :func:`rec_gemm`: aim for 256-512 workgroups.
     Returns 0 when the native skinny kernel cannot take the shape."""
     mb = row_blocks(M)
-    if dtype != _BF16 or mb == 0 or (mb > 1 and batch > 1) or N % 64 or K % 64:
+    kt = 64 if dtype == _BF16 else 32            # K-tile of the bf16 / fp32 ring
+    if dtype not in (_BF16, torch.float32) or (dtype == torch.float32 and not F32_GEMM):
+        return 0
+    if mb == 0 or (mb > 1 and batch > 1) or N % 64 or K % kt:
         return 0
     tiles = (N // 64) * batch * mb
     best = 1
     for s in _SPLITS:
-        if s > max_splits or (K // 64) % s:
+        if s > max_splits or (K // kt) % s:
             continue
         if tiles * s > 512:
             break
@@ -127,7 +135,11 @@ def rec_gemm(a: torch.Tensor, bt: torch.Tensor, out: torch.Tensor, splits: int, 
         return out
     from ..utils import native
     lib = native.require_hip()
-    fn = lib.lib.skr_skinny_gemm_v2 if GEMM_ALGO == "v2" else lib.lib.skr_skinny_gemm
+    if a.dtype == torch.float32:   # fp32 ring: same arguments, no N-tile choice
+        f32 = lib.lib.skr_skinny_gemm_f32
+        fn = lambda *args: f32(*args[:-2], args[-1])   # noqa: E731  (drop bn)
+    else:
+        fn = lib.lib.skr_skinny_gemm_v2 if GEMM_ALGO == "v2" else lib.lib.skr_skinny_gemm
     if nd == 1 and M > 128:   # 128-row blocks as the kernel's batch dimension, sharing B
         mb = row_blocks(M)
         rc = fn(a.data_ptr(), a.stride(0), 128 * a.stride(0), bt.data_ptr(), bt.stride(-2), 0, out.data_ptr(), N,

@@ -694,3 +694,21 @@ def test_hash_normal_kernel_matches_torch_emulation():
     torch.cuda.synchronize()
     assert torch.allclose(k, t, rtol=1e-5, atol=1e-5)
     assert abs(float(k.mean())) < 0.05 and abs(float(k.std()) - 1.0) < 0.05
+
+
+@pytest.mark.parametrize("M,N,K,nd", [(100, 8192, 2048, 1), (37, 256, 24576, 1), (100, 2048, 512, 2), (256, 512, 1024, 1)])
+def test_skinny_gemm_f32_matches_torch(M, N, K, nd):
+    """fp32-operand skinny MFMA kernel (v_mfma_f32_16x16x4_f32) against an
+    fp64 reference: the fp32 parity path of every recurrence."""
+    from sketch_rnn_amd.ops import gemm
+    torch.manual_seed(7)
+    a = torch.randn(nd * M, K, device=DEV)
+    bt = torch.randn(nd, N, K, device=DEV) / math.sqrt(K)
+    S = gemm.plan_splits(M, N, K, nd, torch.float32)
+    assert S >= 1
+    out = torch.full((S, nd * M, N), float("nan"), device=DEV)
+    gemm.rec_gemm(a, bt if nd > 1 else bt[0], out, S, nd)
+    ref = torch.bmm(a.double().view(nd, M, K), bt.double().transpose(1, 2)).reshape(nd * M, N)
+    got = out.sum(0).double()
+    err = (got - ref).abs().max().item()
+    assert err <= 1e-5 * ref.abs().max().item() + 1e-5, (S, err)
