@@ -55,7 +55,11 @@ def hyper_step_ok(model, B: int) -> bool:
 class HyperStepDecoder:
     """In-place decoder state of B <= 128 rows + the per-step launch sequence."""
 
-    def __init__(self, model, B: int, device):
+    def __init__(self, model, B: int, device, cluster: bool = True):
+        """``cluster=False``: the main cell keeps each row in ONE workgroup (no
+        in-launch LayerNorm exchange), so this decoder can run on a stream
+        concurrent with another one's clustered cells without any
+        co-residency requirement."""
         self.lib = native.require_hip().lib
         cfg, p = model.cfg, model.dec
         self.model, self.B, self.dev = model, B, device
@@ -90,6 +94,8 @@ class HyperStepDecoder:
         self.ZP = torch.zeros(B, G + Gh, dtype=f32, device=device)   # per-sketch z projections
         self.ZS = torch.empty(self.S_o, B, 128, dtype=f32, device=device)
         self.clm = _ClusterSync(1, B, H, device)
+        if not cluster:
+            self.clm.C, self.clm.on = 1, False
         self.clh = _ClusterSync(1, B, Hh, device)
         self.sd = _seed_tensor(0, device)
 
@@ -130,8 +136,17 @@ class HyperStepDecoder:
         return w
 
     @torch.no_grad()
+    def prepare(self) -> None:
+        """(Re)derive the low-precision weight operands (cached per weight
+        version). Called by :meth:`begin`; callers running several decoders
+        on forked streams call it on the parent stream first."""
+        self._w = self._weights()
+
+    @torch.no_grad()
     def begin(self, zc, state) -> None:
         """Load the initial state and the per-sketch z projections."""
+        if getattr(self, "_w", None) is None:
+            self.prepare()
         p = self.model.dec
         H = self.H
         h0, c0, hh0, hc0 = state
@@ -189,8 +204,6 @@ class HyperStepDecoder:
     def step(self, x: torch.Tensor, t: int, sample) -> None:
         """One stroke: ``x [B, 5]`` (fp32, contiguous) -> decoder step -> head
         slabs -> ``sample(zs, ldz, nslab, slab, bias)`` (the caller's sampler)."""
-        if t == 0:
-            self._w = self._weights()
         w = self._w
         B, H, G, Gh = self.B, self.H, self.G, self.Gh
         st = torch.cuda.current_stream().cuda_stream

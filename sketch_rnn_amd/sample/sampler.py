@@ -255,21 +255,29 @@ class GraphDecoder:
         self.graph = None
         self.use_graph = use_graph and dev.type == "cuda"
 
+    _MAX_CHUNKS = 8          # concurrent 128-row step decoders (one HIP stream each)
+
     def _steppers(self):
         """Lean in-place HyperLSTM step decoders (``sample/hyper_step.py``), one
-        per chunk of <= 128 rows, when the model qualifies; else None."""
+        per chunk of <= 128 rows, when the model qualifies; else None.
+
+        Chunks run CONCURRENTLY, one stream each (captured as parallel graph
+        branches): each stroke's chain is latency-bound, so a second chain
+        fills the idle CUs. Only chunk 0's main cell uses the clustered
+        LayerNorm exchange (co-resident spin-waits); the others keep every
+        row in one workgroup, so no two spin-waiting launches ever compete
+        for residency."""
         if self.kind != "vae" or self.dev.type != "cuda" or os.environ.get("SKR_STEP_DECODER", "1") == "0":
             return None
         from .hyper_step import HyperStepDecoder, hyper_step_ok
         chunks = [(r0, min(128, self.B - r0)) for r0 in range(0, self.B, 128)]
-        # chunks run one after the other (their LayerNorm cells must not share
-        # the chip: co-resident spin exchange): measured on MI355X, vae_large,
-        # per decode step: B=128 0.067 ms, B=256 0.130 ms (generic path 0.169),
-        # B=1024 0.544 ms (generic path with 128-row GEMM blocks 0.297)
-        if len(chunks) > 2 or not all(hyper_step_ok(self.model, n) for _, n in chunks):
+        if len(chunks) > self._MAX_CHUNKS or not all(hyper_step_ok(self.model, n) for _, n in chunks):
             return None
         if getattr(self, "_stp", None) is None:
-            self._stp = [(r0, n, HyperStepDecoder(self.model, n, self.dev)) for r0, n in chunks]
+            # chunk 0 runs on whatever stream is current at decode time (None)
+            self._stp = [(r0, n, HyperStepDecoder(self.model, n, self.dev, cluster=(i == 0)),
+                          None if i == 0 else torch.cuda.Stream(device=self.dev))
+                         for i, (r0, n) in enumerate(chunks)]
         return self._stp
 
     @torch.no_grad()
@@ -282,23 +290,35 @@ class GraphDecoder:
         lab = self.labels if cfg.num_classes > 0 else None
         zc = model.condition(self.z if cfg.conditional else None, lab, B, self.dev)
         state = model.initial_state(zc, B, self.dev)
-        for r0, n, st in stp:
-            st.begin(zc[r0:r0 + n] if zc is not None else None, [s[r0:r0 + n] for s in state])
-        x = self.x0.clone()
+        x0 = self.x0.clone()
         ld_out = self.out.stride(0)
-        for t in range(N):
-            nx = torch.empty(B, 5, device=self.dev)
-            for r0, n, st in stp:
-                def sample(zs, ldz, nslab, slab, bias, r0=r0, n=n, t=t, nx=nx):
-                    rc = lib.skr_mdn_sample_slabs(
-                        zs.data_ptr(), ldz, nslab, slab, bias.data_ptr(), n, self.Mx, self.mode, self.temp,
-                        int(self.greedy), int(self.fix_pen), self.seed.data_ptr(), t, r0,
-                        self.out[r0, t].data_ptr(), ld_out, nx[r0].data_ptr(), 5, self.done[r0:].data_ptr(),
-                        ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
-                    if rc != 0:
-                        raise RuntimeError("skr_mdn_sample_slabs failed (%d)" % rc)
-                st.step(x[r0:r0 + n], t, sample)
-            x = nx
+        main = torch.cuda.current_stream(self.dev)
+        stp = [(r0, n, st, main if stream is None else stream) for r0, n, st, stream in stp]
+        for _, _, st, _ in stp:                  # weight operands on the parent stream
+            st.prepare()
+        for _, _, _, stream in stp:              # fork: inputs above are ready
+            if stream != main:
+                stream.wait_stream(main)
+        for r0, n, st, stream in stp:
+            with torch.cuda.stream(stream):
+                st.begin(zc[r0:r0 + n] if zc is not None else None, [s[r0:r0 + n] for s in state])
+                x = x0[r0:r0 + n].contiguous()
+                for t in range(N):
+                    nx = torch.empty(n, 5, device=self.dev)
+
+                    def sample(zs, ldz, nslab, slab, bias, r0=r0, n=n, t=t, nx=nx):
+                        rc = lib.skr_mdn_sample_slabs(
+                            zs.data_ptr(), ldz, nslab, slab, bias.data_ptr(), n, self.Mx, self.mode, self.temp,
+                            int(self.greedy), int(self.fix_pen), self.seed.data_ptr(), t, r0,
+                            self.out[r0, t].data_ptr(), ld_out, nx.data_ptr(), 5, self.done[r0:].data_ptr(),
+                            ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
+                        if rc != 0:
+                            raise RuntimeError("skr_mdn_sample_slabs failed (%d)" % rc)
+                    st.step(x, t, sample)
+                    x = nx
+        for _, _, _, stream in stp:
+            if stream != main:
+                main.wait_stream(stream)          # join
 
     @torch.no_grad()
     def _decode(self):
