@@ -24,6 +24,7 @@ Autograd boundaries are whole sequences, so no per-step autograd nodes exist.
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes
 import os
 from typing import Optional
@@ -625,6 +626,76 @@ def _split_override(var: str, planned: int, K: int) -> int:
     return v if v > 0 and planned > 0 and K % (64 * v) == 0 else planned
 
 
+def _hyper_proj_grads(dP1, s, Hh, H, E):
+    """Hyper-norm projection gradients from ``dP1 = [hh | 1]^T dvec``."""
+    dP = dP1[:Hh].view(Hh, 12, H).transpose(0, 1)                  # [12, Hh, H]
+    sV = dP1[Hh].view(12, H)                                       # column sums of dvec
+    Wz3 = s.W_z.view(Hh, 12, E).transpose(0, 1)                    # [12, Hh, E]
+    dW_z = torch.bmm(dP, s.W_a.transpose(1, 2)).transpose(0, 1).reshape(Hh, 12 * E)
+    dWa = torch.bmm(Wz3.transpose(1, 2), dP) + s.b_z.view(12, E, 1) * sV.view(12, 1, H)
+    db_z = torch.bmm(sV.view(12, 1, H), s.W_a.transpose(1, 2)).reshape(12 * E)
+    dbias = sV[8:].reshape(4 * H)                                  # shift-vector grads = bias grads
+    return dW_z, db_z, dWa, dbias
+
+
+class _DeferredWgrad:
+    """Deferred weight gradients (:func:`deferred_wgrad`): pending (stream,
+    keep-alive) pairs joined into the current stream at the context exit."""
+
+    def __init__(self):
+        self.active = False
+        self.pending = []
+
+    def add(self, stream, keep) -> None:
+        self.pending.append((stream, keep))
+
+    def join(self) -> None:
+        cur = torch.cuda.current_stream() if self.pending else None
+        for stream, _ in self.pending:
+            cur.wait_stream(stream)
+        self.pending = []
+
+
+_DEFER = _DeferredWgrad()
+_DEFER_STREAMS = {}
+# SKR_DEFER_WGRAD=1 turns the deferral on. OFF by default -- measured on
+# MI355X (vae_large, bench.py, 20 steps): 29.09 ms/step deferred vs 28.39
+# inline. The weight-gradient GEMM workgroups share the CUs of the
+# persistent encoder backward, whose per-step hand-offs are latency-bound,
+# and stretch it by more than the ~2 ms of GEMM work they hide.
+DEFER_ENABLED = os.environ.get("SKR_DEFER_WGRAD", "0") == "1"
+
+
+def _defer_stream(device):
+    key = str(device)
+    if key not in _DEFER_STREAMS:
+        _DEFER_STREAMS[key] = torch.cuda.Stream(device=device)
+    return _DEFER_STREAMS[key]
+
+
+@contextlib.contextmanager
+def deferred_wgrad():
+    """Inside this context the HyperLSTM backward returns its input-side
+    gradients at once and forms the weight / LayerNorm-parameter gradients
+    (the long-K GEMMs and column sums over every saved step, ~2 ms at
+    vae_large) on an auxiliary stream, overlapping the encoder's backward
+    that autograd runs next; the exit joins that stream into the current
+    one. The returned gradient tensors must not be READ before the exit
+    (autograd only assigns them to ``.grad`` when a parameter has none, as
+    in the trainers, which zero with ``set_to_none``)."""
+    if not DEFER_ENABLED or not torch.cuda.is_available():
+        yield
+        return
+    prev = _DEFER.active
+    _DEFER.active = True
+    try:
+        yield
+    finally:
+        _DEFER.active = prev
+        if not prev:
+            _DEFER.join()
+
+
 class _HyperSeq(torch.autograd.Function):
     """HyperLSTM layer (LN main cell modulated by a LN hyper cell).
 
@@ -951,6 +1022,36 @@ class _HyperSeq(torch.autograd.Function):
             wg.step_done(t)
         dh0 = DAY[:, :, :H].sum(0) + DAM.sum(0)
         dhh0 = DAY[:, :, H:].sum(0)
+        defer = _DEFER.active and wg.stream is None and s.bp
+        if defer:
+            # input-side gradients (needed by the encoder backward next) on the
+            # main stream; every weight / LayerNorm-parameter gradient on the
+            # deferred stream, overlapping whatever autograd runs next
+            S_m, P_m = bproj_reduce(s.x, dXH)
+            S_y, P_y = bproj_reduce(s.x, dRY_lp)
+            if s.zc is not None:
+                dW_x = torch.cat([P_m, s.zc.t() @ S_m], 0)
+                dhx_in = torch.cat([P_y, s.zc.t() @ S_y], 0)
+                dzc = S_m @ s.W_x[IX:].t() + S_y @ s.hW_x[IX:IN].t()
+            else:
+                dW_x, dhx_in, dzc = P_m, P_y, None
+            dx = None
+            aux = _defer_stream(dev)
+            aux.wait_stream(main)
+            with torch.cuda.stream(aux):
+                dW_h, dW_y, dP1, *cs = wwork(0, T)
+                dhW_x = torch.empty_like(s.hW_x)
+                dhW_x[IN:] = dW_y[:H]
+                dhW_x[:IN] = dhx_in
+                dhW_h = dW_y[H:]
+                g_ln, g_hln = cs[:4], cs[4:]
+                dW_z, db_z, dWa, dbias = _hyper_proj_grads(dP1, s, Hh, H, E)
+            # main-stream tensors the deferred work reads stay alive until the join
+            _DEFER.add(aux, (s, dRM_lp, dRY_lp, dVEC, HH1, DLNY, DLNCY, HDLNY, HDLNCY, dhx_in))
+            ctx.s = None
+            return (dx, dzc, dh0, dc_rec, dhh0, dhc_rec, None, dW_x, dW_h, dbias, dhW_x, dhW_h,
+                    g_hln[0], g_hln[1], g_hln[2], g_hln[3], dW_z, db_z, dWa, g_ln[0], g_ln[1], g_ln[2], g_ln[3],
+                    None)
         dW_h, dW_y, dP1, *cs = wg.finish()
         g_ln, g_hln = cs[:4], cs[4:]
         dhW_x = torch.empty_like(s.hW_x)
@@ -978,13 +1079,7 @@ class _HyperSeq(torch.autograd.Function):
                 dx, dzc = dxf[..., :IX], dxf[..., IX:].sum(0)
             else:
                 dx = dxf
-        dP = dP1[:Hh].view(Hh, 12, H).transpose(0, 1)                  # [12, Hh, H]
-        sV = dP1[Hh].view(12, H)                                       # column sums of dvec
-        Wz3 = s.W_z.view(Hh, 12, E).transpose(0, 1)                    # [12, Hh, E]
-        dW_z = torch.bmm(dP, s.W_a.transpose(1, 2)).transpose(0, 1).reshape(Hh, 12 * E)
-        dWa = torch.bmm(Wz3.transpose(1, 2), dP) + s.b_z.view(12, E, 1) * sV.view(12, 1, H)
-        db_z = torch.bmm(sV.view(12, 1, H), s.W_a.transpose(1, 2)).reshape(12 * E)
-        dbias = sV[8:].reshape(4 * H)                                  # shift-vector grads = bias grads
+        dW_z, db_z, dWa, dbias = _hyper_proj_grads(dP1, s, Hh, H, E)
         ctx.s = None
         return (dx, dzc, dh0, dc_rec, dhh0, dhc_rec, None, dW_x, dW_h, dbias, dhW_x, dhW_h,
                 g_hln[0], g_hln[1], g_hln[2], g_hln[3], dW_z, db_z, dWa, g_ln[0], g_ln[1], g_ln[2], g_ln[3], None)
