@@ -140,6 +140,9 @@ def main():
     sync()
     elapsed = time.perf_counter() - t0
     elapsed = dp.max_scalar(elapsed)
+    if device.startswith("cuda"):
+        from sketch_rnn_amd.train.trainer import check_device_faults
+        check_device_faults()   # a timed-out in-launch exchange invalidates the run: fail loudly
     cost = float(out["cost"])
     recon = None
     if not args.no_eval:

@@ -36,6 +36,9 @@ for s in "${steps[@]}"; do
         bench_noov) SKR_WGRAD_OVERLAP=0 run bench_noov 600 python bench.py --steps 10 --warmup 2 ;;
         bench_ch50) SKR_WGRAD_CHUNK=50 run bench_ch50 600 python bench.py --steps 10 --warmup 2 ;;
         bench_env) run "bench_${BENCH_TAG:-env}" 600 python bench.py --steps 10 --warmup 2 ;;
+        bench_split2) SKR_DEC_SPLIT=2 run bench_split2 600 python bench.py --steps 10 --warmup 2 ;;
+        bench_split3) SKR_DEC_SPLIT=3 run bench_split3 600 python bench.py --steps 10 --warmup 2 ;;
+        prof_split2) SKR_DEC_SPLIT=2 run prof_split2 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_split2 -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --no-eval ;;
         bench_nofused) SKR_FUSED=0 run bench_nofused 600 python bench.py --steps 10 --warmup 2 ;;
         bench_wgrad) run bench_wgrad 600 python scripts/bench_wgrad.py ;;
         bench_gemm) run bench_gemm 600 python scripts/bench_gemm.py ;;

@@ -279,6 +279,44 @@ def test_hyper_grouped_gemm_path_bitwise(H, Hh, E):
         assert torch.equal(a, b)
 
 
+@pytest.mark.parametrize("H,Hh,E,B", [(2048, 256, 32, 100), (512, 64, 8, 70)])
+def test_hyper_batch_split_matches_unsplit(H, Hh, E, B):
+    """bf16 HyperLSTM with the batch cut into independent chains on two
+    streams (SKR_DEC_SPLIT) equals the one-chain scan: outputs, final
+    states, input and weight gradients (the weight-gradient sums run over
+    the rows in a different order)."""
+    from sketch_rnn_amd.ops import recurrent
+    torch.manual_seed(5)
+    T, IN, Z = 5, 5, 16
+    p = C.HyperLSTMParams(IN + Z, H, Hh, E).to(DEV)
+    with torch.no_grad():
+        for prm in p.parameters():
+            prm.add_(torch.randn_like(prm) * 0.02)
+    x = torch.randn(T, B, IN, device=DEV)
+    z = torch.randn(B, Z, device=DEV)
+    st = [torch.randn(B, n, device=DEV) * 0.1 for n in (H, H, Hh, Hh)]
+    w = torch.randn(T, B, H, device=DEV)
+    assert recurrent._split_rows(B, 2) is not None
+    res = []
+    try:
+        ops.set_compute_dtype("bf16")
+        ops.set_backend("hip")
+        for split in (1, 2):
+            p.zero_grad()
+            zg = z.detach().clone().requires_grad_()   # x without grad: the model's stroke-projection path
+            out, fin = recurrent.hyper_sequence_hip(p, x, *st, drop_keep=1.0, zc=zg, split=split)
+            (out * w).sum().backward()
+            torch.cuda.synchronize()
+            res.append([out.detach()] + [f.detach() for f in fin] + [zg.grad] +
+                       [q.grad.clone() for q in p.parameters()])
+    finally:
+        ops.set_compute_dtype("fp32")
+    names = ["out", "h", "c", "hh", "hc", "dz"] + [n for n, _ in p.named_parameters()]
+    for n, a, b in zip(names, *res):
+        err = (a.float() - b.float()).abs().max().item()
+        assert err <= 2e-2 * max(b.float().abs().max().item(), 1e-3), (n, err)
+
+
 @pytest.mark.parametrize("dt,cu_stride", [("fp32", 4), ("bf16", 4), ("bf16", 1)])
 def test_hyper_chunked_wgrad_overlap(dt, cu_stride):
     """Weight / LN-parameter gradients accumulated in chunks on the
