@@ -39,6 +39,9 @@ for s in "${steps[@]}"; do
         bench_split2) SKR_DEC_SPLIT=2 run bench_split2 600 python bench.py --steps 10 --warmup 2 ;;
         bench_split3) SKR_DEC_SPLIT=3 run bench_split3 600 python bench.py --steps 10 --warmup 2 ;;
         prof_split2) SKR_DEC_SPLIT=2 run prof_split2 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_split2 -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --no-eval ;;
+        bench_vae_miopen) run bench_vae_miopen 600 python scripts/bench_vae_miopen.py --config vae_small --dtype bf16 ;;
+        bench_vae_miopen_fp32) run bench_vae_miopen_fp32 600 python scripts/bench_vae_miopen.py --config vae_small --dtype fp32 ;;
+        cli_vae_train) run cli_vae_train 600 python -m sketch_rnn_amd.cli.vae_train --preset vae_large --synthetic 2000 --num_steps 80 --log_every 20 --save_every 0 --save_dir /tmp/skr_cli_vae --metrics gpurun_out/cli_vae_train_metrics.jsonl ;;
         bench_nofused) SKR_FUSED=0 run bench_nofused 600 python bench.py --steps 10 --warmup 2 ;;
         bench_wgrad) run bench_wgrad 600 python scripts/bench_wgrad.py ;;
         bench_gemm) run bench_gemm 600 python scripts/bench_gemm.py ;;
