@@ -186,7 +186,9 @@ __device__ __forceinline__ void wait_ahead(int ahead) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
-template <int BN, int NS, bool CBF16 = false>
+// BPOL: cache-policy bits of the weight (B) stream's LDS-DMA loads (0 =
+// default; 2 = nt, SKR_GEMM_NT=1: CDNA4 guide "nt-weights").
+template <int BN, int NS, bool CBF16 = false, int BPOL = 0>
 __device__ __forceinline__ void glds_tile(const __hip_bfloat16* __restrict__ A, int64_t lda,
                                           const __hip_bfloat16* __restrict__ Bt, int64_t ldb,
                                           void* __restrict__ Cv, int64_t ldc, int M, int n0, int64_t k0, int kslice,
@@ -227,7 +229,7 @@ __device__ __forceinline__ void glds_tile(const __hip_bfloat16* __restrict__ A, 
         for (int i = 0; i < B_CH / 4; ++i)
             __builtin_amdgcn_global_load_lds((const void*)(bsrc[i] + ko),
                                              (__attribute__((address_space(3))) void*)(st + BM * BK + (w + 4 * i) * 512),
-                                             16, 0, 0);
+                                             16, 0, BPOL);
     };
 
     f32x4 acc[2][NJ];
@@ -402,14 +404,14 @@ __global__ __launch_bounds__(256) void skinny_gemm_ra_kernel(
                                  blockIdx.x * BN, (int64_t)blockIdx.y * kslice, kslice, smem);
 }
 
-template <int BN, int NS, bool CBF16 = false>
+template <int BN, int NS, bool CBF16 = false, int BPOL = 0>
 __global__ __launch_bounds__(256) void skinny_gemm_glds_kernel(
     const __hip_bfloat16* __restrict__ A, int64_t lda, int64_t a_batch,
     const __hip_bfloat16* __restrict__ Bt, int64_t ldb, int64_t b_batch,
     void* __restrict__ C, int64_t ldc, int64_t c_slab, int64_t c_batch, int M, int kslice) {
     extern __shared__ __attribute__((aligned(16))) __hip_bfloat16 smem[];
     const int64_t co = blockIdx.z * c_batch + blockIdx.y * c_slab;
-    glds_tile<BN, NS, CBF16>(A + blockIdx.z * a_batch, lda, Bt + blockIdx.z * b_batch, ldb,
+    glds_tile<BN, NS, CBF16, BPOL>(A + blockIdx.z * a_batch, lda, Bt + blockIdx.z * b_batch, ldb,
                   CBF16 ? (void*)((__hip_bfloat16*)C + co) : (void*)((float*)C + co), ldc, M, blockIdx.x * BN,
                   (int64_t)blockIdx.y * kslice, kslice, smem);
 }
@@ -439,7 +441,7 @@ struct GemmGroup {
     int n;
 };
 
-template <int BN, int NS>
+template <int BN, int NS, int BPOL = 0>
 __global__ __launch_bounds__(256) void skinny_gemm_group_kernel(const GemmGroup g) {
     extern __shared__ __attribute__((aligned(16))) __hip_bfloat16 smem[];
     const int id = blockIdx.x;
@@ -451,8 +453,8 @@ __global__ __launch_bounds__(256) void skinny_gemm_group_kernel(const GemmGroup 
     const int ntiles = p.N / BN;
     const int split = local / ntiles, nt = local - split * ntiles;
     const int kslice = p.K / p.splits;
-    glds_tile<BN, NS>((const __hip_bfloat16*)p.A, p.lda, (const __hip_bfloat16*)p.Bt, p.ldb, p.C + split * p.c_slab, p.ldc,
-                  p.M, nt * BN, (int64_t)split * kslice, kslice, smem);
+    glds_tile<BN, NS, false, BPOL>((const __hip_bfloat16*)p.A, p.lda, (const __hip_bfloat16*)p.Bt, p.ldb,
+                                   p.C + split * p.c_slab, p.ldc, p.M, nt * BN, (int64_t)split * kslice, kslice, smem);
 }
 
 template <int BN, int NSB>
@@ -837,6 +839,21 @@ static bool areg_on() {
     return g_areg == 1;
 }
 
+// Weight-stream cache policy of the v2 / grouped kernels: SKR_GEMM_NT=1
+// loads the B operand non-temporally (nt); default policy otherwise.
+// OFF by default -- measured on MI355X: vae_large 30.3 vs 28.5 ms/step, the
+// grouped forward GEMM 14.0 vs 12.8 us (profiles/r2s5/bench_gemm_nt.log):
+// each weight is re-read every time step and the default policy keeps it
+// cache-resident between steps.
+static int g_bnt = -1;
+static bool bnt_on() {
+    if (g_bnt < 0) {
+        const char* e = getenv("SKR_GEMM_NT");
+        g_bnt = (e != nullptr && atoi(e) == 1) ? 1 : 0;
+    }
+    return g_bnt == 1;
+}
+
 SKR_API int skr_gemm_set_nstage(int ns) {
     if (ns != 3 && ns != 4 && ns != 6) return -2;
     g_nstage = ns;
@@ -867,6 +884,13 @@ int launch_v2(dim3 grid, hipStream_t s, const void* A, int64_t lda, int64_t a_ba
         return SKR_CHECK_LAUNCH();
     }
     const size_t lds = (size_t)NS * (BM + BN) * BK * 2;
+    if (bnt_on()) {
+        set_lds_attr(skinny_gemm_glds_kernel<BN, NS, CBF16, 2>, lds);
+        hipLaunchKernelGGL((skinny_gemm_glds_kernel<BN, NS, CBF16, 2>), grid, dim3(256), lds, s,
+                           (const __hip_bfloat16*)A, lda, a_batch, (const __hip_bfloat16*)Bt, ldb, b_batch, C, ldc,
+                           c_slab, c_batch, M, kslice);
+        return SKR_CHECK_LAUNCH();
+    }
     set_lds_attr(skinny_gemm_glds_kernel<BN, NS, CBF16>, lds);
     hipLaunchKernelGGL((skinny_gemm_glds_kernel<BN, NS, CBF16>), grid, dim3(256), lds, s, (const __hip_bfloat16*)A,
                        lda, a_batch, (const __hip_bfloat16*)Bt, ldb, b_batch, C, ldc, c_slab, c_batch, M, kslice);
@@ -882,6 +906,11 @@ int launch_group(const GemmGroup& g, hipStream_t s) {
         return SKR_CHECK_LAUNCH();
     }
     const size_t lds = (size_t)NS * (BM + BN) * BK * 2;
+    if (bnt_on()) {
+        set_lds_attr(skinny_gemm_group_kernel<BN, NS, 2>, lds);
+        hipLaunchKernelGGL((skinny_gemm_group_kernel<BN, NS, 2>), dim3(g.start[g.n]), dim3(256), lds, s, g);
+        return SKR_CHECK_LAUNCH();
+    }
     set_lds_attr(skinny_gemm_group_kernel<BN, NS>, lds);
     hipLaunchKernelGGL((skinny_gemm_group_kernel<BN, NS>), dim3(g.start[g.n]), dim3(256), lds, s, g);
     return SKR_CHECK_LAUNCH();
