@@ -83,6 +83,7 @@ struct PFwdArgs {
     const int64_t* seed;
     uint32_t* flags;                          // [L][nd][nrb][kFlagStride] epochs (zeroed per launch)
     int* err;
+    const int* tlen;                          // [B] valid lengths (L = 1) or null, see row_block_steps
 };
 
 struct PBwdLayer {
@@ -105,6 +106,7 @@ struct PBwdArgs {
     const int64_t* seed;
     uint32_t* flags;
     int* err;
+    const int* tlen;                          // as PFwdArgs::tlen (the same lengths as the forward)
 };
 
 namespace {
@@ -127,6 +129,22 @@ __device__ void stage_rows(__hip_bfloat16* lds, const __hip_bfloat16* src, int64
 
 __device__ __forceinline__ bf16x8 lds_frag(const __hip_bfloat16* lds, int row, int K, int chunk) {
     return *(const bf16x8*)(lds + row * K + ((chunk ^ (row & 15)) * 8));
+}
+
+// Steps a row block runs. With per-row valid lengths (the VAE encoder: rows
+// are padded past their length, both directions read only steps < length,
+// like TF's dynamic_rnn with sequence_length) a row block stops after the
+// longest of its rows: Te = max(min(len, T)) over its rows (>= 1). Row blocks
+// never wait on each other, so each keeps its own bound; the tails t >= Te
+// of the tensors read after the launch (top outputs, the carried-h operand of
+// the weight-gradient GEMM, dG) are zero-filled so those products stay exact.
+// The final carried state (hT, cT) is the state after step Te - 1.
+__device__ __forceinline__ int row_block_steps(const int* tlen, int T, int B, int rb, int rows) {
+    if (tlen == nullptr) return T;
+    int te = 1;
+    const int r1 = min(B, (rb + 1) * rows);
+    for (int r = rb * rows; r < r1; ++r) te = max(te, min(tlen[r], T));
+    return te;
 }
 
 // =====================================================================================
@@ -177,8 +195,9 @@ __device__ void fwd_body(const PFwdArgs& a, int l, int g, int rb, int wu, unsign
     // A-fragment row of this lane (clamped) within its tile
     const int arow = (int)grow0 + min(row_t0 + fr, B - 1);
     bool ok = true;
+    const int Te = row_block_steps(a.tlen, T, B, rb, 16 * MTW);
 
-    for (int t = 0; t < T; ++t) {
+    for (int t = 0; t < Te; ++t) {
         // ---- epilogue inputs of step t (independent of the recurrence: issued before the wait)
         float xv[4][4], rs[4], ih[4], ic[4];
         if (epi) {
@@ -287,10 +306,23 @@ __device__ void fwd_body(const PFwdArgs& a, int l, int g, int rb, int wu, unsign
                 P.c_out[so] = cn[e];
                 if (P.c_carry != nullptr) P.c_carry[so + (int64_t)nB * H] = c[e];
                 if (P.h_out != nullptr) P.h_out[so] = hn[e];
-                if (t == T - 1) {
+                if (t == Te - 1) {
                     P.hT[ro] = hc[e];
                     P.cT[ro] = c[e];
                 }
+            }
+        }
+    }
+    // tails past the row block's last step: zero top outputs and carried-h
+    // operand rows (plain stores; nothing in this launch reads them)
+    if (epi && Te < T) {
+        for (int t = Te; t < T; ++t) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                if (!bon[e]) continue;
+                const int64_t ro = (int64_t)brow[e] * H + u;
+                P.hlp[(int64_t)(t + 1) * nB * H + ro] = to_bf16(0.f);
+                if (P.h_out != nullptr) P.h_out[(int64_t)t * nB * H + ro] = 0.f;
             }
         }
     }
@@ -367,9 +399,10 @@ __device__ void bwd_body(const PBwdArgs& a, int l, int g, int rb, int wu, unsign
     const bool keep_on = P.keep < 1.0f;
     const int arow = (int)grow0 + min(row_t0 + fr, B - 1);
     bool ok = true;
+    const int Te = row_block_steps(a.tlen, T, B, rb, 16 * MTW);
 
-    // t = T-1 .. 0 are cell steps; t = -1 only forms dh0 = dG_0 @ W_h^T
-    for (int t = T - 1; t >= -1; --t) {
+    // t = Te-1 .. 0 are cell steps; t = -1 only forms dh0 = dG_0 @ W_h^T
+    for (int t = Te - 1; t >= -1; --t) {
         float ac[4][4], cnw[4], cpv[4], dho[4], rs[4];
         if (epi && t >= 0) {
             const int64_t so = (int64_t)t * nB * H;
@@ -389,7 +422,7 @@ __device__ void bwd_body(const PBwdArgs& a, int l, int g, int rb, int wu, unsign
         if (tile_on) {
             const int k0 = kp * KP;
             // dG_l[t+1] @ W_h^T (own layer, previous reverse step)
-            if (t < T - 1) {
+            if (t < Te - 1) {
                 ok = ok && wait_flags(my_flags, NW, (uint32_t)(T - 1 - t), a.err);
                 const uint32_t base = (uint32_t)(((int64_t)(t + 1) * nB + arow) * G * 2);
 #pragma unroll
@@ -456,7 +489,7 @@ __device__ void bwd_body(const PBwdArgs& a, int l, int g, int rb, int wu, unsign
             for (int e = 0; e < 4; ++e) {
                 const int64_t ro = (int64_t)brow[e] * H + u;
                 float dhr = sr[e];
-                if (t == T - 1) dhr = P.dhT != nullptr ? P.dhT[ro] : 0.f;
+                if (t == Te - 1) dhr = P.dhT != nullptr ? P.dhT[ro] : 0.f;
                 const bool r = rs[e] != 0.f;
                 const float dh = (UP ? su[e] : dho[e]) + (r ? 0.f : dhr);
                 float dc = r ? 0.f : dcr[e];
@@ -500,6 +533,22 @@ __device__ void bwd_body(const PBwdArgs& a, int l, int g, int rb, int wu, unsign
                 float* dp = P.dg + (int64_t)t * nB * G + (int64_t)brow[e] * G + u;
 #pragma unroll
                 for (int q = 0; q < 4; ++q) dp[q * H] = dy[e][q];
+            }
+        }
+    }
+    // dG tails past the row block's last step: zero (read by the weight /
+    // input-projection gradients after the launch)
+    if (epi && Te < T) {
+        for (int t = Te; t < T; ++t) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                if (!bon[e]) continue;
+                const int64_t go = (int64_t)t * nB * G + (int64_t)brow[e] * G + u;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    P.dg_lp[go + q * H] = to_bf16(0.f);
+                    if (P.dg != nullptr) P.dg[go + q * H] = 0.f;
+                }
             }
         }
     }
@@ -572,6 +621,7 @@ int check_common(const A& a) {
     if (a.H != 256 && (a.H != 512 || a.L > 1)) return -2;   // two stacked 512 layers exceed LDS
     if (a.nrb != (a.B + 16 * kMTW - 1) / (16 * kMTW)) return -4;
     if (a.flags == nullptr || a.err == nullptr) return -6;
+    if (a.tlen != nullptr && a.L != 1) return -7;   // stacked layers run the full T
     // 32-bit buffer offsets
     if ((int64_t)(a.T + 1) * a.nd * a.B * 4 * a.H * 2 > 0x7fffffffLL) return -11;
     return 0;

@@ -71,8 +71,11 @@ class Encoder(nn.Module):
         # direction reads each sketch reversed within its length)
         xp = bilstm_input_proj(x, lengths, self.fw.W_x, self.bw.W_x, None if ln else self.fw.bias,
                                None if ln else self.bw.bias)
+        # only h[len - 1] of each row is read: the persistent kernel may stop
+        # each row block after its longest row (TF dynamic_rnn sequence_length)
         outs = ops.bilstm_sequence_packed(xp, self.fw.W_h, self.bw.W_h, zeros, zeros, drop_keep=keep,
-                                          drop_seed=seed, drop_stream=_S_ENC_FW, ln_f=lns[0], ln_b=lns[1])
+                                          drop_seed=seed, drop_stream=_S_ENC_FW, ln_f=lns[0], ln_b=lns[1],
+                                          lengths=lengths)
         idx = (lengths - 1).clamp(min=0).view(1, B, 1).expand(1, B, H)
         last_h = torch.cat([torch.gather(o, 0, idx).squeeze(0) for o in outs], -1)
         mu = last_h @ self.mu_w + self.mu_b

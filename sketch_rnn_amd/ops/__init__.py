@@ -84,14 +84,16 @@ def bilstm_sequence(xp_f, xp_b, W_f, W_b, h0, c0, drop_keep: float = 1.0, drop_s
 
 
 def bilstm_sequence_packed(xp, W_f, W_b, h0, c0, drop_keep: float = 1.0, drop_seed: int = 0,
-                           drop_stream: int = 0, ln_f=None, ln_b=None, forget_bias: float = 1.0):
+                           drop_stream: int = 0, ln_f=None, ln_b=None, forget_bias: float = 1.0, lengths=None):
     """:func:`bilstm_sequence` with both directions' input projections packed
     as ``xp [T, 2B, 4H]`` (forward rows first), e.g. from
-    :func:`.inproj.bilstm_input_proj`."""
+    :func:`.inproj.bilstm_input_proj`. ``lengths [B]`` (optional): outputs at
+    ``t >= lengths[b]`` are never read by the caller, so a backend may skip
+    those steps (their values are then unspecified; the oracle computes them)."""
     if use_hip(xp):
         from .recurrent import bilstm_sequence_packed_hip
         return bilstm_sequence_packed_hip(xp, W_f, W_b, h0, c0, drop_keep, drop_seed, (drop_stream, drop_stream),
-                                          ln_f, ln_b, forget_bias)
+                                          ln_f, ln_b, forget_bias, lengths)
     B = xp.shape[1] // 2
     return bilstm_sequence(xp[:, :B], xp[:, B:], W_f, W_b, h0, c0, drop_keep, drop_seed, drop_stream, ln_f, ln_b,
                            forget_bias)

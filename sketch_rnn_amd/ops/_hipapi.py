@@ -168,6 +168,7 @@ class PFwdArgs(C.Structure):
         ("seed", _p),
         ("flags", _p),
         ("err", _p),
+        ("tlen", _p),
     ]
 
 
@@ -194,6 +195,7 @@ class PBwdArgs(C.Structure):
         ("seed", _p),
         ("flags", _p),
         ("err", _p),
+        ("tlen", _p),
     ]
 
 

@@ -68,7 +68,7 @@ class _PersistLSTM(torch.autograd.Function):
     carried ``(h, c)``."""
 
     @staticmethod
-    def forward(ctx, xp0, W_in1, b1, W_h0, W_h1, h0a, c0a, h0b, c0b, reset, seed, meta):
+    def forward(ctx, xp0, W_in1, b1, W_h0, W_h1, h0a, c0a, h0b, c0b, reset, seed, meta, tlen=None):
         L, nd, keep, stream, fb = meta
         from .recurrent import _seed_tensor, cluster_error_flag
         lib = native.require_hip()
@@ -98,6 +98,8 @@ class _PersistLSTM(torch.autograd.Function):
         a.reset, a.forget_bias, a.seed = _ptr(rst), float(fb), sd.data_ptr()
         flags = torch.empty(L * nd * nrb * 64, dtype=torch.int32, device=dev)   # zeroed by the launcher
         a.flags, a.err = flags.data_ptr(), cluster_error_flag(dev).data_ptr()
+        tl = tlen.to(device=dev, dtype=torch.int32).contiguous() if tlen is not None else None
+        a.tlen = _ptr(tl)
         s = _Saved()
         s.hlp, s.hup, s.c_out, s.c_carry, s.act = [], [], [], [], []
         outs = []
@@ -137,6 +139,7 @@ class _PersistLSTM(torch.autograd.Function):
         s.Wl, s.Wu, s.c0s, s.rst, s.seed, s.meta = Wl, Wu, c0s, rst, sd, meta
         s.shapes = [W.shape for W in Wh]
         s.keep_flags = flags
+        s.tlen = tl
         ctx.s = s
         ctx.dims = (T, B, H, nrb)
         return (top, *outs)
@@ -155,6 +158,7 @@ class _PersistLSTM(torch.autograd.Function):
         b.reset, b.seed = _ptr(s.rst), s.seed.data_ptr()
         flags = torch.empty(L * nd * nrb * 64, dtype=torch.int32, device=dev)   # zeroed by the launcher
         b.flags, b.err = flags.data_ptr(), cluster_error_flag(dev).data_ptr()
+        b.tlen = _ptr(s.tlen)
         dtop = dtop.contiguous() if dtop is not None else None
         dg_lp, dg, dh0, dc0, dih, dic, keep_alive = [], [], [], [], [], [], []
         for l in range(L):
@@ -210,20 +214,29 @@ class _PersistLSTM(torch.autograd.Function):
         ctx.s = None
         return (dg[0], dWin1, db1, dWh[0], dWh[1] if L == 2 else None,
                 dh0t[0], dc0t[0], dh0t[1] if L == 2 else None, dc0t[1] if L == 2 else None,
-                None, None, None)
+                None, None, None, None)
 
 
 def lstm_stack(xp0: torch.Tensor, W_h: Sequence[torch.Tensor], h0: Sequence[torch.Tensor],
                c0: Sequence[torch.Tensor], W_in1: Optional[torch.Tensor] = None, b1: Optional[torch.Tensor] = None,
                reset: Optional[torch.Tensor] = None, nd: int = 1, drop_keep: float = 1.0, drop_seed=0,
-               drop_stream: int = 0, forget_bias: float = 1.0) -> Tuple[torch.Tensor, List[Tuple]]:
+               drop_stream: int = 0, forget_bias: float = 1.0,
+               lengths: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, List[Tuple]]:
     """Run ``len(W_h)`` (1 or 2) stacked LSTM layers over ``xp0`` in one
     persistent launch. Returns the top layer's outputs ``[T, nd*B, H]`` and
-    the final carried ``(h, c)`` of every layer."""
+    the final carried ``(h, c)`` of every layer.
+
+    ``lengths [B]`` (one layer only; the same for every direction): rows are
+    padding from their length on and nothing downstream reads them, so each
+    32-row block stops after its longest row (TF ``dynamic_rnn`` with
+    ``sequence_length`` skips those steps the same way). Outputs past a
+    block's last step are zero and its final state is the one after that
+    step."""
     L = len(W_h)
     meta = (L, nd, float(drop_keep), int(drop_stream), float(forget_bias))
     if L == 2:
         outs = _PersistLSTM.apply(xp0, W_in1, b1, W_h[0], W_h[1], h0[0], c0[0], h0[1], c0[1], reset, drop_seed, meta)
         return outs[0], [(outs[1], outs[2]), (outs[3], outs[4])]
-    outs = _PersistLSTM.apply(xp0, None, None, W_h[0], None, h0[0], c0[0], None, None, reset, drop_seed, meta)
+    outs = _PersistLSTM.apply(xp0, None, None, W_h[0], None, h0[0], c0[0], None, None, reset, drop_seed, meta,
+                              lengths)
     return outs[0], [(outs[1], outs[2])]

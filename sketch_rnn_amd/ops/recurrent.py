@@ -483,9 +483,12 @@ def bilstm_sequence_hip(xp_f, xp_b, W_f, W_b, h0, c0, drop_keep=1.0, drop_seed=0
 
 
 def bilstm_sequence_packed_hip(xp, W_f, W_b, h0, c0, drop_keep=1.0, drop_seed=0, streams=(0, 0),
-                               ln_f=None, ln_b=None, forget_bias=1.0):
+                               ln_f=None, ln_b=None, forget_bias=1.0, lengths=None):
     """As :func:`bilstm_sequence_hip` with the input projections already in
-    the ``[T, 2B, 4H]`` layout (forward-direction rows first; ops/inproj.py)."""
+    the ``[T, 2B, 4H]`` layout (forward-direction rows first; ops/inproj.py).
+    ``lengths [B]``: steps at or past a row's length are padding that nothing
+    reads -- the persistent kernel stops each row block after its longest row
+    (outputs there are zero; :func:`.persist.lstm_stack`)."""
     B = xp.shape[1] // 2
     W = torch.stack([W_f, W_b], 0)
     h = torch.cat([h0, h0], 0)
@@ -494,7 +497,8 @@ def bilstm_sequence_packed_hip(xp, W_f, W_b, h0, c0, drop_keep=1.0, drop_seed=0,
     if persist.persist_ok(W_f.shape[0], 2, 1, ln=ln_f is not None):
         # both directions, every step, one persistent launch (csrc/lstm_persist.hip)
         Hout, _ = persist.lstm_stack(xp, [W], [h], [c], nd=2, drop_keep=drop_keep, drop_seed=drop_seed,
-                                     drop_stream=streams[0], forget_bias=forget_bias)
+                                     drop_stream=streams[0], forget_bias=forget_bias,
+                                     lengths=lengths if PERSIST_LENGTHS else None)
         return Hout[:, :B], Hout[:, B:]
     if ln_f is not None:
         ln = tuple(torch.stack([a, b], 0) for a, b in zip(ln_f, ln_b))
@@ -504,6 +508,11 @@ def bilstm_sequence_packed_hip(xp, W_f, W_b, h0, c0, drop_keep=1.0, drop_seed=0,
                                   (float(forget_bias), float(drop_keep), int(streams[0]), 2,
                                    _inference(xp, W, h, c)))
     return Hout[:, :B], Hout[:, B:]
+
+
+# Length-bounded persistent encoder (SKR_PERSIST_LENGTHS=0 runs every row
+# block for all T steps).
+PERSIST_LENGTHS = os.environ.get("SKR_PERSIST_LENGTHS", "1") != "0"
 
 
 # =====================================================================================

@@ -97,6 +97,48 @@ def test_persistent_bilstm_matches_oracle():
         assert _rel(a, b) < 4e-2, (n, _rel(a, b))
 
 
+def test_persistent_bilstm_lengths_bound_each_row_block():
+    """Encoder use (only h[len - 1] of each row is read): with ``lengths`` the
+    persistent launch stops every 32-row block after its longest row. The
+    read outputs and every gradient equal the full-length launch bit for bit
+    (steps past a row's length carry zero gradient either way; the skipped
+    tails are zero-filled, checked with NaN-poisoned buffers)."""
+    torch.manual_seed(4)
+    T, B, H = 60, 100, 512
+    ops.set_backend("hip")
+    ops.set_compute_dtype("bf16")
+    g = torch.Generator().manual_seed(4)
+    # row blocks with very different longest rows (17, 41, 60, 9)
+    lengths = torch.cat([torch.randint(1, 18, (32,), generator=g), torch.randint(1, 42, (32,), generator=g),
+                         torch.randint(1, 61, (32,), generator=g), torch.randint(1, 10, (4,), generator=g)])
+    lengths[40], lengths[70], lengths[97] = 41, 60, 9
+    lengths = lengths.to(DEV)
+    xp = (torch.randn(T, 2 * B, 4 * H, device=DEV) * 0.5).requires_grad_()
+    W_f = (torch.randn(H, 4 * H, device=DEV) / H ** 0.5).requires_grad_()
+    W_b = (torch.randn(H, 4 * H, device=DEV) / H ** 0.5).requires_grad_()
+    h0 = (0.2 * torch.randn(B, H, device=DEV)).requires_grad_()
+    c0 = (0.2 * torch.randn(B, H, device=DEV)).requires_grad_()
+    R = torch.randn(B, 2 * H, device=DEV)
+    idx = (lengths - 1).clamp(min=0).view(1, B, 1).expand(1, B, H)
+    res = []
+    persist.POISON = True
+    try:
+        for lens in (None, lengths):
+            for t in (xp, W_f, W_b, h0, c0):
+                t.grad = None
+            of, ob = ops.bilstm_sequence_packed(xp, W_f, W_b, h0, c0, drop_keep=0.9, drop_seed=5, drop_stream=2,
+                                                lengths=lens)
+            last = torch.cat([torch.gather(o, 0, idx).squeeze(0) for o in (of, ob)], -1)
+            (last * R).sum().backward()
+            torch.cuda.synchronize()
+            res.append([last.detach()] + [t.grad.clone() for t in (xp, W_f, W_b, h0, c0)])
+    finally:
+        persist.POISON = False
+    for n, a, b in zip(["last_h", "xp", "W_f", "W_b", "h0", "c0"], *res):
+        assert torch.isfinite(b).all(), n
+        assert torch.equal(a, b), (n, float((a - b).abs().max()))
+
+
 def test_persistent_matches_per_step_kernels():
     """Same model, persistent launch vs the per-step fused kernels (both
     bf16): outputs agree to bf16 rounding of the operands."""
