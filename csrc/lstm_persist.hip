@@ -65,7 +65,7 @@ struct PFwdLayer {
     const float* xp; int64_t xp_ts, xp_ld;    // xp[t*ts + row*ld + n] (+bias); ts = ld = 0: a bias vector
     const float* c0;                          // [nd*B][H]
     const float* init_h; const float* init_c; // reset targets [nd*B][H] (read iff reset)
-    __hip_bfloat16* hlp;                      // [T+1][nd*B][H] carried h (next step's operand); hlp[0] = h0 (host)
+    __hip_bfloat16* hlp;                      // [nd][T+1][B][H] carried h (next step's operand); [:, 0] = h0 (host)
     __hip_bfloat16* hup;                      // [T][nd*B][H] pre-reset h for the layer above, or null
     float* h_out;                             // [T][nd*B][H] or null
     float* c_out;                             // [T][nd*B][H] pre-reset c
@@ -92,7 +92,7 @@ struct PBwdLayer {
     const float* dh_out;                      // [T][nd*B][H] grad of this layer's outputs (top layer) or null
     const float* dhT; const float* dcT;       // [nd*B][H] grads into the final carried state, or null
     const float* act; const float* c_out; const float* c_carry; const float* c0;
-    __hip_bfloat16* dg_lp;                    // [T][nd*B][4H] bf16 dG (published)
+    __hip_bfloat16* dg_lp;                    // [nd][T][B][4H] bf16 dG (published)
     float* dg;                                // [T][nd*B][4H] fp32 dG or null
     float* dh0; float* dc0;                   // [nd*B][H] grads into the initial state
     float* dinit_h; float* dinit_c;           // [nd*B][H] grads into the reset targets (with resets)
@@ -169,7 +169,11 @@ __device__ void fwd_body(const PFwdArgs& a, int l, int g, int rb, int wu, unsign
     stage_rows<true>(Ws, P.WT + g * P.w_gs, K, 64, K, H, u0);
     __syncthreads();
 
-    const __amdgpu_buffer_rsrc_t r_h = rsrc(P.hlp, (int64_t)(T + 1) * nB * H * 2);
+    // carried h is direction-major ([nd][T+1][B][H]): a direction's rows are
+    // contiguous per step, so the weight-gradient GEMM reads each direction
+    // as one [T*B, H] matrix without a copy (nd == 1: the plain [T+1][B][H])
+    __hip_bfloat16* const hl = P.hlp + (int64_t)g * (T + 1) * B * H;
+    const __amdgpu_buffer_rsrc_t r_h = rsrc(hl, (int64_t)(T + 1) * B * H * 2);
     const PFwdLayer* Pb = l > 0 ? &a.ly[l - 1] : nullptr;
     const __hip_bfloat16* in_base = (KIN > 0) ? (Pb->hup != nullptr ? Pb->hup : Pb->hlp + (int64_t)nB * H) : nullptr;
     const __amdgpu_buffer_rsrc_t r_in = rsrc(KIN > 0 ? (const void*)in_base : (const void*)P.hlp,
@@ -223,7 +227,7 @@ __device__ void fwd_body(const PFwdArgs& a, int l, int g, int rb, int wu, unsign
             bf16x8 af[NKS];
             const int kc = from_in ? k0 : k0 - KIN;     // column within the source matrix
             const uint32_t base = from_in ? (uint32_t)(((int64_t)t * nB + arow) * H * 2)
-                                          : (uint32_t)(((int64_t)t * nB + arow) * H * 2);
+                                          : (uint32_t)(((int64_t)t * B + (arow - grow0)) * H * 2);
             const __amdgpu_buffer_rsrc_t rr = from_in ? r_in : r_h;
 #pragma unroll
             for (int ks = 0; ks < NKS; ++ks) af[ks] = ld_sc1(rr, base + (uint32_t)((kc + ks * 32 + fq * 8) * 2));
@@ -273,7 +277,7 @@ __device__ void fwd_body(const PFwdArgs& a, int l, int g, int rb, int wu, unsign
                 const int r = lane >> 1, hf = lane & 1;
                 if (row_t0 + r < B) {
                     const u32x4 v = *(const u32x4*)(hw + r * 16 + hf * 8);
-                    const int64_t off = ((int64_t)(t + 1) * nB + grow0 + row_t0 + r) * H + u0 + hf * 8;
+                    const int64_t off = ((int64_t)(t + 1) * B + row_t0 + r) * H + u0 + hf * 8;
                     st_sc1(r_h, (uint32_t)(off * 2), v);
                 }
             }
@@ -321,7 +325,7 @@ __device__ void fwd_body(const PFwdArgs& a, int l, int g, int rb, int wu, unsign
             for (int e = 0; e < 4; ++e) {
                 if (!bon[e]) continue;
                 const int64_t ro = (int64_t)brow[e] * H + u;
-                P.hlp[(int64_t)(t + 1) * nB * H + ro] = to_bf16(0.f);
+                hl[((int64_t)(t + 1) * B + (brow[e] - grow0)) * H + u] = to_bf16(0.f);
                 if (P.h_out != nullptr) P.h_out[(int64_t)t * nB * H + ro] = 0.f;
             }
         }
@@ -374,7 +378,9 @@ __device__ void bwd_body(const PBwdArgs& a, int l, int g, int rb, int wu, unsign
     if (UP) stage_rows<false>(Wu, P.Wu, G, 16, G, H, u0);
     __syncthreads();
 
-    const __amdgpu_buffer_rsrc_t r_g = rsrc(P.dg_lp, (int64_t)T * nB * G * 2);
+    // bf16 dG is direction-major ([nd][T][B][4H], like the carried h)
+    __hip_bfloat16* const gl = P.dg_lp + (int64_t)g * T * B * G;
+    const __amdgpu_buffer_rsrc_t r_g = rsrc(gl, (int64_t)T * B * G * 2);
     const __amdgpu_buffer_rsrc_t r_up = rsrc(UP ? (const void*)a.ly[l + 1].dg_lp : (const void*)P.dg_lp,
                                              (int64_t)T * nB * G * 2);
     uint32_t* my_flags = a.flags + (((int64_t)l * a.nd + g) * a.nrb + rb) * kFlagStride;
@@ -424,7 +430,7 @@ __device__ void bwd_body(const PBwdArgs& a, int l, int g, int rb, int wu, unsign
             // dG_l[t+1] @ W_h^T (own layer, previous reverse step)
             if (t < Te - 1) {
                 ok = ok && wait_flags(my_flags, NW, (uint32_t)(T - 1 - t), a.err);
-                const uint32_t base = (uint32_t)(((int64_t)(t + 1) * nB + arow) * G * 2);
+                const uint32_t base = (uint32_t)(((int64_t)(t + 1) * B + (arow - grow0)) * G * 2);
 #pragma unroll
                 for (int kb = 0; kb < NKS; kb += NCH) {
                     bf16x8 af[NCH];
@@ -520,7 +526,7 @@ __device__ void bwd_body(const PBwdArgs& a, int l, int g, int rb, int wu, unsign
                 const int q = s >> 5, r = (s >> 1) & 15, hf = s & 1;
                 if (row_t0 + r < B) {
                     const u32x4 v = *(const u32x4*)(gw + (q * 16 + r) * 16 + hf * 8);
-                    const int64_t off = ((int64_t)t * nB + grow0 + row_t0 + r) * G + q * H + u0 + hf * 8;
+                    const int64_t off = ((int64_t)t * B + row_t0 + r) * G + q * H + u0 + hf * 8;
                     st_sc1(r_g, (uint32_t)(off * 2), v);
                 }
             }
@@ -543,10 +549,11 @@ __device__ void bwd_body(const PBwdArgs& a, int l, int g, int rb, int wu, unsign
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
                 if (!bon[e]) continue;
-                const int64_t go = (int64_t)t * nB * G + (int64_t)brow[e] * G + u;
+                const int64_t go = (int64_t)t * nB * G + (int64_t)brow[e] * G + u;           // fp32 dG: [T][nd*B][4H]
+                const int64_t gb = ((int64_t)t * B + (brow[e] - grow0)) * G + u;      // bf16 dG: direction-major
 #pragma unroll
                 for (int q = 0; q < 4; ++q) {
-                    P.dg_lp[go + q * H] = to_bf16(0.f);
+                    gl[gb + q * H] = to_bf16(0.f);
                     if (P.dg != nullptr) P.dg[go + q * H] = 0.f;
                 }
             }

@@ -105,10 +105,12 @@ class _PersistLSTM(torch.autograd.Function):
         outs = []
         for l in range(L):
             ly = a.ly[l]
-            hlp = torch.empty(T + 1, NB, H, dtype=bf, device=dev)
+            # carried h, direction-major [nd, T+1, B, H] (the kernel's layout:
+            # each direction is one contiguous [T*B, H] operand of its dW GEMM)
+            hlp = torch.empty(nd, T + 1, B, H, dtype=bf, device=dev)
             if POISON:
                 hlp.fill_(float("nan"))
-            hlp[0].copy_(h0s[l])
+            hlp[:, 0].copy_(h0s[l].view(nd, B, H))
             hup = torch.empty(T, NB, H, dtype=bf, device=dev) if (l < L - 1 and rst is not None) else None
             h_out = torch.empty(T, NB, H, dtype=f32, device=dev) if l == L - 1 else None
             c_out = torch.empty(T, NB, H, dtype=f32, device=dev)
@@ -173,7 +175,7 @@ class _PersistLSTM(torch.autograd.Function):
             ly.dhT, ly.dcT = _ptr(dhT), _ptr(dcT)
             ly.act, ly.c_out, ly.c_carry, ly.c0 = (s.act[l].data_ptr(), s.c_out[l].data_ptr(), _ptr(s.c_carry[l]),
                                                    s.c0s[l].data_ptr())
-            gl = torch.empty(T, NB, G, dtype=bf, device=dev)
+            gl = torch.empty(nd, T, B, G, dtype=bf, device=dev)       # direction-major, like hlp
             if POISON:
                 gl.fill_(float("nan"))
             gf = torch.empty(T, NB, G, dtype=f32, device=dev)
@@ -195,17 +197,15 @@ class _PersistLSTM(torch.autograd.Function):
         # weight gradients: one long-K product per matrix over all T*B rows
         dWh = []
         for l in range(L):
-            A = s.hlp[l][:T]
+            A = s.hlp[l][:, :T]                                        # [nd, T, B, H] (a view: no copy)
             if nd == 1:
                 dW = gemm.wgrad(A.reshape(T * NB, H), dg_lp[l].view(T * NB, G))
             else:
-                An = A.view(T, nd, B, H).permute(1, 0, 2, 3).reshape(nd, T * B, H)
-                Gn = dg_lp[l].view(T, nd, B, G).permute(1, 0, 2, 3).reshape(nd, T * B, G)
-                dW = gemm.wgrad(An, Gn)
+                dW = gemm.wgrad(A.reshape(nd, T * B, H), dg_lp[l].view(nd, T * B, G))
             dWh.append(dW.reshape(s.shapes[l]))
         dWin1 = db1 = None
         if L == 2:
-            src = s.hup[0] if s.hup[0] is not None else s.hlp[0][1:]
+            src = s.hup[0] if s.hup[0] is not None else s.hlp[0][0, 1:]
             dWin1 = gemm.wgrad(src.reshape(T * NB, H), dg_lp[1].view(T * NB, G))
             db1 = colsum(dg[1].view(T * NB, G))[1]
         # the eoc-reset targets are the initial states themselves
