@@ -169,6 +169,7 @@ class PFwdArgs(C.Structure):
         ("flags", _p),
         ("err", _p),
         ("tlen", _p),
+        ("xcd_groups", _i),
     ]
 
 
@@ -196,6 +197,7 @@ class PBwdArgs(C.Structure):
         ("flags", _p),
         ("err", _p),
         ("tlen", _p),
+        ("xcd_groups", _i),
     ]
 
 

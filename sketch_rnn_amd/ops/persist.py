@@ -35,6 +35,13 @@ PERSIST_ENABLED = os.environ.get("SKR_PERSIST", "1") != "0"
 # debug: fill every handed-off buffer with NaN before the launch, so a read
 # that overtakes its hand-off shows up as a NaN instead of a stale value
 POISON = os.environ.get("SKR_PERSIST_POISON", "0") == "1"
+# XCD-aware block remap of the 8-group launches (csrc/lstm_persist.hip
+# xcd_group_bid), OPT-IN (SKR_PERSIST_XCD=1): measured on MI355X, same box,
+# A/B twice -- vae_large 27.42 / 27.29 vs 26.91 / 26.93 ms/step, reference
+# config bf16 4.89 vs 4.59 ms/step (profiles/r2s5/xcd_remap_ab.txt): a group's
+# 32 workgroups publishing and polling on one XCD are slower than spread
+# over all eight
+XCD_GROUPS = os.environ.get("SKR_PERSIST_XCD", "0") == "1"
 _ROWS = 32          # rows per workgroup row block (kMTW = 2 sixteen-row tiles)
 
 
@@ -100,6 +107,7 @@ class _PersistLSTM(torch.autograd.Function):
         a.flags, a.err = flags.data_ptr(), cluster_error_flag(dev).data_ptr()
         tl = tlen.to(device=dev, dtype=torch.int32).contiguous() if tlen is not None else None
         a.tlen = _ptr(tl)
+        a.xcd_groups = int(XCD_GROUPS)
         s = _Saved()
         s.hlp, s.hup, s.c_out, s.c_carry, s.act = [], [], [], [], []
         outs = []
@@ -161,6 +169,7 @@ class _PersistLSTM(torch.autograd.Function):
         flags = torch.empty(L * nd * nrb * 64, dtype=torch.int32, device=dev)   # zeroed by the launcher
         b.flags, b.err = flags.data_ptr(), cluster_error_flag(dev).data_ptr()
         b.tlen = _ptr(s.tlen)
+        b.xcd_groups = int(XCD_GROUPS)
         dtop = dtop.contiguous() if dtop is not None else None
         dg_lp, dg, dh0, dc0, dih, dic, keep_alive = [], [], [], [], [], [], []
         for l in range(L):
