@@ -26,6 +26,7 @@
 #include <cstdlib>
 
 #include "common.h"
+#include "cell_fwd_body.h"
 
 namespace {
 
@@ -188,7 +189,7 @@ __device__ __forceinline__ void wait_ahead(int ahead) {
 
 // BPOL: cache-policy bits of the weight (B) stream's LDS-DMA loads (0 =
 // default; 2 = nt, SKR_GEMM_NT=1: CDNA4 guide "nt-weights").
-template <int BN, int NS, bool CBF16 = false, int BPOL = 0>
+template <int BN, int NS, bool CBF16 = false, int BPOL = 0, bool SC1 = false>
 __device__ __forceinline__ void glds_tile(const __hip_bfloat16* __restrict__ A, int64_t lda,
                                           const __hip_bfloat16* __restrict__ Bt, int64_t ldb,
                                           void* __restrict__ Cv, int64_t ldc, int M, int n0, int64_t k0, int kslice,
@@ -278,6 +279,9 @@ __device__ __forceinline__ void glds_tile(const __hip_bfloat16* __restrict__ A, 
                 const int row = 32 * w + 16 * i + fq * 4 + e;
                 if (row < M) {
                     if constexpr (CBF16) ((__hip_bfloat16*)Cv)[row * ldc + n0 + 16 * j + fr] = skr::to_bf16(acc[i][j][e]);
+                    else if constexpr (SC1)   // write-through: read by other workgroups of this launch
+                        __hip_atomic_store((uint32_t*)Cv + row * ldc + n0 + 16 * j + fr,
+                                           __float_as_uint(acc[i][j][e]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     else ((float*)Cv)[row * ldc + n0 + 16 * j + fr] = acc[i][j][e];
                 }
             }
@@ -471,6 +475,63 @@ __global__ __launch_bounds__(256) void skinny_gemm_group_ra_kernel(const GemmGro
     const int kslice = p.K / p.splits;
     glds_tile_ra<BN, NSB>((const __hip_bfloat16*)p.A, p.lda, (const __hip_bfloat16*)p.Bt, p.ldb, p.C + split * p.c_slab,
                           p.ldc, p.M, nt * BN, (int64_t)split * kslice, kslice, smem);
+}
+
+// Grouped launch with the HyperLSTM's hyper cell in its tail (forward).
+// Problem 0 is the hyper gates' product R_hyp = [h | hh] @ W_y (its
+// workgroups get the lowest ids, so they are dispatched first and are all
+// resident); the other problems (R_main) run as in skinny_gemm_group_kernel.
+// A problem-0 workgroup stores its split-K slab write-through (sc1), drains,
+// and adds one to the step's arrival counter; once all n0 have arrived
+// (bounded relaxed poll by one lane, then ONE agent-scope acquire for the
+// workgroup: CDNA4 guide Guideline 16) it runs the hyper cell
+// (csrc/cell_fwd_body.h: LayerNorm LSTM, 256 units, 4 slabs, one row per
+// workgroup pass) for rows local, local + n0, ... So the cell overlaps the
+// R_main weight stream instead of costing its own launch.
+constexpr unsigned kFuseSpinLimit = 1u << 22;
+
+template <int BN, int NS, int HNS>
+__global__ __launch_bounds__(256) void skinny_gemm_group_hyper_kernel(const GemmGroup g, const FwdArgs hc,
+                                                                      int* __restrict__ counter, int* __restrict__ err) {
+    extern __shared__ __attribute__((aligned(16))) __hip_bfloat16 smem[];
+    const int id = blockIdx.x;
+    int q = 0;
+#pragma unroll
+    for (int i = 1; i < kMaxGroup; ++i) q += (i < g.n && id >= g.start[i]) ? 1 : 0;
+    const GemmProblem& p = g.p[q];
+    const int local = id - g.start[q];
+    const int ntiles = p.N / BN;
+    const int split = local / ntiles, nt = local - split * ntiles;
+    const int kslice = p.K / p.splits;
+    if (q != 0) {
+        glds_tile<BN, NS>((const __hip_bfloat16*)p.A, p.lda, (const __hip_bfloat16*)p.Bt, p.ldb, p.C + split * p.c_slab,
+                          p.ldc, p.M, nt * BN, (int64_t)split * kslice, kslice, smem);
+        return;
+    }
+    glds_tile<BN, NS, false, 0, true>((const __hip_bfloat16*)p.A, p.lda, (const __hip_bfloat16*)p.Bt, p.ldb,
+                                      p.C + split * p.c_slab, p.ldc, p.M, nt * BN, (int64_t)split * kslice, kslice,
+                                      smem);
+    const int n0 = g.start[1];
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave drains its sc1 slab stores
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __hip_atomic_fetch_add(counter, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        unsigned spins = 0;
+        while (__hip_atomic_load(counter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < n0) {
+            __builtin_amdgcn_s_sleep(1);
+            if (++spins > kFuseSpinLimit) {
+                __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                break;
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
+    for (int b = local; b < hc.B; b += n0) {
+        cell_fwd_body<256, 1, HNS, true, 0>(hc, 0, b, 1);
+        __syncthreads();   // the body's LDS scratch is reused by the next row
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -969,6 +1030,57 @@ SKR_API int skr_skinny_gemm_group(const GemmProblem* probs, int n, int bn, hipSt
     if (bn == 128) return g_nstage == 3 ? launch_group<128, 3>(g, s) : launch_group<128, 4>(g, s);
     return g_nstage == 3 ? launch_group<64, 3>(g, s) : g_nstage == 6 ? launch_group<64, 6>(g, s)
                                                                     : launch_group<64, 4>(g, s);
+}
+
+// Grouped bf16 products with the hyper cell fused into the tail (see
+// skinny_gemm_group_hyper_kernel). probs[0] = R_hyp ([B, 4*256] over 4
+// splits: the slabs hc->R points at), probs[1..] = other independent
+// products; hc = the hyper cell's forward arguments (training-mode LayerNorm
+// cell, H = 256, one workgroup per row); counter = an int zeroed before the
+// sequence (one per step); err = timeout flag (the trainers raise on it).
+SKR_API int skr_skinny_gemm_group_hyper(const GemmProblem* probs, int n, const FwdArgs* hc, int* counter, int* err,
+                                        hipStream_t s) {
+    if (n < 1 || n > kMaxGroup || hc == nullptr || counter == nullptr || err == nullptr) return -2;
+    const GemmProblem& h = probs[0];
+    if (hc->H != 256 || (hc->R_nslab != 4 && hc->R_nslab != 9) || h.splits != hc->R_nslab || h.N != 4 * hc->H ||
+        h.M != hc->B || hc->cluster > 1 ||
+        (const void*)hc->R != (const void*)h.C || h.c_slab != hc->R_slab || h.ldc != hc->ld_R)
+        return -3;
+    if (hc->ln_g == nullptr) return -3;   // LayerNorm cell only
+    if (g_nstage != 3 || areg_on()) return -5;
+    GemmGroup g{};
+    g.n = n;
+    g.start[0] = 0;
+    for (int i = 0; i < n; ++i) {
+        const GemmProblem& p = probs[i];
+        if (p.M < 1 || p.M > BM || p.N % 64 != 0 || p.splits < 1 || p.K % p.splits != 0) return -2;
+        if ((p.K / p.splits) % BK != 0 || p.lda % 8 != 0 || p.ldb % 8 != 0) return -3;
+        if (((uintptr_t)p.A | (uintptr_t)p.Bt) & 15) return -4;
+        g.p[i] = p;
+        g.start[i + 1] = g.start[i] + (p.N / 64) * p.splits;
+    }
+    for (int i = n + 1; i <= kMaxGroup; ++i) g.start[i] = g.start[n];
+    // the problem-0 workgroups wait for each other: they are dispatched first
+    // and must all fit on the chip at once (one per CU is always possible)
+    static int cus = 0;   // queried on the first (eager) call, before any graph capture
+    if (cus == 0) {
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+            return -8;
+    }
+    if (g.start[1] > cus) return -8;
+    const size_t lds = (size_t)3 * (BM + 64) * BK * 2;
+    if (hc->R_nslab == 9) {
+        set_lds_attr(skinny_gemm_group_hyper_kernel<64, 3, 9>, lds);
+        hipLaunchKernelGGL((skinny_gemm_group_hyper_kernel<64, 3, 9>), dim3(g.start[g.n]), dim3(256), lds, s, g, *hc,
+                           counter, err);
+    } else {
+        set_lds_attr(skinny_gemm_group_hyper_kernel<64, 3, 4>, lds);
+        hipLaunchKernelGGL((skinny_gemm_group_hyper_kernel<64, 3, 4>), dim3(g.start[g.n]), dim3(256), lds, s, g, *hc,
+                           counter, err);
+    }
+    return SKR_CHECK_LAUNCH();
 }
 
 // fp32 operands: same contract as skr_skinny_gemm_v2 with kslice % 32 == 0

@@ -197,6 +197,28 @@ def rec_gemm_group(jobs) -> None:
         raise RuntimeError("skr_skinny_gemm_group failed (%d)" % rc)
 
 
+def rec_gemm_group_hyper(jobs, hyper_args, counter: torch.Tensor, err: torch.Tensor) -> None:
+    """:func:`rec_gemm_group` whose first job is the HyperLSTM hyper gates'
+    product (4 splits into the slabs the hyper cell reads) with the hyper
+    cell's forward step (``hyper_args``, a filled ``LstmFwdArgs``) run in the
+    launch's tail (csrc/skinny_gemm.hip ``skr_skinny_gemm_group_hyper``).
+    ``counter``: one zeroed int32 per call; ``err``: the timeout flag."""
+    import ctypes
+    from ..utils import native
+    from ._hipapi import GemmProblem
+    lib = native.require_hip()
+    probs = (GemmProblem * len(jobs))()
+    for p, (a, bt, out, s) in zip(probs, jobs):
+        N, K = bt.shape[-2], bt.shape[-1]
+        p.A, p.lda, p.Bt, p.ldb = a.data_ptr(), a.stride(0), bt.data_ptr(), bt.stride(-2)
+        p.C, p.ldc, p.c_slab = out.data_ptr(), N, out.stride(0)
+        p.M, p.N, p.K, p.splits = a.shape[0], N, K, s
+    rc = lib.lib.skr_skinny_gemm_group_hyper(probs, len(jobs), ctypes.byref(hyper_args), counter.data_ptr(),
+                                             err.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    if rc != 0:
+        raise RuntimeError("skr_skinny_gemm_group_hyper failed (%d)" % rc)
+
+
 # ---- inference-time helpers ------------------------------------------------------------
 _WCACHE = {}
 WEIGHTS_EPOCH = [0]

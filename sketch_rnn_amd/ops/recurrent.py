@@ -518,6 +518,11 @@ PERSIST_LENGTHS = os.environ.get("SKR_PERSIST_LENGTHS", "1") != "0"
 # =====================================================================================
 # HyperLSTM sequence
 # =====================================================================================
+# Hyper cell fused into the tail of the grouped forward GEMM launch
+# (csrc/skinny_gemm.hip skinny_gemm_group_hyper_kernel): one launch per
+# forward step fewer. SKR_HYPER_FUSE=0 keeps the separate hyper-cell launch.
+HYPER_FUSE = os.environ.get("SKR_HYPER_FUSE", "0") == "1"
+HYPER_FUSE_SPLITS = int(os.environ.get("SKR_HYPER_FUSE_SPLITS", "9"))   # 4 or 9
 _SIDE_STREAMS = {}
 # Unfolded modulation vectors (csrc/hyper_vec.hip, SKR_UNFOLD_VEC=1): reads
 # 1.7 MB of weights per step instead of the folded P (12.6 MB) but measured
@@ -865,22 +870,38 @@ class _HyperSeq(torch.autograd.Function):
         main, side = torch.cuda.current_stream(), _side_stream(dev)
         st = main.cuda_stream
         group = not fp8 and not TWO_STREAM and gemm.GROUPED and S_m >= 1 and S_y >= 1 and dt == torch.bfloat16
+        # hyper cell in the grouped launch's tail (training: LayerNorm saves on)
+        fuse = HYPER_FUSE and group and not infer and Hh == 256 and S_y >= 1 and clh.C == 1 and B <= 128 and \
+            (K // 64) % HYPER_FUSE_SPLITS == 0
+        if fuse:
+            # more, shorter R_hyp workgroups: each finishes its K slice sooner and
+            # runs about one cell row in the tail (HYPER_FUSE_SPLITS = 9 at K = 2304)
+            S_y = HYPER_FUSE_SPLITS
+            ah.R_nslab = S_y
+            RY = torch.empty(S_y, B, Gh, device=dev, dtype=f32)
+            ah.R = RY.data_ptr()
+            fcnt = torch.zeros(T, dtype=torch.int32, device=dev)     # per-step arrival counters
+            ferr = cluster_error_flag(dev)
         for t in range(T):
             clm.set(am, t)
             clh.set(ah, t)
-            if group:   # R_main and R_hyp in one launch
-                gemm.rec_gemm_group([(A[t, :, :H], WhT, RM[rmi(t)], S_m), (A[t], WyT, RY, S_y)])
-            else:
-                _join(side, main)                        # h_{t-1} written
-                with torch.cuda.stream(side):
-                    rgemm(A[t, :, :H], WhT, RM[rmi(t)], S_m)
-                rgemm(A[t], WyT, RY, S_y)
             ah.xp, ah.c_prev, ah.step = XHY[t].data_ptr(), HCC[t].data_ptr(), t
             ah.h_out = HH[t].data_ptr()
             if not infer:
                 ah.xhat, ah.rstd, ah.chat = HXHAT[t].data_ptr(), HRSTD[t].data_ptr(), HCHAT[t].data_ptr()
             ah.h_lp, ah.c_carry = A[t + 1, :, H:].data_ptr(), HCC[t + 1].data_ptr()
-            _check(lib.lib.skr_lstm_fwd_step(ctypes.byref(ah), 1, 0, st), "hyper_fwd_step")
+            if fuse:    # R_hyp (+ the hyper cell in the tail) and R_main in one launch
+                gemm.rec_gemm_group_hyper([(A[t], WyT, RY, S_y), (A[t, :, :H], WhT, RM[rmi(t)], S_m)], ah,
+                                          fcnt[t:t + 1], ferr)
+            else:
+                if group:   # R_main and R_hyp in one launch
+                    gemm.rec_gemm_group([(A[t, :, :H], WhT, RM[rmi(t)], S_m), (A[t], WyT, RY, S_y)])
+                else:
+                    _join(side, main)                        # h_{t-1} written
+                    with torch.cuda.stream(side):
+                        rgemm(A[t, :, :H], WhT, RM[rmi(t)], S_m)
+                    rgemm(A[t], WyT, RY, S_y)
+                _check(lib.lib.skr_lstm_fwd_step(ctypes.byref(ah), 1, 0, st), "hyper_fwd_step")
             if unfold:
                 _check(lib.lib.skr_hyper_vec_fwd(A[t + 1, :, H:].data_ptr(), K, WzT.data_ptr(), WaT.data_ptr(),
                                                  VEC[t].data_ptr(), H, 12 * H, B, H, Hh, st), "hyper_vec_fwd")

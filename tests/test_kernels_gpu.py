@@ -279,6 +279,61 @@ def test_hyper_grouped_gemm_path_bitwise(H, Hh, E):
         assert torch.equal(a, b)
 
 
+@pytest.mark.parametrize("B,hkeep,splits", [(100, 0.9, 4), (37, 1.0, 4), (100, 0.9, 9)])
+def test_hyper_cell_fused_into_group_gemm_bitwise(B, hkeep, splits):
+    """bf16 HyperLSTM (vae_large shapes) with the hyper cell run in the tail
+    of the grouped forward GEMM launch equals the separate hyper-cell launch:
+    with the same 4 split-K slabs bit for bit (outputs, final states, every
+    gradient: same GEMM tiles, same cell code, the slabs travel write-through
+    inside the launch); with 9 slabs (the default) to fp32 summation order."""
+    from sketch_rnn_amd.ops import gemm, recurrent
+    torch.manual_seed(6)
+    T, IN, Z, H, Hh, E = 6, 5, 16, 2048, 256, 32
+    p = C.HyperLSTMParams(IN + Z, H, Hh, E).to(DEV)
+    with torch.no_grad():
+        for prm in p.parameters():
+            prm.add_(torch.randn_like(prm) * 0.02)
+    x = torch.randn(T, B, IN, device=DEV)
+    z = torch.randn(B, Z, device=DEV)
+    st = [torch.randn(B, n, device=DEV) * 0.1 for n in (H, H, Hh, Hh)]
+    w = torch.randn(T, B, H, device=DEV)
+    calls = []
+    orig = gemm.rec_gemm_group_hyper
+
+    def spy(*a, **k):
+        calls.append(1)
+        return orig(*a, **k)
+
+    res = []
+    saved = recurrent.HYPER_FUSE, recurrent.HYPER_FUSE_SPLITS
+    recurrent.HYPER_FUSE_SPLITS = splits
+    try:
+        ops.set_compute_dtype("bf16")
+        ops.set_backend("hip")
+        gemm.rec_gemm_group_hyper = spy
+        for fuse in (False, True):
+            recurrent.HYPER_FUSE = fuse
+            p.zero_grad()
+            zg = z.detach().clone().requires_grad_()
+            out, fin = recurrent.hyper_sequence_hip(p, x, *st, drop_keep=0.9, drop_seed=3, drop_stream=9,
+                                                    hyp_drop_keep=hkeep, zc=zg)
+            (out * w).sum().backward()
+            torch.cuda.synchronize()
+            res.append([out.detach()] + [f.detach() for f in fin] + [zg.grad] + [q.grad.clone() for q in p.parameters()])
+    finally:
+        recurrent.HYPER_FUSE, recurrent.HYPER_FUSE_SPLITS = saved
+        gemm.rec_gemm_group_hyper = orig
+        ops.set_compute_dtype("fp32")
+    assert len(calls) == T, calls    # the fused launch ran once per forward step
+    names = ["out", "h", "c", "hh", "hc", "dz"] + [n for n, _ in p.named_parameters()]
+    for n, a, b in zip(names, *res):
+        if splits == 4:
+            assert torch.equal(a, b), (n, float((a.float() - b.float()).abs().max()))
+        else:
+            err = (a.float() - b.float()).abs().max().item()
+            assert err <= 1e-2 * max(b.float().abs().max().item(), 1e-3), (n, err)
+
+
 @pytest.mark.parametrize("H,Hh,E,B", [(2048, 256, 32, 100), (512, 64, 8, 70)])
 def test_hyper_batch_split_matches_unsplit(H, Hh, E, B):
     """bf16 HyperLSTM with the batch cut into independent chains on two
