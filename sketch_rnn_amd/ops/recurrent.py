@@ -520,7 +520,12 @@ PERSIST_LENGTHS = os.environ.get("SKR_PERSIST_LENGTHS", "1") != "0"
 # =====================================================================================
 # Hyper cell fused into the tail of the grouped forward GEMM launch
 # (csrc/skinny_gemm.hip skinny_gemm_group_hyper_kernel): one launch per
-# forward step fewer. SKR_HYPER_FUSE=0 keeps the separate hyper-cell launch.
+# forward step fewer. OPT-IN (SKR_HYPER_FUSE=1): measured on MI355X, same
+# box, A/B twice -- 4 R_hyp splits 27.53 / 27.59 vs 26.89 / 26.97 ms/step
+# (the 64 workgroups' barrier + acquire + two cell rows each outlast the
+# R_main stream), 9 splits 26.81 / 26.83 vs 26.93 / 26.92 (+0.4 %, within
+# box-to-box spread; profiles/r2s5/hyper_fuse_ab.txt) -- not worth an
+# in-launch spin-wait in the default path.
 HYPER_FUSE = os.environ.get("SKR_HYPER_FUSE", "0") == "1"
 HYPER_FUSE_SPLITS = int(os.environ.get("SKR_HYPER_FUSE_SPLITS", "9"))   # 4 or 9
 _SIDE_STREAMS = {}

@@ -330,8 +330,8 @@ def test_hyper_cell_fused_into_group_gemm_bitwise(B, hkeep, splits):
         if splits == 4:
             assert torch.equal(a, b), (n, float((a.float() - b.float()).abs().max()))
         else:
-            err = (a.float() - b.float()).abs().max().item()
-            assert err <= 1e-2 * max(b.float().abs().max().item(), 1e-3), (n, err)
+            err = (a.float() - b.float()).abs().max().item()   # 9 vs 4 split-K partial sums
+            assert err <= 2e-2 * max(b.float().abs().max().item(), 1e-3), (n, err)
 
 
 @pytest.mark.parametrize("H,Hh,E,B", [(2048, 256, 32, 100), (512, 64, 8, 70)])
