@@ -46,6 +46,7 @@ for s in "${steps[@]}"; do
         ab_xcd_ref) SKR_PERSIST_XCD=0 run ref_xcd0 600 python scripts/bench_reference.py --dtype bf16 && SKR_PERSIST_XCD=1 run ref_xcd1 600 python scripts/bench_reference.py --dtype bf16 ;;
         bench_dp1) run bench_dp1 600 python scripts/bench_dp1.py ;;
         ab_hfuse) SKR_HYPER_FUSE=0 run bench_hf0 600 python bench.py --steps 20 --warmup 3 && SKR_HYPER_FUSE=1 run bench_hf1 600 python bench.py --steps 20 --warmup 3 && SKR_HYPER_FUSE=0 run bench_hf0b 600 python bench.py --steps 20 --warmup 3 && SKR_HYPER_FUSE=1 run bench_hf1b 600 python bench.py --steps 20 --warmup 3 ;;
+        ab_say) SKR_HYP_SAY=8 run bench_say8 600 python bench.py --steps 20 --warmup 3 && SKR_HYP_SAY=4 run bench_say4 600 python bench.py --steps 20 --warmup 3 && SKR_HYP_SAY=8 run bench_say8b 600 python bench.py --steps 20 --warmup 3 && SKR_HYP_SAY=4 run bench_say4b 600 python bench.py --steps 20 --warmup 3 ;;
         bench_nofused) SKR_FUSED=0 run bench_nofused 600 python bench.py --steps 10 --warmup 2 ;;
         bench_wgrad) run bench_wgrad 600 python scripts/bench_wgrad.py ;;
         bench_gemm) run bench_gemm 600 python scripts/bench_gemm.py ;;

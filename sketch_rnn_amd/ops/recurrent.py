@@ -962,7 +962,13 @@ class _HyperSeq(torch.autograd.Function):
         dVEC = torch.empty(T, B, 12 * H, device=dev, dtype=ldt)
         S_h = _split_override("SKR_HYP_SH", gemm.plan_splits(B, Hh, 12 * H, 1, ldt), 12 * H)
         S_am = _split_override("SKR_HYP_SAM", gemm.plan_splits(B, H, G, 1, ldt), G)
-        S_ay = _split_override("SKR_HYP_SAY", gemm.plan_splits(B, K, Gh, 1, ldt), Gh)
+        # d[h | hh] = dR_hyp @ W_y^T: at most 4 split-K slabs -- the next step's
+        # two cells read every slab; measured on MI355X (vae_large, same box,
+        # A/B twice): 4 slabs 26.67 / 26.57 vs 8 (the plan) 26.76 / 26.86 ms/step
+        S_ay = gemm.plan_splits(B, K, Gh, 1, ldt)
+        if S_ay > 4:
+            S_ay = next(d for d in (4, 3, 2, 1) if (Gh // 64) % d == 0)
+        S_ay = _split_override("SKR_HYP_SAY", S_ay, Gh)
         DHZ = torch.empty(max(S_h, 1), B, Hh, device=dev, dtype=f32)    # slabs of dhh from the vec path
         DAM = torch.zeros(max(S_am, 1), B, H, device=dev, dtype=f32)    # slabs of dh from the main gates
         DAY = torch.zeros(max(S_ay, 1), B, K, device=dev, dtype=f32)    # slabs of d[h | hh] from the hyper gates
