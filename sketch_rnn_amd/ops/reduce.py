@@ -42,4 +42,7 @@ def colsum(x: torch.Tensor, y: Optional[torch.Tensor] = None, splits: Optional[i
                             torch.cuda.current_stream().cuda_stream)
     if rc != 0:
         raise RuntimeError("skr_colsum failed (%d)" % rc)
-    return (part[0].sum(0) if y is not None else None), part[1].sum(0)
+    if y is None:
+        return None, part[1].sum(0)
+    tot = part.sum(1)   # both second passes in one reduction launch
+    return tot[0], tot[1]
