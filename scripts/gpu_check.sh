@@ -48,6 +48,7 @@ for s in "${steps[@]}"; do
         ab_hfuse) SKR_HYPER_FUSE=0 run bench_hf0 600 python bench.py --steps 20 --warmup 3 && SKR_HYPER_FUSE=1 run bench_hf1 600 python bench.py --steps 20 --warmup 3 && SKR_HYPER_FUSE=0 run bench_hf0b 600 python bench.py --steps 20 --warmup 3 && SKR_HYPER_FUSE=1 run bench_hf1b 600 python bench.py --steps 20 --warmup 3 ;;
         ab_say) SKR_HYP_SAY=8 run bench_say8 600 python bench.py --steps 20 --warmup 3 && SKR_HYP_SAY=4 run bench_say4 600 python bench.py --steps 20 --warmup 3 && SKR_HYP_SAY=8 run bench_say8b 600 python bench.py --steps 20 --warmup 3 && SKR_HYP_SAY=4 run bench_say4b 600 python bench.py --steps 20 --warmup 3 ;;
         ab_splits) run bench_def 600 python bench.py --steps 20 --warmup 3 && SKR_HYP_SH=16 run bench_sh16 600 python bench.py --steps 20 --warmup 3 && SKR_HYP_SY=2 run bench_sy2 600 python bench.py --steps 20 --warmup 3 && run bench_defb 600 python bench.py --steps 20 --warmup 3 && SKR_HYP_SH=16 run bench_sh16b 600 python bench.py --steps 20 --warmup 3 && SKR_HYP_SY=2 run bench_sy2b 600 python bench.py --steps 20 --warmup 3 ;;
+        ab_headdw) run bench_hd16 600 python bench.py --steps 20 --warmup 3 && SKR_HEAD_DW_SLABS=64 run bench_hd64 600 python bench.py --steps 20 --warmup 3 && SKR_HEAD_DW_SLABS=32 run bench_hd32 600 python bench.py --steps 20 --warmup 3 && run bench_hd16b 600 python bench.py --steps 20 --warmup 3 && SKR_HEAD_DW_SLABS=64 run bench_hd64b 600 python bench.py --steps 20 --warmup 3 && SKR_HEAD_DW_SLABS=32 run bench_hd32b 600 python bench.py --steps 20 --warmup 3 ;;
         bench_nofused) SKR_FUSED=0 run bench_nofused 600 python bench.py --steps 10 --warmup 2 ;;
         bench_wgrad) run bench_wgrad 600 python scripts/bench_wgrad.py ;;
         bench_gemm) run bench_gemm 600 python scripts/bench_gemm.py ;;

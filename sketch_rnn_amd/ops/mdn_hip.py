@@ -5,10 +5,18 @@ from __future__ import annotations
 
 import ctypes as C
 import math
+import os
 
 import torch
 
 from ..utils import native
+
+# Row slabs of the head's [dW; db] reduction (csrc/mdn_head.hip mdn_head_dw):
+# each workgroup's row loop is latency-bound, so more slabs = more loads in
+# flight. Measured on MI355X (vae_large, same box, A/B twice): 16 slabs
+# 26.72 / 26.65, 32 slabs 26.59 / 26.62, 64 slabs 26.62 / 26.62 ms/step.
+# SKR_HEAD_DW_SLABS overrides.
+HEAD_DW_SLABS = int(os.environ.get("SKR_HEAD_DW_SLABS", "32"))
 
 
 def _stream() -> int:
@@ -137,7 +145,7 @@ class _MDNHead(torch.autograd.Function):
                 raise RuntimeError("skr_mdn_head_dx failed (%d)" % rc)
             dX = dX.view(ctx.xshape)
         if ctx.needs_input_grad[1] or ctx.needs_input_grad[2]:
-            S = 16
+            S = HEAD_DW_SLABS   # row slabs: workgroups = (Hd/64 + 1) * S, each a latency-bound row loop
             rows_per = (-(-N // S) + 31) // 32 * 32
             S = -(-N // rows_per)
             slab = torch.empty(S, Hd + 64, NOUTP, device=dev, dtype=torch.float32)
