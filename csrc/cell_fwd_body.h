@@ -15,6 +15,21 @@ constexpr int kRecSlabs = 8;      // ceiling of the unrolled dh_rec / dh_rec2 sl
 constexpr unsigned kSpinLimit = 1u << 21;
 constexpr int kSlots = 16;        // 8-byte granules per workgroup slot (128 B)
 
+// Diagnostic build only (csrc/bench/cell_bench.hip defines SKR_TRACE_CELL):
+// s_memrealtime stamps per workgroup at entry / loads landed / after each
+// LayerNorm exchange / stores drained.
+#ifdef SKR_TRACE_CELL
+__device__ uint64_t* g_cell_trace;
+#define SKR_STAMP(i)                                                                              \
+    do {                                                                                          \
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");                                          \
+        if (g_cell_trace && threadIdx.x == 0)                                                     \
+            g_cell_trace[((int64_t)b * C + c) * 8 + (i)] = __builtin_amdgcn_s_memrealtime();      \
+    } while (0)
+#else
+#define SKR_STAMP(i) do {} while (0)
+#endif
+
 // Publish `nv` floats of this workgroup (LDS `mine`) as tagged granules and
 // gather the row's C*nv values into LDS `all` ([C][nv]).
 __device__ void cluster_allgather(uint64_t* part, int* err, int b, int c, int C, const float* mine, int nv,
@@ -85,6 +100,7 @@ __device__ __forceinline__ void cell_fwd_body(const FwdArgs& a, const int c, con
     // xhat / rstd / chat only -- the backward recomputes the gate activations
     // from xhat -- plain layers save act
     const bool save = LN ? a.xhat != nullptr : a.act != nullptr;
+    SKR_STAMP(0);
 
     // ---- every load up front (clamped indices; results of u >= H discarded)
     float g[UPT][4], cp[UPT], lg[UPT][4], lb[UPT][4], lcg[UPT], lcb[UPT];
@@ -125,6 +141,7 @@ __device__ __forceinline__ void cell_fwd_body(const FwdArgs& a, const int c, con
     // The saves (xhat, bf16 R, c') are stored only after the second
     // exchange: stores queued on a CU delay its in-launch hand-offs.
     float xs[UPT][4];   // xhat (LN)
+    SKR_STAMP(1);
     if (LN) {
         float s[8];
 #pragma unroll
@@ -139,6 +156,7 @@ __device__ __forceinline__ void cell_fwd_body(const FwdArgs& a, const int c, con
             }
         }
         row_sum<8, NW>(s, lds, mine, all, a.part, a.err, a.step + 1, b, c, C);
+        SKR_STAMP(2);
         float mean[4], var[4];
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
@@ -191,6 +209,7 @@ __device__ __forceinline__ void cell_fwd_body(const FwdArgs& a, const int c, con
             s2[1] += cn[k] * cn[k];
         }
         row_sum<2, NW>(s2, lds, mine, all, a.part + (int64_t)a.B * C * kSlots, a.err, a.step + 1, b, c, C);
+        SKR_STAMP(3);
         const float mean = s2[0] / (float)H;
         const float var = fmaxf(s2[1] / (float)H - mean * mean, 0.f);
         const float rc = rsqrtf(var + kLnEps);
@@ -232,6 +251,7 @@ __device__ __forceinline__ void cell_fwd_body(const FwdArgs& a, const int c, con
         else if (a.lp_kind == 2) ((float*)a.h_lp)[b * a.ld_lp + u] = hc;
         else if (a.lp_kind == 3) ((uint8_t*)a.h_lp)[b * a.ld_lp + u] = to_fp8(hc * kFp8ActScale);
     }
+    SKR_STAMP(4);
 }
 
 }  // namespace

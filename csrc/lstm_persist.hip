@@ -84,7 +84,6 @@ struct PFwdArgs {
     uint32_t* flags;                          // [L][nd][nrb][kFlagStride] epochs (zeroed per launch)
     int* err;
     const int* tlen;                          // [B] valid lengths (L = 1) or null, see row_block_steps
-    int xcd_groups;                           // 1: XCD-aware block remap (xcd_group_bid)
 };
 
 struct PBwdLayer {
@@ -108,7 +107,6 @@ struct PBwdArgs {
     uint32_t* flags;
     int* err;
     const int* tlen;                          // as PFwdArgs::tlen (the same lengths as the forward)
-    int xcd_groups;                           // as PFwdArgs::xcd_groups
 };
 
 namespace {
@@ -335,23 +333,12 @@ __device__ void fwd_body(const PFwdArgs& a, int l, int g, int rb, int wu, unsign
     (void)ok;
 }
 
-// Speed-only block remap: with exactly 8 (layer, direction, row block)
-// groups -- the biLSTM encoder (2 x 4 row blocks) and the 2-layer reference
-// stack (2 x 4) -- group = blockIdx % 8, so a group's NW workgroups, which
-// hand h (dG) to each other every step, share one XCD under the round-robin
-// dispatch (CDNA4 guide T1). Correctness never depends on it: every hand-off
-// is the placement-independent sc1 protocol of handoff.h. Opt-in
-// (xcd_groups): measured slower than the linear order (ops/persist.py).
-__device__ __forceinline__ int xcd_group_bid(int bid, int ngroups, int NW, int on) {
-    return (on && ngroups == 8) ? (bid % 8) * NW + bid / 8 : bid;
-}
-
 template <int H, int MTW>
 __global__ __launch_bounds__(NTHR) void lstm_persist_fwd(const PFwdArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     constexpr int NW = H / U;
     const int per_l = a.nd * a.nrb * NW;
-    int bid = xcd_group_bid(blockIdx.x, a.L * a.nd * a.nrb, NW, a.xcd_groups);
+    int bid = blockIdx.x;
     const int l = bid / per_l;
     bid -= l * per_l;
     const int g = bid / (a.nrb * NW);
@@ -580,7 +567,7 @@ __global__ __launch_bounds__(NTHR) void lstm_persist_bwd(const PBwdArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     constexpr int NW = H / U;
     const int per_l = a.nd * a.nrb * NW;
-    int bid = xcd_group_bid(blockIdx.x, a.L * a.nd * a.nrb, NW, a.xcd_groups);
+    int bid = blockIdx.x;
     const int l = bid / per_l;
     bid -= l * per_l;
     const int g = bid / (a.nrb * NW);

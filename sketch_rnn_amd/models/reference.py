@@ -81,7 +81,7 @@ class SketchRNN(nn.Module):
         inp = xt
         final = []
         L = len(self.layers)
-        if cfg.model == "lstm" and L <= 2 and ops.use_hip(x) and persist.persist_ok(cfg.rnn_size, 1, L):
+        if cfg.model == "lstm" and L <= 2 and ops.use_hip(x) and persist.persist_ok(cfg.rnn_size, 1, L, B=B):
             # the whole stack as ONE persistent launch (csrc/lstm_persist.hip):
             # layer 1's input projection runs inside the recurrence, so the
             # two layers advance as a wavefront

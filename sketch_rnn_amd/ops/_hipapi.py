@@ -169,7 +169,6 @@ class PFwdArgs(C.Structure):
         ("flags", _p),
         ("err", _p),
         ("tlen", _p),
-        ("xcd_groups", _i),
     ]
 
 
@@ -197,25 +196,6 @@ class PBwdArgs(C.Structure):
         ("flags", _p),
         ("err", _p),
         ("tlen", _p),
-        ("xcd_groups", _i),
-    ]
-
-
-class WFwdArgs(C.Structure):
-    """Mirror of ``WFwdArgs`` in csrc/lstm_wide.hip (wide persistent LN-LSTM)."""
-    _fields_ = [
-        ("T", _i), ("B", _i), ("H", _i),
-        ("WT", _p),
-        ("xp", _p), ("xp_ts", _i64), ("xp_ld", _i64),
-        ("c0", _p),
-        ("ln_g", _p), ("ln_b", _p), ("lnc_g", _p), ("lnc_b", _p),
-        ("forget_bias", _f), ("keep", _f),
-        ("seed", _p), ("stream", _u32),
-        ("hlp", _p), ("ldh", _i64),
-        ("gbuf", _p), ("h_out", _p), ("cc", _p),
-        ("xhat", _p), ("rstd", _p), ("chat", _p),
-        ("flags", _p), ("err", _p),
-        ("trace", _p),
     ]
 
 
@@ -303,7 +283,7 @@ class HipLib:
         lib.skr_adam_step.restype = _i
         lib.skr_global_norm.argtypes = [_p, _i64, _p, _p, _p]
         lib.skr_global_norm.restype = _i
-        for fn in (lib.skr_skinny_gemm, lib.skr_skinny_gemm_v2):
+        for fn in (lib.skr_skinny_gemm_v2,):
             fn.argtypes = [_p, _i64, _i64, _p, _i64, _i64, _p, _i64, _i64, _i64, _i, _i, _i, _i, _i, _i, _p]
             fn.restype = _i
         lib.skr_skinny_gemm_f32.argtypes = [_p, _i64, _i64, _p, _i64, _i64, _p, _i64, _i64, _i64, _i, _i, _i, _i, _i,
@@ -337,8 +317,6 @@ class HipLib:
         lib.skr_gemm_set_nstage.restype = _i
         lib.skr_skinny_gemm_group.argtypes = [C.POINTER(GemmProblem), _i, _i, _p]
         lib.skr_skinny_gemm_group.restype = _i
-        lib.skr_skinny_gemm_group_hyper.argtypes = [C.POINTER(GemmProblem), _i, C.POINTER(LstmFwdArgs), _p, _p, _p]
-        lib.skr_skinny_gemm_group_hyper.restype = _i
         lib.skr_lstm_fused_fwd.argtypes = [C.POINTER(FusedFwdArgs), _p]
         lib.skr_lstm_fused_fwd.restype = _i
         lib.skr_lstm_fused_bwd.argtypes = [C.POINTER(FusedBwdArgs), _p]
@@ -355,12 +333,6 @@ class HipLib:
         lib.skr_mdn_head_dx.restype = _i
         lib.skr_mdn_head_dw.argtypes = [C.POINTER(HeadDw), _i, _i, _p, _p, _p]
         lib.skr_mdn_head_dw.restype = _i
-        lib.skr_lstm_wide_fwd.argtypes = [C.POINTER(WFwdArgs), _p]
-        lib.skr_lstm_wide_fwd.restype = _i
-        lib.skr_lstm_wide_flag_words.argtypes = [_i, _i]
-        lib.skr_lstm_wide_flag_words.restype = _i
-        lib.skr_hyper_vec_fwd.argtypes = [_p, _i64, _p, _p, _p, _i64, _i64, _i, _i, _i, _p]
-        lib.skr_hyper_vec_fwd.restype = _i
         lib.skr_skinny_gemm_fp8_v2.argtypes = [C.POINTER(GemmProblem8), _i, _p]
         lib.skr_skinny_gemm_fp8_v2.restype = _i
         lib.skr_skinny_gemm_group_fp8.argtypes = [C.POINTER(GemmProblem8), _i, _p]
@@ -371,17 +343,12 @@ class HipLib:
         lib.skr_hash_normal.restype = _i
         lib.skr_decode_ref.argtypes = [C.POINTER(DecArgs), _p]
         lib.skr_decode_ref.restype = _i
-        lib.skr_stream_create_cumask.argtypes = [_i, _i, _i, C.POINTER(_p)]
-        lib.skr_stream_create_cumask.restype = _i
-        lib.skr_stream_destroy.argtypes = [_p]
-        lib.skr_stream_destroy.restype = _i
         for name, cls in (("skr_lstm_fwd_args_size", LstmFwdArgs), ("skr_lstm_bwd_args_size", LstmBwdArgs),
                           ("skr_gru_fwd_args_size", GruFwdArgs), ("skr_gru_bwd_args_size", GruBwdArgs),
                           ("skr_lstm_fused_fwd_args_size", FusedFwdArgs),
                           ("skr_lstm_fused_bwd_args_size", FusedBwdArgs),
                           ("skr_lstm_persist_fwd_args_size", PFwdArgs),
                           ("skr_lstm_persist_bwd_args_size", PBwdArgs),
-                          ("skr_lstm_wide_fwd_args_size", WFwdArgs),
                           ("skr_mdn_head_fwd_args_size", HeadFwd),
                           ("skr_mdn_head_dx_args_size", HeadDx),
                           ("skr_mdn_head_dw_args_size", HeadDw),

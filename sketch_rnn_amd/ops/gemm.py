@@ -75,8 +75,6 @@ def wgrad(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
     return out if batched else out[0]
 
 
-# skinny GEMM kernel: "v2" = LDS-DMA ring (csrc/skinny_gemm.hip), "v1" = register-staged
-GEMM_ALGO = os.environ.get("SKR_GEMM", "v2")
 
 _SPLITS = (1, 2, 4, 8, 16, 32)  # powers of two: the cell kernels sum <= 8 slabs unrolled
 
@@ -139,7 +137,7 @@ def rec_gemm(a: torch.Tensor, bt: torch.Tensor, out: torch.Tensor, splits: int, 
         f32 = lib.lib.skr_skinny_gemm_f32
         fn = lambda *args: f32(*args[:-2], args[-1])   # noqa: E731  (drop bn)
     else:
-        fn = lib.lib.skr_skinny_gemm_v2 if GEMM_ALGO == "v2" else lib.lib.skr_skinny_gemm
+        fn = lib.lib.skr_skinny_gemm_v2
     if nd == 1 and M > 128:   # 128-row blocks as the kernel's batch dimension, sharing B
         mb = row_blocks(M)
         rc = fn(a.data_ptr(), a.stride(0), 128 * a.stride(0), bt.data_ptr(), bt.stride(-2), 0, out.data_ptr(), N,
@@ -177,7 +175,7 @@ def rec_gemm_group(jobs) -> None:
     (nd = 1, M <= 128, bf16, splits >= 1) in ONE grouped launch
     (csrc/skinny_gemm.hip ``skr_skinny_gemm_group``); falls back to one
     launch per product when a job does not qualify."""
-    ok = GROUPED and GEMM_ALGO == "v2" and 1 <= len(jobs) <= 4 and all(
+    ok = GROUPED and 1 <= len(jobs) <= 4 and all(
         a.is_cuda and a.dtype == _BF16 and s >= 1 and a.shape[0] <= 128 for a, _, _, s in jobs)
     if not ok:
         for a, bt, out, s in jobs:
@@ -195,28 +193,6 @@ def rec_gemm_group(jobs) -> None:
     rc = lib.lib.skr_skinny_gemm_group(probs, len(jobs), 0, torch.cuda.current_stream().cuda_stream)
     if rc != 0:
         raise RuntimeError("skr_skinny_gemm_group failed (%d)" % rc)
-
-
-def rec_gemm_group_hyper(jobs, hyper_args, counter: torch.Tensor, err: torch.Tensor) -> None:
-    """:func:`rec_gemm_group` whose first job is the HyperLSTM hyper gates'
-    product (4 splits into the slabs the hyper cell reads) with the hyper
-    cell's forward step (``hyper_args``, a filled ``LstmFwdArgs``) run in the
-    launch's tail (csrc/skinny_gemm.hip ``skr_skinny_gemm_group_hyper``).
-    ``counter``: one zeroed int32 per call; ``err``: the timeout flag."""
-    import ctypes
-    from ..utils import native
-    from ._hipapi import GemmProblem
-    lib = native.require_hip()
-    probs = (GemmProblem * len(jobs))()
-    for p, (a, bt, out, s) in zip(probs, jobs):
-        N, K = bt.shape[-2], bt.shape[-1]
-        p.A, p.lda, p.Bt, p.ldb = a.data_ptr(), a.stride(0), bt.data_ptr(), bt.stride(-2)
-        p.C, p.ldc, p.c_slab = out.data_ptr(), N, out.stride(0)
-        p.M, p.N, p.K, p.splits = a.shape[0], N, K, s
-    rc = lib.lib.skr_skinny_gemm_group_hyper(probs, len(jobs), ctypes.byref(hyper_args), counter.data_ptr(),
-                                             err.data_ptr(), torch.cuda.current_stream().cuda_stream)
-    if rc != 0:
-        raise RuntimeError("skr_skinny_gemm_group_hyper failed (%d)" % rc)
 
 
 # ---- inference-time helpers ------------------------------------------------------------

@@ -35,22 +35,32 @@ PERSIST_ENABLED = os.environ.get("SKR_PERSIST", "1") != "0"
 # debug: fill every handed-off buffer with NaN before the launch, so a read
 # that overtakes its hand-off shows up as a NaN instead of a stale value
 POISON = os.environ.get("SKR_PERSIST_POISON", "0") == "1"
-# XCD-aware block remap of the 8-group launches (csrc/lstm_persist.hip
-# xcd_group_bid), OPT-IN (SKR_PERSIST_XCD=1): measured on MI355X, same box,
-# A/B twice -- vae_large 27.42 / 27.29 vs 26.91 / 26.93 ms/step, reference
-# config bf16 4.89 vs 4.59 ms/step (profiles/r2s5/xcd_remap_ab.txt): a group's
-# 32 workgroups publishing and polling on one XCD are slower than spread
-# over all eight
-XCD_GROUPS = os.environ.get("SKR_PERSIST_XCD", "0") == "1"
 _ROWS = 32          # rows per workgroup row block (kMTW = 2 sixteen-row tiles)
 
 
-def persist_ok(H: int, nd: int = 1, L: int = 1, ln: bool = False) -> bool:
+def _cu_count() -> int:
+    if not torch.cuda.is_available():
+        return 256
+    return torch.cuda.get_device_properties(torch.cuda.current_device()).multi_processor_count
+
+
+def persist_ok(H: int, nd: int = 1, L: int = 1, ln: bool = False, B: Optional[int] = None) -> bool:
+    """Eligibility of the persistent kernels. ``B``: rows per direction; the
+    grid (L * nd * ceil(B / 32) row blocks x H / 16 workgroups) must fit one
+    workgroup per CU, since every workgroup spin-waits on its peers (the
+    launcher refuses a larger grid: -8). Callers fall back to the per-step
+    kernels otherwise."""
     if not PERSIST_ENABLED or ln or gemm.lp_dtype() != torch.bfloat16:
         return False
     if L == 2:
-        return nd == 1 and H == 256
-    return L == 1 and nd in (1, 2) and H in (256, 512)
+        shape_ok = nd == 1 and H == 256
+    else:
+        shape_ok = L == 1 and nd in (1, 2) and H in (256, 512)
+    if not shape_ok:
+        return False
+    if B is not None and L * nd * (-(-B // _ROWS)) * (H // 16) > _cu_count():
+        return False
+    return True
 
 
 def _ptr(t: Optional[torch.Tensor]):
@@ -107,7 +117,6 @@ class _PersistLSTM(torch.autograd.Function):
         a.flags, a.err = flags.data_ptr(), cluster_error_flag(dev).data_ptr()
         tl = tlen.to(device=dev, dtype=torch.int32).contiguous() if tlen is not None else None
         a.tlen = _ptr(tl)
-        a.xcd_groups = int(XCD_GROUPS)
         s = _Saved()
         s.hlp, s.hup, s.c_out, s.c_carry, s.act = [], [], [], [], []
         outs = []
@@ -169,7 +178,6 @@ class _PersistLSTM(torch.autograd.Function):
         flags = torch.empty(L * nd * nrb * 64, dtype=torch.int32, device=dev)   # zeroed by the launcher
         b.flags, b.err = flags.data_ptr(), cluster_error_flag(dev).data_ptr()
         b.tlen = _ptr(s.tlen)
-        b.xcd_groups = int(XCD_GROUPS)
         dtop = dtop.contiguous() if dtop is not None else None
         dg_lp, dg, dh0, dc0, dih, dic, keep_alive = [], [], [], [], [], [], []
         for l in range(L):

@@ -8,7 +8,7 @@ LayerNorm / hyper modulation / gates / dropout / eoc reset and writes the
 next GEMM's operand directly. The backward runs the mirror image in reverse
 and leaves all weight gradients to single large GEMMs over the whole
 sequence after the scan (optionally chunked onto an auxiliary stream during
-the scan: ``_ChunkedWgrad``, off by default -- see WGRAD_OVERLAP). Launched from Python but designed to be captured
+the scan. Launched from Python but designed to be captured
 whole into a HIP graph (no allocation depends on data, no host sync).
 
 * ``_LSTMSeq`` handles ``nd`` independent recurrences of the same shape in
@@ -24,7 +24,6 @@ Autograd boundaries are whole sequences, so no per-step autograd nodes exist.
 """
 from __future__ import annotations
 
-import contextlib
 import ctypes
 import os
 from typing import Optional
@@ -186,73 +185,6 @@ def _fused_ok(H: int, ln: bool, fp8: bool, ldt) -> bool:
     return FUSED_ENABLED and not ln and not fp8 and ldt == torch.bfloat16 and H in (256, 512)
 
 
-# ---- wide persistent LayerNorm-LSTM forward (csrc/lstm_wide.hip) ---------------------
-# A LayerNorm layer with H in {1024, 2048}, bf16 operands, one
-# direction, no eoc resets and at most min(128, H/8) rows can run its whole
-# forward recurrence as ONE launch: W_h stays in LDS across all CUs, two
-# in-launch hand-offs per step (gate tiles to row owners, h rows back). The
-# backward consumes the same saves as the per-step kernels. OPT-IN
-# (SKR_WIDE=1): measured slower than the per-step chain on MI355X (27 vs ~20
-# us per step at H = 2048, B = 100; csrc/lstm_wide.hip, STATUS).
-WIDE_ENABLED = os.environ.get("SKR_WIDE", "0") == "1"
-WIDE_TRACE = os.environ.get("SKR_WIDE_TRACE", "0") == "1"
-WIDE_TRACES = []
-
-
-def _wide_ok(H, BB, nd, ln, fp8, ldt, reset, xp) -> bool:
-    return (WIDE_ENABLED and xp.is_cuda and nd == 1 and ln and not fp8 and ldt == torch.bfloat16
-            and reset is None and xp.shape[0] > 0 and H % 1024 == 0 and 1024 <= H <= 2048
-            and 1 <= BB <= min(128, H // 8))
-
-
-def _wide_forward(ctx, xp, W_h, Wl, WlT, h0, c0, ln_g, ln_b, lnc_g, lnc_b, seed, meta):
-    from ._hipapi import WFwdArgs
-    forget_bias, keep, stream, nd, infer = meta
-    lib = native.require_hip()
-    T, B, G = xp.shape
-    H = G // 4
-    dev, f32, bf = xp.device, torch.float32, torch.bfloat16
-    A = torch.empty(T + 1, B, H, device=dev, dtype=bf)
-    A[0].copy_(h0)
-    CC = torch.empty(T + 1, B, H, device=dev, dtype=f32)
-    CC[0].copy_(c0)
-    Hout = torch.empty(T, B, H, device=dev, dtype=f32)
-    gbuf = torch.empty(T, B, 2, G, device=dev, dtype=f32)   # per-K-half partial gate rows
-    flags = torch.empty(lib.lib.skr_lstm_wide_flag_words(H, B), device=dev, dtype=torch.int32)
-    XHAT = None if infer else torch.empty(T, B, G, device=dev, dtype=f32)
-    RSTD = None if infer else torch.empty(T, B, 5, device=dev, dtype=f32)
-    CHAT = None if infer else torch.empty(T, B, H, device=dev, dtype=f32)
-    lnp = [t.contiguous() for t in (ln_g, ln_b, lnc_g, lnc_b)]
-    sd = _seed_tensor(seed, dev)
-    c0c = c0.contiguous()
-    a = WFwdArgs()
-    a.T, a.B, a.H = T, B, H
-    a.WT = WlT.data_ptr()
-    a.xp, a.xp_ts, a.xp_ld = xp.data_ptr(), B * G, G
-    a.c0 = c0c.data_ptr()
-    a.ln_g, a.ln_b, a.lnc_g, a.lnc_b = (t.data_ptr() for t in lnp)
-    a.forget_bias, a.keep = float(forget_bias), float(keep)
-    a.seed, a.stream = sd.data_ptr(), int(stream)
-    a.hlp, a.ldh = A.data_ptr(), H
-    a.gbuf, a.h_out, a.cc = gbuf.data_ptr(), Hout.data_ptr(), CC.data_ptr()
-    a.xhat, a.rstd, a.chat = _ptr(XHAT), _ptr(RSTD), _ptr(CHAT)
-    a.flags, a.err = flags.data_ptr(), cluster_error_flag(dev).data_ptr()
-    trace = None
-    if WIDE_TRACE:   # diagnostic: per-step s_memtime stamps of every wave (scripts/wide_trace.py)
-        trace = torch.zeros(T, H // 8, 16, 4, device=dev, dtype=torch.int64)
-        a.trace = trace.data_ptr()
-        WIDE_TRACES.append(trace)
-    _check(lib.lib.skr_lstm_wide_fwd(ctypes.byref(a), _stream()), "lstm_wide_fwd")
-    s = _Saved()
-    s.Wl, s.A, s.CC, s.Cout, s.ACT, s.XHAT, s.RSTD, s.CHAT = Wl, A, CC, None, None, XHAT, RSTD, CHAT
-    s.reset, s.seed, s.meta, s.lnp = None, sd, meta, lnp
-    s.wshape = W_h.shape
-    s.keep_alive = (gbuf, flags, c0c)
-    ctx.s = s
-    ctx.dims = (T, B, H)
-    return Hout, Hout[T - 1].clone(), CC[T].clone()
-
-
 # =====================================================================================
 # LSTM / LayerNorm-LSTM sequence (nd groups)
 # =====================================================================================
@@ -276,8 +208,6 @@ class _LSTMSeq(torch.autograd.Function):
         else:
             Wl = gemm.lp(W_h.reshape(nd, H, G)).contiguous()   # B^T of the backward product dG @ W^T
             WlT = Wl.transpose(1, 2).contiguous()              # B^T of the forward product h @ W
-        if _wide_ok(H, BB, nd, ln, fp8, ldt, reset, xp):
-            return _wide_forward(ctx, xp, W_h, Wl, WlT, h0, c0, ln_g, ln_b, lnc_g, lnc_b, seed, meta)
         if fp8:
             WQ = gemm.derived(W_h, "lstm_fp8", lambda W: gemm.quantize_fp8_rows(W.reshape(H, G).t()))
             S = gemm.plan_splits_fp8(Bg, G, H)
@@ -494,7 +424,7 @@ def bilstm_sequence_packed_hip(xp, W_f, W_b, h0, c0, drop_keep=1.0, drop_seed=0,
     h = torch.cat([h0, h0], 0)
     c = torch.cat([c0, c0], 0)
     from . import persist
-    if persist.persist_ok(W_f.shape[0], 2, 1, ln=ln_f is not None):
+    if persist.persist_ok(W_f.shape[0], 2, 1, ln=ln_f is not None, B=B):
         # both directions, every step, one persistent launch (csrc/lstm_persist.hip)
         Hout, _ = persist.lstm_stack(xp, [W], [h], [c], nd=2, drop_keep=drop_keep, drop_seed=drop_seed,
                                      drop_stream=streams[0], forget_bias=forget_bias,
@@ -518,126 +448,6 @@ PERSIST_LENGTHS = os.environ.get("SKR_PERSIST_LENGTHS", "1") != "0"
 # =====================================================================================
 # HyperLSTM sequence
 # =====================================================================================
-# Hyper cell fused into the tail of the grouped forward GEMM launch
-# (csrc/skinny_gemm.hip skinny_gemm_group_hyper_kernel): one launch per
-# forward step fewer. OPT-IN (SKR_HYPER_FUSE=1): measured on MI355X, same
-# box, A/B twice -- 4 R_hyp splits 27.53 / 27.59 vs 26.89 / 26.97 ms/step
-# (the 64 workgroups' barrier + acquire + two cell rows each outlast the
-# R_main stream), 9 splits 26.81 / 26.83 vs 26.93 / 26.92 (+0.4 %, within
-# box-to-box spread; profiles/r2s5/hyper_fuse_ab.txt) -- not worth an
-# in-launch spin-wait in the default path.
-HYPER_FUSE = os.environ.get("SKR_HYPER_FUSE", "0") == "1"
-HYPER_FUSE_SPLITS = int(os.environ.get("SKR_HYPER_FUSE_SPLITS", "9"))   # 4 or 9
-_SIDE_STREAMS = {}
-# Unfolded modulation vectors (csrc/hyper_vec.hip, SKR_UNFOLD_VEC=1): reads
-# 1.7 MB of weights per step instead of the folded P (12.6 MB) but measured
-# 7.2 us/step against 6.6 us for the folded skinny GEMM on MI355X (vae_large,
-# rocprofv3 kernel trace): the step is bound by the 4.9 MB bf16 vec write and
-# launch latency, not by the weight stream. Off by default.
-UNFOLD_VEC = os.environ.get("SKR_UNFOLD_VEC", "0") == "1"
-# Concurrent branch on a second stream (SKR_TWO_STREAM=1). Off by default:
-# measured on MI355X, a cross-stream join inside a HIP graph costs 5-11 us
-# per step (rocprofv3 kernel trace), more than the overlap it buys.
-TWO_STREAM = os.environ.get("SKR_TWO_STREAM", "0") == "1"
-
-
-def _side_stream(device) -> "torch.cuda.Stream":
-    """The stream of a step's concurrent branch: an auxiliary stream per
-    device (created eagerly, so a later HIP-graph capture only records on
-    it), or the current stream when TWO_STREAM is off."""
-    if not TWO_STREAM:
-        return torch.cuda.current_stream(device)
-    key = str(device)
-    if key not in _SIDE_STREAMS:
-        _SIDE_STREAMS[key] = torch.cuda.Stream(device=device)
-    return _SIDE_STREAMS[key]
-
-
-def _join(waiter, other) -> None:
-    if waiter != other:
-        waiter.wait_stream(other)
-
-
-# Weight gradients overlapped with the backward scan (SKR_WGRAD_OVERLAP=1):
-# every WGRAD_CHUNK reverse steps the products over the rows just finished
-# go to an auxiliary stream while the scan continues; the last chunk runs on
-# the main stream after one join. SKR_WGRAD_CU_STRIDE = s > 1 confines the
-# auxiliary stream to every s-th CU (csrc/streams.hip); 1 = unrestricted.
-# OFF by default -- measured on MI355X (vae_large, bench.py, 10 steps):
-# no overlap 30.8 ms/step; overlap on an unrestricted stream 35.3 ms; on a
-# 64-CU (stride 4) or 32-CU (stride 8) masked stream 112-114 ms. The scan's
-# LayerNorm cell kernels spin-wait on co-resident peer workgroups, and
-# long-running GEMM workgroups delay those peers' dispatch, so every step of
-# the scan stretches by far more than the hidden GEMM time.
-WGRAD_OVERLAP = os.environ.get("SKR_WGRAD_OVERLAP", "0") == "1"
-WGRAD_CHUNK = int(os.environ.get("SKR_WGRAD_CHUNK", "25"))
-WGRAD_CU_STRIDE = int(os.environ.get("SKR_WGRAD_CU_STRIDE", "1"))
-_WGRAD_STREAMS = {}
-
-
-def _wgrad_stream(device):
-    """The auxiliary weight-gradient stream of ``device`` (created once,
-    before any graph capture records on it), or None when overlap is off."""
-    if not WGRAD_OVERLAP or device.type != "cuda":
-        return None
-    key = str(device)
-    if key not in _WGRAD_STREAMS:
-        if WGRAD_CU_STRIDE > 1:
-            lib = native.require_hip()
-            n_cu = torch.cuda.get_device_properties(device).multi_processor_count
-            h = ctypes.c_void_p()
-            rc = lib.lib.skr_stream_create_cumask(n_cu, 0, WGRAD_CU_STRIDE, ctypes.byref(h))
-            if rc != 0:
-                raise RuntimeError("skr_stream_create_cumask failed (%d)" % rc)
-            _WGRAD_STREAMS[key] = torch.cuda.ExternalStream(h.value, device=device)
-        else:
-            _WGRAD_STREAMS[key] = torch.cuda.Stream(device=device)
-    return _WGRAD_STREAMS[key]
-
-
-class _ChunkedWgrad:
-    """Accumulates ``sum_t f(rows of steps [t0, t1))`` for a list of
-    row-separable gradient products while a reverse scan runs.
-
-    ``work(t0, t1)`` returns the chunk's partial results (new fp32 tensors
-    of the shapes in ``shapes``). They are accumulated into buffers
-    allocated up front on the main stream (the first chunk copies), so no
-    tensor allocated on the auxiliary stream outlives its chunk.
-    ``step_done(t)`` is called after reverse step ``t``; ``finish()`` joins
-    the auxiliary stream and runs the last chunk on the main stream,
-    returning the totals. Without an auxiliary stream the whole range is one
-    chunk at ``finish()``."""
-
-    def __init__(self, T: int, work, shapes, device, stream, chunk: int):
-        self.T, self.work, self.stream, self.chunk = T, work, stream, max(1, chunk)
-        self.hi = T
-        self.acc = None
-        if stream is not None:
-            self.acc = [torch.empty(s, device=device, dtype=torch.float32) for s in shapes]
-
-    def step_done(self, t: int) -> None:
-        if self.stream is None or t <= 0 or self.hi - t < self.chunk:
-            return
-        first = self.hi == self.T
-        self.stream.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(self.stream):
-            for a, p in zip(self.acc, self.work(t, self.hi)):
-                a.copy_(p) if first else a.add_(p)
-        self.hi = t
-
-    def finish(self):
-        if self.stream is not None and self.hi < self.T:
-            torch.cuda.current_stream().wait_stream(self.stream)
-        if self.hi > 0:
-            parts = self.work(0, self.hi)
-            if self.hi == self.T:
-                self.acc = parts
-            else:
-                for a, p in zip(self.acc, parts):
-                    a.add_(p)
-        return self.acc
-
-
 def _split_override(var: str, planned: int, K: int) -> int:
     """Split-K factor of a per-step HyperLSTM product: the planned one, or
     ``$var`` (tuning sweeps) when it divides K into whole 64-wide K tiles."""
@@ -657,81 +467,15 @@ def _hyper_proj_grads(dP1, s, Hh, H, E):
     return dW_z, db_z, dWa, dbias
 
 
-class _DeferredWgrad:
-    """Deferred weight gradients (:func:`deferred_wgrad`): pending (stream,
-    keep-alive) pairs joined into the current stream at the context exit."""
-
-    def __init__(self):
-        self.active = False
-        self.pending = []
-
-    def add(self, stream, keep) -> None:
-        self.pending.append((stream, keep))
-
-    def join(self) -> None:
-        cur = torch.cuda.current_stream() if self.pending else None
-        for stream, _ in self.pending:
-            cur.wait_stream(stream)
-        self.pending = []
-
-
-_DEFER = _DeferredWgrad()
-_DEFER_STREAMS = {}
-# SKR_DEFER_WGRAD=1 turns the deferral on. OFF by default -- measured on
-# MI355X (vae_large, bench.py, 20 steps): 29.09 ms/step deferred vs 28.39
-# inline. The weight-gradient GEMM workgroups share the CUs of the
-# persistent encoder backward, whose per-step hand-offs are latency-bound,
-# and stretch it by more than the ~2 ms of GEMM work they hide.
-DEFER_ENABLED = os.environ.get("SKR_DEFER_WGRAD", "0") == "1"
-
-
-def _defer_stream(device):
-    key = str(device)
-    if key not in _DEFER_STREAMS:
-        _DEFER_STREAMS[key] = torch.cuda.Stream(device=device)
-    return _DEFER_STREAMS[key]
-
-
-@contextlib.contextmanager
-def deferred_wgrad():
-    """Inside this context the HyperLSTM backward returns its input-side
-    gradients at once and forms the weight / LayerNorm-parameter gradients
-    (the long-K GEMMs and column sums over every saved step, ~2 ms at
-    vae_large) on an auxiliary stream, overlapping the encoder's backward
-    that autograd runs next; the exit joins that stream into the current
-    one. The returned gradient tensors must not be READ before the exit
-    (autograd only assigns them to ``.grad`` when a parameter has none, as
-    in the trainers, which zero with ``set_to_none``)."""
-    if not DEFER_ENABLED or not torch.cuda.is_available():
-        yield
-        return
-    prev = _DEFER.active
-    _DEFER.active = True
-    try:
-        yield
-    finally:
-        _DEFER.active = prev
-        if not prev:
-            _DEFER.join()
-
-
 class _HyperSeq(torch.autograd.Function):
     """HyperLSTM layer (LN main cell modulated by a LN hyper cell).
 
-    Per forward step the recurrent products are split by consumer so the
-    step's two dependency chains overlap on two streams:
-
-    * side stream: ``R_main = h_{t-1} @ W_h`` (the big one, N = 4H);
-    * main stream: ``R_hyp = [h_{t-1} | hh_{t-1}] @ [hW_x[IN:]; hW_h]`` ->
-      hyper cell -> ``vec = hh_t @ P`` (skinny GEMMs + fused cell kernel);
-    * join -> fused main cell (LN + modulation + gates + carry).
-
-    The backward mirrors it: after the main cell's backward, ``dh`` from the
-    main gates (``dR_main @ W_h^T``) runs on the side stream while the
-    ``dvec -> dhh`` product, the hyper cell's backward and
-    ``dR_hyp @ [hW_x[IN:]; hW_h]^T`` run on the main stream; the next main
-    cell sums both split-K slab sets while loading. Weight gradients are
-    single large GEMMs over all T*B rows after the scan.
+    Forward per step: [grouped GEMM R_main + R_hyp] -> [hyper cell] ->
+    [vec = hh @ P + q] -> [main cell]; backward per step: [main cell bwd] ->
+    [grouped GEMM dR_main W_h^T + dvec P^T] -> [hyper cell bwd] ->
+    [dR_hyp W_y^T]; weight gradients are long-K GEMMs over all T*B rows after
+    the scan. (A persistent one-launch forward was built and measured slower:
+    csrc/experiments/hyper_persist.hip.)
     """
 
     @staticmethod
@@ -815,25 +559,10 @@ class _HyperSeq(torch.autograd.Function):
         A[0, :, :H].copy_(_to_fp8_act(h0) if fp8 else h0)
         A[0, :, H:].copy_(_to_fp8_act(hh0) if fp8 else hh0)
         # R_main: the backward re-reads it (the hyper-modulation gradient
-        # dg * R). With bf16 modulation vectors the main cell saves a bf16 copy
-        # of the summed R, so the GEMM's fp32 split-K slabs live in ONE buffer
-        # reused by every step (cache-resident) instead of T saved slab sets;
-        # at inference nothing is saved either
+        # dg * R) as the bf16 copy the main cell saves (RLP); with fp32 GEMM
+        # operands the fp32 split-K slabs of every step are kept instead
         vbf = not fp8 and dt == torch.bfloat16 and B <= 128 and S_v == 1
-        # unfolded modulation vectors (csrc/hyper_vec.hip): per step W_z + W_a
-        # (1.7 MB) instead of the folded P (12H x Hh); E = 32 embeddings
-        unfold = vbf and UNFOLD_VEC and E == 32 and Hh in (64, 128, 256, 512) and H % 64 == 0
-        if unfold:
-            if infer:
-                WzT = gemm.derived(W_z, "hvWzT", lambda W: W.to(dt).t().contiguous())
-                WaT = gemm.derived(W_a, "hvWaT", lambda W: W.to(dt).transpose(1, 2).contiguous())
-            else:
-                WzT = W_z.to(dt).t().contiguous()                     # [12E, Hh]
-                WaT = W_a.to(dt).transpose(1, 2).contiguous()         # [12, H, E]
         RLP = torch.empty(T, B, G, device=dev, dtype=torch.bfloat16) if (vbf and not infer) else None
-        RM = torch.empty(T if (RLP is None and not infer) else 1, max(S_m, 1), B, G, device=dev, dtype=f32)
-        rmi = (lambda t: t) if RM.shape[0] == T else (lambda t: 0)
-        RY = torch.empty(max(S_y, 1), B, Gh, device=dev, dtype=f32)
         CC = torch.empty(T + 1, B, H, device=dev, dtype=f32)
         CC[0].copy_(c0)
         HCC = torch.empty(T + 1, B, Hh, device=dev, dtype=f32)
@@ -847,10 +576,14 @@ class _HyperSeq(torch.autograd.Function):
         HXHAT, HRSTD, HCHAT = sv(T, B, Gh), sv(T, B, 5), sv(T, B, Hh)
         # modulation vectors in bf16 when the GEMMs are bf16 (read only by the main cells)
         VEC = torch.empty(T, B, 12 * H, device=dev, dtype=torch.bfloat16 if vbf else f32)
-        mod = 2 if vbf else 1
         sd = _seed_tensor(seed, dev)
         hln = [t.contiguous() for t in (hln_g, hln_b, hlnc_g, hlnc_b)]
         mln = [t.contiguous() for t in (ln_g, ln_b, lnc_g, lnc_b)]
+        bias_c = bias.contiguous()
+        RM = torch.empty(T if (RLP is None and not infer) else 1, max(S_m, 1), B, G, device=dev, dtype=f32)
+        rmi = (lambda t: t) if RM.shape[0] == T else (lambda t: 0)
+        RY = torch.empty(max(S_y, 1), B, Gh, device=dev, dtype=f32)
+        mod = 2 if vbf else 1
         # hyper cell args (LN-LSTM, no modulation)
         ah = LstmFwdArgs()
         ah.B, ah.H = B, Hh
@@ -865,28 +598,14 @@ class _HyperSeq(torch.autograd.Function):
         am.B, am.H = B, H
         am.ld_xp, am.ld_R = G, G
         am.R_nslab, am.R_slab = max(S_m, 1), B * G
-        bias_c = bias.contiguous()
         am.vec_gs, am.vec_ld, am.vec_bias, am.bias = H, 12 * H, q.data_ptr(), bias_c.data_ptr()
         am.ln_g, am.ln_b, am.lnc_g, am.lnc_b = (t.data_ptr() for t in mln)
         am.forget_bias, am.keep = float(forget_bias), float(keep)
         am.seed, am.stream = sd.data_ptr(), int(stream)
         am.ld_lp, am.lp_kind = K, _lp_kind(A)
         clm, clh = _ClusterSync(T, B, H, dev), _ClusterSync(T, B, Hh, dev)
-        main, side = torch.cuda.current_stream(), _side_stream(dev)
-        st = main.cuda_stream
-        group = not fp8 and not TWO_STREAM and gemm.GROUPED and S_m >= 1 and S_y >= 1 and dt == torch.bfloat16
-        # hyper cell in the grouped launch's tail (training: LayerNorm saves on)
-        fuse = HYPER_FUSE and group and not infer and Hh == 256 and S_y >= 1 and clh.C == 1 and B <= 128 and \
-            (K // 64) % HYPER_FUSE_SPLITS == 0
-        if fuse:
-            # more, shorter R_hyp workgroups: each finishes its K slice sooner and
-            # runs about one cell row in the tail (HYPER_FUSE_SPLITS = 9 at K = 2304)
-            S_y = HYPER_FUSE_SPLITS
-            ah.R_nslab = S_y
-            RY = torch.empty(S_y, B, Gh, device=dev, dtype=f32)
-            ah.R = RY.data_ptr()
-            fcnt = torch.zeros(T, dtype=torch.int32, device=dev)     # per-step arrival counters
-            ferr = cluster_error_flag(dev)
+        st = _stream()
+        group = not fp8 and gemm.GROUPED and S_m >= 1 and S_y >= 1 and dt == torch.bfloat16
         for t in range(T):
             clm.set(am, t)
             clh.set(ah, t)
@@ -895,26 +614,16 @@ class _HyperSeq(torch.autograd.Function):
             if not infer:
                 ah.xhat, ah.rstd, ah.chat = HXHAT[t].data_ptr(), HRSTD[t].data_ptr(), HCHAT[t].data_ptr()
             ah.h_lp, ah.c_carry = A[t + 1, :, H:].data_ptr(), HCC[t + 1].data_ptr()
-            if fuse:    # R_hyp (+ the hyper cell in the tail) and R_main in one launch
-                gemm.rec_gemm_group_hyper([(A[t], WyT, RY, S_y), (A[t, :, :H], WhT, RM[rmi(t)], S_m)], ah,
-                                          fcnt[t:t + 1], ferr)
+            if group:   # R_main and R_hyp in one launch
+                gemm.rec_gemm_group([(A[t, :, :H], WhT, RM[rmi(t)], S_m), (A[t], WyT, RY, S_y)])
             else:
-                if group:   # R_main and R_hyp in one launch
-                    gemm.rec_gemm_group([(A[t, :, :H], WhT, RM[rmi(t)], S_m), (A[t], WyT, RY, S_y)])
-                else:
-                    _join(side, main)                        # h_{t-1} written
-                    with torch.cuda.stream(side):
-                        rgemm(A[t, :, :H], WhT, RM[rmi(t)], S_m)
-                    rgemm(A[t], WyT, RY, S_y)
-                _check(lib.lib.skr_lstm_fwd_step(ctypes.byref(ah), 1, 0, st), "hyper_fwd_step")
-            if unfold:
-                _check(lib.lib.skr_hyper_vec_fwd(A[t + 1, :, H:].data_ptr(), K, WzT.data_ptr(), WaT.data_ptr(),
-                                                 VEC[t].data_ptr(), H, 12 * H, B, H, Hh, st), "hyper_vec_fwd")
-            elif vbf:
+                rgemm(A[t, :, :H], WhT, RM[rmi(t)], S_m)
+                rgemm(A[t], WyT, RY, S_y)
+            _check(lib.lib.skr_lstm_fwd_step(ctypes.byref(ah), 1, 0, st), "hyper_fwd_step")
+            if vbf:
                 gemm.rec_gemm_bf16out(A[t + 1, :, H:], PlT, VEC[t])
             else:
                 rgemm(A[t + 1, :, H:], PlT, VEC[t].unsqueeze(0), S_v)
-            _join(main, side)                            # R_main(t) done
             am.xp, am.R, am.vec = XH[t].data_ptr(), RM[rmi(t)].data_ptr(), VEC[t].data_ptr()
             am.r_lp = RLP[t].data_ptr() if RLP is not None else None
             am.c_prev, am.step = CC[t].data_ptr(), t
@@ -926,10 +635,10 @@ class _HyperSeq(torch.autograd.Function):
         hT = Hout[T - 1].clone()    # no resets: the carried h is h'
         hhT = HH[T - 1].clone()
         s = _Saved()
-        for k, v in dict(xl=xl, x=x, zc=zc, bp=bp, XH=XH, Whl=Whl, Wyl=Wyl, Pl=Pl, q=q, bias_c=bias_c, S_m=S_m, A=A, RM=RM, RLP=RLP, CC=CC,
-                         HCC=HCC, XHAT=XHAT, RSTD=RSTD, CHAT=CHAT, HH=HH,
-                         HXHAT=HXHAT, HRSTD=HRSTD, HCHAT=HCHAT, VEC=VEC, seed=sd, meta=meta, W_x=W_x,
-                         hW_x=hW_x, W_z=W_z, b_z=b_z, W_a=W_a, mln=mln, hln=hln).items():
+        for k, v in dict(xl=xl, x=x, zc=zc, bp=bp, XH=XH, Whl=Whl, Wyl=Wyl, Pl=Pl, q=q, S_m=S_m, A=A, RM=RM,
+                         RLP=RLP, CC=CC, HCC=HCC, XHAT=XHAT, RSTD=RSTD, CHAT=CHAT, HH=HH, HXHAT=HXHAT, HRSTD=HRSTD,
+                         HCHAT=HCHAT, VEC=VEC, seed=sd, meta=meta, W_x=W_x, hW_x=hW_x, W_z=W_z, b_z=b_z, W_a=W_a,
+                         mln=mln, hln=hln).items():
             setattr(s, k, v)
         ctx.s = s
         ctx.dims = (T, B, IX, IN, H, Hh, E)
@@ -1002,30 +711,8 @@ class _HyperSeq(torch.autograd.Function):
         ah.keep, ah.seed, ah.stream = float(hkeep), s.seed.data_ptr(), int(stream) + 1
         ah.ld_dG, ah.ld_dG_lp, ah.dG_lp_kind = Gh, Gh, 1 if lp_on else 0
         clm, clh = _ClusterSync(T, B, H, dev), _ClusterSync(T, B, Hh, dev)
-        main, side = torch.cuda.current_stream(), _side_stream(dev)
-        st = main.cuda_stream
-        group = lp_on and not TWO_STREAM and gemm.GROUPED and S_am >= 1 and S_h >= 1
-        # weight / LayerNorm-parameter gradients: row-separable products over
-        # the T*B saved rows, accumulated chunk by chunk on the auxiliary
-        # stream while the scan continues (see _ChunkedWgrad)
-        A2 = s.A[:T].reshape(TB, K)
-        # hyper-norm projections, vec_k = (hh @ W_z_k + b_z_k) @ W_a_k: ONE long-K
-        # GEMM dP = [hh | 1]^T @ dvec gives dP_k = hh^T dvec_k and (ones row) the
-        # column sums of dvec; the per-k factors are then tiny batched products
-        HH1 = torch.zeros(TB, Hh + 8, device=dev, dtype=ldt)
-        HH1[:, :Hh] = s.HH.view(TB, Hh)
-        HH1[:, Hh] = 1.0
-        dRMf, dRYf, dVECf = dRM_lp.view(TB, G), dRY_lp.view(TB, Gh), dVEC.view(TB, 12 * H)
-
-        def wwork(t0, t1):
-            r = slice(t0 * B, t1 * B)
-            out = [gemm.wgrad(A2[r, :H], dRMf[r]), gemm.wgrad(A2[r], dRYf[r]), gemm.wgrad(HH1[r], dVECf[r])]
-            for dy, xh, n in ((DLNY, s.XHAT, G), (DLNCY, s.CHAT, H), (HDLNY, s.HXHAT, Gh), (HDLNCY, s.HCHAT, Hh)):
-                out += list(colsum(dy[t0:t1].view(-1, n), xh[t0:t1].view(-1, n)))
-            return out
-
-        wg = _ChunkedWgrad(T, wwork, [(H, G), (K, Gh), (Hh + 8, 12 * H), (G,), (G,), (H,), (H,), (Gh,), (Gh,),
-                                      (Hh,), (Hh,)], dev, _wgrad_stream(dev), WGRAD_CHUNK)
+        st = _stream()
+        group = lp_on and gemm.GROUPED and S_am >= 1 and S_h >= 1
         for t in range(T - 1, -1, -1):
             clm.set(am, t)
             clh.set(ah, t)
@@ -1047,9 +734,7 @@ class _HyperSeq(torch.autograd.Function):
             if group:   # dR_main @ W_h^T and dvec @ P^T in one launch
                 gemm.rec_gemm_group([(dRM_lp[t], s.Whl, DAM, S_am), (dVEC[t], s.Pl, DHZ, S_h)])
             else:
-                _join(side, main)                        # dR_main(t) written, DAM consumed
-                with torch.cuda.stream(side):
-                    gemm.rec_gemm(dRM_lp[t], s.Whl, DAM, S_am)
+                gemm.rec_gemm(dRM_lp[t], s.Whl, DAM, S_am)
                 gemm.rec_gemm(dVEC[t], s.Pl, DHZ, S_h)
             ah.c_prev = s.HCC[t].data_ptr()
             ah.xhat, ah.rstd, ah.chat = s.HXHAT[t].data_ptr(), s.HRSTD[t].data_ptr(), s.HCHAT[t].data_ptr()
@@ -1059,42 +744,23 @@ class _HyperSeq(torch.autograd.Function):
             ah.dlny, ah.dlncy = HDLNY[t].data_ptr(), HDLNCY[t].data_ptr()
             _check(lib.lib.skr_lstm_bwd_step(ctypes.byref(ah), 1, 0, st), "hyper_bwd_step")
             gemm.rec_gemm(dRY_lp[t], s.Wyl, DAY, S_ay)
-            _join(main, side)                            # dh (main gates) for step t-1 ready
-            wg.step_done(t)
         dh0 = DAY[:, :, :H].sum(0) + DAM.sum(0)
         dhh0 = DAY[:, :, H:].sum(0)
-        defer = _DEFER.active and wg.stream is None and s.bp
-        if defer:
-            # input-side gradients (needed by the encoder backward next) on the
-            # main stream; every weight / LayerNorm-parameter gradient on the
-            # deferred stream, overlapping whatever autograd runs next
-            S_m, P_m = bproj_reduce(s.x, dXH)
-            S_y, P_y = bproj_reduce(s.x, dRY_lp)
-            if s.zc is not None:
-                dW_x = torch.cat([P_m, s.zc.t() @ S_m], 0)
-                dhx_in = torch.cat([P_y, s.zc.t() @ S_y], 0)
-                dzc = S_m @ s.W_x[IX:].t() + S_y @ s.hW_x[IX:IN].t()
-            else:
-                dW_x, dhx_in, dzc = P_m, P_y, None
-            dx = None
-            aux = _defer_stream(dev)
-            aux.wait_stream(main)
-            with torch.cuda.stream(aux):
-                dW_h, dW_y, dP1, *cs = wwork(0, T)
-                dhW_x = torch.empty_like(s.hW_x)
-                dhW_x[IN:] = dW_y[:H]
-                dhW_x[:IN] = dhx_in
-                dhW_h = dW_y[H:]
-                g_ln, g_hln = cs[:4], cs[4:]
-                dW_z, db_z, dWa, dbias = _hyper_proj_grads(dP1, s, Hh, H, E)
-            # main-stream tensors the deferred work reads stay alive until the join
-            _DEFER.add(aux, (s, dRM_lp, dRY_lp, dVEC, HH1, DLNY, DLNCY, HDLNY, HDLNCY, dhx_in))
-            ctx.s = None
-            return (dx, dzc, dh0, dc_rec, dhh0, dhc_rec, None, dW_x, dW_h, dbias, dhW_x, dhW_h,
-                    g_hln[0], g_hln[1], g_hln[2], g_hln[3], dW_z, db_z, dWa, g_ln[0], g_ln[1], g_ln[2], g_ln[3],
-                    None)
-        dW_h, dW_y, dP1, *cs = wg.finish()
-        g_ln, g_hln = cs[:4], cs[4:]
+        # weight / LayerNorm-parameter gradients: long-K products over the T*B saved rows
+        A2 = s.A[:T].reshape(TB, K)
+        # hyper-norm projections, vec_k = (hh @ W_z_k + b_z_k) @ W_a_k: ONE long-K
+        # GEMM dP = [hh | 1]^T @ dvec gives dP_k = hh^T dvec_k and (ones row) the
+        # column sums of dvec; the per-k factors are then tiny batched products
+        HH1 = torch.zeros(TB, Hh + 8, device=dev, dtype=ldt)
+        HH1[:, :Hh] = s.HH.view(TB, Hh)
+        HH1[:, Hh] = 1.0
+        dW_h = gemm.wgrad(A2[:, :H], dRM_lp.view(TB, G))
+        dW_y = gemm.wgrad(A2, dRY_lp.view(TB, Gh))
+        dP1 = gemm.wgrad(HH1, dVEC.view(TB, 12 * H))
+        g_ln, g_hln = [], []
+        for dy, xh, n, out in ((DLNY, s.XHAT, G, g_ln), (DLNCY, s.CHAT, H, g_ln), (HDLNY, s.HXHAT, Gh, g_hln),
+                               (HDLNCY, s.HCHAT, Hh, g_hln)):
+            out += list(colsum(dy.view(-1, n), xh.view(-1, n)))
         dhW_x = torch.empty_like(s.hW_x)
         dhW_x[IN:] = dW_y[:H]
         dhW_h = dW_y[H:]
@@ -1126,71 +792,10 @@ class _HyperSeq(torch.autograd.Function):
                 g_hln[0], g_hln[1], g_hln[2], g_hln[3], dW_z, db_z, dWa, g_ln[0], g_ln[1], g_ln[2], g_ln[3], None)
 
 
-# Batch-split HyperLSTM scan (SKR_DEC_SPLIT = k > 1): the batch rows are cut
-# into k chunks whose scans run as INDEPENDENT chains on k streams (chunk 0 on
-# the current stream). Every per-step launch of the H = 2048 recurrence is
-# latency-bound (GEMM ramp / split-K slabs, LayerNorm exchanges), so two
-# chains interleave on the chip with no cross-stream join inside the scan --
-# only one fork before and one join after it. Autograd runs each chunk's
-# backward on its forward stream, so the reverse scans overlap the same way.
-# Chunk i > 0 hashes its dropout masks with stream id drop_stream + 64 i.
-# OPT-IN: measured on MI355X (vae_large, bench.py, 10 steps) 36.7 ms/step
-# with k = 2 against 28.5 unsplit. A half-batch launch costs 85 % of a
-# full-batch one (grouped GEMM 12.2 vs 14 us, main cell fwd 9.9 vs 13.9,
-# bwd 13.5 vs 17.5: the per-launch latency does not scale with rows), and
-# the kernel trace shows the two chains' launches serialised on one queue
-# (decoder kernels 34.3 ms busy = 34.3 ms union), so the split doubles the
-# launches without overlapping them.
-DEC_SPLIT = int(os.environ.get("SKR_DEC_SPLIT", "1"))
-_SPLIT_STREAMS = {}
-
-
-def _split_streams(device, n):
-    key = str(device)
-    lst = _SPLIT_STREAMS.setdefault(key, [])
-    while len(lst) < n:
-        lst.append(torch.cuda.Stream(device=device))
-    return lst[:n]
-
-
-def _split_rows(B: int, k: int):
-    """k contiguous, near-equal row chunks, or None when B is too small to
-    split (fewer than 32 rows per chunk)."""
-    if k <= 1 or B < 32 * k:
-        return None
-    per = -(-B // k)
-    cuts, r = [], 0
-    while r < B:
-        cuts.append((r, min(B, r + per)))
-        r += per
-    return cuts if len(cuts) > 1 else None
-
-
 def hyper_sequence_hip(p, x, h0, c0, hh0, hc0, forget_bias=1.0, drop_keep=1.0, drop_seed=0, drop_stream=0,
-                       hyp_drop_keep=1.0, zc=None, split=None):
+                       hyp_drop_keep=1.0, zc=None):
     if not p.use_layer_norm:
         raise NotImplementedError("HIP HyperLSTM path requires use_layer_norm=True")
-    k = DEC_SPLIT if split is None else split
-    cuts = _split_rows(x.shape[1], k) if x.is_cuda else None
-    if cuts is not None:
-        main = torch.cuda.current_stream(x.device)
-        streams = [main] + _split_streams(x.device, len(cuts) - 1)
-        outs, finals = [], []
-        for i, ((r0, r1), s) in enumerate(zip(cuts, streams)):
-            if s is not main:
-                s.wait_stream(main)
-            with torch.cuda.stream(s):
-                o, f = hyper_sequence_hip(p, x[:, r0:r1].contiguous(), h0[r0:r1], c0[r0:r1], hh0[r0:r1], hc0[r0:r1],
-                                          forget_bias, drop_keep, drop_seed, drop_stream + 64 * i,
-                                          hyp_drop_keep, None if zc is None else zc[r0:r1], split=1)
-            if s is not main:
-                for t in (o,) + tuple(f):
-                    t.record_stream(main)
-            outs.append(o)
-            finals.append(f)
-        for s in streams[1:]:
-            main.wait_stream(s)
-        return torch.cat(outs, 1), tuple(torch.cat(parts, 0) for parts in zip(*finals))
     outs = _HyperSeq.apply(x, zc, h0, c0, hh0, hc0, drop_seed, p.W_x, p.W_h, p.bias, p.hyp_W_x, p.hyp_W_h,
                            p.hyp_ln_gamma, p.hyp_ln_beta, p.hyp_lnc_gamma, p.hyp_lnc_beta, p.W_z, p.b_z, p.W_a,
                            p.ln_gamma, p.ln_beta, p.lnc_gamma, p.lnc_beta,

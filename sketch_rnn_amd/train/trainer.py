@@ -27,7 +27,6 @@ from ..config import RefConfig, VAEConfig
 from ..models.reference import SketchRNN
 from ..models.vae import SketchVAE
 from ..ops import gemm
-from ..ops.recurrent import deferred_wgrad
 from ..parallel import dp
 from ..utils.trace import GpuPhaseTimer, PhaseTimes, phase
 from . import schedules
@@ -261,10 +260,7 @@ class VAETrainer:
         self.opt.zero_grad(set_to_none=True)
         out = self.model.loss(strokes, lengths, labels if self.cfg.num_classes > 0 else None,
                               kl_weight=self.kl_w, train=True, seed=self.seed)
-        # decoder weight gradients on an auxiliary stream, overlapping the
-        # encoder backward (joined at the context exit, before the gather)
-        with deferred_wgrad():
-            out["cost"].backward()
+        out["cost"].backward()
         self.opt.gather_grads()
         return {k: v.detach() for k, v in out.items()}
 

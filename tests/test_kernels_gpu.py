@@ -24,8 +24,6 @@ def _restore():
     yield
     ops.set_backend("auto")
     ops.set_compute_dtype("fp32")
-    from sketch_rnn_amd.ops import recurrent
-    recurrent.UNFOLD_VEC = False
     from sketch_rnn_amd.ops.recurrent import check_cluster_errors
     torch.cuda.synchronize()
     check_cluster_errors(DEV)
@@ -219,35 +217,50 @@ def test_hyper_sequence_matches_oracle(H, Hh, E, keep):
     _close(g_h, g_t, 2e-3, 2e-4, "grad")
 
 
-@pytest.mark.parametrize("H,Hh,E,unfold", [(512, 64, 8, True), (2048, 256, 32, True), (2048, 256, 32, False)])
-def test_hyper_sequence_bf16_close(H, Hh, E, unfold):
-    """bf16 HyperLSTM (grouped GEMMs, bf16 modulation vectors; E = 32: the
-    unfolded modulation-vector kernel csrc/hyper_vec.hip, or the folded
-    P GEMM) against the fp32 oracle at bf16 tolerances."""
-    from sketch_rnn_amd.ops import recurrent
-    recurrent.UNFOLD_VEC = unfold
-    torch.manual_seed(12)
-    T, B, IN = 6, 100, 5
-    p = C.HyperLSTMParams(IN + 16, H, Hh, E).to(DEV)
-    with torch.no_grad():
+def _hyper_setup(seed, T, B, IN, Z, H, Hh, E, jitter=0.05, state=0.0):
+    torch.manual_seed(seed)
+    p = C.HyperLSTMParams(IN + Z, H, Hh, E).to(DEV)
+    with torch.no_grad():  # move off the degenerate init so every path carries signal
         for prm in p.parameters():
-            prm.add_(torch.randn_like(prm) * 0.05)
+            prm.add_(torch.randn_like(prm) * jitter)
     x = torch.randn(T, B, IN, device=DEV)
-    zc = torch.randn(B, 16, device=DEV, requires_grad=True)
-    st = [torch.zeros(B, n, device=DEV) for n in (H, H, Hh, Hh)]
+    z = torch.randn(B, Z, device=DEV) if Z else None
+    st = [torch.randn(B, n, device=DEV) * state for n in (H, H, Hh, Hh)]
     w = torch.randn(T, B, H, device=DEV)
+    return p, x, z, st, w
+
+
+def _hyper_run(p, x, z, st, w, keep=0.9, hkeep=1.0, fin_w=True):
+    """One forward + backward of ops.hyper_sequence; returns [out, finals...,
+    dz, parameter grads]."""
+    p.zero_grad()
+    zg = z.detach().clone().requires_grad_() if z is not None else None
+    out, fin = ops.hyper_sequence(p, x, *st, drop_keep=keep, drop_seed=4, drop_stream=9, hyp_drop_keep=hkeep, zc=zg)
+    loss = (out * w).sum()
+    if fin_w:
+        loss = loss + sum((f * (0.5 + 0.1 * k)).sum() for k, f in enumerate(fin))
+    loss.backward()
+    torch.cuda.synchronize()
+    return [out.detach()] + [f.detach() for f in fin] + ([zg.grad] if zg is not None else []) + \
+        [q.grad.clone() for q in p.parameters()]
+
+
+def _names(p, z=True):
+    return ["out", "h", "c", "hh", "hc"] + (["dz"] if z else []) + [n for n, _ in p.named_parameters()]
+
+
+@pytest.mark.parametrize("H,Hh,E", [(512, 64, 8), (2048, 256, 32)])
+def test_hyper_sequence_bf16_close(H, Hh, E):
+    """bf16 HyperLSTM (grouped GEMMs, bf16 modulation vectors) against the
+    fp32 oracle at bf16 tolerances."""
+    p, x, z, st, w = _hyper_setup(12, 6, 100, 5, 16, H, Hh, E)
     res = []
     for backend, dt in (("hip", "bf16"), ("torch", "fp32")):
         ops.set_backend(backend)
         ops.set_compute_dtype(dt)
-        p.zero_grad()
-        z = zc.detach().clone().requires_grad_()
-        out, _ = ops.hyper_sequence(p, x, *st, drop_keep=0.9, drop_seed=4, drop_stream=9, zc=z)
-        (out * w).sum().backward()
-        res.append([out.detach(), z.grad] + [q.grad.clone() for q in p.parameters()])
-    recurrent.UNFOLD_VEC = False
+        res.append(_hyper_run(p, x, z, st, w, fin_w=False))
     _close(res[0][:1], res[1][:1], 3e-2, 3e-2, "out")
-    _close(res[0][1:], res[1][1:], 6e-2, 6e-2, "grad")
+    _close(res[0][5:], res[1][5:], 6e-2, 6e-2, "grad")
 
 
 @pytest.mark.parametrize("H,Hh,E", [(2048, 256, 32), (512, 64, 8)])
@@ -255,12 +268,7 @@ def test_hyper_grouped_gemm_path_bitwise(H, Hh, E):
     """bf16 HyperLSTM with the grouped per-step GEMM launches equals the
     one-launch-per-product path bit for bit (same tiles, same sums)."""
     from sketch_rnn_amd.ops import gemm
-    torch.manual_seed(3)
-    T, B, IN = 4, 100, 13
-    p = C.HyperLSTMParams(IN, H, Hh, E).to(DEV)
-    x = torch.randn(T, B, IN, device=DEV, requires_grad=True)
-    st = [torch.zeros(B, n, device=DEV) for n in (H, H, Hh, Hh)]
-    w = torch.randn(T, B, H, device=DEV)
+    p, x, z, st, w = _hyper_setup(3, 4, 100, 13, 0, H, Hh, E, jitter=0.0)
     saved = gemm.GROUPED
     res = []
     try:
@@ -268,147 +276,44 @@ def test_hyper_grouped_gemm_path_bitwise(H, Hh, E):
         ops.set_backend("hip")
         for grouped in (True, False):
             gemm.GROUPED = grouped
-            p.zero_grad()
-            xg = x.detach().clone().requires_grad_()
-            out, _ = ops.hyper_sequence(p, xg, *st, drop_keep=0.9, drop_seed=3, drop_stream=9)
-            (out * w).sum().backward()
-            res.append([out.detach(), xg.grad] + [q.grad.clone() for q in p.parameters()])
+            res.append(_hyper_run(p, x, z, st, w))
     finally:
         gemm.GROUPED = saved
     for a, b in zip(*res):
         assert torch.equal(a, b)
 
 
-@pytest.mark.parametrize("B,hkeep,splits", [(100, 0.9, 4), (37, 1.0, 4), (100, 0.9, 9)])
-def test_hyper_cell_fused_into_group_gemm_bitwise(B, hkeep, splits):
-    """bf16 HyperLSTM (vae_large shapes) with the hyper cell run in the tail
-    of the grouped forward GEMM launch equals the separate hyper-cell launch:
-    with the same 4 split-K slabs bit for bit (outputs, final states, every
-    gradient: same GEMM tiles, same cell code, the slabs travel write-through
-    inside the launch); with 9 slabs (the default) to fp32 summation order."""
-    from sketch_rnn_amd.ops import gemm, recurrent
-    torch.manual_seed(6)
-    T, IN, Z, H, Hh, E = 6, 5, 16, 2048, 256, 32
-    p = C.HyperLSTMParams(IN + Z, H, Hh, E).to(DEV)
-    with torch.no_grad():
-        for prm in p.parameters():
-            prm.add_(torch.randn_like(prm) * 0.02)
-    x = torch.randn(T, B, IN, device=DEV)
-    z = torch.randn(B, Z, device=DEV)
-    st = [torch.randn(B, n, device=DEV) * 0.1 for n in (H, H, Hh, Hh)]
-    w = torch.randn(T, B, H, device=DEV)
-    calls = []
-    orig = gemm.rec_gemm_group_hyper
-
-    def spy(*a, **k):
-        calls.append(1)
-        return orig(*a, **k)
-
-    res = []
-    saved = recurrent.HYPER_FUSE, recurrent.HYPER_FUSE_SPLITS
-    recurrent.HYPER_FUSE_SPLITS = splits
-    try:
-        ops.set_compute_dtype("bf16")
-        ops.set_backend("hip")
-        gemm.rec_gemm_group_hyper = spy
-        for fuse in (False, True):
-            recurrent.HYPER_FUSE = fuse
-            p.zero_grad()
-            zg = z.detach().clone().requires_grad_()
-            out, fin = recurrent.hyper_sequence_hip(p, x, *st, drop_keep=0.9, drop_seed=3, drop_stream=9,
-                                                    hyp_drop_keep=hkeep, zc=zg)
-            (out * w).sum().backward()
-            torch.cuda.synchronize()
-            res.append([out.detach()] + [f.detach() for f in fin] + [zg.grad] + [q.grad.clone() for q in p.parameters()])
-    finally:
-        recurrent.HYPER_FUSE, recurrent.HYPER_FUSE_SPLITS = saved
-        gemm.rec_gemm_group_hyper = orig
-        ops.set_compute_dtype("fp32")
-    assert len(calls) == T, calls    # the fused launch ran once per forward step
-    names = ["out", "h", "c", "hh", "hc", "dz"] + [n for n, _ in p.named_parameters()]
-    for n, a, b in zip(names, *res):
-        if splits == 4:
-            assert torch.equal(a, b), (n, float((a.float() - b.float()).abs().max()))
-        else:
-            err = (a.float() - b.float()).abs().max().item()   # 9 vs 4 split-K partial sums
-            assert err <= 2e-2 * max(b.float().abs().max().item(), 1e-3), (n, err)
-
-
-@pytest.mark.parametrize("H,Hh,E,B", [(2048, 256, 32, 100), (512, 64, 8, 70)])
-def test_hyper_batch_split_matches_unsplit(H, Hh, E, B):
-    """bf16 HyperLSTM with the batch cut into independent chains on two
-    streams (SKR_DEC_SPLIT) equals the one-chain scan: outputs, final
-    states, input and weight gradients (the weight-gradient sums run over
-    the rows in a different order)."""
-    from sketch_rnn_amd.ops import recurrent
-    torch.manual_seed(5)
-    T, IN, Z = 5, 5, 16
-    p = C.HyperLSTMParams(IN + Z, H, Hh, E).to(DEV)
-    with torch.no_grad():
-        for prm in p.parameters():
-            prm.add_(torch.randn_like(prm) * 0.02)
-    x = torch.randn(T, B, IN, device=DEV)
-    z = torch.randn(B, Z, device=DEV)
-    st = [torch.randn(B, n, device=DEV) * 0.1 for n in (H, H, Hh, Hh)]
-    w = torch.randn(T, B, H, device=DEV)
-    assert recurrent._split_rows(B, 2) is not None
-    res = []
-    try:
-        ops.set_compute_dtype("bf16")
-        ops.set_backend("hip")
-        for split in (1, 2):
-            p.zero_grad()
-            zg = z.detach().clone().requires_grad_()   # x without grad: the model's stroke-projection path
-            out, fin = recurrent.hyper_sequence_hip(p, x, *st, drop_keep=1.0, zc=zg, split=split)
-            (out * w).sum().backward()
-            torch.cuda.synchronize()
-            res.append([out.detach()] + [f.detach() for f in fin] + [zg.grad] +
-                       [q.grad.clone() for q in p.parameters()])
-    finally:
-        ops.set_compute_dtype("fp32")
-    names = ["out", "h", "c", "hh", "hc", "dz"] + [n for n, _ in p.named_parameters()]
-    for n, a, b in zip(names, *res):
-        err = (a.float() - b.float()).abs().max().item()
-        assert err <= 2e-2 * max(b.float().abs().max().item(), 1e-3), (n, err)
-
-
-@pytest.mark.parametrize("dt,cu_stride", [("fp32", 4), ("bf16", 4), ("bf16", 1)])
-def test_hyper_chunked_wgrad_overlap(dt, cu_stride):
-    """Weight / LN-parameter gradients accumulated in chunks on the
-    auxiliary (optionally CU-masked) stream while the backward scan runs
-    equal the one-shot reduction after the scan (same products, different
-    summation order), with and without HIP-graph capture."""
-    from sketch_rnn_amd.ops import recurrent
-    torch.manual_seed(4)
-    T, B, IN, H, Hh, E = 9, 100, 13, 512, 64, 8
-    p = C.HyperLSTMParams(IN, H, Hh, E).to(DEV)
-    with torch.no_grad():
-        for prm in p.parameters():
-            prm.add_(torch.randn_like(prm) * 0.05)
-    x = torch.randn(T, B, IN, device=DEV)
-    st = [torch.zeros(B, n, device=DEV) for n in (H, H, Hh, Hh)]
-    w = torch.randn(T, B, H, device=DEV)
-    saved = (recurrent.WGRAD_OVERLAP, recurrent.WGRAD_CHUNK, recurrent.WGRAD_CU_STRIDE)
-    res = []
-    try:
-        ops.set_backend("hip")
+def test_hyper_long_sequence_vs_oracle():
+    """T = 250 (the vae_large sequence length), H = 2048, the model's own
+    initialisation. The recurrence is chaotic over 250 steps: a 1e-6 input
+    perturbation of the fp32 oracle itself grows to ~0.1 in the outputs
+    (scripts/long_seq_drift.py, profiles/r3/long_seq_drift.jsonl), so no fixed
+    tolerance separates a kernel bug from rounding at t = 250. Checked
+    instead: (1) the HIP fp32 path tracks the fp32 oracle -- outputs, dz and
+    every weight gradient -- inside 4x the oracle's own sensitivity to that
+    perturbation; (2) the bf16 path stays within 6 % over the first 20 steps
+    (bf16 rounding ~1e-2 at t = 1, then the same exponential growth the
+    perturbation shows: ~4e-2 at t = 20, saturated by t ~ 100)."""
+    p, x, z, st, w = _hyper_setup(8, 250, 8, 5, 16, 2048, 256, 32, jitter=0.0)
+    runs = {}
+    for name, backend, dt, xx in (("ref", "torch", "fp32", x), ("pert", "torch", "fp32", x + 1e-6 * torch.randn_like(x)),
+                                  ("hip32", "hip", "fp32", x), ("hip16", "hip", "bf16", x)):
+        ops.set_backend(backend)
         ops.set_compute_dtype(dt)
-        recurrent.WGRAD_CU_STRIDE = cu_stride
-        recurrent._WGRAD_STREAMS.clear()
-        for on in (False, True):
-            recurrent.WGRAD_OVERLAP, recurrent.WGRAD_CHUNK = on, 2
-            p.zero_grad()
-            xg = x.detach().clone().requires_grad_()
-            out, _ = ops.hyper_sequence(p, xg, *st, drop_keep=0.9, drop_seed=3, drop_stream=9)
-            (out * w).sum().backward()
-            res.append([xg.grad] + [q.grad.clone() for q in p.parameters()])
-        torch.cuda.synchronize()
-    finally:
-        recurrent.WGRAD_OVERLAP, recurrent.WGRAD_CHUNK, recurrent.WGRAD_CU_STRIDE = saved
-        recurrent._WGRAD_STREAMS.clear()
-    for (n, _), a, b in zip([("x", None)] + list(p.named_parameters()), *res):
-        err = (a - b).abs().max().item()
-        assert err <= 1e-5 * max(b.abs().max().item(), 1.0), (n, err)
+        runs[name] = _hyper_run(p, xx, z, st, w, keep=1.0, fin_w=False)
+    for i, n in enumerate(_names(p)):
+        if n in ("h", "c", "hh", "hc"):
+            continue
+        ref = runs["ref"][i].float()
+        scale = max(ref.abs().max().item(), 1e-3)
+        e_h = (runs["hip32"][i].float() - ref).abs().max().item()
+        e_p = (runs["pert"][i].float() - ref).abs().max().item()
+        ok = e_h <= 4 * e_p + 1e-4 * scale
+        assert ok, (n, e_h, e_p, scale)
+    out16, out32 = runs["hip16"][0][:20].float(), runs["ref"][0][:20].float()
+    err = (out16 - out32).abs().max().item()
+    ok = err <= 6e-2 * out32.abs().max().item()
+    assert ok, ("bf16 out, t < 20", err)
 
 
 @pytest.mark.parametrize("M,N,K,nd", [(100, 9216, 2304, 1), (100, 2304, 9216, 1), (100, 256, 24576, 1),
