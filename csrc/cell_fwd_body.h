@@ -113,6 +113,15 @@ __device__ __forceinline__ void cell_fwd_body(const FwdArgs& a, const int c, con
         const int uc = min(u, H - 1);
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
+            if constexpr (MOD == 3) {   // precomputed pre-activations (csrc/hyper_mod.hip)
+                g[k][q] = a.gpre[(int64_t)b * 4 * H + q * H + uc];
+                rsv[k][q] = 0.f;
+                if (LN) {
+                    lg[k][q] = ln_g[q * H + uc];
+                    lb[k][q] = ln_b[q * H + uc];
+                }
+                continue;
+            }
             const float xv = a.xp[b * a.ld_xp + q * H + uc];
             const float rv = slab_sum<NS>(a.R, b * a.ld_R + q * H + uc, a.R_nslab, a.R_slab);
             if (MOD) {
@@ -155,7 +164,24 @@ __device__ __forceinline__ void cell_fwd_body(const FwdArgs& a, const int c, con
                 s[4 + q] += v * v;
             }
         }
-        row_sum<8, NW>(s, lds, mine, all, a.part, a.err, a.step + 1, b, c, C);
+        if constexpr (MOD == 3) {   // the row's statistics: sum of the per-tile partials
+#pragma unroll
+            for (int q = 0; q < 8; ++q) s[q] = 0.f;
+            const float* gs = a.gstats + (int64_t)b * 4 * a.gstat_tiles * 2;
+            for (int i = tid; i < 4 * a.gstat_tiles; i += NT) {
+                const int gq = i / a.gstat_tiles;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    if (q == gq) {
+                        s[q] += gs[2 * i];
+                        s[4 + q] += gs[2 * i + 1];
+                    }
+                }
+            }
+            block_sum<8, NW>(s, lds);
+        } else {
+            row_sum<8, NW>(s, lds, mine, all, a.part, a.err, a.step + 1, b, c, C);
+        }
         SKR_STAMP(2);
         float mean[4], var[4];
 #pragma unroll

@@ -1,0 +1,190 @@
+// HyperLSTM modulation step (forward), one launch per time step:
+//
+//   vec   = hh_t @ P + q (+ the main bias in the shift block)       [B, 12 H]
+//   g     = xh * vec_x + R * vec_h + vec_b                           [B, 4 H]
+//   stats = per (row, gate, 32-unit tile): sum g, sum g^2
+//
+// Reference recurrence: /root/reference model.py:66-95 (static unroll);
+// HyperLSTM semantics: sketch_rnn_amd/models/cells.py hyper_lstm_step.
+//
+// Why fused: the main cell's LayerNorm needs row statistics over all 2048
+// units of each gate, so as its own kernel it spends one in-launch exchange
+// between the workgroups of a row on them (~3 us per step). This kernel
+// already owns every (row, unit) of the gate pre-activations it produces, so
+// it emits per-tile partial sums (64 tiles per gate); the main cell
+// (csrc/cell_fwd_body.h, MOD 3) sums them while loading -- one exchange per
+// step fewer -- and reads the finished g (32 KB per row) instead of x-proj,
+// the R slabs and the modulation vectors (144 KB per row).
+// The saves the backward needs are written here too: vec (bf16, q folded in:
+// the backward cell runs with a zero vec_bias) and the bf16 summed R.
+//
+// Tiling: workgroup (gate q, 32-unit tile u0) -> 4 x 64 = 256 workgroups of
+// 384 threads. Wave w owns MFMA column tile w: k-block q + 4 (w / 2) (x, h,
+// shift modulation of gate q), units u0 + 16 (w % 2) .. +15; its P
+// fragments (8 k-steps, K = Hh = 256) live in VGPRs; hh (all rows, bf16) is
+// staged once in LDS (XOR-swizzled rows). v_mfma_f32_16x16x32_bf16: lane l
+// holds A[row l & 15][k 8 (l >> 4)..+7], B[k 8 (l >> 4)..+7][col l & 15];
+// C: col l & 15, rows 4 (l >> 4) + i.
+#include "common.h"
+
+namespace {
+
+using namespace skr;
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+
+constexpr int HH = 256, NTH = 384, TU = 32;      // hyper units (K), threads, units per tile
+constexpr int MAXB = 112, NRT = MAXB / 16;
+
+__device__ __forceinline__ int sw(int row, int chunk) { return row * HH + ((chunk ^ (row & 15)) << 3); }
+
+__device__ __forceinline__ uint32_t pack_bf(float a, float b) {
+    return (uint32_t)__bfloat16_as_ushort(__float2bfloat16(a)) |
+           ((uint32_t)__bfloat16_as_ushort(__float2bfloat16(b)) << 16);
+}
+
+template <int NS>
+__global__ __launch_bounds__(NTH) void hyper_mod_fwd(const __hip_bfloat16* __restrict__ hh, int64_t ld_hh,
+                                                     const __hip_bfloat16* __restrict__ PlT,   // [12H][HH]
+                                                     const float* __restrict__ qb,             // [12H]
+                                                     const float* __restrict__ xh,             // [B][4H]
+                                                     const float* __restrict__ R, int64_t r_slab,   // [NS][B][4H]
+                                                     __hip_bfloat16* __restrict__ vec,          // [B][12H]
+                                                     float* __restrict__ gout,                  // [B][4H]
+                                                     __hip_bfloat16* __restrict__ rlp,          // [B][4H] or null
+                                                     float* __restrict__ stats,                 // [B][4][H/TU][2]
+                                                     int B, int H) {
+    __shared__ __attribute__((aligned(16))) __hip_bfloat16 sA[MAXB * HH];   // 56 KB
+    __shared__ __attribute__((aligned(16))) float sV[6][MAXB][16];          // 42 KB
+    const int q = blockIdx.y, u0 = blockIdx.x * TU, ntile = H / TU;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int fr = lane & 15, fq = lane >> 4;
+    const int G = 4 * H, NV = 12 * H;
+    // ---- every global load up front: this wave's P fragments, the
+    // epilogue's x-projection and R slabs (thread -> rows rg, rg + 48, rg + 96;
+    // units u0 + 4 ug .. +3), and hh for the LDS stage
+    const int vcol = (q + 4 * (w >> 1)) * H + u0 + 16 * (w & 1);   // first modulation column of tile w
+    bf16x8 pf[8];
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks) pf[ks] = *(const bf16x8*)(PlT + (int64_t)(vcol + fr) * HH + 32 * ks + 8 * fq);
+    const float qv = qb[vcol + fr];
+    constexpr int RPT = (MAXB + NTH / 8 - 1) / (NTH / 8);    // rows per thread (3)
+    const int rg = tid >> 3, ug = tid & 7, ul = 4 * ug;
+    f32x4 x4[RPT], r4[RPT];
+#pragma unroll
+    for (int k = 0; k < RPT; ++k) {
+        const int rr = min(rg + k * (NTH / 8), B - 1);
+        const int64_t go = (int64_t)rr * G + q * H + u0 + ul;
+        x4[k] = *(const f32x4*)(xh + go);
+        r4[k] = *(const f32x4*)(R + go);
+#pragma unroll
+        for (int sl = 1; sl < NS; ++sl) {
+            const f32x4 t = *(const f32x4*)(R + sl * r_slab + go);
+            r4[k] += t;
+        }
+    }
+    constexpr int NPC = MAXB * (HH / 8), SPT = (NPC + NTH - 1) / NTH;   // 16-byte hh pieces (per thread: 10)
+    bf16x8 hv[SPT];
+#pragma unroll
+    for (int k = 0; k < SPT; ++k) {
+        const int i = min(tid + k * NTH, NPC - 1), r = i / (HH / 8), c = i % (HH / 8);
+        hv[k] = *(const bf16x8*)(hh + (int64_t)min(r, B - 1) * ld_hh + 8 * c);
+    }
+#pragma unroll
+    for (int k = 0; k < SPT; ++k) {
+        const int i = tid + k * NTH, r = i / (HH / 8), c = i % (HH / 8);
+        if (i >= NPC) break;
+        if (r >= B) hv[k] = bf16x8{};
+        *(bf16x8*)(sA + sw(r, c)) = hv[k];
+    }
+    __syncthreads();
+    f32x4 acc[NRT];
+#pragma unroll
+    for (int rt = 0; rt < NRT; ++rt) acc[rt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks)
+#pragma unroll
+        for (int rt = 0; rt < NRT; ++rt) {
+            const bf16x8 a = *(const bf16x8*)(sA + sw(16 * rt + fr, 4 * ks + fq));
+            acc[rt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, pf[ks], acc[rt], 0, 0, 0);
+        }
+    // modulation vectors (+ q) -> bf16 -> LDS: the epilogue needs all three
+    // blocks of a unit in one thread. The bf16-rounded value is what the
+    // backward will read, so g is formed from it too.
+#pragma unroll
+    for (int rt = 0; rt < NRT; ++rt)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            sV[w][16 * rt + 4 * fq + i][fr] = __bfloat162float(__float2bfloat16(acc[rt][i] + qv));
+    __syncthreads();
+    // ---- epilogue (no loads left): 8 threads per row (lanes 8k..8k+7)
+    const int ch = ul >> 4, cu = ul & 15;          // column tile half, column inside it
+#pragma unroll
+    for (int k = 0; k < RPT; ++k) {
+        const int r = rg + k * (NTH / 8);
+        if (r >= ((B + 7) & ~7)) break;            // uniform over each 8-lane row group and each wave
+        const bool on = r < B;
+        const int rr = on ? r : B - 1;
+        float g[4], s1 = 0.f, s2 = 0.f;
+        float vx[4], vh[4], vb[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            vx[i] = sV[0 + ch][rr][cu + i];
+            vh[i] = sV[2 + ch][rr][cu + i];
+            vb[i] = sV[4 + ch][rr][cu + i];
+            g[i] = x4[k][i] * vx[i] + r4[k][i] * vh[i] + vb[i];
+            s1 += g[i];
+            s2 += g[i] * g[i];
+        }
+        s1 += __shfl_xor(s1, 1, 64);
+        s2 += __shfl_xor(s2, 1, 64);
+        s1 += __shfl_xor(s1, 2, 64);
+        s2 += __shfl_xor(s2, 2, 64);
+        s1 += __shfl_xor(s1, 4, 64);
+        s2 += __shfl_xor(s2, 4, 64);
+        if (on) {
+            const int64_t go = (int64_t)rr * G + q * H + u0 + ul;
+            *(f32x4*)(gout + go) = f32x4{g[0], g[1], g[2], g[3]};
+            if (rlp) *(u32x2*)(rlp + go) = u32x2{pack_bf(r4[k][0], r4[k][1]), pack_bf(r4[k][2], r4[k][3])};
+            const int64_t vo = (int64_t)rr * NV + u0 + ul;
+            *(u32x2*)(vec + vo + q * H) = u32x2{pack_bf(vx[0], vx[1]), pack_bf(vx[2], vx[3])};
+            *(u32x2*)(vec + vo + (4 + q) * H) = u32x2{pack_bf(vh[0], vh[1]), pack_bf(vh[2], vh[3])};
+            *(u32x2*)(vec + vo + (8 + q) * H) = u32x2{pack_bf(vb[0], vb[1]), pack_bf(vb[2], vb[3])};
+            if (ug == 0) {
+                float* sp = stats + (((int64_t)rr * 4 + q) * ntile + blockIdx.x) * 2;
+                sp[0] = s1;
+                sp[1] = s2;
+            }
+        }
+    }
+}
+
+}  // namespace
+
+// hh [B][Hh] bf16 rows (stride ld_hh), PlT [12H][Hh] bf16, qb [12H] fp32
+// (q, with the main bias added to blocks 8..11), xh [B][4H] fp32, R = sum of
+// nslab fp32 slabs [B][4H] (stride r_slab), outputs vec [B][12H] bf16,
+// g [B][4H] fp32, rlp [B][4H] bf16 (or null), stats [B][4][H/32][2] fp32.
+SKR_API int skr_hyper_mod_fwd(const void* hh, int64_t ld_hh, const void* PlT, const float* qb, const float* xh,
+                              const float* R, int64_t r_slab, int nslab, void* vec, float* g, void* rlp,
+                              float* stats, int B, int H, int Hh, hipStream_t s) {
+    if (B <= 0) return 0;
+    if (B > MAXB || Hh != HH || H % TU != 0) return -2;
+    if (((uintptr_t)hh | (uintptr_t)PlT | (uintptr_t)xh | (uintptr_t)R | (uintptr_t)vec | (uintptr_t)g |
+         (uintptr_t)rlp) & 15 || (ld_hh % 8) || (r_slab % 4))
+        return -4;
+    const dim3 grid(H / TU, 4);
+    const auto* a = (const __hip_bfloat16*)hh;
+    const auto* p = (const __hip_bfloat16*)PlT;
+    auto* v = (__hip_bfloat16*)vec;
+    auto* rl = (__hip_bfloat16*)rlp;
+    switch (nslab) {
+        case 1: hipLaunchKernelGGL(hyper_mod_fwd<1>, grid, dim3(NTH), 0, s, a, ld_hh, p, qb, xh, R, r_slab, v, g, rl, stats, B, H); break;
+        case 2: hipLaunchKernelGGL(hyper_mod_fwd<2>, grid, dim3(NTH), 0, s, a, ld_hh, p, qb, xh, R, r_slab, v, g, rl, stats, B, H); break;
+        case 4: hipLaunchKernelGGL(hyper_mod_fwd<4>, grid, dim3(NTH), 0, s, a, ld_hh, p, qb, xh, R, r_slab, v, g, rl, stats, B, H); break;
+        default: return -3;
+    }
+    return SKR_CHECK_LAUNCH();
+}

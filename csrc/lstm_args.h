@@ -37,6 +37,11 @@ struct FwdArgs {
     uint64_t* part;                    // [2][B][cluster][16] tagged partial statistics (zeroed per sequence)
     int* err;                          // set to 1 if a cluster wait timed out
     __hip_bfloat16* r_lp;              // MOD: bf16 copy of the summed R ([B, ld_R]) for the backward, or null
+    // MOD 3 (HyperLSTM main cell after csrc/hyper_mod.hip): the gate
+    // pre-activations g [B, 4H] and per-tile LayerNorm partial sums
+    // [B][4][gstat_tiles][2] are precomputed -- no statistics exchange for
+    // the gates; xp / R / vec / bias are not read
+    const float* gpre; const float* gstats; int gstat_tiles;
 };
 
 struct BwdArgs {

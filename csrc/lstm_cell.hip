@@ -268,6 +268,7 @@ using KernelT = void (*)(const A);
 
 template <int NT, int UPT, int NS>
 KernelT<FwdArgs> pick(bool ln, int mod, const FwdArgs*) {
+    if (mod == 3) return cell_fwd<NT, UPT, 1, true, 3>;
     if (mod == 2) return cell_fwd<NT, UPT, NS, true, 2>;
     if (mod) return cell_fwd<NT, UPT, NS, true, 1>;
     if (ln) return cell_fwd<NT, UPT, NS, true, 0>;
@@ -349,6 +350,12 @@ inline int64_t coresident_capacity(const void* k, int nt) {
 template <typename A>
 int launch(const A& a, bool ln, int mod, hipStream_t s) {
     if (mod && !ln) return -3;
+    if constexpr (std::is_same<A, FwdArgs>::value) {
+        if (mod == 3 && (a.gpre == nullptr || a.gstats == nullptr || a.gstat_tiles < 1 || a.r_lp != nullptr)) return -3;
+    }
+    if constexpr (std::is_same<A, BwdArgs>::value) {
+        if (mod == 3) return -3;
+    }
     if (a.B <= 0) return 0;
     const int H = a.H;
     const int C = a.cluster > 1 ? a.cluster : 1;
@@ -387,7 +394,7 @@ int launch(const A& a, bool ln, int mod, hipStream_t s) {
 // mirrors of FwdArgs / BwdArgs in sketch_rnn_amd/ops/_hipapi.py).
 // args->cluster = C workgroups per row (<= 1: one).
 SKR_API int skr_lstm_fwd_step(const FwdArgs* args, int ln, int mod, hipStream_t s) {
-    return launch(*args, ln != 0, mod, s);   // mod: 0 none, 1 fp32 vec, 2 bf16 vec
+    return launch(*args, ln != 0, mod, s);   // mod: 0 none, 1 fp32 vec, 2 bf16 vec, 3 precomputed g + stats
 }
 
 SKR_API int skr_lstm_bwd_step(const BwdArgs* args, int ln, int mod, hipStream_t s) {

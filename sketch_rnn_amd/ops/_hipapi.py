@@ -37,6 +37,7 @@ class LstmFwdArgs(C.Structure):
         ("c_carry", _p),
         ("cluster", _i), ("part", _p), ("err", _p),
         ("r_lp", _p),
+        ("gpre", _p), ("gstats", _p), ("gstat_tiles", _i),
     ]
 
 
@@ -337,6 +338,8 @@ class HipLib:
         lib.skr_skinny_gemm_fp8_v2.restype = _i
         lib.skr_skinny_gemm_group_fp8.argtypes = [C.POINTER(GemmProblem8), _i, _p]
         lib.skr_skinny_gemm_group_fp8.restype = _i
+        lib.skr_hyper_mod_fwd.argtypes = [_p, _i64, _p, _p, _p, _p, _i64, _i, _p, _p, _p, _p, _i, _i, _i, _p]
+        lib.skr_hyper_mod_fwd.restype = _i
         lib.skr_cast_transpose_bf16.argtypes = [_p, _i64, _i64, _i, _i, _i, _p, _i64, _i64, _p, _i64, _i64, _p]
         lib.skr_cast_transpose_bf16.restype = _i
         lib.skr_hash_normal.argtypes = [_p, _u32, _u32, _p, _i64, _p]

@@ -159,8 +159,8 @@ class _ClusterSync:
     """Per-pass cell geometry + the tagged partial-statistics exchange buffer
     (zeroed once per pass; tags = step + 1 make earlier steps' slots stale)."""
 
-    def __init__(self, T: int, BB: int, H: int, device, ln: bool = True):
-        self.C = cell_geometry(H, BB, ln)
+    def __init__(self, T: int, BB: int, H: int, device, ln: bool = True, C: int = 0):
+        self.C = C if C > 0 else cell_geometry(H, BB, ln)
         self.on = ln and self.C > 1
         if self.on:
             # [phase][row][workgroup][16 x 8-byte granules]: one 128-byte line per slot
@@ -448,6 +448,13 @@ PERSIST_LENGTHS = os.environ.get("SKR_PERSIST_LENGTHS", "1") != "0"
 # =====================================================================================
 # HyperLSTM sequence
 # =====================================================================================
+# The modulation GEMM fused with the main gates' pre-activations and
+# LayerNorm partial sums (csrc/hyper_mod.hip); SKR_HYPER_MOD=0 keeps the
+# plain bf16-output GEMM + the main cell's in-launch statistics exchange.
+HYPER_MOD = os.environ.get("SKR_HYPER_MOD", "1") != "0"
+HYPER_MAIN_C = int(os.environ.get("SKR_HYPER_MAIN_C", "0"))   # workgroups per row of the MOD-3 main cell (0: policy)
+
+
 def _split_override(var: str, planned: int, K: int) -> int:
     """Split-K factor of a per-step HyperLSTM product: the planned one, or
     ``$var`` (tuning sweeps) when it divides K into whole 64-wide K tiles."""
@@ -584,6 +591,19 @@ class _HyperSeq(torch.autograd.Function):
         rmi = (lambda t: t) if RM.shape[0] == T else (lambda t: 0)
         RY = torch.empty(max(S_y, 1), B, Gh, device=dev, dtype=f32)
         mod = 2 if vbf else 1
+        # modulation step fused with the gate pre-activations and their
+        # LayerNorm partial sums (csrc/hyper_mod.hip): the main cell then needs
+        # no statistics exchange for the gates (MOD 3) and VEC carries q (and
+        # the main bias in its shift block) -- the backward uses a zero vec_bias
+        hmod = HYPER_MOD and vbf and dev.type == "cuda" and Hh == 256 and B <= 112 and H % 32 == 0 and S_m in (1, 2, 4)
+        if hmod:
+            mod = 3
+            qb = q.detach().clone()
+            qb[8:] += bias_c.detach().view(4, H)
+            qb = qb.reshape(12 * H).contiguous()
+            GP = torch.empty(B, G, device=dev, dtype=f32)
+            GS = torch.empty(B, 4, H // 32, 2, device=dev, dtype=f32)
+            XHc = XH.contiguous()
         # hyper cell args (LN-LSTM, no modulation)
         ah = LstmFwdArgs()
         ah.B, ah.H = B, Hh
@@ -603,7 +623,8 @@ class _HyperSeq(torch.autograd.Function):
         am.forget_bias, am.keep = float(forget_bias), float(keep)
         am.seed, am.stream = sd.data_ptr(), int(stream)
         am.ld_lp, am.lp_kind = K, _lp_kind(A)
-        clm, clh = _ClusterSync(T, B, H, dev), _ClusterSync(T, B, Hh, dev)
+        clm = _ClusterSync(T, B, H, dev, C=HYPER_MAIN_C if hmod else 0)
+        clh = _ClusterSync(T, B, Hh, dev)
         st = _stream()
         group = not fp8 and gemm.GROUPED and S_m >= 1 and S_y >= 1 and dt == torch.bfloat16
         for t in range(T):
@@ -620,12 +641,18 @@ class _HyperSeq(torch.autograd.Function):
                 rgemm(A[t, :, :H], WhT, RM[rmi(t)], S_m)
                 rgemm(A[t], WyT, RY, S_y)
             _check(lib.lib.skr_lstm_fwd_step(ctypes.byref(ah), 1, 0, st), "hyper_fwd_step")
-            if vbf:
+            if hmod:
+                _check(lib.lib.skr_hyper_mod_fwd(A[t + 1, :, H:].data_ptr(), K, PlT.data_ptr(), qb.data_ptr(),
+                                                 XHc[t].data_ptr(), RM[rmi(t)].data_ptr(), B * G, S_m,
+                                                 VEC[t].data_ptr(), GP.data_ptr(), _ptr(RLP[t] if RLP is not None else None),
+                                                 GS.data_ptr(), B, H, Hh, st), "hyper_mod_fwd")
+                am.gpre, am.gstats, am.gstat_tiles = GP.data_ptr(), GS.data_ptr(), H // 32
+            elif vbf:
                 gemm.rec_gemm_bf16out(A[t + 1, :, H:], PlT, VEC[t])
             else:
                 rgemm(A[t + 1, :, H:], PlT, VEC[t].unsqueeze(0), S_v)
             am.xp, am.R, am.vec = XH[t].data_ptr(), RM[rmi(t)].data_ptr(), VEC[t].data_ptr()
-            am.r_lp = RLP[t].data_ptr() if RLP is not None else None
+            am.r_lp = RLP[t].data_ptr() if (RLP is not None and not hmod) else None
             am.c_prev, am.step = CC[t].data_ptr(), t
             am.h_out = Hout[t].data_ptr()
             if not infer:
@@ -638,7 +665,7 @@ class _HyperSeq(torch.autograd.Function):
         for k, v in dict(xl=xl, x=x, zc=zc, bp=bp, XH=XH, Whl=Whl, Wyl=Wyl, Pl=Pl, q=q, S_m=S_m, A=A, RM=RM,
                          RLP=RLP, CC=CC, HCC=HCC, XHAT=XHAT, RSTD=RSTD, CHAT=CHAT, HH=HH, HXHAT=HXHAT, HRSTD=HRSTD,
                          HCHAT=HCHAT, VEC=VEC, seed=sd, meta=meta, W_x=W_x, hW_x=hW_x, W_z=W_z, b_z=b_z, W_a=W_a,
-                         mln=mln, hln=hln).items():
+                         mln=mln, hln=hln, vec_folded=hmod).items():
             setattr(s, k, v)
         ctx.s = s
         ctx.dims = (T, B, IX, IN, H, Hh, E)
@@ -697,7 +724,9 @@ class _HyperSeq(torch.autograd.Function):
         am.ln_b, am.forget_bias = s.mln[1].data_ptr(), float(forget_bias)
         am.ld_xp, am.ld_R = G, G
         am.R_nslab, am.R_slab = max(s.S_m, 1), B * G
-        am.vec_gs, am.vec_ld, am.vec_bias = H, 12 * H, s.q.data_ptr()
+        # csrc/hyper_mod.hip folds q into the saved vectors
+        vbias = torch.zeros(12 * H, device=dev, dtype=f32) if s.vec_folded else s.q
+        am.vec_gs, am.vec_ld, am.vec_bias = H, 12 * H, vbias.data_ptr()
         am.keep, am.seed, am.stream = float(keep), s.seed.data_ptr(), int(stream)
         am.ld_dG, am.ld_dG_lp, am.dG_lp_kind = G, G, 1 if lp_on else 0
         am.ld_dxp, am.dxp_kind, am.dvec_kind = G, 1 if lp_on else 2, 1 if lp_on else 2

@@ -263,6 +263,34 @@ def test_hyper_sequence_bf16_close(H, Hh, E):
     _close(res[0][5:], res[1][5:], 6e-2, 6e-2, "grad")
 
 
+@pytest.mark.parametrize("B,keep,hkeep", [(100, 0.9, 0.9), (37, 1.0, 1.0)])
+def test_hyper_mod_path_vs_oracle(B, keep, hkeep):
+    """The fused modulation step (csrc/hyper_mod.hip: vec + gate
+    pre-activations + LayerNorm partial sums; the main cell without its
+    statistics exchange) is as close to the fp32 oracle as the plain chain
+    (bf16-output modulation GEMM + in-launch exchange): per output / gradient,
+    error(fused) <= 1.5 error(plain) + 1e-3 of the largest element."""
+    from sketch_rnn_amd.ops import recurrent
+    p, x, z, st, w = _hyper_setup(6, 7, B, 5, 16, 2048, 256, 32, jitter=0.02, state=0.1)
+    runs = {}
+    try:
+        for name, backend, dt, fused in (("ref", "torch", "fp32", True), ("fused", "hip", "bf16", True),
+                                         ("plain", "hip", "bf16", False)):
+            recurrent.HYPER_MOD = fused
+            ops.set_backend(backend)
+            ops.set_compute_dtype(dt)
+            runs[name] = _hyper_run(p, x, z, st, w, keep, hkeep)
+    finally:
+        recurrent.HYPER_MOD = True
+    for i, n in enumerate(_names(p)):
+        ref = runs["ref"][i].float()
+        scale = max(ref.abs().max().item(), 1e-3)
+        e_f = (runs["fused"][i].float() - ref).abs().max().item()
+        e_p = (runs["plain"][i].float() - ref).abs().max().item()
+        ok = e_f <= 1.5 * e_p + 1e-3 * scale
+        assert ok, (n, e_f, e_p, scale)
+
+
 @pytest.mark.parametrize("H,Hh,E", [(2048, 256, 32), (512, 64, 8)])
 def test_hyper_grouped_gemm_path_bitwise(H, Hh, E):
     """bf16 HyperLSTM with the grouped per-step GEMM launches equals the
