@@ -146,7 +146,7 @@ def main():
     cost = float(out["cost"])
     recon = None
     if not args.no_eval:
-        ev = trainer.evaluate(test, max_batches=1)
+        ev = trainer.evaluate(test)      # the whole held-out split (test.num_batches batches)
         recon = ev["r_cost"]
     global_batch = args.batch * world
     positions_per_s = global_batch * args.seq_len * args.steps / elapsed
@@ -179,6 +179,9 @@ def main():
             "valid_fraction": round(value / positions_per_s, 4),
             "train_cost": round(cost, 4),
             "test_recon_nll": None if recon is None else round(recon, 4),
+            "test_recon_nll_note": "mean over the full synthetic test split (%d sketches) after %d random-init "
+                                   "training steps: a smoke value, not a quality result (see profiles/ for "
+                                   "the convergence runs)" % (test.num_batches * args.batch, args.warmup + args.steps),
         }
         print(json.dumps(rec), flush=True)
 

@@ -94,15 +94,28 @@ def main(argv=None) -> int:
     py_rng = random.Random(a.seed)
     accepted, attempts = [], 0
     if a.device_sampler and device.startswith("cuda"):
-        from ..sample.fused import FusedRefDecoder, fused_decode_ok
+        from ..sample.fused import FusedRefDecoder, NotCoResident, fused_decode_ok
+
+        def graph_decoder():
+            return GraphDecoder(model, a.batch, a.sample_length, a.temperature,
+                                fix_pen_temperature=a.fix_pen_temperature)
+        dec = None
         if fused_decode_ok(model) and not a.graph_decoder:   # one launch per batch (csrc/decode_ref.hip)
-            dec = FusedRefDecoder(model, a.batch, a.sample_length, a.temperature,
-                                  fix_pen_temperature=a.fix_pen_temperature)
-        else:
-            dec = GraphDecoder(model, a.batch, a.sample_length, a.temperature,
-                               fix_pen_temperature=a.fix_pen_temperature)
+            try:
+                dec = FusedRefDecoder(model, a.batch, a.sample_length, a.temperature,
+                                      fix_pen_temperature=a.fix_pen_temperature)
+            except NotCoResident as e:
+                print("fused decoder unavailable (%s); using the graph decoder" % e)
+        if dec is None:
+            dec = graph_decoder()
         while len(accepted) < a.num_picture and attempts < a.max_attempts:
-            strokes, lengths = dec.run(seed=rng.randint(1 << 30))
+            seed = rng.randint(1 << 30)
+            try:
+                strokes, lengths = dec.run(seed=seed)
+            except NotCoResident as e:           # a smaller device than the chunking assumed
+                print("fused decoder unavailable (%s); using the graph decoder" % e)
+                dec = graph_decoder()
+                strokes, lengths = dec.run(seed=seed)
             s_np, l_np = strokes.cpu().numpy(), lengths.cpu().numpy()
             for k in range(a.batch):
                 attempts += 1

@@ -66,9 +66,11 @@ def mdn_loss_hip(z, target, M, mode="magenta", stroke_importance=200.0, is_train
 # ---------------------------------------------------------------------------------
 def head_fused_ok(x: torch.Tensor, W: torch.Tensor, M: int) -> bool:
     """The fused MDN head applies to bf16 HIP training on the GPU with M <= 24
-    mixtures and a decoder width that is a multiple of 128."""
+    mixtures, a decoder width that is a multiple of 128 and at least one row
+    (an empty batch takes the unfused path, whose reductions handle N = 0)."""
     from . import gemm, use_hip
     return (FUSED_HEAD and x.is_cuda and use_hip(x) and gemm.lp_dtype() == torch.bfloat16 and 1 <= M <= 24
+            and x.numel() > 0
             and W.shape[0] % 128 == 0 and W.shape[1] == 3 + 6 * M)
 
 

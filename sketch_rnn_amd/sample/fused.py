@@ -36,10 +36,16 @@ def fused_decode_ok(model) -> bool:
             and cfg.num_layers in (1, 2) and 1 <= cfg.num_mixture <= 32)
 
 
-def _chunk_rows(L: int, mtw: int) -> int:
+class NotCoResident(RuntimeError):
+    """The launch's workgroups cannot all be resident at once on this device
+    (``skr_decode_ref`` returned -8); callers fall back to ``GraphDecoder``."""
+
+
+def _chunk_rows(L: int, mtw: int, cus: int = 256) -> int:
     """Rows one launch can take: every workgroup must be co-resident (one
-    ~100 KB-LDS workgroup per CU, 256 CUs; L*16 + 1 workgroups per row block)."""
-    return (256 // (L * (_H // 16) + 1)) * 16 * mtw
+    ~100 KB-LDS workgroup per CU, ``cus`` CUs -- 256 on MI355X; L*16 + 1
+    workgroups per row block)."""
+    return (cus // (L * (_H // 16) + 1)) * 16 * mtw
 
 
 class FusedRefDecoder:
@@ -61,7 +67,11 @@ class FusedRefDecoder:
         self.noutp = -(-self.nout // 16) * 16
         self.dev = next(model.parameters()).device
         self.mtw = 1 if self.B <= 16 else 2
-        self.rows = _chunk_rows(self.L, self.mtw)
+        cus = torch.cuda.get_device_properties(self.dev).multi_processor_count if self.dev.type == "cuda" else 256
+        self.rows = _chunk_rows(self.L, self.mtw, cus)
+        if self.rows <= 0:
+            raise NotCoResident("FusedRefDecoder: %d CUs cannot hold one row block (%d workgroups)"
+                                % (cus, self.L * (_H // 16) + 1))
         self.seed = torch.zeros(1, dtype=torch.int64, device=self.dev)
         self._w = None
         self._sig = None
@@ -122,6 +132,8 @@ class FusedRefDecoder:
         a.zout = zout.data_ptr() if zout is not None else None
         a.seed, a.flags, a.err = self.seed.data_ptr(), flags.data_ptr(), cluster_error_flag(dev).data_ptr()
         rc = self.lib.lib.skr_decode_ref(ctypes.byref(a), ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
+        if rc == -8:
+            raise NotCoResident("skr_decode_ref: workgroups cannot be co-resident on this device (code -8)")
         if rc != 0:
             raise RuntimeError("skr_decode_ref: launch failed (code %d)" % rc)
         keep += [flags, done]

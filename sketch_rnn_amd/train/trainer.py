@@ -40,15 +40,23 @@ class DivergenceError(RuntimeError):
 
 def check_device_faults() -> None:
     """Raise when a kernel reported a fault through a device flag since the
-    last check: the clustered LayerNorm cell kernels set it when an in-launch
-    wait on a peer workgroup timed out (that step's outputs are invalid).
-    Costs one tiny device read; trainers call it at every log interval."""
+    last check. Every kernel with in-launch waits on peer workgroups (the
+    clustered LayerNorm cells, the persistent LSTM stack, the fused decoders,
+    the hyper-fused GEMM) bounds its spins and sets the flag when one timed
+    out -- that step's outputs are invalid. Under DP the flag is max-reduced
+    over the ranks, so every rank raises at the same step instead of the
+    healthy ones blocking in their next collective. Trainers call it at every
+    log interval and before every checkpoint save (all ranks together)."""
     from ..ops import recurrent
+    bad = 0
     for f in list(recurrent._ERR_FLAGS.values()):
         if int(f.item()) != 0:
             f.zero_()
-            raise DivergenceError("LayerNorm cell kernel: in-launch exchange with a peer workgroup timed out "
-                                  "(workgroups not co-resident); the step's results are invalid")
+            bad = 1
+    if dp.max_scalar(float(bad)) != 0:
+        raise DivergenceError("device fault: an in-launch wait on a peer workgroup timed out on %s "
+                              "(workgroups not co-resident); the step's results are invalid"
+                              % ("this rank" if bad else "another rank"))
 
 
 def _to_device(a, device, dtype=torch.float32):
@@ -440,25 +448,36 @@ class VAETrainer:
             return self._train_loop(num_steps, eval_every, log_every)
         finally:
             if self._prefetch is not None:
+                consumed = self._prefetch.consumed_state
                 self._prefetch.close()
                 self._prefetch = None
+                # the producer drew batches ahead of the consumer: rewind the
+                # dataset to the last batch actually trained on, so a later
+                # train() / save() continues the same sequence
+                if consumed is not None and hasattr(self.train_set, "load_state_dict"):
+                    self.train_set.load_state_dict(consumed)
 
     def _train_loop(self, num_steps, eval_every, log_every):
         cfg = self.cfg
         num_steps = cfg.num_steps if num_steps is None else num_steps
         pf = self._prefetch
         t0 = time.time()
+        valid = 0.0     # this rank's non-padding stroke points since the last log line
         while self.step < num_steps:
             with phase("data", self.host_times):
                 raw = pf.get() if pf is not None else self.train_set.random_batch(self.rank, self.world)
+                valid += float(np.asarray(raw[1]).sum())
                 batch = self.batch_to_device(raw)
             with phase("step", self.host_times):
                 out = self.train_step(*batch)
             if self.step % log_every == 0 or self.step == num_steps:
                 check_device_faults()
                 vals = {k: float(v) for k, v in out.items()}
-                dt = (time.time() - t0) / log_every
+                n_int = (self.step - 1) % log_every + 1          # steps since the last log line
+                dt = (time.time() - t0) / n_int
                 t0 = time.time()
+                valid_all = dp.sum_scalar(valid)                # every rank's batches (bench.py's metric)
+                valid = 0.0
                 if self.rank == 0:
                     self.log("step: %d, lr: %.6f, klw: %0.4f, cost: %.4f, recon: %.4f, kl: %.4f, time/step: %.4f" % (
                         self.step, self.opt.lr, schedules.kl_weight(cfg, self.step - 1), vals["cost"],
@@ -467,7 +486,8 @@ class VAETrainer:
                     if self.metrics_path:
                         rec = dict(step=self.step, **vals, time=dt, lr=self.opt.lr,
                                    kl_weight=schedules.kl_weight(cfg, self.step - 1),
-                                   strokes_per_s=self.world * cfg.batch_size * cfg.max_seq_len / max(dt, 1e-9),
+                                   strokes_per_s=valid_all / max(dt * n_int, 1e-9),      # valid points
+                                   positions_per_s=self.world * cfg.batch_size * cfg.max_seq_len / max(dt, 1e-9),
                                    skipped=self.opt.skipped_steps(),
                                    host_ms=self.host_times.mean_ms(), gpu_ms=self.gpu_times.collect())
                         self.host_times.reset()
@@ -484,5 +504,7 @@ class VAETrainer:
                     self.log("valid: cost %.4f recon %.4f kl %.4f" % (ev["cost"], ev["r_cost"], ev["kl_cost"]))
             if cfg.save_every and self.step % cfg.save_every == 0:
                 with phase("save", self.host_times):
+                    check_device_faults()     # never checkpoint a step whose exchange timed out
                     self.save()
+        check_device_faults()
         return self.save()

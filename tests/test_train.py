@@ -323,6 +323,8 @@ def test_vae_metrics_jsonl_and_phases(tmp_path):
         assert {"cost", "r_cost", "kl_cost", "grad_norm", "lr", "kl_weight", "strokes_per_s", "skipped",
                 "host_ms"} <= set(r)
         assert "data" in r["host_ms"] and "step" in r["host_ms"] and r["skipped"] == 0
+        # strokes_per_s counts valid (non-padding) points, like bench.py; positions_per_s the padded grid
+        assert 0 < r["strokes_per_s"] < r["positions_per_s"]
     pt = PhaseTimes()
     with phase("x", pt):
         pass
@@ -362,3 +364,27 @@ def test_vae_resume_with_prefetch_is_exact(tmp_path):
     assert c.resume() and c.step == 3
     c.train(num_steps=6, log_every=3)
     assert torch.equal(a.opt.flat, c.opt.flat)
+
+
+def test_vae_train_twice_continues_the_batch_sequence(tmp_path):
+    """The prefetcher draws batches ahead; train() rewinds the dataset to the
+    last batch consumed when it returns, so train(3); train(6) sees the same
+    batches as one train(6) (checkpoint-free continuation)."""
+    from sketch_rnn_amd.train.trainer import VAETrainer
+    cfg = VAEConfig(enc_rnn_size=8, dec_rnn_size=16, z_size=4, num_mixture=2, max_seq_len=24, batch_size=4,
+                    save_every=0)
+    (train, valid, test), _ = _vae_sets(cfg)
+    a = VAETrainer(cfg, train, valid, test, save_dir=str(tmp_path / "a"), log=lambda s: None)
+    a.train(num_steps=6, log_every=3)
+    (train, valid, test), _ = _vae_sets(cfg)
+    b = VAETrainer(cfg, train, valid, test, save_dir=str(tmp_path / "b"), log=lambda s: None)
+    b.train(num_steps=3, log_every=3)
+    b.train(num_steps=6, log_every=3)
+    assert torch.equal(a.opt.flat, b.opt.flat)
+
+
+def test_fused_decoder_chunking_follows_cu_count():
+    from sketch_rnn_amd.sample.fused import _chunk_rows
+    assert _chunk_rows(2, 2) == (256 // 33) * 32
+    assert _chunk_rows(2, 1, cus=80) == (80 // 33) * 16
+    assert _chunk_rows(2, 1, cus=32) == 0      # -> NotCoResident, the CLI uses GraphDecoder
