@@ -1,0 +1,331 @@
+// Long-K weight-gradient GEMM: C = A^T . B over the T*B saved rows of a
+// sequence (reference: /root/reference/model.py:182, tf.gradients over every
+// Linear of the unrolled RNN).
+//
+//   A [K, M] bf16 (row stride lda)    B [K, N] bf16 (row stride ldb)
+//   C [M, N] fp32 = sum_k A[k, :]^T B[k, :]        (+ optional colsum(B) [N])
+//
+// K = T*B = 25,000 rows for the headline decoder; M, N are weight dims
+// (2048 x 8192, 256 x 24576, 2304 x 1024, 512 x 2048 per direction).
+//
+// Both operands arrive with K as the ROW index, so an MFMA fragment (8
+// consecutive k of one output row/column) is a COLUMN of the staged tile.
+// gfx950's ds_read_b64_tr_b16 delivers exactly that: per 16-lane group it
+// reads a 4-row x 16-column block and hands lane i column i -- two reads
+// make a v_mfma_f32_32x32x16_bf16 operand (lane l: k = 8 (l >> 5) .. +7 of
+// row/column l & 31). No register transposes, no second LDS image.
+//
+// Tiling (one workgroup per CU, 512 threads = 8 waves):
+//   * output tile 256 x 256, wave (wm, wn) = 4 x 2 owns 64 x 128 = 2 x 4
+//     MFMA 32x32 tiles (128 fp32 accumulators per lane);
+//   * K-step 32 rows: 16 KB of A + 16 KB of B per step, 4.2 MFLOP -- the
+//     256 x 256 tile is what keeps the per-CU ingest (~75 GB/s at the MFMA
+//     peak) inside what L2 feeds one CU;
+//   * LDS-DMA ring (global_load_lds_dwordx4, 1 KiB per wave instruction = 2
+//     tile rows), 4 stages x 32 KB, one counted vmcnt wait + one s_barrier per
+//     K-step (the skinny GEMM's ring, csrc/skinny_gemm.hip);
+//   * LDS rows of 512 B with the 16-byte chunk index XOR (row & 3) << 2
+//     (applied on the per-lane GLOBAL address, since a DMA wave writes 1 KiB
+//     linearly): the 32 lanes of a transposed read's half touch 4 rows x 4
+//     chunks, which the XOR spreads over all 64 banks -- conflict-free;
+//   * split-K over gridDim (S slabs of fp32 partials, summed by a second
+//     deterministic pass) only when the output has too few tiles to fill the
+//     chip; tile order is XCD-aware: workgroup id % 8 picks the XCD, and
+//     consecutive tiles of one XCD form 4-row groups, so the A and B tiles a
+//     K-step needs are shared in that XCD's L2;
+//   * the K tail (K % 32 rows): clamped loads, then the invalid rows of the
+//     last stage are zeroed in LDS before use.
+// Measured (scripts/bench_wgrad.py, profiles/r3/wgrad_bench.jsonl): 804 /
+// 471 / 143 / 130 us for the dW_h / dP+colsum / dW_y / encoder shapes
+// against hipBLASLt's 837 / 700 / 174 / 168. A variant with fragments
+// double-buffered across K-steps and a 5-stage ring was slower on dW_h (940).
+// Optional colsum(B) (the bias gradient folded into a projection's weight
+// gradient: HyperLSTM dVEC): waves wm == 0 add their B fragments in fp32.
+#include "common.h"
+
+namespace {
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(16))) float f32x16;
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+
+constexpr int TM = 256, TN = 256, BK = 32, NT = 512, NSTG = 4;
+constexpr int ROWB = 512;                 // bytes per LDS tile row (256 bf16)
+constexpr int OPB = BK * ROWB;            // 16 KB per operand per stage
+constexpr int STGB = 2 * OPB;             // 32 KB per stage
+constexpr int GPW = 4;                    // DMA instructions per wave per K-step
+
+struct WgArgs {
+    const __hip_bfloat16* A; int64_t lda, a_bs;
+    const __hip_bfloat16* B; int64_t ldb, b_bs;
+    float* C; int64_t c_bs;               // slab s of batch z at C + z * c_bs + s * M * N
+    float* cs;                            // colsum slabs [batch][S][N] or null
+    int64_t K; int M, N, S, kslice, tiles_m, tiles_n, total, per_xcd;
+};
+
+__device__ __forceinline__ int swz(int row, int chunk) { return chunk ^ ((row & 3) << 2); }
+
+template <int AHEAD_MAX>
+__device__ __forceinline__ void wait_ahead(int ahead) {
+    if constexpr (AHEAD_MAX >= 2) if (ahead >= 2) { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * GPW) : "memory"); return; }
+    if (ahead == 1) { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GPW) : "memory"); return; }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+// ds_read_b64_tr_b16 through inline asm: the compiler models the builtin's
+// LDS read as aliasing every in-flight LDS-DMA write and drains the whole
+// prefetch ring (s_waitcnt vmcnt(0)) in front of it. The asm read is opaque
+// to the waitcnt pass, so the kernel waits for it explicitly (frag_wait) --
+// tied to the destination registers, so no use can be scheduled above it.
+__device__ __forceinline__ s16x4 tr_read(uint32_t addr) {
+    s16x4 v;
+    asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(v) : "v"(addr));
+    return v;
+}
+
+struct Frags {
+    s16x4 a[2][2], b[4][2];   // [tile][k half]: two transposed reads per MFMA operand
+};
+
+// wait until at most N LDS reads are outstanding (the younger fragment set's)
+template <int N>
+__device__ __forceinline__ void frag_wait(Frags& f) {
+    asm volatile("s_waitcnt lgkmcnt(%12)"
+                 : "+v"(f.a[0][0]), "+v"(f.a[0][1]), "+v"(f.a[1][0]), "+v"(f.a[1][1]), "+v"(f.b[0][0]),
+                   "+v"(f.b[0][1]), "+v"(f.b[1][0]), "+v"(f.b[1][1]), "+v"(f.b[2][0]), "+v"(f.b[2][1]),
+                   "+v"(f.b[3][0]), "+v"(f.b[3][1])
+                 : "n"(N));
+}
+
+__device__ __forceinline__ bf16x8 join(const s16x4 (&h)[2]) {
+    typedef short s16x8 __attribute__((ext_vector_type(8)));
+    const s16x8 v = {h[0][0], h[0][1], h[0][2], h[0][3], h[1][0], h[1][1], h[1][2], h[1][3]};
+    return __builtin_bit_cast(bf16x8, v);
+}
+
+template <bool CS>
+__global__ __launch_bounds__(NT) void wgrad_kernel(const WgArgs g) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    // ---- workgroup -> (batch, split, tile): XCD-major linear order
+    const int xcd = blockIdx.x & 7, lin = xcd * g.per_xcd + (blockIdx.x >> 3);
+    if (lin >= g.total) return;                       // whole workgroup, before any barrier
+    const int tiles = g.tiles_m * g.tiles_n;
+    const int t = lin % tiles, zs = lin / tiles;      // zs = batch * S + split
+    const int split = zs % g.S, z = zs / g.S;
+    const int gsz = 4 * g.tiles_n, grp = t / gsz, fm = grp * 4;
+    const int gm = min(g.tiles_m - fm, 4);
+    const int tm = fm + (t % gsz) % gm, tn = (t % gsz) / gm;
+    const int m0 = tm * TM, n0 = tn * TN;
+    const int64_t k0 = (int64_t)split * g.kslice;
+    const int64_t kend = min(g.K, k0 + g.kslice);
+    const int nk = (int)((kend - k0 + BK - 1) / BK);
+    const int tail = (int)(kend - k0) - (nk - 1) * BK;     // valid rows of the last K-step (1..32)
+    const __hip_bfloat16* A = g.A + z * g.a_bs;
+    const __hip_bfloat16* B = g.B + z * g.b_bs;
+
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    // ---- DMA sources: wave w moves tile rows {2w, 2w+1} and {2w+16, 2w+17} of A and of B
+    const int hr = lane >> 5, lc = lane & 31;
+    const __hip_bfloat16* asrc[2];
+    const __hip_bfloat16* bsrc[2];
+    int rowk[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const int R = 2 * w + 16 * i + hr;
+        rowk[i] = R;
+        const int c = swz(R, lc);
+        asrc[i] = A + m0 + 8 * c;
+        bsrc[i] = B + n0 + 8 * c;
+    }
+    auto issue = [&](int kt) {
+        char* st = smem + (kt % NSTG) * STGB;
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const int64_t kr = min(k0 + (int64_t)kt * BK + rowk[i], kend - 1);   // clamped: finite data
+            __builtin_amdgcn_global_load_lds((const void*)(asrc[i] + kr * g.lda),
+                                             (__attribute__((address_space(3))) void*)(st + (2 * w + 16 * i) * ROWB),
+                                             16, 0, 0);
+            __builtin_amdgcn_global_load_lds((const void*)(bsrc[i] + kr * g.ldb),
+                                             (__attribute__((address_space(3))) void*)(st + OPB + (2 * w + 16 * i) * ROWB),
+                                             16, 0, 0);
+        }
+    };
+
+    // ---- fragment read offsets (bytes inside an operand tile), fixed across K-steps
+    const int wm = w >> 1, wn = w & 1;
+    const int G = lane >> 4, h = G >> 1, q = (lane >> 2) & 3, p = lane & 3;
+    int aoff[2][2][2], boff[4][2][2];     // [tile][k16 half][read]
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int rd = 0; rd < 2; ++rd) {
+            const int row = 16 * ks + 8 * h + 4 * rd + q;
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                const int col = 64 * wm + 32 * i + 16 * (G & 1) + 4 * p;
+                aoff[i][ks][rd] = row * ROWB + (swz(row, col >> 3) << 4) + 8 * (p & 1);
+            }
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int col = 128 * wn + 32 * j + 16 * (G & 1) + 4 * p;
+                boff[j][ks][rd] = row * ROWB + (swz(row, col >> 3) << 4) + 8 * (p & 1);
+            }
+        }
+
+    f32x16 acc[2][4];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+    float cs[4] = {0.f, 0.f, 0.f, 0.f};
+
+    auto zero_tail = [&](char* st) {
+        // rows past kend hold clamped (duplicate) data: zero them in both operands
+        const int per = (BK - tail) * ROWB / 16;              // 16-byte pieces per operand
+        for (int i = tid; i < 2 * per; i += NT) {
+            const int op = i / per, r = i - op * per;
+            *(int4*)(st + op * OPB + tail * ROWB + 16 * r) = int4{0, 0, 0, 0};
+        }
+        skr::lds_barrier();
+    };
+    const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)smem;
+    // 12 transposed reads per fragment set (2 A tiles + 4 B tiles, 2 reads each)
+    auto read_frags = [&](int stage, int ks, Frags& f) {
+        const uint32_t st = lds0 + stage * STGB;
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int rd = 0; rd < 2; ++rd) f.a[i][rd] = tr_read(st + aoff[i][ks][rd]);
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int rd = 0; rd < 2; ++rd) f.b[j][rd] = tr_read(st + OPB + boff[j][ks][rd]);
+    };
+    auto mfmas = [&](const Frags& f) {
+        bf16x8 af[2], bfr[4];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) af[i] = join(f.a[i]);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) bfr[j] = join(f.b[j]);
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+        if constexpr (CS) {
+            if (wm == 0) {
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) cs[j] += (float)bfr[j][e];
+            }
+        }
+    };
+
+#pragma unroll
+    for (int s = 0; s < NSTG - 1; ++s)
+        if (s < nk) issue(s);
+    for (int kt = 0; kt < nk; ++kt) {
+        wait_ahead<NSTG - 2>(min(nk - 1 - kt, NSTG - 2));
+        __builtin_amdgcn_s_barrier();     // stage kt landed for every wave; stage kt-1 is free
+        if (kt + NSTG - 1 < nk) issue(kt + NSTG - 1);
+        if (kt == nk - 1 && tail < BK) zero_tail(smem + (kt % NSTG) * STGB);
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+            Frags f;
+            read_frags(kt % NSTG, ks, f);
+            frag_wait<0>(f);
+            mfmas(f);
+        }
+    }
+    // ---- epilogue: fp32 slab (lane: column r; registers: rows (e&3) + 8(e>>2) + 4h)
+    float* C = g.C + z * g.c_bs + (int64_t)split * g.M * g.N;
+    const int r = lane & 31;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int col = n0 + 128 * wn + 32 * j + r;
+#pragma unroll
+            for (int e = 0; e < 16; ++e) {
+                const int row = m0 + 64 * wm + 32 * i + (e & 3) + 8 * (e >> 2) + 4 * h;
+                C[(int64_t)row * g.N + col] = acc[i][j][e];
+            }
+        }
+    if constexpr (CS) {
+        if (wm == 0) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const float v = cs[j] + __shfl_xor(cs[j], 32, 64);
+                if (lane < 32) g.cs[(int64_t)zs * g.N + n0 + 128 * wn + 32 * j + r] = v;
+            }
+        }
+    }
+}
+
+// out[z][i] = sum_s slab[z][s][i] (i < n, n % 4 == 0), fixed order: deterministic
+__global__ __launch_bounds__(256) void slab_sum_kernel(const float* __restrict__ src, int S, int64_t n, int nb,
+                                                       float* __restrict__ out) {
+    const int64_t i4 = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
+    if (i4 >= n * nb) return;
+    const int64_t z = i4 / n, i = i4 - z * n;
+    const float* p = src + z * S * n + i;
+    float4 a = *(const float4*)p;
+    for (int s = 1; s < S; ++s) {
+        const float4 b = *(const float4*)(p + s * n);
+        a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+    }
+    *(float4*)(out + i4) = a;
+}
+
+}  // namespace
+
+// C[z] = A[z]^T . B[z] (+ cs[z] = colsum(B[z]) when cs != null) for z < nb.
+// A [K, M] bf16 (lda, batch stride a_bs elements), B [K, N] bf16 (ldb, b_bs).
+// S split-K slabs: slab s of batch z at work + (z * S + s) * M * N (fp32);
+// with S == 1 the kernel writes C directly (work unused). cs_work [nb][S][N].
+// Requirements: M % 256 == 0, N % 256 == 0, lda, ldb % 8 == 0, 16-byte
+// aligned bases (returns -2 / -4 otherwise: callers use a library GEMM).
+SKR_API int skr_wgrad(const void* A, int64_t lda, int64_t a_bs, const void* B, int64_t ldb, int64_t b_bs,
+                      int64_t K, int M, int N, int nb, int S, float* C, float* work, float* cs, float* cs_work,
+                      hipStream_t s) {
+    if (K <= 0 || M <= 0 || N <= 0 || nb <= 0) return -2;
+    if (M % TM || N % TN || lda % 8 || ldb % 8 || a_bs % 8 || b_bs % 8 || S < 1) return -2;
+    if (((uintptr_t)A | (uintptr_t)B | (uintptr_t)C) & 15) return -4;
+    if (S > 1 && work == nullptr) return -3;
+    if (cs != nullptr && S > 1 && cs_work == nullptr) return -3;
+    WgArgs g;
+    g.A = (const __hip_bfloat16*)A; g.lda = lda; g.a_bs = a_bs;
+    g.B = (const __hip_bfloat16*)B; g.ldb = ldb; g.b_bs = b_bs;
+    g.C = S > 1 ? work : C;
+    g.c_bs = (int64_t)S * M * N;
+    g.cs = cs == nullptr ? nullptr : (S > 1 ? cs_work : cs);
+    g.K = K; g.M = M; g.N = N; g.S = S;
+    g.kslice = (int)(((K + S - 1) / S + BK - 1) / BK * BK);
+    if ((int64_t)g.kslice * (S - 1) >= K) return -5;   // an empty split
+    g.tiles_m = M / TM; g.tiles_n = N / TN;
+    g.total = nb * S * g.tiles_m * g.tiles_n;
+    g.per_xcd = (g.total + 7) / 8;
+    const int grid = 8 * g.per_xcd;
+    const size_t lds = (size_t)NSTG * STGB;
+    static bool attr = false;
+    if (!attr) {
+        if (hipFuncSetAttribute((const void*)wgrad_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess ||
+            hipFuncSetAttribute((const void*)wgrad_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+            return -6;
+        attr = true;
+    }
+    if (g.cs != nullptr) hipLaunchKernelGGL(wgrad_kernel<true>, dim3(grid), dim3(NT), lds, s, g);
+    else hipLaunchKernelGGL(wgrad_kernel<false>, dim3(grid), dim3(NT), lds, s, g);
+    if (S > 1) {
+        const int64_t n = (int64_t)M * N;
+        hipLaunchKernelGGL(slab_sum_kernel, dim3((unsigned)((n * nb / 4 + 255) / 256)), dim3(256), 0, s, work, S, n, nb, C);
+        if (cs != nullptr)
+            hipLaunchKernelGGL(slab_sum_kernel, dim3((unsigned)((N * nb / 4 + 255) / 256)), dim3(256), 0, s, cs_work, S,
+                               (int64_t)N, nb, cs);
+    }
+    return SKR_CHECK_LAUNCH();
+}

@@ -31,7 +31,7 @@ import time
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
 
 
-def run_arm(arm: str, args) -> dict:
+def run_arm(arm: str, args, seed: int = 0) -> dict:
     import torch
     from sketch_rnn_amd import ops
     from sketch_rnn_amd.config import PRESETS
@@ -41,18 +41,19 @@ def run_arm(arm: str, args) -> dict:
 
     backend, dtype = arm.split("-")
     ops.set_backend(backend)
-    cfg = PRESETS[args.config].replace(batch_size=args.batch, max_seq_len=args.seq_len, save_every=0)
+    cfg = PRESETS[args.config].replace(batch_size=args.batch, max_seq_len=args.seq_len, save_every=0, seed=seed)
     strokes, labels = synthetic_corpus(args.sketches, seed=1234, max_len=args.seq_len,
                                        n_classes=max(cfg.num_classes, 1))
     n_test = max(args.batch, len(strokes) // 10)
     train = StrokeDataset(strokes[n_test:], args.batch, args.seq_len, random_scale_factor=cfg.random_scale_factor,
-                          augment_stroke_prob=cfg.augment_stroke_prob, labels=labels[n_test:], seed=7)
+                          augment_stroke_prob=cfg.augment_stroke_prob, labels=labels[n_test:], seed=7 + 101 * seed)
     scale = train.normalize()
     test = StrokeDataset(strokes[:n_test], args.batch, args.seq_len, labels=labels[:n_test], seed=8)
     test.normalize(scale)
-    torch.manual_seed(0)
+    torch.manual_seed(seed)
     trainer = VAETrainer(cfg, train, None, test, device="cuda", save_dir="/tmp/skr_converge",
                          use_graph=(backend == "hip"), log=lambda s: None, compute_dtype=dtype)
+    trainer.seed.fill_(1000003 * seed)       # dropout / reparameterisation noise stream of this seed
     curve = []
     t0 = time.perf_counter()
     for step in range(1, args.steps + 1):
@@ -62,10 +63,10 @@ def run_arm(arm: str, args) -> dict:
             curve.append({"step": step, "test_recon_nll": round(ev["r_cost"], 5), "test_kl": round(ev["kl_cost"], 5),
                           "train_cost": round(float(out["cost"]), 5),
                           "wall_s": round(time.perf_counter() - t0, 1)})
-            print("%s step %d: test recon NLL %.4f (train cost %.4f, %.0f s)"
-                  % (arm, step, ev["r_cost"], float(out["cost"]), time.perf_counter() - t0),
+            print("%s seed %d step %d: test recon NLL %.4f (train cost %.4f, %.0f s)"
+                  % (arm, seed, step, ev["r_cost"], float(out["cost"]), time.perf_counter() - t0),
                   file=sys.stderr, flush=True)
-    return {"arm": arm, "config": args.config, "steps": args.steps, "batch": args.batch, "seq_len": args.seq_len,
+    return {"arm": arm, "seed": seed, "config": args.config, "steps": args.steps, "batch": args.batch, "seq_len": args.seq_len,
             "curve": curve, "final_test_recon_nll": curve[-1]["test_recon_nll"],
             "skipped_steps": trainer.opt.skipped_steps()}
 
@@ -79,19 +80,39 @@ def main():
     ap.add_argument("--seq-len", type=int, default=250)
     ap.add_argument("--sketches", type=int, default=5000)
     ap.add_argument("--arms", default="hip-bf16,hip-fp32")
+    ap.add_argument("--seeds", default="0", help="comma list: init, data-order and noise seed of each run")
     ap.add_argument("--out", default=None)
     args = ap.parse_args()
-    res = [run_arm(a, args) for a in args.arms.split(",")]
-    ref = next((r for r in res if r["arm"].endswith("fp32")), None)
-    for r in res:
-        if ref is not None and r is not ref:
-            r["rel_gap_vs_%s" % ref["arm"]] = round(
-                (r["final_test_recon_nll"] - ref["final_test_recon_nll"]) / abs(ref["final_test_recon_nll"]), 5)
-        print(json.dumps(r), flush=True)
+    import numpy as np
+    seeds = [int(x) for x in args.seeds.split(",")]
+    arms = args.arms.split(",")
+    res = []
+    for sd in seeds:
+        for a in arms:
+            r = run_arm(a, args, sd)
+            res.append(r)
+            print(json.dumps(r), flush=True)
+            if args.out:
+                with open(args.out, "a") as f:
+                    f.write(json.dumps(r) + "\n")
+    # mean +- std of the final test recon NLL per arm over the seeds
+    summ = {"summary": True, "config": args.config, "steps": args.steps, "seeds": seeds, "arms": {}}
+    for a in arms:
+        v = np.array([r["final_test_recon_nll"] for r in res if r["arm"] == a])
+        summ["arms"][a] = {"mean": round(float(v.mean()), 5), "std": round(float(v.std(ddof=1)) if len(v) > 1 else 0.0, 5),
+                           "finals": [float(x) for x in v]}
+    ref = next((a for a in arms if a.endswith("fp32")), None)
+    if ref is not None:
+        m0 = summ["arms"][ref]["mean"]
+        for a in arms:
+            if a != ref:
+                d = summ["arms"][a]["mean"] - m0
+                summ["arms"][a]["rel_gap_vs_%s" % ref] = round(d / abs(m0), 5)
+                summ["arms"][a]["gap_in_%s_std" % ref] = round(d / max(summ["arms"][ref]["std"], 1e-12), 3)
+    print(json.dumps(summ), flush=True)
     if args.out:
         with open(args.out, "a") as f:
-            for r in res:
-                f.write(json.dumps(r) + "\n")
+            f.write(json.dumps(summ) + "\n")
 
 
 if __name__ == "__main__":

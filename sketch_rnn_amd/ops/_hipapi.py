@@ -307,6 +307,10 @@ class HipLib:
         lib.skr_bproj_bwd.restype = _i
         lib.skr_colsum.argtypes = [_p, _i, _p, _i64, _i64, _i64, _i64, _i, _i, _p, _p, _p]
         lib.skr_colsum.restype = _i
+        lib.skr_wgrad.argtypes = [_p, _i64, _i64, _p, _i64, _i64, _i64, _i, _i, _i, _i, _p, _p, _p, _p, _p]
+        lib.skr_wgrad.restype = _i
+        lib.skr_occupancy_hog.argtypes = [_i, _i, _i, _i, _p, _p]
+        lib.skr_occupancy_hog.restype = _i
         lib.skr_gru_fwd.argtypes = [C.POINTER(GruFwdArgs), _i, _p]
         lib.skr_gru_fwd.restype = _i
         lib.skr_gru_bwd.argtypes = [C.POINTER(GruBwdArgs), _i, _p]

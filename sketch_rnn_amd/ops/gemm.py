@@ -46,19 +46,70 @@ def bmm(a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor] = None) ->
     return torch.bmm(a, b, out_dtype=torch.float32)
 
 
-def wgrad(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
+def _wgrad_hip_ok(a: torch.Tensor, b: torch.Tensor) -> bool:
+    """Shapes the hand-written kernel (csrc/wgrad_gemm.hip) takes: bf16
+    operands on the GPU, M and N multiples of its 256 x 256 output tile,
+    rows 16-byte aligned (anything else: hipBLASLt)."""
+    from . import use_hip
+    if not (WGRAD_HIP and a.is_cuda and use_hip(a) and a.dtype == _BF16 and b.dtype == _BF16):
+        return False
+    M, N = a.shape[-1], b.shape[-1]
+    return (M % 256 == 0 and N % 256 == 0 and a.stride(-1) == 1 and b.stride(-1) == 1
+            and all(st % 8 == 0 for st in a.stride()[:-1] + b.stride()[:-1])
+            and a.data_ptr() % 16 == 0 and b.data_ptr() % 16 == 0)
+
+
+WGRAD_HIP = os.environ.get("SKR_WGRAD_HIP", "1") != "0"
+
+
+def _wgrad_hip(a, b, colsum):
+    from ..utils import native
+    lib = native.require_hip()
+    n, K, M = a.shape
+    N = b.shape[-1]
+    tiles = n * (M // 256) * (N // 256)
+    # split K only to fill the chip: whole waves of <= 256 workgroups (one per CU)
+    S = max(1, min(256 // tiles, K // 1024)) if tiles < 192 else 1
+    dev = a.device
+    out = torch.empty(n, M, N, device=dev, dtype=torch.float32)
+    work = torch.empty(n * S, M, N, device=dev, dtype=torch.float32) if S > 1 else None
+    cs = torch.empty(n, N, device=dev, dtype=torch.float32) if colsum else None
+    csw = torch.empty(n * S, N, device=dev, dtype=torch.float32) if (colsum and S > 1) else None
+    ptr = lambda t: t.data_ptr() if t is not None else None
+    rc = lib.lib.skr_wgrad(a.data_ptr(), a.stride(1), a.stride(0) if n > 1 else 0, b.data_ptr(), b.stride(1),
+                           b.stride(0) if n > 1 else 0, K, M, N, n, S, out.data_ptr(), ptr(work), ptr(cs), ptr(csw),
+                           torch.cuda.current_stream().cuda_stream)
+    if rc != 0:
+        raise RuntimeError("skr_wgrad failed (%d) for [%d, %d]^T [%d, %d] x %d" % (rc, K, M, K, N, n))
+    return out, cs
+
+
+def wgrad(a: torch.Tensor, b: torch.Tensor, colsum: bool = False):
     """Weight gradient ``a^T @ b`` over a long row dimension (K = T*B rows):
     ``a [K, M], b [K, N] -> [M, N]`` (or batched ``[n, K, *] -> [n, M, N]``),
-    fp32 output. When the output has few 256x256 tiles (an encoder / small
-    decoder layer: 16-64 tiles for the whole chip) K is split S ways into one
-    batched product whose partial outputs are summed: measured on MI355X
-    (scripts/bench_wgrad.py) the encoder's two [512 x 2048] gradients over
-    25000 rows take 168 us at S = 10 against 285 us as a plain batched GEMM."""
+    fp32 output. ``colsum``: also return the column sums of ``b`` (a bias
+    gradient that rides on the same pass over ``b``): ``(out, colsum)``.
+
+    bf16 operands on the GPU run the hand-written MFMA kernel
+    (csrc/wgrad_gemm.hip: 256 x 256 tiles, ds_read_b64_tr_b16 operands,
+    split-K only to fill the chip). Other dtypes / shapes use hipBLASLt:
+    when the output has few 256x256 tiles K is split S ways into one batched
+    product whose partial outputs are summed (measured on MI355X,
+    scripts/bench_wgrad.py: the encoder's two [512 x 2048] gradients over
+    25000 rows took 168 us at S = 10 against 285 us as a plain batched GEMM)."""
     if a.dtype != b.dtype:
         a, b = a.to(_BF16), b.to(_BF16)
     batched = a.dim() == 3
     if not batched:
         a, b = a.unsqueeze(0), b.unsqueeze(0)
+    if _wgrad_hip_ok(a, b):
+        out, cs = _wgrad_hip(a, b, colsum)
+        if not batched:
+            out, cs = out[0], (cs[0] if cs is not None else None)
+        return (out, cs) if colsum else out
+    if colsum:   # ones column appended to a: the extra output row is colsum(b)
+        ones = torch.ones(a.shape[:-1] + (8,), device=a.device, dtype=a.dtype)
+        a = torch.cat([a, ones], -1)
     n, K, M = a.shape
     N = b.shape[-1]
     tiles = n * -(-M // 256) * -(-N // 256)
@@ -72,7 +123,12 @@ def wgrad(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
     else:
         out = bmm(a.reshape(n * S, K // S, M).transpose(1, 2), b.reshape(n * S, K // S, N))
         out = out.view(n, S, M, N).sum(1)
-    return out if batched else out[0]
+    cs = None
+    if colsum:
+        out, cs = out[:, :M - 8], out[:, M - 8]
+    if not batched:
+        out, cs = out[0], (cs[0] if cs is not None else None)
+    return (out, cs) if colsum else out
 
 
 

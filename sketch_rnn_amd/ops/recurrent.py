@@ -462,10 +462,11 @@ def _split_override(var: str, planned: int, K: int) -> int:
     return v if v > 0 and planned > 0 and K % (64 * v) == 0 else planned
 
 
-def _hyper_proj_grads(dP1, s, Hh, H, E):
-    """Hyper-norm projection gradients from ``dP1 = [hh | 1]^T dvec``."""
-    dP = dP1[:Hh].view(Hh, 12, H).transpose(0, 1)                  # [12, Hh, H]
-    sV = dP1[Hh].view(12, H)                                       # column sums of dvec
+def _hyper_proj_grads(dP1, sV, s, Hh, H, E):
+    """Hyper-norm projection gradients from ``dP1 = hh^T dvec`` and the
+    column sums ``sV`` of dvec."""
+    dP = dP1.view(Hh, 12, H).transpose(0, 1)                       # [12, Hh, H]
+    sV = sV.view(12, H)
     Wz3 = s.W_z.view(Hh, 12, E).transpose(0, 1)                    # [12, Hh, E]
     dW_z = torch.bmm(dP, s.W_a.transpose(1, 2)).transpose(0, 1).reshape(Hh, 12 * E)
     dWa = torch.bmm(Wz3.transpose(1, 2), dP) + s.b_z.view(12, E, 1) * sV.view(12, 1, H)
@@ -778,14 +779,14 @@ class _HyperSeq(torch.autograd.Function):
         # weight / LayerNorm-parameter gradients: long-K products over the T*B saved rows
         A2 = s.A[:T].reshape(TB, K)
         # hyper-norm projections, vec_k = (hh @ W_z_k + b_z_k) @ W_a_k: ONE long-K
-        # GEMM dP = [hh | 1]^T @ dvec gives dP_k = hh^T dvec_k and (ones row) the
-        # column sums of dvec; the per-k factors are then tiny batched products
-        HH1 = torch.zeros(TB, Hh + 8, device=dev, dtype=ldt)
-        HH1[:, :Hh] = s.HH.view(TB, Hh)
-        HH1[:, Hh] = 1.0
+        # GEMM dP = hh^T @ dvec gives dP_k = hh^T dvec_k, and the same pass over
+        # dvec its column sums; the per-k factors are then tiny batched products
         dW_h = gemm.wgrad(A2[:, :H], dRM_lp.view(TB, G))
         dW_y = gemm.wgrad(A2, dRY_lp.view(TB, Gh))
-        dP1 = gemm.wgrad(HH1, dVEC.view(TB, 12 * H))
+        # hh_t rows: the bf16 GEMM operand of step t + 1 (no resets on this path,
+        # so it is exactly bf16(HH[t])) -- no conversion pass
+        HHl = s.A[1:T + 1].reshape(TB, K)[:, H:] if lp_on else s.HH.view(TB, Hh)
+        dP1, sV = gemm.wgrad(HHl, dVEC.view(TB, 12 * H), colsum=True)
         g_ln, g_hln = [], []
         for dy, xh, n, out in ((DLNY, s.XHAT, G, g_ln), (DLNCY, s.CHAT, H, g_ln), (HDLNY, s.HXHAT, Gh, g_hln),
                                (HDLNCY, s.HCHAT, Hh, g_hln)):
@@ -815,7 +816,7 @@ class _HyperSeq(torch.autograd.Function):
                 dx, dzc = dxf[..., :IX], dxf[..., IX:].sum(0)
             else:
                 dx = dxf
-        dW_z, db_z, dWa, dbias = _hyper_proj_grads(dP1, s, Hh, H, E)
+        dW_z, db_z, dWa, dbias = _hyper_proj_grads(dP1, sV, s, Hh, H, E)
         ctx.s = None
         return (dx, dzc, dh0, dc_rec, dhh0, dhc_rec, None, dW_x, dW_h, dbias, dhW_x, dhW_h,
                 g_hln[0], g_hln[1], g_hln[2], g_hln[3], dW_z, db_z, dWa, g_ln[0], g_ln[1], g_ln[2], g_ln[3], None)
