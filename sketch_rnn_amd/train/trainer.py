@@ -239,6 +239,18 @@ class VAETrainer:
         # syncs: the overlapped step measured 4.1 s/step against 20 ms for the
         # plain step (2 ranks on one GPU, vae_small; 41 ms with a device sync
         # between phases), so gloo keeps the plain step unless forced.
+        # Concurrency decision (RCCL): overlap stays ON. The kernels that spin
+        # on peer workgroups (lstm_persist_bwd of the encoder, the clustered
+        # LayerNorm / HyperLSTM cells) never wait on a collective, so an RCCL
+        # kernel holding CU slots only delays their unplaced workgroups until it
+        # retires; the bounded spins last ~seconds, an all-reduce kernel's
+        # residency milliseconds. Measured on MI355X with an occupancy hog on a
+        # second stream (tests/test_dp_concurrency_gpu.py,
+        # profiles/r3/dp_concurrency_hog.jsonl): 64x512-thread/32 KB-LDS and
+        # whole-chip 256x1024 hogs for 20 ms, and a half-chip hog for 200 ms,
+        # beside the encoder backward (solo 1.3 ms) and the H=2048 HyperLSTM
+        # cells: every run finished right after the hog (20.2-21.7 / 200.2 ms),
+        # no fault flag, outputs and gradients bit-identical to the solo run.
         ov = os.environ.get("SKR_DP_OVERLAP", "auto")
         if ov == "auto":
             ov = "1" if (self.world > 1 and dp.backend() == "nccl") or self.device.type == "cpu" else "0"
