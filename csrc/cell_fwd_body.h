@@ -248,9 +248,9 @@ __device__ __forceinline__ void cell_fwd_body(const FwdArgs& a, const int c, con
             th[k] = tanhf(ch * lcg[k] + lcb[k]);
             if (!on[k]) continue;
             if (save) {
-                a.chat[ro] = ch;
+                st_save(a.chat, ro, ch, a.save_lp);
 #pragma unroll
-                for (int q = 0; q < 4; ++q) a.xhat[(int64_t)b * 4 * H + q * H + u] = xs[k][q];
+                for (int q = 0; q < 4; ++q) st_save(a.xhat, (int64_t)b * 4 * H + q * H + u, xs[k][q], a.save_lp);
             }
             if (a.c_out != nullptr) a.c_out[ro] = cn[k];
             if (MOD && a.r_lp != nullptr) {

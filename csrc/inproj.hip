@@ -46,9 +46,11 @@ __global__ __launch_bounds__(256) void inproj_fwd(const float* __restrict__ x, c
     }
 }
 
-template <int IN>
+// LP: dxp is the persistent encoder's bf16 gate gradient, direction-major
+// [2][T][B][G] (no fp32 copy of it is ever written); else fp32 [T][2B][G].
+template <int IN, bool LP>
 __global__ __launch_bounds__(256) void inproj_bwd(const float* __restrict__ x, const int64_t* __restrict__ len,
-                                                  const float* __restrict__ dxp, float* __restrict__ part,
+                                                  const void* __restrict__ dxp, float* __restrict__ part,
                                                   int T, int B, int G) {
     const int g = blockIdx.x * 256 + threadIdx.x;
     const int rs = blockIdx.y, RS = gridDim.y, d = blockIdx.z;
@@ -59,10 +61,11 @@ __global__ __launch_bounds__(256) void inproj_bwd(const float* __restrict__ x, c
 #pragma unroll
     for (int i = 0; i <= IN; ++i) acc[i] = 0.f;
     for (int t = t0; t < t1; ++t) {
-        const float* drow = dxp + ((int64_t)t * 2 * B + (int64_t)d * B) * G + g;
+        const int64_t r0 = LP ? ((int64_t)d * T + t) * B : (int64_t)t * 2 * B + (int64_t)d * B;
 #pragma unroll 4
         for (int b = 0; b < B; ++b) {
-            const float dv = drow[(int64_t)b * G];
+            const int64_t o = (r0 + b) * G + g;
+            const float dv = LP ? __bfloat162float(((const __hip_bfloat16*)dxp)[o]) : ((const float*)dxp)[o];
             const float* xr = x + ((int64_t)src_row(t, d, len, b) * B + b) * IN;
 #pragma unroll
             for (int i = 0; i < IN; ++i) acc[i] += xr[i] * dv;
@@ -82,9 +85,12 @@ int launch_fwd(const float* x, const int64_t* len, const float* W, const float* 
 }
 
 template <int IN>
-int launch_bwd(const float* x, const int64_t* len, const float* dxp, float* part, int T, int B, int G, int RS,
+int launch_bwd(const float* x, const int64_t* len, const void* dxp, int lp, float* part, int T, int B, int G, int RS,
                hipStream_t s) {
-    hipLaunchKernelGGL(inproj_bwd<IN>, dim3((G + 255) / 256, RS, 2), dim3(256), 0, s, x, len, dxp, part, T, B, G);
+    if (lp)
+        hipLaunchKernelGGL((inproj_bwd<IN, true>), dim3((G + 255) / 256, RS, 2), dim3(256), 0, s, x, len, dxp, part, T, B, G);
+    else
+        hipLaunchKernelGGL((inproj_bwd<IN, false>), dim3((G + 255) / 256, RS, 2), dim3(256), 0, s, x, len, dxp, part, T, B, G);
     return SKR_CHECK_LAUNCH();
 }
 
@@ -101,13 +107,14 @@ SKR_API int skr_inproj_fwd(const float* x, const int64_t* len, const float* W, c
     }
 }
 
-// dxp [T, 2B, G] -> part [RS, 2, IN + 1, G]: rows i < IN are dW_d[i], row IN is dbias_d.
-SKR_API int skr_inproj_bwd(const float* x, const int64_t* len, const float* dxp, float* part, int T, int B, int IN,
-                           int G, int RS, hipStream_t s) {
+// dxp [T, 2B, G] fp32 (lp = 0) or [2, T, B, G] bf16 (lp = 1) -> part [RS, 2, IN + 1, G]:
+// rows i < IN are dW_d[i], row IN is dbias_d.
+SKR_API int skr_inproj_bwd(const float* x, const int64_t* len, const void* dxp, int lp, float* part, int T, int B,
+                           int IN, int G, int RS, hipStream_t s) {
     if (T <= 0 || B <= 0 || G <= 0 || RS <= 0) return -2;
     switch (IN) {
-        case 3: return launch_bwd<3>(x, len, dxp, part, T, B, G, RS, s);
-        case 5: return launch_bwd<5>(x, len, dxp, part, T, B, G, RS, s);
+        case 3: return launch_bwd<3>(x, len, dxp, lp, part, T, B, G, RS, s);
+        case 5: return launch_bwd<5>(x, len, dxp, lp, part, T, B, G, RS, s);
         default: return -2;
     }
 }

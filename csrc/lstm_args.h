@@ -42,6 +42,9 @@ struct FwdArgs {
     // [B][4][gstat_tiles][2] are precomputed -- no statistics exchange for
     // the gates; xp / R / vec / bias are not read
     const float* gpre; const float* gstats; int gstat_tiles;
+    // LN saves in bf16 (xhat / chat buffers hold __hip_bfloat16; the forward
+    // itself runs on the fp32 values, like a bf16 activation save)
+    int save_lp;
 };
 
 struct BwdArgs {
@@ -78,6 +81,7 @@ struct BwdArgs {
     // store them): act = sig/tanh(xhat * ln_g + ln_b (+ forget_bias on f))
     const float* ln_b; float forget_bias;
     const __hip_bfloat16* r_lp;        // MOD: R from the forward's bf16 copy (stride ld_R) instead of the slabs
+    int save_lp;                       // LN: xhat / chat read and dlny / dlncy written as bf16
 };
 
 // hyper modulation vectors: MOD 1 fp32, MOD 2 bf16
@@ -85,6 +89,19 @@ template <int MOD>
 __device__ __forceinline__ float ldvec(const void* v, int64_t i) {
     if constexpr (MOD == 2) return __bfloat162float(((const __hip_bfloat16*)v)[i]);
     else return ((const float*)v)[i];
+}
+
+// LN saves: fp32 or (lp) bf16 element i. The load is branch-free (one
+// dword load + selects): the cells issue every load up front, and a branch
+// between two loads would split that batch.
+__device__ __forceinline__ float ld_save(const void* p, int64_t i, bool lp) {
+    const int64_t off = lp ? (i << 1) : (i << 2);
+    const uint32_t w = *(const uint32_t*)((const char*)p + (off & ~(int64_t)3));
+    return __uint_as_float(lp ? ((off & 2) ? (w & 0xffff0000u) : (w << 16)) : w);
+}
+__device__ __forceinline__ void st_save(void* p, int64_t i, float v, bool lp) {
+    if (lp) ((__hip_bfloat16*)p)[i] = __float2bfloat16(v);
+    else ((float*)p)[i] = v;
 }
 
 __device__ __forceinline__ float dropout_mult(bool on, uint32_t key, int64_t idx, float keep) {

@@ -106,12 +106,12 @@ __global__ __launch_bounds__(NT) void cell_bwd(const BwdArgs a) {
         dcc[k] = a.dc_rec[ro];
         cp[k] = a.c_prev[ro];
         if (LN) {
-            cx[k] = a.chat[ro];
+            cx[k] = ld_save(a.chat, ro, a.save_lp);
             lcg[k] = lnc_g[uc];
             lcb[k] = lnc_b[uc];
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
-                xh[k][q] = a.xhat[(int64_t)b * 4 * H + q * H + uc];
+                xh[k][q] = ld_save(a.xhat, (int64_t)b * 4 * H + q * H + uc, a.save_lp);
                 lg[k][q] = ln_g[q * H + uc];
                 lb[k][q] = ln_b[q * H + uc];
             }
@@ -221,10 +221,10 @@ __global__ __launch_bounds__(NT) void cell_bwd(const BwdArgs a) {
             if (!on[k]) continue;
             const int u = base + k * NT + tid;
             const int64_t ro = (int64_t)b * H + u;
-            a.dlncy[ro] = dlc[k];
+            st_save(a.dlncy, ro, dlc[k], a.save_lp);
             a.dc_rec[ro] = dcr[k];
 #pragma unroll
-            for (int q = 0; q < 4; ++q) a.dlny[(int64_t)b * 4 * H + q * H + u] = dly[k][q];
+            for (int q = 0; q < 4; ++q) st_save(a.dlny, (int64_t)b * 4 * H + q * H + u, dly[k][q], a.save_lp);
         }
 #pragma unroll
         for (int q = 0; q < 4; ++q) {

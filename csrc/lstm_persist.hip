@@ -73,6 +73,8 @@ struct PFwdLayer {
     float* act;                               // [T][nd*B][4H] sig(i), tanh(j), sig(f+fb), sig(o)
     float* hT; float* cT;                     // [nd*B][H] final carried state (fp32)
     float keep; uint32_t stream;
+    float* h_last;                            // [B][nd*H] h at each row's last valid step (needs tlen), the
+                                              // directions side by side (the encoder's [h_fw | h_bw]), or null
 };
 
 struct PFwdArgs {
@@ -97,6 +99,7 @@ struct PBwdLayer {
     float* dh0; float* dc0;                   // [nd*B][H] grads into the initial state
     float* dinit_h; float* dinit_c;           // [nd*B][H] grads into the reset targets (with resets)
     float keep; uint32_t stream;
+    const float* dh_last;                     // [B][nd*H] grad of h_last (added at each row's last step) or null
 };
 
 struct PBwdArgs {
@@ -147,6 +150,12 @@ __device__ __forceinline__ int row_block_steps(const int* tlen, int T, int B, in
     return te;
 }
 
+// Last valid step of row r: the one whose h the encoder reads (h[len - 1],
+// len clamped to [1, T] like the gather it replaces).
+__device__ __forceinline__ int row_last_step(const int* tlen, int T, int r) {
+    return tlen == nullptr ? T - 1 : max(min(tlen[r], T), 1) - 1;
+}
+
 // =====================================================================================
 // forward
 // =====================================================================================
@@ -193,8 +202,12 @@ __device__ void fwd_body(const PFwdArgs& a, int l, int g, int rb, int wu, unsign
         brow[e] = (int)grow0 + min(r, B - 1);
     }
     float c[4];
+    int tlast[4];
 #pragma unroll
-    for (int e = 0; e < 4; ++e) c[e] = epi ? P.c0[(int64_t)brow[e] * H + u] : 0.f;
+    for (int e = 0; e < 4; ++e) {
+        c[e] = epi ? P.c0[(int64_t)brow[e] * H + u] : 0.f;
+        tlast[e] = row_last_step(a.tlen, T, brow[e] - (int)grow0);
+    }
     const bool keep_on = P.keep < 1.0f;
     // A-fragment row of this lane (clamped) within its tile
     const int arow = (int)grow0 + min(row_t0 + fr, B - 1);
@@ -310,6 +323,8 @@ __device__ void fwd_body(const PFwdArgs& a, int l, int g, int rb, int wu, unsign
                 P.c_out[so] = cn[e];
                 if (P.c_carry != nullptr) P.c_carry[so + (int64_t)nB * H] = c[e];
                 if (P.h_out != nullptr) P.h_out[so] = hn[e];
+                if (P.h_last != nullptr && t == tlast[e])
+                    P.h_last[(int64_t)(brow[e] - grow0) * a.nd * H + g * H + u] = hn[e];
                 if (t == Te - 1) {
                     P.hT[ro] = hc[e];
                     P.cT[ro] = c[e];
@@ -396,11 +411,14 @@ __device__ void bwd_body(const PBwdArgs& a, int l, int g, int rb, int wu, unsign
         bon[e] = epi && r < B;
         brow[e] = (int)grow0 + min(r, B - 1);
     }
-    float dcr[4], dih[4], dic[4];
+    float dcr[4], dih[4], dic[4], dhl[4];
+    int tlast[4];
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
         dcr[e] = (epi && P.dcT != nullptr) ? P.dcT[(int64_t)brow[e] * H + u] : 0.f;
         dih[e] = dic[e] = 0.f;
+        tlast[e] = row_last_step(a.tlen, T, brow[e] - (int)grow0);
+        dhl[e] = (epi && P.dh_last != nullptr) ? P.dh_last[(int64_t)(brow[e] - grow0) * a.nd * H + g * H + u] : 0.f;
     }
     const bool keep_on = P.keep < 1.0f;
     const int arow = (int)grow0 + min(row_t0 + fr, B - 1);
@@ -420,7 +438,7 @@ __device__ void bwd_body(const PBwdArgs& a, int l, int g, int rb, int wu, unsign
                 for (int q = 0; q < 4; ++q) ac[e][q] = ap[q * H];
                 cnw[e] = P.c_out[so + ro];
                 cpv[e] = t == 0 ? P.c0[ro] : (P.c_carry != nullptr ? P.c_carry[so + ro] : P.c_out[so - (int64_t)nB * H + ro]);
-                dho[e] = (!UP && P.dh_out != nullptr) ? P.dh_out[so + ro] : 0.f;
+                dho[e] = ((!UP && P.dh_out != nullptr) ? P.dh_out[so + ro] : 0.f) + (t == tlast[e] ? dhl[e] : 0.f);
                 rs[e] = a.reset != nullptr ? a.reset[(int64_t)t * nB + brow[e]] : 0.f;
             }
         }

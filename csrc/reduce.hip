@@ -22,61 +22,112 @@ __device__ __forceinline__ float ldx(const void* x, int64_t i) {
     else return ((const float*)x)[i];
 }
 
-template <bool XBF16>
-__global__ __launch_bounds__(256) void colsum_kernel(const void* __restrict__ X, const float* __restrict__ Y,
+// V consecutive columns from element offset i (V = 4: one 8-byte bf16 or
+// 16-byte fp32 vector load per row; V = 1: scalar)
+template <bool BF, int V>
+__device__ __forceinline__ void ldv(const void* x, int64_t i, float (&v)[V]) {
+    if constexpr (V == 4) {
+        if constexpr (BF) {
+            const uint2 u = *(const uint2*)((const __hip_bfloat16*)x + i);
+            v[0] = __uint_as_float(u.x << 16);
+            v[1] = __uint_as_float(u.x & 0xffff0000u);
+            v[2] = __uint_as_float(u.y << 16);
+            v[3] = __uint_as_float(u.y & 0xffff0000u);
+        } else {
+            const float4 f = *(const float4*)((const float*)x + i);
+            v[0] = f.x; v[1] = f.y; v[2] = f.z; v[3] = f.w;
+        }
+    } else {
+        v[0] = ldx<BF>(x, i);
+    }
+}
+
+template <bool XBF16, bool YBF16, int V>
+__global__ __launch_bounds__(256) void colsum_kernel(const void* __restrict__ X, const void* __restrict__ Y,
                                                      int64_t R1, int64_t s1, int64_t R2, int64_t s2, int C,
                                                      float* __restrict__ part_xy, float* __restrict__ part_x) {
-    const int c = blockIdx.x * 256 + threadIdx.x;
+    const int c = (blockIdx.x * 256 + threadIdx.x) * V;
     if (c >= C) return;
     const int64_t R = R1 * R2;
     const int64_t per = (R + gridDim.y - 1) / gridDim.y;
     const int64_t r0 = blockIdx.y * per, r1 = min(R, r0 + per);
-    float sxy = 0.f, sx = 0.f;
+    float sxy[V], sx[V];
+#pragma unroll
+    for (int k = 0; k < V; ++k) sxy[k] = sx[k] = 0.f;
     // walk (i, j) incrementally: no 64-bit division per element
     int64_t i = r0 / R2, j = r0 % R2;
     int64_t r = r0;
-    for (; r + 4 <= r1; r += 4) {
-        float xv[4], yv[4];
+    constexpr int U = V == 4 ? 2 : 4;     // rows in flight per thread
+    for (; r + U <= r1; r += U) {
+        float xv[U][V], yv[U][V];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
+        for (int k = 0; k < U; ++k) {
             const int64_t off = i * s1 + j * s2 + c;
-            xv[k] = ldx<XBF16>(X, off);
-            yv[k] = Y ? Y[off] : 0.f;
+            ldv<XBF16, V>(X, off, xv[k]);
+            if (Y) ldv<YBF16, V>(Y, off, yv[k]);
+            else
+#pragma unroll
+                for (int e = 0; e < V; ++e) yv[k][e] = 0.f;
             if (++j == R2) {
                 j = 0;
                 ++i;
             }
         }
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            sx += xv[k];
-            sxy += xv[k] * yv[k];
-        }
+        for (int k = 0; k < U; ++k)
+#pragma unroll
+            for (int e = 0; e < V; ++e) {
+                sx[e] += xv[k][e];
+                sxy[e] += xv[k][e] * yv[k][e];
+            }
     }
     for (; r < r1; ++r) {
         const int64_t off = i * s1 + j * s2 + c;
-        const float xv = ldx<XBF16>(X, off);
-        sx += xv;
-        if (Y) sxy += xv * Y[off];
+        float xv[V], yv[V];
+        ldv<XBF16, V>(X, off, xv);
+        if (Y) ldv<YBF16, V>(Y, off, yv);
+#pragma unroll
+        for (int e = 0; e < V; ++e) {
+            sx[e] += xv[e];
+            if (Y) sxy[e] += xv[e] * yv[e];
+        }
         if (++j == R2) {
             j = 0;
             ++i;
         }
     }
-    part_x[(int64_t)blockIdx.y * C + c] = sx;
-    if (Y) part_xy[(int64_t)blockIdx.y * C + c] = sxy;
+#pragma unroll
+    for (int e = 0; e < V; ++e) {
+        part_x[(int64_t)blockIdx.y * C + c + e] = sx[e];
+        if (Y) part_xy[(int64_t)blockIdx.y * C + c + e] = sxy[e];
+    }
 }
 
 }  // namespace
 
-// x_kind: 1 bf16, 2 fp32. Y (fp32, same strides) may be null (then part_xy unused).
-SKR_API int skr_colsum(const void* X, int x_kind, const float* Y, int64_t R1, int64_t s1, int64_t R2, int64_t s2,
-                       int C, int RS, float* part_xy, float* part_x, hipStream_t s) {
+// x_kind / y_kind: 1 bf16, 2 fp32. Y (same strides) may be null (then part_xy unused).
+// Four columns per thread when C, the strides and the bases allow 8-byte
+// (bf16) / 16-byte (fp32) vector loads.
+SKR_API int skr_colsum(const void* X, int x_kind, const void* Y, int y_kind, int64_t R1, int64_t s1, int64_t R2,
+                       int64_t s2, int C, int RS, float* part_xy, float* part_x, hipStream_t s) {
     if (C <= 0 || RS <= 0 || R1 * R2 <= 0) return -2;
-    const dim3 grid((C + 255) / 256, RS);
-    if (x_kind == 1)
-        hipLaunchKernelGGL(colsum_kernel<true>, grid, dim3(256), 0, s, X, Y, R1, s1, R2, s2, C, part_xy, part_x);
-    else
-        hipLaunchKernelGGL(colsum_kernel<false>, grid, dim3(256), 0, s, X, Y, R1, s1, R2, s2, C, part_xy, part_x);
+    const bool xb = x_kind == 1, yb = y_kind == 1;
+    const uintptr_t al = (uintptr_t)X | (uintptr_t)(Y ? Y : X);
+    const bool v4 = C % 4 == 0 && s1 % 4 == 0 && s2 % 4 == 0 && (al & 15) == 0;
+    const int V = v4 ? 4 : 1;
+    const dim3 grid((C / V + 255) / 256, RS);
+#define SKR_CS(XB, YB, VV) hipLaunchKernelGGL((colsum_kernel<XB, YB, VV>), grid, dim3(256), 0, s, X, Y, R1, s1, R2, s2, C, part_xy, part_x)
+    if (v4) {
+        if (xb && yb) SKR_CS(true, true, 4);
+        else if (xb) SKR_CS(true, false, 4);
+        else if (yb) SKR_CS(false, true, 4);
+        else SKR_CS(false, false, 4);
+    } else {
+        if (xb && yb) SKR_CS(true, true, 1);
+        else if (xb) SKR_CS(true, false, 1);
+        else if (yb) SKR_CS(false, true, 1);
+        else SKR_CS(false, false, 1);
+    }
+#undef SKR_CS
     return SKR_CHECK_LAUNCH();
 }

@@ -64,8 +64,16 @@ class Encoder(nn.Module):
         T, B, _ = x.shape
         H = cfg.enc_rnn_size
         keep = cfg.recurrent_dropout_prob if (train and cfg.use_recurrent_dropout) else 1.0
-        zeros = x.new_zeros(B, H)
         ln = isinstance(self.fw, C.LNLSTMParams)
+        from ..ops import persist
+        if not ln and persist.bilstm_last_ok(x, H, B):
+            # one autograd node: input projection + persistent biLSTM writing
+            # only h[len - 1] of each row (ops/persist.py _PersistBiEncoder)
+            last_h = persist.bilstm_last_h(x, lengths, self.fw.W_x, self.bw.W_x, self.fw.bias, self.bw.bias,
+                                           self.fw.W_h, self.bw.W_h, drop_keep=keep, drop_seed=seed,
+                                           drop_stream=_S_ENC_FW)
+            return last_h @ self.mu_w + self.mu_b, last_h @ self.sig_w + self.sig_b
+        zeros = x.new_zeros(B, H)
         lns = [(p.ln_gamma, p.ln_beta, p.lnc_gamma, p.lnc_beta) if ln else None for p in (self.fw, self.bw)]
         # both directions' projections in one [T, 2B, 4H] tensor (the backward
         # direction reads each sketch reversed within its length)

@@ -38,6 +38,7 @@ class LstmFwdArgs(C.Structure):
         ("cluster", _i), ("part", _p), ("err", _p),
         ("r_lp", _p),
         ("gpre", _p), ("gstats", _p), ("gstat_tiles", _i),
+        ("save_lp", _i),
     ]
 
 
@@ -71,6 +72,7 @@ class LstmBwdArgs(C.Structure):
         ("cluster", _i), ("part", _p), ("err", _p),
         ("ln_b", _p), ("forget_bias", _f),
         ("r_lp", _p),
+        ("save_lp", _i),
     ]
 
 
@@ -157,6 +159,7 @@ class PFwdLayer(C.Structure):
         ("hlp", _p), ("hup", _p), ("h_out", _p), ("c_out", _p), ("c_carry", _p), ("act", _p),
         ("hT", _p), ("cT", _p),
         ("keep", _f), ("stream", _u32),
+        ("h_last", _p),
     ]
 
 
@@ -185,6 +188,7 @@ class PBwdLayer(C.Structure):
         ("dh0", _p), ("dc0", _p),
         ("dinit_h", _p), ("dinit_c", _p),
         ("keep", _f), ("stream", _u32),
+        ("dh_last", _p),
     ]
 
 
@@ -299,13 +303,13 @@ class HipLib:
         lib.skr_mdn_sample_slabs.restype = _i
         lib.skr_inproj_fwd.argtypes = [_p, _p, _p, _p, _p, _i, _i, _i, _i, _p]
         lib.skr_inproj_fwd.restype = _i
-        lib.skr_inproj_bwd.argtypes = [_p, _p, _p, _p, _i, _i, _i, _i, _i, _p]
+        lib.skr_inproj_bwd.argtypes = [_p, _p, _p, _i, _p, _i, _i, _i, _i, _i, _p]
         lib.skr_inproj_bwd.restype = _i
         lib.skr_bproj_fwd.argtypes = [_p, _p, _p, _p, _i, _i, _i, _i, _p]
         lib.skr_bproj_fwd.restype = _i
         lib.skr_bproj_bwd.argtypes = [_p, _p, _i, _i64, _p, _p, _i, _i, _i, _i, _p]
         lib.skr_bproj_bwd.restype = _i
-        lib.skr_colsum.argtypes = [_p, _i, _p, _i64, _i64, _i64, _i64, _i, _i, _p, _p, _p]
+        lib.skr_colsum.argtypes = [_p, _i, _p, _i, _i64, _i64, _i64, _i64, _i, _i, _p, _p, _p]
         lib.skr_colsum.restype = _i
         lib.skr_wgrad.argtypes = [_p, _i64, _i64, _p, _i64, _i64, _i64, _i, _i, _i, _i, _p, _p, _p, _p, _p]
         lib.skr_wgrad.restype = _i

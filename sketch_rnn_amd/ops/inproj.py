@@ -66,7 +66,7 @@ class _BiInProj(torch.autograd.Function):
         dxp = dxp.contiguous()
         RS = min(T, 64)
         part = torch.empty(RS, 2, IN + 1, G, device=x.device, dtype=torch.float32)
-        rc = lib.lib.skr_inproj_bwd(x.data_ptr(), ln.data_ptr(), dxp.data_ptr(), part.data_ptr(), T, B, IN, G, RS,
+        rc = lib.lib.skr_inproj_bwd(x.data_ptr(), ln.data_ptr(), dxp.data_ptr(), 0, part.data_ptr(), T, B, IN, G, RS,
                                     torch.cuda.current_stream().cuda_stream)
         if rc != 0:
             raise RuntimeError("skr_inproj_bwd failed (%d)" % rc)

@@ -225,9 +225,11 @@ class _LSTMSeq(torch.autograd.Function):
         keep_plain = not ln and (fused or not infer)
         Cout = torch.empty(T, BB, H, device=dev, dtype=f32) if keep_plain else None
         ACT = torch.empty(T, BB, G, device=dev, dtype=f32) if keep_plain else None
-        XHAT = torch.empty(T, BB, G, device=dev, dtype=f32) if ln and not infer else None
+        slp = ln and _ln_saves_lp(infer)
+        sdt = torch.bfloat16 if slp else f32
+        XHAT = torch.empty(T, BB, G, device=dev, dtype=sdt) if ln and not infer else None
         RSTD = torch.empty(T, BB, 5, device=dev, dtype=f32) if ln and not infer else None
-        CHAT = torch.empty(T, BB, H, device=dev, dtype=f32) if ln and not infer else None
+        CHAT = torch.empty(T, BB, H, device=dev, dtype=sdt) if ln and not infer else None
         rst = reset.contiguous().to(f32) if reset is not None else None
         # carried h differs from h' only on reset rows: without resets hT = h'_{T-1}
         HC = torch.empty(2, BB, H, device=dev, dtype=f32) if rst is not None else None
@@ -237,6 +239,7 @@ class _LSTMSeq(torch.autograd.Function):
         lnp = [t.contiguous() if t is not None else None for t in (ln_g, ln_b, lnc_g, lnc_b)]
         sd = _seed_tensor(seed, dev)
         a = LstmFwdArgs()
+        a.save_lp = int(slp)
         a.B, a.H, a.grp_rows = BB, H, BB // nd if nd > 1 else 0
         a.ld_xp, a.ld_R = G, G
         a.ln_g, a.ln_b, a.lnc_g, a.lnc_b = (_ptr(t) for t in lnp)
@@ -292,6 +295,7 @@ class _LSTMSeq(torch.autograd.Function):
         cT = CC[T].clone()
         s = _Saved()
         s.Wl, s.A, s.CC, s.Cout, s.ACT, s.XHAT, s.RSTD, s.CHAT = Wl, A, CC, Cout, ACT, XHAT, RSTD, CHAT
+        s.slp = slp
         s.reset, s.seed, s.meta, s.lnp = rst, sd, meta, lnp
         s.wshape = W_h.shape
         ctx.s = s
@@ -320,9 +324,11 @@ class _LSTMSeq(torch.autograd.Function):
         dHout = dHout.contiguous() if dHout is not None else None
         dinit_h = torch.zeros(BB, H, device=dev, dtype=f32) if s.reset is not None else None
         dinit_c = torch.zeros(BB, H, device=dev, dtype=f32) if s.reset is not None else None
-        DLNY = torch.empty(T, BB, G, device=dev, dtype=f32) if ln else None
-        DLNCY = torch.empty(T, BB, H, device=dev, dtype=f32) if ln else None
+        sdt = torch.bfloat16 if s.slp else f32
+        DLNY = torch.empty(T, BB, G, device=dev, dtype=sdt) if ln else None
+        DLNCY = torch.empty(T, BB, H, device=dev, dtype=sdt) if ln else None
         a = LstmBwdArgs()
+        a.save_lp = int(s.slp)
         a.B, a.H, a.grp_rows = BB, H, B if nd > 1 else 0
         a.ld_dh_rec, a.dhr_nslab, a.dhr_slab = H, max(S, 1), BB * H
         a.dho_nslab = 1
@@ -452,7 +458,17 @@ PERSIST_LENGTHS = os.environ.get("SKR_PERSIST_LENGTHS", "1") != "0"
 # LayerNorm partial sums (csrc/hyper_mod.hip); SKR_HYPER_MOD=0 keeps the
 # plain bf16-output GEMM + the main cell's in-launch statistics exchange.
 HYPER_MOD = os.environ.get("SKR_HYPER_MOD", "1") != "0"
-HYPER_MAIN_C = int(os.environ.get("SKR_HYPER_MAIN_C", "0"))   # workgroups per row of the MOD-3 main cell (0: policy)
+HYPER_MAIN_C = int(os.environ.get("SKR_HYPER_MAIN_C", "0"))
+# LayerNorm saves (xhat, chat and their gradients dlny / dlncy) in bf16 in
+# bf16 training: half the bytes of the cells' saves and of the gamma / beta
+# reductions (csrc/lstm_args.h save_lp; the forward runs on fp32 values, the
+# backward recomputes the gate activations from the bf16 save, like any bf16
+# activation save). SKR_LN_SAVES_LP=0 keeps them fp32.
+LN_SAVES_LP = os.environ.get("SKR_LN_SAVES_LP", "1") != "0"
+
+
+def _ln_saves_lp(infer: bool) -> bool:
+    return LN_SAVES_LP and not infer and gemm.lp_dtype() == torch.bfloat16   # workgroups per row of the MOD-3 main cell (0: policy)
 
 
 def _split_override(var: str, planned: int, K: int) -> int:
@@ -579,9 +595,11 @@ class _HyperSeq(torch.autograd.Function):
         HH = torch.empty(T, B, Hh, device=dev, dtype=f32)
         # saves for the backward (both cells are LayerNorm cells: xhat / rstd /
         # chat; the kernels recompute the gate activations); none at inference
-        sv = (lambda *shape: None) if infer else (lambda *shape: torch.empty(*shape, device=dev, dtype=f32))
-        XHAT, RSTD, CHAT = sv(T, B, G), sv(T, B, 5), sv(T, B, H)
-        HXHAT, HRSTD, HCHAT = sv(T, B, Gh), sv(T, B, 5), sv(T, B, Hh)
+        slp = _ln_saves_lp(infer)
+        sdt = torch.bfloat16 if slp else f32
+        sv = (lambda *shape, dt=f32: None) if infer else (lambda *shape, dt=f32: torch.empty(*shape, device=dev, dtype=dt))
+        XHAT, RSTD, CHAT = sv(T, B, G, dt=sdt), sv(T, B, 5), sv(T, B, H, dt=sdt)
+        HXHAT, HRSTD, HCHAT = sv(T, B, Gh, dt=sdt), sv(T, B, 5), sv(T, B, Hh, dt=sdt)
         # modulation vectors in bf16 when the GEMMs are bf16 (read only by the main cells)
         VEC = torch.empty(T, B, 12 * H, device=dev, dtype=torch.bfloat16 if vbf else f32)
         sd = _seed_tensor(seed, dev)
@@ -607,6 +625,7 @@ class _HyperSeq(torch.autograd.Function):
             XHc = XH.contiguous()
         # hyper cell args (LN-LSTM, no modulation)
         ah = LstmFwdArgs()
+        ah.save_lp = int(slp)
         ah.B, ah.H = B, Hh
         ah.ld_xp, ah.ld_R = Gh, Gh
         ah.R, ah.R_nslab, ah.R_slab = RY.data_ptr(), max(S_y, 1), B * Gh
@@ -616,6 +635,7 @@ class _HyperSeq(torch.autograd.Function):
         ah.ld_lp, ah.lp_kind = K, _lp_kind(A)
         # main cell args (LN + modulation)
         am = LstmFwdArgs()
+        am.save_lp = int(slp)
         am.B, am.H = B, H
         am.ld_xp, am.ld_R = G, G
         am.R_nslab, am.R_slab = max(S_m, 1), B * G
@@ -665,7 +685,7 @@ class _HyperSeq(torch.autograd.Function):
         s = _Saved()
         for k, v in dict(xl=xl, x=x, zc=zc, bp=bp, XH=XH, Whl=Whl, Wyl=Wyl, Pl=Pl, q=q, S_m=S_m, A=A, RM=RM,
                          RLP=RLP, CC=CC, HCC=HCC, XHAT=XHAT, RSTD=RSTD, CHAT=CHAT, HH=HH, HXHAT=HXHAT, HRSTD=HRSTD,
-                         HCHAT=HCHAT, VEC=VEC, seed=sd, meta=meta, W_x=W_x, hW_x=hW_x, W_z=W_z, b_z=b_z, W_a=W_a,
+                         HCHAT=HCHAT, VEC=VEC, seed=sd, meta=meta, slp=slp, W_x=W_x, hW_x=hW_x, W_z=W_z, b_z=b_z, W_a=W_a,
                          mln=mln, hln=hln, vec_folded=hmod).items():
             setattr(s, k, v)
         ctx.s = s
@@ -692,10 +712,11 @@ class _HyperSeq(torch.autograd.Function):
         dRM_lp = torch.empty(T, B, G, device=dev, dtype=ldt) if lp_on else dRM
         dRY_lp = torch.empty(T, B, Gh, device=dev, dtype=ldt) if lp_on else dRY
         dXH = torch.empty(T, B, G, device=dev, dtype=ldt)   # only a GEMM operand downstream
-        DLNY = torch.empty(T, B, G, device=dev, dtype=f32)
-        DLNCY = torch.empty(T, B, H, device=dev, dtype=f32)
-        HDLNY = torch.empty(T, B, Gh, device=dev, dtype=f32)
-        HDLNCY = torch.empty(T, B, Hh, device=dev, dtype=f32)
+        sdt = torch.bfloat16 if s.slp else f32
+        DLNY = torch.empty(T, B, G, device=dev, dtype=sdt)
+        DLNCY = torch.empty(T, B, H, device=dev, dtype=sdt)
+        HDLNY = torch.empty(T, B, Gh, device=dev, dtype=sdt)
+        HDLNCY = torch.empty(T, B, Hh, device=dev, dtype=sdt)
         dVEC = torch.empty(T, B, 12 * H, device=dev, dtype=ldt)
         S_h = _split_override("SKR_HYP_SH", gemm.plan_splits(B, Hh, 12 * H, 1, ldt), 12 * H)
         S_am = _split_override("SKR_HYP_SAM", gemm.plan_splits(B, H, G, 1, ldt), G)
@@ -717,6 +738,7 @@ class _HyperSeq(torch.autograd.Function):
         dhc_rec = dhcT.contiguous().clone() if dhcT is not None else torch.zeros(B, Hh, device=dev, dtype=f32)
         dHout = dHout.contiguous() if dHout is not None else None
         am = LstmBwdArgs()
+        am.save_lp = int(s.slp)
         am.B, am.H = B, H
         am.dh_rec, am.ld_dh_rec, am.dhr_nslab, am.dhr_slab = DAY.data_ptr(), K, max(S_ay, 1), B * K
         am.dh_rec2, am.ld_dh_rec2, am.dhr2_nslab, am.dhr2_slab = DAM.data_ptr(), H, max(S_am, 1), B * H
@@ -732,6 +754,7 @@ class _HyperSeq(torch.autograd.Function):
         am.ld_dG, am.ld_dG_lp, am.dG_lp_kind = G, G, 1 if lp_on else 0
         am.ld_dxp, am.dxp_kind, am.dvec_kind = G, 1 if lp_on else 2, 1 if lp_on else 2
         ah = LstmBwdArgs()
+        ah.save_lp = int(s.slp)
         ah.B, ah.H = B, Hh
         ah.dh_out, ah.dho_nslab, ah.dho_slab = DHZ.data_ptr(), max(S_h, 1), B * Hh
         ah.dh_rec, ah.ld_dh_rec, ah.dc_rec = DAY[0, :, H:].data_ptr(), K, dhc_rec.data_ptr()

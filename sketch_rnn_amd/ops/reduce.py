@@ -1,7 +1,7 @@
 """Column reductions for sequence parameter gradients (``csrc/reduce.hip``).
 
 ``colsum(x, y)`` returns ``(sum_rows(x * y), sum_rows(x))`` for ``x, y``
-shaped ``[R1, R2, C]`` (any strides with a contiguous last dim) -- the
+(fp32 or bf16, fp32 accumulation) shaped ``[R1, R2, C]`` (any strides with a contiguous last dim) -- the
 LayerNorm gamma/beta and bias gradients of the recurrent layers, computed in
 one pass over the saved ``[T*B, C]`` streams. PyTorch fallback on the CPU.
 """
@@ -30,14 +30,15 @@ def colsum(x: torch.Tensor, y: Optional[torch.Tensor] = None, splits: Optional[i
     lib = native.require_hip()
     R1, R2, C = x.shape
     if y is not None:
-        assert y.dtype == torch.float32 and y.shape == x.shape and y.stride() == x.stride()
-    if splits is None:
-        splits = -(-1024 // -(-C // 256))
+        assert y.dtype in (torch.float32, torch.bfloat16) and y.shape == x.shape and y.stride() == x.stride()
+    if splits is None:   # ~1024 workgroups; a thread sums 4 columns when C % 4 == 0 (csrc/reduce.hip)
+        splits = -(-1024 // -(-C // (1024 if C % 4 == 0 else 256)))
     RS = max(1, min(splits, (R1 * R2) // 16))
     part = torch.empty(2, RS, C, device=x.device, dtype=torch.float32)
     kind = 1 if x.dtype == torch.bfloat16 else 2
     assert x.dtype in (torch.bfloat16, torch.float32)
-    rc = lib.lib.skr_colsum(x.data_ptr(), kind, y.data_ptr() if y is not None else None, R1, x.stride(0), R2,
+    ykind = 1 if (y is not None and y.dtype == torch.bfloat16) else 2
+    rc = lib.lib.skr_colsum(x.data_ptr(), kind, y.data_ptr() if y is not None else None, ykind, R1, x.stride(0), R2,
                             x.stride(1), C, RS, part[0].data_ptr(), part[1].data_ptr(),
                             torch.cuda.current_stream().cuda_stream)
     if rc != 0:
