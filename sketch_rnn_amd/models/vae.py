@@ -31,6 +31,8 @@ from ..ops.inproj import bilstm_input_proj, stroke_input_proj
 
 # dropout hash streams
 _S_ENC_FW, _S_ENC_BW, _S_DEC, _S_IN, _S_OUT, _S_EPS = 11, 13, 17, 23, 29, 31
+# SKR_LATENT_FUSED=0: the latent layer as separate torch ops (the oracle form)
+LATENT_FUSED = __import__("os").environ.get("SKR_LATENT_FUSED", "1") != "0"
 
 
 def _gaussian(shape, std, gen):
@@ -59,7 +61,13 @@ class Encoder(nn.Module):
         self.sig_b = nn.Parameter(torch.zeros(cfg.z_size))
 
     def forward(self, x: torch.Tensor, lengths: torch.Tensor, train: bool, seed: int):
-        """``x [T, B, 5]`` time-major."""
+        """``x [T, B, 5]`` time-major -> ``(mu, presig)``."""
+        last_h = self.last_hidden(x, lengths, train, seed)
+        return last_h @ self.mu_w + self.mu_b, last_h @ self.sig_w + self.sig_b
+
+    def last_hidden(self, x: torch.Tensor, lengths: torch.Tensor, train: bool, seed: int) -> torch.Tensor:
+        """``[h_fw[len-1] | h_bw[len-1]]`` ([B, 2H]): the encoder summary the
+        latent heads read."""
         cfg = self.cfg
         T, B, _ = x.shape
         H = cfg.enc_rnn_size
@@ -69,10 +77,9 @@ class Encoder(nn.Module):
         if not ln and persist.bilstm_last_ok(x, H, B):
             # one autograd node: input projection + persistent biLSTM writing
             # only h[len - 1] of each row (ops/persist.py _PersistBiEncoder)
-            last_h = persist.bilstm_last_h(x, lengths, self.fw.W_x, self.bw.W_x, self.fw.bias, self.bw.bias,
-                                           self.fw.W_h, self.bw.W_h, drop_keep=keep, drop_seed=seed,
-                                           drop_stream=_S_ENC_FW)
-            return last_h @ self.mu_w + self.mu_b, last_h @ self.sig_w + self.sig_b
+            return persist.bilstm_last_h(x, lengths, self.fw.W_x, self.bw.W_x, self.fw.bias, self.bw.bias,
+                                         self.fw.W_h, self.bw.W_h, drop_keep=keep, drop_seed=seed,
+                                         drop_stream=_S_ENC_FW)
         zeros = x.new_zeros(B, H)
         lns = [(p.ln_gamma, p.ln_beta, p.lnc_gamma, p.lnc_beta) if ln else None for p in (self.fw, self.bw)]
         # both directions' projections in one [T, 2B, 4H] tensor (the backward
@@ -85,10 +92,7 @@ class Encoder(nn.Module):
                                           drop_seed=seed, drop_stream=_S_ENC_FW, ln_f=lns[0], ln_b=lns[1],
                                           lengths=lengths)
         idx = (lengths - 1).clamp(min=0).view(1, B, 1).expand(1, B, H)
-        last_h = torch.cat([torch.gather(o, 0, idx).squeeze(0) for o in outs], -1)
-        mu = last_h @ self.mu_w + self.mu_b
-        presig = last_h @ self.sig_w + self.sig_b
-        return mu, presig
+        return torch.cat([torch.gather(o, 0, idx).squeeze(0) for o in outs], -1)
 
 
 class SketchVAE(nn.Module):
@@ -205,7 +209,27 @@ class SketchVAE(nn.Module):
         dev = strokes.device
         z = None
         kl = strokes.new_zeros(())
-        if cfg.conditional:
+        from ..ops import latent as L
+        H, Hh = cfg.dec_rnn_size, cfg.hyper_num_units
+        widths = {"hyper": (H, Hh, H, Hh), "lstm": (H, H), "layer_norm": (H, H)}[cfg.dec_model]
+        if cfg.conditional and self.class_emb is None and L.latent_ok(strokes.float(), len(widths)) and \
+                LATENT_FUSED:
+            # encoder summary -> (mu, presig, z, KL, decoder state) as one node (ops/latent.py)
+            last_h = self.encoder.last_hidden(strokes[:, 1:].transpose(0, 1), lengths, train, seed)
+            if split_encoder:
+                enc = (last_h,)
+                last_h = last_h.detach().requires_grad_()
+                enc_cut = (enc, (last_h,))
+            from ..ops.recurrent import _seed_tensor
+            mu, presig, z, kl, *segs = L.latent(last_h, self.encoder.mu_w, self.encoder.mu_b, self.encoder.sig_w,
+                                                self.encoder.sig_b, self.init_w, self.init_b,
+                                                _seed_tensor(seed, dev), widths, cfg.kl_tolerance, _S_EPS, eps=eps)
+            # segment order = the state layout of initial_state: hyper [h, hh, c, hc] -> (h, c, hh, hc);
+            # LSTMCell [c, h] -> (h, c); LayerNormLSTMCell [h, c]
+            state = {"hyper": lambda q: (q[0], q[2], q[1], q[3]), "lstm": lambda q: (q[1], q[0]),
+                     "layer_norm": lambda q: (q[0], q[1])}[cfg.dec_model](segs)
+            zc = z
+        elif cfg.conditional:
             mu, presig = self.encode(strokes, lengths, train, seed)
             if split_encoder:
                 enc = (mu, presig)
@@ -217,8 +241,11 @@ class SketchVAE(nn.Module):
             z = mu + sigma * eps
             kl_raw = -0.5 * torch.mean(1 + presig - mu * mu - torch.exp(presig))
             kl = torch.clamp(kl_raw, min=cfg.kl_tolerance)
-        zc = self.condition(z, labels, B, dev)
-        state = self.initial_state(zc, B, dev)
+            zc = self.condition(z, labels, B, dev)
+            state = self.initial_state(zc, B, dev)
+        else:
+            zc = self.condition(z, labels, B, dev)
+            state = self.initial_state(zc, B, dev)
         x_in = strokes[:, :Nmax].transpose(0, 1)
         out, _ = self.decode(x_in, zc, state, train, seed, out_dropout=False)
         target = strokes[:, 1:].transpose(0, 1).reshape(-1, 5)

@@ -313,6 +313,14 @@ class HipLib:
         lib.skr_colsum.restype = _i
         lib.skr_wgrad.argtypes = [_p, _i64, _i64, _p, _i64, _i64, _i64, _i, _i, _i, _i, _p, _p, _p, _p, _p]
         lib.skr_wgrad.restype = _i
+        lib.skr_latent_mid.argtypes = [_p, _p, _p, _p, _u32, _i, _f, _p, _p, _p, _p, _p]
+        lib.skr_latent_mid.restype = _i
+        lib.skr_latent_mid_bwd.argtypes = [_p, _p, _p, _p, _f, _p, _p, _p, _p, _p, _i, _p, _p, _p]
+        lib.skr_latent_mid_bwd.restype = _i
+        lib.skr_tanh_split.argtypes = [_p, _i, _i, _i, C.POINTER(_i), C.POINTER(_p), _p]
+        lib.skr_tanh_split.restype = _i
+        lib.skr_tanh_split_bwd.argtypes = [_i, _i, _i, C.POINTER(_i), C.POINTER(_p), C.POINTER(_p), _p, _p]
+        lib.skr_tanh_split_bwd.restype = _i
         lib.skr_occupancy_hog.argtypes = [_i, _i, _i, _i, _p, _p]
         lib.skr_occupancy_hog.restype = _i
         lib.skr_gru_fwd.argtypes = [C.POINTER(GruFwdArgs), _i, _p]

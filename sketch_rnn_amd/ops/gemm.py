@@ -62,7 +62,20 @@ def _wgrad_hip_ok(a: torch.Tensor, b: torch.Tensor) -> bool:
 WGRAD_HIP = os.environ.get("SKR_WGRAD_HIP", "1") != "0"
 
 
-def _wgrad_hip(a, b, colsum):
+def grad_slot(param: torch.Tensor, shape) -> Optional[torch.Tensor]:
+    """The optimizer-arena slice reserved for ``param``'s gradient
+    (train/optim.py FlatAdam) when it has exactly ``shape`` and is
+    contiguous: a weight-gradient kernel writes there directly, and the
+    tensor it returns becomes ``param.grad`` without a copy."""
+    t = getattr(param, "_grad_slot", None)
+    # only while the gradient is unbound (zero_grad(set_to_none=True)): with
+    # param.grad set to the slot, autograd would add the slot to itself
+    if t is None or param.grad is not None or tuple(t.shape) != tuple(shape) or not t.is_contiguous() or t.dtype != torch.float32:
+        return None
+    return t
+
+
+def _wgrad_hip(a, b, colsum, out=None):
     from ..utils import native
     lib = native.require_hip()
     n, K, M = a.shape
@@ -71,7 +84,7 @@ def _wgrad_hip(a, b, colsum):
     # split K only to fill the chip: whole waves of <= 256 workgroups (one per CU)
     S = max(1, min(256 // tiles, K // 1024)) if tiles < 192 else 1
     dev = a.device
-    out = torch.empty(n, M, N, device=dev, dtype=torch.float32)
+    out = out.view(n, M, N) if out is not None else torch.empty(n, M, N, device=dev, dtype=torch.float32)
     work = torch.empty(n * S, M, N, device=dev, dtype=torch.float32) if S > 1 else None
     cs = torch.empty(n, N, device=dev, dtype=torch.float32) if colsum else None
     csw = torch.empty(n * S, N, device=dev, dtype=torch.float32) if (colsum and S > 1) else None
@@ -84,11 +97,13 @@ def _wgrad_hip(a, b, colsum):
     return out, cs
 
 
-def wgrad(a: torch.Tensor, b: torch.Tensor, colsum: bool = False):
+def wgrad(a: torch.Tensor, b: torch.Tensor, colsum: bool = False, out: Optional[torch.Tensor] = None):
     """Weight gradient ``a^T @ b`` over a long row dimension (K = T*B rows):
     ``a [K, M], b [K, N] -> [M, N]`` (or batched ``[n, K, *] -> [n, M, N]``),
     fp32 output. ``colsum``: also return the column sums of ``b`` (a bias
     gradient that rides on the same pass over ``b``): ``(out, colsum)``.
+    ``out``: a contiguous fp32 destination (e.g. :func:`grad_slot`), used by
+    the hand-written kernel path.
 
     bf16 operands on the GPU run the hand-written MFMA kernel
     (csrc/wgrad_gemm.hip: 256 x 256 tiles, ds_read_b64_tr_b16 operands,
@@ -103,7 +118,7 @@ def wgrad(a: torch.Tensor, b: torch.Tensor, colsum: bool = False):
     if not batched:
         a, b = a.unsqueeze(0), b.unsqueeze(0)
     if _wgrad_hip_ok(a, b):
-        out, cs = _wgrad_hip(a, b, colsum)
+        out, cs = _wgrad_hip(a, b, colsum, out)
         if not batched:
             out, cs = out[0], (cs[0] if cs is not None else None)
         return (out, cs) if colsum else out

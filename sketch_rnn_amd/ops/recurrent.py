@@ -685,7 +685,7 @@ class _HyperSeq(torch.autograd.Function):
         s = _Saved()
         for k, v in dict(xl=xl, x=x, zc=zc, bp=bp, XH=XH, Whl=Whl, Wyl=Wyl, Pl=Pl, q=q, S_m=S_m, A=A, RM=RM,
                          RLP=RLP, CC=CC, HCC=HCC, XHAT=XHAT, RSTD=RSTD, CHAT=CHAT, HH=HH, HXHAT=HXHAT, HRSTD=HRSTD,
-                         HCHAT=HCHAT, VEC=VEC, seed=sd, meta=meta, slp=slp, W_x=W_x, hW_x=hW_x, W_z=W_z, b_z=b_z, W_a=W_a,
+                         HCHAT=HCHAT, VEC=VEC, seed=sd, meta=meta, slp=slp, W_h=W_h, W_x=W_x, hW_x=hW_x, W_z=W_z, b_z=b_z, W_a=W_a,
                          mln=mln, hln=hln, vec_folded=hmod).items():
             setattr(s, k, v)
         ctx.s = s
@@ -804,7 +804,7 @@ class _HyperSeq(torch.autograd.Function):
         # hyper-norm projections, vec_k = (hh @ W_z_k + b_z_k) @ W_a_k: ONE long-K
         # GEMM dP = hh^T @ dvec gives dP_k = hh^T dvec_k, and the same pass over
         # dvec its column sums; the per-k factors are then tiny batched products
-        dW_h = gemm.wgrad(A2[:, :H], dRM_lp.view(TB, G))
+        dW_h = gemm.wgrad(A2[:, :H], dRM_lp.view(TB, G), out=gemm.grad_slot(s.W_h, (H, G)))
         dW_y = gemm.wgrad(A2, dRY_lp.view(TB, Gh))
         # hh_t rows: the bf16 GEMM operand of step t + 1 (no resets on this path,
         # so it is exactly bf16(HH[t])) -- no conversion pass

@@ -63,6 +63,10 @@ class FlatAdam:
             self.flat[o:o + n].copy_(p.detach().reshape(-1))
             p.data = self.flat[o:o + n].view_as(p)
             p.grad = self.grad[o:o + n].view_as(p)
+            # the arena slot a backward kernel may write this gradient into
+            # directly (ops.gemm.grad_slot): autograd then keeps that tensor as
+            # p.grad and gather_grads has nothing to copy for it
+            p._grad_slot = p.grad
         # device scalars: [lr, step, grad_norm, clip_scale, skipped_now, skipped_total, -, -]
         self.scalars = torch.zeros(8, device=dev, dtype=torch.float32)
         self.set_lr(lr)

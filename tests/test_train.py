@@ -388,3 +388,15 @@ def test_fused_decoder_chunking_follows_cu_count():
     assert _chunk_rows(2, 2) == (256 // 33) * 32
     assert _chunk_rows(2, 1, cus=80) == (80 // 33) * 16
     assert _chunk_rows(2, 1, cus=32) == 0      # -> NotCoResident, the CLI uses GraphDecoder
+
+
+def test_grad_slot_only_when_unbound():
+    from sketch_rnn_amd.ops import gemm
+    from sketch_rnn_amd.train.optim import FlatAdam
+    w = torch.nn.Parameter(torch.randn(4, 8))
+    opt = FlatAdam([w], lr=0.1)
+    assert gemm.grad_slot(w, (4, 8)) is None            # p.grad bound to the arena view
+    opt.zero_grad(set_to_none=True)
+    slot = gemm.grad_slot(w, (4, 8))
+    assert slot is not None and slot.data_ptr() == opt.grad.data_ptr()
+    assert gemm.grad_slot(w, (8, 4)) is None
