@@ -321,6 +321,10 @@ class HipLib:
         lib.skr_tanh_split.restype = _i
         lib.skr_tanh_split_bwd.argtypes = [_i, _i, _i, C.POINTER(_i), C.POINTER(_p), C.POINTER(_p), _p, _p]
         lib.skr_tanh_split_bwd.restype = _i
+        lib.skr_hyper_fold.argtypes = [_p, _p, _p, _p, _i, _i, _i, _p, _p, _p, _p, _p]
+        lib.skr_hyper_fold.restype = _i
+        lib.skr_hyper_fold_bwd.argtypes = [_p, _p, _p, _p, _p, _i, _i, _i, _p, _p, _p, _p]
+        lib.skr_hyper_fold_bwd.restype = _i
         lib.skr_occupancy_hog.argtypes = [_i, _i, _i, _i, _p, _p]
         lib.skr_occupancy_hog.restype = _i
         lib.skr_gru_fwd.argtypes = [C.POINTER(GruFwdArgs), _i, _p]

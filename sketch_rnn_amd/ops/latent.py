@@ -36,6 +36,7 @@ class _Latent(torch.autograd.Function):
     @staticmethod
     def forward(ctx, h, w_mu, b_mu, w_sig, b_sig, w_init, b_init, seed, eps, meta):
         widths, kl_tol, stream = meta
+        ctx.set_materialize_grads(False)   # mu / presig are usually unused: None grads
         lib = native.require_hip().lib
         st = torch.cuda.current_stream().cuda_stream
         h = h.contiguous()

@@ -86,6 +86,7 @@ class _MDNHead(torch.autograd.Function):
     def forward(ctx, X, W, b, target, seed, meta):
         from ._hipapi import HeadDx, HeadDw, HeadFwd  # noqa: F401 (bound in native)
         M, mode, F, mask_pen, log_floor, keep, stream = meta
+        ctx.set_materialize_grads(False)   # the shape / pen terms are usually unused: None grads
         lib = native.require_hip()
         Hd, NOUT = W.shape
         NOUTP = _noutp(NOUT)
@@ -129,10 +130,13 @@ class _MDNHead(torch.autograd.Function):
         NOUT = W.shape[1]
         NOUTP = dz.shape[1]
         dev = X2.device
-        z0 = torch.zeros((), device=dev)
-        gt = g_total if g_total is not None else z0
-        scale = torch.stack([gt + (g_pen if g_pen is not None else z0),
-                             gt + (g_shape if g_shape is not None else z0)]).float().contiguous()
+        if g_pen is None and g_shape is None and g_total is not None:   # the training loss: one copy
+            scale = g_total.float().reshape(1).expand(2).contiguous()
+        else:
+            z0 = torch.zeros((), device=dev)
+            gt = g_total if g_total is not None else z0
+            scale = torch.stack([gt + (g_pen if g_pen is not None else z0),
+                                 gt + (g_shape if g_shape is not None else z0)]).float().contiguous()
         dX = dW = db = None
         if ctx.needs_input_grad[0]:
             Wb = torch.zeros(Hd, NOUTP, device=dev, dtype=torch.bfloat16)

@@ -1,14 +1,13 @@
-"""Native recurrences on the GPU: per-step library GEMM + fused HIP cell kernel.
+"""Native recurrences on the GPU: per-step skinny GEMM + fused HIP cell kernel.
 
 Step ``t`` of a layer is two launches: ``R = h_{t-1} @ W_h`` (the skinny
-split-K MFMA GEMM of ``csrc/skinny_gemm.hip``; hipBLASLt for fp32 operands)
-and one fused cell kernel
-(``csrc/lstm_cell.hip``) that adds the hoisted input projection, applies
-LayerNorm / hyper modulation / gates / dropout / eoc reset and writes the
-next GEMM's operand directly. The backward runs the mirror image in reverse
-and leaves all weight gradients to single large GEMMs over the whole
-sequence after the scan (optionally chunked onto an auxiliary stream during
-the scan. Launched from Python but designed to be captured
+split-K MFMA GEMM of ``csrc/skinny_gemm.hip``; fp32 operands use its fp32
+MFMA variant) and one fused cell kernel (``csrc/lstm_cell.hip``) that adds
+the hoisted input projection, applies LayerNorm / hyper modulation / gates /
+dropout / eoc reset and writes the next GEMM's operand directly. The
+backward runs the mirror image in reverse and leaves all weight gradients
+to single long-K GEMMs over the whole sequence after the scan
+(``csrc/wgrad_gemm.hip``). Launched from Python but designed to be captured
 whole into a HIP graph (no allocation depends on data, no host sync).
 
 * ``_LSTMSeq`` handles ``nd`` independent recurrences of the same shape in
@@ -16,9 +15,11 @@ whole into a HIP graph (no allocation depends on data, no host sync).
   encoder as ``2B`` rows, one batched GEMM, per-direction LN parameters).
 * ``_HyperSeq`` folds the two-stage hyper-norm projections
   ``vec_k = (hh @ W_z_k + b_z_k) @ W_a_k`` into ``vec = hh @ P + q`` with
-  ``P = [W_z_k W_a_k]_k`` built once per call, so each time step costs one
-  extra GEMM forward and one backward; all hyper-projection weight
-  gradients are reduced after the scan from the saved ``dvec`` stream.
+  ``P = [W_z_k W_a_k]_k`` built once per call (``csrc/hyper_fold.hip``); a
+  forward step is [grouped R_main + R_hyp GEMM] -> [hyper cell] -> [fused
+  modulation step, ``csrc/hyper_mod.hip``] -> [main cell]; all
+  hyper-projection weight gradients are reduced after the scan from the
+  saved ``dvec`` stream.
 
 Autograd boundaries are whole sequences, so no per-step autograd nodes exist.
 """
@@ -478,9 +479,25 @@ def _split_override(var: str, planned: int, K: int) -> int:
     return v if v > 0 and planned > 0 and K % (64 * v) == 0 else planned
 
 
+def _fold_ok(H: int, Hh: int, E: int) -> bool:
+    """Shapes of csrc/hyper_fold.hip (the vae_large / vae_classcond decoders)."""
+    return H % 256 == 0 and Hh % 16 == 0 and 1 <= E <= 32
+
+
 def _hyper_proj_grads(dP1, sV, s, Hh, H, E):
     """Hyper-norm projection gradients from ``dP1 = hh^T dvec`` and the
     column sums ``sV`` of dvec."""
+    if dP1.is_cuda and _fold_ok(H, Hh, E):   # three small reductions, two launches (csrc/hyper_fold.hip)
+        lib = native.require_hip()
+        dev = dP1.device
+        dW_z = torch.empty(Hh, 12 * E, device=dev)
+        db_z = torch.empty(12 * E, device=dev)
+        dWa = torch.empty(12, E, H, device=dev)
+        _check(lib.lib.skr_hyper_fold_bwd(dP1.contiguous().data_ptr(), sV.contiguous().data_ptr(),
+                                          s.W_z.detach().contiguous().data_ptr(), s.b_z.detach().contiguous().data_ptr(),
+                                          s.W_a.detach().contiguous().data_ptr(), Hh, H, E, dW_z.data_ptr(),
+                                          db_z.data_ptr(), dWa.data_ptr(), _stream()), "hyper_fold_bwd")
+        return dW_z, db_z, dWa, sV[8 * H:].reshape(4 * H)
     dP = dP1.view(Hh, 12, H).transpose(0, 1)                       # [12, Hh, H]
     sV = sV.view(12, H)
     Wz3 = s.W_z.view(Hh, 12, E).transpose(0, 1)                    # [12, Hh, E]
@@ -506,6 +523,9 @@ class _HyperSeq(torch.autograd.Function):
     def forward(ctx, x, zc, h0, c0, hh0, hc0, seed, W_x, W_h, bias, hW_x, hW_h, hln_g, hln_b, hlnc_g, hlnc_b,
                 W_z, b_z, W_a, ln_g, ln_b, lnc_g, lnc_b, meta):
         forget_bias, keep, hkeep, stream, E, infer = meta   # infer: no autograd graph is being built
+        # unused outputs (the final states in training) get None grads, not
+        # materialised zero tensors (fills + copies inside the captured step)
+        ctx.set_materialize_grads(False)
         lib = native.require_hip()
         T, B, IX = x.shape                      # input = [x | zc broadcast over T]
         IN = W_x.shape[0]
@@ -542,6 +562,7 @@ class _HyperSeq(torch.autograd.Function):
             q = torch.bmm(b_z.view(12, 1, E), W_a).reshape(12, H).contiguous()
             return P.to(dt).contiguous(), q
 
+        qb_f = None
         if infer:
             Whl = Wyl = Pl = None
             WhT = gemm.derived(W_h, "hypWhT%s" % dt, lambda W: gemm.lp(W).t().contiguous())
@@ -555,10 +576,21 @@ class _HyperSeq(torch.autograd.Function):
             WyT = torch.empty(Gh, K, dtype=dt, device=dev)
             gemm.cast_transpose(hW_x[IN:], Wyl[:H], WyT[:, :H])
             gemm.cast_transpose(hW_h, Wyl[H:], WyT[:, H:])
-            Wz3 = W_z.view(Hh, 12, E).permute(1, 0, 2)
-            Pf = torch.bmm(Wz3, W_a).permute(1, 0, 2).reshape(Hh, 12 * H)
-            q = torch.bmm(b_z.view(12, 1, E), W_a).reshape(12, H).contiguous()
-            Pl, PlT = gemm.cast_transpose(Pf)    # B^T for the backward dvec @ P^T / the forward hh @ P
+            if _fold_ok(H, Hh, E):   # P and q in both bf16 layouts, one launch (csrc/hyper_fold.hip)
+                Pl = torch.empty(Hh, 12 * H, dtype=dt, device=dev)
+                PlT = torch.empty(12 * H, Hh, dtype=dt, device=dev)
+                q = torch.empty(12, H, device=dev, dtype=f32)
+                qb_f = torch.empty(12 * H, device=dev, dtype=f32)
+                _check(lib.lib.skr_hyper_fold(W_z.detach().contiguous().data_ptr(), b_z.detach().contiguous().data_ptr(),
+                                              W_a.detach().contiguous().data_ptr(), bias.detach().contiguous().data_ptr(),
+                                              Hh, H, E, Pl.data_ptr(), PlT.data_ptr(), q.data_ptr(), qb_f.data_ptr(),
+                                              _stream()), "hyper_fold")
+            else:
+                Wz3 = W_z.view(Hh, 12, E).permute(1, 0, 2)
+                Pf = torch.bmm(Wz3, W_a).permute(1, 0, 2).reshape(Hh, 12 * H)
+                q = torch.bmm(b_z.view(12, 1, E), W_a).reshape(12, H).contiguous()
+                Pl, PlT = gemm.cast_transpose(Pf)    # B^T for the backward dvec @ P^T / the forward hh @ P
+                qb_f = None
         else:
             Whl = gemm.lp(W_h).contiguous()      # [H, G]: B^T of dR_main @ W_h^T
             WhT = Whl.t().contiguous()           # [G, H]: B^T of h @ W_h
@@ -617,9 +649,12 @@ class _HyperSeq(torch.autograd.Function):
         hmod = HYPER_MOD and vbf and dev.type == "cuda" and Hh == 256 and B <= 112 and H % 32 == 0 and S_m in (1, 2, 4)
         if hmod:
             mod = 3
-            qb = q.detach().clone()
-            qb[8:] += bias_c.detach().view(4, H)
-            qb = qb.reshape(12 * H).contiguous()
+            if qb_f is not None:   # q + the main bias on the shift block, from the fold kernel
+                qb = qb_f
+            else:
+                qb = q.detach().clone()
+                qb[8:] += bias_c.detach().view(4, H)
+                qb = qb.reshape(12 * H).contiguous()
             GP = torch.empty(B, G, device=dev, dtype=f32)
             GS = torch.empty(B, 4, H // 32, 2, device=dev, dtype=f32)
             XHc = XH.contiguous()

@@ -775,3 +775,49 @@ def test_wgrad_kernel_vs_fp32(n, K, M, N, cs, sliced):
         cerr = float((cs1 - cref).abs().max())
         assert cerr <= 1e-4 * float(cref.abs().max()) + 1e-3, cerr
         assert torch.equal(cs1, cs2)
+
+
+@pytest.mark.parametrize("Hh,H,E", [(256, 2048, 32), (64, 256, 8)])
+def test_hyper_fold_kernels_vs_torch(Hh, H, E):
+    """csrc/hyper_fold.hip: P = W_z W_a per block in both bf16 layouts, q, qb,
+    and the projection gradients, against the fp32 torch products (the
+    headline shape, and E < 32 with its zero-padded LDS tile)."""
+    from sketch_rnn_amd.ops import recurrent
+    from sketch_rnn_amd.utils import native
+    torch.manual_seed(0)
+    Wz = torch.randn(Hh, 12 * E, device=DEV) * 0.2
+    bz = torch.randn(12 * E, device=DEV) * 0.2
+    Wa = torch.randn(12, E, H, device=DEV) * 0.2
+    bias = torch.randn(4 * H, device=DEV)
+    lib = native.require_hip().lib
+    Pl = torch.empty(Hh, 12 * H, dtype=torch.bfloat16, device=DEV)
+    PlT = torch.empty(12 * H, Hh, dtype=torch.bfloat16, device=DEV)
+    q = torch.empty(12, H, device=DEV)
+    qb = torch.empty(12 * H, device=DEV)
+    st = torch.cuda.current_stream().cuda_stream
+    assert lib.skr_hyper_fold(Wz.data_ptr(), bz.data_ptr(), Wa.data_ptr(), bias.data_ptr(), Hh, H, E,
+                              Pl.data_ptr(), PlT.data_ptr(), q.data_ptr(), qb.data_ptr(), st) == 0
+    Pref = torch.bmm(Wz.view(Hh, 12, E).permute(1, 0, 2), Wa).permute(1, 0, 2).reshape(Hh, 12 * H)
+    qref = torch.bmm(bz.view(12, 1, E), Wa).reshape(12, H)
+    assert float((Pl.float() - Pref).abs().max()) <= 1e-2 * float(Pref.abs().max())
+    assert torch.equal(PlT, Pl.t().contiguous())
+    assert torch.allclose(q, qref, rtol=1e-5, atol=1e-5)
+    qbr = qref.clone()
+    qbr[8:] += bias.view(4, H)
+    assert torch.allclose(qb, qbr.reshape(-1), rtol=1e-5, atol=1e-5)
+    dP = torch.randn(Hh, 12 * H, device=DEV)
+    sV = torch.randn(12 * H, device=DEV)
+
+    class S:
+        pass
+    s = S()
+    s.W_z, s.b_z, s.W_a = Wz, bz, Wa
+    got = recurrent._hyper_proj_grads(dP, sV, s, Hh, H, E)
+    dPv = dP.view(Hh, 12, H).transpose(0, 1)
+    Wz3 = Wz.view(Hh, 12, E).transpose(0, 1)
+    ref = (torch.bmm(dPv, Wa.transpose(1, 2)).transpose(0, 1).reshape(Hh, 12 * E),
+           torch.bmm(sV.view(12, 1, H), Wa.transpose(1, 2)).reshape(12 * E),
+           torch.bmm(Wz3.transpose(1, 2), dPv) + bz.view(12, E, 1) * sV.view(12, 1, H),
+           sV[8 * H:])
+    for a, b in zip(got, ref):
+        assert torch.allclose(a, b, rtol=1e-4, atol=1e-3 * float(b.abs().max())), float((a - b).abs().max())
