@@ -208,10 +208,10 @@ __device__ __forceinline__ void cell_fwd_body(const FwdArgs& a, const int c, con
     for (int k = 0; k < UPT; ++k) {
         const int u = base + k * NT + tid;
         const int64_t ro = (int64_t)b * H + u;
-        const float i = sigmoidf_(g[k][0]);
-        const float tj = tanhf(g[k][1]);
-        const float f = sigmoidf_(g[k][2] + a.forget_bias);
-        const float o = sigmoidf_(g[k][3]);
+        const float i = cell_sig(g[k][0]);
+        const float tj = cell_tanh(g[k][1]);
+        const float f = cell_sig(g[k][2] + a.forget_bias);
+        const float o = cell_sig(g[k][3]);
         const float m = dropout_mult(keep_on, key, ro, a.keep);
         cn[k] = on[k] ? cp[k] * f + i * tj * m : 0.f;
         og[k] = o;
@@ -245,7 +245,7 @@ __device__ __forceinline__ void cell_fwd_body(const FwdArgs& a, const int c, con
             const int u = base + k * NT + tid;
             const int64_t ro = (int64_t)b * H + u;
             const float ch = (cn[k] - mean) * rc;
-            th[k] = tanhf(ch * lcg[k] + lcb[k]);
+            th[k] = cell_tanh(ch * lcg[k] + lcb[k]);
             if (!on[k]) continue;
             if (save) {
                 st_save(a.chat, ro, ch, a.save_lp);
@@ -260,7 +260,7 @@ __device__ __forceinline__ void cell_fwd_body(const FwdArgs& a, const int c, con
         }
     } else {
 #pragma unroll
-        for (int k = 0; k < UPT; ++k) th[k] = tanhf(cn[k]);
+        for (int k = 0; k < UPT; ++k) th[k] = cell_tanh(cn[k]);
     }
     // ---- outputs + carry (reference eoc reset)
 #pragma unroll

@@ -34,6 +34,17 @@ __device__ __forceinline__ float hash_uniform(uint32_t key, uint32_t idx) {
 
 __device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + expf(-x)); }
 
+// Hardware-instruction activations: v_exp_f32 (exp2) + v_rcp_f32, ~1 ulp each
+// (absolute error ~1e-7 on sigma, ~2e-7 on tanh), against ~25-45 VALU ops
+// per call for the IEEE-exact expf / division / tanhf. Saturate correctly:
+// exp2 overflows to +inf -> rcp 0, underflows to 0 -> rcp 1.
+__device__ __forceinline__ float sigmoid_fast(float x) {
+    return __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-1.4426950408889634f * x));
+}
+__device__ __forceinline__ float tanh_fast(float x) {
+    return 2.0f * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-2.8853900817779268f * x)) - 1.0f;
+}
+
 // ---------------------------------------------------------------------------
 // reductions (wave64 shuffles, then LDS across the block's waves)
 // ---------------------------------------------------------------------------

@@ -84,6 +84,18 @@ struct BwdArgs {
     int save_lp;                       // LN: xhat / chat read and dlny / dlncy written as bf16
 };
 
+// Gate / cell activations of the LSTM-family cell kernels: the hardware
+// exp2 + reciprocal forms (common.h sigmoid_fast / tanh_fast, ~1e-7 absolute
+// error, a few VALU ops instead of ~25-45 for expf + IEEE division / tanhf);
+// -DSKR_EXACT_ACT builds the IEEE forms (A/B and numerics experiments).
+#ifdef SKR_EXACT_ACT
+__device__ __forceinline__ float cell_sig(float x) { return sigmoidf_(x); }
+__device__ __forceinline__ float cell_tanh(float x) { return tanhf(x); }
+#else
+__device__ __forceinline__ float cell_sig(float x) { return sigmoid_fast(x); }
+__device__ __forceinline__ float cell_tanh(float x) { return tanh_fast(x); }
+#endif
+
 // hyper modulation vectors: MOD 1 fp32, MOD 2 bf16
 template <int MOD>
 __device__ __forceinline__ float ldvec(const void* v, int64_t i) {

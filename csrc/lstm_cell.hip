@@ -143,10 +143,10 @@ __global__ __launch_bounds__(NT) void cell_bwd(const BwdArgs a) {
     if (LN) {
 #pragma unroll
         for (int k = 0; k < UPT; ++k) {
-            ac[k][0] = sigmoidf_(xh[k][0] * lg[k][0] + lb[k][0]);
-            ac[k][1] = tanhf(xh[k][1] * lg[k][1] + lb[k][1]);
-            ac[k][2] = sigmoidf_(xh[k][2] * lg[k][2] + lb[k][2] + a.forget_bias);
-            ac[k][3] = sigmoidf_(xh[k][3] * lg[k][3] + lb[k][3]);
+            ac[k][0] = cell_sig(xh[k][0] * lg[k][0] + lb[k][0]);
+            ac[k][1] = cell_tanh(xh[k][1] * lg[k][1] + lb[k][1]);
+            ac[k][2] = cell_sig(xh[k][2] * lg[k][2] + lb[k][2] + a.forget_bias);
+            ac[k][3] = cell_sig(xh[k][3] * lg[k][3] + lb[k][3]);
         }
     }
     // ---- output: h' = th * o
@@ -165,7 +165,7 @@ __global__ __launch_bounds__(NT) void cell_bwd(const BwdArgs a) {
             a.dinit_c[ro] += dcc[k];
         }
         const float o = ac[k][3];
-        const float t = LN ? tanhf(cx[k] * lcg[k] + lcb[k]) : tanhf(cx[k]);
+        const float t = LN ? cell_tanh(cx[k] * lcg[k] + lcb[k]) : cell_tanh(cx[k]);
         dout[k] = dh * t;
         const float dcn = dh * o * (1.f - t * t);
         if (LN) {

@@ -83,19 +83,27 @@ def build_host(force=False):
     return target
 
 
-def build_hip(force=False, jobs=8):
+# Experiment builds (A/B against the default library, loaded with
+# SKR_HIP_LIB=<path>): extra defines per variant.
+VARIANTS = {"exact_act": ["-DSKR_EXACT_ACT"]}
+
+
+def build_hip(force=False, jobs=8, variant=None):
     hipcc = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
     srcs = sorted(glob.glob(os.path.join(CSRC, "*.hip")))
     hdrs = sorted(glob.glob(os.path.join(CSRC, "*.h")))
-    target = os.path.join(OUT, "libskrnn_hip.so")
-    os.makedirs(BUILD, exist_ok=True)
-    os.makedirs(OUT, exist_ok=True)
+    build, out, name = BUILD, OUT, "libskrnn_hip.so"
+    if variant:
+        build, out, name = BUILD + "_" + variant, os.path.join(OUT, "variants"), "libskrnn_hip_%s.so" % variant
+    target = os.path.join(out, name)
+    os.makedirs(build, exist_ok=True)
+    os.makedirs(out, exist_ok=True)
     flags = ["-O3", "-std=c++17", "-fPIC", "--offload-arch=" + ARCH, "-Wall", "-Wno-unused-function",
-             "-munsafe-fp-atomics", "-I" + CSRC]
+             "-munsafe-fp-atomics", "-I" + CSRC] + (VARIANTS[variant] if variant else [])
     tool = [_toolchain_id(hipcc)]
     objs, jobs_list = [], []
     for s in srcs:
-        o = os.path.join(BUILD, os.path.basename(s) + ".o")
+        o = os.path.join(build, os.path.basename(s) + ".o")
         objs.append(o)
         cmd = [hipcc] + flags + ["-c", s, "-o", o]
         if force or _stale(o, [s] + hdrs, cmd + tool):
@@ -133,7 +141,11 @@ def main():
     ap.add_argument("--force", action="store_true")
     ap.add_argument("--only", choices=["host", "hip"])
     ap.add_argument("-j", type=int, default=8)
+    ap.add_argument("--variant", choices=sorted(VARIANTS), help="experiment build of the HIP library only")
     a = ap.parse_args()
+    if a.variant:
+        print(build_hip(a.force, a.j, a.variant))
+        return
     if a.only in (None, "host"):
         build_host(a.force)
     if a.only in (None, "hip"):

@@ -104,7 +104,7 @@ def hyper_sequence(p, x, h0, c0, hh0, hc0, forget_bias: float = 1.0, drop_keep: 
     """HyperLSTM over the input ``[x | zc broadcast over time]`` (``zc``
     optional: a per-sequence input whose projection is computed once)."""
     if use_hip(x):
-        from .recurrent import hyper_sequence_hip
+        from .hyper import hyper_sequence_hip
         return hyper_sequence_hip(p, x, h0, c0, hh0, hc0, forget_bias, drop_keep, drop_seed,
                                   drop_stream, hyp_drop_keep, zc)
     if zc is not None:

@@ -282,6 +282,12 @@ class HipLib:
         lib.skr_lstm_fwd_step.restype = _i
         lib.skr_lstm_bwd_step.argtypes = [C.POINTER(LstmBwdArgs), _i, _i, _p]
         lib.skr_lstm_bwd_step.restype = _i
+        lib.skr_row_fwd_step.argtypes = [C.POINTER(LstmFwdArgs), _i, _p]
+        lib.skr_row_fwd_step.restype = _i
+        lib.skr_row_bwd_step.argtypes = [C.POINTER(LstmBwdArgs), _i, _p]
+        lib.skr_row_bwd_step.restype = _i
+        lib.skr_row_supported.argtypes = [_i]
+        lib.skr_row_supported.restype = _i
         lib.skr_mdn_loss.argtypes = [_p, _i64, _p, _i64, _i64, _i, _i, _f, _i, _f, _p, _p, _p, _p]
         lib.skr_mdn_loss.restype = _i
         lib.skr_adam_step.argtypes = [_p, _p, _p, _p, _p, _p, _i64, _f, _f, _f, _i, _f, _i, _p]

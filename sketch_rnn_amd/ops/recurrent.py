@@ -13,13 +13,8 @@ whole into a HIP graph (no allocation depends on data, no host sync).
 * ``_LSTMSeq`` handles ``nd`` independent recurrences of the same shape in
   one launch per step (``nd = 2``: both directions of the bidirectional
   encoder as ``2B`` rows, one batched GEMM, per-direction LN parameters).
-* ``_HyperSeq`` folds the two-stage hyper-norm projections
-  ``vec_k = (hh @ W_z_k + b_z_k) @ W_a_k`` into ``vec = hh @ P + q`` with
-  ``P = [W_z_k W_a_k]_k`` built once per call (``csrc/hyper_fold.hip``); a
-  forward step is [grouped R_main + R_hyp GEMM] -> [hyper cell] -> [fused
-  modulation step, ``csrc/hyper_mod.hip``] -> [main cell]; all
-  hyper-projection weight gradients are reduced after the scan from the
-  saved ``dvec`` stream.
+* The HyperLSTM sequence (grouped GEMMs, fused modulation step) lives in
+  :mod:`.hyper` and uses the cell launchers and geometry defined here.
 
 Autograd boundaries are whole sequences, so no per-step autograd nodes exist.
 """
@@ -34,7 +29,6 @@ import torch
 from ..utils import native
 from . import gemm
 from ._hipapi import FusedBwdArgs, FusedFwdArgs, LstmBwdArgs, LstmFwdArgs
-from .inproj import bproj_fwd, bproj_ok, bproj_reduce
 from .reduce import colsum
 
 
@@ -176,6 +170,52 @@ class _ClusterSync:
             args.part, args.err = None, None
 
 
+# ---- row-per-workgroup LayerNorm cells (csrc/row_cell.hip) --------------------------
+# One workgroup per row, vector loads, workgroup-local LayerNorm statistics
+# (no in-launch exchange) -- against the clustered kernels of lstm_cell.hip
+# (C workgroups per row, scalar loads, tagged-slot exchanges). Measured on
+# MI355X at the vae_large shapes (B = 100; profiles/r3/row_cells_ab.txt):
+# faster for the HyperLSTM main-cell backward (15.4 vs 16.9 us), slower
+# everywhere else (main forward 13.5 vs 9.5, hyper cell 11.6 / 8.2 vs
+# 5.1 / 6.6): 100 rows occupy 100 CUs, and a CU streams only ~10-20 GB/s
+# at these latencies, so spreading a row's bytes over 8 CUs wins whenever
+# the row kernel saves no exchange-heavy phase. SKR_ROW_CELLS: "main"
+# (default: the main-cell backward only), "all" (every eligible LayerNorm
+# cell), "0" (none).
+ROW_CELLS = os.environ.get("SKR_ROW_CELLS", "main")
+ROW_STATS = {"row": 0, "cluster": 0}   # launches by kind (tests check which kernels the hot path takes)
+
+
+def _row_on(mod: int, fwd: bool) -> bool:
+    if ROW_CELLS == "all":
+        return True
+    return ROW_CELLS == "main" and not fwd and mod == 2
+
+
+def _cell_fwd(lib, a, ln: bool, mod: int, st: int, what: str) -> None:
+    if ln and mod in (0, 3) and _row_on(mod, True):
+        rc = lib.lib.skr_row_fwd_step(ctypes.byref(a), mod, st)
+        if rc == 0:
+            ROW_STATS["row"] += 1
+            return
+        if rc not in (-2, -3, -4):   # -2/-3/-4: shape, mode or layout the row kernels do not take
+            _check(rc, what + " (row)")
+    ROW_STATS["cluster"] += 1
+    _check(lib.lib.skr_lstm_fwd_step(ctypes.byref(a), int(ln), mod, st), what)
+
+
+def _cell_bwd(lib, a, ln: bool, mod: int, st: int, what: str) -> None:
+    if ln and mod in (0, 2) and _row_on(mod, False):
+        rc = lib.lib.skr_row_bwd_step(ctypes.byref(a), mod, st)
+        if rc == 0:
+            ROW_STATS["row"] += 1
+            return
+        if rc not in (-2, -3, -4):
+            _check(rc, what + " (row)")
+    ROW_STATS["cluster"] += 1
+    _check(lib.lib.skr_lstm_bwd_step(ctypes.byref(a), int(ln), mod, st), what)
+
+
 # ---- fused GEMM + cell forward step (csrc/lstm_fused.hip) ---------------------------
 # Plain LSTM (no LayerNorm) layers with H in {256, 512} and bf16 operands run
 # each forward step as ONE launch. SKR_FUSED=0 keeps the GEMM + cell pair.
@@ -288,7 +328,7 @@ class _LSTMSeq(torch.autograd.Function):
             a.h_carry = HC[t % 2].data_ptr() if HC is not None else None
             a.h_lp = A[t + 1].data_ptr()
             a.c_carry = CC[t + 1].data_ptr()
-            _check(lib.lib.skr_lstm_fwd_step(ctypes.byref(a), int(ln), 0, st), "lstm_fwd_step")
+            _cell_fwd(lib, a, ln, 0, st, "lstm_fwd_step")
         if T == 0:
             hT = h0.clone()
         else:
@@ -377,7 +417,7 @@ class _LSTMSeq(torch.autograd.Function):
             a.step = t
             a.dG = dG[t].data_ptr()
             a.dG_lp = dG_lp[t].data_ptr() if lp_on else None
-            _check(lib.lib.skr_lstm_bwd_step(ctypes.byref(a), int(ln), 0, st), "lstm_bwd_step")
+            _cell_bwd(lib, a, ln, 0, st, "lstm_bwd_step")
             gemm.rec_gemm(dG_lp[t] if lp_on else dG[t], s.Wl, DH, S, nd)
         dh_rec = DH.sum(0) if DH.shape[0] > 1 else DH[0]
         dGs = dG_lp if lp_on else dG
@@ -452,14 +492,6 @@ def bilstm_sequence_packed_hip(xp, W_f, W_b, h0, c0, drop_keep=1.0, drop_seed=0,
 PERSIST_LENGTHS = os.environ.get("SKR_PERSIST_LENGTHS", "1") != "0"
 
 
-# =====================================================================================
-# HyperLSTM sequence
-# =====================================================================================
-# The modulation GEMM fused with the main gates' pre-activations and
-# LayerNorm partial sums (csrc/hyper_mod.hip); SKR_HYPER_MOD=0 keeps the
-# plain bf16-output GEMM + the main cell's in-launch statistics exchange.
-HYPER_MOD = os.environ.get("SKR_HYPER_MOD", "1") != "0"
-HYPER_MAIN_C = int(os.environ.get("SKR_HYPER_MAIN_C", "0"))
 # LayerNorm saves (xhat, chat and their gradients dlny / dlncy) in bf16 in
 # bf16 training: half the bytes of the cells' saves and of the gamma / beta
 # reductions (csrc/lstm_args.h save_lp; the forward runs on fp32 values, the
@@ -469,425 +501,4 @@ LN_SAVES_LP = os.environ.get("SKR_LN_SAVES_LP", "1") != "0"
 
 
 def _ln_saves_lp(infer: bool) -> bool:
-    return LN_SAVES_LP and not infer and gemm.lp_dtype() == torch.bfloat16   # workgroups per row of the MOD-3 main cell (0: policy)
-
-
-def _split_override(var: str, planned: int, K: int) -> int:
-    """Split-K factor of a per-step HyperLSTM product: the planned one, or
-    ``$var`` (tuning sweeps) when it divides K into whole 64-wide K tiles."""
-    v = int(os.environ.get(var, "0"))
-    return v if v > 0 and planned > 0 and K % (64 * v) == 0 else planned
-
-
-def _fold_ok(H: int, Hh: int, E: int) -> bool:
-    """Shapes of csrc/hyper_fold.hip (the vae_large / vae_classcond decoders)."""
-    return H % 256 == 0 and Hh % 16 == 0 and 1 <= E <= 32
-
-
-def _hyper_proj_grads(dP1, sV, s, Hh, H, E):
-    """Hyper-norm projection gradients from ``dP1 = hh^T dvec`` and the
-    column sums ``sV`` of dvec."""
-    if dP1.is_cuda and _fold_ok(H, Hh, E):   # three small reductions, two launches (csrc/hyper_fold.hip)
-        lib = native.require_hip()
-        dev = dP1.device
-        dW_z = torch.empty(Hh, 12 * E, device=dev)
-        db_z = torch.empty(12 * E, device=dev)
-        dWa = torch.empty(12, E, H, device=dev)
-        _check(lib.lib.skr_hyper_fold_bwd(dP1.contiguous().data_ptr(), sV.contiguous().data_ptr(),
-                                          s.W_z.detach().contiguous().data_ptr(), s.b_z.detach().contiguous().data_ptr(),
-                                          s.W_a.detach().contiguous().data_ptr(), Hh, H, E, dW_z.data_ptr(),
-                                          db_z.data_ptr(), dWa.data_ptr(), _stream()), "hyper_fold_bwd")
-        return dW_z, db_z, dWa, sV[8 * H:].reshape(4 * H)
-    dP = dP1.view(Hh, 12, H).transpose(0, 1)                       # [12, Hh, H]
-    sV = sV.view(12, H)
-    Wz3 = s.W_z.view(Hh, 12, E).transpose(0, 1)                    # [12, Hh, E]
-    dW_z = torch.bmm(dP, s.W_a.transpose(1, 2)).transpose(0, 1).reshape(Hh, 12 * E)
-    dWa = torch.bmm(Wz3.transpose(1, 2), dP) + s.b_z.view(12, E, 1) * sV.view(12, 1, H)
-    db_z = torch.bmm(sV.view(12, 1, H), s.W_a.transpose(1, 2)).reshape(12 * E)
-    dbias = sV[8:].reshape(4 * H)                                  # shift-vector grads = bias grads
-    return dW_z, db_z, dWa, dbias
-
-
-class _HyperSeq(torch.autograd.Function):
-    """HyperLSTM layer (LN main cell modulated by a LN hyper cell).
-
-    Forward per step: [grouped GEMM R_main + R_hyp] -> [hyper cell] ->
-    [vec = hh @ P + q] -> [main cell]; backward per step: [main cell bwd] ->
-    [grouped GEMM dR_main W_h^T + dvec P^T] -> [hyper cell bwd] ->
-    [dR_hyp W_y^T]; weight gradients are long-K GEMMs over all T*B rows after
-    the scan. (A persistent one-launch forward was built and measured slower:
-    csrc/experiments/hyper_persist.hip.)
-    """
-
-    @staticmethod
-    def forward(ctx, x, zc, h0, c0, hh0, hc0, seed, W_x, W_h, bias, hW_x, hW_h, hln_g, hln_b, hlnc_g, hlnc_b,
-                W_z, b_z, W_a, ln_g, ln_b, lnc_g, lnc_b, meta):
-        forget_bias, keep, hkeep, stream, E, infer = meta   # infer: no autograd graph is being built
-        # unused outputs (the final states in training) get None grads, not
-        # materialised zero tensors (fills + copies inside the captured step)
-        ctx.set_materialize_grads(False)
-        lib = native.require_hip()
-        T, B, IX = x.shape                      # input = [x | zc broadcast over T]
-        IN = W_x.shape[0]
-        H, Hh = W_h.shape[0], hW_h.shape[0]
-        G, Gh = 4 * H, 4 * Hh
-        K = H + Hh
-        dev = x.device
-        f32 = torch.float32
-        TB = T * B
-        bp = bproj_ok(x) and not x.requires_grad
-        xl = None
-        if bp:   # stroke rows per position, z rows once per sequence (csrc/inproj.hip)
-            XH = bproj_fwd(x, W_x[:IX], zc @ W_x[IX:] if zc is not None else None)
-            XHY = bproj_fwd(x, hW_x[:IX], zc @ hW_x[IX:IN] if zc is not None else None)
-        else:
-            if zc is not None:
-                x = torch.cat([x, zc.unsqueeze(0).expand(T, B, zc.shape[-1])], -1)
-            xl = gemm.lp(x.reshape(TB, IN).contiguous())
-            if infer:
-                XH = gemm.mm(xl, gemm.derived(W_x, "lp%s" % gemm.lp_dtype(), gemm.lp)).view(T, B, G)
-                XHY = gemm.mm(xl, gemm.derived(hW_x, "lpx%d%s" % (IN, gemm.lp_dtype()),
-                                               lambda W: gemm.lp(W[:IN]).contiguous())).view(T, B, Gh)
-            else:
-                XH = gemm.mm(xl, gemm.lp(W_x)).view(T, B, G)
-                XHY = gemm.mm(xl, gemm.lp(hW_x[:IN])).view(T, B, Gh)
-        dt = gemm.lp_dtype()
-
-        def wy(hW_x, hW_h):                      # [K, Gh]: B^T of dR_hyp @ W_y^T
-            return torch.cat([hW_x[IN:], hW_h], 0).to(dt).contiguous()
-
-        def fold(W_z, b_z, W_a):                 # hyper-norm projections folded: vec = hh @ P + q
-            Wz3 = W_z.view(Hh, 12, E).permute(1, 0, 2)                      # [12, Hh, E]
-            P = torch.bmm(Wz3, W_a).permute(1, 0, 2).reshape(Hh, 12 * H)   # [Hh, 12H]
-            q = torch.bmm(b_z.view(12, 1, E), W_a).reshape(12, H).contiguous()
-            return P.to(dt).contiguous(), q
-
-        qb_f = None
-        if infer:
-            Whl = Wyl = Pl = None
-            WhT = gemm.derived(W_h, "hypWhT%s" % dt, lambda W: gemm.lp(W).t().contiguous())
-            WyT = gemm.derived((hW_x, hW_h), "hypWyT%s" % dt, lambda a, b: wy(a, b).t().contiguous())
-            PlT, q = gemm.derived((W_z, b_z, W_a), "hypP%s" % dt,
-                                  lambda a, b, c: (lambda P, q: (P.t().contiguous(), q))(*fold(a, b, c)))
-        elif dt == torch.bfloat16 and W_h.is_cuda:
-            # both bf16 layouts of each weight in one pass (csrc/convert.hip)
-            Whl, WhT = gemm.cast_transpose(W_h)  # [H, G]: B^T of dR_main @ W_h^T; [G, H]: B^T of h @ W_h
-            Wyl = torch.empty(K, Gh, dtype=dt, device=dev)
-            WyT = torch.empty(Gh, K, dtype=dt, device=dev)
-            gemm.cast_transpose(hW_x[IN:], Wyl[:H], WyT[:, :H])
-            gemm.cast_transpose(hW_h, Wyl[H:], WyT[:, H:])
-            if _fold_ok(H, Hh, E):   # P and q in both bf16 layouts, one launch (csrc/hyper_fold.hip)
-                Pl = torch.empty(Hh, 12 * H, dtype=dt, device=dev)
-                PlT = torch.empty(12 * H, Hh, dtype=dt, device=dev)
-                q = torch.empty(12, H, device=dev, dtype=f32)
-                qb_f = torch.empty(12 * H, device=dev, dtype=f32)
-                _check(lib.lib.skr_hyper_fold(W_z.detach().contiguous().data_ptr(), b_z.detach().contiguous().data_ptr(),
-                                              W_a.detach().contiguous().data_ptr(), bias.detach().contiguous().data_ptr(),
-                                              Hh, H, E, Pl.data_ptr(), PlT.data_ptr(), q.data_ptr(), qb_f.data_ptr(),
-                                              _stream()), "hyper_fold")
-            else:
-                Wz3 = W_z.view(Hh, 12, E).permute(1, 0, 2)
-                Pf = torch.bmm(Wz3, W_a).permute(1, 0, 2).reshape(Hh, 12 * H)
-                q = torch.bmm(b_z.view(12, 1, E), W_a).reshape(12, H).contiguous()
-                Pl, PlT = gemm.cast_transpose(Pf)    # B^T for the backward dvec @ P^T / the forward hh @ P
-                qb_f = None
-        else:
-            Whl = gemm.lp(W_h).contiguous()      # [H, G]: B^T of dR_main @ W_h^T
-            WhT = Whl.t().contiguous()           # [G, H]: B^T of h @ W_h
-            Wyl = wy(hW_x, hW_h)
-            WyT = Wyl.t().contiguous()           # [Gh, K]
-            Pl, q = fold(W_z, b_z, W_a)          # B^T for the backward dvec @ P^T
-            PlT = Pl.t().contiguous()            # B^T for the forward  hh @ P
-        fp8 = infer and _fp8_ok(B, G, H, Gh, K, 12 * H, Hh)
-        if fp8:
-            WhT = gemm.derived(WhT, "q8", gemm.quantize_fp8_rows)
-            WyT = gemm.derived(WyT, "q8", gemm.quantize_fp8_rows)
-            PlT = gemm.derived(PlT, "q8", gemm.quantize_fp8_rows)
-            S_m, S_y = gemm.plan_splits_fp8(B, G, H), gemm.plan_splits_fp8(B, Gh, K)
-            S_v = gemm.plan_splits_fp8(B, 12 * H, Hh, max_splits=1)
-        else:
-            S_m = _split_override("SKR_HYP_SM", gemm.plan_splits(B, G, H, 1, dt), H)
-            S_y = _split_override("SKR_HYP_SY", gemm.plan_splits(B, Gh, K, 1, dt), K)
-            S_v = gemm.plan_splits(B, 12 * H, Hh, 1, dt, max_splits=1)
-        rgemm = (lambda a, b, out, S: gemm.rec_gemm_fp8(a, b, out, S)) if fp8 else \
-            (lambda a, b, out, S: gemm.rec_gemm(a, b, out, S))
-        A = torch.empty(T + 1, B, K, device=dev, dtype=torch.uint8 if fp8 else dt)
-        A[0, :, :H].copy_(_to_fp8_act(h0) if fp8 else h0)
-        A[0, :, H:].copy_(_to_fp8_act(hh0) if fp8 else hh0)
-        # R_main: the backward re-reads it (the hyper-modulation gradient
-        # dg * R) as the bf16 copy the main cell saves (RLP); with fp32 GEMM
-        # operands the fp32 split-K slabs of every step are kept instead
-        vbf = not fp8 and dt == torch.bfloat16 and B <= 128 and S_v == 1
-        RLP = torch.empty(T, B, G, device=dev, dtype=torch.bfloat16) if (vbf and not infer) else None
-        CC = torch.empty(T + 1, B, H, device=dev, dtype=f32)
-        CC[0].copy_(c0)
-        HCC = torch.empty(T + 1, B, Hh, device=dev, dtype=f32)
-        HCC[0].copy_(hc0)
-        Hout = torch.empty(T, B, H, device=dev, dtype=f32)
-        HH = torch.empty(T, B, Hh, device=dev, dtype=f32)
-        # saves for the backward (both cells are LayerNorm cells: xhat / rstd /
-        # chat; the kernels recompute the gate activations); none at inference
-        slp = _ln_saves_lp(infer)
-        sdt = torch.bfloat16 if slp else f32
-        sv = (lambda *shape, dt=f32: None) if infer else (lambda *shape, dt=f32: torch.empty(*shape, device=dev, dtype=dt))
-        XHAT, RSTD, CHAT = sv(T, B, G, dt=sdt), sv(T, B, 5), sv(T, B, H, dt=sdt)
-        HXHAT, HRSTD, HCHAT = sv(T, B, Gh, dt=sdt), sv(T, B, 5), sv(T, B, Hh, dt=sdt)
-        # modulation vectors in bf16 when the GEMMs are bf16 (read only by the main cells)
-        VEC = torch.empty(T, B, 12 * H, device=dev, dtype=torch.bfloat16 if vbf else f32)
-        sd = _seed_tensor(seed, dev)
-        hln = [t.contiguous() for t in (hln_g, hln_b, hlnc_g, hlnc_b)]
-        mln = [t.contiguous() for t in (ln_g, ln_b, lnc_g, lnc_b)]
-        bias_c = bias.contiguous()
-        RM = torch.empty(T if (RLP is None and not infer) else 1, max(S_m, 1), B, G, device=dev, dtype=f32)
-        rmi = (lambda t: t) if RM.shape[0] == T else (lambda t: 0)
-        RY = torch.empty(max(S_y, 1), B, Gh, device=dev, dtype=f32)
-        mod = 2 if vbf else 1
-        # modulation step fused with the gate pre-activations and their
-        # LayerNorm partial sums (csrc/hyper_mod.hip): the main cell then needs
-        # no statistics exchange for the gates (MOD 3) and VEC carries q (and
-        # the main bias in its shift block) -- the backward uses a zero vec_bias
-        hmod = HYPER_MOD and vbf and dev.type == "cuda" and Hh == 256 and B <= 112 and H % 32 == 0 and S_m in (1, 2, 4)
-        if hmod:
-            mod = 3
-            if qb_f is not None:   # q + the main bias on the shift block, from the fold kernel
-                qb = qb_f
-            else:
-                qb = q.detach().clone()
-                qb[8:] += bias_c.detach().view(4, H)
-                qb = qb.reshape(12 * H).contiguous()
-            GP = torch.empty(B, G, device=dev, dtype=f32)
-            GS = torch.empty(B, 4, H // 32, 2, device=dev, dtype=f32)
-            XHc = XH.contiguous()
-        # hyper cell args (LN-LSTM, no modulation)
-        ah = LstmFwdArgs()
-        ah.save_lp = int(slp)
-        ah.B, ah.H = B, Hh
-        ah.ld_xp, ah.ld_R = Gh, Gh
-        ah.R, ah.R_nslab, ah.R_slab = RY.data_ptr(), max(S_y, 1), B * Gh
-        ah.ln_g, ah.ln_b, ah.lnc_g, ah.lnc_b = (t.data_ptr() for t in hln)
-        ah.forget_bias, ah.keep = float(forget_bias), float(hkeep)
-        ah.seed, ah.stream = sd.data_ptr(), int(stream) + 1
-        ah.ld_lp, ah.lp_kind = K, _lp_kind(A)
-        # main cell args (LN + modulation)
-        am = LstmFwdArgs()
-        am.save_lp = int(slp)
-        am.B, am.H = B, H
-        am.ld_xp, am.ld_R = G, G
-        am.R_nslab, am.R_slab = max(S_m, 1), B * G
-        am.vec_gs, am.vec_ld, am.vec_bias, am.bias = H, 12 * H, q.data_ptr(), bias_c.data_ptr()
-        am.ln_g, am.ln_b, am.lnc_g, am.lnc_b = (t.data_ptr() for t in mln)
-        am.forget_bias, am.keep = float(forget_bias), float(keep)
-        am.seed, am.stream = sd.data_ptr(), int(stream)
-        am.ld_lp, am.lp_kind = K, _lp_kind(A)
-        clm = _ClusterSync(T, B, H, dev, C=HYPER_MAIN_C if hmod else 0)
-        clh = _ClusterSync(T, B, Hh, dev)
-        st = _stream()
-        group = not fp8 and gemm.GROUPED and S_m >= 1 and S_y >= 1 and dt == torch.bfloat16
-        for t in range(T):
-            clm.set(am, t)
-            clh.set(ah, t)
-            ah.xp, ah.c_prev, ah.step = XHY[t].data_ptr(), HCC[t].data_ptr(), t
-            ah.h_out = HH[t].data_ptr()
-            if not infer:
-                ah.xhat, ah.rstd, ah.chat = HXHAT[t].data_ptr(), HRSTD[t].data_ptr(), HCHAT[t].data_ptr()
-            ah.h_lp, ah.c_carry = A[t + 1, :, H:].data_ptr(), HCC[t + 1].data_ptr()
-            if group:   # R_main and R_hyp in one launch
-                gemm.rec_gemm_group([(A[t, :, :H], WhT, RM[rmi(t)], S_m), (A[t], WyT, RY, S_y)])
-            else:
-                rgemm(A[t, :, :H], WhT, RM[rmi(t)], S_m)
-                rgemm(A[t], WyT, RY, S_y)
-            _check(lib.lib.skr_lstm_fwd_step(ctypes.byref(ah), 1, 0, st), "hyper_fwd_step")
-            if hmod:
-                _check(lib.lib.skr_hyper_mod_fwd(A[t + 1, :, H:].data_ptr(), K, PlT.data_ptr(), qb.data_ptr(),
-                                                 XHc[t].data_ptr(), RM[rmi(t)].data_ptr(), B * G, S_m,
-                                                 VEC[t].data_ptr(), GP.data_ptr(), _ptr(RLP[t] if RLP is not None else None),
-                                                 GS.data_ptr(), B, H, Hh, st), "hyper_mod_fwd")
-                am.gpre, am.gstats, am.gstat_tiles = GP.data_ptr(), GS.data_ptr(), H // 32
-            elif vbf:
-                gemm.rec_gemm_bf16out(A[t + 1, :, H:], PlT, VEC[t])
-            else:
-                rgemm(A[t + 1, :, H:], PlT, VEC[t].unsqueeze(0), S_v)
-            am.xp, am.R, am.vec = XH[t].data_ptr(), RM[rmi(t)].data_ptr(), VEC[t].data_ptr()
-            am.r_lp = RLP[t].data_ptr() if (RLP is not None and not hmod) else None
-            am.c_prev, am.step = CC[t].data_ptr(), t
-            am.h_out = Hout[t].data_ptr()
-            if not infer:
-                am.xhat, am.rstd, am.chat = XHAT[t].data_ptr(), RSTD[t].data_ptr(), CHAT[t].data_ptr()
-            am.h_lp, am.c_carry = A[t + 1, :, :H].data_ptr(), CC[t + 1].data_ptr()
-            _check(lib.lib.skr_lstm_fwd_step(ctypes.byref(am), 1, mod, st), "hyper_main_fwd_step")
-        hT = Hout[T - 1].clone()    # no resets: the carried h is h'
-        hhT = HH[T - 1].clone()
-        s = _Saved()
-        for k, v in dict(xl=xl, x=x, zc=zc, bp=bp, XH=XH, Whl=Whl, Wyl=Wyl, Pl=Pl, q=q, S_m=S_m, A=A, RM=RM,
-                         RLP=RLP, CC=CC, HCC=HCC, XHAT=XHAT, RSTD=RSTD, CHAT=CHAT, HH=HH, HXHAT=HXHAT, HRSTD=HRSTD,
-                         HCHAT=HCHAT, VEC=VEC, seed=sd, meta=meta, slp=slp, W_h=W_h, W_x=W_x, hW_x=hW_x, W_z=W_z, b_z=b_z, W_a=W_a,
-                         mln=mln, hln=hln, vec_folded=hmod).items():
-            setattr(s, k, v)
-        ctx.s = s
-        ctx.dims = (T, B, IX, IN, H, Hh, E)
-        return Hout, hT, CC[T].clone(), hhT, HCC[T].clone()
-
-    @staticmethod
-    def backward(ctx, dHout, dhT, dcT, dhhT, dhcT):
-        s = ctx.s
-        T, B, IX, IN, H, Hh, E = ctx.dims
-        forget_bias, keep, hkeep, stream, _, _ = s.meta
-        lib = native.require_hip()
-        dev = s.A.device
-        f32 = torch.float32
-        G, Gh = 4 * H, 4 * Hh
-        K = H + Hh
-        TB = T * B
-        lp_on = s.Whl.dtype == torch.bfloat16
-        ldt = torch.bfloat16 if lp_on else f32
-        # d(recurrent pre-activations): only GEMM operands downstream, so with
-        # bf16 operands the cell kernels write the bf16 copy alone
-        dRM = None if lp_on else torch.empty(T, B, G, device=dev, dtype=f32)
-        dRY = None if lp_on else torch.empty(T, B, Gh, device=dev, dtype=f32)
-        dRM_lp = torch.empty(T, B, G, device=dev, dtype=ldt) if lp_on else dRM
-        dRY_lp = torch.empty(T, B, Gh, device=dev, dtype=ldt) if lp_on else dRY
-        dXH = torch.empty(T, B, G, device=dev, dtype=ldt)   # only a GEMM operand downstream
-        sdt = torch.bfloat16 if s.slp else f32
-        DLNY = torch.empty(T, B, G, device=dev, dtype=sdt)
-        DLNCY = torch.empty(T, B, H, device=dev, dtype=sdt)
-        HDLNY = torch.empty(T, B, Gh, device=dev, dtype=sdt)
-        HDLNCY = torch.empty(T, B, Hh, device=dev, dtype=sdt)
-        dVEC = torch.empty(T, B, 12 * H, device=dev, dtype=ldt)
-        S_h = _split_override("SKR_HYP_SH", gemm.plan_splits(B, Hh, 12 * H, 1, ldt), 12 * H)
-        S_am = _split_override("SKR_HYP_SAM", gemm.plan_splits(B, H, G, 1, ldt), G)
-        # d[h | hh] = dR_hyp @ W_y^T: at most 4 split-K slabs -- the next step's
-        # two cells read every slab; measured on MI355X (vae_large, same box,
-        # A/B twice): 4 slabs 26.67 / 26.57 vs 8 (the plan) 26.76 / 26.86 ms/step
-        S_ay = gemm.plan_splits(B, K, Gh, 1, ldt)
-        if S_ay > 4:
-            S_ay = next(d for d in (4, 3, 2, 1) if (Gh // 64) % d == 0)
-        S_ay = _split_override("SKR_HYP_SAY", S_ay, Gh)
-        DHZ = torch.empty(max(S_h, 1), B, Hh, device=dev, dtype=f32)    # slabs of dhh from the vec path
-        DAM = torch.zeros(max(S_am, 1), B, H, device=dev, dtype=f32)    # slabs of dh from the main gates
-        DAY = torch.zeros(max(S_ay, 1), B, K, device=dev, dtype=f32)    # slabs of d[h | hh] from the hyper gates
-        if dhT is not None:
-            DAY[0, :, :H].copy_(dhT)
-        if dhhT is not None:
-            DAY[0, :, H:].copy_(dhhT)
-        dc_rec = dcT.contiguous().clone() if dcT is not None else torch.zeros(B, H, device=dev, dtype=f32)
-        dhc_rec = dhcT.contiguous().clone() if dhcT is not None else torch.zeros(B, Hh, device=dev, dtype=f32)
-        dHout = dHout.contiguous() if dHout is not None else None
-        am = LstmBwdArgs()
-        am.save_lp = int(s.slp)
-        am.B, am.H = B, H
-        am.dh_rec, am.ld_dh_rec, am.dhr_nslab, am.dhr_slab = DAY.data_ptr(), K, max(S_ay, 1), B * K
-        am.dh_rec2, am.ld_dh_rec2, am.dhr2_nslab, am.dhr2_slab = DAM.data_ptr(), H, max(S_am, 1), B * H
-        am.dc_rec, am.dho_nslab = dc_rec.data_ptr(), 1
-        am.ln_g, am.lnc_g, am.lnc_b = s.mln[0].data_ptr(), s.mln[2].data_ptr(), s.mln[3].data_ptr()
-        am.ln_b, am.forget_bias = s.mln[1].data_ptr(), float(forget_bias)
-        am.ld_xp, am.ld_R = G, G
-        am.R_nslab, am.R_slab = max(s.S_m, 1), B * G
-        # csrc/hyper_mod.hip folds q into the saved vectors
-        vbias = torch.zeros(12 * H, device=dev, dtype=f32) if s.vec_folded else s.q
-        am.vec_gs, am.vec_ld, am.vec_bias = H, 12 * H, vbias.data_ptr()
-        am.keep, am.seed, am.stream = float(keep), s.seed.data_ptr(), int(stream)
-        am.ld_dG, am.ld_dG_lp, am.dG_lp_kind = G, G, 1 if lp_on else 0
-        am.ld_dxp, am.dxp_kind, am.dvec_kind = G, 1 if lp_on else 2, 1 if lp_on else 2
-        ah = LstmBwdArgs()
-        ah.save_lp = int(s.slp)
-        ah.B, ah.H = B, Hh
-        ah.dh_out, ah.dho_nslab, ah.dho_slab = DHZ.data_ptr(), max(S_h, 1), B * Hh
-        ah.dh_rec, ah.ld_dh_rec, ah.dc_rec = DAY[0, :, H:].data_ptr(), K, dhc_rec.data_ptr()
-        ah.dhr_nslab, ah.dhr_slab = max(S_ay, 1), B * K
-        ah.ln_g, ah.lnc_g, ah.lnc_b = s.hln[0].data_ptr(), s.hln[2].data_ptr(), s.hln[3].data_ptr()
-        ah.ln_b, ah.forget_bias = s.hln[1].data_ptr(), float(forget_bias)
-        ah.keep, ah.seed, ah.stream = float(hkeep), s.seed.data_ptr(), int(stream) + 1
-        ah.ld_dG, ah.ld_dG_lp, ah.dG_lp_kind = Gh, Gh, 1 if lp_on else 0
-        clm, clh = _ClusterSync(T, B, H, dev), _ClusterSync(T, B, Hh, dev)
-        st = _stream()
-        group = lp_on and gemm.GROUPED and S_am >= 1 and S_h >= 1
-        for t in range(T - 1, -1, -1):
-            clm.set(am, t)
-            clh.set(ah, t)
-            am.dh_out = dHout[t].data_ptr() if dHout is not None else None
-            am.c_prev = s.CC[t].data_ptr()
-            am.xhat, am.rstd, am.chat = s.XHAT[t].data_ptr(), s.RSTD[t].data_ptr(), s.CHAT[t].data_ptr()
-            am.xp, am.vec = s.XH[t].data_ptr(), s.VEC[t].data_ptr()
-            if s.RLP is not None:
-                am.R, am.r_lp = None, s.RLP[t].data_ptr()
-            else:
-                am.R, am.r_lp = s.RM[t].data_ptr(), None
-            am.step = t
-            am.dG = None if lp_on else dRM[t].data_ptr()
-            am.dG_lp = dRM_lp[t].data_ptr() if lp_on else None
-            am.dxp, am.dvec = dXH[t].data_ptr(), dVEC[t].data_ptr()
-            am.dlny, am.dlncy = DLNY[t].data_ptr(), DLNCY[t].data_ptr()
-            _check(lib.lib.skr_lstm_bwd_step(ctypes.byref(am), 1, 2 if s.VEC.dtype == torch.bfloat16 else 1, st),
-                   "hyper_main_bwd_step")
-            if group:   # dR_main @ W_h^T and dvec @ P^T in one launch
-                gemm.rec_gemm_group([(dRM_lp[t], s.Whl, DAM, S_am), (dVEC[t], s.Pl, DHZ, S_h)])
-            else:
-                gemm.rec_gemm(dRM_lp[t], s.Whl, DAM, S_am)
-                gemm.rec_gemm(dVEC[t], s.Pl, DHZ, S_h)
-            ah.c_prev = s.HCC[t].data_ptr()
-            ah.xhat, ah.rstd, ah.chat = s.HXHAT[t].data_ptr(), s.HRSTD[t].data_ptr(), s.HCHAT[t].data_ptr()
-            ah.step = t
-            ah.dG = None if lp_on else dRY[t].data_ptr()
-            ah.dG_lp = dRY_lp[t].data_ptr() if lp_on else None
-            ah.dlny, ah.dlncy = HDLNY[t].data_ptr(), HDLNCY[t].data_ptr()
-            _check(lib.lib.skr_lstm_bwd_step(ctypes.byref(ah), 1, 0, st), "hyper_bwd_step")
-            gemm.rec_gemm(dRY_lp[t], s.Wyl, DAY, S_ay)
-        dh0 = DAY[:, :, :H].sum(0) + DAM.sum(0)
-        dhh0 = DAY[:, :, H:].sum(0)
-        # weight / LayerNorm-parameter gradients: long-K products over the T*B saved rows
-        A2 = s.A[:T].reshape(TB, K)
-        # hyper-norm projections, vec_k = (hh @ W_z_k + b_z_k) @ W_a_k: ONE long-K
-        # GEMM dP = hh^T @ dvec gives dP_k = hh^T dvec_k, and the same pass over
-        # dvec its column sums; the per-k factors are then tiny batched products
-        dW_h = gemm.wgrad(A2[:, :H], dRM_lp.view(TB, G), out=gemm.grad_slot(s.W_h, (H, G)))
-        dW_y = gemm.wgrad(A2, dRY_lp.view(TB, Gh))
-        # hh_t rows: the bf16 GEMM operand of step t + 1 (no resets on this path,
-        # so it is exactly bf16(HH[t])) -- no conversion pass
-        HHl = s.A[1:T + 1].reshape(TB, K)[:, H:] if lp_on else s.HH.view(TB, Hh)
-        dP1, sV = gemm.wgrad(HHl, dVEC.view(TB, 12 * H), colsum=True)
-        g_ln, g_hln = [], []
-        for dy, xh, n, out in ((DLNY, s.XHAT, G, g_ln), (DLNCY, s.CHAT, H, g_ln), (HDLNY, s.HXHAT, Gh, g_hln),
-                               (HDLNCY, s.HCHAT, Hh, g_hln)):
-            out += list(colsum(dy.view(-1, n), xh.view(-1, n)))
-        dhW_x = torch.empty_like(s.hW_x)
-        dhW_x[IN:] = dW_y[:H]
-        dhW_h = dW_y[H:]
-        dx = dzc = None
-        if s.bp:   # input-side gradients from one read of dXH / dR_hyp each
-            S_m, P_m = bproj_reduce(s.x, dXH)
-            S_y, P_y = bproj_reduce(s.x, dRY_lp)
-            if s.zc is not None:
-                dW_x = torch.cat([P_m, s.zc.t() @ S_m], 0)
-                dhW_x[:IN] = torch.cat([P_y, s.zc.t() @ S_y], 0)
-                dzc = S_m @ s.W_x[IX:].t() + S_y @ s.hW_x[IX:IN].t()
-            else:
-                dW_x = P_m
-                dhW_x[:IN] = P_y
-        else:
-            dXHl, dXHYl = gemm.lp(dXH.view(TB, G)), gemm.lp(dRY_lp.view(TB, Gh))
-            dW_x = gemm.wgrad(s.xl, dXHl)
-            dhW_x[:IN] = gemm.wgrad(s.xl, dXHYl)
-            dxf = gemm.mm(dXHl, gemm.lp(s.W_x).t())
-            dxf += gemm.mm(dXHYl, gemm.lp(s.hW_x[:IN]).t())
-            dxf = dxf.view(T, B, IN)
-            if s.zc is not None:
-                dx, dzc = dxf[..., :IX], dxf[..., IX:].sum(0)
-            else:
-                dx = dxf
-        dW_z, db_z, dWa, dbias = _hyper_proj_grads(dP1, sV, s, Hh, H, E)
-        ctx.s = None
-        return (dx, dzc, dh0, dc_rec, dhh0, dhc_rec, None, dW_x, dW_h, dbias, dhW_x, dhW_h,
-                g_hln[0], g_hln[1], g_hln[2], g_hln[3], dW_z, db_z, dWa, g_ln[0], g_ln[1], g_ln[2], g_ln[3], None)
-
-
-def hyper_sequence_hip(p, x, h0, c0, hh0, hc0, forget_bias=1.0, drop_keep=1.0, drop_seed=0, drop_stream=0,
-                       hyp_drop_keep=1.0, zc=None):
-    if not p.use_layer_norm:
-        raise NotImplementedError("HIP HyperLSTM path requires use_layer_norm=True")
-    outs = _HyperSeq.apply(x, zc, h0, c0, hh0, hc0, drop_seed, p.W_x, p.W_h, p.bias, p.hyp_W_x, p.hyp_W_h,
-                           p.hyp_ln_gamma, p.hyp_ln_beta, p.hyp_lnc_gamma, p.hyp_lnc_beta, p.W_z, p.b_z, p.W_a,
-                           p.ln_gamma, p.ln_beta, p.lnc_gamma, p.lnc_beta,
-                           (float(forget_bias), float(drop_keep), float(hyp_drop_keep), int(drop_stream), p.embed,
-                            _inference(x, zc, h0, p.W_h, p.W_x)))
-    Hout, hT, cT, hhT, hcT = outs
-    return Hout, (hT, cT, hhT, hcT)
+    return LN_SAVES_LP and not infer and gemm.lp_dtype() == torch.bfloat16

@@ -21,7 +21,9 @@ import numpy as np
 
 LIB_DIR = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "_lib")
 HOST_LIB = os.path.join(LIB_DIR, "libskrnn_host.so")
-HIP_LIB = os.path.join(LIB_DIR, "libskrnn_hip.so")
+# SKR_HIP_LIB: load another build of the kernel library (A/B experiments,
+# e.g. scripts/build_native.py --variant exact_act)
+HIP_LIB = os.environ.get("SKR_HIP_LIB") or os.path.join(LIB_DIR, "libskrnn_hip.so")
 
 _host = None
 _hip = None

@@ -270,7 +270,7 @@ def test_hyper_mod_path_vs_oracle(B, keep, hkeep):
     statistics exchange) is as close to the fp32 oracle as the plain chain
     (bf16-output modulation GEMM + in-launch exchange): per output / gradient,
     error(fused) <= 1.5 error(plain) + 1e-3 of the largest element."""
-    from sketch_rnn_amd.ops import recurrent
+    from sketch_rnn_amd.ops import hyper as recurrent
     p, x, z, st, w = _hyper_setup(6, 7, B, 5, 16, 2048, 256, 32, jitter=0.02, state=0.1)
     runs = {}
     try:
@@ -782,7 +782,7 @@ def test_hyper_fold_kernels_vs_torch(Hh, H, E):
     """csrc/hyper_fold.hip: P = W_z W_a per block in both bf16 layouts, q, qb,
     and the projection gradients, against the fp32 torch products (the
     headline shape, and E < 32 with its zero-padded LDS tile)."""
-    from sketch_rnn_amd.ops import recurrent
+    from sketch_rnn_amd.ops import hyper
     from sketch_rnn_amd.utils import native
     torch.manual_seed(0)
     Wz = torch.randn(Hh, 12 * E, device=DEV) * 0.2
@@ -812,7 +812,7 @@ def test_hyper_fold_kernels_vs_torch(Hh, H, E):
         pass
     s = S()
     s.W_z, s.b_z, s.W_a = Wz, bz, Wa
-    got = recurrent._hyper_proj_grads(dP, sV, s, Hh, H, E)
+    got = hyper._hyper_proj_grads(dP, sV, s, Hh, H, E)
     dPv = dP.view(Hh, 12, H).transpose(0, 1)
     Wz3 = Wz.view(Hh, 12, E).transpose(0, 1)
     ref = (torch.bmm(dPv, Wa.transpose(1, 2)).transpose(0, 1).reshape(Hh, 12 * E),
