@@ -1,7 +1,5 @@
-// Forward cell step of the LSTM-family cell kernels as a device function,
-// shared by the per-step cell launch (csrc/lstm_cell.hip: workgroup (c, b) =
-// (blockIdx.x, blockIdx.y)) and the grouped GEMM launch that runs the
-// HyperLSTM's hyper cell in its tail (csrc/skinny_gemm.hip, hyper_fused).
+// Forward cell step of the LSTM-family cell kernels as a device function
+// (csrc/lstm_cell.hip: workgroup (c, b) = (blockIdx.x, blockIdx.y)).
 // Semantics and geometry: csrc/lstm_cell.hip header comment.
 #pragma once
 #include "lstm_args.h"

@@ -15,8 +15,9 @@
 // (csrc/cell_fwd_body.h, MOD 3) sums them while loading -- one exchange per
 // step fewer -- and reads the finished g (32 KB per row) instead of x-proj,
 // the R slabs and the modulation vectors (144 KB per row).
-// The saves the backward needs are written here too: vec (bf16, q folded in:
-// the backward cell runs with a zero vec_bias) and the bf16 summed R.
+// The saves the backward needs are written here too: the x and h blocks of
+// vec (bf16, q folded in: the backward cell runs with a zero vec_bias) and
+// the bf16 summed R.
 //
 // Tiling: workgroup (gate q, 32-unit tile u0) -> 4 x 64 = 256 workgroups of
 // 384 threads. Wave w owns MFMA column tile w: k-block q + 4 (w / 2) (x, h,
@@ -151,7 +152,8 @@ __global__ __launch_bounds__(NTH) void hyper_mod_fwd(const __hip_bfloat16* __res
             const int64_t vo = (int64_t)rr * NV + u0 + ul;
             *(u32x2*)(vec + vo + q * H) = u32x2{pack_bf(vx[0], vx[1]), pack_bf(vx[2], vx[3])};
             *(u32x2*)(vec + vo + (4 + q) * H) = u32x2{pack_bf(vh[0], vh[1]), pack_bf(vh[2], vh[3])};
-            *(u32x2*)(vec + vo + (8 + q) * H) = u32x2{pack_bf(vb[0], vb[1]), pack_bf(vb[2], vb[3])};
+            // (the shift block 8..11 is not stored: the backward reads only
+            // the x and h modulations -- d(shift) = dg needs no saved value)
             if (ug == 0) {
                 float* sp = stats + (((int64_t)rr * 4 + q) * ntile + blockIdx.x) * 2;
                 sp[0] = s1;
@@ -165,7 +167,7 @@ __global__ __launch_bounds__(NTH) void hyper_mod_fwd(const __hip_bfloat16* __res
 
 // hh [B][Hh] bf16 rows (stride ld_hh), PlT [12H][Hh] bf16, qb [12H] fp32
 // (q, with the main bias added to blocks 8..11), xh [B][4H] fp32, R = sum of
-// nslab fp32 slabs [B][4H] (stride r_slab), outputs vec [B][12H] bf16,
+// nslab fp32 slabs [B][4H] (stride r_slab), outputs vec [B][12H] bf16 (blocks 0..7 written),
 // g [B][4H] fp32, rlp [B][4H] bf16 (or null), stats [B][4][H/32][2] fp32.
 SKR_API int skr_hyper_mod_fwd(const void* hh, int64_t ld_hh, const void* PlT, const float* qb, const float* xh,
                               const float* R, int64_t r_slab, int nslab, void* vec, float* g, void* rlp,

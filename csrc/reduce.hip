@@ -103,7 +103,29 @@ __global__ __launch_bounds__(256) void colsum_kernel(const void* __restrict__ X,
     }
 }
 
+// Second pass: out[c] = sum over the RS row-slice partials, in slice order
+// (deterministic). out_xy null when there is no Y.
+__global__ __launch_bounds__(256) void colsum_finish(const float* __restrict__ part_xy, const float* __restrict__ part_x,
+                                                     int RS, int C, float* __restrict__ out_xy,
+                                                     float* __restrict__ out_x) {
+    const int c = blockIdx.x * 256 + threadIdx.x;
+    if (c >= C) return;
+    float sx = 0.f, sxy = 0.f;
+    for (int r = 0; r < RS; ++r) {
+        sx += part_x[(int64_t)r * C + c];
+        if (out_xy) sxy += part_xy[(int64_t)r * C + c];
+    }
+    out_x[c] = sx;
+    if (out_xy) out_xy[c] = sxy;
+}
+
 }  // namespace
+
+// Both passes: partials into part_* ([RS][C] each), then the column totals
+// into out_xy / out_x (out_xy ignored without Y).
+SKR_API int skr_colsum2(const void* X, int x_kind, const void* Y, int y_kind, int64_t R1, int64_t s1, int64_t R2,
+                        int64_t s2, int C, int RS, float* part_xy, float* part_x, float* out_xy, float* out_x,
+                        hipStream_t s);
 
 // x_kind / y_kind: 1 bf16, 2 fp32. Y (same strides) may be null (then part_xy unused).
 // Four columns per thread when C, the strides and the bases allow 8-byte
@@ -129,5 +151,43 @@ SKR_API int skr_colsum(const void* X, int x_kind, const void* Y, int y_kind, int
         else SKR_CS(false, false, 1);
     }
 #undef SKR_CS
+    return SKR_CHECK_LAUNCH();
+}
+
+SKR_API int skr_colsum2(const void* X, int x_kind, const void* Y, int y_kind, int64_t R1, int64_t s1, int64_t R2,
+                        int64_t s2, int C, int RS, float* part_xy, float* part_x, float* out_xy, float* out_x,
+                        hipStream_t s) {
+    const int rc = skr_colsum(X, x_kind, Y, y_kind, R1, s1, R2, s2, C, RS, part_xy, part_x, s);
+    if (rc != 0) return rc;
+    hipLaunchKernelGGL(colsum_finish, dim3((C + 255) / 256), dim3(256), 0, s, part_xy, part_x, RS, C,
+                       Y ? out_xy : nullptr, out_x);
+    return SKR_CHECK_LAUNCH();
+}
+
+// out[r][c] = sum_s a[s*a_slab + r*a_ld + c] + sum_s b[s*b_slab + r*b_ld + c]
+// (b may be null): the gradient into a recurrence's initial state from the
+// split-K dh slabs of its first step (HyperLSTM: the d[h | hh] and dR_main
+// slabs), in slab order. One launch instead of a reduction per source + add.
+namespace {
+__global__ __launch_bounds__(256) void slab_sum2_kernel(const float* __restrict__ a, int na, int64_t a_slab, int64_t a_ld,
+                                                        const float* __restrict__ b, int nb, int64_t b_slab, int64_t b_ld,
+                                                        int rows, int cols, float* __restrict__ out) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= (int64_t)rows * cols) return;
+    const int r = (int)(i / cols), c = (int)(i - (int64_t)r * cols);
+    float v = 0.f;
+    for (int s = 0; s < na; ++s) v += a[s * a_slab + r * a_ld + c];
+    for (int s = 0; s < nb; ++s) v += b[s * b_slab + r * b_ld + c];
+    out[i] = v;
+}
+}  // namespace
+
+SKR_API int skr_slab_sum2(const float* a, int na, int64_t a_slab, int64_t a_ld, const float* b, int nb, int64_t b_slab,
+                          int64_t b_ld, int rows, int cols, float* out, hipStream_t s) {
+    if (rows <= 0 || cols <= 0) return 0;
+    if (a == nullptr || na < 1 || (b == nullptr && nb > 0)) return -2;
+    const int64_t n = (int64_t)rows * cols;
+    hipLaunchKernelGGL(slab_sum2_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, a, na, a_slab, a_ld,
+                       b, b ? nb : 0, b_slab, b_ld, rows, cols, out);
     return SKR_CHECK_LAUNCH();
 }

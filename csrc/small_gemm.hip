@@ -1,0 +1,132 @@
+// Small fp32 GEMMs of the VAE's per-sequence layers: the latent heads
+// (mu / presig = h W + b), the decoder's initial state (z W_init + b), the
+// z part of the decoder input projections (z W_x[z rows]) and their
+// gradients. Every one has a batch-sized dimension (B = 100) and another of
+// at most a few thousand: 0.1-100 MFLOP each, too small for MFMA tiling to
+// matter and too odd-shaped (K = 100 contractions, transposed operands) for
+// the skinny / wgrad kernels. One generic kernel with arbitrary operand
+// strides (so transposes are views, never copies) and a deterministic
+// split-K (fixed-order two-pass sum) replaces the ~15 library GEMM calls
+// per vae_large training step.
+//
+//   C[m, n] = (acc ? C[m, n] : 0) + bias[n] + sum_k A[m*sam + k*sak] * B[k*sbk + n*sbn]
+//
+// Tile: 64 x 64 outputs per workgroup (256 threads, 4 x 4 per thread at
+// rows ty + 16 i, columns tx + 16 j), K staged through LDS 32 at a time.
+// Split-K: S > 1 slices write fp32 partials to work[S][M][N]; a second
+// launch sums them in slice order (+ bias, + C if acc).
+#include "common.h"
+
+namespace {
+
+constexpr int TM = 64, TN = 64, TK = 32, NT = 256;
+
+__global__ __launch_bounds__(NT) void small_gemm_kernel(const float* __restrict__ A, int64_t sam, int64_t sak,
+                                                        const float* __restrict__ B, int64_t sbk, int64_t sbn,
+                                                        float* __restrict__ C, int64_t ldc, const float* __restrict__ bias,
+                                                        int M, int N, int K, int kslice, int acc,
+                                                        float* __restrict__ work) {
+    __shared__ float As[TK][TM + 1];
+    __shared__ float Bs[TK][TN + 1];
+    const int tid = threadIdx.x, tx = tid & 15, ty = tid >> 4;
+    const int m0 = blockIdx.y * TM, n0 = blockIdx.x * TN, s = blockIdx.z;
+    const int k0 = s * kslice, k1 = min(K, k0 + kslice);
+    float c[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) c[i][j] = 0.f;
+    // loader mapping: 256 threads x 8 elements per operand tile; the fastest
+    // thread index runs along the operand's unit-stride axis when it has one
+    const bool a_krow = sak == 1;   // A rows are K-contiguous
+    const bool b_ncol = sbn == 1;   // B rows are N-contiguous
+    for (int kb = k0; kb < k1; kb += TK) {
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+            const int e = tid + r * NT;   // 0 .. 2047
+            const int mm = a_krow ? e / TK : e % TM, kk = a_krow ? e % TK : e / TM;
+            const int gm = m0 + mm, gk = kb + kk;
+            As[kk][mm] = (gm < M && gk < k1) ? A[gm * sam + gk * sak] : 0.f;
+            const int nn = b_ncol ? e % TN : e / TK, kq = b_ncol ? e / TN : e % TK;
+            const int gn = n0 + nn, gq = kb + kq;
+            Bs[kq][nn] = (gn < N && gq < k1) ? B[gq * sbk + gn * sbn] : 0.f;
+        }
+        __syncthreads();
+#pragma unroll 8
+        for (int kk = 0; kk < TK; ++kk) {
+            float a[4], b[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) a[i] = As[kk][ty + 16 * i];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) b[j] = Bs[kk][tx + 16 * j];
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) c[i][j] += a[i] * b[j];
+        }
+        __syncthreads();
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int m = m0 + ty + 16 * i;
+        if (m >= M) continue;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int n = n0 + tx + 16 * j;
+            if (n >= N) continue;
+            if (work != nullptr) {
+                work[((int64_t)s * M + m) * N + n] = c[i][j];
+            } else {
+                float v = c[i][j] + (bias ? bias[n] : 0.f);
+                if (acc) v += C[m * ldc + n];
+                C[m * ldc + n] = v;
+            }
+        }
+    }
+}
+
+__global__ void small_gemm_reduce(const float* __restrict__ work, int S, int M, int N, float* __restrict__ C,
+                                  int64_t ldc, const float* __restrict__ bias, int acc) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (int64_t)M * N) return;
+    const int m = (int)(i / N), n = (int)(i - (int64_t)m * N);
+    float v = 0.f;
+    for (int s = 0; s < S; ++s) v += work[(int64_t)s * M * N + i];
+    v += bias ? bias[n] : 0.f;
+    if (acc) v += C[m * ldc + n];
+    C[m * ldc + n] = v;
+}
+
+}  // namespace
+
+// Split-K factor the launcher uses for an (M, N, K) problem (the Python side
+// sizes the workspace with it): ~256 workgroups, K slices of >= 64.
+SKR_API int skr_small_gemm_splits(int M, int N, int K) {
+    if (M <= 0 || N <= 0 || K <= 0) return 1;
+    const int tiles = ((M + TM - 1) / TM) * ((N + TN - 1) / TN);
+    int S = 256 / tiles;
+    S = S < 1 ? 1 : S;
+    const int maxS = (K + 63) / 64;
+    return S < maxS ? S : maxS;
+}
+
+SKR_API int skr_small_gemm(const float* A, int64_t sam, int64_t sak, const float* B, int64_t sbk, int64_t sbn,
+                           float* C, int64_t ldc, const float* bias, int M, int N, int K, int acc, float* work,
+                           int64_t work_elems, hipStream_t s) {
+    if (M <= 0 || N <= 0) return 0;
+    if (K <= 0) return -2;
+    int S = skr_small_gemm_splits(M, N, K);
+    int kslice = (K + S - 1) / S;
+    kslice = (kslice + TK - 1) / TK * TK;
+    S = (K + kslice - 1) / kslice;
+    if (S > 1 && (work == nullptr || work_elems < (int64_t)S * M * N)) return -3;
+    const dim3 grid((N + TN - 1) / TN, (M + TM - 1) / TM, S);
+    hipLaunchKernelGGL(small_gemm_kernel, grid, dim3(NT), 0, s, A, sam, sak, B, sbk, sbn, C, ldc, bias, M, N, K,
+                       kslice, acc, S > 1 ? work : nullptr);
+    if (S > 1) {
+        const int64_t n = (int64_t)M * N;
+        hipLaunchKernelGGL(small_gemm_reduce, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, work, S, M, N, C,
+                           ldc, bias, acc);
+    }
+    return SKR_CHECK_LAUNCH();
+}

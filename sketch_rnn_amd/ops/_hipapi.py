@@ -288,6 +288,14 @@ class HipLib:
         lib.skr_row_bwd_step.restype = _i
         lib.skr_row_supported.argtypes = [_i]
         lib.skr_row_supported.restype = _i
+        lib.skr_colsum2.argtypes = [_p, _i, _p, _i, _i64, _i64, _i64, _i64, _i, _i, _p, _p, _p, _p, _p]
+        lib.skr_colsum2.restype = _i
+        lib.skr_slab_sum2.argtypes = [_p, _i, _i64, _i64, _p, _i, _i64, _i64, _i, _i, _p, _p]
+        lib.skr_slab_sum2.restype = _i
+        lib.skr_small_gemm_splits.argtypes = [_i, _i, _i]
+        lib.skr_small_gemm_splits.restype = _i
+        lib.skr_small_gemm.argtypes = [_p, _i64, _i64, _p, _i64, _i64, _p, _i64, _p, _i, _i, _i, _i, _p, _i64, _p]
+        lib.skr_small_gemm.restype = _i
         lib.skr_mdn_loss.argtypes = [_p, _i64, _p, _i64, _i64, _i, _i, _f, _i, _f, _p, _p, _p, _p]
         lib.skr_mdn_loss.restype = _i
         lib.skr_adam_step.argtypes = [_p, _p, _p, _p, _p, _p, _i64, _f, _f, _f, _i, _f, _i, _p]

@@ -38,6 +38,43 @@ def mm(a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor] = None) -> 
     return torch.mm(a, b, out_dtype=torch.float32)
 
 
+def small_mm(a: torch.Tensor, b: torch.Tensor, bias: Optional[torch.Tensor] = None,
+             out: Optional[torch.Tensor] = None, acc: bool = False) -> torch.Tensor:
+    """fp32 ``a @ b (+ bias) (+ out if acc)`` for the small per-sequence
+    products (latent heads, initial state, z projections and their grads):
+    ``csrc/small_gemm.hip`` on the GPU -- operands may be transposed views
+    (arbitrary strides, no copies), deterministic split-K -- and torch
+    elsewhere. ``out`` needs unit column stride."""
+    M, K = a.shape
+    N = b.shape[1]
+    if not a.is_cuda:
+        y = a @ b
+        if bias is not None:
+            y = y + bias
+        if out is None:
+            return y
+        if acc:
+            out += y
+        else:
+            out.copy_(y)
+        return out
+    from ..utils import native
+    lib = native.require_hip().lib
+    assert a.dtype == b.dtype == torch.float32 and b.shape[0] == K
+    if out is None:
+        out = torch.empty(M, N, device=a.device)
+    assert out.stride(1) == 1 and out.shape == (M, N)
+    S = lib.skr_small_gemm_splits(M, N, K)
+    work = torch.empty(S * M * N if S > 1 else 1, device=a.device)
+    bc = bias.contiguous() if bias is not None else None
+    rc = lib.skr_small_gemm(a.data_ptr(), a.stride(0), a.stride(1), b.data_ptr(), b.stride(0), b.stride(1),
+                            out.data_ptr(), out.stride(0), bc.data_ptr() if bc is not None else None, M, N, K,
+                            int(acc), work.data_ptr(), work.numel(), torch.cuda.current_stream().cuda_stream)
+    if rc != 0:
+        raise RuntimeError("skr_small_gemm failed (%d) for M=%d N=%d K=%d" % (rc, M, N, K))
+    return out
+
+
 def bmm(a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
     if a.dtype == torch.float32 and b.dtype == torch.float32:
         return torch.bmm(a, b, out=out) if out is not None else torch.bmm(a, b)

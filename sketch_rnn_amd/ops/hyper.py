@@ -100,8 +100,8 @@ class _HyperSeq(torch.autograd.Function):
         bp = bproj_ok(x) and not x.requires_grad
         xl = None
         if bp:   # stroke rows per position, z rows once per sequence (csrc/inproj.hip)
-            XH = bproj_fwd(x, W_x[:IX], zc @ W_x[IX:] if zc is not None else None)
-            XHY = bproj_fwd(x, hW_x[:IX], zc @ hW_x[IX:IN] if zc is not None else None)
+            XH = bproj_fwd(x, W_x[:IX], gemm.small_mm(zc, W_x[IX:]) if zc is not None else None)
+            XHY = bproj_fwd(x, hW_x[:IX], gemm.small_mm(zc, hW_x[IX:IN]) if zc is not None else None)
         else:
             if zc is not None:
                 x = torch.cat([x, zc.unsqueeze(0).expand(T, B, zc.shape[-1])], -1)
@@ -325,8 +325,12 @@ class _HyperSeq(torch.autograd.Function):
             S_ay = next(d for d in (4, 3, 2, 1) if (Gh // 64) % d == 0)
         S_ay = _split_override("SKR_HYP_SAY", S_ay, Gh)
         DHZ = torch.empty(max(S_h, 1), B, Hh, device=dev, dtype=f32)    # slabs of dhh from the vec path
-        DAM = torch.zeros(max(S_am, 1), B, H, device=dev, dtype=f32)    # slabs of dh from the main gates
-        DAY = torch.zeros(max(S_ay, 1), B, K, device=dev, dtype=f32)    # slabs of d[h | hh] from the hyper gates
+        # dh slabs of step t + 1 read by step t; the last step reads none (null
+        # sources) unless gradients flow into the final states
+        fin = dhT is not None or dhhT is not None
+        alloc = torch.zeros if (fin or T == 0) else torch.empty
+        DAM = alloc(max(S_am, 1), B, H, device=dev, dtype=f32)    # slabs of dh from the main gates
+        DAY = alloc(max(S_ay, 1), B, K, device=dev, dtype=f32)    # slabs of d[h | hh] from the hyper gates
         if dhT is not None:
             DAY[0, :, :H].copy_(dhT)
         if dhhT is not None:
@@ -363,9 +367,14 @@ class _HyperSeq(torch.autograd.Function):
         clm, clh = _ClusterSync(T, B, H, dev), _ClusterSync(T, B, Hh, dev)
         st = _stream()
         group = lp_on and gemm.GROUPED and S_am >= 1 and S_h >= 1
+        first = not fin   # (the last time step runs first)
         for t in range(T - 1, -1, -1):
             clm.set(am, t)
             clh.set(ah, t)
+            if t == T - 1 or t == T - 2:   # null dh sources on the first backward step only
+                am.dh_rec = None if (first and t == T - 1) else DAY.data_ptr()
+                am.dh_rec2 = None if (first and t == T - 1) else DAM.data_ptr()
+                ah.dh_rec = None if (first and t == T - 1) else DAY[0, :, H:].data_ptr()
             am.dh_out = dHout[t].data_ptr() if dHout is not None else None
             am.c_prev = s.CC[t].data_ptr()
             am.xhat, am.rstd, am.chat = s.XHAT[t].data_ptr(), s.RSTD[t].data_ptr(), s.CHAT[t].data_ptr()
@@ -393,8 +402,16 @@ class _HyperSeq(torch.autograd.Function):
             ah.dlny, ah.dlncy = HDLNY[t].data_ptr(), HDLNCY[t].data_ptr()
             _cell_bwd(lib, ah, True, 0, st, "hyper_bwd_step")
             gemm.rec_gemm(dRY_lp[t], s.Wyl, DAY, S_ay)
-        dh0 = DAY[:, :, :H].sum(0) + DAM.sum(0)
-        dhh0 = DAY[:, :, H:].sum(0)
+        if not DAY.is_cuda:
+            dh0 = DAY[:, :, :H].sum(0) + DAM.sum(0)
+            dhh0 = DAY[:, :, H:].sum(0)
+        else:   # the initial-state gradients from step 0's dh slabs, one launch each (csrc/reduce.hip)
+            dh0 = torch.empty(B, H, device=dev, dtype=f32)
+            dhh0 = torch.empty(B, Hh, device=dev, dtype=f32)
+            _check(lib.lib.skr_slab_sum2(DAY.data_ptr(), DAY.shape[0], B * K, K, DAM.data_ptr(), DAM.shape[0], B * H, H,
+                                         B, H, dh0.data_ptr(), st), "slab_sum2 dh0")
+            _check(lib.lib.skr_slab_sum2(DAY[0, :, H:].data_ptr(), DAY.shape[0], B * K, K, None, 0, 0, 0, B, Hh,
+                                         dhh0.data_ptr(), st), "slab_sum2 dhh0")
         # weight / LayerNorm-parameter gradients: long-K products over the T*B saved rows
         A2 = s.A[:T].reshape(TB, K)
         # hyper-norm projections, vec_k = (hh @ W_z_k + b_z_k) @ W_a_k: ONE long-K
@@ -418,9 +435,13 @@ class _HyperSeq(torch.autograd.Function):
             S_m, P_m = bproj_reduce(s.x, dXH)
             S_y, P_y = bproj_reduce(s.x, dRY_lp)
             if s.zc is not None:
-                dW_x = torch.cat([P_m, s.zc.t() @ S_m], 0)
-                dhW_x[:IN] = torch.cat([P_y, s.zc.t() @ S_y], 0)
-                dzc = S_m @ s.W_x[IX:].t() + S_y @ s.hW_x[IX:IN].t()
+                dW_x = torch.empty_like(s.W_x)
+                dW_x[:IX] = P_m
+                gemm.small_mm(s.zc.t(), S_m, out=dW_x[IX:])
+                dhW_x[:IX] = P_y
+                gemm.small_mm(s.zc.t(), S_y, out=dhW_x[IX:IN])
+                dzc = gemm.small_mm(S_m, s.W_x[IX:].t())
+                gemm.small_mm(S_y, s.hW_x[IX:IN].t(), out=dzc, acc=True)
             else:
                 dW_x = P_m
                 dhW_x[:IN] = P_y

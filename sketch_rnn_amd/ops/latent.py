@@ -9,8 +9,8 @@
 
 returns ``(mu, presig, z, kl, *segments)``. Reference semantics: the magenta
 sketch_rnn encoder head / reparameterisation / KL and the decoder's initial
-state (our torch form: models/vae.py ``SketchVAE.loss``). The three GEMMs are
-library GEMMs with their bias fused; everything between them is two small
+state (our torch form: models/vae.py ``SketchVAE.loss``). The three GEMMs and
+their gradients run on csrc/small_gemm.hip (bias fused); everything between them is two small
 kernels forward and two backward instead of ~35 elementwise launches.
 """
 from __future__ import annotations
@@ -21,6 +21,8 @@ from typing import Optional, Sequence
 import torch
 
 from ..utils import native
+from .gemm import small_mm
+from .reduce import colsum
 
 
 def latent_ok(h: torch.Tensor, n_seg: int) -> bool:
@@ -40,8 +42,8 @@ class _Latent(torch.autograd.Function):
         lib = native.require_hip().lib
         st = torch.cuda.current_stream().cuda_stream
         h = h.contiguous()
-        mu = torch.addmm(b_mu, h, w_mu)
-        ps = torch.addmm(b_sig, h, w_sig)
+        mu = small_mm(h, w_mu, b_mu)
+        ps = small_mm(h, w_sig, b_sig)
         B, Z = mu.shape
         dev = h.device
         z = torch.empty(B, Z, device=dev)
@@ -54,7 +56,7 @@ class _Latent(torch.autograd.Function):
                                 kl_raw.data_ptr(), kl.data_ptr(), st)
         if rc != 0:
             raise RuntimeError("skr_latent_mid failed (%d)" % rc)
-        pre = torch.addmm(b_init, z, w_init)
+        pre = small_mm(z, w_init, b_init)
         S = pre.shape[1]
         segs = [torch.empty(B, w, device=dev) for w in widths]
         wa = (ctypes.c_int * len(widths))(*widths)
@@ -80,9 +82,9 @@ class _Latent(torch.autograd.Function):
         rc = lib.skr_tanh_split_bwd(B, S, len(widths), wa, _ptrs(segs), _ptrs(dsegs), dpre.data_ptr(), st)
         if rc != 0:
             raise RuntimeError("skr_tanh_split_bwd failed (%d)" % rc)
-        dW_init = z.t() @ dpre
-        db_init = dpre.sum(0)
-        dz_int = dpre @ w_init.t()
+        dW_init = small_mm(z.t(), dpre)
+        db_init = colsum(dpre)[1]
+        dz_int = small_mm(dpre, w_init.t())
         dmu_t = torch.empty(B, Z, device=dev)
         dps_t = torch.empty(B, Z, device=dev)
         c = lambda t: t.contiguous() if t is not None else None   # noqa: E731
@@ -93,10 +95,11 @@ class _Latent(torch.autograd.Function):
                                     dps_t.data_ptr(), st)
         if rc != 0:
             raise RuntimeError("skr_latent_mid_bwd failed (%d)" % rc)
-        dh = torch.addmm(dmu_t @ w_mu.t(), dps_t, w_sig.t())
-        dW_mu = h.t() @ dmu_t
-        dW_sig = h.t() @ dps_t
-        return dh, dW_mu, dmu_t.sum(0), dW_sig, dps_t.sum(0), dW_init, db_init, None, None, None
+        dh = small_mm(dmu_t, w_mu.t())
+        small_mm(dps_t, w_sig.t(), out=dh, acc=True)
+        dW_mu = small_mm(h.t(), dmu_t)
+        dW_sig = small_mm(h.t(), dps_t)
+        return dh, dW_mu, colsum(dmu_t)[1], dW_sig, colsum(dps_t)[1], dW_init, db_init, None, None, None
 
 
 def latent(h, w_mu, b_mu, w_sig, b_sig, w_init, b_init, seed: torch.Tensor, widths: Sequence[int],

@@ -35,15 +35,14 @@ def colsum(x: torch.Tensor, y: Optional[torch.Tensor] = None, splits: Optional[i
         splits = -(-1024 // -(-C // (1024 if C % 4 == 0 else 256)))
     RS = max(1, min(splits, (R1 * R2) // 16))
     part = torch.empty(2, RS, C, device=x.device, dtype=torch.float32)
+    tot = torch.empty(2, C, device=x.device, dtype=torch.float32)
     kind = 1 if x.dtype == torch.bfloat16 else 2
     assert x.dtype in (torch.bfloat16, torch.float32)
     ykind = 1 if (y is not None and y.dtype == torch.bfloat16) else 2
-    rc = lib.lib.skr_colsum(x.data_ptr(), kind, y.data_ptr() if y is not None else None, ykind, R1, x.stride(0), R2,
-                            x.stride(1), C, RS, part[0].data_ptr(), part[1].data_ptr(),
-                            torch.cuda.current_stream().cuda_stream)
+    # both passes in HIP: row-slice partials, then the fixed-order column totals
+    rc = lib.lib.skr_colsum2(x.data_ptr(), kind, y.data_ptr() if y is not None else None, ykind, R1, x.stride(0), R2,
+                             x.stride(1), C, RS, part[0].data_ptr(), part[1].data_ptr(), tot[0].data_ptr(),
+                             tot[1].data_ptr(), torch.cuda.current_stream().cuda_stream)
     if rc != 0:
         raise RuntimeError("skr_colsum failed (%d)" % rc)
-    if y is None:
-        return None, part[1].sum(0)
-    tot = part.sum(1)   # both second passes in one reduction launch
-    return tot[0], tot[1]
+    return (tot[0] if y is not None else None), tot[1]

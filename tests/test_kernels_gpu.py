@@ -821,3 +821,26 @@ def test_hyper_fold_kernels_vs_torch(Hh, H, E):
            sV[8 * H:])
     for a, b in zip(got, ref):
         assert torch.allclose(a, b, rtol=1e-4, atol=1e-3 * float(b.abs().max())), float((a - b).abs().max())
+
+
+@pytest.mark.parametrize("M,N,K,ta,tb,bias,acc", [(100, 128, 1024, False, False, True, False),
+                                                  (100, 4608, 128, False, False, True, False),
+                                                  (128, 4608, 100, True, False, False, False),
+                                                  (100, 128, 8192, False, True, False, True),
+                                                  (1024, 128, 100, True, False, False, False),
+                                                  (37, 70, 45, True, True, True, True)])
+def test_small_gemm_matches_torch(M, N, K, ta, tb, bias, acc):
+    """csrc/small_gemm.hip (the latent / initial-state / z-projection
+    products and their gradients): transposed views, bias, accumulate and
+    split-K against the fp32 torch product."""
+    from sketch_rnn_amd.ops import gemm
+    torch.manual_seed(0)
+    a = torch.randn(K, M, device=DEV).t() if ta else torch.randn(M, K, device=DEV)
+    b = torch.randn(N, K, device=DEV).t() if tb else torch.randn(K, N, device=DEV)
+    bv = torch.randn(N, device=DEV) if bias else None
+    base = torch.randn(M, N, device=DEV)
+    out = base.clone()
+    gemm.small_mm(a, b, bv, out=out, acc=acc)
+    ref = (a.double() @ b.double()) + (bv.double() if bias else 0) + (base.double() if acc else 0)
+    err = (out.double() - ref).abs().max().item()
+    assert err <= 1e-4 * max(ref.abs().max().item(), 1.0) * math.sqrt(K / 64), err
