@@ -10,7 +10,9 @@
 // backward dvec @ P^T, P^T [12H, Hh] for the forward hh @ P), q (fp32) and
 // qb = q + the main bias on the shift block -- one launch instead of a
 // batched library GEMM, a permute copy, a cast-transpose and the bias add.
-// Backward, from dP = hh^T dvec [Hh, 12H] and sV = colsum(dvec) [12H]:
+// Backward, from dP = hh^T dvec [Hh, 12H] and sV = colsum(dvec) [12H]
+// (ops/hyper.py _hyper_proj_grads, batched strided products on
+// csrc/small_gemm.hip):
 //   dW_a[j][e][u] = sum_k W_z[k][jE+e] dP[k][jH+u] + b_z[jE+e] sV[jH+u]
 //   dW_z[k][jE+e] = sum_u dP[k][jH+u] W_a[j][e][u]
 //   db_z[jE+e]    = sum_u sV[jH+u] W_a[j][e][u]
@@ -64,87 +66,6 @@ __global__ __launch_bounds__(NTH) void hyper_fold(const float* __restrict__ Wz, 
     }
 }
 
-// dW_a: grid (12H / 64); block = 64 columns (j, u) x 4 waves, wave w sums
-// k in [w Hh / 4, (w + 1) Hh / 4) with E accumulators per lane; the four
-// partials are added in a fixed order through LDS (deterministic)
-__global__ __launch_bounds__(NTH) void hyper_fold_dwa(const float* __restrict__ dP, const float* __restrict__ sV,
-                                                      const float* __restrict__ Wz, const float* __restrict__ bz,
-                                                      int Hh, int H, int E, float* __restrict__ dWa) {
-    __shared__ float part[4][MAXE][65];
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, NC = 12 * H;
-    const int c = blockIdx.x * 64 + lane;
-    const int j = (blockIdx.x * 64) / H, u = c - j * H;
-    const int kq = Hh / 4, k0 = w * kq;
-    float acc[MAXE];
-#pragma unroll
-    for (int e = 0; e < MAXE; ++e) acc[e] = 0.f;
-    const float* wz = Wz + j * E;
-#pragma unroll 4
-    for (int k = k0; k < k0 + kq; ++k) {
-        const float d = dP[(int64_t)k * NC + c];
-        const float* wr = wz + (int64_t)k * 12 * E;   // wave-uniform row: scalar loads
-#pragma unroll
-        for (int e = 0; e < MAXE; ++e)
-            if (e < E) acc[e] += wr[e] * d;
-    }
-#pragma unroll
-    for (int e = 0; e < MAXE; ++e) part[w][e][lane] = acc[e];
-    __syncthreads();
-    if (w != 0) return;
-    const float sv = sV[c];
-    for (int e = 0; e < E; ++e) {
-        const float v = ((part[0][e][lane] + part[1][e][lane]) + part[2][e][lane]) + part[3][e][lane];
-        dWa[((int64_t)j * E + e) * H + u] = v + bz[j * E + e] * sv;
-    }
-}
-
-// dW_z and db_z: grid (12, Hh / KT + 1); block (j, kt) reduces over u in
-// 256-wide chunks staged in LDS; thread (k, e) of the KT x E tile (the last
-// y-block computes db_z from sV)
-__global__ __launch_bounds__(NTH) void hyper_fold_dwz(const float* __restrict__ dP, const float* __restrict__ sV,
-                                                      const float* __restrict__ Wa, int Hh, int H, int E,
-                                                      float* __restrict__ dWz, float* __restrict__ dbz) {
-    __shared__ float wa[MAXE][NTH + 1];
-    __shared__ float dp[KT][NTH + 1];
-    const int tid = threadIdx.x, j = blockIdx.x, NC = 12 * H;
-    const bool brow = blockIdx.y * KT >= Hh;           // the db_z block
-    const int k0 = blockIdx.y * KT;
-    const int rows = brow ? 1 : KT;
-    const int k = tid / MAXE, e = tid % MAXE;          // 8 x 32 thread tile: k < 8, two passes
-    float acc[2] = {0.f, 0.f};
-    for (int u0 = 0; u0 < H; u0 += NTH) {
-        __syncthreads();
-        for (int i = tid; i < E * NTH; i += NTH) {
-            const int ee = i / NTH, uu = i - ee * NTH;
-            wa[ee][uu] = Wa[((int64_t)j * E + ee) * H + u0 + uu];
-        }
-        for (int i = tid; i < rows * NTH; i += NTH) {
-            const int kk = i / NTH, uu = i - kk * NTH;
-            dp[kk][uu] = brow ? sV[j * H + u0 + uu] : dP[(int64_t)(k0 + kk) * NC + j * H + u0 + uu];
-        }
-        __syncthreads();
-        if (e < E) {
-#pragma unroll
-            for (int p = 0; p < 2; ++p) {
-                const int kk = k + 8 * p;
-                if (kk < rows) {
-                    float s = 0.f;
-                    for (int uu = 0; uu < NTH; ++uu) s += dp[kk][uu] * wa[e][uu];
-                    acc[p] += s;
-                }
-            }
-        }
-    }
-    if (e >= E) return;
-#pragma unroll
-    for (int p = 0; p < 2; ++p) {
-        const int kk = k + 8 * p;
-        if (kk >= rows) continue;
-        if (brow) dbz[j * E + e] = acc[p];
-        else dWz[(int64_t)(k0 + kk) * 12 * E + j * E + e] = acc[p];
-    }
-}
-
 }  // namespace
 
 // W_z [Hh, 12E], b_z [12E], W_a [12, E, H] fp32; bias [4H] or null (qb shift term);
@@ -155,15 +76,5 @@ SKR_API int skr_hyper_fold(const float* Wz, const float* bz, const float* Wa, co
     if (((uintptr_t)PT & 15) || (Hh % 8)) return -4;
     hipLaunchKernelGGL(hyper_fold, dim3(12 * H / NTH, Hh / KT), dim3(NTH), 0, s, Wz, bz, Wa, bias, Hh, H, E,
                        (__hip_bfloat16*)P, (__hip_bfloat16*)PT, q, qb);
-    return SKR_CHECK_LAUNCH();
-}
-
-// dP [Hh, 12H], sV [12H] fp32 -> dW_z [Hh, 12E], db_z [12E], dW_a [12, E, H]
-SKR_API int skr_hyper_fold_bwd(const float* dP, const float* sV, const float* Wz, const float* bz, const float* Wa,
-                               int Hh, int H, int E, float* dWz, float* dbz, float* dWa, hipStream_t s) {
-    if (H % NTH || Hh % KT || E < 1 || E > MAXE) return -2;
-    if (Hh % 4) return -2;
-    hipLaunchKernelGGL(hyper_fold_dwa, dim3(12 * H / 64), dim3(NTH), 0, s, dP, sV, Wz, bz, Hh, H, E, dWa);
-    hipLaunchKernelGGL(hyper_fold_dwz, dim3(12, Hh / KT + 1), dim3(NTH), 0, s, dP, sV, Wa, Hh, H, E, dWz, dbz);
     return SKR_CHECK_LAUNCH();
 }

@@ -25,11 +25,16 @@ __global__ __launch_bounds__(NT) void small_gemm_kernel(const float* __restrict_
                                                         const float* __restrict__ B, int64_t sbk, int64_t sbn,
                                                         float* __restrict__ C, int64_t ldc, const float* __restrict__ bias,
                                                         int M, int N, int K, int kslice, int acc,
-                                                        float* __restrict__ work) {
+                                                        float* __restrict__ work, int S, int64_t a_batch,
+                                                        int64_t b_batch, int64_t c_batch) {
     __shared__ float As[TK][TM + 1];
     __shared__ float Bs[TK][TN + 1];
     const int tid = threadIdx.x, tx = tid & 15, ty = tid >> 4;
-    const int m0 = blockIdx.y * TM, n0 = blockIdx.x * TN, s = blockIdx.z;
+    const int m0 = blockIdx.y * TM, n0 = blockIdx.x * TN, s = blockIdx.z % S, bt = blockIdx.z / S;
+    A += bt * a_batch;
+    B += bt * b_batch;
+    C += bt * c_batch;
+    if (work != nullptr) work += (int64_t)bt * S * M * N;
     const int k0 = s * kslice, k1 = min(K, k0 + kslice);
     float c[4][4];
 #pragma unroll
@@ -86,9 +91,11 @@ __global__ __launch_bounds__(NT) void small_gemm_kernel(const float* __restrict_
 }
 
 __global__ void small_gemm_reduce(const float* __restrict__ work, int S, int M, int N, float* __restrict__ C,
-                                  int64_t ldc, const float* __restrict__ bias, int acc) {
+                                  int64_t ldc, const float* __restrict__ bias, int acc, int64_t c_batch) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= (int64_t)M * N) return;
+    work += (int64_t)blockIdx.y * S * M * N;
+    C += blockIdx.y * c_batch;
     const int m = (int)(i / N), n = (int)(i - (int64_t)m * N);
     float v = 0.f;
     for (int s = 0; s < S; ++s) v += work[(int64_t)s * M * N + i];
@@ -110,23 +117,34 @@ SKR_API int skr_small_gemm_splits(int M, int N, int K) {
     return S < maxS ? S : maxS;
 }
 
-SKR_API int skr_small_gemm(const float* A, int64_t sam, int64_t sak, const float* B, int64_t sbk, int64_t sbn,
-                           float* C, int64_t ldc, const float* bias, int M, int N, int K, int acc, float* work,
-                           int64_t work_elems, hipStream_t s) {
-    if (M <= 0 || N <= 0) return 0;
+// nbatch independent problems of the same shape: operand / output bases
+// advance by a_batch / b_batch / c_batch elements (a shared bias); workspace
+// nbatch * S * M * N floats when S > 1.
+SKR_API int skr_small_gemm_batched(const float* A, int64_t a_batch, int64_t sam, int64_t sak, const float* B,
+                                   int64_t b_batch, int64_t sbk, int64_t sbn, float* C, int64_t c_batch, int64_t ldc,
+                                   const float* bias, int M, int N, int K, int acc, int nbatch, float* work,
+                                   int64_t work_elems, hipStream_t s) {
+    if (M <= 0 || N <= 0 || nbatch <= 0) return 0;
     if (K <= 0) return -2;
     int S = skr_small_gemm_splits(M, N, K);
     int kslice = (K + S - 1) / S;
     kslice = (kslice + TK - 1) / TK * TK;
     S = (K + kslice - 1) / kslice;
-    if (S > 1 && (work == nullptr || work_elems < (int64_t)S * M * N)) return -3;
-    const dim3 grid((N + TN - 1) / TN, (M + TM - 1) / TM, S);
+    if (S > 1 && (work == nullptr || work_elems < (int64_t)nbatch * S * M * N)) return -3;
+    const dim3 grid((N + TN - 1) / TN, (M + TM - 1) / TM, S * nbatch);
     hipLaunchKernelGGL(small_gemm_kernel, grid, dim3(NT), 0, s, A, sam, sak, B, sbk, sbn, C, ldc, bias, M, N, K,
-                       kslice, acc, S > 1 ? work : nullptr);
+                       kslice, acc, S > 1 ? work : nullptr, S, a_batch, b_batch, c_batch);
     if (S > 1) {
         const int64_t n = (int64_t)M * N;
-        hipLaunchKernelGGL(small_gemm_reduce, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, work, S, M, N, C,
-                           ldc, bias, acc);
+        hipLaunchKernelGGL(small_gemm_reduce, dim3((unsigned)((n + 255) / 256), nbatch), dim3(256), 0, s, work, S,
+                           M, N, C, ldc, bias, acc, c_batch);
     }
     return SKR_CHECK_LAUNCH();
+}
+
+SKR_API int skr_small_gemm(const float* A, int64_t sam, int64_t sak, const float* B, int64_t sbk, int64_t sbn,
+                           float* C, int64_t ldc, const float* bias, int M, int N, int K, int acc, float* work,
+                           int64_t work_elems, hipStream_t s) {
+    return skr_small_gemm_batched(A, 0, sam, sak, B, 0, sbk, sbn, C, 0, ldc, bias, M, N, K, acc, 1, work, work_elems,
+                                  s);
 }

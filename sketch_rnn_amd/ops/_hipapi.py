@@ -292,6 +292,9 @@ class HipLib:
         lib.skr_colsum2.restype = _i
         lib.skr_slab_sum2.argtypes = [_p, _i, _i64, _i64, _p, _i, _i64, _i64, _i, _i, _p, _p]
         lib.skr_slab_sum2.restype = _i
+        lib.skr_small_gemm_batched.argtypes = [_p, _i64, _i64, _i64, _p, _i64, _i64, _i64, _p, _i64, _i64, _p, _i, _i,
+                                               _i, _i, _i, _p, _i64, _p]
+        lib.skr_small_gemm_batched.restype = _i
         lib.skr_small_gemm_splits.argtypes = [_i, _i, _i]
         lib.skr_small_gemm_splits.restype = _i
         lib.skr_small_gemm.argtypes = [_p, _i64, _i64, _p, _i64, _i64, _p, _i64, _p, _i, _i, _i, _i, _p, _i64, _p]
@@ -337,8 +340,6 @@ class HipLib:
         lib.skr_tanh_split_bwd.restype = _i
         lib.skr_hyper_fold.argtypes = [_p, _p, _p, _p, _i, _i, _i, _p, _p, _p, _p, _p]
         lib.skr_hyper_fold.restype = _i
-        lib.skr_hyper_fold_bwd.argtypes = [_p, _p, _p, _p, _p, _i, _i, _i, _p, _p, _p, _p]
-        lib.skr_hyper_fold_bwd.restype = _i
         lib.skr_occupancy_hog.argtypes = [_i, _i, _i, _i, _p, _p]
         lib.skr_occupancy_hog.restype = _i
         lib.skr_gru_fwd.argtypes = [C.POINTER(GruFwdArgs), _i, _p]

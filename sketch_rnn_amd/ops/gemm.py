@@ -75,6 +75,27 @@ def small_mm(a: torch.Tensor, b: torch.Tensor, bias: Optional[torch.Tensor] = No
     return out
 
 
+def small_mm_batched(a: torch.Tensor, a_off: int, a_batch: int, sam: int, sak: int,
+                     b: torch.Tensor, b_off: int, b_batch: int, sbk: int, sbn: int,
+                     c: torch.Tensor, c_off: int, c_batch: int, ldc: int,
+                     M: int, N: int, K: int, nbatch: int, acc: bool = False) -> None:
+    """``nbatch`` fp32 products on raw element strides (``csrc/small_gemm.hip``):
+    for batch i, ``C_i[m, n] (+)= sum_k A_i[m*sam + k*sak] B_i[k*sbk + n*sbn]``
+    with ``A_i = a + a_off + i*a_batch`` (likewise B, C). Used where the
+    operands are blocks of one buffer that no single view describes (the
+    per-block hyper-projection gradients)."""
+    from ..utils import native
+    lib = native.require_hip().lib
+    assert a.dtype == b.dtype == c.dtype == torch.float32
+    S = lib.skr_small_gemm_splits(M, N, K)
+    work = torch.empty(nbatch * S * M * N if S > 1 else 1, device=c.device)
+    rc = lib.skr_small_gemm_batched(a.data_ptr() + 4 * a_off, a_batch, sam, sak, b.data_ptr() + 4 * b_off, b_batch,
+                                    sbk, sbn, c.data_ptr() + 4 * c_off, c_batch, ldc, None, M, N, K, int(acc), nbatch,
+                                    work.data_ptr(), work.numel(), torch.cuda.current_stream().cuda_stream)
+    if rc != 0:
+        raise RuntimeError("skr_small_gemm_batched failed (%d) for M=%d N=%d K=%d x%d" % (rc, M, N, K, nbatch))
+
+
 def bmm(a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
     if a.dtype == torch.float32 and b.dtype == torch.float32:
         return torch.bmm(a, b, out=out) if out is not None else torch.bmm(a, b)

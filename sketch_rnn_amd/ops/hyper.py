@@ -49,16 +49,20 @@ def _fold_ok(H: int, Hh: int, E: int) -> bool:
 def _hyper_proj_grads(dP1, sV, s, Hh, H, E):
     """Hyper-norm projection gradients from ``dP1 = hh^T dvec`` and the
     column sums ``sV`` of dvec."""
-    if dP1.is_cuda and _fold_ok(H, Hh, E):   # three small reductions, two launches (csrc/hyper_fold.hip)
-        lib = native.require_hip()
+    if dP1.is_cuda:   # per-block products as batched strided GEMMs over the 12 blocks (csrc/small_gemm.hip)
         dev = dP1.device
+        dP1, sV = dP1.contiguous(), sV.contiguous()
+        Wz, bz, Wa = (t.detach().contiguous() for t in (s.W_z, s.b_z, s.W_a))
+        NC = 12 * H
         dW_z = torch.empty(Hh, 12 * E, device=dev)
         db_z = torch.empty(12 * E, device=dev)
         dWa = torch.empty(12, E, H, device=dev)
-        _check(lib.lib.skr_hyper_fold_bwd(dP1.contiguous().data_ptr(), sV.contiguous().data_ptr(),
-                                          s.W_z.detach().contiguous().data_ptr(), s.b_z.detach().contiguous().data_ptr(),
-                                          s.W_a.detach().contiguous().data_ptr(), Hh, H, E, dW_z.data_ptr(),
-                                          db_z.data_ptr(), dWa.data_ptr(), _stream()), "hyper_fold_bwd")
+        # dW_a[j] = W_z[:, jE:(j+1)E]^T dP[:, jH:(j+1)H] + b_z[jE:(j+1)E] (x) sV[jH:(j+1)H]
+        gemm.small_mm_batched(bz, 0, E, 1, 0, sV, 0, H, 0, 1, dWa, 0, E * H, H, E, H, 1, 12)
+        gemm.small_mm_batched(Wz, 0, E, 1, 12 * E, dP1, 0, H, NC, 1, dWa, 0, E * H, H, E, H, Hh, 12, acc=True)
+        # dW_z[:, jE:(j+1)E] = dP[:, jH:(j+1)H] W_a[j]^T;  db_z[jE:(j+1)E] = sV[jH:(j+1)H] W_a[j]^T
+        gemm.small_mm_batched(dP1, 0, H, NC, 1, Wa, 0, E * H, 1, H, dW_z, 0, E, 12 * E, Hh, E, H, 12)
+        gemm.small_mm_batched(sV, 0, H, 0, 1, Wa, 0, E * H, 1, H, db_z, 0, E, 0, 1, E, H, 12)
         return dW_z, db_z, dWa, sV[8 * H:].reshape(4 * H)
     dP = dP1.view(Hh, 12, H).transpose(0, 1)                       # [12, Hh, H]
     sV = sV.view(12, H)
