@@ -274,14 +274,14 @@ KernelT<FwdArgs> pick(bool ln, int mod, const FwdArgs*) {
     if (ln) return cell_fwd<NT, UPT, NS, true, 0>;
     return cell_fwd<NT, UPT, NS, false, 0>;
 }
-// dh_out slab ceiling of a backward step for the unrolled loads: 1, 8, 32,
+// dh_out slab ceiling of a backward step for the unrolled loads: 1, 8, 32, 64,
 // or 0 (runtime loops) when a source does not fit the ceilings
 inline int dh_ceiling(const BwdArgs& a) {
     if ((a.dh_rec && (a.dhr_nslab < 1 || a.dhr_nslab > kRecSlabs)) ||
         (a.dh_rec2 && (a.dhr2_nslab < 1 || a.dhr2_nslab > kRecSlabs)))
         return 0;
     const int n = a.dh_out ? a.dho_nslab : 1;
-    return n == 1 ? 1 : (n >= 2 && n <= 8) ? 8 : (n > 8 && n <= 32) ? 32 : 0;
+    return n == 1 ? 1 : (n >= 2 && n <= 8) ? 8 : (n > 8 && n <= 32) ? 32 : (n > 32 && n <= 64) ? 64 : 0;
 }
 
 template <int NT, int UPT, int NS, int MOD>
@@ -290,6 +290,7 @@ KernelT<BwdArgs> pick_dh(int d) {
         case 1: return cell_bwd<NT, UPT, NS, true, MOD, 1>;
         case 8: return cell_bwd<NT, UPT, NS, true, MOD, 8>;
         case 32: return cell_bwd<NT, UPT, NS, true, MOD, 32>;
+        case 64: return cell_bwd<NT, UPT, NS, true, MOD, 64>;
         default: return cell_bwd<NT, UPT, NS, true, MOD, 0>;
     }
 }

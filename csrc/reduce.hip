@@ -103,20 +103,38 @@ __global__ __launch_bounds__(256) void colsum_kernel(const void* __restrict__ X,
     }
 }
 
-// Second pass: out[c] = sum over the RS row-slice partials, in slice order
-// (deterministic). out_xy null when there is no Y.
+// Second pass: out[c] = sum over the RS row-slice partials (out_xy null when
+// there is no Y). Workgroup = 64 columns x 4 waves; wave w sums slices
+// w, w + 4, ... eight loads in flight at a time, then the four wave sums are
+// added in wave order -- deterministic.
 __global__ __launch_bounds__(256) void colsum_finish(const float* __restrict__ part_xy, const float* __restrict__ part_x,
                                                      int RS, int C, float* __restrict__ out_xy,
                                                      float* __restrict__ out_x) {
-    const int c = blockIdx.x * 256 + threadIdx.x;
-    if (c >= C) return;
+    __shared__ float red[2][4][64];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int c = blockIdx.x * 64 + lane, cc = min(c, C - 1);
     float sx = 0.f, sxy = 0.f;
-    for (int r = 0; r < RS; ++r) {
-        sx += part_x[(int64_t)r * C + c];
-        if (out_xy) sxy += part_xy[(int64_t)r * C + c];
+    for (int r0 = w; r0 < RS; r0 += 32) {
+        float tx[8], txy[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const int r = min(r0 + 4 * k, RS - 1);
+            tx[k] = part_x[(int64_t)r * C + cc];
+            txy[k] = out_xy ? part_xy[(int64_t)r * C + cc] : 0.f;
+        }
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const bool on = r0 + 4 * k < RS;
+            sx += on ? tx[k] : 0.f;
+            sxy += on ? txy[k] : 0.f;
+        }
     }
-    out_x[c] = sx;
-    if (out_xy) out_xy[c] = sxy;
+    red[0][w][lane] = sx;
+    red[1][w][lane] = sxy;
+    __syncthreads();
+    if (w != 0 || c >= C) return;
+    out_x[c] = ((red[0][0][lane] + red[0][1][lane]) + red[0][2][lane]) + red[0][3][lane];
+    if (out_xy) out_xy[c] = ((red[1][0][lane] + red[1][1][lane]) + red[1][2][lane]) + red[1][3][lane];
 }
 
 }  // namespace
@@ -159,7 +177,7 @@ SKR_API int skr_colsum2(const void* X, int x_kind, const void* Y, int y_kind, in
                         hipStream_t s) {
     const int rc = skr_colsum(X, x_kind, Y, y_kind, R1, s1, R2, s2, C, RS, part_xy, part_x, s);
     if (rc != 0) return rc;
-    hipLaunchKernelGGL(colsum_finish, dim3((C + 255) / 256), dim3(256), 0, s, part_xy, part_x, RS, C,
+    hipLaunchKernelGGL(colsum_finish, dim3((C + 63) / 64), dim3(256), 0, s, part_xy, part_x, RS, C,
                        Y ? out_xy : nullptr, out_x);
     return SKR_CHECK_LAUNCH();
 }

@@ -11,8 +11,10 @@
 //
 //   C[m, n] = (acc ? C[m, n] : 0) + bias[n] + sum_k A[m*sam + k*sak] * B[k*sbk + n*sbn]
 //
-// Tile: 64 x 64 outputs per workgroup (256 threads, 4 x 4 per thread at
-// rows ty + 16 i, columns tx + 16 j), K staged through LDS 32 at a time.
+// Tile: 64 x 64 outputs per workgroup (256 threads, a 4 x 4 block each:
+// rows 4 ty .., columns 4 tx .., one 16-byte LDS read per operand per k), K
+// staged through LDS 32 at a time with the next chunk's global loads in
+// flight (registers) during the current chunk's math.
 // Split-K: S > 1 slices write fp32 partials to work[S][M][N]; a second
 // launch sums them in slice order (+ bias, + C if acc).
 #include "common.h"
@@ -27,8 +29,10 @@ __global__ __launch_bounds__(NT) void small_gemm_kernel(const float* __restrict_
                                                         int M, int N, int K, int kslice, int acc,
                                                         float* __restrict__ work, int S, int64_t a_batch,
                                                         int64_t b_batch, int64_t c_batch) {
-    __shared__ float As[TK][TM + 1];
-    __shared__ float Bs[TK][TN + 1];
+    // LDS rows padded to 68 floats: 16-byte aligned, so a thread's 4 rows /
+    // 4 columns are one ds_read_b128 each
+    __shared__ __attribute__((aligned(16))) float As[TK][TM + 4];
+    __shared__ __attribute__((aligned(16))) float Bs[TK][TN + 4];
     const int tid = threadIdx.x, tx = tid & 15, ty = tid >> 4;
     const int m0 = blockIdx.y * TM, n0 = blockIdx.x * TN, s = blockIdx.z % S, bt = blockIdx.z / S;
     A += bt * a_batch;
@@ -45,25 +49,39 @@ __global__ __launch_bounds__(NT) void small_gemm_kernel(const float* __restrict_
     // thread index runs along the operand's unit-stride axis when it has one
     const bool a_krow = sak == 1;   // A rows are K-contiguous
     const bool b_ncol = sbn == 1;   // B rows are N-contiguous
-    for (int kb = k0; kb < k1; kb += TK) {
+    float ra[8], rb[8];
+    auto load = [&](int kb) {   // next K chunk into registers (in flight during the current chunk's math)
 #pragma unroll
         for (int r = 0; r < 8; ++r) {
             const int e = tid + r * NT;   // 0 .. 2047
             const int mm = a_krow ? e / TK : e % TM, kk = a_krow ? e % TK : e / TM;
             const int gm = m0 + mm, gk = kb + kk;
-            As[kk][mm] = (gm < M && gk < k1) ? A[gm * sam + gk * sak] : 0.f;
+            ra[r] = (gm < M && gk < k1) ? A[gm * sam + gk * sak] : 0.f;
             const int nn = b_ncol ? e % TN : e / TK, kq = b_ncol ? e / TN : e % TK;
             const int gn = n0 + nn, gq = kb + kq;
-            Bs[kq][nn] = (gn < N && gq < k1) ? B[gq * sbk + gn * sbn] : 0.f;
+            rb[r] = (gn < N && gq < k1) ? B[gq * sbk + gn * sbn] : 0.f;
         }
+    };
+    auto stash = [&]() {
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+            const int e = tid + r * NT;
+            const int mm = a_krow ? e / TK : e % TM, kk = a_krow ? e % TK : e / TM;
+            As[kk][mm] = ra[r];
+            const int nn = b_ncol ? e % TN : e / TK, kq = b_ncol ? e / TN : e % TK;
+            Bs[kq][nn] = rb[r];
+        }
+    };
+    if (k0 < k1) load(k0);
+    for (int kb = k0; kb < k1; kb += TK) {
+        stash();
         __syncthreads();
+        if (kb + TK < k1) load(kb + TK);
 #pragma unroll 8
         for (int kk = 0; kk < TK; ++kk) {
-            float a[4], b[4];
-#pragma unroll
-            for (int i = 0; i < 4; ++i) a[i] = As[kk][ty + 16 * i];
-#pragma unroll
-            for (int j = 0; j < 4; ++j) b[j] = Bs[kk][tx + 16 * j];
+            const float4 a4 = *(const float4*)&As[kk][4 * ty];
+            const float4 b4 = *(const float4*)&Bs[kk][4 * tx];
+            const float a[4] = {a4.x, a4.y, a4.z, a4.w}, b[4] = {b4.x, b4.y, b4.z, b4.w};
 #pragma unroll
             for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -73,11 +91,11 @@ __global__ __launch_bounds__(NT) void small_gemm_kernel(const float* __restrict_
     }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-        const int m = m0 + ty + 16 * i;
+        const int m = m0 + 4 * ty + i;
         if (m >= M) continue;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-            const int n = n0 + tx + 16 * j;
+            const int n = n0 + 4 * tx + j;
             if (n >= N) continue;
             if (work != nullptr) {
                 work[((int64_t)s * M + m) * N + n] = c[i][j];
