@@ -22,6 +22,7 @@
 #include <cstdlib>
 
 #include "common.h"
+#include "cell_bwd_body.h"
 
 namespace {
 
@@ -191,9 +192,7 @@ struct GemmGroup {
 };
 
 template <int BN, int NS>
-__global__ __launch_bounds__(256) void skinny_gemm_group_kernel(const GemmGroup g) {
-    extern __shared__ __attribute__((aligned(16))) __hip_bfloat16 smem[];
-    const int id = blockIdx.x;
+__device__ __forceinline__ void group_tile(const GemmGroup& g, const int id, __hip_bfloat16* smem) {
     int q = 0;
 #pragma unroll
     for (int i = 1; i < kMaxGroup; ++i) q += (i < g.n && id >= g.start[i]) ? 1 : 0;
@@ -204,6 +203,29 @@ __global__ __launch_bounds__(256) void skinny_gemm_group_kernel(const GemmGroup 
     const int kslice = p.K / p.splits;
     glds_tile<BN, NS>((const __hip_bfloat16*)p.A, p.lda, (const __hip_bfloat16*)p.Bt, p.ldb, p.C + split * p.c_slab,
                       p.ldc, p.M, nt * BN, (int64_t)split * kslice, kslice, smem);
+}
+
+template <int BN, int NS>
+__global__ __launch_bounds__(256) void skinny_gemm_group_kernel(const GemmGroup g) {
+    extern __shared__ __attribute__((aligned(16))) __hip_bfloat16 smem[];
+    group_tile<BN, NS>(g, blockIdx.x, smem);
+}
+
+// Grouped GEMM tiles + the rows of one backward LayerNorm cell step in ONE
+// launch: workgroups [0, B) run the cell rows (one workgroup per row, 256
+// threads, one unit per thread: H <= 256), the rest the GEMM tiles. The
+// HyperLSTM backward runs its hyper cell -- which needs only the dvec P^T
+// slabs of this step -- beside dR_main W_h^T, which only the next step's
+// main cell reads: the 100-CU cell step hides under the weight stream
+// instead of being its own launch on the critical path.
+template <int BN, int NS, int DHS>
+__global__ __launch_bounds__(256) void skinny_gemm_group_cellbwd_kernel(const GemmGroup g, const skr::BwdArgs cell) {
+    extern __shared__ __attribute__((aligned(16))) __hip_bfloat16 smem[];
+    if ((int)blockIdx.x < cell.B) {
+        cell_bwd_body<256, 1, 1, true, 0, DHS>(cell, 0, blockIdx.x, 1);
+        return;
+    }
+    group_tile<BN, NS>(g, blockIdx.x - cell.B, smem);
 }
 
 // ---------------------------------------------------------------------------
@@ -627,6 +649,48 @@ SKR_API int skr_skinny_gemm_group(const GemmProblem* probs, int n, int bn, hipSt
     if (bn == 128) return g_nstage == 3 ? launch_group<128, 3>(g, s) : launch_group<128, 4>(g, s);
     return g_nstage == 3 ? launch_group<64, 3>(g, s) : g_nstage == 6 ? launch_group<64, 6>(g, s)
                                                                     : launch_group<64, 4>(g, s);
+}
+
+// skr_skinny_gemm_group (64-wide tiles, 3-stage ring) plus one backward
+// LayerNorm cell step (lstm_cell.hip semantics, mod 0, one workgroup per
+// row: H <= 256, no cluster, no resets) in the same launch.
+SKR_API int skr_skinny_gemm_group_cellbwd(const GemmProblem* probs, int n, const skr::BwdArgs* cell, hipStream_t s) {
+    if (n < 1 || n > kMaxGroup || cell == nullptr) return -2;
+    const skr::BwdArgs& a = *cell;
+    if (a.H < 1 || a.H > 256 || a.cluster > 1 || a.reset != nullptr || a.B < 1) return -2;
+    if ((a.dh_rec && (a.dhr_nslab < 1 || a.dhr_nslab > kRecSlabs)) ||
+        (a.dh_rec2 && (a.dhr2_nslab < 1 || a.dhr2_nslab > kRecSlabs)))
+        return -3;
+    const int no = a.dh_out ? a.dho_nslab : 1;
+    const int dhs = no == 1 ? 1 : no <= 8 ? 8 : no <= 32 ? 32 : no <= 64 ? 64 : 0;
+    if (dhs == 0) return -3;
+    GemmGroup g{};
+    g.n = n;
+    g.start[0] = 0;
+    for (int i = 0; i < n; ++i) {
+        const GemmProblem& p = probs[i];
+        if (p.M < 1 || p.M > BM || p.N % 64 != 0 || p.splits < 1 || p.K % p.splits != 0) return -2;
+        if ((p.K / p.splits) % BK != 0 || p.lda % 8 != 0 || p.ldb % 8 != 0) return -3;
+        if (((uintptr_t)p.A | (uintptr_t)p.Bt) & 15) return -4;
+        g.p[i] = p;
+        g.start[i + 1] = g.start[i] + (p.N / 64) * p.splits;
+    }
+    for (int i = n + 1; i <= kMaxGroup; ++i) g.start[i] = g.start[n];
+    const size_t lds = (size_t)3 * (BM + 64) * BK * 2;
+    const dim3 grid(a.B + g.start[n]);
+#define SKR_GC(D)                                                                                           \
+    do {                                                                                                    \
+        set_lds_attr(skinny_gemm_group_cellbwd_kernel<64, 3, D>, lds);                                      \
+        hipLaunchKernelGGL((skinny_gemm_group_cellbwd_kernel<64, 3, D>), grid, dim3(256), lds, s, g, a);    \
+    } while (0)
+    switch (dhs) {
+        case 1: SKR_GC(1); break;
+        case 8: SKR_GC(8); break;
+        case 32: SKR_GC(32); break;
+        default: SKR_GC(64); break;
+    }
+#undef SKR_GC
+    return SKR_CHECK_LAUNCH();
 }
 
 // fp32 operands: same contract as skr_skinny_gemm_v2 with kslice % 32 == 0

@@ -353,6 +353,8 @@ class HipLib:
         lib.skr_gemm_set_nstage.restype = _i
         lib.skr_skinny_gemm_group.argtypes = [C.POINTER(GemmProblem), _i, _i, _p]
         lib.skr_skinny_gemm_group.restype = _i
+        lib.skr_skinny_gemm_group_cellbwd.argtypes = [C.POINTER(GemmProblem), _i, C.POINTER(LstmBwdArgs), _p]
+        lib.skr_skinny_gemm_group_cellbwd.restype = _i
         lib.skr_lstm_fused_fwd.argtypes = [C.POINTER(FusedFwdArgs), _p]
         lib.skr_lstm_fused_fwd.restype = _i
         lib.skr_lstm_fused_bwd.argtypes = [C.POINTER(FusedBwdArgs), _p]

@@ -324,6 +324,33 @@ def rec_gemm_group(jobs) -> None:
         raise RuntimeError("skr_skinny_gemm_group failed (%d)" % rc)
 
 
+def _problems(jobs):
+    from ._hipapi import GemmProblem
+    probs = (GemmProblem * len(jobs))()
+    for p, (a, bt, out, s) in zip(probs, jobs):
+        assert a.is_cuda and a.dtype == _BF16 and s >= 1 and a.shape[0] <= 128
+        N, K = bt.shape[-2], bt.shape[-1]
+        p.A, p.lda, p.Bt, p.ldb = a.data_ptr(), a.stride(0), bt.data_ptr(), bt.stride(-2)
+        p.C, p.ldc, p.c_slab = out.data_ptr(), N, out.stride(0)
+        p.M, p.N, p.K, p.splits = a.shape[0], N, K, s
+    return probs
+
+
+def rec_gemm_group_cellbwd(jobs, cell_args) -> None:
+    """:func:`rec_gemm_group` products plus one backward LayerNorm cell step
+    (``cell_args``: a filled ``LstmBwdArgs``, one workgroup per row, H <= 256)
+    in ONE launch (``skr_skinny_gemm_group_cellbwd``): the cell rows run
+    beside the GEMM tiles."""
+    import ctypes
+    from ..utils import native
+    lib = native.require_hip()
+    probs = _problems(jobs)
+    rc = lib.lib.skr_skinny_gemm_group_cellbwd(probs, len(jobs), ctypes.byref(cell_args),
+                                               torch.cuda.current_stream().cuda_stream)
+    if rc != 0:
+        raise RuntimeError("skr_skinny_gemm_group_cellbwd failed (%d)" % rc)
+
+
 # ---- inference-time helpers ------------------------------------------------------------
 _WCACHE = {}
 WEIGHTS_EPOCH = [0]

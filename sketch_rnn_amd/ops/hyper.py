@@ -23,8 +23,8 @@ from ..utils import native
 from . import gemm
 from ._hipapi import LstmBwdArgs, LstmFwdArgs
 from .inproj import bproj_fwd, bproj_ok, bproj_reduce
-from .recurrent import (_cell_bwd, _cell_fwd, _check, _ClusterSync, _fp8_ok, _inference, _ln_saves_lp, _lp_kind,
-                        _ptr, _Saved, _seed_tensor, _stream, _to_fp8_act)
+from .recurrent import (ROW_STATS, _cell_bwd, _cell_fwd, _check, _ClusterSync, _fp8_ok, _inference, _ln_saves_lp,
+                        _lp_kind, _ptr, _Saved, _seed_tensor, _stream, _to_fp8_act, cell_geometry)
 from .reduce import colsum
 
 # The modulation GEMM fused with the main gates' pre-activations and
@@ -32,6 +32,15 @@ from .reduce import colsum
 # plain bf16-output GEMM + the main cell's in-launch statistics exchange.
 HYPER_MOD = os.environ.get("SKR_HYPER_MOD", "1") != "0"
 HYPER_MAIN_C = int(os.environ.get("SKR_HYPER_MAIN_C", "0"))   # workgroups per row of the MOD-3 main cell (0: policy)
+# Backward step as [main cell] -> [dvec P^T] -> [hyper cell + dR_main W_h^T in
+# one launch, csrc/skinny_gemm.hip skr_skinny_gemm_group_cellbwd] -> [dR_hyp
+# W_y^T]: the hyper cell (one workgroup per row) runs beside the tiles of the
+# product only the next step reads. SKR_HYPER_BWD_FUSE=0 keeps [main cell] ->
+# [dR_main W_h^T + dvec P^T] -> [hyper cell] -> [dR_hyp W_y^T].
+HYPER_BWD_FUSE = os.environ.get("SKR_HYPER_BWD_FUSE", "1") != "0"
+# (The forward twin -- h W_y alone, then the hyper cell beside h W_h in one
+# launch -- measured 0.15 ms/step slower on vae_large and was removed:
+# profiles/r3/hyper_fused_cell_ab.txt.)
 
 
 def _split_override(var: str, planned: int, K: int) -> int:
@@ -319,7 +328,12 @@ class _HyperSeq(torch.autograd.Function):
         HDLNY = torch.empty(T, B, Gh, device=dev, dtype=sdt)
         HDLNCY = torch.empty(T, B, Hh, device=dev, dtype=sdt)
         dVEC = torch.empty(T, B, 12 * H, device=dev, dtype=ldt)
-        S_h = _split_override("SKR_HYP_SH", gemm.plan_splits(B, Hh, 12 * H, 1, ldt), 12 * H)
+        clh_C = cell_geometry(Hh, B, True) if lp_on else 0
+        bfuse = HYPER_BWD_FUSE and lp_on and dev.type == "cuda" and Hh <= 256 and clh_C == 1 and \
+            gemm.plan_splits(B, H, G, 1, ldt) >= 1
+        # dvec P^T alone in the fused order: 64 splits fill the chip (24576 = 64 x 384)
+        S_h0 = 64 if (bfuse and (12 * H) % (64 * 64) == 0) else gemm.plan_splits(B, Hh, 12 * H, 1, ldt)
+        S_h = _split_override("SKR_HYP_SH", S_h0, 12 * H)
         S_am = _split_override("SKR_HYP_SAM", gemm.plan_splits(B, H, G, 1, ldt), G)
         # d[h | hh] = dR_hyp @ W_y^T: at most 4 split-K slabs -- the next step's
         # two cells read every slab; measured on MI355X (vae_large, same box,
@@ -393,18 +407,23 @@ class _HyperSeq(torch.autograd.Function):
             am.dxp, am.dvec = dXH[t].data_ptr(), dVEC[t].data_ptr()
             am.dlny, am.dlncy = DLNY[t].data_ptr(), DLNCY[t].data_ptr()
             _cell_bwd(lib, am, True, 2 if s.VEC.dtype == torch.bfloat16 else 1, st, "hyper_main_bwd_step")
-            if group:   # dR_main @ W_h^T and dvec @ P^T in one launch
-                gemm.rec_gemm_group([(dRM_lp[t], s.Whl, DAM, S_am), (dVEC[t], s.Pl, DHZ, S_h)])
-            else:
-                gemm.rec_gemm(dRM_lp[t], s.Whl, DAM, S_am)
-                gemm.rec_gemm(dVEC[t], s.Pl, DHZ, S_h)
             ah.c_prev = s.HCC[t].data_ptr()
             ah.xhat, ah.rstd, ah.chat = s.HXHAT[t].data_ptr(), s.HRSTD[t].data_ptr(), s.HCHAT[t].data_ptr()
             ah.step = t
             ah.dG = None if lp_on else dRY[t].data_ptr()
             ah.dG_lp = dRY_lp[t].data_ptr() if lp_on else None
             ah.dlny, ah.dlncy = HDLNY[t].data_ptr(), HDLNCY[t].data_ptr()
-            _cell_bwd(lib, ah, True, 0, st, "hyper_bwd_step")
+            if bfuse:   # dvec P^T, then the hyper cell beside dR_main W_h^T (one launch)
+                gemm.rec_gemm(dVEC[t], s.Pl, DHZ, S_h)
+                gemm.rec_gemm_group_cellbwd([(dRM_lp[t], s.Whl, DAM, S_am)], ah)
+                ROW_STATS["cluster"] += 1   # (the clustered cell body, C = 1)
+            else:
+                if group:   # dR_main @ W_h^T and dvec @ P^T in one launch
+                    gemm.rec_gemm_group([(dRM_lp[t], s.Whl, DAM, S_am), (dVEC[t], s.Pl, DHZ, S_h)])
+                else:
+                    gemm.rec_gemm(dRM_lp[t], s.Whl, DAM, S_am)
+                    gemm.rec_gemm(dVEC[t], s.Pl, DHZ, S_h)
+                _cell_bwd(lib, ah, True, 0, st, "hyper_bwd_step")
             gemm.rec_gemm(dRY_lp[t], s.Wyl, DAY, S_ay)
         if not DAY.is_cuda:
             dh0 = DAY[:, :, :H].sum(0) + DAM.sum(0)

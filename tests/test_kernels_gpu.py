@@ -844,3 +844,26 @@ def test_small_gemm_matches_torch(M, N, K, ta, tb, bias, acc):
     ref = (a.double() @ b.double()) + (bv.double() if bias else 0) + (base.double() if acc else 0)
     err = (out.double() - ref).abs().max().item()
     assert err <= 1e-4 * max(ref.abs().max().item(), 1.0) * math.sqrt(K / 64), err
+
+
+def test_hyper_backward_fused_cell_launch_bitwise(monkeypatch):
+    """The backward order [main cell] -> [dvec P^T] -> [hyper cell + dR_main
+    W_h^T in one launch] -> [dR_hyp W_y^T] (skr_skinny_gemm_group_cellbwd)
+    equals the unfused order bit for bit at equal split counts, and stays as
+    close to the fp32 oracle as the bf16 tolerance test requires."""
+    from sketch_rnn_amd.ops import hyper
+    monkeypatch.setenv("SKR_HYP_SH", "64")
+    p, x, z, st, w = _hyper_setup(4, 6, 100, 5, 16, 2048, 256, 32, jitter=0.02, state=0.1)
+    ops.set_compute_dtype("bf16")
+    ops.set_backend("hip")
+    res = []
+    saved = hyper.HYPER_BWD_FUSE
+    try:
+        for fuse in (True, False):
+            hyper.HYPER_BWD_FUSE = fuse
+            res.append(_hyper_run(p, x, z, st, w))
+    finally:
+        hyper.HYPER_BWD_FUSE = saved
+    for n, a, b in zip(_names(p), *res):
+        assert torch.equal(a, b), n
+
