@@ -1,4 +1,4 @@
-# final validation of the committed state: full GPU suite, smoke, headline bench, profile
+# final validation: full GPU suite, smoke, headline bench (twice)
 set -u
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
@@ -7,5 +7,4 @@ timeout -k 10 600 python -u -m pytest tests -m gpu -q --maxfail=5 --timeout 300 
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || exit $?; tail -1 gpurun_out/smoke.log
 timeout -k 10 300 python bench.py > gpurun_out/b_default.log 2>&1 || exit $?; tail -1 gpurun_out/b_default.log | cut -c1-260
 timeout -k 10 300 python bench.py --steps 20 --warmup 3 > gpurun_out/b_final.log 2>&1 || exit $?; tail -1 gpurun_out/b_final.log | cut -c150-200
-timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof6 -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --no-eval > gpurun_out/prof6.log 2>&1 || exit $?
 echo done

@@ -331,9 +331,9 @@ class _HyperSeq(torch.autograd.Function):
         clh_C = cell_geometry(Hh, B, True) if lp_on else 0
         bfuse = HYPER_BWD_FUSE and lp_on and dev.type == "cuda" and Hh <= 256 and clh_C == 1 and \
             gemm.plan_splits(B, H, G, 1, ldt) >= 1
-        # dvec P^T alone in the fused order: 64 splits fill the chip (24576 = 64 x 384)
-        S_h0 = 64 if (bfuse and (12 * H) % (64 * 64) == 0) else gemm.plan_splits(B, Hh, 12 * H, 1, ldt)
-        S_h = _split_override("SKR_HYP_SH", S_h0, 12 * H)
+        # dvec P^T: the planned 32 splits also in the fused order (64 measured
+        # 0.15 ms/step slower: 25.03 / 25.00 vs 24.83 / 24.88, profiles/r3/hyper_fused_cell_ab.txt)
+        S_h = _split_override("SKR_HYP_SH", gemm.plan_splits(B, Hh, 12 * H, 1, ldt), 12 * H)
         S_am = _split_override("SKR_HYP_SAM", gemm.plan_splits(B, H, G, 1, ldt), G)
         # d[h | hh] = dR_hyp @ W_y^T: at most 4 split-K slabs -- the next step's
         # two cells read every slab; measured on MI355X (vae_large, same box,
