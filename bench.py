@@ -143,7 +143,8 @@ def main():
     if device.startswith("cuda"):
         from sketch_rnn_amd.train.trainer import check_device_faults
         check_device_faults()   # a timed-out in-launch exchange invalidates the run: fail loudly
-    cost = float(out["cost"])
+    # global mean over ranks (reduced with the last gradient bucket) under DP
+    cost = trainer.reduced_scalars()["cost"] if trainer.reducer is not None else float(out["cost"])
     recon = None
     if not args.no_eval:
         ev = trainer.evaluate(test)      # the whole held-out split (test.num_batches batches)
@@ -152,8 +153,13 @@ def main():
     positions_per_s = global_batch * args.seq_len * args.steps / elapsed
     value = sum(valid[i % len(valid)] for i in range(args.steps)) / elapsed
     if rank == 0:
+        # the headline metric string names the BASELINE.json config; other
+        # presets say which model they measured
+        metric = "train strokes/sec (whole node) + test recon NLL, enc512/dec2048 QuickDraw" \
+            if args.config == "vae_large" else "train strokes/sec (whole node) + test recon NLL, %s (enc%d/dec%d %s)" % (
+                args.config, cfg.enc_rnn_size, cfg.dec_rnn_size, cfg.dec_model)
         rec = {
-            "metric": "train strokes/sec (whole node) + test recon NLL, enc512/dec2048 QuickDraw",
+            "metric": metric,
             "value": round(value, 1),
             "unit": "strokes/s",
             "n_gpus": world,
@@ -172,6 +178,8 @@ def main():
                 "global_batch": global_batch,
                 "seq_len": args.seq_len,
                 "parallelism": "dp%d" % world,
+                "dist_backend": dp.backend() or "none",
+                "world_size_observed": world,
                 "backend": ops.get_backend(),
                 "hip_graph": bool(trainer.use_graph),
             },

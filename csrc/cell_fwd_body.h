@@ -13,7 +13,7 @@ constexpr int kRecSlabs = 8;      // ceiling of the unrolled dh_rec / dh_rec2 sl
 constexpr unsigned kSpinLimit = 1u << 21;
 constexpr int kSlots = 16;        // 8-byte granules per workgroup slot (128 B)
 
-// Diagnostic build only (csrc/bench/cell_bench.hip defines SKR_TRACE_CELL):
+// Diagnostic build only (-DSKR_TRACE_CELL; the round-3 cell bench, removed from the tree, defined it):
 // s_memrealtime stamps per workgroup at entry / loads landed / after each
 // LayerNorm exchange / stores drained.
 #ifdef SKR_TRACE_CELL

@@ -5,7 +5,9 @@
 // multiple of 64 elements, so one float4-vectorised launch updates every
 // tensor. Scalars live on the device so the step is graph-capturable:
 //   scal[0] = lr, scal[1] = t (incremented on device), scal[2] = |g|, scal[3] = clip scale,
-//   scal[4] = 1 if this step was skipped, scal[5] = number of skipped steps
+//   scal[4] = 1 if this step was skipped, scal[5] = number of skipped steps,
+//   scal[6] = gradient scale (data parallel: 1/world folded in here instead of
+//   a separate pass over the summed arena; <= 0 reads as 1)
 // Failure detection: the global gradient norm is computed every step (all
 // clip modes); with nonfinite_policy = 1 a step whose norm is NaN/Inf is
 // skipped on the device (no update, t not advanced) and counted, so a
@@ -18,12 +20,27 @@ namespace {
 
 constexpr int kBlock = 256;
 
+__device__ __forceinline__ float grad_scale(const float* scal) {
+    const float s = scal ? scal[6] : 1.f;
+    return s > 0.f ? s : 1.f;
+}
+
+// The norm is taken over the SCALED elements (g * gs rounded to fp32 first),
+// so a folded 1/world gives bit for bit the norm of a pre-scaled arena.
 __global__ __launch_bounds__(kBlock) void sumsq_partial_kernel(const float4* __restrict__ g, int64_t n4,
-                                                               double* __restrict__ partial) {
+                                                               double* __restrict__ partial,
+                                                               const float* __restrict__ scal) {
     __shared__ float lds[kBlock / 64];
+    const float gs = grad_scale(scal);
     float acc = 0.f;
     for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n4; i += (int64_t)gridDim.x * kBlock) {
-        const float4 v = g[i];
+        float4 v = g[i];
+        if (gs != 1.f) {
+            v.x *= gs;
+            v.y *= gs;
+            v.z *= gs;
+            v.w *= gs;
+        }
         acc += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
     }
     float a1[1] = {acc};
@@ -60,6 +77,7 @@ __global__ __launch_bounds__(kBlock) void adam_kernel(float4* __restrict__ p, co
     const float t = scal[1];
     const float lr_t = scal[0] * sqrtf(1.f - powf(b2, t)) / (1.f - powf(b1, t));
     const float sc = scal[3];
+    const float gs = grad_scale(scal);
     for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n4; i += (int64_t)gridDim.x * kBlock) {
         float4 gg = g[i], mm = m[i], vv = v[i], pp = p[i];
         float* gv = &gg.x;
@@ -69,6 +87,7 @@ __global__ __launch_bounds__(kBlock) void adam_kernel(float4* __restrict__ p, co
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             float x = gv[k];
+            if (gs != 1.f) x *= gs;
             if (clip_mode == 1) x *= sc;
             else if (clip_mode == 2) x = fminf(fmaxf(x, -clip), clip);
             mv[k] = b1 * mv[k] + (1.f - b1) * x;
@@ -98,7 +117,8 @@ SKR_API int skr_adam_step(float* p, const float* g, float* m, float* v, float* s
     if (n % 4 != 0) return -2;
     const int64_t n4 = n / 4;
     const int grid = grid_for(n4);
-    hipLaunchKernelGGL(sumsq_partial_kernel, dim3(grid), dim3(kBlock), 0, s, (const float4*)g, n4, partial);
+    hipLaunchKernelGGL(sumsq_partial_kernel, dim3(grid), dim3(kBlock), 0, s, (const float4*)g, n4, partial,
+                       (const float*)scal);
     hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(64), 0, s, partial, grid, scal, clip_mode, clip,
                        nonfinite_policy);
     hipLaunchKernelGGL(adam_kernel, dim3(grid), dim3(kBlock), 0, s, (float4*)p, (const float4*)g, (float4*)m,
@@ -111,7 +131,8 @@ SKR_API int skr_global_norm(const float* g, int64_t n, double* partial, float* s
     if (n % 4 != 0) return -2;
     const int64_t n4 = n / 4;
     const int grid = grid_for(n4);
-    hipLaunchKernelGGL(sumsq_partial_kernel, dim3(grid), dim3(kBlock), 0, s, (const float4*)g, n4, partial);
+    hipLaunchKernelGGL(sumsq_partial_kernel, dim3(grid), dim3(kBlock), 0, s, (const float4*)g, n4, partial,
+                       (const float*)nullptr);
     hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(64), 0, s, partial, grid, scal_tmp, 1, 1.0f, 0);
     return SKR_CHECK_LAUNCH();
 }

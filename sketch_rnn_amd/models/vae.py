@@ -198,11 +198,19 @@ class SketchVAE(nn.Module):
     def loss(self, strokes: torch.Tensor, lengths: torch.Tensor, labels: Optional[torch.Tensor] = None,
              kl_weight: float = 1.0, train: bool = True, seed: int = 0,
              eps: Optional[torch.Tensor] = None, split_encoder: bool = False) -> Dict[str, torch.Tensor]:
-        """``split_encoder``: cut the autograd graph at the encoder outputs
-        (``mu``, ``presig``); ``cost.backward()`` then stops there and the
-        result carries ``"_enc": ((mu, presig), (mu_cut, presig_cut))`` so the
-        caller runs the encoder's backward as a separate phase
-        (``torch.autograd.backward(enc, [t.grad for t in cut])``)."""
+        """``split_encoder``: cut the autograd graph at the encoder outputs;
+        ``cost.backward()`` then stops there and the result carries
+        ``"_enc": (enc, cut)`` so the caller runs the encoder's backward as a
+        separate phase (``torch.autograd.backward(enc, [t.grad for t in cut])``).
+        The cut point depends on the latent path:
+
+        * fused latent layer (``ops/latent.py``, the GPU default): the cut is
+          at the encoder summary ``last_h`` -- ``enc = (last_h,)``,
+          ``cut = (last_h_detached,)``. The latent heads (``mu_w``, ``mu_b``,
+          ``sig_w``, ``sig_b``) sit after the cut, so their gradients are
+          produced in phase A even though the parameters belong to the
+          encoder (the trainer's late arena part);
+        * torch latent layer: the cut is at ``(mu, presig)``."""
         cfg = self.cfg
         B = strokes.shape[0]
         Nmax = strokes.shape[1] - 1
@@ -212,7 +220,8 @@ class SketchVAE(nn.Module):
         from ..ops import latent as L
         H, Hh = cfg.dec_rnn_size, cfg.hyper_num_units
         widths = {"hyper": (H, Hh, H, Hh), "lstm": (H, H), "layer_norm": (H, H)}[cfg.dec_model]
-        if cfg.conditional and self.class_emb is None and L.latent_ok(strokes.float(), len(widths)) and \
+        # (eligibility from a parameter: no fp32 copy of the stroke batch per call)
+        if cfg.conditional and self.class_emb is None and L.latent_ok(self.encoder.mu_w, len(widths)) and \
                 LATENT_FUSED:
             # encoder summary -> (mu, presig, z, KL, decoder state) as one node (ops/latent.py)
             last_h = self.encoder.last_hidden(strokes[:, 1:].transpose(0, 1), lengths, train, seed)

@@ -1,10 +1,21 @@
-"""Library GEMMs (hipBLASLt via torch) with a selectable operand precision.
+"""GEMM dispatch with a selectable operand precision (fp32 / bf16 / fp8).
 
-Plain, unfused GEMMs -- the hoisted input projections, the recurrent
-``h @ W_h`` of each step, the weight-gradient reductions and the head --
-go to hipBLASLt. In ``bf16`` mode operands are bf16 and the result is
-written in fp32 (``torch.mm(..., out_dtype=float32)``: hipBLASLt bf16 x
-bf16 -> fp32), so accumulation and everything downstream stay fp32.
+Where each product runs (vae_large: no library GEMM in the profile,
+profiles/r3/vae_large_kernel_summary.txt):
+
+* per-time-step recurrent products (``h @ W_h``, the grouped HyperLSTM
+  products, their backward twins): hand-written MFMA skinny split-K GEMMs,
+  ``csrc/skinny_gemm.hip`` (:func:`rec_gemm`, :func:`rec_gemm_group`, the
+  fp8 ``rec_gemm_fp8*`` variants);
+* long-K weight gradients over all T*B rows: ``csrc/wgrad_gemm.hip``
+  (:func:`wgrad`; bf16, 256-multiple shapes);
+* small products (z-projections, hyper-norm factors): ``csrc/small_gemm.hip``
+  (:func:`small_mm`, :func:`small_mm_batched`);
+* everything else -- fp32 / odd-shaped weight gradients (:func:`wgrad`'s
+  fallback), the generic :func:`mm` / :func:`bmm` helpers used off the
+  flagship path -- goes to hipBLASLt through torch. In ``bf16`` mode
+  operands are bf16 and results fp32 (``torch.mm(..., out_dtype=float32)``),
+  so accumulation and everything downstream stay fp32.
 """
 from __future__ import annotations
 

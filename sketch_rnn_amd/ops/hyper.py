@@ -90,8 +90,8 @@ class _HyperSeq(torch.autograd.Function):
     [vec = hh @ P + q] -> [main cell]; backward per step: [main cell bwd] ->
     [grouped GEMM dR_main W_h^T + dvec P^T] -> [hyper cell bwd] ->
     [dR_hyp W_y^T]; weight gradients are long-K GEMMs over all T*B rows after
-    the scan. (A persistent one-launch forward was built and measured slower:
-    csrc/experiments/hyper_persist.hip.)
+    the scan. (A persistent one-launch forward was built in round 3 and
+    measured slower, 45.6 vs 36.5 us per step: profiles/r3/hyper_persist_*.)
     """
 
     @staticmethod

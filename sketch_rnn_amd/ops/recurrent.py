@@ -95,7 +95,7 @@ class _Saved:
 # ---- cell-kernel geometry (csrc/lstm_cell.hip) --------------------------------------
 # A row of H hidden units runs on C workgroups (C == 1 and H > 256: one
 # 1024-thread workgroup per row). Policy: 256-unit workgroups (measured
-# fastest at H = 2048 with LayerNorm, csrc/bench/cell_bench.hip, despite the
+# fastest at H = 2048 with LayerNorm by the round-2 cell bench, despite the
 # in-launch exchange). SKR_CELL_C overrides C; SKR_CLUSTER=0 forces C = 1.
 CLUSTER_ENABLED = os.environ.get("SKR_CLUSTER", "1") != "0"
 CELL_C = int(os.environ.get("SKR_CELL_C", "0"))

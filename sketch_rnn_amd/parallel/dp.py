@@ -10,9 +10,13 @@ Design for MI355X / xGMI:
   gradients becomes 4 ring all-reduces -- large enough to be link-bandwidth
   bound on the 7 xGMI links, small enough that the first bucket's
   reduction overlaps the remaining backward when issued from a hook;
-* the average (1/world) is one in-place scale of the arena after the sums;
-* scalars for logging (recon / KL / pen) are averaged with one all-reduce;
-  schedules (lr, KL weight) are pure functions of the step and need none;
+* the average (1/world) is folded into the optimizer (``fold_scale``: the
+  clip + Adam kernels multiply by ``scalars[6]``), so the summed arena is
+  never re-read and re-written just to scale it;
+* the step's loss scalars (cost / recon / KL / pen / valid count) ride in the
+  arena's tail (:attr:`..train.optim.FlatAdam.tail`) inside the LAST bucket:
+  their cross-rank sum costs no collective of its own; schedules (lr, KL
+  weight) are pure functions of the step and need none;
 * :func:`broadcast_params` makes rank 0's initial weights authoritative.
 """
 from __future__ import annotations
@@ -94,14 +98,18 @@ class GradReducer:
     1/world average is folded into the unpack copy.
 
     ``force``: issue the collectives even at world size 1 (exercises the
-    RCCL path on a single-GPU box; the result is the identity)."""
+    RCCL path on a single-GPU box; the result is the identity).
+
+    ``fold_scale``: leave the summed gradients unscaled; the consumer applies
+    1/world itself (FlatAdam.set_grad_scale) -- no extra pass over the arena."""
 
     def __init__(self, grad: torch.Tensor, bucket_mb: float = 32.0, split: Optional[int] = None,
-                 wire_dtype: str = "fp32", force: bool = False):
+                 wire_dtype: str = "fp32", force: bool = False, fold_scale: bool = False):
         if wire_dtype not in ("fp32", "bf16"):
             raise ValueError("wire_dtype must be fp32 or bf16, got %r" % (wire_dtype,))
         self.grad = grad
         self.wire_dtype = wire_dtype
+        self.fold_scale = fold_scale
         self.world = world_size()
         self.active = self.world > 1 or (force and is_dist())
         n = grad.numel()
@@ -127,8 +135,8 @@ class GradReducer:
         return [dist.all_reduce(b, op=dist.ReduceOp.SUM, async_op=True) for b in self.parts[part]]
 
     def all_reduce(self, async_op: bool = False):
-        """Sum every bucket across ranks (all in flight at once), then one
-        in-place 1/world scale of the arena. Plain SUM is used rather than a
+        """Sum every bucket across ranks (all in flight at once), then
+        (unless ``fold_scale``) one in-place 1/world scale of the arena. Plain SUM is used rather than a
         pre-multiplied sum so the call pattern is the same on every RCCL
         version."""
         if not self.active:
@@ -145,7 +153,7 @@ class GradReducer:
             w.wait()
         if not self.active:
             return
-        inv = 1.0 / self.world
+        inv = 1.0 if self.fold_scale else 1.0 / self.world
         if self.wire_dtype == "bf16":
             for part in self._started:
                 for (a, b), w in zip(self.ranges[part], self.parts[part]):

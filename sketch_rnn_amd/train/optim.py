@@ -24,7 +24,14 @@ Failure detection: the global gradient norm is computed every
 step; ``nonfinite="skip"`` drops a step whose gradient norm is NaN/Inf on the
 device (no parameter or moment update, ``t`` not advanced) and counts it in
 ``scalars[5]`` -- no host sync per step. ``"apply"`` keeps TF semantics.
-Device scalars: ``[lr, t, grad_norm, clip_scale, skipped_now, skipped_total, -, -]``.
+Device scalars: ``[lr, t, grad_norm, clip_scale, skipped_now, skipped_total, grad_scale, -]``.
+
+Data parallelism: the gradient buffer carries a small TAIL
+after the arena (:attr:`FlatAdam.tail`, ``TAIL`` floats) that rides in the
+last all-reduce bucket -- the step's loss scalars are packed there, so their
+cross-rank sum needs no collective of its own -- and the 1/world average is
+``grad_scale`` (``scalars[6]``), applied inside the norm and Adam kernels
+instead of as a separate pass over the summed arena.
 """
 from __future__ import annotations
 
@@ -35,6 +42,8 @@ import torch
 
 
 class FlatAdam:
+    TAIL = 64   # floats after the arena in grad_full (reduced with the last bucket)
+
     def __init__(self, params: Iterable[torch.nn.Parameter], lr: float = 1e-3, betas=(0.9, 0.999),
                  eps: float = 1e-8, clip_mode: Optional[str] = None, clip: float = 0.0,
                  align: int = 64, nonfinite: str = "skip"):
@@ -55,7 +64,10 @@ class FlatAdam:
         self.numel = off
         self.offset_of = {id(p): o for p, o in zip(self.params, self.offsets)}
         self.flat = torch.zeros(off, device=dev, dtype=torch.float32)
-        self.grad = torch.zeros(off, device=dev, dtype=torch.float32)
+        # gradients + the reduced tail (loss scalars); Adam reads only [:numel]
+        self.grad_full = torch.zeros(off + self.TAIL, device=dev, dtype=torch.float32)
+        self.grad = self.grad_full[:off]
+        self.tail = self.grad_full[off:]
         self.m = torch.zeros(off, device=dev, dtype=torch.float32)
         self.v = torch.zeros(off, device=dev, dtype=torch.float32)
         for p, o in zip(self.params, self.offsets):
@@ -67,8 +79,9 @@ class FlatAdam:
             # directly (ops.gemm.grad_slot): autograd then keeps that tensor as
             # p.grad and gather_grads has nothing to copy for it
             p._grad_slot = p.grad
-        # device scalars: [lr, step, grad_norm, clip_scale, skipped_now, skipped_total, -, -]
+        # device scalars: [lr, step, grad_norm, clip_scale, skipped_now, skipped_total, grad_scale, -]
         self.scalars = torch.zeros(8, device=dev, dtype=torch.float32)
+        self.scalars[6] = 1.0
         self.set_lr(lr)
         self.step_count = 0
 
@@ -76,6 +89,12 @@ class FlatAdam:
     def set_lr(self, lr: float) -> None:
         self.lr = float(lr)
         self.scalars[0].fill_(self.lr)
+
+    def set_grad_scale(self, scale: float) -> None:
+        """Factor applied to every gradient element before the norm, clip and
+        Adam (data parallel: 1/world over a SUM all-reduce)."""
+        self.grad_scale = float(scale)
+        self.scalars[6].fill_(self.grad_scale)
 
     def zero_grad(self, set_to_none: bool = False) -> None:
         """``set_to_none``: unbind ``p.grad`` so autograd hands over the
@@ -127,8 +146,9 @@ class FlatAdam:
 
     @torch.no_grad()
     def _step_torch(self) -> None:
-        g = self.grad
         sc = self.scalars
+        gs = torch.where(sc[6] > 0, sc[6], torch.ones_like(sc[6]))   # no host sync (graph capture)
+        g = self.grad * gs
         norm = torch.sqrt((g.double() * g.double()).sum()).float()
         sc[2] = norm
         skip = (~torch.isfinite(norm)) & (self.nonfinite == "skip")
@@ -164,7 +184,9 @@ class FlatAdam:
     def load_state_dict(self, sd):
         self.m.copy_(sd["m"])
         self.v.copy_(sd["v"])
+        gs = self.scalars[6].clone()
         self.scalars.copy_(sd["scalars"])
+        self.scalars[6] = gs            # a property of this run's world size, not of the checkpoint
         self.step_count = int(sd["step_count"])
         self.lr = float(self.scalars[0])
 

@@ -260,8 +260,12 @@ class VAETrainer:
         split = self.opt.offset_of[id(late[0])] if self.overlap else None
         # SKR_DP_WIRE=bf16: gradients cross the xGMI ring in bf16 (half the bytes)
         wire = dp_wire_dtype or os.environ.get("SKR_DP_WIRE", "fp32")
-        self.reducer = dp.GradReducer(self.opt.grad, split=split, wire_dtype=wire,
-                                      force=force_reducer) if reduce_on else None
+        # the arena plus its tail (this step's loss scalars, summed in the last
+        # bucket); the 1/world average is folded into the clip + Adam kernels
+        self.reducer = dp.GradReducer(self.opt.grad_full, split=split, wire_dtype=wire,
+                                      force=force_reducer, fold_scale=True) if reduce_on else None
+        if reduce_on:
+            self.opt.set_grad_scale(1.0 / self.world)
         self._enc_pending = None
         self.save_dir = save_dir
         self.log = log
@@ -276,12 +280,35 @@ class VAETrainer:
         self.host_times = PhaseTimes()            # data / step / eval / save wall time
         self.gpu_times = GpuPhaseTimer(enabled=metrics_path is not None)
 
+    # loss scalars packed into the gradient arena's tail (summed over ranks
+    # with the last all-reduce bucket; the trainer logs their global mean)
+    _TAIL_KEYS = ("cost", "r_cost", "kl_cost", "shape_cost", "pen_cost")
+
+    def _pack_scalars(self, out, lengths):
+        if self.reducer is None:
+            return
+        vals = [out[k].detach().reshape(()).float() for k in self._TAIL_KEYS if k in out]
+        vals.append(lengths.sum().to(torch.float32))
+        self.opt.tail[:len(vals)].copy_(torch.stack(vals))
+
+    def reduced_scalars(self) -> Dict[str, float]:
+        """The last step's loss scalars averaged over ranks and the global
+        count of valid stroke points (from the reduced arena tail; one host
+        read). Only meaningful with an active reducer."""
+        keys = [k for k in self._TAIL_KEYS if k in self._last_keys]
+        t = self.opt.tail[:len(keys) + 1].tolist()
+        res = {k: v / self.world for k, v in zip(keys, t)}
+        res["valid_points"] = t[len(keys)]
+        return res
+
     def _fwd_bwd(self, strokes, lengths, labels):
         self.opt.zero_grad(set_to_none=True)
         out = self.model.loss(strokes, lengths, labels if self.cfg.num_classes > 0 else None,
                               kl_weight=self.kl_w, train=True, seed=self.seed)
         out["cost"].backward()
         self.opt.gather_grads()
+        self._pack_scalars(out, lengths)
+        self._last_keys = tuple(out)
         return {k: v.detach() for k, v in out.items()}
 
     def _opt_step(self):
@@ -298,6 +325,8 @@ class VAETrainer:
         out["cost"].backward()
         self.opt.gather_grads(self._early)
         self._enc_pending = (enc, [t.grad for t in cut])
+        self._pack_scalars(out, lengths)
+        self._last_keys = tuple(out)
         return {k: v.detach() for k, v in out.items()}
 
     def _bwd_b(self):
@@ -475,6 +504,7 @@ class VAETrainer:
         pf = self._prefetch
         t0 = time.time()
         valid = 0.0     # this rank's non-padding stroke points since the last log line
+        n_int = 0       # steps since the last log line (resume / repeated train() safe)
         while self.step < num_steps:
             with phase("data", self.host_times):
                 raw = pf.get() if pf is not None else self.train_set.random_batch(self.rank, self.world)
@@ -482,10 +512,14 @@ class VAETrainer:
                 batch = self.batch_to_device(raw)
             with phase("step", self.host_times):
                 out = self.train_step(*batch)
+            n_int += 1
             if self.step % log_every == 0 or self.step == num_steps:
                 check_device_faults()
-                vals = {k: float(v) for k, v in out.items()}
-                n_int = (self.step - 1) % log_every + 1          # steps since the last log line
+                if self.reducer is not None:   # global means, from the arena tail (no extra collective)
+                    vals = self.reduced_scalars()
+                    vals.pop("valid_points")
+                else:
+                    vals = {k: float(v) for k, v in out.items()}
                 dt = (time.time() - t0) / n_int
                 t0 = time.time()
                 valid_all = dp.sum_scalar(valid)                # every rank's batches (bench.py's metric)
@@ -505,6 +539,7 @@ class VAETrainer:
                         self.host_times.reset()
                         with open(self.metrics_path, "a") as f:
                             f.write(json.dumps(rec) + "\n")
+                n_int = 0
                 skipped = self.opt.skipped_steps()
                 if skipped > self.max_skipped:
                     raise DivergenceError("%d steps with a non-finite gradient (last cost %r at step %d)"
@@ -518,5 +553,11 @@ class VAETrainer:
                 with phase("save", self.host_times):
                     check_device_faults()     # never checkpoint a step whose exchange timed out
                     self.save()
+                    # every rank waits for rank 0's write: no rank starts the next
+                    # step's collectives (whose kernels would then hold CUs waiting
+                    # on rank 0) while rank 0 is still busy writing
+                    dp.barrier()
         check_device_faults()
-        return self.save()
+        path = self.save()
+        dp.barrier()
+        return path

@@ -185,3 +185,62 @@ def test_bench_multi_rank_cpu(tmp_path):
     rec = json.loads(lines[0])
     assert rec["n_gpus"] == 2 and rec["config"]["global_batch"] == 8 and rec["config"]["parallelism"] == "dp2"
     assert 0 < rec["value"] <= rec["positions_per_s"] and 0 < rec["valid_fraction"] <= 1
+
+
+def _scalars_worker(rank, world, port, out_dir):
+    """The loss scalars packed into the arena tail come out of the last
+    bucket as the sum over ranks: the trainer's logged cost is the mean of
+    the per-rank costs, and the valid-point count is the global one."""
+    dp = _init(rank, world, port)
+    from sketch_rnn_amd.cli.vae_train import make_datasets
+    from sketch_rnn_amd.config import VAEConfig
+    from sketch_rnn_amd.train.trainer import VAETrainer
+    cfg = VAEConfig(enc_rnn_size=8, dec_rnn_size=16, z_size=4, num_mixture=2, max_seq_len=24, batch_size=4,
+                    save_every=0, seed=0)
+    (tr_set, va, te), _ = make_datasets(cfg, None, 40, rank=rank)
+    logs = []
+    tr = VAETrainer(cfg, tr_set, va, te, save_dir=os.path.join(out_dir, "s"), log=logs.append)
+    assert tr.reducer is not None and tr.reducer.fold_scale and float(tr.opt.scalars[6]) == 0.5
+    batch = tr.batch_to_device(tr_set.random_batch(rank, world))
+    out = tr.train_step(*batch)
+    red = tr.reduced_scalars()
+    tr.train(num_steps=2, log_every=1)          # one more step through the logging loop
+    glob2 = tr.reduced_scalars()
+    torch.save({"local": {k: float(v) for k, v in out.items()}, "red": red, "n": float(batch[1].sum()),
+                "log": logs, "glob2": glob2}, os.path.join(out_dir, "s%d.pt" % rank))
+    dp.barrier()
+    torch.distributed.destroy_process_group()
+
+
+def test_dp_loss_scalars_reduced_in_last_bucket(tmp_path):
+    _spawn(_scalars_worker, tmp_path)
+    s = [torch.load(tmp_path / ("s%d.pt" % k), weights_only=True) for k in range(2)]
+    for k in ("cost", "r_cost", "kl_cost"):
+        mean = (s[0]["local"][k] + s[1]["local"][k]) / 2
+        assert abs(s[0]["red"][k] - mean) < 1e-5 * max(1.0, abs(mean)), (k, s[0]["red"][k], mean)
+        assert s[0]["red"][k] == s[1]["red"][k]
+    assert s[0]["red"]["valid_points"] == s[0]["n"] + s[1]["n"]
+    # rank 0 logged the global mean of the step it reported
+    line = [ln for ln in s[0]["log"] if ln.startswith("step: 2,")][0]
+    assert ("cost: %.4f" % s[0]["glob2"]["cost"]) in line
+    assert s[1]["log"] == [] or all(not ln.startswith("step:") for ln in s[1]["log"])
+
+
+def test_grad_scale_fold_is_bitwise_equal_to_prescaled_arena():
+    """1/world folded into the clip + Adam step (FlatAdam.set_grad_scale)
+    equals scaling the summed arena first, bit for bit (both clip modes)."""
+    from sketch_rnn_amd.train.optim import FlatAdam
+    for mode, clip in (("global_norm", 0.5), ("value", 0.01)):
+        ps = [torch.nn.Parameter(torch.randn(37, 5, generator=torch.Generator().manual_seed(1))),
+              torch.nn.Parameter(torch.randn(300, generator=torch.Generator().manual_seed(2)))]
+        a = FlatAdam([torch.nn.Parameter(p.detach().clone()) for p in ps], lr=0.01, clip_mode=mode, clip=clip)
+        b = FlatAdam([torch.nn.Parameter(p.detach().clone()) for p in ps], lr=0.01, clip_mode=mode, clip=clip)
+        for it in range(3):
+            g = torch.randn(a.numel, generator=torch.Generator().manual_seed(10 + it)) * 3.0
+            a.grad.copy_(g * (1.0 / 3.0))          # the separate pass
+            b.grad.copy_(g)
+            b.set_grad_scale(1.0 / 3.0)            # folded
+            a.step()
+            b.step()
+            assert torch.equal(a.flat, b.flat) and torch.equal(a.m, b.m) and torch.equal(a.v, b.v)
+            assert torch.equal(a.scalars[2], b.scalars[2])

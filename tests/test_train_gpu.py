@@ -139,3 +139,24 @@ def test_rccl_world1_reducer_matches_single_graph(tmp_path):
         assert (w - ws).abs().mean() < 1e-4, (key, (w - ws).abs().mean())
 
 
+
+def test_hip_adam_grad_scale_fold_bitwise():
+    """csrc/optim.hip with the 1/world scale folded in (scalars[6]) equals the
+    kernel run on a pre-scaled arena, bit for bit (norm, clip, moments)."""
+    from sketch_rnn_amd import ops
+    from sketch_rnn_amd.train.optim import FlatAdam
+    assert ops.use_hip(torch.zeros(1, device="cuda"))
+    for mode, clip in (("global_norm", 0.5), ("value", 0.01)):
+        ps = [torch.randn(1000, 7, generator=torch.Generator().manual_seed(1)), torch.randn(4099)]
+        a = FlatAdam([torch.nn.Parameter(p.cuda()) for p in ps], lr=0.01, clip_mode=mode, clip=clip)
+        b = FlatAdam([torch.nn.Parameter(p.cuda()) for p in ps], lr=0.01, clip_mode=mode, clip=clip)
+        b.set_grad_scale(1.0 / 8.0)
+        for it in range(3):
+            g = torch.randn(a.numel, generator=torch.Generator().manual_seed(10 + it)).cuda() * 8.0
+            a.grad.copy_(g * (1.0 / 8.0))
+            b.grad.copy_(g)
+            a.step()
+            b.step()
+        torch.cuda.synchronize()
+        assert torch.equal(a.flat, b.flat) and torch.equal(a.m, b.m) and torch.equal(a.v, b.v)
+        assert torch.equal(a.scalars[:6], b.scalars[:6])
