@@ -1,0 +1,127 @@
+// Main loop of the skinny bf16 GEMM tiles (csrc/skinny_gemm.hip,
+// csrc/hyper_step.hip): one [M <= 128, BN] tile of A . Bt^T over the K range
+// [k0, k0 + kslice), accumulated in registers.
+//
+// LDS-DMA ring. Tiles move global -> LDS with global_load_lds_dwordx4
+// (no staging registers, no ds_write), NS buffers deep: NS-1 K-tiles are in
+// flight while one is multiplied. One counted `s_waitcnt vmcnt(N)` plus a raw
+// s_barrier per K-tile (a __syncthreads() would drain every prefetch, CDNA4
+// guide "Pipelining across barriers"). LDS rows are 128 B (BK = 64 bf16) with
+// the 16-byte chunk index XOR-swizzled by (row >> 1) & 7 -- applied on the
+// per-lane GLOBAL address, since an LDS-DMA wave writes 1 KiB linearly -- so
+// the 16 rows of a ds_read_b128 fragment read hit 16 distinct bank quads.
+//
+// Block: 256 threads (4 waves); wave w owns rows 32w..32w+31 x all BN
+// columns (2 x BN/16 accumulators). MFMA v_mfma_f32_16x16x32_bf16: lane l
+// holds A[row l&15][k 8(l>>4) .. +7] and B[k 8(l>>4) .. +7][col l&15];
+// C/D: col = l&15, row = 4(l>>4) + i.
+//
+// (Weight loads use the default cache policy: every weight is re-read each
+// time step and stays Infinity-Cache resident; nt loads measured slower,
+// 30.3 vs 28.5 ms/step on vae_large, profiles/r2s5/bench_gemm_nt.log.)
+#pragma once
+#include "common.h"
+
+namespace skr {
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8_t;
+typedef __attribute__((ext_vector_type(4))) float f32x4_t;
+
+constexpr int BM = 128, BK = 64;
+
+template <int GPW, int NS>
+__device__ __forceinline__ void wait_ahead(int ahead) {
+    // tile kt landed (for this wave) once at most `ahead` younger tiles are pending
+    if constexpr (NS - 2 >= 4) if (ahead >= 4) { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * GPW) : "memory"); return; }
+    if constexpr (NS - 2 >= 3) if (ahead == 3) { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * GPW) : "memory"); return; }
+    if constexpr (NS - 2 >= 2) if (ahead == 2) { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * GPW) : "memory"); return; }
+    if (ahead == 1) { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GPW) : "memory"); return; }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+// LDS bytes of the ring.
+template <int BN, int NS>
+constexpr int glds_lds_bytes() { return NS * (BM + BN) * BK * 2; }
+
+template <int BN, int NS>
+__device__ __forceinline__ void glds_mma(const __hip_bfloat16* __restrict__ A, int64_t lda,
+                                         const __hip_bfloat16* __restrict__ Bt, int64_t ldb, int M, int n0,
+                                         int64_t k0, int kslice, __hip_bfloat16* smem, f32x4_t (&acc)[2][BN / 16]) {
+    constexpr int NJ = BN / 16;
+    constexpr int A_CH = BM / 8, B_CH = BN / 8;     // 1-KiB chunks (8 rows) per tile
+    constexpr int GPW = (A_CH + B_CH) / 4;          // glds per wave per tile
+    constexpr int TILE = (BM + BN) * BK;            // bf16 elements per stage
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int n = kslice / BK;
+
+    // per-lane source rows / swizzled chunk (fixed across tiles)
+    const int r8 = lane >> 3, slot = lane & 7;
+    const __hip_bfloat16* asrc[A_CH / 4];
+    const __hip_bfloat16* bsrc[B_CH / 4];
+#pragma unroll
+    for (int i = 0; i < A_CH / 4; ++i) {
+        const int row = (w + 4 * i) * 8 + r8;
+        const int kc = slot ^ ((row >> 1) & 7);
+        // rows past M: every lane of the chunk reads the same 16 bytes (one
+        // line instead of 1 KiB; the wave's glds count stays uniform)
+        asrc[i] = row < M ? A + (int64_t)row * lda + k0 + kc * 8 : A + (int64_t)(M - 1) * lda + k0;
+    }
+#pragma unroll
+    for (int i = 0; i < B_CH / 4; ++i) {
+        const int row = (w + 4 * i) * 8 + r8;
+        const int kc = slot ^ ((row >> 1) & 7);
+        bsrc[i] = Bt + (int64_t)(n0 + row) * ldb + k0 + kc * 8;
+    }
+    auto issue = [&](int kt) {
+        __hip_bfloat16* st = smem + (kt % NS) * TILE;
+        const int64_t ko = (int64_t)kt * BK;
+#pragma unroll
+        for (int i = 0; i < A_CH / 4; ++i)
+            __builtin_amdgcn_global_load_lds((const void*)(asrc[i] + ko),
+                                             (__attribute__((address_space(3))) void*)(st + (w + 4 * i) * 512), 16, 0, 0);
+#pragma unroll
+        for (int i = 0; i < B_CH / 4; ++i)
+            __builtin_amdgcn_global_load_lds((const void*)(bsrc[i] + ko),
+                                             (__attribute__((address_space(3))) void*)(st + BM * BK + (w + 4 * i) * 512),
+                                             16, 0, 0);
+    };
+
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+    const int fr = lane & 15, fq = lane >> 4;
+#pragma unroll
+    for (int p = 0; p < NS - 1; ++p)
+        if (p < n) issue(p);
+    for (int kt = 0; kt < n; ++kt) {
+        wait_ahead<GPW, NS>(min(n - 1 - kt, NS - 2));
+        __builtin_amdgcn_s_barrier();  // ... and for every wave; buffer (kt-1) % NS is free
+        if (kt + NS - 1 < n) issue(kt + NS - 1);
+        const __hip_bfloat16* As = smem + (kt % NS) * TILE;
+        const __hip_bfloat16* Bs = As + BM * BK;
+#pragma unroll
+        for (int ks = 0; ks < BK; ks += 32) {
+            const int kc = ks / 8 + fq;
+            bf16x8_t af[2], bfr[NJ];
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                const int row = 32 * w + 16 * i + fr;
+                af[i] = *(const bf16x8_t*)(&As[row * BK + ((kc ^ ((row >> 1) & 7)) * 8)]);
+            }
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) {
+                const int row = 16 * j + fr;
+                bfr[j] = *(const bf16x8_t*)(&Bs[row * BK + ((kc ^ ((row >> 1) & 7)) * 8)]);
+            }
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int j = 0; j < NJ; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+        }
+    }
+}
+
+}  // namespace skr
