@@ -268,6 +268,12 @@ __device__ __forceinline__ void cell_fwd_body(const FwdArgs& a, const int c, con
         const int64_t ro = (int64_t)b * H + u;
         const float h = th[k] * og[k];
         a.h_out[ro] = h;
+        if constexpr (!LN && MOD != 0 && MOD != 3) {   // (the LN path stores it after its exchanges)
+            if (a.r_lp != nullptr) {
+#pragma unroll
+                for (int q = 0; q < 4; ++q) a.r_lp[b * a.ld_R + q * H + u] = to_bf16(rsv[k][q]);
+            }
+        }
         const float hc = r ? a.init_h[ro] : h;
         if (a.h_carry != nullptr) a.h_carry[ro] = hc;   // (== h_out without resets: callers skip it)
         a.c_carry[ro] = r ? a.init_c[ro] : cn[k];

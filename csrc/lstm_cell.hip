@@ -71,11 +71,13 @@ __global__ __launch_bounds__(NT) void cell_bwd(const BwdArgs a) {
 template <typename A>
 using KernelT = void (*)(const A);
 
+// MOD without LN: the HyperLSTM with a plain main cell (use_layer_norm=False;
+// the hyper cell itself is always a LayerNorm cell)
 template <int NT, int UPT, int NS>
 KernelT<FwdArgs> pick(bool ln, int mod, const FwdArgs*) {
-    if (mod == 3) return cell_fwd<NT, UPT, 1, true, 3>;
-    if (mod == 2) return cell_fwd<NT, UPT, NS, true, 2>;
-    if (mod) return cell_fwd<NT, UPT, NS, true, 1>;
+    if (mod == 3) return ln ? cell_fwd<NT, UPT, 1, true, 3> : cell_fwd<NT, UPT, 1, false, 3>;
+    if (mod == 2) return ln ? cell_fwd<NT, UPT, NS, true, 2> : cell_fwd<NT, UPT, NS, false, 2>;
+    if (mod) return ln ? cell_fwd<NT, UPT, NS, true, 1> : cell_fwd<NT, UPT, NS, false, 1>;
     if (ln) return cell_fwd<NT, UPT, NS, true, 0>;
     return cell_fwd<NT, UPT, NS, false, 0>;
 }
@@ -108,8 +110,8 @@ KernelT<BwdArgs> pick(bool ln, int mod, const BwdArgs* a) {
         if (ln && mod == 2) return pick_dh<NT, UPT, NS, 2>(dh_ceiling(*a));
         if (ln && mod == 0) return pick_dh<NT, UPT, NS, 0>(dh_ceiling(*a));
     }
-    if (mod == 2) return cell_bwd<NT, UPT, NS, true, 2>;
-    if (mod) return cell_bwd<NT, UPT, NS, true, 1>;
+    if (mod == 2) return ln ? cell_bwd<NT, UPT, NS, true, 2> : cell_bwd<NT, UPT, NS, false, 2>;
+    if (mod) return ln ? cell_bwd<NT, UPT, NS, true, 1> : cell_bwd<NT, UPT, NS, false, 1>;
     if (ln) return cell_bwd<NT, UPT, NS, true, 0>;
     return cell_bwd<NT, UPT, NS, false, 0>;
 }
@@ -155,7 +157,6 @@ inline int64_t coresident_capacity(const void* k, int nt) {
 // otherwise 256 threads with UPT units each.
 template <typename A>
 int launch(const A& a, bool ln, int mod, hipStream_t s) {
-    if (mod && !ln) return -3;
     if constexpr (std::is_same<A, FwdArgs>::value) {
         if (mod == 3 && (a.gpre == nullptr || a.gstats == nullptr || a.gstat_tiles < 1 || a.r_lp != nullptr)) return -3;
     }

@@ -104,6 +104,7 @@ class VAEConfig:
     hyper_num_units: int = 256
     hyper_embedding_size: int = 32
     hyper_use_recurrent_dropout: bool = False
+    hyper_use_layer_norm: bool = True   # LayerNorm main cell of the HyperLSTM (the hyper cell always has one)
     # class-conditional z (345 QuickDraw classes in the large config)
     num_classes: int = 0
     class_embed: str = "add"          # add | concat

@@ -114,7 +114,7 @@ class SketchVAE(nn.Module):
             self.dec = C.LNLSTMParams(in_size, H, gen=gen)
         elif cfg.dec_model == "hyper":
             self.dec = C.HyperLSTMParams(in_size, H, cfg.hyper_num_units, cfg.hyper_embedding_size,
-                                         use_layer_norm=True, gen=gen)
+                                         use_layer_norm=cfg.hyper_use_layer_norm, gen=gen)
         else:
             raise ValueError(cfg.dec_model)
         self.state_size = 2 * (H + (cfg.hyper_num_units if cfg.dec_model == "hyper" else 0))

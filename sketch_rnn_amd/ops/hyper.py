@@ -221,18 +221,24 @@ class _HyperSeq(torch.autograd.Function):
         slp = _ln_saves_lp(infer)
         sdt = torch.bfloat16 if slp else f32
         sv = (lambda *shape, dt=f32: None) if infer else (lambda *shape, dt=f32: torch.empty(*shape, device=dev, dtype=dt))
-        XHAT, RSTD, CHAT = sv(T, B, G, dt=sdt), sv(T, B, 5), sv(T, B, H, dt=sdt)
+        mln_on = ln_g is not None   # LayerNorm main cell (use_layer_norm); the hyper cell always is one
+        if mln_on:
+            XHAT, RSTD, CHAT = sv(T, B, G, dt=sdt), sv(T, B, 5), sv(T, B, H, dt=sdt)
+            ACT = COUT = None
+        else:   # plain main cell: gate activations + c' (csrc/cell_fwd_body.h !LN saves)
+            XHAT = RSTD = CHAT = None
+            ACT, COUT = sv(T, B, G), sv(T, B, H)
         HXHAT, HRSTD, HCHAT = sv(T, B, Gh, dt=sdt), sv(T, B, 5), sv(T, B, Hh, dt=sdt)
         # modulation vectors in bf16 when the GEMMs are bf16 (read only by the main cells)
         VEC = None if (hfused and infer) else torch.empty(T, B, 12 * H, device=dev,
                                                           dtype=torch.bfloat16 if vbf else f32)
         sd = _seed_tensor(seed, dev)
         hln = [t.contiguous() for t in (hln_g, hln_b, hlnc_g, hlnc_b)]
-        mln = [t.contiguous() for t in (ln_g, ln_b, lnc_g, lnc_b)]
+        mln = [t.contiguous() for t in (ln_g, ln_b, lnc_g, lnc_b)] if mln_on else [None] * 4
         bias_c = bias.contiguous()
         RM = None if hfused else torch.empty(T if (RLP is None and not infer) else 1, max(S_m, 1), B, G, device=dev,
                                              dtype=f32)
-        rmi = (lambda t: t) if RM.shape[0] == T else (lambda t: 0)
+        rmi = (lambda t: t) if (RM is not None and RM.shape[0] == T) else (lambda t: 0)
         RY = torch.empty(max(S_y, 1), B, Gh, device=dev, dtype=f32)
         mod = 2 if vbf else 1
         # modulation step fused with the gate pre-activations and their
@@ -299,14 +305,22 @@ class _HyperSeq(torch.autograd.Function):
         am.ld_xp, am.ld_R = G, G
         am.R_nslab, am.R_slab = max(S_m, 1), B * G
         am.vec_gs, am.vec_ld, am.vec_bias, am.bias = H, 12 * H, q.data_ptr(), bias_c.data_ptr()
-        am.ln_g, am.ln_b, am.lnc_g, am.lnc_b = (t.data_ptr() for t in mln)
+        am.ln_g, am.ln_b, am.lnc_g, am.lnc_b = (_ptr(t) for t in mln)
         am.forget_bias, am.keep = float(forget_bias), float(keep)
         am.seed, am.stream = sd.data_ptr(), int(stream)
         am.ld_lp, am.lp_kind = K, _lp_kind(A)
-        clm = _ClusterSync(T, B, H, dev, C=HYPER_MAIN_C if hmod else 0)
+        clm = _ClusterSync(T, B, H, dev, ln=mln_on, C=HYPER_MAIN_C if hmod else 0)
         clh = _ClusterSync(T, B, Hh, dev)
         st = _stream()
         group = not fp8 and gemm.GROUPED and S_m >= 1 and S_y >= 1 and dt == torch.bfloat16
+
+        def _main_saves(am, t):   # the backward's inputs from the main cell (none at inference)
+            if infer:
+                return
+            if mln_on:
+                am.xhat, am.rstd, am.chat = XHAT[t].data_ptr(), RSTD[t].data_ptr(), CHAT[t].data_ptr()
+            else:
+                am.act, am.c_out = ACT[t].data_ptr(), COUT[t].data_ptr()
         for t in range(T):
             clm.set(am, t)
             clh.set(ah, t)
@@ -324,10 +338,9 @@ class _HyperSeq(torch.autograd.Function):
                 am.xp, am.R, am.vec, am.r_lp = XH[t].data_ptr(), None, None, None
                 am.c_prev, am.step = CC[t].data_ptr(), t
                 am.h_out = Hout[t].data_ptr()
-                if not infer:
-                    am.xhat, am.rstd, am.chat = XHAT[t].data_ptr(), RSTD[t].data_ptr(), CHAT[t].data_ptr()
+                _main_saves(am, t)
                 am.h_lp, am.c_carry = A[t + 1, :, :H].data_ptr(), CC[t + 1].data_ptr()
-                _cell_fwd(lib, am, True, 3, st, "hyper_main_fwd_step")
+                _cell_fwd(lib, am, mln_on, 3, st, "hyper_main_fwd_step")
                 continue
             ah.xp, ah.c_prev, ah.step = XHY[t].data_ptr(), HCC[t].data_ptr(), t
             ah.h_out = HH[t].data_ptr()
@@ -354,17 +367,16 @@ class _HyperSeq(torch.autograd.Function):
             am.r_lp = RLP[t].data_ptr() if (RLP is not None and not hmod) else None
             am.c_prev, am.step = CC[t].data_ptr(), t
             am.h_out = Hout[t].data_ptr()
-            if not infer:
-                am.xhat, am.rstd, am.chat = XHAT[t].data_ptr(), RSTD[t].data_ptr(), CHAT[t].data_ptr()
+            _main_saves(am, t)
             am.h_lp, am.c_carry = A[t + 1, :, :H].data_ptr(), CC[t + 1].data_ptr()
-            _cell_fwd(lib, am, True, mod, st, "hyper_main_fwd_step")
+            _cell_fwd(lib, am, mln_on, mod, st, "hyper_main_fwd_step")
         hT = Hout[T - 1].clone()    # no resets: the carried h is h'
         hhT = HH[T - 1].clone()
         s = _Saved()
         for k, v in dict(xl=xl, x=x, zc=zc, bp=bp, XH=XH, Whl=Whl, Wyl=Wyl, Pl=Pl, q=q, S_m=S_m, A=A, RM=RM,
                          RLP=RLP, CC=CC, HCC=HCC, XHAT=XHAT, RSTD=RSTD, CHAT=CHAT, HH=HH, HXHAT=HXHAT, HRSTD=HRSTD,
                          HCHAT=HCHAT, VEC=VEC, seed=sd, meta=meta, slp=slp, W_h=W_h, W_x=W_x, hW_x=hW_x, W_z=W_z, b_z=b_z, W_a=W_a,
-                         mln=mln, hln=hln, vec_folded=hmod or hfused).items():
+                         mln=mln, hln=hln, vec_folded=hmod or hfused, mln_on=mln_on, ACT=ACT, COUT=COUT).items():
             setattr(s, k, v)
         ctx.s = s
         ctx.dims = (T, B, IX, IN, H, Hh, E)
@@ -391,8 +403,8 @@ class _HyperSeq(torch.autograd.Function):
         dRY_lp = torch.empty(T, B, Gh, device=dev, dtype=ldt) if lp_on else dRY
         dXH = torch.empty(T, B, G, device=dev, dtype=ldt)   # only a GEMM operand downstream
         sdt = torch.bfloat16 if s.slp else f32
-        DLNY = torch.empty(T, B, G, device=dev, dtype=sdt)
-        DLNCY = torch.empty(T, B, H, device=dev, dtype=sdt)
+        DLNY = torch.empty(T, B, G, device=dev, dtype=sdt) if s.mln_on else None
+        DLNCY = torch.empty(T, B, H, device=dev, dtype=sdt) if s.mln_on else None
         HDLNY = torch.empty(T, B, Gh, device=dev, dtype=sdt)
         HDLNCY = torch.empty(T, B, Hh, device=dev, dtype=sdt)
         dVEC = torch.empty(T, B, 12 * H, device=dev, dtype=ldt)
@@ -430,8 +442,8 @@ class _HyperSeq(torch.autograd.Function):
         am.dh_rec, am.ld_dh_rec, am.dhr_nslab, am.dhr_slab = DAY.data_ptr(), K, max(S_ay, 1), B * K
         am.dh_rec2, am.ld_dh_rec2, am.dhr2_nslab, am.dhr2_slab = DAM.data_ptr(), H, max(S_am, 1), B * H
         am.dc_rec, am.dho_nslab = dc_rec.data_ptr(), 1
-        am.ln_g, am.lnc_g, am.lnc_b = s.mln[0].data_ptr(), s.mln[2].data_ptr(), s.mln[3].data_ptr()
-        am.ln_b, am.forget_bias = s.mln[1].data_ptr(), float(forget_bias)
+        am.ln_g, am.lnc_g, am.lnc_b = _ptr(s.mln[0]), _ptr(s.mln[2]), _ptr(s.mln[3])
+        am.ln_b, am.forget_bias = _ptr(s.mln[1]), float(forget_bias)
         am.ld_xp, am.ld_R = G, G
         am.R_nslab, am.R_slab = max(s.S_m, 1), B * G
         # csrc/hyper_mod.hip folds q into the saved vectors
@@ -450,7 +462,7 @@ class _HyperSeq(torch.autograd.Function):
         ah.ln_b, ah.forget_bias = s.hln[1].data_ptr(), float(forget_bias)
         ah.keep, ah.seed, ah.stream = float(hkeep), s.seed.data_ptr(), int(stream) + 1
         ah.ld_dG, ah.ld_dG_lp, ah.dG_lp_kind = Gh, Gh, 1 if lp_on else 0
-        clm, clh = _ClusterSync(T, B, H, dev), _ClusterSync(T, B, Hh, dev)
+        clm, clh = _ClusterSync(T, B, H, dev, ln=s.mln_on), _ClusterSync(T, B, Hh, dev)
         st = _stream()
         group = lp_on and gemm.GROUPED and S_am >= 1 and S_h >= 1
         first = not fin   # (the last time step runs first)
@@ -480,7 +492,11 @@ class _HyperSeq(torch.autograd.Function):
                 ah.dh_rec = None if (first and t == T - 1) else DAY[0, :, H:].data_ptr()
             am.dh_out = dHout[t].data_ptr() if dHout is not None else None
             am.c_prev = s.CC[t].data_ptr()
-            am.xhat, am.rstd, am.chat = s.XHAT[t].data_ptr(), s.RSTD[t].data_ptr(), s.CHAT[t].data_ptr()
+            if s.mln_on:
+                am.xhat, am.rstd, am.chat = s.XHAT[t].data_ptr(), s.RSTD[t].data_ptr(), s.CHAT[t].data_ptr()
+                am.dlny, am.dlncy = DLNY[t].data_ptr(), DLNCY[t].data_ptr()
+            else:
+                am.act, am.c_new = s.ACT[t].data_ptr(), s.COUT[t].data_ptr()
             am.xp, am.vec = s.XH[t].data_ptr(), s.VEC[t].data_ptr()
             if s.RLP is not None:
                 am.R, am.r_lp = None, s.RLP[t].data_ptr()
@@ -490,8 +506,7 @@ class _HyperSeq(torch.autograd.Function):
             am.dG = None if lp_on else dRM[t].data_ptr()
             am.dG_lp = dRM_lp[t].data_ptr() if lp_on else None
             am.dxp, am.dvec = dXH[t].data_ptr(), dVEC[t].data_ptr()
-            am.dlny, am.dlncy = DLNY[t].data_ptr(), DLNCY[t].data_ptr()
-            _cell_bwd(lib, am, True, 2 if s.VEC.dtype == torch.bfloat16 else 1, st, "hyper_main_bwd_step")
+            _cell_bwd(lib, am, s.mln_on, 2 if s.VEC.dtype == torch.bfloat16 else 1, st, "hyper_main_bwd_step")
             ah.c_prev = s.HCC[t].data_ptr()
             ah.xhat, ah.rstd, ah.chat = s.HXHAT[t].data_ptr(), s.HRSTD[t].data_ptr(), s.HCHAT[t].data_ptr()
             ah.step = t
@@ -543,6 +558,9 @@ class _HyperSeq(torch.autograd.Function):
         g_ln, g_hln = [], []
         for dy, xh, n, out in ((DLNY, s.XHAT, G, g_ln), (DLNCY, s.CHAT, H, g_ln), (HDLNY, s.HXHAT, Gh, g_hln),
                                (HDLNCY, s.HCHAT, Hh, g_hln)):
+            if dy is None:   # plain main cell: no LayerNorm parameters
+                out += [None, None]
+                continue
             out += list(colsum(dy.view(-1, n), xh.view(-1, n)))
         dhW_x = torch.empty_like(s.hW_x)
         dhW_x[IN:] = dW_y[:H]
@@ -581,11 +599,10 @@ class _HyperSeq(torch.autograd.Function):
 
 def hyper_sequence_hip(p, x, h0, c0, hh0, hc0, forget_bias=1.0, drop_keep=1.0, drop_seed=0, drop_stream=0,
                        hyp_drop_keep=1.0, zc=None):
-    if not p.use_layer_norm:
-        raise NotImplementedError("HIP HyperLSTM path requires use_layer_norm=True")
+    ln = [p.ln_gamma, p.ln_beta, p.lnc_gamma, p.lnc_beta] if p.use_layer_norm else [None] * 4
     outs = _HyperSeq.apply(x, zc, h0, c0, hh0, hc0, drop_seed, p.W_x, p.W_h, p.bias, p.hyp_W_x, p.hyp_W_h,
                            p.hyp_ln_gamma, p.hyp_ln_beta, p.hyp_lnc_gamma, p.hyp_lnc_beta, p.W_z, p.b_z, p.W_a,
-                           p.ln_gamma, p.ln_beta, p.lnc_gamma, p.lnc_beta,
+                           *ln,
                            (float(forget_bias), float(drop_keep), float(hyp_drop_keep), int(drop_stream), p.embed,
                             _inference(x, zc, h0, p.W_h, p.W_x)))
     Hout, hT, cT, hhT, hcT = outs

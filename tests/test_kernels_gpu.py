@@ -217,6 +217,42 @@ def test_hyper_sequence_matches_oracle(H, Hh, E, keep):
     _close(g_h, g_t, 2e-3, 2e-4, "grad")
 
 
+@pytest.mark.parametrize("dt,B,H,Hh,E", [("fp32", 4, 256, 64, 8), ("bf16", 100, 2048, 256, 32),
+                                          ("bf16", 24, 512, 64, 8)])
+def test_hyper_no_layernorm_vs_oracle(dt, B, H, Hh, E):
+    """HyperLSTM with a plain main cell (use_layer_norm=False; the hyper cell
+    stays a LayerNorm cell, models/cells.py hyper_lstm_step) on the HIP
+    kernels against the fp32 oracle: fp32 operands tight, bf16 at bf16
+    tolerances. The LayerNorm parameters do not exist on this path."""
+    torch.manual_seed(3)
+    T, IN = 5, 13
+    p = C.HyperLSTMParams(IN, H, Hh, E, use_layer_norm=False).to(DEV)
+    assert not hasattr(p, "ln_gamma")
+    with torch.no_grad():
+        for prm in p.parameters():
+            prm.add_(torch.randn_like(prm) * 0.05)
+    x = torch.randn(T, B, IN, device=DEV)
+    st = [torch.randn(B, n, device=DEV) * 0.3 for n in (H, H, Hh, Hh)]
+    w = torch.randn(T, B, H, device=DEV)
+    res = []
+    for backend, d in (("hip", dt), ("torch", "fp32")):
+        ops.set_backend(backend)
+        ops.set_compute_dtype(d)
+        p.zero_grad()
+        out, fin = ops.hyper_sequence(p, x, *st, drop_keep=0.9, drop_seed=4, drop_stream=9, hyp_drop_keep=0.9)
+        loss = (out * w).sum() + sum((f * (0.5 + 0.1 * k)).sum() for k, f in enumerate(fin))
+        loss.backward()
+        torch.cuda.synchronize()
+        res.append([out.detach()] + [f.detach() for f in fin] + [q.grad.clone() for q in p.parameters()])
+    ops.set_compute_dtype("fp32")
+    if dt == "fp32":
+        _close(res[0][:5], res[1][:5], 2e-4, 2e-5, "out")
+        _close(res[0][5:], res[1][5:], 2e-3, 2e-4, "grad")
+    else:
+        _close(res[0][:1], res[1][:1], 3e-2, 3e-2, "out")
+        _close(res[0][5:], res[1][5:], 6e-2, 6e-2, "grad")
+
+
 def _hyper_setup(seed, T, B, IN, Z, H, Hh, E, jitter=0.05, state=0.0):
     torch.manual_seed(seed)
     p = C.HyperLSTMParams(IN + Z, H, Hh, E).to(DEV)

@@ -156,12 +156,15 @@ def _vae_batch(cfg, B=4, seed=0):
     return torch.as_tensor(x), torch.as_tensor(lens), torch.as_tensor(lab)
 
 
-@pytest.mark.parametrize("dec_model,enc_model,nc,embed", [("lstm", "lstm", 0, "add"), ("layer_norm", "layer_norm", 0, "add"),
-                                                          ("hyper", "lstm", 3, "add"), ("lstm", "lstm", 3, "concat")])
-def test_vae_loss_and_grads(dec_model, enc_model, nc, embed):
+@pytest.mark.parametrize("dec_model,enc_model,nc,embed,hln", [("lstm", "lstm", 0, "add", True),
+                                                              ("layer_norm", "layer_norm", 0, "add", True),
+                                                              ("hyper", "lstm", 3, "add", True),
+                                                              ("hyper", "lstm", 0, "add", False),
+                                                              ("lstm", "lstm", 3, "concat", True)])
+def test_vae_loss_and_grads(dec_model, enc_model, nc, embed, hln):
     cfg = VAEConfig(enc_rnn_size=16, dec_rnn_size=24, z_size=8, num_mixture=3, max_seq_len=20, dec_model=dec_model,
                     enc_model=enc_model, hyper_num_units=12, hyper_embedding_size=4, num_classes=nc,
-                    class_embed=embed, use_input_dropout=True, use_output_dropout=True)
+                    class_embed=embed, use_input_dropout=True, use_output_dropout=True, hyper_use_layer_norm=hln)
     m = SketchVAE(cfg, seed=0)
     x, lens, lab = _vae_batch(cfg)
     out = m.loss(x, lens, lab if nc else None, kl_weight=0.3, train=True, seed=2)
