@@ -55,8 +55,23 @@ typedef unsigned int u32x2v __attribute__((ext_vector_type(2)));
 constexpr int kBN = 64, kNS = 3;                 // main / hyper GEMM tiles: 64 columns, 3-stage ring
 constexpr int kEP = 32;                          // embedding padded to one MFMA K step
 constexpr int kZS = 3 * kEP + 8;                 // sZ row stride (bf16): conflict-free 16-byte reads
-constexpr int kGS = kBN + 4;                     // staging row stride (fp32)
-constexpr int kLds = glds_lds_bytes<kBN, kNS>(); // 73,728 B
+constexpr int kLds = glds_lds_bytes<kBN, kNS>(); // 73,728 B (the backward launch)
+// forward launch: the main tiles' epilogue (W_z slice 48 KB + four [32][kZS] z tiles) outgrows the ring
+constexpr int kLdsF = 96 * 256 * 2 + 4 * 32 * kZS * 2 > kLds ? 96 * 256 * 2 + 4 * 32 * kZS * 2 : kLds;
+
+// Diagnostic build only (scripts/build_native.py --variant trace_hstep,
+// scripts/hstep_trace.py): s_memrealtime stamps (100 MHz) per workgroup at
+// the phase boundaries, [block][8] of the last launch.
+#ifdef SKR_TRACE_HSTEP
+__device__ uint64_t* g_hstep_trace;
+#define HS_STAMP(i)                                                                               \
+    do {                                                                                          \
+        if (g_hstep_trace && threadIdx.x == 0)                                                    \
+            g_hstep_trace[(int64_t)blockIdx.x * 8 + (i)] = __builtin_amdgcn_s_memrealtime();      \
+    } while (0)
+#else
+#define HS_STAMP(i) do {} while (0)
+#endif
 
 struct HypFwdArgs {
     int B, H, Hh, S_y;
@@ -73,17 +88,16 @@ struct HypFwdArgs {
     const float* qb;              // [12H] b_z @ W_a (+ the main bias on blocks 8..11)
     float forget_bias, hkeep;
     const int64_t* seed; uint32_t hstream;
-    float* RY;                    // [S_y][B][4Hh] in-launch
-    float* XCH;                   // [4H/64][2][2][2][4][64] f32x4 (8192 floats per tile) in-launch
+    float* RY;                    // [S_y][4Hh/64] fragment-native slab tiles (8192 floats each) in-launch
     __hip_bfloat16* A_next;       // [B][K]: hh_t written into columns H..
     float* HH;                    // [B][Hh]
     float* hc_out;                // [B][Hh]
     void* hxhat; float* hrstd; void* hchat;   // hyper LN saves (null at inference)
     float* GP;                    // [B][4H]
-    float* GS;                    // [B][4][H/64][2]
+    float* GS;                    // [B][4][H/32][2]
     __hip_bfloat16* VEC;          // [B][12H] (blocks 0..7 written) or null
     __hip_bfloat16* RLP;          // [B][4H] or null
-    uint32_t* sync;               // [2 + 2 * 4H/64], zeroed per sequence
+    uint32_t* sync;               // [2], zeroed per sequence
     int* err;
     int save_lp;
 };
@@ -109,49 +123,66 @@ __device__ __forceinline__ void wg_arrive(uint32_t* c) {
     if (threadIdx.x == 0) __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// Split-K slabs handed over inside a launch are stored fragment-native: each
+// lane's f32x4 accumulator (4 consecutive rows of one column) as ONE 16-byte
+// write-through store -- 4-byte sc1 stores (one fabric write each) took
+// 4-6 us per tile under the weight stream (scripts/hstep_trace.py). Layout per
+// slab tile: [4 waves][2 row tiles][4 col tiles][64 lanes][4 rows] floats
+// (8192 floats for 128 rows x 64 columns); frag_idx maps (row, column).
+__device__ __forceinline__ int64_t frag_idx(int64_t tile, int row, int c) {
+    const int w = row >> 5, i = (row >> 4) & 1, fq = (row >> 2) & 3, e = row & 3, j = c >> 4, fr = c & 15;
+    return (((((tile * 4 + w) * 2 + i) * 4 + j) * 64 + fq * 16 + fr) << 2) + e;
+}
+
+__device__ __forceinline__ void st_frag_tile(__amdgpu_buffer_rsrc_t r, int64_t tile, const f32x4 (&acc)[2][4]) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            st_sc1(r, (uint32_t)((((((tile * 4 + w) * 2 + i) * 4 + j) * 64 + lane) * 16)), as_u4(acc[i][j]));
+}
+
 // ---- role 1: R_hyp split-K tile ---------------------------------------------------------
 __device__ void rhyp_tile(const HypFwdArgs& a, int id, __hip_bfloat16* smem) {
     const int K = a.H + a.Hh, Gh = 4 * a.Hh, ntY = Gh / kBN;
     const int nt = id % ntY, s = id / ntY, ksl = K / a.S_y;
     f32x4 acc[2][kBN / 16];
+    HS_STAMP(0);
     glds_mma<kBN, kNS>(a.A, K, a.WyT, K, a.B, nt * kBN, (int64_t)s * ksl, ksl, smem, acc);
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, fr = lane & 15, fq = lane >> 4;
-    const auto r = rsrc(a.RY, (int64_t)a.S_y * a.B * Gh * 4);
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < kBN / 16; ++j)
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                const int row = 32 * w + 16 * i + 4 * fq + e;
-                if (row < a.B)
-                    st_sc1_f32(r, (uint32_t)((((int64_t)s * a.B + row) * Gh + nt * kBN + 16 * j + fr) * 4), acc[i][j][e]);
-            }
+    HS_STAMP(1);
+    st_frag_tile(rsrc(a.RY, (int64_t)a.S_y * ntY * 8192 * 4), (int64_t)s * ntY + nt, acc);
     wg_arrive(&a.sync[0]);
+    HS_STAMP(2);
 }
 
 // ---- role 2: hyper LayerNorm-LSTM cell, one row ------------------------------------------
+// The hand-off (hh_t, 16-byte sc1 stores) is published first; the saves for
+// the backward and the fp32 outputs (read by later launches) are stored after
+// the arrival, off the chain.
 __device__ void hyper_row(const HypFwdArgs& a, int b, int nY) {
+    HS_STAMP(0);
     if (!wg_wait(&a.sync[0], (a.step + 1) * (uint32_t)nY, a.err)) return;
+    HS_STAMP(1);
     __shared__ float lds[4 * 8];
     __shared__ __attribute__((aligned(16))) __hip_bfloat16 hrow[256];
-    const int tid = threadIdx.x, Hh = a.Hh, Gh = 4 * Hh, K = a.H + Hh;
+    const int tid = threadIdx.x, Hh = a.Hh, Gh = 4 * Hh, K = a.H + Hh, ntY = Gh / kBN;
     const bool on = tid < Hh;
     const int u = on ? tid : Hh - 1;
-    const auto ry = rsrc(a.RY, (int64_t)a.S_y * a.B * Gh * 4);
+    const auto ry = rsrc(a.RY, (int64_t)a.S_y * ntY * 8192 * 4);
     float g[4], lg[4], lb[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
         float rs[8];
-        const int64_t idx = (int64_t)b * Gh + q * Hh + u;
+        const int col = q * Hh + u;
 #pragma unroll
         for (int s = 0; s < 8; ++s) {
             const int ss = min(s, a.S_y - 1);
-            rs[s] = ld_sc1_f32(ry, (uint32_t)((ss * (int64_t)a.B * Gh + idx) * 4));
+            rs[s] = ld_sc1_f32(ry, (uint32_t)(frag_idx((int64_t)ss * ntY + (col >> 6), b, col & 63) * 4));
         }
-        g[q] = a.XHY[idx] + slab_fold<8>(rs, a.S_y);
-        lg[q] = a.hln_g[q * Hh + u];
-        lb[q] = a.hln_b[q * Hh + u];
+        g[q] = a.XHY[(int64_t)b * Gh + col] + slab_fold<8>(rs, a.S_y);
+        lg[q] = a.hln_g[col];
+        lb[q] = a.hln_b[col];
     }
     const float cp = a.hc_prev[(int64_t)b * Hh + u];
     const float lcg = a.hlnc_g[u], lcb = a.hlnc_b[u];
@@ -172,8 +203,6 @@ __device__ void hyper_row(const HypFwdArgs& a, int b, int nY) {
         xs[q] = (g[q] - mean) * rs[q];
         g[q] = xs[q] * lg[q] + lb[q];
     }
-    const bool save = a.hxhat != nullptr;
-    if (save && tid < 4) a.hrstd[b * 5 + tid] = rs[tid];
     const int64_t ro = (int64_t)b * Hh + u;
     const bool keep_on = a.hkeep < 1.0f;
     const uint32_t key = keep_on ? hash_key(*a.seed, a.hstream, a.step) : 0u;
@@ -185,9 +214,20 @@ __device__ void hyper_row(const HypFwdArgs& a, int b, int nY) {
     const float mean = s2[0] / (float)Hh;
     const float var = fmaxf(s2[1] / (float)Hh - mean * mean, 0.f);
     const float rc = rsqrtf(var + kLnEps);
-    if (save && tid == 0) a.hrstd[b * 5 + 4] = rc;
     const float ch = (cn - mean) * rc;
     const float h = cell_tanh(ch * lcg + lcb) * og;
+    if (on) hrow[tid] = to_bf16(h);
+    lds_barrier();
+    // hh_t into the next operand, 16-byte write-through stores (read in this launch)
+    if (tid < Hh / 8) {
+        const auto an = rsrc(a.A_next, (int64_t)a.B * K * 2);
+        st_sc1(an, (uint32_t)(((int64_t)b * K + a.H + 8 * tid) * 2), *(const u32x4v*)&hrow[8 * tid]);
+    }
+    wg_arrive(&a.sync[1]);
+    HS_STAMP(2);
+    const bool save = a.hxhat != nullptr;
+    if (save && tid < 4) a.hrstd[b * 5 + tid] = rs[tid];
+    if (save && tid == 0) a.hrstd[b * 5 + 4] = rc;
     if (on) {
         a.HH[ro] = h;
         a.hc_out[ro] = cn;
@@ -196,39 +236,37 @@ __device__ void hyper_row(const HypFwdArgs& a, int b, int nY) {
 #pragma unroll
             for (int q = 0; q < 4; ++q) st_save(a.hxhat, (int64_t)b * Gh + q * Hh + tid, xs[q], a.save_lp);
         }
-        hrow[tid] = to_bf16(h);
     }
-    lds_barrier();
-    // hh_t into the next operand, 16-byte write-through stores (read in this launch)
-    if (tid < Hh / 8) {
-        const auto an = rsrc(a.A_next, (int64_t)a.B * K * 2);
-        st_sc1(an, (uint32_t)(((int64_t)b * K + a.H + 8 * tid) * 2), *(const u32x4v*)&hrow[8 * tid]);
-    }
-    wg_arrive(&a.sync[1]);
 }
 
-// ---- role 3: main tile (R split-K half + modulation + gate pre-activations) -------------
-template <int HHC>   // 16-byte chunks per W_z row (Hh / 8)
-__device__ void main_tile(const HypFwdArgs& a, int r, __hip_bfloat16* smem) {
-    const int H = a.H, Hh = a.Hh, G = 4 * H, K = H + Hh, NV = 12 * H;
-    const int grp = r >> 4, s = (r >> 3) & 1, nt = 8 * grp + (r & 7);
-    const int n0 = nt * kBN, q = n0 / H, u0 = n0 - q * H;
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, fr = lane & 15, fq = lane >> 4;
-    const bool keep = (w >> 1) == s;                 // split 0 finishes rows 0..63, split 1 rows 64..127
-    const bool rows_on = keep && 32 * w < a.B;
+// ---- role 3: main tile (R = h W_h over the full K, modulation, gate pre-activations) ----
+// 32 columns (units u0 .. u0 + 31 of gate q) x all rows, no split-K: nothing
+// to exchange between workgroups (a split-K pair's partial exchange cost
+// 8.5 us under the stream, scripts/hstep_trace.py).
+constexpr int kBNm = 32, kGSm = kBNm + 4;
 
-    f32x4 acc[2][4];
-    glds_mma<kBN, kNS>(a.A, K, a.WhT, H, a.B, n0, (int64_t)s * (H / 2), H / 2, smem, acc);
+template <int HHC>   // 16-byte chunks per W_z row (Hh / 8)
+__device__ void main_tile(const HypFwdArgs& a, int nt, __hip_bfloat16* smem) {
+    constexpr int NJ = kBNm / 16;
+    const int H = a.H, Hh = a.Hh, G = 4 * H, K = H + Hh, NV = 12 * H;
+    const int n0 = nt * kBNm, q = n0 / H, u0 = n0 - q * H;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, fr = lane & 15, fq = lane >> 4;
+    const bool rows_on = 32 * w < a.B;
+
+    f32x4 acc[2][NJ];
+    HS_STAMP(0);
+    glds_mma<kBNm, kNS>(a.A, K, a.WhT, H, a.B, n0, 0, H, smem, acc);
+    HS_STAMP(1);
 
     // ---- prefetch what does not depend on this launch: x-projection, W_a
     // fragments, q; the W_z slice of gate q into LDS (the ring is free)
-    float xv[2][4][4];
-    bf16x8 waf[3][4];
-    float qv[3][4];
+    float xv[2][NJ][4];
+    bf16x8 waf[3][NJ];
+    float qv[3][NJ];
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
+        for (int j = 0; j < NJ; ++j)
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
                 const int row = min(32 * w + 16 * i + 4 * fq + e, a.B - 1);
@@ -237,7 +275,7 @@ __device__ void main_tile(const HypFwdArgs& a, int r, __hip_bfloat16* smem) {
 #pragma unroll
     for (int k = 0; k < 3; ++k)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
+        for (int j = 0; j < NJ; ++j) {
             const int64_t col = (int64_t)(q + 4 * k) * H + u0 + 16 * j + fr;
             waf[k][j] = *(const bf16x8*)(a.WaT + col * kEP + 8 * fq);
             qv[k][j] = a.qb[col];
@@ -245,44 +283,16 @@ __device__ void main_tile(const HypFwdArgs& a, int r, __hip_bfloat16* smem) {
     __syncthreads();                                // every wave is past the ring
     constexpr int SWM = (HHC < 16 ? HHC : 16) - 1;
     __hip_bfloat16* sWz = smem;                     // [96][Hh], 16-byte chunks XOR-swizzled by row
-    __hip_bfloat16* sZ = smem + 96 * HHC * 8 + (w & 1) * (32 * kZS);       // this wave's [32][kZS]
-    float* sG = (float*)(smem + 96 * HHC * 8 + 2 * 32 * kZS) + (w & 1) * (16 * kGS);   // [16][kGS]
+    __hip_bfloat16* sZ = smem + 96 * HHC * 8 + w * (32 * kZS);   // this wave's [32][kZS]
     for (int c = tid; c < 96 * HHC; c += 256) {
         const int row = c / HHC, ch = c - row * HHC, kb = q + 4 * (row >> 5), e = row & 31;
         const bf16x8 v = *(const bf16x8*)(a.WzT + ((int64_t)kb * kEP + e) * Hh + 8 * ch);
         *(bf16x8*)(sWz + row * Hh + ((ch ^ (row & SWM)) << 3)) = v;
     }
-
-    // ---- split-K exchange: hand the partner the half of the rows it finishes
-    const auto xr = rsrc(a.XCH, (int64_t)(G / kBN) * 8192 * 4);   // 2048 f32x4 per tile
-    if (!keep) {
-#pragma unroll
-        for (int i = 0; i < 2; ++i)
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const int64_t o = (((((int64_t)nt * 2 + (1 - s)) * 2 + (w & 1)) * 2 + i) * 4 + j) * 64 + lane;
-                st_sc1(xr, (uint32_t)(o * 16), as_u4(acc[i][j]));
-            }
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();                                // also: the W_z slice is in LDS
-    if (tid == 0) __hip_atomic_store(&a.sync[2 + 2 * nt + s], a.step + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    bool ok = true;
-    if (rows_on) {
-        ok = wait_flags(&a.sync[2 + 2 * nt + (1 - s)], 1, a.step + 1, a.err);
-        if (ok) {
-#pragma unroll
-            for (int i = 0; i < 2; ++i)
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    const int64_t o = (((((int64_t)nt * 2 + s) * 2 + (w & 1)) * 2 + i) * 4 + j) * 64 + lane;
-                    const f32x4 p = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(xr, (uint32_t)(o * 16), 0, kSc1));
-                    acc[i][j] = s == 0 ? acc[i][j] + p : p + acc[i][j];   // R = p0 + p1 in both
-                }
-        }
-    }
-    // ---- wait for every hyper row (hh_t)
-    if (!wg_wait(&a.sync[1], (a.step + 1) * (uint32_t)a.B, a.err) || !ok || !rows_on) return;
+    HS_STAMP(2);
+    // ---- wait for every hyper row (hh_t); the barrier also publishes the W_z slice
+    if (!wg_wait(&a.sync[1], (a.step + 1) * (uint32_t)a.B, a.err) || !rows_on) return;
+    HS_STAMP(3);
 
     // zd = hh_t @ W_z (cols: 3 blocks x 32 embeddings), rows 32w .. 32w + 31
     const auto an = rsrc(a.A_next, (int64_t)a.B * K * 2);
@@ -292,20 +302,22 @@ __device__ void main_tile(const HypFwdArgs& a, int r, __hip_bfloat16* smem) {
     for (int i = 0; i < 2; ++i)
 #pragma unroll
         for (int c = 0; c < 6; ++c) za[i][c] = f32x4{0.f, 0.f, 0.f, 0.f};
+    bf16x8 hf[2][KS];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const int row = 32 * w + 16 * i + fr;
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks)
+            hf[i][ks] = row < a.B ? ld_sc1(an, (uint32_t)(((int64_t)row * K + H + 32 * ks + 8 * fq) * 2)) : bf16x8{};
+    }
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) {
-        bf16x8 hf[2];
-#pragma unroll
-        for (int i = 0; i < 2; ++i) {
-            const int row = 32 * w + 16 * i + fr;
-            hf[i] = row < a.B ? ld_sc1(an, (uint32_t)(((int64_t)row * K + H + 32 * ks + 8 * fq) * 2)) : bf16x8{};
-        }
 #pragma unroll
         for (int c = 0; c < 6; ++c) {
             const int row = (c >> 1) * 32 + 16 * (c & 1) + fr, ch = 4 * ks + fq;
             const bf16x8 bf = *(const bf16x8*)(sWz + row * Hh + ((ch ^ (row & SWM)) << 3));
 #pragma unroll
-            for (int i = 0; i < 2; ++i) za[i][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(hf[i], bf, za[i][c], 0, 0, 0);
+            for (int i = 0; i < 2; ++i) za[i][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(hf[i][ks], bf, za[i][c], 0, 0, 0);
         }
     }
     // bf16(zd) -> LDS [row][3 x 32], read back as the A operand of vec = zd @ W_a
@@ -317,22 +329,27 @@ __device__ void main_tile(const HypFwdArgs& a, int r, __hip_bfloat16* smem) {
             for (int e = 0; e < 4; ++e)
                 sZ[(16 * i + 4 * fq + e) * kZS + (c >> 1) * 32 + 16 * (c & 1) + fr] = to_bf16(za[i][c][e]);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    bf16x8 zf[2][3];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int k = 0; k < 3; ++k) zf[i][k] = *(const bf16x8*)(sZ + (16 * i + fr) * kZS + 32 * k + 8 * fq);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    float* sG = (float*)sZ;                          // the wave's z region, free again: [16][kGSm] stage
+    HS_STAMP(4);
 
     const bool save = a.VEC != nullptr;
-    const int tile = u0 / kBN, ntile = H / kBN;
+    const int tile = u0 / kBNm, ntile = H / kBNm;
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
-        bf16x8 zf[3];
-#pragma unroll
-        for (int k = 0; k < 3; ++k) zf[k] = *(const bf16x8*)(sZ + (16 * i + fr) * kZS + 32 * k + 8 * fq);
-        float gv[4][4], vx[4][4], vh[4][4];
+        float gv[NJ][4], vx[NJ][4], vh[NJ][4];
         float s1[4] = {0.f, 0.f, 0.f, 0.f}, s2[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
+        for (int j = 0; j < NJ; ++j) {
             f32x4 v[3];
 #pragma unroll
             for (int k = 0; k < 3; ++k)
-                v[k] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(zf[k], waf[k][j], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+                v[k] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(zf[i][k], waf[k][j], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
                 // the bf16-rounded vectors are what the backward reads: g uses them too
@@ -347,7 +364,7 @@ __device__ void main_tile(const HypFwdArgs& a, int r, __hip_bfloat16* smem) {
                 s2[e] += gg * gg;
             }
         }
-        // per-row sums over the tile's 64 units: 16-lane DPP row reductions
+        // per-row sums over the tile's 32 units: 16-lane DPP row reductions
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
 #define SKR_ROWSUM(x) x += dpp_f32<0xB1>(x); x += dpp_f32<0x4E>(x); x += dpp_f32<0x141>(x); x += dpp_f32<0x140>(x);
@@ -366,18 +383,18 @@ __device__ void main_tile(const HypFwdArgs& a, int r, __hip_bfloat16* smem) {
                 }
             }
         }
-        // row-contiguous 16-byte stores through a per-wave LDS stage: g (fp32),
+        // row-contiguous 16-byte stores through the wave's LDS stage: g (fp32),
         // then R and the x / h modulation vectors (bf16) for the backward
         auto stage_store = [&](auto&& val, int kind) {
 #pragma unroll
-            for (int j = 0; j < 4; ++j)
+            for (int j = 0; j < NJ; ++j)
 #pragma unroll
-                for (int e = 0; e < 4; ++e) sG[(4 * fq + e) * kGS + 16 * j + fr] = val(j, e);
+                for (int e = 0; e < 4; ++e) sG[(4 * fq + e) * kGSm + 16 * j + fr] = val(j, e);
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
-            for (int p = 0; p < 4; ++p) {
-                const int rr = (lane >> 4) + 4 * p, c4 = lane & 15, row = rbase + rr;
-                const f32x4 v4 = *(const f32x4*)(sG + rr * kGS + 4 * c4);
+            for (int p = 0; p < 2; ++p) {
+                const int rr = (lane >> 3) + 8 * p, c4 = lane & 7, row = rbase + rr;
+                const f32x4 v4 = *(const f32x4*)(sG + rr * kGSm + 4 * c4);
                 if (row < a.B) {
                     if (kind == 0) {
                         *(f32x4*)(a.GP + (int64_t)row * G + n0 + 4 * c4) = v4;
@@ -401,6 +418,7 @@ __device__ void main_tile(const HypFwdArgs& a, int r, __hip_bfloat16* smem) {
             stage_store([&](int j, int e) { return vh[j][e]; }, 3);
         }
     }
+    HS_STAMP(5);
 }
 
 template <int HHC>
@@ -449,7 +467,7 @@ struct HypBwdArgs {
     const __hip_bfloat16* dRM;    // [B][4H]
     const __hip_bfloat16* Whl;    // [H][4H]
     const __hip_bfloat16* Wyl;    // [K][4Hh]
-    float* DHZ;                   // [S_h][B][Hh] in-launch
+    float* DHZ;                   // [S_h][Hh/64] fragment-native slab tiles (8192 floats each) in-launch
     float* DAM;                   // [S_am][B][H]
     float* DAY;                   // [S_ay][B][K]: read (hh part, previous launch) then written
     int dhr_on;                   // 0: no carried-h source this step (first step, no final-state grads)
@@ -470,27 +488,21 @@ __device__ void dvec_tile(const HypBwdArgs& a, int id, __hip_bfloat16* smem) {
     const int NV = 12 * a.H, ntV = a.Hh / kBN;
     const int nt = id % ntV, s = id / ntV, ksl = NV / a.S_h;
     f32x4 acc[2][kBN / 16];
+    HS_STAMP(0);
     glds_mma<kBN, kNS>(a.dVEC, NV, a.Pl, NV, a.B, nt * kBN, (int64_t)s * ksl, ksl, smem, acc);
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, fr = lane & 15, fq = lane >> 4;
-    const auto r = rsrc(a.DHZ, (int64_t)a.S_h * a.B * a.Hh * 4);
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < kBN / 16; ++j)
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                const int row = 32 * w + 16 * i + 4 * fq + e;
-                if (row < a.B)
-                    st_sc1_f32(r, (uint32_t)((((int64_t)s * a.B + row) * a.Hh + nt * kBN + 16 * j + fr) * 4), acc[i][j][e]);
-            }
+    HS_STAMP(1);
+    st_frag_tile(rsrc(a.DHZ, (int64_t)a.S_h * ntV * 8192 * 4), (int64_t)s * ntV + nt, acc);
     wg_arrive(&a.sync[0]);
+    HS_STAMP(2);
 }
 
 __device__ void drm_tile(const HypBwdArgs& a, int id, __hip_bfloat16* smem) {
     const int G = 4 * a.H, ntM = a.H / kBN;
     const int nt = id % ntM, s = id / ntM, ksl = G / a.S_am;
     f32x4 acc[2][kBN / 16];
+    HS_STAMP(0);
     glds_mma<kBN, kNS>(a.dRM, G, a.Whl, G, a.B, nt * kBN, (int64_t)s * ksl, ksl, smem, acc);
+    HS_STAMP(1);
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, fr = lane & 15, fq = lane >> 4;
     float* C = a.DAM + (int64_t)s * a.B * a.H;
 #pragma unroll
@@ -502,6 +514,7 @@ __device__ void drm_tile(const HypBwdArgs& a, int id, __hip_bfloat16* smem) {
                 const int row = 32 * w + 16 * i + 4 * fq + e;
                 if (row < a.B) C[(int64_t)row * a.H + nt * kBN + 16 * j + fr] = acc[i][j][e];
             }
+    HS_STAMP(2);
 }
 
 // hyper LayerNorm-LSTM cell backward, one row (csrc/cell_bwd_body.h semantics:
@@ -509,20 +522,22 @@ __device__ void drm_tile(const HypBwdArgs& a, int id, __hip_bfloat16* smem) {
 // ceiling of the dvec-path slab count
 template <int DHS>
 __device__ void hyper_row_bwd(const HypBwdArgs& a, int b, int nV) {
+    HS_STAMP(0);
     if (!wg_wait(&a.sync[0], a.epoch * (uint32_t)nV, a.err)) return;
+    HS_STAMP(1);
     __shared__ float lds[4 * 8];
     __shared__ __attribute__((aligned(16))) __hip_bfloat16 drow[4 * 256];
-    const int tid = threadIdx.x, Hh = a.Hh, Gh = 4 * Hh, K = a.H + Hh;
+    const int tid = threadIdx.x, Hh = a.Hh, Gh = 4 * Hh, K = a.H + Hh, ntV = Hh / kBN;
     const bool on = tid < Hh;
     const int u = on ? tid : Hh - 1;
     const int64_t ro = (int64_t)b * Hh + u;
     // dh from the vec path (this launch, sc1) + the carried-h path (previous launch)
-    const auto dz = rsrc(a.DHZ, (int64_t)a.S_h * a.B * Hh * 4);
+    const auto dz = rsrc(a.DHZ, (int64_t)a.S_h * ntV * 8192 * 4);
     float t3[DHS];
 #pragma unroll
     for (int s = 0; s < DHS; ++s) {
         const int ss = min(s, a.S_h - 1);
-        t3[s] = ld_sc1_f32(dz, (uint32_t)((ss * (int64_t)a.B * Hh + ro) * 4));
+        t3[s] = ld_sc1_f32(dz, (uint32_t)(frag_idx((int64_t)ss * ntV + (u >> 6), b, u & 63) * 4));
     }
     float t1[8];
     if (a.dhr_on) {
@@ -574,17 +589,14 @@ __device__ void hyper_row_bwd(const HypBwdArgs& a, int b, int nV) {
         acc[q] = dg;
         acc[4 + q] = dg * xh[q];
     }
+    float rsq[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) rsq[q] = a.hrstd[b * 5 + q];
     block_sum<8, 4>(acc, lds);
     if (on) {
-        st_save(a.hdlncy, ro, dcn, a.save_lp);
-        a.dhc_rec[ro] = dcr;
 #pragma unroll
-        for (int q = 0; q < 4; ++q) st_save(a.hdlny, (int64_t)b * Gh + q * Hh + u, dly[q], a.save_lp);
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const float rs = a.hrstd[b * 5 + q];
-            drow[q * Hh + tid] = to_bf16(rs * (dy[q] - acc[q] / (float)Hh - xh[q] * acc[4 + q] / (float)Hh));
-        }
+        for (int q = 0; q < 4; ++q)
+            drow[q * Hh + tid] = to_bf16(rsq[q] * (dy[q] - acc[q] / (float)Hh - xh[q] * acc[4 + q] / (float)Hh));
     }
     lds_barrier();
     if (tid < Gh / 8) {   // dR_hyp row, 16-byte write-through stores (read in this launch)
@@ -592,6 +604,13 @@ __device__ void hyper_row_bwd(const HypBwdArgs& a, int b, int nV) {
         st_sc1(dr, (uint32_t)(((int64_t)b * Gh + 8 * tid) * 2), *(const u32x4v*)&drow[8 * tid]);
     }
     wg_arrive(&a.sync[1]);
+    HS_STAMP(2);
+    if (on) {   // saves for the parameter gradients and the carried-c gradient: after the hand-off
+        st_save(a.hdlncy, ro, dcn, a.save_lp);
+        a.dhc_rec[ro] = dcr;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) st_save(a.hdlny, (int64_t)b * Gh + q * Hh + u, dly[q], a.save_lp);
+    }
 }
 
 // d[h | hh] slab = dR_hyp[:, ks] @ W_y[n-tile, ks]^T; the weight slice is
@@ -604,6 +623,7 @@ __device__ void dry_tile(const HypBwdArgs& a, int id, __hip_bfloat16* smem) {
     const int nt = id % ntY, s = id / ntY, k0 = s * KSL, n0 = nt * kBN;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, fr = lane & 15, fq = lane >> 4;
     bf16x8 wv[PER];
+    HS_STAMP(0);
 #pragma unroll
     for (int p = 0; p < PER; ++p) {
         const int c = tid + 256 * p, row = c / NCH, ch = c - row * NCH;
@@ -614,7 +634,9 @@ __device__ void dry_tile(const HypBwdArgs& a, int id, __hip_bfloat16* smem) {
         const int c = tid + 256 * p, row = c / NCH, ch = c - row * NCH;
         *(bf16x8*)(smem + row * KSL + ((ch ^ (row & SWM)) << 3)) = wv[p];
     }
+    HS_STAMP(1);
     if (!wg_wait(&a.sync[1], a.epoch * (uint32_t)a.B, a.err)) return;   // (its barrier also publishes the slice)
+    HS_STAMP(2);
     const auto dr = rsrc(a.dRY, (int64_t)a.B * Gh * 2);
     bf16x8 af[2][KS];
 #pragma unroll
@@ -648,6 +670,7 @@ __device__ void dry_tile(const HypBwdArgs& a, int id, __hip_bfloat16* smem) {
                 const int row = 32 * w + 16 * i + 4 * fq + e;
                 if (row < a.B) C[(int64_t)row * K + n0 + 16 * j + fr] = acc[i][j][e];
             }
+    HS_STAMP(3);
 }
 
 template <int KSL, int DHS>
@@ -670,27 +693,26 @@ __global__ __launch_bounds__(256, 2) void hyper_bwd_step(const HypBwdArgs a) {
 // S_y <= 8.
 SKR_API int skr_hyper_fwd_step(const HypFwdArgs* args, hipStream_t s) {
     const HypFwdArgs& a = *args;
-    if (a.B < 1 || a.B > BM || a.H % 128 != 0 || (a.Hh != 64 && a.Hh != 128 && a.Hh != 256)) return -2;
-    if (a.S_y < 1 || a.S_y > 8 || ((a.H + a.Hh) / a.S_y) % BK != 0 || (a.H + a.Hh) % a.S_y != 0 || (a.H / 2) % BK)
-        return -3;
-    if (!a.A || !a.WhT || !a.WyT || !a.XH || !a.XHY || !a.hc_prev || !a.WzT || !a.WaT || !a.qb || !a.RY || !a.XCH ||
+    if (a.B < 1 || a.B > BM || a.H % 64 != 0 || (a.Hh != 64 && a.Hh != 128 && a.Hh != 256)) return -2;
+    if (a.S_y < 1 || a.S_y > 8 || ((a.H + a.Hh) / a.S_y) % BK != 0 || (a.H + a.Hh) % a.S_y != 0) return -3;
+    if (!a.A || !a.WhT || !a.WyT || !a.XH || !a.XHY || !a.hc_prev || !a.WzT || !a.WaT || !a.qb || !a.RY ||
         !a.A_next || !a.HH || !a.hc_out || !a.GP || !a.GS || !a.sync || !a.err || !a.seed)
         return -4;
     if (((uintptr_t)a.A | (uintptr_t)a.WhT | (uintptr_t)a.WyT | (uintptr_t)a.WzT | (uintptr_t)a.WaT |
-         (uintptr_t)a.A_next | (uintptr_t)a.GP | (uintptr_t)a.XCH) & 15)
+         (uintptr_t)a.A_next | (uintptr_t)a.GP | (uintptr_t)a.RY) & 15)
         return -4;
-    const int nY = (4 * a.Hh / kBN) * a.S_y, nR = (4 * a.H / kBN) * 2;
-    const int grid = nY + a.B + nR;
+    const int nY = (4 * a.Hh / kBN) * a.S_y, nR = 4 * a.H / kBNm;
+    const int grid = nY + a.B + nR, waiting = a.B + nR;
     auto launch = [&](auto kern) {
         static bool attr = false;
         if (!attr) {
-            (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, kLds);
+            (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsF);
             attr = true;
         }
-        // every workgroup waits only on co-resident ones: refuse a grid the
-        // device cannot hold at once (2 per CU by LDS)
-        if (!grid_fits((const void*)kern, 256, kLds, grid, 2)) return -8;
-        hipLaunchKernelGGL(kern, dim3(grid), dim3(256), kLds, s, a);
+        // the waiting workgroups (hyper rows, main tiles) must leave at least
+        // one slot for a producer, whatever the dispatch order (2 per CU by LDS)
+        if (!grid_fits((const void*)kern, 256, kLdsF, waiting + 1, 2)) return -8;
+        hipLaunchKernelGGL(kern, dim3(grid), dim3(256), kLdsF, s, a);
         return SKR_CHECK_LAUNCH();
     };
     switch (a.Hh) {
@@ -749,3 +771,14 @@ SKR_API int skr_hyper_bwd_step(const HypBwdArgs* args, hipStream_t s) {
 }
 
 SKR_API int skr_hyper_bwd_args_size() { return (int)sizeof(HypBwdArgs); }
+
+// Diagnostic build: point the phase stamps at a device buffer ([grid][8] uint64; null: off).
+SKR_API int skr_hstep_trace(void* buf) {
+#ifdef SKR_TRACE_HSTEP
+    uint64_t* p = (uint64_t*)buf;
+    return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_hstep_trace), &p, sizeof(p));
+#else
+    (void)buf;
+    return -1;
+#endif
+}

@@ -286,7 +286,7 @@ class HypFwdArgs(C.Structure):
         ("WzT", _p), ("WaT", _p), ("qb", _p),
         ("forget_bias", _f), ("hkeep", _f),
         ("seed", _p), ("hstream", _u32),
-        ("RY", _p), ("XCH", _p), ("A_next", _p), ("HH", _p), ("hc_out", _p),
+        ("RY", _p), ("A_next", _p), ("HH", _p), ("hc_out", _p),
         ("hxhat", _p), ("hrstd", _p), ("hchat", _p),
         ("GP", _p), ("GS", _p), ("VEC", _p), ("RLP", _p),
         ("sync", _p), ("err", _p),
@@ -419,6 +419,8 @@ class HipLib:
         lib.skr_hyper_fwd_step.restype = _i
         lib.skr_hyper_bwd_step.argtypes = [C.POINTER(HypBwdArgs), _p]
         lib.skr_hyper_bwd_step.restype = _i
+        lib.skr_hstep_trace.argtypes = [_p]
+        lib.skr_hstep_trace.restype = _i
         lib.skr_cast_transpose_bf16.argtypes = [_p, _i64, _i64, _i, _i, _i, _p, _i64, _i64, _p, _i64, _i64, _p]
         lib.skr_cast_transpose_bf16.restype = _i
         lib.skr_hash_normal.argtypes = [_p, _u32, _u32, _p, _i64, _p]

@@ -200,7 +200,7 @@ class _HyperSeq(torch.autograd.Function):
         rgemm = (lambda a, b, out, S: gemm.rec_gemm_fp8(a, b, out, S)) if fp8 else \
             (lambda a, b, out, S: gemm.rec_gemm(a, b, out, S))
         hfused = (HYPER_FUSED and not fp8 and dt == torch.bfloat16 and dev.type == "cuda" and B <= 128 and
-                  H % 128 == 0 and Hh in (64, 128, 256) and E <= 32 and 1 <= S_y <= 8 and K % S_y == 0 and
+                  H % 64 == 0 and Hh in (64, 128, 256) and E <= 32 and 1 <= S_y <= 8 and K % S_y == 0 and
                   (K // S_y) % 64 == 0)
         A = torch.empty(T + 1, B, K, device=dev, dtype=torch.uint8 if fp8 else dt)
         A[0, :, :H].copy_(_to_fp8_act(h0) if fp8 else h0)
@@ -264,9 +264,9 @@ class _HyperSeq(torch.autograd.Function):
                 return WzT, WaT
             WzT, WaT = gemm.derived((W_z, W_a), "hypunfold", unfold) if infer else unfold(W_z, W_a)
             GP = torch.empty(B, G, device=dev, dtype=f32)
-            GS = torch.empty(B, 4, H // 64, 2, device=dev, dtype=f32)
-            XCH = torch.empty((G // 64) * 8192, device=dev, dtype=f32)
-            SYNC = torch.zeros(2 + 2 * (G // 64), device=dev, dtype=torch.int32)
+            GS = torch.empty(B, 4, H // 32, 2, device=dev, dtype=f32)
+            RYf = torch.empty(S_y * (Gh // 64) * 8192, device=dev, dtype=f32)   # fragment-native slab tiles
+            SYNC = torch.zeros(2, device=dev, dtype=torch.int32)
             XHc, XHYc = XH.contiguous(), XHY.contiguous()
             hf = HypFwdArgs()
             hf.B, hf.H, hf.Hh, hf.S_y = B, H, Hh, S_y
@@ -274,7 +274,7 @@ class _HyperSeq(torch.autograd.Function):
             hf.hln_g, hf.hln_b, hf.hlnc_g, hf.hlnc_b = (t_.data_ptr() for t_ in hln)
             hf.forget_bias, hf.hkeep = float(forget_bias), float(hkeep)
             hf.seed, hf.hstream = sd.data_ptr(), int(stream) + 1
-            hf.RY, hf.XCH, hf.GP, hf.GS, hf.sync = (t_.data_ptr() for t_ in (RY, XCH, GP, GS, SYNC))
+            hf.RY, hf.GP, hf.GS, hf.sync = (t_.data_ptr() for t_ in (RYf, GP, GS, SYNC))
             hf.err = cluster_error_flag(dev).data_ptr()
             hf.save_lp = int(slp)
         if hmod:
@@ -334,7 +334,7 @@ class _HyperSeq(torch.autograd.Function):
                 hf.VEC = VEC[t].data_ptr() if VEC is not None else None
                 hf.RLP = RLP[t].data_ptr() if RLP is not None else None
                 _check(lib.lib.skr_hyper_fwd_step(ctypes.byref(hf), st), "hyper_fwd_step")
-                am.gpre, am.gstats, am.gstat_tiles = GP.data_ptr(), GS.data_ptr(), H // 64
+                am.gpre, am.gstats, am.gstat_tiles = GP.data_ptr(), GS.data_ptr(), H // 32
                 am.xp, am.R, am.vec, am.r_lp = XH[t].data_ptr(), None, None, None
                 am.c_prev, am.step = CC[t].data_ptr(), t
                 am.h_out = Hout[t].data_ptr()
@@ -423,6 +423,7 @@ class _HyperSeq(torch.autograd.Function):
             S_ay = next(d for d in (4, 3, 2, 1) if (Gh // 64) % d == 0)
         S_ay = _split_override("SKR_HYP_SAY", S_ay, Gh)
         DHZ = torch.empty(max(S_h, 1), B, Hh, device=dev, dtype=f32)    # slabs of dhh from the vec path
+        DHZf = None
         # dh slabs of step t + 1 read by step t; the last step reads none (null
         # sources) unless gradients flow into the final states
         fin = dhT is not None or dhhT is not None
@@ -472,10 +473,11 @@ class _HyperSeq(torch.autograd.Function):
                and K % 64 == 0)
         BWD_STATS["fused" if hbs else "chain"] += 1
         if hbs:
+            DHZf = torch.empty(S_h * (Hh // 64) * 8192, device=dev, dtype=f32)   # fragment-native slab tiles
             hb = HypBwdArgs()
             hb.B, hb.H, hb.Hh, hb.S_h, hb.S_am, hb.S_ay = B, H, Hh, S_h, S_am, S_ay
             hb.Pl, hb.Whl, hb.Wyl = s.Pl.data_ptr(), s.Whl.data_ptr(), s.Wyl.data_ptr()
-            hb.DHZ, hb.DAM, hb.DAY = DHZ.data_ptr(), DAM.data_ptr(), DAY.data_ptr()
+            hb.DHZ, hb.DAM, hb.DAY = DHZf.data_ptr(), DAM.data_ptr(), DAY.data_ptr()
             hb.dhc_rec = dhc_rec.data_ptr()
             hb.hln_g, hb.hln_b, hb.hlnc_g, hb.hlnc_b = (t_.data_ptr() for t_ in s.hln)
             hb.forget_bias, hb.hkeep = float(forget_bias), float(hkeep)

@@ -456,6 +456,34 @@ def test_hyper_long_sequence_vs_oracle():
     assert ok, ("bf16 out, t < 20", err)
 
 
+def test_hyper_bf16_gradients_b100_t50_cosine():
+    """Shipped numerics at the headline geometry: B = 100 rows (the fused
+    forward / backward launches, the row-kernel backward), H = 2048, T = 50,
+    the model's own initialisation, dropout on. Every weight gradient of the
+    bf16 HIP path points the same way as the fp32 oracle's: cosine >= 0.98
+    (bf16 rounding alone measures ~0.999+); for scale, the same statistic of
+    the oracle against itself with the input perturbed by 1e-6 is recorded
+    in the assertion message."""
+    p, x, z, st, w = _hyper_setup(21, 50, 100, 5, 16, 2048, 256, 32, jitter=0.0, state=0.0)
+    runs = {}
+    for name, backend, dt, xx in (("ref", "torch", "fp32", x), ("pert", "torch", "fp32", x + 1e-6 * torch.randn_like(x)),
+                                  ("bf16", "hip", "bf16", x)):
+        ops.set_backend(backend)
+        ops.set_compute_dtype(dt)
+        runs[name] = _hyper_run(p, xx, z, st, w, keep=0.9, hkeep=0.9, fin_w=False)
+    ops.set_compute_dtype("fp32")
+    names = _names(p)
+    for i, n in enumerate(names):
+        if n in ("out", "h", "c", "hh", "hc"):
+            continue
+        ref, got, pert = (runs[k][i].double().flatten() for k in ("ref", "bf16", "pert"))
+        if ref.norm() == 0:
+            continue
+        cos = float(got @ ref / (got.norm() * ref.norm()))
+        cos_p = float(pert @ ref / (pert.norm() * ref.norm()))
+        assert cos >= 0.98, (n, cos, cos_p)
+
+
 @pytest.mark.parametrize("M,N,K,nd", [(100, 9216, 2304, 1), (100, 2304, 9216, 1), (100, 256, 24576, 1),
                                       (100, 24576, 256, 1), (7, 64, 64, 1), (128, 2048, 512, 2),
                                       (100, 512, 2048, 2), (256, 8192, 2048, 1), (512, 1024, 256, 1)])
