@@ -85,7 +85,7 @@ def build_host(force=False):
 
 # Experiment builds (A/B against the default library, loaded with
 # SKR_HIP_LIB=<path>): extra defines per variant.
-VARIANTS = {"exact_act": ["-DSKR_EXACT_ACT"], "trace_hstep": ["-DSKR_TRACE_HSTEP"]}
+VARIANTS = {"exact_act": ["-DSKR_EXACT_ACT"]}
 
 
 def build_hip(force=False, jobs=8, variant=None):

@@ -275,44 +275,6 @@ class GemmProblem8(C.Structure):
     ]
 
 
-class HypFwdArgs(C.Structure):
-    """Mirror of ``HypFwdArgs`` in csrc/hyper_step.hip (fused HyperLSTM forward step)."""
-    _fields_ = [
-        ("B", _i), ("H", _i), ("Hh", _i), ("S_y", _i),
-        ("step", _u32),
-        ("A", _p), ("WhT", _p), ("WyT", _p),
-        ("XH", _p), ("XHY", _p), ("hc_prev", _p),
-        ("hln_g", _p), ("hln_b", _p), ("hlnc_g", _p), ("hlnc_b", _p),
-        ("WzT", _p), ("WaT", _p), ("qb", _p),
-        ("forget_bias", _f), ("hkeep", _f),
-        ("seed", _p), ("hstream", _u32),
-        ("RY", _p), ("A_next", _p), ("HH", _p), ("hc_out", _p),
-        ("hxhat", _p), ("hrstd", _p), ("hchat", _p),
-        ("GP", _p), ("GS", _p), ("VEC", _p), ("RLP", _p),
-        ("sync", _p), ("err", _p),
-        ("save_lp", _i),
-    ]
-
-
-class HypBwdArgs(C.Structure):
-    """Mirror of ``HypBwdArgs`` in csrc/hyper_step.hip (fused HyperLSTM backward step)."""
-    _fields_ = [
-        ("B", _i), ("H", _i), ("Hh", _i), ("S_h", _i), ("S_am", _i), ("S_ay", _i),
-        ("epoch", _u32), ("step", _u32),
-        ("dVEC", _p), ("Pl", _p), ("dRM", _p), ("Whl", _p), ("Wyl", _p),
-        ("DHZ", _p), ("DAM", _p), ("DAY", _p),
-        ("dhr_on", _i),
-        ("dhc_rec", _p), ("hc_prev", _p),
-        ("hchat", _p), ("hxhat", _p), ("hrstd", _p),
-        ("hln_g", _p), ("hln_b", _p), ("hlnc_g", _p), ("hlnc_b", _p),
-        ("forget_bias", _f), ("hkeep", _f),
-        ("seed", _p), ("hstream", _u32),
-        ("dRY", _p), ("hdlny", _p), ("hdlncy", _p),
-        ("sync", _p), ("err", _p),
-        ("save_lp", _i),
-    ]
-
-
 class HipLib:
     def __init__(self, lib: C.CDLL):
         self.lib = lib
@@ -415,12 +377,6 @@ class HipLib:
         lib.skr_skinny_gemm_group_fp8.restype = _i
         lib.skr_hyper_mod_fwd.argtypes = [_p, _i64, _p, _p, _p, _p, _i64, _i, _p, _p, _p, _p, _i, _i, _i, _p]
         lib.skr_hyper_mod_fwd.restype = _i
-        lib.skr_hyper_fwd_step.argtypes = [C.POINTER(HypFwdArgs), _p]
-        lib.skr_hyper_fwd_step.restype = _i
-        lib.skr_hyper_bwd_step.argtypes = [C.POINTER(HypBwdArgs), _p]
-        lib.skr_hyper_bwd_step.restype = _i
-        lib.skr_hstep_trace.argtypes = [_p]
-        lib.skr_hstep_trace.restype = _i
         lib.skr_cast_transpose_bf16.argtypes = [_p, _i64, _i64, _i, _i, _i, _p, _i64, _i64, _p, _i64, _i64, _p]
         lib.skr_cast_transpose_bf16.restype = _i
         lib.skr_hash_normal.argtypes = [_p, _u32, _u32, _p, _i64, _p]
@@ -438,8 +394,6 @@ class HipLib:
                           ("skr_mdn_head_dw_args_size", HeadDw),
                           ("skr_decode_ref_args_size", DecArgs),
                           ("skr_gemm_problem_size", GemmProblem),
-                          ("skr_hyper_fwd_args_size", HypFwdArgs),
-                          ("skr_hyper_bwd_args_size", HypBwdArgs),
                           ("skr_gemm_problem8_size", GemmProblem8)):
             fn = getattr(lib, name)
             fn.restype = _i

@@ -15,18 +15,16 @@ geometry, seeds) lives in :mod:`.recurrent`.
 """
 from __future__ import annotations
 
-import ctypes
 import os
 
 import torch
 
 from ..utils import native
 from . import gemm
-from ._hipapi import HypBwdArgs, HypFwdArgs, LstmBwdArgs, LstmFwdArgs
+from ._hipapi import LstmBwdArgs, LstmFwdArgs
 from .inproj import bproj_fwd, bproj_ok, bproj_reduce
 from .recurrent import (ROW_STATS, _cell_bwd, _cell_fwd, _check, _ClusterSync, _fp8_ok, _inference, _ln_saves_lp,
-                        _lp_kind, _ptr, _Saved, _seed_tensor, _stream, _to_fp8_act, cell_geometry,
-                        cluster_error_flag)
+                        _lp_kind, _ptr, _Saved, _seed_tensor, _stream, _to_fp8_act, cell_geometry)
 from .reduce import colsum
 
 # The modulation GEMM fused with the main gates' pre-activations and
@@ -40,17 +38,11 @@ HYPER_MAIN_C = int(os.environ.get("SKR_HYPER_MAIN_C", "0"))   # workgroups per r
 # product only the next step reads. SKR_HYPER_BWD_FUSE=0 keeps [main cell] ->
 # [dR_main W_h^T + dvec P^T] -> [hyper cell] -> [dR_hyp W_y^T].
 HYPER_BWD_FUSE = os.environ.get("SKR_HYPER_BWD_FUSE", "1") != "0"
-# Forward step as TWO launches (csrc/hyper_step.hip + the MOD-3 main cell):
-# R_hyp, the hyper cell, h @ W_h and the unfolded modulation (zd = hh @ W_z,
-# vec = zd @ W_a + q) with the gate pre-activations in one launch.
-# SKR_HYPER_FUSED=0 keeps the four-launch chain below.
-HYPER_FUSED = os.environ.get("SKR_HYPER_FUSED", "1") != "0"
-FWD_STATS = {"fused": 0, "chain": 0}   # sequences by forward schedule (tests check the hot path's)
-# Backward step as TWO launches: [main cell] -> [dvec P^T | hyper cell |
-# dR_hyp W_y^T chained in-launch, beside dR_main W_h^T] (csrc/hyper_step.hip
-# skr_hyper_bwd_step). SKR_HYPER_BWD_STEP=0 keeps the four-launch order.
-HYPER_BWD_STEP = os.environ.get("SKR_HYPER_BWD_STEP", "1") != "0"
-BWD_STATS = {"fused": 0, "chain": 0}
+# (Round 4 measured one-launch forward / backward steps -- R_hyp, hyper cell,
+# h @ W_h and the modulation with in-launch hand-offs; the backward chain
+# beside dR_main W_h^T -- at +1.5 / +3.8 ms per training step: every
+# in-launch dependency level cost as much as a kernel boundary,
+# profiles/r4/hyper_fused_step_ab.txt.)
 # (The forward twin -- h W_y alone, then the hyper cell beside h W_h in one
 # launch -- measured 0.15 ms/step slower on vae_large and was removed:
 # profiles/r3/hyper_fused_cell_ab.txt.)
@@ -199,16 +191,13 @@ class _HyperSeq(torch.autograd.Function):
             S_v = gemm.plan_splits(B, 12 * H, Hh, 1, dt, max_splits=1)
         rgemm = (lambda a, b, out, S: gemm.rec_gemm_fp8(a, b, out, S)) if fp8 else \
             (lambda a, b, out, S: gemm.rec_gemm(a, b, out, S))
-        hfused = (HYPER_FUSED and not fp8 and dt == torch.bfloat16 and dev.type == "cuda" and B <= 128 and
-                  H % 64 == 0 and Hh in (64, 128, 256) and E <= 32 and 1 <= S_y <= 8 and K % S_y == 0 and
-                  (K // S_y) % 64 == 0)
         A = torch.empty(T + 1, B, K, device=dev, dtype=torch.uint8 if fp8 else dt)
         A[0, :, :H].copy_(_to_fp8_act(h0) if fp8 else h0)
         A[0, :, H:].copy_(_to_fp8_act(hh0) if fp8 else hh0)
         # R_main: the backward re-reads it (the hyper-modulation gradient
         # dg * R) as the bf16 copy the main cell saves (RLP); with fp32 GEMM
         # operands the fp32 split-K slabs of every step are kept instead
-        vbf = not fp8 and dt == torch.bfloat16 and B <= 128 and (S_v == 1 or hfused)
+        vbf = not fp8 and dt == torch.bfloat16 and B <= 128 and S_v == 1
         RLP = torch.empty(T, B, G, device=dev, dtype=torch.bfloat16) if (vbf and not infer) else None
         CC = torch.empty(T + 1, B, H, device=dev, dtype=f32)
         CC[0].copy_(c0)
@@ -230,53 +219,21 @@ class _HyperSeq(torch.autograd.Function):
             ACT, COUT = sv(T, B, G), sv(T, B, H)
         HXHAT, HRSTD, HCHAT = sv(T, B, Gh, dt=sdt), sv(T, B, 5), sv(T, B, Hh, dt=sdt)
         # modulation vectors in bf16 when the GEMMs are bf16 (read only by the main cells)
-        VEC = None if (hfused and infer) else torch.empty(T, B, 12 * H, device=dev,
-                                                          dtype=torch.bfloat16 if vbf else f32)
+        VEC = torch.empty(T, B, 12 * H, device=dev, dtype=torch.bfloat16 if vbf else f32)
         sd = _seed_tensor(seed, dev)
         hln = [t.contiguous() for t in (hln_g, hln_b, hlnc_g, hlnc_b)]
         mln = [t.contiguous() for t in (ln_g, ln_b, lnc_g, lnc_b)] if mln_on else [None] * 4
         bias_c = bias.contiguous()
-        RM = None if hfused else torch.empty(T if (RLP is None and not infer) else 1, max(S_m, 1), B, G, device=dev,
-                                             dtype=f32)
-        rmi = (lambda t: t) if (RM is not None and RM.shape[0] == T) else (lambda t: 0)
+        RM = torch.empty(T if (RLP is None and not infer) else 1, max(S_m, 1), B, G, device=dev, dtype=f32)
+        rmi = (lambda t: t) if RM.shape[0] == T else (lambda t: 0)
         RY = torch.empty(max(S_y, 1), B, Gh, device=dev, dtype=f32)
         mod = 2 if vbf else 1
         # modulation step fused with the gate pre-activations and their
         # LayerNorm partial sums (csrc/hyper_mod.hip): the main cell then needs
         # no statistics exchange for the gates (MOD 3) and VEC carries q (and
         # the main bias in its shift block) -- the backward uses a zero vec_bias
-        hmod = not hfused and HYPER_MOD and vbf and dev.type == "cuda" and Hh == 256 and B <= 112 and H % 32 == 0 and \
+        hmod = HYPER_MOD and vbf and dev.type == "cuda" and Hh == 256 and B <= 112 and H % 32 == 0 and \
             S_m in (1, 2, 4)
-        FWD_STATS["fused" if hfused else "chain"] += 1
-        if hfused:   # csrc/hyper_step.hip: q + the main bias on the shift block, unfolded projections in bf16
-            if qb_f is not None:
-                qb = qb_f
-            else:
-                qb = q.detach().clone()
-                qb[8:] += bias_c.detach().view(4, H)
-                qb = qb.reshape(12 * H).contiguous()
-
-            def unfold(W_z, W_a):    # [12 x 32, Hh] and [12, H, 32] bf16 (embedding padded to 32)
-                WzT = torch.zeros(12, 32, Hh, device=dev, dtype=torch.bfloat16)
-                WzT[:, :E] = W_z.detach().view(Hh, 12, E).permute(1, 2, 0)
-                WaT = torch.zeros(12, H, 32, device=dev, dtype=torch.bfloat16)
-                WaT[:, :, :E] = W_a.detach().permute(0, 2, 1)
-                return WzT, WaT
-            WzT, WaT = gemm.derived((W_z, W_a), "hypunfold", unfold) if infer else unfold(W_z, W_a)
-            GP = torch.empty(B, G, device=dev, dtype=f32)
-            GS = torch.empty(B, 4, H // 32, 2, device=dev, dtype=f32)
-            RYf = torch.empty(S_y * (Gh // 64) * 8192, device=dev, dtype=f32)   # fragment-native slab tiles
-            SYNC = torch.zeros(2, device=dev, dtype=torch.int32)
-            XHc, XHYc = XH.contiguous(), XHY.contiguous()
-            hf = HypFwdArgs()
-            hf.B, hf.H, hf.Hh, hf.S_y = B, H, Hh, S_y
-            hf.WhT, hf.WyT, hf.WzT, hf.WaT, hf.qb = (t_.data_ptr() for t_ in (WhT, WyT, WzT, WaT, qb))
-            hf.hln_g, hf.hln_b, hf.hlnc_g, hf.hlnc_b = (t_.data_ptr() for t_ in hln)
-            hf.forget_bias, hf.hkeep = float(forget_bias), float(hkeep)
-            hf.seed, hf.hstream = sd.data_ptr(), int(stream) + 1
-            hf.RY, hf.GP, hf.GS, hf.sync = (t_.data_ptr() for t_ in (RYf, GP, GS, SYNC))
-            hf.err = cluster_error_flag(dev).data_ptr()
-            hf.save_lp = int(slp)
         if hmod:
             mod = 3
             if qb_f is not None:   # q + the main bias on the shift block, from the fold kernel
@@ -324,24 +281,6 @@ class _HyperSeq(torch.autograd.Function):
         for t in range(T):
             clm.set(am, t)
             clh.set(ah, t)
-            if hfused:   # [R_hyp | hyper cell | h W_h + modulation + gate pre-activations] -> [main cell]
-                hf.step = t
-                hf.A, hf.A_next = A[t].data_ptr(), A[t + 1].data_ptr()
-                hf.XH, hf.XHY = XHc[t].data_ptr(), XHYc[t].data_ptr()
-                hf.hc_prev, hf.hc_out, hf.HH = HCC[t].data_ptr(), HCC[t + 1].data_ptr(), HH[t].data_ptr()
-                if not infer:
-                    hf.hxhat, hf.hrstd, hf.hchat = HXHAT[t].data_ptr(), HRSTD[t].data_ptr(), HCHAT[t].data_ptr()
-                hf.VEC = VEC[t].data_ptr() if VEC is not None else None
-                hf.RLP = RLP[t].data_ptr() if RLP is not None else None
-                _check(lib.lib.skr_hyper_fwd_step(ctypes.byref(hf), st), "hyper_fwd_step")
-                am.gpre, am.gstats, am.gstat_tiles = GP.data_ptr(), GS.data_ptr(), H // 32
-                am.xp, am.R, am.vec, am.r_lp = XH[t].data_ptr(), None, None, None
-                am.c_prev, am.step = CC[t].data_ptr(), t
-                am.h_out = Hout[t].data_ptr()
-                _main_saves(am, t)
-                am.h_lp, am.c_carry = A[t + 1, :, :H].data_ptr(), CC[t + 1].data_ptr()
-                _cell_fwd(lib, am, mln_on, 3, st, "hyper_main_fwd_step")
-                continue
             ah.xp, ah.c_prev, ah.step = XHY[t].data_ptr(), HCC[t].data_ptr(), t
             ah.h_out = HH[t].data_ptr()
             if not infer:
@@ -376,7 +315,7 @@ class _HyperSeq(torch.autograd.Function):
         for k, v in dict(xl=xl, x=x, zc=zc, bp=bp, XH=XH, Whl=Whl, Wyl=Wyl, Pl=Pl, q=q, S_m=S_m, A=A, RM=RM,
                          RLP=RLP, CC=CC, HCC=HCC, XHAT=XHAT, RSTD=RSTD, CHAT=CHAT, HH=HH, HXHAT=HXHAT, HRSTD=HRSTD,
                          HCHAT=HCHAT, VEC=VEC, seed=sd, meta=meta, slp=slp, W_h=W_h, W_x=W_x, hW_x=hW_x, W_z=W_z, b_z=b_z, W_a=W_a,
-                         mln=mln, hln=hln, vec_folded=hmod or hfused, mln_on=mln_on, ACT=ACT, COUT=COUT).items():
+                         mln=mln, hln=hln, vec_folded=hmod, mln_on=mln_on, ACT=ACT, COUT=COUT).items():
             setattr(s, k, v)
         ctx.s = s
         ctx.dims = (T, B, IX, IN, H, Hh, E)
@@ -423,7 +362,6 @@ class _HyperSeq(torch.autograd.Function):
             S_ay = next(d for d in (4, 3, 2, 1) if (Gh // 64) % d == 0)
         S_ay = _split_override("SKR_HYP_SAY", S_ay, Gh)
         DHZ = torch.empty(max(S_h, 1), B, Hh, device=dev, dtype=f32)    # slabs of dhh from the vec path
-        DHZf = None
         # dh slabs of step t + 1 read by step t; the last step reads none (null
         # sources) unless gradients flow into the final states
         fin = dhT is not None or dhhT is not None
@@ -467,24 +405,6 @@ class _HyperSeq(torch.autograd.Function):
         st = _stream()
         group = lp_on and gemm.GROUPED and S_am >= 1 and S_h >= 1
         first = not fin   # (the last time step runs first)
-        hbs = (HYPER_BWD_STEP and lp_on and dev.type == "cuda" and B <= 128 and H % 64 == 0 and Hh in (64, 128, 256)
-               and 1 <= S_h <= 64 and (12 * H) % S_h == 0 and (12 * H // S_h) % 64 == 0 and S_am >= 1 and
-               (G // S_am) % 64 == 0 and 1 <= S_ay <= 8 and Gh % S_ay == 0 and Gh // S_ay in (64, 128, 256)
-               and K % 64 == 0)
-        BWD_STATS["fused" if hbs else "chain"] += 1
-        if hbs:
-            DHZf = torch.empty(S_h * (Hh // 64) * 8192, device=dev, dtype=f32)   # fragment-native slab tiles
-            hb = HypBwdArgs()
-            hb.B, hb.H, hb.Hh, hb.S_h, hb.S_am, hb.S_ay = B, H, Hh, S_h, S_am, S_ay
-            hb.Pl, hb.Whl, hb.Wyl = s.Pl.data_ptr(), s.Whl.data_ptr(), s.Wyl.data_ptr()
-            hb.DHZ, hb.DAM, hb.DAY = DHZf.data_ptr(), DAM.data_ptr(), DAY.data_ptr()
-            hb.dhc_rec = dhc_rec.data_ptr()
-            hb.hln_g, hb.hln_b, hb.hlnc_g, hb.hlnc_b = (t_.data_ptr() for t_ in s.hln)
-            hb.forget_bias, hb.hkeep = float(forget_bias), float(hkeep)
-            hb.seed, hb.hstream = s.seed.data_ptr(), int(stream) + 1
-            HSYNC = torch.zeros(2, device=dev, dtype=torch.int32)
-            hb.sync, hb.err = HSYNC.data_ptr(), cluster_error_flag(dev).data_ptr()
-            hb.save_lp = int(s.slp)
         for t in range(T - 1, -1, -1):
             clm.set(am, t)
             clh.set(ah, t)
@@ -515,15 +435,6 @@ class _HyperSeq(torch.autograd.Function):
             ah.dG = None if lp_on else dRY[t].data_ptr()
             ah.dG_lp = dRY_lp[t].data_ptr() if lp_on else None
             ah.dlny, ah.dlncy = HDLNY[t].data_ptr(), HDLNCY[t].data_ptr()
-            if hbs:   # [dvec P^T -> hyper cell -> dR_hyp W_y^T] beside dR_main W_h^T, one launch
-                hb.epoch, hb.step = T - t, t
-                hb.dVEC, hb.dRM, hb.dRY = dVEC[t].data_ptr(), dRM_lp[t].data_ptr(), dRY_lp[t].data_ptr()
-                hb.dhr_on = 0 if (first and t == T - 1) else 1
-                hb.hc_prev = s.HCC[t].data_ptr()
-                hb.hchat, hb.hxhat, hb.hrstd = s.HCHAT[t].data_ptr(), s.HXHAT[t].data_ptr(), s.HRSTD[t].data_ptr()
-                hb.hdlny, hb.hdlncy = HDLNY[t].data_ptr(), HDLNCY[t].data_ptr()
-                _check(lib.lib.skr_hyper_bwd_step(ctypes.byref(hb), st), "hyper_bwd_step")
-                continue
             if bfuse:   # dvec P^T, then the hyper cell beside dR_main W_h^T (one launch)
                 gemm.rec_gemm(dVEC[t], s.Pl, DHZ, S_h)
                 gemm.rec_gemm_group_cellbwd([(dRM_lp[t], s.Whl, DAM, S_am)], ah)
