@@ -362,6 +362,20 @@ def rec_gemm_group_cellbwd(jobs, cell_args) -> None:
         raise RuntimeError("skr_skinny_gemm_group_cellbwd failed (%d)" % rc)
 
 
+def rec_gemm_group_cellbwd_dz(jobs, cell_args, dz_args) -> None:
+    """:func:`rec_gemm_group_cellbwd` with the hyper cell's dh formed from the
+    unfolded projections' dz slabs (``dz_args``: a filled ``DzArgs``;
+    ``skr_skinny_gemm_group_cellbwd_dz``)."""
+    import ctypes
+    from ..utils import native
+    lib = native.require_hip()
+    probs = _problems(jobs)
+    rc = lib.lib.skr_skinny_gemm_group_cellbwd_dz(probs, len(jobs), ctypes.byref(cell_args), ctypes.byref(dz_args),
+                                                  torch.cuda.current_stream().cuda_stream)
+    if rc != 0:
+        raise RuntimeError("skr_skinny_gemm_group_cellbwd_dz failed (%d)" % rc)
+
+
 # ---- inference-time helpers ------------------------------------------------------------
 _WCACHE = {}
 WEIGHTS_EPOCH = [0]
