@@ -76,8 +76,9 @@ __device__ __forceinline__ void cell_bwd_body(const BwdArgs& a, const int c, con
                 xv[k][q] = a.xp[b * a.ld_xp + q * H + uc];
                 rv[k][q] = a.r_lp != nullptr ? __bfloat162float(a.r_lp[b * a.ld_R + q * H + uc])
                                              : slab_sum<NS>(a.R, b * a.ld_R + q * H + uc, a.R_nslab, a.R_slab);
-                ax[k][q] = ldvec<MOD>(a.vec, q * a.vec_gs + vo) + a.vec_bias[q * H + uc];
-                ah[k][q] = ldvec<MOD>(a.vec, (4 + q) * a.vec_gs + vo) + a.vec_bias[(4 + q) * H + uc];
+                // (vec_bias null: the saved vectors already carry q, csrc/hyper_mod.hip)
+                ax[k][q] = ldvec<MOD>(a.vec, q * a.vec_gs + vo) + (a.vec_bias ? a.vec_bias[q * H + uc] : 0.f);
+                ah[k][q] = ldvec<MOD>(a.vec, (4 + q) * a.vec_gs + vo) + (a.vec_bias ? a.vec_bias[(4 + q) * H + uc] : 0.f);
             }
         }
     }

@@ -403,9 +403,9 @@ class _HyperSeq(torch.autograd.Function):
         am.ln_b, am.forget_bias = _ptr(s.mln[1]), float(forget_bias)
         am.ld_xp, am.ld_R = G, G
         am.R_nslab, am.R_slab = max(s.S_m, 1), B * G
-        # csrc/hyper_mod.hip folds q into the saved vectors
-        vbias = torch.zeros(12 * H, device=dev, dtype=f32) if s.vec_folded else s.q
-        am.vec_gs, am.vec_ld, am.vec_bias = H, 12 * H, vbias.data_ptr()
+        # csrc/hyper_mod.hip folds q into the saved vectors: no bias to add (and
+        # none to load -- 64 KB per row of the main-cell backward)
+        am.vec_gs, am.vec_ld, am.vec_bias = H, 12 * H, None if s.vec_folded else s.q.data_ptr()
         am.keep, am.seed, am.stream = float(keep), s.seed.data_ptr(), int(stream)
         am.ld_dG, am.ld_dG_lp, am.dG_lp_kind = G, G, 1 if lp_on else 0
         am.ld_dxp, am.dxp_kind, am.dvec_kind = G, 1 if lp_on else 2, 1 if lp_on else 2
