@@ -50,7 +50,7 @@ typedef __attribute__((ext_vector_type(4))) float f32x4;
 typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 
 constexpr int HH = 256, NTH = 384, TU = 32;      // hyper units (K), threads, units per tile
-constexpr int MAXB = 112, NRT = MAXB / 16;
+constexpr int MAXB = 128, NRT = MAXB / 16;
 constexpr int EP = 32, ZS = EP + 8;               // embedding padded to one MFMA K step; sZ row stride
 
 __device__ __forceinline__ int sw(int row, int chunk) { return row * HH + ((chunk ^ (row & 15)) << 3); }

@@ -135,11 +135,34 @@ __global__ __launch_bounds__(256) void skinny_gemm_group_cellbwd_kernel(const Ge
 }
 
 // ---------------------------------------------------------------------------
+// fp8 K-tiles (128 bytes per LDS row, chunk-swizzled like the bf16 ring) go
+// through gfx950's block-scaled v_mfma_scale_f32_16x16x128_f8f6f4 (e4m3 x
+// e4m3, both E8M0 block scales = 127, i.e. x1: the per-column weight scale
+// and the activation scale are applied in the epilogue): ONE instruction per
+// 16 x 16 tile per K-tile, at twice the bf16 rate per clock -- the CDNA3-era
+// v_mfma_f32_16x16x32_fp8_fp8 runs at the bf16 rate, so fp8 operands only
+// halved the bytes (round 3 measured it equal to bf16). Lane (r, g) =
+// (l & 15, l >> 4) feeds row (A) / column (B) r with bytes [32 g, 32 g + 32)
+// of the K-tile -- the same k order on both operands.
+typedef __attribute__((ext_vector_type(8))) int i32x8;
+
+__device__ __forceinline__ i32x8 frag8x32(const uint8_t* S, int row) {
+    const int fq = (threadIdx.x & 63) >> 4, sw = (row >> 1) & 7;
+    const int4 lo = *(const int4*)(&S[row * 128 + (((2 * fq) ^ sw) * 16)]);
+    const int4 hi = *(const int4*)(&S[row * 128 + (((2 * fq + 1) ^ sw) * 16)]);
+    return i32x8{lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+}
+
+__device__ __forceinline__ f32x4 mfma_fp8_k128(i32x8 a, i32x8 b, f32x4 c) {
+    return __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a, b, c, 0, 0, 0, 127, 0, 127);
+}
+
+// ---------------------------------------------------------------------------
 // fp8 (OCP e4m3) variant of the v2 ring for inference-time recurrent
 // products: operands are bytes, a K-tile is 128 elements (the same 128-byte
-// LDS rows and swizzle as the bf16 kernel), v_mfma_f32_16x16x32_fp8_fp8
-// (lane l: 8 bytes of row l&15 at k 8(l>>4)). Epilogue applies the per-
-// output-column weight scale and the activation scale: C = acc * sa * sb[n].
+// LDS rows and swizzle as the bf16 kernel), one MX-scaled MFMA per tile pair
+// (mfma_fp8_k128). Epilogue applies the per-output-column weight scale and
+// the activation scale: C = acc * sa * sb[n].
 constexpr int BK8 = 128;
 
 template <int BN>
@@ -208,25 +231,16 @@ __global__ __launch_bounds__(256) void skinny_gemm_fp8_kernel(
         if (kt + NSTAGE - 1 < n) issue(kt + NSTAGE - 1);
         const uint8_t* As = smem8 + (kt % NSTAGE) * TILE;
         const uint8_t* Bs = As + BM * BK8;
+        {
+            i32x8 af[2], bfr[NJ];
 #pragma unroll
-        for (int ks = 0; ks < BK8 / 32; ++ks) {
-            const int c16 = ks * 2 + (fq >> 1), half = (fq & 1) * 8;
-            long af[2], bfr[NJ];
+            for (int i = 0; i < 2; ++i) af[i] = frag8x32(As, 32 * w + 16 * i + fr);
 #pragma unroll
-            for (int i = 0; i < 2; ++i) {
-                const int row = 32 * w + 16 * i + fr;
-                af[i] = *(const long*)(&As[row * BK8 + ((c16 ^ ((row >> 1) & 7)) * 16) + half]);
-            }
-#pragma unroll
-            for (int j = 0; j < NJ; ++j) {
-                const int row = 16 * j + fr;
-                bfr[j] = *(const long*)(&Bs[row * BK8 + ((c16 ^ ((row >> 1) & 7)) * 16) + half]);
-            }
+            for (int j = 0; j < NJ; ++j) bfr[j] = frag8x32(Bs, 16 * j + fr);
 #pragma unroll
             for (int i = 0; i < 2; ++i)
 #pragma unroll
-                for (int j = 0; j < NJ; ++j)
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(af[i], bfr[j], acc[i][j], 0, 0, 0);
+                for (int j = 0; j < NJ; ++j) acc[i][j] = mfma_fp8_k128(af[i], bfr[j], acc[i][j]);
         }
     }
 #pragma unroll
@@ -244,7 +258,7 @@ __global__ __launch_bounds__(256) void skinny_gemm_fp8_kernel(
 
 // fp8 v2: the same tile as glds_tile (ring depth NS, counted waits, grouped
 // launch, optional bf16 output) on e4m3 operands: K-tiles of 128 bytes,
-// v_mfma_f32_16x16x32_fp8_fp8, epilogue C = acc * a_scale * b_scale[n]. At
+// one MX-scaled K=128 MFMA per tile pair, epilogue C = acc * a_scale * b_scale[n]. At
 // NS = 3 a stage is (128 + 64) x 128 B = 24 KiB: two workgroups per CU, like
 // the bf16 ring, while every byte moved carries twice the K extent.
 template <int BN, int NS, bool CBF16>
@@ -302,25 +316,16 @@ __device__ __forceinline__ void glds_tile_fp8(const uint8_t* __restrict__ A, int
         if (kt + NS - 1 < n) issue(kt + NS - 1);
         const uint8_t* As = smem8 + (kt % NS) * TILE;
         const uint8_t* Bs = As + BM * BK8;
+        {
+            i32x8 af[2], bfr[NJ];
 #pragma unroll
-        for (int ks = 0; ks < BK8 / 32; ++ks) {
-            const int c16 = ks * 2 + (fq >> 1), half = (fq & 1) * 8;
-            long af[2], bfr[NJ];
+            for (int i = 0; i < 2; ++i) af[i] = frag8x32(As, 32 * w + 16 * i + fr);
 #pragma unroll
-            for (int i = 0; i < 2; ++i) {
-                const int row = 32 * w + 16 * i + fr;
-                af[i] = *(const long*)(&As[row * BK8 + ((c16 ^ ((row >> 1) & 7)) * 16) + half]);
-            }
-#pragma unroll
-            for (int j = 0; j < NJ; ++j) {
-                const int row = 16 * j + fr;
-                bfr[j] = *(const long*)(&Bs[row * BK8 + ((c16 ^ ((row >> 1) & 7)) * 16) + half]);
-            }
+            for (int j = 0; j < NJ; ++j) bfr[j] = frag8x32(Bs, 16 * j + fr);
 #pragma unroll
             for (int i = 0; i < 2; ++i)
 #pragma unroll
-                for (int j = 0; j < NJ; ++j)
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(af[i], bfr[j], acc[i][j], 0, 0, 0);
+                for (int j = 0; j < NJ; ++j) acc[i][j] = mfma_fp8_k128(af[i], bfr[j], acc[i][j]);
         }
     }
 #pragma unroll

@@ -236,7 +236,7 @@ class _HyperSeq(torch.autograd.Function):
         # LayerNorm partial sums (csrc/hyper_mod.hip): the main cell then needs
         # no statistics exchange for the gates (MOD 3) and VEC carries q (and
         # the main bias in its shift block) -- the backward uses a zero vec_bias
-        hmod = HYPER_MOD and vbf and dev.type == "cuda" and Hh == 256 and B <= 112 and H % 32 == 0 and \
+        hmod = HYPER_MOD and vbf and dev.type == "cuda" and Hh == 256 and B <= 128 and H % 32 == 0 and \
             S_m in (1, 2, 4) and E <= 32
         ZS = None
         if hmod:

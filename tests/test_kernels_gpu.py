@@ -299,7 +299,7 @@ def test_hyper_sequence_bf16_close(H, Hh, E):
     _close(res[0][5:], res[1][5:], 6e-2, 6e-2, "grad")
 
 
-@pytest.mark.parametrize("B,keep,hkeep", [(100, 0.9, 0.9), (37, 1.0, 1.0)])
+@pytest.mark.parametrize("B,keep,hkeep", [(100, 0.9, 0.9), (37, 1.0, 1.0), (128, 0.9, 1.0)])
 def test_hyper_mod_path_vs_oracle(B, keep, hkeep):
     """The fused modulation step (csrc/hyper_mod.hip: vec + gate
     pre-activations + LayerNorm partial sums; the main cell without its
