@@ -60,8 +60,24 @@ __device__ __forceinline__ uint32_t pack_bf(float a, float b) {
            ((uint32_t)__bfloat16_as_ushort(__float2bfloat16(b)) << 16);
 }
 
+}  // namespace
+
+// Decode-step inputs (sample/hyper_step.py, csrc/decode_step.hip): hh from
+// the hyper cell's fp32 output (the fp8 decode keeps no bf16 copy of it) and
+// the main x-projection formed here from the sampled stroke x [B][5]:
+// xh[b][n] = zp[b][n] + sum_k x[b][k] w5[k][n]. Null members: the training
+// sequence's inputs (bf16 hh operand, precomputed xh).
+struct ModDecode {
+    const float* hh32;
+    const float* x5;
+    const float* w5; int64_t ldw5;
+    const float* zp; int64_t ldzp;
+};
+
+namespace {
+
 template <int NS>
-__global__ __launch_bounds__(NTH) void hyper_mod_fwd(const __hip_bfloat16* __restrict__ hh, int64_t ld_hh,
+__global__ __launch_bounds__(NTH) void hyper_mod_fwd(const ModDecode dec, const __hip_bfloat16* __restrict__ hh, int64_t ld_hh,
                                                      const __hip_bfloat16* __restrict__ WzT,   // [12][EP][HH]
                                                      const __hip_bfloat16* __restrict__ WaT,   // [12][H][EP]
                                                      const float* __restrict__ bz, int E,      // [12 E]
@@ -100,7 +116,15 @@ __global__ __launch_bounds__(NTH) void hyper_mod_fwd(const __hip_bfloat16* __res
     for (int k = 0; k < RPT; ++k) {
         const int rr = min(rg + k * (NTH / 8), B - 1);
         const int64_t go = (int64_t)rr * G + q * H + u0 + ul;
-        x4[k] = *(const f32x4*)(xh + go);
+        if (dec.x5 != nullptr) {
+            const int col = q * H + u0 + ul;
+            f32x4 v = *(const f32x4*)(dec.zp + rr * dec.ldzp + col);
+#pragma unroll
+            for (int k5 = 0; k5 < 5; ++k5) v += dec.x5[rr * 5 + k5] * *(const f32x4*)(dec.w5 + k5 * dec.ldw5 + col);
+            x4[k] = v;
+        } else {
+            x4[k] = *(const f32x4*)(xh + go);
+        }
         r4[k] = *(const f32x4*)(R + go);
 #pragma unroll
         for (int sl = 1; sl < NS; ++sl) {
@@ -113,7 +137,14 @@ __global__ __launch_bounds__(NTH) void hyper_mod_fwd(const __hip_bfloat16* __res
 #pragma unroll
     for (int k = 0; k < SPT; ++k) {
         const int i = min(tid + k * NTH, NPC - 1), r = i / (HH / 8), c = i % (HH / 8);
-        hv[k] = *(const bf16x8*)(hh + (int64_t)min(r, B - 1) * ld_hh + 8 * c);
+        if (dec.hh32 != nullptr) {
+            const float* src = dec.hh32 + (int64_t)min(r, B - 1) * HH + 8 * c;
+            const f32x4 lo = *(const f32x4*)src, hi = *(const f32x4*)(src + 4);
+            hv[k] = bf16x8{(__bf16)lo[0], (__bf16)lo[1], (__bf16)lo[2], (__bf16)lo[3],
+                           (__bf16)hi[0], (__bf16)hi[1], (__bf16)hi[2], (__bf16)hi[3]};
+        } else {
+            hv[k] = *(const bf16x8*)(hh + (int64_t)min(r, B - 1) * ld_hh + 8 * c);
+        }
     }
 #pragma unroll
     for (int k = 0; k < SPT; ++k) {
@@ -215,7 +246,10 @@ __global__ __launch_bounds__(NTH) void hyper_mod_fwd(const __hip_bfloat16* __res
 SKR_API int skr_hyper_mod_fwd(const void* hh, int64_t ld_hh, const void* WzT, const void* WaT, const float* bz,
                               int E, float* zsave, const float* qb, const float* xh, const float* R, int64_t r_slab,
                               int nslab, void* vec, float* g, void* rlp, float* stats, int B, int H, int Hh,
-                              hipStream_t s) {
+                              const ModDecode* dec, hipStream_t s) {
+    const ModDecode dz = dec ? *dec : ModDecode{};
+    if (dz.x5 && (((uintptr_t)dz.w5 | (uintptr_t)dz.zp) & 15 || dz.ldw5 % 4 || dz.ldzp % 4)) return -4;
+    if (dz.hh32 && ((uintptr_t)dz.hh32 & 15)) return -4;
     if (B <= 0) return 0;
     if (B > MAXB || Hh != HH || H % TU != 0 || E < 1 || E > EP) return -2;
     if (((uintptr_t)hh | (uintptr_t)WzT | (uintptr_t)WaT | (uintptr_t)xh | (uintptr_t)R | (uintptr_t)vec |
@@ -227,7 +261,7 @@ SKR_API int skr_hyper_mod_fwd(const void* hh, int64_t ld_hh, const void* WzT, co
     const auto* wa = (const __hip_bfloat16*)WaT;
     auto* v = (__hip_bfloat16*)vec;
     auto* rl = (__hip_bfloat16*)rlp;
-#define SKR_HM(NS_) hipLaunchKernelGGL(hyper_mod_fwd<NS_>, grid, dim3(NTH), 0, s, a, ld_hh, wz, wa, bz, E, zsave, qb, \
+#define SKR_HM(NS_) hipLaunchKernelGGL(hyper_mod_fwd<NS_>, grid, dim3(NTH), 0, s, dz, a, ld_hh, wz, wa, bz, E, zsave, qb, \
                                        xh, R, r_slab, v, g, rl, stats, B, H)
     switch (nslab) {
         case 1: SKR_HM(1); break;

@@ -109,4 +109,35 @@ __device__ inline MdnDraw mdn_sample_wave(const float* zr, int M, int mode, floa
     return d;
 }
 
+// Head output row b as the sum of `nslab` split-K partial slabs of the head
+// GEMM (csrc/skinny_gemm.hip, z = h @ W_out, no bias) plus the bias, by a
+// 256-thread workgroup: wave w folds the slabs s = w mod 4 of every column
+// with independent (unrolled, clamped) loads, the four partial rows meet in
+// LDS (`part` [4][256]), and zrow [nout] is ready after the call (every thread
+// passed its barrier).
+__device__ inline void fold_head_slabs(const float* __restrict__ zs, int64_t ldz, int nslab, int64_t slab,
+                                       const float* __restrict__ bias, int nout, int b, float (*part)[256],
+                                       float* zrow) {
+    constexpr int kU = 8;                  // slabs per unrolled batch (per wave)
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const float* zb = zs + (int64_t)b * ldz;
+#pragma unroll
+    for (int cc = 0; cc < 4; ++cc) {
+        const int c = lane + 64 * cc;
+        if (c >= nout) break;
+        float v = 0.f;
+        for (int s0 = w; s0 < nslab; s0 += 4 * kU) {
+            float t[kU];
+#pragma unroll
+            for (int k = 0; k < kU; ++k) t[k] = zb[(int64_t)min(s0 + 4 * k, nslab - 1) * slab + c];
+#pragma unroll
+            for (int k = 0; k < kU; ++k) v += (s0 + 4 * k < nslab) ? t[k] : 0.f;
+        }
+        part[w][c] = v;
+    }
+    __syncthreads();
+    if (tid < nout) zrow[tid] = bias[tid] + ((part[0][tid] + part[1][tid]) + (part[2][tid] + part[3][tid]));
+    __syncthreads();
+}
+
 }  // namespace skr

@@ -61,28 +61,10 @@ __global__ __launch_bounds__(256) void mdn_sample_slabs_kernel(const float* __re
                                                                float* __restrict__ out_row, int64_t ld_out,
                                                                float* __restrict__ next_x, int64_t ld_next,
                                                                int* __restrict__ done) {
-    constexpr int kU = 8;                  // slabs per unrolled batch (per wave)
     __shared__ float part[4][256];
     __shared__ float zrow[256];
     const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const float* zb = zs + (int64_t)b * ldz;
-#pragma unroll
-    for (int cc = 0; cc < 4; ++cc) {
-        const int c = lane + 64 * cc;
-        if (c >= nout) break;
-        float v = 0.f;
-        for (int s0 = w; s0 < nslab; s0 += 4 * kU) {
-            float t[kU];
-#pragma unroll
-            for (int k = 0; k < kU; ++k) t[k] = zb[(int64_t)min(s0 + 4 * k, nslab - 1) * slab + c];
-#pragma unroll
-            for (int k = 0; k < kU; ++k) v += (s0 + 4 * k < nslab) ? t[k] : 0.f;
-        }
-        part[w][c] = v;
-    }
-    __syncthreads();
-    if (tid < nout) zrow[tid] = bias[tid] + ((part[0][tid] + part[1][tid]) + (part[2][tid] + part[3][tid]));
-    __syncthreads();
+    skr::fold_head_slabs(zs, ldz, nslab, slab, bias, nout, b, part, zrow);
     if (w != 0) return;
     const uint32_t key = skr::hash_key(*seed, 0x5A3Du, step);
     const skr::MdnDraw d = skr::mdn_sample_wave(zrow, M, mode, temp, greedy, fix_pen, key, (uint32_t)(row0 + b), step);

@@ -286,6 +286,14 @@ class DzArgs(C.Structure):
     ]
 
 
+class ModDecode(C.Structure):
+    """Mirror of ``ModDecode`` in csrc/hyper_mod.hip (decode-mode inputs of the
+    HyperLSTM modulation kernel: fp32 hyper state, x-projection from the stroke)."""
+    _fields_ = [
+        ("hh32", _p), ("x5", _p), ("w5", _p), ("ldw5", _i64), ("zp", _p), ("ldzp", _i64),
+    ]
+
+
 class HipLib:
     def __init__(self, lib: C.CDLL):
         self.lib = lib
@@ -390,7 +398,7 @@ class HipLib:
         lib.skr_skinny_gemm_group_fp8.argtypes = [C.POINTER(GemmProblem8), _i, _p]
         lib.skr_skinny_gemm_group_fp8.restype = _i
         lib.skr_hyper_mod_fwd.argtypes = [_p, _i64, _p, _p, _p, _i, _p, _p, _p, _p, _i64, _i, _p, _p, _p, _p, _i, _i,
-                                          _i, _p]
+                                          _i, C.POINTER(ModDecode), _p]
         lib.skr_hyper_mod_fwd.restype = _i
         lib.skr_cast_transpose_bf16.argtypes = [_p, _i64, _i64, _i, _i, _i, _p, _i64, _i64, _p, _i64, _i64, _p]
         lib.skr_cast_transpose_bf16.restype = _i

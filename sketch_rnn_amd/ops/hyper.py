@@ -314,7 +314,7 @@ class _HyperSeq(torch.autograd.Function):
                                                  bz_c.data_ptr(), E, _ptr(ZS[t] if ZS is not None else None),
                                                  qb.data_ptr(), XHc[t].data_ptr(), RM[rmi(t)].data_ptr(), B * G, S_m,
                                                  VEC[t].data_ptr(), GP.data_ptr(), _ptr(RLP[t] if RLP is not None else None),
-                                                 GS.data_ptr(), B, H, Hh, st), "hyper_mod_fwd")
+                                                 GS.data_ptr(), B, H, Hh, None, st), "hyper_mod_fwd")
                 am.gpre, am.gstats, am.gstat_tiles = GP.data_ptr(), GS.data_ptr(), H // 32
             elif vbf:
                 gemm.rec_gemm_bf16out(A[t + 1, :, H:], PlT, VEC[t])
