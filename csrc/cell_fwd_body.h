@@ -78,8 +78,13 @@ __device__ __forceinline__ void row_sum(float (&v)[N], float* lds, float* mine, 
     }
 }
 
+// x5 / w5 (decode step, csrc/decode_step.hip): the x-projection is formed
+// here from the row's 5 stroke values, xp[b] + sum_k x5[k] w5[k][col] (the
+// summation order of skr_bproj_fwd, csrc/inproj.hip); null: xp is complete.
 template <int NT, int UPT, int NS, bool LN, int MOD>
-__device__ __forceinline__ void cell_fwd_body(const FwdArgs& a, const int c, const int b, const int C) {
+__device__ __forceinline__ void cell_fwd_body(const FwdArgs& a, const int c, const int b, const int C,
+                                              const float* x5 = nullptr, const float* w5 = nullptr,
+                                              int64_t ldw5 = 0) {
     constexpr int NW = NT / 64;
     __shared__ float lds[NW * 8];
     __shared__ float mine[8];
@@ -120,7 +125,11 @@ __device__ __forceinline__ void cell_fwd_body(const FwdArgs& a, const int c, con
                 }
                 continue;
             }
-            const float xv = a.xp[b * a.ld_xp + q * H + uc];
+            float xv = a.xp[b * a.ld_xp + q * H + uc];
+            if (x5 != nullptr) {
+#pragma unroll
+                for (int i = 0; i < 5; ++i) xv += x5[i] * w5[i * ldw5 + q * H + uc];
+            }
             const float rv = slab_sum<NS>(a.R, b * a.ld_R + q * H + uc, a.R_nslab, a.R_slab);
             if (MOD) {
                 const int64_t vo = (int64_t)b * a.vec_ld + uc;

@@ -221,8 +221,10 @@ __global__ __launch_bounds__(NTH) void hyper_mod_fwd(const ModDecode dec, const 
             *(f32x4*)(gout + go) = f32x4{g[0], g[1], g[2], g[3]};
             if (rlp) *(u32x2*)(rlp + go) = u32x2{pack_bf(r4[k][0], r4[k][1]), pack_bf(r4[k][2], r4[k][3])};
             const int64_t vo = (int64_t)rr * NV + u0 + ul;
-            *(u32x2*)(vec + vo + q * H) = u32x2{pack_bf(vx[0], vx[1]), pack_bf(vx[2], vx[3])};
-            *(u32x2*)(vec + vo + (4 + q) * H) = u32x2{pack_bf(vh[0], vh[1]), pack_bf(vh[2], vh[3])};
+            if (vec) {   // (null at inference)
+                *(u32x2*)(vec + vo + q * H) = u32x2{pack_bf(vx[0], vx[1]), pack_bf(vx[2], vx[3])};
+                *(u32x2*)(vec + vo + (4 + q) * H) = u32x2{pack_bf(vh[0], vh[1]), pack_bf(vh[2], vh[3])};
+            }
             // (the shift block 8..11 is not stored: the backward reads only
             // the x and h modulations -- d(shift) = dg needs no saved value)
             if (ug == 0) {
@@ -241,7 +243,7 @@ __global__ __launch_bounds__(NTH) void hyper_mod_fwd(const ModDecode dec, const 
 // embeddings past E zero), bz [12E] fp32, qb [12H] fp32 (b_z @ W_a, with the
 // main bias added to blocks 8..11), xh [B][4H] fp32, R = sum of nslab fp32
 // slabs [B][4H] (stride r_slab); outputs vec [B][12H] bf16 (blocks 0..7
-// written), g [B][4H] fp32, rlp [B][4H] bf16 (or null), stats [B][4][H/32][2]
+// written; null at inference), g [B][4H] fp32, rlp [B][4H] bf16 (or null), stats [B][4][H/32][2]
 // fp32, zsave [B][12E] fp32 (or null).
 SKR_API int skr_hyper_mod_fwd(const void* hh, int64_t ld_hh, const void* WzT, const void* WaT, const float* bz,
                               int E, float* zsave, const float* qb, const float* xh, const float* R, int64_t r_slab,

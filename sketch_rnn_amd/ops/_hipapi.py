@@ -294,6 +294,20 @@ class ModDecode(C.Structure):
     ]
 
 
+class DecodeSample(C.Structure):
+    """Mirror of ``DecodeSample`` in csrc/decode_step.hip (the previous stroke's
+    sampler folded into the decode-step hyper cell)."""
+    _fields_ = [
+        ("active", _i),
+        ("zs", _p), ("ldz", _i64), ("nslab", _i), ("slab", _i64),
+        ("bias", _p), ("nout", _i),
+        ("M", _i), ("mode", _i), ("temp", _f), ("greedy", _i), ("fix_pen", _i),
+        ("seed", _p), ("step", _u32), ("row0", _i),
+        ("out_row", _p), ("ld_out", _i64),
+        ("done", _p),
+    ]
+
+
 class HipLib:
     def __init__(self, lib: C.CDLL):
         self.lib = lib
@@ -404,6 +418,8 @@ class HipLib:
         lib.skr_cast_transpose_bf16.restype = _i
         lib.skr_hash_normal.argtypes = [_p, _u32, _u32, _p, _i64, _p]
         lib.skr_hash_normal.restype = _i
+        lib.skr_decode_hyper_cell.argtypes = [C.POINTER(LstmFwdArgs), C.POINTER(DecodeSample), _p, _p, _i64, _p]
+        lib.skr_decode_hyper_cell.restype = _i
         lib.skr_decode_ref.argtypes = [C.POINTER(DecArgs), _p]
         lib.skr_decode_ref.restype = _i
         for name, cls in (("skr_lstm_fwd_args_size", LstmFwdArgs), ("skr_lstm_bwd_args_size", LstmBwdArgs),
@@ -418,6 +434,7 @@ class HipLib:
                           ("skr_decode_ref_args_size", DecArgs),
                           ("skr_gemm_problem_size", GemmProblem),
                           ("skr_dz_args_size", DzArgs),
+                          ("skr_decode_sample_size", DecodeSample),
                           ("skr_gemm_problem8_size", GemmProblem8)):
             fn = getattr(lib, name)
             fn.restype = _i

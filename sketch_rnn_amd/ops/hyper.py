@@ -52,6 +52,18 @@ UNFOLD_BWD = True
 # profiles/r3/hyper_fused_cell_ab.txt.)
 
 
+def unfold_norm(W_z: torch.Tensor, W_a: torch.Tensor):
+    """The hyper-norm projections of csrc/hyper_mod.hip in bf16: W_z [Hh, 12E]
+    -> WzT [12][32][Hh] (W_z^T per block) and W_a [12, E, H] -> WaT [12][H][32]
+    (unit-major), embeddings padded to 32 with zeros."""
+    Hh, (nb, E, H) = W_z.shape[0], W_a.shape
+    WzT = torch.zeros(nb, 32, Hh, device=W_z.device, dtype=torch.bfloat16)
+    WzT[:, :E] = W_z.detach().view(Hh, nb, E).permute(1, 2, 0)
+    WaT = torch.zeros(nb, H, 32, device=W_z.device, dtype=torch.bfloat16)
+    WaT[:, :, :E] = W_a.detach().permute(0, 2, 1)
+    return WzT, WaT
+
+
 def _split_override(var: str, planned: int, K: int) -> int:
     """Split-K factor of a per-step HyperLSTM product: the planned one, or
     ``$var`` (tuning sweeps) when it divides K into whole 64-wide K tiles."""
@@ -243,13 +255,7 @@ class _HyperSeq(torch.autograd.Function):
             # the hyper-norm projections unfolded (csrc/hyper_mod.hip): W_z^T and W_a
             # per block in bf16, embeddings padded to 32; z = hh W_z + b_z saved
             # for the parameter gradients
-            def unfold(W_z, W_a):
-                WzT = torch.zeros(12, 32, Hh, device=dev, dtype=torch.bfloat16)
-                WzT[:, :E] = W_z.detach().view(Hh, 12, E).permute(1, 2, 0)
-                WaT = torch.zeros(12, H, 32, device=dev, dtype=torch.bfloat16)
-                WaT[:, :, :E] = W_a.detach().permute(0, 2, 1)
-                return WzT, WaT
-            WzT, WaT = gemm.derived((W_z, W_a), "hypunfold", unfold) if infer else unfold(W_z, W_a)
+            WzT, WaT = gemm.derived((W_z, W_a), "hypunfold", unfold_norm) if infer else unfold_norm(W_z, W_a)
             bz_c = b_z.detach().contiguous()
             ZS = None if infer else torch.empty(T, B, 12 * E, device=dev, dtype=f32)
             mod = 3

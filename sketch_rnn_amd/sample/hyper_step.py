@@ -22,6 +22,23 @@ seven kernels, all hand-written:
 
 Rows are processed in chunks of at most 128 (one MFMA row tile).
 
+Four-launch stroke (:meth:`HyperStepDecoder.step_fused`, the
+:class:`~.sampler.GraphDecoder` path when ``hyper_num_units == 256``):
+
+1. grouped skinny GEMM ``{h W_h, [h | hh] W_y, h W_out}`` -- the head of the
+   PREVIOUS stroke's ``h`` rides in the step's own GEMM launch;
+2. ``skr_decode_hyper_cell`` (csrc/decode_step.hip): samples stroke t-1 from
+   the head slabs (same keyed draws as ``skr_mdn_sample_slabs``), writes it
+   out and forms the hyper cell's x-projection from it in-register, then the
+   hyper LayerNorm cell;
+3. ``skr_hyper_mod_fwd`` (csrc/hyper_mod.hip) in decode mode: unfolded
+   hyper-norm projections ``bf16(hh W_z) W_a + q`` on MFMA, the main cell's
+   x-projection from the stroke, the modulated gate pre-activations and their
+   LayerNorm partial sums;
+4. the main LayerNorm cell (MOD 3: pre-activations precomputed).
+
+After the last stroke :meth:`finish` runs the head GEMM + sampler once.
+
 Compute dtype ``fp8`` (BASELINE config 5): the four GEMMs run on OCP e4m3
 operands (``v_mfma_f32_16x16x32_fp8_fp8``, per-output-column weight scales;
 the cells write the bf16-free operand buffer as e4m3 x 64 -- |h| <= 1, so a
@@ -30,11 +47,12 @@ static scale maps it onto [-64, 64] with subnormals down to ~3e-5).
 from __future__ import annotations
 
 import ctypes
+import os
 
 import torch
 
 from ..ops import gemm
-from ..ops._hipapi import LstmFwdArgs
+from ..ops._hipapi import DecodeSample, LstmFwdArgs, ModDecode
 from ..ops.recurrent import _ClusterSync, _seed_tensor
 from ..utils import native
 
@@ -81,6 +99,15 @@ class HyperStepDecoder:
             self.S_y = gemm.plan_splits(B, Gh, K, 1, bf)
             self.S_o = gemm.plan_splits(B, 128, H, 1, bf)
         assert min(self.S_m, self.S_y, self.S_o) >= 1
+        # four-launch stroke (step_fused): hyper_mod's shape limits (Hh == 256,
+        # E <= 32, 32-unit tiles, <= 4 main-GEMM slabs)
+        self.fused = Hh == 256 and self.E <= 32 and H % 32 == 0 and \
+            os.environ.get("SKR_DECODE_FUSED", "1") != "0"
+        if self.fused:
+            self.S_m = 4 if self.S_m >= 4 else 2 if self.S_m >= 2 else 1
+            self.X = torch.zeros(B, 5, dtype=f32, device=device)
+            self.GP = torch.empty(B, G, dtype=f32, device=device)
+            self.GS = torch.empty(B, 4, H // 32, 2, dtype=f32, device=device)
         # state / operand buffers (resident for the whole decode)
         self.A = torch.zeros(B, K, dtype=torch.uint8 if self.fp8 else bf, device=device)   # [h | hh] GEMM operand
         self.CC = torch.zeros(B, H, dtype=f32, device=device)
@@ -119,21 +146,37 @@ class HyperStepDecoder:
             Wt[: W.shape[1]] = W.t().to(dt)
             return Wt
 
+        self._fold = lambda: gemm.derived((p.W_z, p.b_z, p.W_a), "hypP%s" % dt, fold)
         w = dict(
             WhT=gemm.derived(p.W_h, "hypWhT%s" % dt, lambda W: W.to(dt).t().contiguous()),
             WyT=gemm.derived((p.hyp_W_x, p.hyp_W_h), "hypWyT%s" % dt, wy),
-            PQ=gemm.derived((p.W_z, p.b_z, p.W_a), "hypP%s" % dt, fold),
             W5=gemm.derived((p.W_x, p.hyp_W_x), "stepW5",
                             lambda a, b: torch.cat([a[:5], b[:5]], 1).float().contiguous()),
             WoT=gemm.derived(m.output_w, "stepWoT", wout),
             bo=m.output_b.detach().float().contiguous(),
         )
+        if self.fused:
+            from ..ops.hyper import unfold_norm
+
+            def qbias(b_z, W_a, bias):
+                q = torch.bmm(b_z.detach().view(12, 1, E), W_a.detach()).reshape(12, H)
+                q[8:] += bias.detach().view(4, H)
+                return q.reshape(12 * H).float().contiguous()
+            w["UNF"] = gemm.derived((p.W_z, p.W_a), "hypunfold", unfold_norm)
+            w["QB"] = gemm.derived((p.b_z, p.W_a, p.bias), "hypQB", qbias)
+            w["bz"] = p.b_z.detach().float().contiguous()
         if self.fp8:   # per-output-column e4m3 weights
             w["WhT"] = gemm.derived(w["WhT"], "q8", gemm.quantize_fp8_rows)
             w["WyT"] = gemm.derived(w["WyT"], "q8", gemm.quantize_fp8_rows)
-            w["PQ"] = (gemm.derived(w["PQ"][0], "q8", gemm.quantize_fp8_rows), w["PQ"][1])
             w["WoT"] = gemm.derived(w["WoT"], "q8", gemm.quantize_fp8_rows)
         return w
+
+    def _pq(self):
+        """Folded modulation weights (P^T, q) of the seven-launch :meth:`step`."""
+        if "PQ" not in self._w:
+            P, q = self._fold()
+            self._w["PQ"] = (gemm.derived(P, "q8", gemm.quantize_fp8_rows) if self.fp8 else P, q)
+        return self._w["PQ"]
 
     @torch.no_grad()
     def prepare(self) -> None:
@@ -143,8 +186,9 @@ class HyperStepDecoder:
         self._w = self._weights()
 
     @torch.no_grad()
-    def begin(self, zc, state) -> None:
-        """Load the initial state and the per-sketch z projections."""
+    def begin(self, zc, state, x0=None) -> None:
+        """Load the initial state, the per-sketch z projections and (fused
+        path) the first stroke ``x0 [B, 5]``."""
         if getattr(self, "_w", None) is None:
             self.prepare()
         p = self.model.dec
@@ -167,6 +211,8 @@ class HyperStepDecoder:
         for cl in (self.clm, self.clh):
             if cl.on:
                 cl.part.zero_()
+        if x0 is not None and self.fused:
+            self.X.copy_(x0)
 
     def _cell_args(self, t: int):
         p, w = self.model.dec, self._w
@@ -189,8 +235,8 @@ class HyperStepDecoder:
         am.B, am.H = B, H
         am.xp, am.ld_xp = self.XP.data_ptr(), G + Gh
         am.R, am.ld_R, am.R_nslab, am.R_slab = self.RM.data_ptr(), G, self.S_m, B * G
-        PlT, q = w["PQ"]
-        am.vec, am.vec_gs, am.vec_ld, am.vec_bias = self.VEC.data_ptr(), H, 12 * H, q.data_ptr()
+        if "PQ" in w:
+            am.vec, am.vec_gs, am.vec_ld, am.vec_bias = self.VEC.data_ptr(), H, 12 * H, w["PQ"][1].data_ptr()
         am.bias = p.bias.data_ptr()
         am.ln_g, am.ln_b, am.lnc_g, am.lnc_b = (x.data_ptr() for x in lnm)
         am.forget_bias, am.keep = 1.0, 1.0
@@ -205,6 +251,7 @@ class HyperStepDecoder:
         """One stroke: ``x [B, 5]`` (fp32, contiguous) -> decoder step -> head
         slabs -> ``sample(zs, ldz, nslab, slab, bias)`` (the caller's sampler)."""
         w = self._w
+        PQ = self._pq()
         B, H, G, Gh = self.B, self.H, self.G, self.Gh
         st = torch.cuda.current_stream().cuda_stream
         rc = self.lib.skr_bproj_fwd(x.data_ptr(), w["W5"].data_ptr(), self.ZP.data_ptr(), self.XP.data_ptr(),
@@ -217,9 +264,66 @@ class HyperStepDecoder:
         ah, am = self._cell_args(t)
         if self.lib.skr_lstm_fwd_step(ctypes.byref(ah), 1, 0, st) != 0:
             raise RuntimeError("hyper cell step failed")
-        (gemm.rec_gemm_fp8_v2(self.A[:, H:], w["PQ"][0], self.VEC, 1) if f8 else
-         gemm.rec_gemm_bf16out(self.A[:, H:], w["PQ"][0], self.VEC))
+        (gemm.rec_gemm_fp8_v2(self.A[:, H:], PQ[0], self.VEC, 1) if f8 else
+         gemm.rec_gemm_bf16out(self.A[:, H:], PQ[0], self.VEC))
         if self.lib.skr_lstm_fwd_step(ctypes.byref(am), 1, 2, st) != 0:
             raise RuntimeError("main cell step failed")
         (gemm.rec_gemm_fp8_v2 if f8 else gemm.rec_gemm)(self.A[:, :H], w["WoT"], self.ZS, self.S_o)
         sample(self.ZS, 128, self.S_o, B * 128, w["bo"])
+
+    # -- four-launch stroke -------------------------------------------------------
+    def sample_args(self, step: int, row0: int, out_row: torch.Tensor, done: torch.Tensor, seed: torch.Tensor,
+                    M: int, mode: int, temp: float, greedy: bool, fix_pen: bool) -> DecodeSample:
+        """Sampler of stroke ``step`` (written to ``out_row [B, 5]``, row
+        stride ``out_row.stride(0)``) for :meth:`step_fused` of stroke step+1."""
+        s = DecodeSample()
+        s.active = 1
+        s.zs, s.ldz, s.nslab, s.slab = self.ZS.data_ptr(), 128, self.S_o, self.B * 128
+        s.bias, s.nout = self._w["bo"].data_ptr(), self.nout
+        s.M, s.mode, s.temp, s.greedy, s.fix_pen = M, mode, float(temp), int(greedy), int(fix_pen)
+        s.seed, s.step, s.row0 = seed.data_ptr(), step, row0
+        s.out_row, s.ld_out = out_row.data_ptr(), out_row.stride(0)
+        s.done = done.data_ptr()
+        return s
+
+    @torch.no_grad()
+    def step_fused(self, t: int, smp: DecodeSample = None) -> None:
+        """One stroke in four launches (module docstring). ``smp``: the sampler
+        of stroke t-1 (:meth:`sample_args`), or None -- the stroke is
+        ``self.X`` (t == 0, or teacher-forced)."""
+        assert self.fused
+        w, lib = self._w, self.lib
+        B, H, Hh, G, Gh, K = self.B, self.H, self.Hh, self.G, self.Gh, self.K
+        st = torch.cuda.current_stream().cuda_stream
+        f8 = self.fp8
+        jobs = [(self.A[:, :H], w["WhT"], self.RM, self.S_m), (self.A, w["WyT"], self.RY, self.S_y)]
+        if smp is not None:
+            jobs.append((self.A[:, :H], w["WoT"], self.ZS, self.S_o))
+        (gemm.rec_gemm_fp8_group if f8 else gemm.rec_gemm_group)(jobs)
+        ah, am = self._cell_args(t)
+        ah.xp = self.ZP[:, G:].data_ptr()          # z part; the stroke part is formed in the kernel
+        if smp is None:
+            smp = DecodeSample()
+        rc = lib.skr_decode_hyper_cell(ctypes.byref(ah), ctypes.byref(smp), self.X.data_ptr(),
+                                       w["W5"][:, G:].data_ptr(), G + Gh, st)
+        if rc != 0:
+            raise RuntimeError("skr_decode_hyper_cell failed (%d)" % rc)
+        dec = ModDecode()
+        dec.hh32 = self.HH.data_ptr() if f8 else None
+        dec.x5, dec.w5, dec.ldw5 = self.X.data_ptr(), w["W5"].data_ptr(), G + Gh
+        dec.zp, dec.ldzp = self.ZP.data_ptr(), G + Gh
+        WzT, WaT = w["UNF"]
+        rc = lib.skr_hyper_mod_fwd(None if f8 else self.A[:, H:].data_ptr(), K, WzT.data_ptr(), WaT.data_ptr(),
+                                   w["bz"].data_ptr(), self.E, None, w["QB"].data_ptr(), None, self.RM.data_ptr(),
+                                   B * G, self.S_m, None, self.GP.data_ptr(), None, self.GS.data_ptr(), B, H, Hh,
+                                   ctypes.byref(dec), st)
+        if rc != 0:
+            raise RuntimeError("skr_hyper_mod_fwd (decode) failed (%d)" % rc)
+        am.gpre, am.gstats, am.gstat_tiles = self.GP.data_ptr(), self.GS.data_ptr(), H // 32
+        if lib.skr_lstm_fwd_step(ctypes.byref(am), 1, 3, st) != 0:
+            raise RuntimeError("main cell step failed")
+
+    @torch.no_grad()
+    def head(self) -> None:
+        """Head GEMM of the current ``h`` into the split-K slabs ``ZS``."""
+        (gemm.rec_gemm_fp8_v2 if self.fp8 else gemm.rec_gemm)(self.A[:, :self.H], self._w["WoT"], self.ZS, self.S_o)

@@ -300,6 +300,25 @@ class GraphDecoder:
             if stream != main:
                 stream.wait_stream(main)
         for r0, n, st, stream in stp:
+            if st.fused:       # four launches per stroke (hyper_step.py module docstring)
+                with torch.cuda.stream(stream):
+                    st.begin(zc[r0:r0 + n] if zc is not None else None, [s[r0:r0 + n] for s in state],
+                             x0=x0[r0:r0 + n])
+                    done = self.done[r0:r0 + n]
+                    for t in range(N):
+                        smp = None if t == 0 else st.sample_args(
+                            t - 1, r0, self.out[r0:r0 + n, t - 1], done, self.seed, self.Mx, self.mode, self.temp,
+                            self.greedy, self.fix_pen)
+                        st.step_fused(t, smp)
+                    st.head()          # the last stroke: head + sampler
+                    rc = lib.skr_mdn_sample_slabs(
+                        st.ZS.data_ptr(), 128, st.S_o, n * 128, st._w["bo"].data_ptr(), n, self.Mx, self.mode,
+                        self.temp, int(self.greedy), int(self.fix_pen), self.seed.data_ptr(), N - 1, r0,
+                        self.out[r0, N - 1].data_ptr(), ld_out, st.X.data_ptr(), 5, done.data_ptr(),
+                        ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
+                    if rc != 0:
+                        raise RuntimeError("skr_mdn_sample_slabs failed (%d)" % rc)
+                continue
             with torch.cuda.stream(stream):
                 st.begin(zc[r0:r0 + n] if zc is not None else None, [s[r0:r0 + n] for s in state])
                 x = x0[r0:r0 + n].contiguous()

@@ -198,3 +198,112 @@ def test_graph_decoder_hyper_concurrent_chunks():
     finally:
         ops.set_backend("auto")
         ops.set_compute_dtype("fp32")
+
+
+def _hyper256(seed=1, H=512, E=16):
+    cfg = VAEConfig(enc_rnn_size=64, dec_rnn_size=H, z_size=32, dec_model="hyper", hyper_num_units=256,
+                    hyper_embedding_size=E, num_classes=0, max_seq_len=32)
+    return cfg, SketchVAE(cfg, seed=seed).to(DEV).eval()
+
+
+@pytest.mark.parametrize("dtype,B", [("bf16", 100), ("bf16", 128), ("fp8", 96)])
+def test_hyper_step_fused_matches_decode_step(dtype, B):
+    """The four-launch stroke (decode_step.hip hyper cell + hyper_mod decode
+    mode + MOD-3 main cell), teacher-forced, against the generic T = 1 path:
+    head outputs within bf16 (fp8: e4m3) tolerances over several strokes."""
+    from sketch_rnn_amd.sample.hyper_step import HyperStepDecoder
+    native.require_hip()
+    ops.set_backend("hip")
+    ops.set_compute_dtype(dtype)
+    try:
+        cfg, m = _hyper256()
+        g = torch.Generator(device=DEV).manual_seed(3)
+        z = torch.randn(B, cfg.z_size, device=DEV, generator=g)
+        zc = m.condition(z, None, B, DEV)
+        state = m.initial_state(zc, B, DEV)
+        st = HyperStepDecoder(m, B, torch.device(DEV))
+        assert st.fused
+        st.begin(zc, state)
+        for t in range(6):
+            x = torch.zeros(B, 5, device=DEV)
+            x[:, :2] = torch.randn(B, 2, device=DEV, generator=g) * 0.5
+            x[:, 2] = 1.0
+            st.X.copy_(x)
+            st.step_fused(t, None)
+            st.head()
+            got = st.ZS[:, :, : cfg.n_out].sum(0) + st._w["bo"][: cfg.n_out]
+            ops.set_compute_dtype("bf16")
+            ref, state = m.decode_step(x, zc, state)
+            ops.set_compute_dtype(dtype)
+            torch.cuda.synchronize()
+            rel = float((got - ref).norm() / ref.norm())
+            assert rel < (6e-2 if dtype == "fp8" else 2e-2), (t, rel)
+    finally:
+        ops.set_backend("auto")
+        ops.set_compute_dtype("fp32")
+
+
+def test_hyper_step_fused_sampler_matches_slab_sampler():
+    """The sampler folded into the decode hyper cell draws exactly what
+    skr_mdn_sample_slabs draws from the same head slabs (stroke, next input,
+    eos flags)."""
+    import ctypes
+    from sketch_rnn_amd.sample.hyper_step import HyperStepDecoder
+    lib = native.require_hip().lib
+    ops.set_backend("hip")
+    ops.set_compute_dtype("bf16")
+    try:
+        cfg, m = _hyper256(seed=5)
+        B, M = 100, cfg.num_mixture
+        zc = m.condition(torch.randn(B, cfg.z_size, device=DEV), None, B, DEV)
+        st = HyperStepDecoder(m, B, torch.device(DEV))
+        x0 = torch.zeros(B, 5, device=DEV)
+        x0[:, 2] = 1
+        st.begin(zc, m.initial_state(zc, B, DEV), x0=x0)
+        seed = torch.tensor([11], dtype=torch.int64, device=DEV)
+        out = torch.zeros(B, 4, 5, device=DEV)
+        done = torch.zeros(B, dtype=torch.int32, device=DEV)
+        done[::7] = 1
+        done_ref = done.clone()
+        st.step_fused(0, None)
+        st.step_fused(1, st.sample_args(0, 3, out[:, 0], done, seed, M, 1, 0.6, False, False))
+        torch.cuda.synchronize()
+        out_ref, nx_ref = torch.zeros(B, 5, device=DEV), torch.zeros(B, 5, device=DEV)
+        rc = lib.skr_mdn_sample_slabs(st.ZS.data_ptr(), 128, st.S_o, B * 128, st._w["bo"].data_ptr(), B, M, 1, 0.6,
+                                      0, 0, seed.data_ptr(), 0, 3, out_ref.data_ptr(), 5, nx_ref.data_ptr(), 5,
+                                      done_ref.data_ptr(), ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
+        assert rc == 0
+        torch.cuda.synchronize()
+        assert torch.equal(out[:, 0], out_ref)
+        assert torch.equal(st.X, nx_ref)
+        assert torch.equal(done, done_ref)
+    finally:
+        ops.set_backend("auto")
+        ops.set_compute_dtype("fp32")
+
+
+def test_graph_decoder_hyper_fused_chunks():
+    """B > 128 decode on the four-launch stroke: graph replay == eager,
+    deterministic, seeded, eos padding intact."""
+    native.require_hip()
+    ops.set_backend("hip")
+    ops.set_compute_dtype("bf16")
+    try:
+        cfg, m = _hyper256(seed=4)
+        a = SM.GraphDecoder(m, batch=300, steps=32, temperature=0.5, use_graph=True)
+        b = SM.GraphDecoder(m, batch=300, steps=32, temperature=0.5, use_graph=False)
+        stp = a._steppers()
+        assert stp is not None and len(stp) == 3 and all(s[2].fused for s in stp)
+        sa, la = a.run(seed=2)
+        sa2, _ = a.run(seed=2)
+        sb, lb = b.run(seed=2)
+        sc, _ = a.run(seed=3)
+        torch.cuda.synchronize()
+        assert torch.equal(sa, sa2) and torch.equal(la, lb)
+        assert torch.allclose(sa, sb, atol=1e-4)
+        assert not torch.equal(sa, sc)
+        for r in range(300):
+            assert torch.all(sa[r, la[r]:, 4] == 1)
+    finally:
+        ops.set_backend("auto")
+        ops.set_compute_dtype("fp32")
