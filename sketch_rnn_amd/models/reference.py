@@ -25,9 +25,19 @@ import torch
 import torch.nn as nn
 
 from .. import ops
-from ..ops import gemm, persist
+from ..ops import gemm, inproj, persist
 from ..config import RefConfig
 from . import cells as C
+
+
+def _stroke_proj(xt: torch.Tensor, W: torch.Tensor, bias: torch.Tensor) -> torch.Tensor:
+    """Layer-0 input projection ``x @ W_x + b`` of the stroke-5 input ([T, B, 5]
+    -> [T, B, 4H] fp32): csrc/inproj.hip on the HIP backend (one write of xp;
+    dW / dbias from one read of dxp), an fp32 addmm elsewhere."""
+    if ops.use_hip(xt) and inproj.bproj_ok(xt) and not xt.requires_grad:
+        return inproj.stroke_input_proj(xt, None, W, bias)
+    T, B, _ = xt.shape
+    return torch.addmm(bias, xt.reshape(T * B, -1), W).view(T, B, -1)
 
 
 class SketchRNN(nn.Module):
@@ -86,7 +96,7 @@ class SketchRNN(nn.Module):
             # layer 1's input projection runs inside the recurrence, so the
             # two layers advance as a wavefront
             p0 = self.layers[0]
-            xp0 = torch.addmm(p0.bias, xt.reshape(T * B, -1), p0.W_x).view(T, B, -1)
+            xp0 = _stroke_proj(xt, p0.W_x, p0.bias)
             out, final = persist.lstm_stack(
                 xp0, [p.W_h for p in self.layers], [s[0] for s in state], [s[1] for s in state],
                 W_in1=self.layers[1].W_x if L == 2 else None, b1=self.layers[1].bias if L == 2 else None,
@@ -96,7 +106,7 @@ class SketchRNN(nn.Module):
             if cfg.model == "lstm":
                 h0, c0 = state[l]
                 if l == 0:   # K = 5: a trivial fp32 product
-                    xp = torch.addmm(p.bias, inp.reshape(T * B, -1), p.W_x).view(T, B, -1)
+                    xp = _stroke_proj(inp, p.W_x, p.bias)
                 else:        # hoisted layer-l input projection in the compute precision (bf16 MFMA)
                     xp = gemm.linear(inp.reshape(T * B, -1), p.W_x, p.bias).view(T, B, -1)
                 out, (hT, cT) = ops.lstm_sequence(xp, p.W_h, h0, c0, forget_bias=1.0, reset=reset,

@@ -1,8 +1,10 @@
 """GRU and vanilla-RNN recurrences on the GPU (reference ``--model gru`` /
 ``--model rnn``, model.py:16-23): per step, skinny split-K MFMA GEMMs
 (``csrc/skinny_gemm.hip``) plus the fused elementwise kernels of
-``csrc/gru_cell.hip``; input projections and weight gradients are single
-large GEMMs over all T*B rows. Same eoc reset semantics as the LSTM path
+``csrc/gru_cell.hip``. Stroke-5 (layer-0) input projections and their
+weight / bias gradients run on ``csrc/inproj.hip`` (fp32, one pass each
+way); recurrent weight gradients on ``csrc/wgrad_gemm.hip`` (bf16,
+256-multiple shapes; :func:`.gemm.wgrad`). Same eoc reset semantics as the LSTM path
 (carry replaced by ``reset_h`` after a step whose input has eoc set, and the
 carried gradient of that step routed to ``reset_h``).
 """
@@ -13,9 +15,15 @@ import ctypes
 import torch
 
 from ..utils import native
-from . import gemm
+from . import gemm, inproj
 from ._hipapi import GruBwdArgs, GruFwdArgs
 from .recurrent import _check
+
+
+def _stroke_input(x: torch.Tensor, ctx) -> bool:
+    """Layer-0 stroke input (3 or 5 features, no gradient wanted): the input
+    projection and its weight gradients run on csrc/inproj.hip in fp32."""
+    return inproj.bproj_ok(x) and not ctx.needs_input_grad[0]
 
 
 def _kind(t: torch.Tensor) -> int:
@@ -30,9 +38,17 @@ class _GRUSeq(torch.autograd.Function):
         H = W_gh.shape[0]
         dev, f32 = x.device, torch.float32
         TB = T * B
-        xl = gemm.lp(x.reshape(TB, IN).contiguous())
-        XG = (gemm.mm(xl, gemm.lp(W_gx)) + b_g).view(T, B, 2 * H)
-        XC = (gemm.mm(xl, gemm.lp(W_cx)) + b_c).view(T, B, H)
+        stroke = _stroke_input(x, ctx)
+        if stroke:   # [x @ W_gx + b_g | x @ W_cx + b_c] in one fp32 pass (csrc/inproj.hip)
+            xl = x.contiguous().float()
+            XP = inproj.bproj_fwd(xl, torch.cat([W_gx, W_cx], 1),
+                                  torch.cat([b_g, b_c]).expand(B, 3 * H))
+            XG, XC, ld_x = XP[..., :2 * H], XP[..., 2 * H:], 3 * H
+        else:
+            xl = gemm.lp(x.reshape(TB, IN).contiguous())
+            XG = (gemm.mm(xl, gemm.lp(W_gx)) + b_g).view(T, B, 2 * H)
+            XC = (gemm.mm(xl, gemm.lp(W_cx)) + b_c).view(T, B, H)
+            ld_x = 0
         dt = gemm.lp_dtype()
         Wg, Wc = gemm.lp(W_gh).contiguous(), gemm.lp(W_ch).contiguous()   # B^T of the backward products
         WgT, WcT = Wg.t().contiguous(), Wc.t().contiguous()               # B^T of h @ W_gh, (r*h) @ W_ch
@@ -52,7 +68,7 @@ class _GRUSeq(torch.autograd.Function):
         rh = reset_h.contiguous() if reset_h is not None else None
         a = GruFwdArgs()
         a.B, a.H = B, H
-        a.ld_xg, a.ld_xc = 2 * H, H
+        a.ld_xg, a.ld_xc = (ld_x, ld_x) if stroke else (2 * H, H)
         a.Rg, a.ld_Rg, a.Rg_nslab, a.Rg_slab = RG.data_ptr(), 2 * H, max(S_g, 1), B * 2 * H
         a.Rc, a.ld_Rc, a.Rc_nslab, a.Rc_slab = RC.data_ptr(), H, max(S_c, 1), B * H
         a.init_h = rh.data_ptr() if rh is not None else None
@@ -68,7 +84,7 @@ class _GRUSeq(torch.autograd.Function):
             a.h_carry, a.h_lp = HP[t + 1].data_ptr(), HL[t + 1].data_ptr()
             _check(lib.lib.skr_gru_fwd(ctypes.byref(a), 1, st), "gru_fwd_out")
         ctx.save_for_backward(xl, W_gx, W_cx, Wg, Wc, HL, HP, RU, RH, CAND, rst)
-        ctx.has_reset = rst is not None
+        ctx.has_reset, ctx.stroke = rst is not None, stroke
         return HOUT, HP[T].clone()
 
     @staticmethod
@@ -118,11 +134,18 @@ class _GRUSeq(torch.autograd.Function):
         dpg2, dpc2 = DPG_lp.view(TB, 2 * H), DPC_lp.view(TB, H)
         dW_gh = gemm.wgrad(HL[:T].reshape(TB, H), dpg2)
         dW_ch = gemm.wgrad(RH.reshape(TB, H), dpc2)
-        dW_gx = gemm.wgrad(xl, dpg2)
-        dW_cx = gemm.wgrad(xl, dpc2)
-        db_g, db_c = DPG.view(TB, 2 * H).sum(0), DPC.view(TB, H).sum(0)
-        dx = gemm.mm(dpg2, gemm.lp(W_gx).t()) + gemm.mm(dpc2, gemm.lp(W_cx).t())
-        return (dx.view(T, B, -1), dh0, None, dinit, dW_gx, dW_gh, db_g, dW_cx, dW_ch, db_c)
+        if ctx.stroke:   # dW_x, dbias from one read of the fp32 gate gradients each
+            db_g, dW_gx = inproj.bproj_reduce(xl, DPG)
+            db_c, dW_cx = inproj.bproj_reduce(xl, DPC)
+            db_g, db_c = db_g.sum(0), db_c.sum(0)
+        else:
+            dW_gx = gemm.wgrad(xl, dpg2)
+            dW_cx = gemm.wgrad(xl, dpc2)
+            db_g, db_c = DPG.view(TB, 2 * H).sum(0), DPC.view(TB, H).sum(0)
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = (gemm.mm(dpg2, gemm.lp(W_gx).t()) + gemm.mm(dpc2, gemm.lp(W_cx).t())).view(T, B, -1)
+        return (dx, dh0, None, dinit, dW_gx, dW_gh, db_g, dW_cx, dW_ch, db_c)
 
 
 class _RNNSeq(torch.autograd.Function):
@@ -133,8 +156,13 @@ class _RNNSeq(torch.autograd.Function):
         H = W_h.shape[0]
         dev, f32 = x.device, torch.float32
         TB = T * B
-        xl = gemm.lp(x.reshape(TB, IN).contiguous())
-        XP = (gemm.mm(xl, gemm.lp(W_x)) + bias).view(T, B, H)
+        stroke = _stroke_input(x, ctx)
+        if stroke:
+            xl = x.contiguous().float()
+            XP = inproj.bproj_fwd(xl, W_x, bias.expand(B, H))
+        else:
+            xl = gemm.lp(x.reshape(TB, IN).contiguous())
+            XP = (gemm.mm(xl, gemm.lp(W_x)) + bias).view(T, B, H)
         dt = gemm.lp_dtype()
         Wl = gemm.lp(W_h).contiguous()
         WlT = Wl.t().contiguous()
@@ -162,7 +190,7 @@ class _RNNSeq(torch.autograd.Function):
             a.reset = rst[t].data_ptr() if rst is not None else None
             _check(lib.lib.skr_gru_fwd(ctypes.byref(a), 2, st), "rnn_fwd")
         ctx.save_for_backward(xl, W_x, Wl, HL, HN, rst)
-        ctx.has_reset = rst is not None
+        ctx.has_reset, ctx.stroke = rst is not None, stroke
         return HOUT, HP[T].clone()
 
     @staticmethod
@@ -196,11 +224,15 @@ class _RNNSeq(torch.autograd.Function):
             gemm.rec_gemm(DP_lp[t], Wl, DHG, S)
         dh0 = DHG.sum(0)
         dp2 = DP_lp.view(TB, H)
-        dW_h = gemm.mm(HL[:T].reshape(TB, H).t(), dp2)
-        dW_x = gemm.mm(xl.t(), dp2)
-        dbias = DP.view(TB, H).sum(0)
-        dx = gemm.mm(dp2, gemm.lp(W_x).t())
-        return (dx.view(T, B, -1), dh0, None, dinit, dW_x, dW_h, dbias)
+        dW_h = gemm.wgrad(HL[:T].reshape(TB, H), dp2)
+        if ctx.stroke:
+            dbias, dW_x = inproj.bproj_reduce(xl, DP)
+            dbias = dbias.sum(0)
+        else:
+            dW_x = gemm.wgrad(xl, dp2)
+            dbias = DP.view(TB, H).sum(0)
+        dx = gemm.mm(dp2, gemm.lp(W_x).t()).view(T, B, -1) if ctx.needs_input_grad[0] else None
+        return (dx, dh0, None, dinit, dW_x, dW_h, dbias)
 
 
 def gru_sequence_hip(p, x, h0, reset=None, reset_h=None):

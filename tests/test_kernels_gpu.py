@@ -571,10 +571,14 @@ def test_fused_adam_matches_oracle():
             torch.testing.assert_close(o1.scalars[:2], o2.scalars[:2])
 
 
-@pytest.mark.parametrize("kind,H,reset,dtype", [("gru", 64, False, "fp32"), ("gru", 256, True, "fp32"),
-                                                ("gru", 300, True, "bf16"), ("rnn", 256, True, "fp32"),
-                                                ("rnn", 128, False, "bf16")])
-def test_gru_rnn_sequence_matches_oracle(kind, H, reset, dtype):
+@pytest.mark.parametrize("kind,H,reset,dtype,xgrad", [("gru", 64, False, "fp32", True), ("gru", 256, True, "fp32", True),
+                                                      ("gru", 300, True, "bf16", True), ("rnn", 256, True, "fp32", True),
+                                                      ("rnn", 128, False, "bf16", True),
+                                                      # data input (layer 0): csrc/inproj.hip projection + grads
+                                                      ("gru", 256, True, "bf16", False),
+                                                      ("rnn", 256, True, "bf16", False),
+                                                      ("gru", 64, False, "fp32", False)])
+def test_gru_rnn_sequence_matches_oracle(kind, H, reset, dtype, xgrad):
     torch.manual_seed(11)
     T, B, IN = 9, 6, 5
     Pcls = C.GRUParams if kind == "gru" else C.RNNParams
@@ -586,14 +590,15 @@ def test_gru_rnn_sequence_matches_oracle(kind, H, reset, dtype):
     def run(backend):
         ops.set_backend(backend)
         ops.set_compute_dtype(dtype if backend == "hip" else "fp32")
-        xs = [x.detach().clone().requires_grad_(), h0.detach().clone().requires_grad_()]
+        xs = [x.detach().clone().requires_grad_(xgrad), h0.detach().clone().requires_grad_()]
         for q in p.parameters():
             q.grad = None
         out, hT = (ops.gru_sequence if kind == "gru" else ops.rnn_sequence)(p, xs[0], xs[1], reset=rst,
                                                                              reset_h=xs[1] if reset else None)
         w = _weights([out, hT])
         ((out * w[0]).sum() + (hT * w[1]).sum()).backward()
-        return [out.detach(), hT.detach()], [xs[0].grad, xs[1].grad] + [q.grad.clone() for q in p.parameters()]
+        gx = [xs[0].grad] if xgrad else []
+        return [out.detach(), hT.detach()], gx + [xs[1].grad] + [q.grad.clone() for q in p.parameters()]
 
     o_h, g_h = run("hip")
     o_t, g_t = run("torch")
