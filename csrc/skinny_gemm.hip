@@ -516,14 +516,13 @@ SKR_API int skr_skinny_gemm_v2(const void* A, int64_t lda, int64_t a_batch, cons
     // 64-wide N tiles: with the 3-deep ring two workgroups share a CU and
     // 64 beat 128 on every recurrent shape (scripts/bench_gemm.py)
     if (bn == 0) bn = (g_nstage == 3) ? 64 : ((N % 128 == 0 && (N / 128) * splits * batch >= 144) ? 128 : 64);
-    if (M < 1 || M > BM || (bn != 32 && bn != 64 && bn != 128) || N % bn != 0 || splits < 1 || K % splits != 0)
+    if (M < 1 || M > BM || (bn != 64 && bn != 128) || N % bn != 0 || splits < 1 || K % splits != 0)
         return -2;
     const int kslice = K / splits;
     if (kslice % BK != 0 || lda % 8 != 0 || ldb % 8 != 0) return -3;
     if (((uintptr_t)A | (uintptr_t)Bt) & 15) return -4;
     const dim3 grid(N / bn, splits, batch);
 #define SKR_V2(BN_, NS_) launch_v2<BN_, NS_>(grid, s, A, lda, a_batch, Bt, ldb, b_batch, C, ldc, c_slab, c_batch, M, kslice)
-    if (bn == 32) return SKR_V2(32, 3);   // (narrow outputs: the per-block HyperLSTM dz = dvec W_a^T)
     if (bn == 128) return g_nstage == 3 ? SKR_V2(128, 3) : SKR_V2(128, 4);
     return g_nstage == 3 ? SKR_V2(64, 3) : g_nstage == 6 ? SKR_V2(64, 6) : SKR_V2(64, 4);
 #undef SKR_V2
@@ -605,86 +604,6 @@ SKR_API int skr_skinny_gemm_group_cellbwd(const GemmProblem* probs, int n, const
 #undef SKR_GC
     return SKR_CHECK_LAUNCH();
 }
-
-// As skr_skinny_gemm_group_cellbwd with the hyper cell's dh from the
-// unfolded hyper-norm projections: the cell rows first sum the dz split-K
-// slabs of their row (dz = dvec W_a^T per block, [nslab][B][ncol]) and form
-// dh = dz W_z^T (W_z bf16 [Hh][ncol], embeddings padded to 32 per block),
-// store it to the row's scratch (read back by the same thread in the cell
-// body), and keep the summed dz for the W_z / W_a / b_z gradients.
-struct DzArgs {
-    const float* dz; int nslab; int64_t slab;
-    int ncol;
-    const __hip_bfloat16* wz;
-    float* dho;
-    float* dzsum;
-};
-
-namespace {
-constexpr int kDzMaxCol = 384;
-
-template <int BN, int NS>
-__global__ __launch_bounds__(256) void skinny_gemm_group_cellbwd_dz_kernel(const GemmGroup g, const skr::BwdArgs cell,
-                                                                          const DzArgs z) {
-    extern __shared__ __attribute__((aligned(16))) __hip_bfloat16 smem[];
-    if ((int)blockIdx.x < cell.B) {
-        __shared__ __attribute__((aligned(16))) float dzs[kDzMaxCol];
-        const int b = blockIdx.x, tid = threadIdx.x;
-        for (int c = tid; c < z.ncol; c += 256) {
-            float v = 0.f;
-            for (int s = 0; s < z.nslab; ++s) v += z.dz[s * z.slab + (int64_t)b * z.ncol + c];
-            dzs[c] = v;
-            if (z.dzsum) z.dzsum[(int64_t)b * z.ncol + c] = v;
-        }
-        __syncthreads();
-        if (tid < cell.H) {
-            const bf16x8* wr = (const bf16x8*)(z.wz + (int64_t)tid * z.ncol);
-            float acc = 0.f;
-            for (int c8 = 0; c8 < z.ncol / 8; ++c8) {
-                const bf16x8 w8 = wr[c8];
-#pragma unroll
-                for (int k = 0; k < 8; ++k) acc += dzs[8 * c8 + k] * (float)w8[k];
-            }
-            z.dho[(int64_t)b * cell.H + tid] = acc;   // read back by this same thread in the cell body
-        }
-        cell_bwd_body<256, 1, 1, true, 0, 1>(cell, 0, b, 1);
-        return;
-    }
-    group_tile<BN, NS>(g, blockIdx.x - cell.B, smem);
-}
-}  // namespace
-
-SKR_API int skr_skinny_gemm_group_cellbwd_dz(const GemmProblem* probs, int n, const skr::BwdArgs* cell,
-                                             const DzArgs* z, hipStream_t s) {
-    if (n < 1 || n > kMaxGroup || cell == nullptr || z == nullptr) return -2;
-    const skr::BwdArgs& a = *cell;
-    if (a.H < 1 || a.H > 256 || a.cluster > 1 || a.reset != nullptr || a.B < 1) return -2;
-    if (a.dh_out != z->dho || a.dho_nslab != 1 || z->ncol < 8 || z->ncol > kDzMaxCol || z->ncol % 8 || z->nslab < 1 ||
-        ((uintptr_t)z->wz & 15))
-        return -3;
-    if ((a.dh_rec && (a.dhr_nslab < 1 || a.dhr_nslab > kRecSlabs)) ||
-        (a.dh_rec2 && (a.dhr2_nslab < 1 || a.dhr2_nslab > kRecSlabs)))
-        return -3;
-    GemmGroup g{};
-    g.n = n;
-    g.start[0] = 0;
-    for (int i = 0; i < n; ++i) {
-        const GemmProblem& p = probs[i];
-        if (p.M < 1 || p.M > BM || p.N % 64 != 0 || p.splits < 1 || p.K % p.splits != 0) return -2;
-        if ((p.K / p.splits) % BK != 0 || p.lda % 8 != 0 || p.ldb % 8 != 0) return -3;
-        if (((uintptr_t)p.A | (uintptr_t)p.Bt) & 15) return -4;
-        g.p[i] = p;
-        g.start[i + 1] = g.start[i] + (p.N / 64) * p.splits;
-    }
-    for (int i = n + 1; i <= kMaxGroup; ++i) g.start[i] = g.start[n];
-    const size_t lds = (size_t)3 * (BM + 64) * BK * 2;
-    set_lds_attr(skinny_gemm_group_cellbwd_dz_kernel<64, 3>, lds);
-    hipLaunchKernelGGL((skinny_gemm_group_cellbwd_dz_kernel<64, 3>), dim3(a.B + g.start[n]), dim3(256), lds, s, g, a,
-                       *z);
-    return SKR_CHECK_LAUNCH();
-}
-
-SKR_API int skr_dz_args_size() { return (int)sizeof(DzArgs); }
 
 // fp32 operands: same contract as skr_skinny_gemm_v2 with kslice % 32 == 0
 // (64-wide N tiles, 3-deep ring of (128 + 64) x 128 B stages).

@@ -275,17 +275,6 @@ class GemmProblem8(C.Structure):
     ]
 
 
-class DzArgs(C.Structure):
-    """Mirror of ``DzArgs`` in csrc/skinny_gemm.hip (the unfolded HyperLSTM hyper-cell backward)."""
-    _fields_ = [
-        ("dz", _p), ("nslab", _i), ("slab", _i64),
-        ("ncol", _i),
-        ("wz", _p),
-        ("dho", _p),
-        ("dzsum", _p),
-    ]
-
-
 class ModDecode(C.Structure):
     """Mirror of ``ModDecode`` in csrc/hyper_mod.hip (decode-mode inputs of the
     HyperLSTM modulation kernel: fp32 hyper state, x-projection from the stroke)."""
@@ -388,9 +377,6 @@ class HipLib:
         lib.skr_skinny_gemm_group.restype = _i
         lib.skr_skinny_gemm_group_cellbwd.argtypes = [C.POINTER(GemmProblem), _i, C.POINTER(LstmBwdArgs), _p]
         lib.skr_skinny_gemm_group_cellbwd.restype = _i
-        lib.skr_skinny_gemm_group_cellbwd_dz.argtypes = [C.POINTER(GemmProblem), _i, C.POINTER(LstmBwdArgs),
-                                                         C.POINTER(DzArgs), _p]
-        lib.skr_skinny_gemm_group_cellbwd_dz.restype = _i
         lib.skr_lstm_fused_fwd.argtypes = [C.POINTER(FusedFwdArgs), _p]
         lib.skr_lstm_fused_fwd.restype = _i
         lib.skr_lstm_fused_bwd.argtypes = [C.POINTER(FusedBwdArgs), _p]
@@ -411,8 +397,8 @@ class HipLib:
         lib.skr_skinny_gemm_fp8_v2.restype = _i
         lib.skr_skinny_gemm_group_fp8.argtypes = [C.POINTER(GemmProblem8), _i, _p]
         lib.skr_skinny_gemm_group_fp8.restype = _i
-        lib.skr_hyper_mod_fwd.argtypes = [_p, _i64, _p, _p, _p, _i, _p, _p, _p, _p, _i64, _i, _p, _p, _p, _p, _i, _i,
-                                          _i, C.POINTER(ModDecode), _p]
+        lib.skr_hyper_mod_fwd.argtypes = [_p, _i64, _p, _p, _p, _p, _i64, _i, _p, _p, _p, _p, _i, _i, _i,
+                                          C.POINTER(ModDecode), _p]
         lib.skr_hyper_mod_fwd.restype = _i
         lib.skr_cast_transpose_bf16.argtypes = [_p, _i64, _i64, _i, _i, _i, _p, _i64, _i64, _p, _i64, _i64, _p]
         lib.skr_cast_transpose_bf16.restype = _i
@@ -433,7 +419,6 @@ class HipLib:
                           ("skr_mdn_head_dw_args_size", HeadDw),
                           ("skr_decode_ref_args_size", DecArgs),
                           ("skr_gemm_problem_size", GemmProblem),
-                          ("skr_dz_args_size", DzArgs),
                           ("skr_decode_sample_size", DecodeSample),
                           ("skr_gemm_problem8_size", GemmProblem8)):
             fn = getattr(lib, name)

@@ -215,7 +215,6 @@ def wgrad(a: torch.Tensor, b: torch.Tensor, colsum: bool = False, out: Optional[
     return (out, cs) if colsum else out
 
 
-
 _SPLITS = (1, 2, 4, 8, 16, 32)  # powers of two: the cell kernels sum <= 8 slabs unrolled
 
 
@@ -360,20 +359,6 @@ def rec_gemm_group_cellbwd(jobs, cell_args) -> None:
                                                torch.cuda.current_stream().cuda_stream)
     if rc != 0:
         raise RuntimeError("skr_skinny_gemm_group_cellbwd failed (%d)" % rc)
-
-
-def rec_gemm_group_cellbwd_dz(jobs, cell_args, dz_args) -> None:
-    """:func:`rec_gemm_group_cellbwd` with the hyper cell's dh formed from the
-    unfolded projections' dz slabs (``dz_args``: a filled ``DzArgs``;
-    ``skr_skinny_gemm_group_cellbwd_dz``)."""
-    import ctypes
-    from ..utils import native
-    lib = native.require_hip()
-    probs = _problems(jobs)
-    rc = lib.lib.skr_skinny_gemm_group_cellbwd_dz(probs, len(jobs), ctypes.byref(cell_args), ctypes.byref(dz_args),
-                                                  torch.cuda.current_stream().cuda_stream)
-    if rc != 0:
-        raise RuntimeError("skr_skinny_gemm_group_cellbwd_dz failed (%d)" % rc)
 
 
 # ---- inference-time helpers ------------------------------------------------------------

@@ -21,7 +21,7 @@ import torch
 
 from ..utils import native
 from . import gemm
-from ._hipapi import DzArgs, LstmBwdArgs, LstmFwdArgs
+from ._hipapi import LstmBwdArgs, LstmFwdArgs
 from .inproj import bproj_fwd, bproj_ok, bproj_reduce
 from .recurrent import (ROW_STATS, _cell_bwd, _cell_fwd, _check, _ClusterSync, _fp8_ok, _inference, _ln_saves_lp,
                         _lp_kind, _ptr, _Saved, _seed_tensor, _stream, _to_fp8_act, cell_geometry)
@@ -38,10 +38,10 @@ HYPER_MAIN_C = int(os.environ.get("SKR_HYPER_MAIN_C", "0"))   # workgroups per r
 # product only the next step reads. SKR_HYPER_BWD_FUSE=0 keeps [main cell] ->
 # [dR_main W_h^T + dvec P^T] -> [hyper cell] -> [dR_hyp W_y^T].
 HYPER_BWD_FUSE = os.environ.get("SKR_HYPER_BWD_FUSE", "1") != "0"
-# Backward of the unfolded hyper-norm projections (dz = dvec W_a^T, dh = dz
-# W_z^T in the hyper cell's launch, per-block weight gradients) whenever the
-# forward saved z; False: the folded dvec P^T path (tests compare the two).
-UNFOLD_BWD = True
+# (Round 4 measured the hyper-norm projections unfolded -- vec = bf16(hh W_z)
+# W_a + q forward, dz = dvec W_a^T / dh = dz W_z^T backward -- at 27.8 vs
+# 24.6 ms per training step: W_z re-read from L2 by every workgroup costs more
+# than the folded P it replaces; profiles/r4/unfold_ab.txt.)
 # (Round 4 measured one-launch forward / backward steps -- R_hyp, hyper cell,
 # h @ W_h and the modulation with in-launch hand-offs; the backward chain
 # beside dR_main W_h^T -- at +1.5 / +3.8 ms per training step: every
@@ -50,18 +50,6 @@ UNFOLD_BWD = True
 # (The forward twin -- h W_y alone, then the hyper cell beside h W_h in one
 # launch -- measured 0.15 ms/step slower on vae_large and was removed:
 # profiles/r3/hyper_fused_cell_ab.txt.)
-
-
-def unfold_norm(W_z: torch.Tensor, W_a: torch.Tensor):
-    """The hyper-norm projections of csrc/hyper_mod.hip in bf16: W_z [Hh, 12E]
-    -> WzT [12][32][Hh] (W_z^T per block) and W_a [12, E, H] -> WaT [12][H][32]
-    (unit-major), embeddings padded to 32 with zeros."""
-    Hh, (nb, E, H) = W_z.shape[0], W_a.shape
-    WzT = torch.zeros(nb, 32, Hh, device=W_z.device, dtype=torch.bfloat16)
-    WzT[:, :E] = W_z.detach().view(Hh, nb, E).permute(1, 2, 0)
-    WaT = torch.zeros(nb, H, 32, device=W_z.device, dtype=torch.bfloat16)
-    WaT[:, :, :E] = W_a.detach().permute(0, 2, 1)
-    return WzT, WaT
 
 
 def _split_override(var: str, planned: int, K: int) -> int:
@@ -249,15 +237,8 @@ class _HyperSeq(torch.autograd.Function):
         # no statistics exchange for the gates (MOD 3) and VEC carries q (and
         # the main bias in its shift block) -- the backward uses a zero vec_bias
         hmod = HYPER_MOD and vbf and dev.type == "cuda" and Hh == 256 and B <= 128 and H % 32 == 0 and \
-            S_m in (1, 2, 4) and E <= 32
-        ZS = None
+            S_m in (1, 2, 4)
         if hmod:
-            # the hyper-norm projections unfolded (csrc/hyper_mod.hip): W_z^T and W_a
-            # per block in bf16, embeddings padded to 32; z = hh W_z + b_z saved
-            # for the parameter gradients
-            WzT, WaT = gemm.derived((W_z, W_a), "hypunfold", unfold_norm) if infer else unfold_norm(W_z, W_a)
-            bz_c = b_z.detach().contiguous()
-            ZS = None if infer else torch.empty(T, B, 12 * E, device=dev, dtype=f32)
             mod = 3
             if qb_f is not None:   # q + the main bias on the shift block, from the fold kernel
                 qb = qb_f
@@ -316,9 +297,8 @@ class _HyperSeq(torch.autograd.Function):
                 rgemm(A[t], WyT, RY, S_y)
             _cell_fwd(lib, ah, True, 0, st, "hyper_fwd_step")
             if hmod:
-                _check(lib.lib.skr_hyper_mod_fwd(A[t + 1, :, H:].data_ptr(), K, WzT.data_ptr(), WaT.data_ptr(),
-                                                 bz_c.data_ptr(), E, _ptr(ZS[t] if ZS is not None else None),
-                                                 qb.data_ptr(), XHc[t].data_ptr(), RM[rmi(t)].data_ptr(), B * G, S_m,
+                _check(lib.lib.skr_hyper_mod_fwd(A[t + 1, :, H:].data_ptr(), K, PlT.data_ptr(), qb.data_ptr(),
+                                                 XHc[t].data_ptr(), RM[rmi(t)].data_ptr(), B * G, S_m,
                                                  VEC[t].data_ptr(), GP.data_ptr(), _ptr(RLP[t] if RLP is not None else None),
                                                  GS.data_ptr(), B, H, Hh, None, st), "hyper_mod_fwd")
                 am.gpre, am.gstats, am.gstat_tiles = GP.data_ptr(), GS.data_ptr(), H // 32
@@ -339,7 +319,7 @@ class _HyperSeq(torch.autograd.Function):
         for k, v in dict(xl=xl, x=x, zc=zc, bp=bp, XH=XH, Whl=Whl, Wyl=Wyl, Pl=Pl, q=q, S_m=S_m, A=A, RM=RM,
                          RLP=RLP, CC=CC, HCC=HCC, XHAT=XHAT, RSTD=RSTD, CHAT=CHAT, HH=HH, HXHAT=HXHAT, HRSTD=HRSTD,
                          HCHAT=HCHAT, VEC=VEC, seed=sd, meta=meta, slp=slp, W_h=W_h, W_x=W_x, hW_x=hW_x, W_z=W_z, b_z=b_z, W_a=W_a,
-                         mln=mln, hln=hln, vec_folded=hmod, mln_on=mln_on, ACT=ACT, COUT=COUT, Z=ZS).items():
+                         mln=mln, hln=hln, vec_folded=hmod, mln_on=mln_on, ACT=ACT, COUT=COUT).items():
             setattr(s, k, v)
         ctx.s = s
         ctx.dims = (T, B, IX, IN, H, Hh, E)
@@ -429,24 +409,6 @@ class _HyperSeq(torch.autograd.Function):
         st = _stream()
         group = lp_on and gemm.GROUPED and S_am >= 1 and S_h >= 1
         first = not fin   # (the last time step runs first)
-        # unfolded hyper-norm projections (the forward saved z): dz = dvec_k W_a_k^T
-        # per block as one batched 32-column GEMM, then the hyper cell's launch
-        # forms dh = dz W_z^T per row (csrc/skinny_gemm.hip cellbwd_dz) -- the
-        # folded P (12.6 MB per step) is never read
-        unf = UNFOLD_BWD and s.Z is not None and bfuse
-        if unf:
-            Wa32 = torch.zeros(12, 32, H, device=dev, dtype=torch.bfloat16)
-            Wa32[:, :E] = s.W_a.detach()
-            WzP = torch.zeros(Hh, 12, 32, device=dev, dtype=torch.bfloat16)
-            WzP[:, :, :E] = s.W_z.detach().view(Hh, 12, E)
-            S_z = max(d for d in (1, 2, 4, 8, 16, 32) if (H // 64) % d == 0 and 12 * d <= 256)
-            DZ = torch.empty(S_z, B, 384, device=dev, dtype=f32)
-            DHO = torch.empty(B, Hh, device=dev, dtype=f32)
-            DZS = torch.empty(T, B, 384, device=dev, dtype=f32)   # summed dz per step (parameter gradients)
-            ah.dh_out, ah.dho_nslab, ah.dho_slab = DHO.data_ptr(), 1, B * Hh
-            dza = DzArgs()
-            dza.dz, dza.nslab, dza.slab, dza.ncol = DZ.data_ptr(), S_z, B * 384, 384
-            dza.wz, dza.dho = WzP.data_ptr(), DHO.data_ptr()
         for t in range(T - 1, -1, -1):
             clm.set(am, t)
             clh.set(ah, t)
@@ -477,13 +439,7 @@ class _HyperSeq(torch.autograd.Function):
             ah.dG = None if lp_on else dRY[t].data_ptr()
             ah.dG_lp = dRY_lp[t].data_ptr() if lp_on else None
             ah.dlny, ah.dlncy = HDLNY[t].data_ptr(), HDLNCY[t].data_ptr()
-            if unf:   # dz = dvec W_a^T per block, then the hyper cell (dh = dz W_z^T) beside dR_main W_h^T
-                _check(lib.lib.skr_skinny_gemm_v2(dVEC[t].data_ptr(), 12 * H, H, Wa32.data_ptr(), H, 32 * H,
-                                                  DZ.data_ptr(), 384, B * 384, 32, B, 32, H, S_z, 12, 32, st), "dz gemm")
-                dza.dzsum = DZS[t].data_ptr()
-                gemm.rec_gemm_group_cellbwd_dz([(dRM_lp[t], s.Whl, DAM, S_am)], ah, dza)
-                ROW_STATS["cluster"] += 1
-            elif bfuse:   # dvec P^T, then the hyper cell beside dR_main W_h^T (one launch)
+            if bfuse:   # dvec P^T, then the hyper cell beside dR_main W_h^T (one launch)
                 gemm.rec_gemm(dVEC[t], s.Pl, DHZ, S_h)
                 gemm.rec_gemm_group_cellbwd([(dRM_lp[t], s.Whl, DAM, S_am)], ah)
                 ROW_STATS["cluster"] += 1   # (the clustered cell body, C = 1)
@@ -515,18 +471,7 @@ class _HyperSeq(torch.autograd.Function):
         # hh_t rows: the bf16 GEMM operand of step t + 1 (no resets on this path,
         # so it is exactly bf16(HH[t])) -- no conversion pass
         HHl = s.A[1:T + 1].reshape(TB, K)[:, H:] if lp_on else s.HH.view(TB, Hh)
-        if unf:   # vec_k = z_k W_a_k, z = hh W_z + b_z: per-block long-K products over the saved z / dz
-            dV2 = dVEC.view(TB, 12 * H)
-            Zl = gemm.lp(s.Z.view(TB, 12 * E))
-            dWa = torch.empty(12, E, H, device=dev, dtype=f32)
-            for k in range(12):
-                gemm.mm(Zl[:, k * E:(k + 1) * E].t(), dV2[:, k * H:(k + 1) * H], out=dWa[k])
-            dz = DZS.view(TB, 12, 32)[:, :, :E].reshape(TB, 12 * E)
-            dW_z = gemm.mm(HHl.t(), gemm.lp(dz))
-            db_z = dz.sum(0)
-            dbias = dVEC[:, :, 8 * H:].sum(dim=(0, 1), dtype=f32)
-        else:
-            dP1, sV = gemm.wgrad(HHl, dVEC.view(TB, 12 * H), colsum=True)
+        dP1, sV = gemm.wgrad(HHl, dVEC.view(TB, 12 * H), colsum=True)
         g_ln, g_hln = [], []
         for dy, xh, n, out in ((DLNY, s.XHAT, G, g_ln), (DLNCY, s.CHAT, H, g_ln), (HDLNY, s.HXHAT, Gh, g_hln),
                                (HDLNCY, s.HCHAT, Hh, g_hln)):
@@ -563,8 +508,7 @@ class _HyperSeq(torch.autograd.Function):
                 dx, dzc = dxf[..., :IX], dxf[..., IX:].sum(0)
             else:
                 dx = dxf
-        if not unf:
-            dW_z, db_z, dWa, dbias = _hyper_proj_grads(dP1, sV, s, Hh, H, E)
+        dW_z, db_z, dWa, dbias = _hyper_proj_grads(dP1, sV, s, Hh, H, E)
         ctx.s = None
         return (dx, dzc, dh0, dc_rec, dhh0, dhc_rec, None, dW_x, dW_h, dbias, dhW_x, dhW_h,
                 g_hln[0], g_hln[1], g_hln[2], g_hln[3], dW_z, db_z, dWa, g_ln[0], g_ln[1], g_ln[2], g_ln[3], None)

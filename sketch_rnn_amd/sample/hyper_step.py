@@ -31,10 +31,10 @@ Four-launch stroke (:meth:`HyperStepDecoder.step_fused`, the
    the head slabs (same keyed draws as ``skr_mdn_sample_slabs``), writes it
    out and forms the hyper cell's x-projection from it in-register, then the
    hyper LayerNorm cell;
-3. ``skr_hyper_mod_fwd`` (csrc/hyper_mod.hip) in decode mode: unfolded
-   hyper-norm projections ``bf16(hh W_z) W_a + q`` on MFMA, the main cell's
-   x-projection from the stroke, the modulated gate pre-activations and their
-   LayerNorm partial sums;
+3. ``skr_hyper_mod_fwd`` (csrc/hyper_mod.hip) in decode mode: the
+   modulation vectors ``hh P + q`` on MFMA, the main cell's x-projection
+   from the stroke, the modulated gate pre-activations and their LayerNorm
+   partial sums;
 4. the main LayerNorm cell (MOD 3: pre-activations precomputed).
 
 After the last stroke :meth:`finish` runs the head GEMM + sampler once.
@@ -155,16 +155,15 @@ class HyperStepDecoder:
             WoT=gemm.derived(m.output_w, "stepWoT", wout),
             bo=m.output_b.detach().float().contiguous(),
         )
-        if self.fused:
-            from ..ops.hyper import unfold_norm
+        if self.fused:   # bf16 folded P^T for csrc/hyper_mod.hip, q + the main bias on the shift block
+            P, q = self._fold()
 
-            def qbias(b_z, W_a, bias):
-                q = torch.bmm(b_z.detach().view(12, 1, E), W_a.detach()).reshape(12, H)
-                q[8:] += bias.detach().view(4, H)
-                return q.reshape(12 * H).float().contiguous()
-            w["UNF"] = gemm.derived((p.W_z, p.W_a), "hypunfold", unfold_norm)
-            w["QB"] = gemm.derived((p.b_z, p.W_a, p.bias), "hypQB", qbias)
-            w["bz"] = p.b_z.detach().float().contiguous()
+            def qbias(q, bias):
+                qb = q.detach().clone()
+                qb[8:] += bias.detach().view(4, H)
+                return qb.reshape(12 * H).float().contiguous()
+            w["PL"] = P
+            w["QB"] = gemm.derived((q, p.bias), "hypQB", qbias)
         if self.fp8:   # per-output-column e4m3 weights
             w["WhT"] = gemm.derived(w["WhT"], "q8", gemm.quantize_fp8_rows)
             w["WyT"] = gemm.derived(w["WyT"], "q8", gemm.quantize_fp8_rows)
@@ -312,11 +311,9 @@ class HyperStepDecoder:
         dec.hh32 = self.HH.data_ptr() if f8 else None
         dec.x5, dec.w5, dec.ldw5 = self.X.data_ptr(), w["W5"].data_ptr(), G + Gh
         dec.zp, dec.ldzp = self.ZP.data_ptr(), G + Gh
-        WzT, WaT = w["UNF"]
-        rc = lib.skr_hyper_mod_fwd(None if f8 else self.A[:, H:].data_ptr(), K, WzT.data_ptr(), WaT.data_ptr(),
-                                   w["bz"].data_ptr(), self.E, None, w["QB"].data_ptr(), None, self.RM.data_ptr(),
-                                   B * G, self.S_m, None, self.GP.data_ptr(), None, self.GS.data_ptr(), B, H, Hh,
-                                   ctypes.byref(dec), st)
+        rc = lib.skr_hyper_mod_fwd(None if f8 else self.A[:, H:].data_ptr(), K, w["PL"].data_ptr(),
+                                   w["QB"].data_ptr(), None, self.RM.data_ptr(), B * G, self.S_m, None,
+                                   self.GP.data_ptr(), None, self.GS.data_ptr(), B, H, Hh, ctypes.byref(dec), st)
         if rc != 0:
             raise RuntimeError("skr_hyper_mod_fwd (decode) failed (%d)" % rc)
         am.gpre, am.gstats, am.gstat_tiles = self.GP.data_ptr(), self.GS.data_ptr(), H // 32
