@@ -41,7 +41,7 @@ typedef __attribute__((ext_vector_type(4))) float f32x4;
 typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 
 constexpr int HH = 256, NTH = 384, TU = 32;      // hyper units (K), threads, units per tile
-constexpr int MAXB = 128, NRT = MAXB / 16;
+constexpr int MAXB = 128;                        // rows (16-row MFMA tiles: NRT <= 8)
 
 __device__ __forceinline__ int sw(int row, int chunk) { return row * HH + ((chunk ^ (row & 15)) << 3); }
 
@@ -66,7 +66,9 @@ struct ModDecode {
 
 namespace {
 
-template <int NS>
+// NRT: 16-row tiles staged and multiplied (rows up to 16 NRT; a B = 100 launch
+// pays for 112 rows, not MAXB).
+template <int NS, int NRT>
 __global__ __launch_bounds__(NTH) void hyper_mod_fwd(const ModDecode dec, const __hip_bfloat16* __restrict__ hh, int64_t ld_hh,
                                                      const __hip_bfloat16* __restrict__ PlT,   // [12H][HH]
                                                      const float* __restrict__ qb,             // [12H]
@@ -77,8 +79,9 @@ __global__ __launch_bounds__(NTH) void hyper_mod_fwd(const ModDecode dec, const 
                                                      __hip_bfloat16* __restrict__ rlp,          // [B][4H] or null
                                                      float* __restrict__ stats,                 // [B][4][H/TU][2]
                                                      int B, int H) {
-    __shared__ __attribute__((aligned(16))) __hip_bfloat16 sA[MAXB * HH];   // 64 KB
-    __shared__ __attribute__((aligned(16))) float sV[6][MAXB][16];          // 48 KB
+    constexpr int MB = 16 * NRT;
+    __shared__ __attribute__((aligned(16))) __hip_bfloat16 sA[MB * HH];     // <= 64 KB
+    __shared__ __attribute__((aligned(16))) float sV[6][MB][16];            // <= 48 KB
     const int q = blockIdx.y, u0 = blockIdx.x * TU, ntile = H / TU;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int fr = lane & 15, fq = lane >> 4;
@@ -91,7 +94,7 @@ __global__ __launch_bounds__(NTH) void hyper_mod_fwd(const ModDecode dec, const 
 #pragma unroll
     for (int ks = 0; ks < 8; ++ks) pf[ks] = *(const bf16x8*)(PlT + (int64_t)(vcol + fr) * HH + 32 * ks + 8 * fq);
     const float qv = qb[vcol + fr];
-    constexpr int RPT = (MAXB + NTH / 8 - 1) / (NTH / 8);    // rows per thread (3)
+    constexpr int RPT = (MB + NTH / 8 - 1) / (NTH / 8);      // rows per thread (<= 3)
     const int rg = tid >> 3, ug = tid & 7, ul = 4 * ug;
     f32x4 x4[RPT], r4[RPT];
 #pragma unroll
@@ -114,7 +117,7 @@ __global__ __launch_bounds__(NTH) void hyper_mod_fwd(const ModDecode dec, const 
             r4[k] += t;
         }
     }
-    constexpr int NPC = MAXB * (HH / 8), SPT = (NPC + NTH - 1) / NTH;   // 16-byte hh pieces (per thread: 10)
+    constexpr int NPC = MB * (HH / 8), SPT = (NPC + NTH - 1) / NTH;     // 16-byte hh pieces per thread
     bf16x8 hv[SPT];
 #pragma unroll
     for (int k = 0; k < SPT; ++k) {
@@ -225,11 +228,19 @@ SKR_API int skr_hyper_mod_fwd(const void* hh, int64_t ld_hh, const void* PlT, co
     const auto* p = (const __hip_bfloat16*)PlT;
     auto* v = (__hip_bfloat16*)vec;
     auto* rl = (__hip_bfloat16*)rlp;
-    switch (nslab) {
-        case 1: hipLaunchKernelGGL(hyper_mod_fwd<1>, grid, dim3(NTH), 0, s, dz, a, ld_hh, p, qb, xh, R, r_slab, v, g, rl, stats, B, H); break;
-        case 2: hipLaunchKernelGGL(hyper_mod_fwd<2>, grid, dim3(NTH), 0, s, dz, a, ld_hh, p, qb, xh, R, r_slab, v, g, rl, stats, B, H); break;
-        case 4: hipLaunchKernelGGL(hyper_mod_fwd<4>, grid, dim3(NTH), 0, s, dz, a, ld_hh, p, qb, xh, R, r_slab, v, g, rl, stats, B, H); break;
-        default: return -3;
+    const int nrt = B <= 32 ? 2 : B <= 64 ? 4 : B <= 112 ? 7 : 8;
+    if (nslab != 1 && nslab != 2 && nslab != 4) return -3;
+#define SKR_HM(NS_, NRT_) \
+    hipLaunchKernelGGL((hyper_mod_fwd<NS_, NRT_>), grid, dim3(NTH), 0, s, dz, a, ld_hh, p, qb, xh, R, r_slab, v, g, rl, stats, B, H)
+#define SKR_HM_NS(NRT_) \
+    do { if (nslab == 1) SKR_HM(1, NRT_); else if (nslab == 2) SKR_HM(2, NRT_); else SKR_HM(4, NRT_); } while (0)
+    switch (nrt) {
+        case 2: SKR_HM_NS(2); break;
+        case 4: SKR_HM_NS(4); break;
+        case 7: SKR_HM_NS(7); break;
+        default: SKR_HM_NS(8); break;
     }
+#undef SKR_HM_NS
+#undef SKR_HM
     return SKR_CHECK_LAUNCH();
 }

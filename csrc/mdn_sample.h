@@ -114,7 +114,8 @@ __device__ inline MdnDraw mdn_sample_wave(const float* zr, int M, int mode, floa
 // 256-thread workgroup: wave w folds the slabs s = w mod 4 of every column
 // with independent (unrolled, clamped) loads, the four partial rows meet in
 // LDS (`part` [4][256]), and zrow [nout] is ready after the call (every thread
-// passed its barrier).
+// passed its barrier). LDS-only barriers: global loads the caller issued
+// before the call stay in flight.
 __device__ inline void fold_head_slabs(const float* __restrict__ zs, int64_t ldz, int nslab, int64_t slab,
                                        const float* __restrict__ bias, int nout, int b, float (*part)[256],
                                        float* zrow) {
@@ -135,9 +136,9 @@ __device__ inline void fold_head_slabs(const float* __restrict__ zs, int64_t ldz
         }
         part[w][c] = v;
     }
-    __syncthreads();
+    lds_barrier();
     if (tid < nout) zrow[tid] = bias[tid] + ((part[0][tid] + part[1][tid]) + (part[2][tid] + part[3][tid]));
-    __syncthreads();
+    lds_barrier();
 }
 
 }  // namespace skr

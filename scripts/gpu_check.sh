@@ -65,7 +65,9 @@ for s in "${steps[@]}"; do
         bench_sample_1k) run bench_sample_1k 600 python scripts/bench_sample.py --batch 1024 ;;
         bench_sample_1k_fp8) run bench_sample_1k_fp8 600 python scripts/bench_sample.py --batch 1024 --dtype fp8 ;;
         sample_ab) for bb in 128 1024; do for dt in bf16 fp8; do SKR_DECODE_FUSED=0 run sample_b${bb}_${dt}_f0 300 python scripts/bench_sample.py --batch $bb --dtype $dt --host-steps 2 && SKR_DECODE_FUSED=1 run sample_b${bb}_${dt}_f1 300 python scripts/bench_sample.py --batch $bb --dtype $dt --host-steps 2; done; done ;;
+        sample_f1) for bb in 128 1024; do for dt in bf16 fp8; do run sample_b${bb}_${dt}_f1 300 python scripts/bench_sample.py --batch $bb --dtype $dt --host-steps 2; done; done ;;
         prof_sample_fused) run prof_sample_fused 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_sample_fused -o run --output-format csv -- python scripts/bench_sample.py --batch 128 --reps 1 --host-steps 2 ;;
+        prof_sample_fused8) run prof_sample_fused8 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_sample_fused8 -o run --output-format csv -- python scripts/bench_sample.py --batch 128 --reps 1 --host-steps 2 --dtype fp8 ;;
         bench_ref) run bench_ref 600 python scripts/bench_reference.py ;;
         bench_ref_bf16) run bench_ref_bf16 600 python scripts/bench_reference.py --dtype bf16 ;;
         bench_ref_torch) run bench_ref_torch 600 python scripts/bench_reference.py --backend torch --steps 5 ;;
