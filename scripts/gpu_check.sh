@@ -66,6 +66,11 @@ for s in "${steps[@]}"; do
         bench_sample_1k_fp8) run bench_sample_1k_fp8 600 python scripts/bench_sample.py --batch 1024 --dtype fp8 ;;
         sample_ab) for bb in 128 1024; do for dt in bf16 fp8; do SKR_DECODE_FUSED=0 run sample_b${bb}_${dt}_f0 300 python scripts/bench_sample.py --batch $bb --dtype $dt --host-steps 2 && SKR_DECODE_FUSED=1 run sample_b${bb}_${dt}_f1 300 python scripts/bench_sample.py --batch $bb --dtype $dt --host-steps 2; done; done ;;
         sample_f1) for bb in 128 1024; do for dt in bf16 fp8; do run sample_b${bb}_${dt}_f1 300 python scripts/bench_sample.py --batch $bb --dtype $dt --host-steps 2; done; done ;;
+        ab_group_bn) for bn in 64 128 64 128; do SKR_GROUP_BN=$bn run sample_b128_bn${bn} 300 python scripts/bench_sample.py --batch 128 --host-steps 2 && SKR_GROUP_BN=$bn run sample_b1024_bn${bn} 300 python scripts/bench_sample.py --batch 1024 --host-steps 2; done; SKR_GROUP_BN=128 run bench_bn128 600 python bench.py --steps 10 --warmup 2 ;;
+        fp8_gate) run fp8_gate 900 python scripts/fp8_gate.py ;;
+        prof_small) run prof_small 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_small -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --no-eval --config vae_small ;;
+        prof_ln) run prof_ln 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_ln -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --no-eval --config vae_layernorm ;;
+        bench_b128) run bench_b128 600 python bench.py --steps 10 --warmup 2 --batch 128 ;;
         prof_sample_fused) run prof_sample_fused 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_sample_fused -o run --output-format csv -- python scripts/bench_sample.py --batch 128 --reps 1 --host-steps 2 ;;
         prof_sample_fused8) run prof_sample_fused8 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_sample_fused8 -o run --output-format csv -- python scripts/bench_sample.py --batch 128 --reps 1 --host-steps 2 --dtype fp8 ;;
         bench_ref) run bench_ref 600 python scripts/bench_reference.py ;;

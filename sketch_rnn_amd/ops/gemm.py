@@ -309,6 +309,10 @@ def rec_gemm_bf16out(a: torch.Tensor, bt: torch.Tensor, out: torch.Tensor) -> to
 GROUPED = os.environ.get("SKR_GEMM_GROUP", "1") != "0"   # SKR_GEMM_GROUP=0: independent per-step products as separate launches
 
 
+# N-tile width of the grouped launch (0: the kernel's default, 64); tuning knob
+GROUP_BN = int(os.environ.get("SKR_GROUP_BN", "0"))
+
+
 def rec_gemm_group(jobs) -> None:
     """Several independent :func:`rec_gemm` products ``(a, bt, out, splits)``
     (nd = 1, M <= 128, bf16, splits >= 1) in ONE grouped launch
@@ -329,7 +333,7 @@ def rec_gemm_group(jobs) -> None:
         p.A, p.lda, p.Bt, p.ldb = a.data_ptr(), a.stride(0), bt.data_ptr(), bt.stride(-2)
         p.C, p.ldc, p.c_slab = out.data_ptr(), N, out.stride(0)
         p.M, p.N, p.K, p.splits = a.shape[0], N, K, s
-    rc = lib.lib.skr_skinny_gemm_group(probs, len(jobs), 0, torch.cuda.current_stream().cuda_stream)
+    rc = lib.lib.skr_skinny_gemm_group(probs, len(jobs), GROUP_BN, torch.cuda.current_stream().cuda_stream)
     if rc != 0:
         raise RuntimeError("skr_skinny_gemm_group failed (%d)" % rc)
 

@@ -444,6 +444,14 @@ def lstm_sequence_hip(xp, W_h, h0, c0, forget_bias=1.0, reset=None, reset_h=None
         ln = (None, None, None, None)
     if reset is not None and reset_h is None:
         raise ValueError("reset requires reset_h / reset_c")
+    from . import persist
+    if (ln[0] is None and reset is None and xp.shape[0] > 1 and not _inference(xp, W_h, h0, c0)
+            and persist.persist_ok(W_h.shape[0], 1, 1, ln=False, B=xp.shape[1])):
+        # a plain layer in training (the vae_small decoder): the whole sequence,
+        # forward and backward, as one persistent launch each (csrc/lstm_persist.hip)
+        Hout, fin = persist.lstm_stack(xp, [W_h], [h0], [c0], drop_keep=drop_keep, drop_seed=drop_seed,
+                                       drop_stream=drop_stream, forget_bias=forget_bias)
+        return Hout, fin[0]
     Hout, hT, cT = _LSTMSeq.apply(xp, W_h, h0, c0, reset_h, reset_c, *ln, reset, drop_seed,
                                   (float(forget_bias), float(drop_keep), int(drop_stream), 1,
                                    _inference(xp, W_h, h0, c0)))

@@ -246,3 +246,44 @@ def test_fused_encoder_last_h_matches_unfused_and_oracle():
         assert _rel(a, b) < 2e-2, _rel(a, b)
     for n in g_t:
         assert _rel(g_f[n], g_t[n]) < 5e-2, (n, _rel(g_f[n], g_t[n]))
+
+
+@pytest.mark.parametrize("H,keep", [(512, 0.9), (256, 1.0)])
+def test_plain_training_layer_runs_persistent_and_matches_oracle(H, keep):
+    """A plain LSTM layer in training (the vae_small decoder: z-dependent
+    input projection, initial state with a gradient) takes the persistent
+    kernels (ops.lstm_sequence -> persist.lstm_stack) and matches the fp32
+    PyTorch oracle within bf16 tolerances -- outputs, dh0 / dc0, dW_h, dxp --
+    with the same hashed recurrent-dropout masks."""
+    from sketch_rnn_amd.ops import recurrent
+    B, T = 100, 48
+    g = torch.Generator(device=DEV).manual_seed(H)
+    xp = (torch.randn(T, B, 4 * H, device=DEV, generator=g) * 0.5)
+    W = torch.randn(H, 4 * H, device=DEV, generator=g) / H ** 0.5
+    h0 = torch.randn(B, H, device=DEV, generator=g) * 0.3
+    c0 = torch.randn(B, H, device=DEV, generator=g) * 0.3
+    w_out = torch.randn(T, B, H, device=DEV, generator=g)
+    res = {}
+    for name, backend, dt in (("ref", "torch", "fp32"), ("hip", "hip", "bf16")):
+        ops.set_backend(backend)
+        ops.set_compute_dtype(dt)
+        ins = [t.detach().clone().requires_grad_() for t in (xp, W, h0, c0)]
+        calls = {}
+        orig = persist.lstm_stack
+
+        def spy(*a, **k):
+            calls["n"] = calls.get("n", 0) + 1
+            return orig(*a, **k)
+        persist.lstm_stack = spy
+        try:
+            out, (hT, cT) = ops.lstm_sequence(ins[0], ins[1], ins[2], ins[3], drop_keep=keep, drop_seed=7,
+                                              drop_stream=3)
+        finally:
+            persist.lstm_stack = orig
+        ((out * w_out).sum() + hT.sum() + cT.sum()).backward()
+        res[name] = (out.detach(), [t.grad for t in ins], calls.get("n", 0))
+    assert res["hip"][2] == 1, "the persistent path was not taken"
+    assert _rel(res["hip"][0], res["ref"][0]) < 2e-2
+    for n, a, b in zip(("dxp", "dW_h", "dh0", "dc0"), res["hip"][1], res["ref"][1]):
+        assert _rel(a, b) < 4e-2, (n, _rel(a, b))
+    del recurrent
