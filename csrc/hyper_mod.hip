@@ -69,7 +69,7 @@ namespace {
 // NRT: 16-row tiles staged and multiplied (rows up to 16 NRT; a B = 100 launch
 // pays for 112 rows, not MAXB).
 template <int NS, int NRT>
-__global__ __launch_bounds__(NTH) void hyper_mod_fwd(const ModDecode dec, const __hip_bfloat16* __restrict__ hh, int64_t ld_hh,
+__global__ __launch_bounds__(NTH) void hyper_mod_fwd(ModDecode dec, const __hip_bfloat16* __restrict__ hh, int64_t ld_hh,
                                                      const __hip_bfloat16* __restrict__ PlT,   // [12H][HH]
                                                      const float* __restrict__ qb,             // [12H]
                                                      const float* __restrict__ xh,             // [B][4H]
@@ -80,6 +80,23 @@ __global__ __launch_bounds__(NTH) void hyper_mod_fwd(const ModDecode dec, const 
                                                      float* __restrict__ stats,                 // [B][4][H/TU][2]
                                                      int B, int H) {
     constexpr int MB = 16 * NRT;
+    {   // row block blockIdx.z (B > MAXB: the wide decode): rows r0 .. r0 + MAXB - 1
+        const int r0 = blockIdx.z * MAXB;
+        B = min(MAXB, B - r0);
+        const int64_t G4 = (int64_t)r0 * 4 * H;
+        if (hh) hh += (int64_t)r0 * ld_hh;
+        if (dec.hh32) dec.hh32 += (int64_t)r0 * HH;
+        if (dec.x5) {
+            dec.x5 += (int64_t)r0 * 5;
+            dec.zp += (int64_t)r0 * dec.ldzp;
+        }
+        if (xh) xh += G4;
+        R += G4;
+        gout += G4;
+        if (rlp) rlp += G4;
+        if (vec) vec += (int64_t)r0 * 12 * H;
+        stats += (int64_t)r0 * 4 * (H / TU) * 2;
+    }
     __shared__ __attribute__((aligned(16))) __hip_bfloat16 sA[MB * HH];     // <= 64 KB
     __shared__ __attribute__((aligned(16))) float sV[6][MB][16];            // <= 48 KB
     const int q = blockIdx.y, u0 = blockIdx.x * TU, ntile = H / TU;
@@ -210,7 +227,7 @@ __global__ __launch_bounds__(NTH) void hyper_mod_fwd(const ModDecode dec, const 
 // nslab fp32 slabs [B][4H] (stride r_slab), outputs vec [B][12H] bf16 (blocks
 // 0..7 written; null at inference), g [B][4H] fp32, rlp [B][4H] bf16 (or
 // null), stats [B][4][H/32][2] fp32. dec: decode-step inputs (ModDecode) or
-// null.
+// null. B > 128 (a multiple of 128): 128-row blocks over gridDim.z.
 SKR_API int skr_hyper_mod_fwd(const void* hh, int64_t ld_hh, const void* PlT, const float* qb, const float* xh,
                               const float* R, int64_t r_slab, int nslab, void* vec, float* g, void* rlp,
                               float* stats, int B, int H, int Hh, const ModDecode* dec, hipStream_t s) {
@@ -219,11 +236,11 @@ SKR_API int skr_hyper_mod_fwd(const void* hh, int64_t ld_hh, const void* PlT, co
     if (dz.hh32 && ((uintptr_t)dz.hh32 & 15)) return -4;
     if ((dz.x5 == nullptr && xh == nullptr) || (dz.hh32 == nullptr && hh == nullptr)) return -3;
     if (B <= 0) return 0;
-    if (B > MAXB || Hh != HH || H % TU != 0) return -2;
+    if ((B > MAXB && B % MAXB != 0) || Hh != HH || H % TU != 0) return -2;
     if (((uintptr_t)hh | (uintptr_t)PlT | (uintptr_t)xh | (uintptr_t)R | (uintptr_t)vec | (uintptr_t)g |
          (uintptr_t)rlp) & 15 || (ld_hh % 8) || (r_slab % 4))
         return -4;
-    const dim3 grid(H / TU, 4);
+    const dim3 grid(H / TU, 4, (B + MAXB - 1) / MAXB);
     const auto* a = (const __hip_bfloat16*)hh;
     const auto* p = (const __hip_bfloat16*)PlT;
     auto* v = (__hip_bfloat16*)vec;

@@ -78,7 +78,9 @@ __global__ __launch_bounds__(256) void skinny_gemm_glds_kernel(
 // h @ W_h for the main gates and [h | hh] @ W_y for the hyper gates; in the
 // backward dR_main @ W_h^T and dvec @ P^T) then share one kernel boundary
 // and fill the chip together instead of each leaving most CUs idle.
-// Workgroup id -> (problem, split, N tile) through the prefix sums `start`.
+// Workgroup id -> (problem, row block, split, N tile) through the prefix
+// sums `start`. A problem with M > 128 rows (M % 128 == 0: the wide decode
+// of sample/hyper_step.py) runs as M / 128 row blocks sharing B.
 }  // namespace
 
 struct GemmProblem {
@@ -97,18 +99,37 @@ struct GemmGroup {
     int n;
 };
 
+// (row block, split, N tile) of workgroup `local` of a problem: row blocks of
+// 128 rows outermost, then splits, then N tiles
+struct TileIdx { int rb, rows, split, nt; };
+__device__ __forceinline__ TileIdx tile_idx(int local, int M, int N, int splits, int bn) {
+    const int ntiles = N / bn, per_rb = ntiles * splits;
+    TileIdx t;
+    t.rb = local / per_rb;
+    const int rem = local - t.rb * per_rb;
+    t.split = rem / ntiles;
+    t.nt = rem - t.split * ntiles;
+    t.rows = min(BM, M - t.rb * BM);
+    return t;
+}
+
+__host__ __device__ constexpr int row_blocks_of(int M) { return M <= BM ? 1 : (M + BM - 1) / BM; }
+
+template <typename P>
+__device__ __forceinline__ int64_t split_off(const P& p, const TileIdx& t) {
+    return (int64_t)t.split * p.c_slab + (int64_t)t.rb * BM * p.ldc;
+}
+
 template <int BN, int NS>
 __device__ __forceinline__ void group_tile(const GemmGroup& g, const int id, __hip_bfloat16* smem) {
     int q = 0;
 #pragma unroll
     for (int i = 1; i < kMaxGroup; ++i) q += (i < g.n && id >= g.start[i]) ? 1 : 0;
     const GemmProblem& p = g.p[q];
-    const int local = id - g.start[q];
-    const int ntiles = p.N / BN;
-    const int split = local / ntiles, nt = local - split * ntiles;
+    const TileIdx t = tile_idx(id - g.start[q], p.M, p.N, p.splits, BN);
     const int kslice = p.K / p.splits;
-    glds_tile<BN, NS>((const __hip_bfloat16*)p.A, p.lda, (const __hip_bfloat16*)p.Bt, p.ldb, p.C + split * p.c_slab,
-                      p.ldc, p.M, nt * BN, (int64_t)split * kslice, kslice, smem);
+    glds_tile<BN, NS>((const __hip_bfloat16*)p.A + (int64_t)t.rb * BM * p.lda, p.lda, (const __hip_bfloat16*)p.Bt,
+                      p.ldb, p.C + split_off(p, t), p.ldc, t.rows, t.nt * BN, (int64_t)t.split * kslice, kslice, smem);
 }
 
 template <int BN, int NS>
@@ -551,11 +572,11 @@ SKR_API int skr_skinny_gemm_group(const GemmProblem* probs, int n, int bn, hipSt
     g.start[0] = 0;
     for (int i = 0; i < n; ++i) {
         const GemmProblem& p = probs[i];
-        if (p.M < 1 || p.M > BM || p.N % bn != 0 || p.splits < 1 || p.K % p.splits != 0) return -2;
+        if (p.M < 1 || (p.M > BM && p.M % BM != 0) || p.N % bn != 0 || p.splits < 1 || p.K % p.splits != 0) return -2;
         if ((p.K / p.splits) % BK != 0 || p.lda % 8 != 0 || p.ldb % 8 != 0) return -3;
         if (((uintptr_t)p.A | (uintptr_t)p.Bt) & 15) return -4;
         g.p[i] = p;
-        g.start[i + 1] = g.start[i] + (p.N / bn) * p.splits;
+        g.start[i + 1] = g.start[i] + (p.N / bn) * p.splits * row_blocks_of(p.M);
     }
     for (int i = n + 1; i <= kMaxGroup; ++i) g.start[i] = g.start[n];
     if (bn == 128) return g_nstage == 3 ? launch_group<128, 3>(g, s) : launch_group<128, 4>(g, s);
@@ -648,12 +669,11 @@ __global__ __launch_bounds__(256) void skinny_gemm_group_fp8_kernel(const GemmGr
 #pragma unroll
     for (int i = 1; i < kMaxGroup; ++i) q += (i < g.n && id >= g.start[i]) ? 1 : 0;
     const GemmProblem8& p = g.p[q];
-    const int local = id - g.start[q];
-    const int ntiles = p.N / BN;
-    const int split = local / ntiles, nt = local - split * ntiles;
+    const TileIdx t = tile_idx(id - g.start[q], p.M, p.N, p.splits, BN);
     const int kslice = p.K / p.splits;
-    glds_tile_fp8<BN, NS, false>((const uint8_t*)p.A, p.lda, (const uint8_t*)p.Bt, p.ldb, p.b_scale, p.a_scale,
-                                 p.C + split * p.c_slab, p.ldc, p.M, nt * BN, (int64_t)split * kslice, kslice, smem8);
+    glds_tile_fp8<BN, NS, false>((const uint8_t*)p.A + (int64_t)t.rb * BM * p.lda, p.lda, (const uint8_t*)p.Bt,
+                                 p.ldb, p.b_scale, p.a_scale, p.C + split_off(p, t), p.ldc, t.rows, t.nt * BN,
+                                 (int64_t)t.split * kslice, kslice, smem8);
 }
 
 constexpr int kNs8 = 3;
@@ -704,10 +724,13 @@ SKR_API int skr_skinny_gemm_group_fp8(const GemmProblem8* probs, int n, hipStrea
     g.n = n;
     g.start[0] = 0;
     for (int i = 0; i < n; ++i) {
-        const int rc = check8(probs[i]);
+        GemmProblem8 p1 = probs[i];
+        if (p1.M > BM && p1.M % BM != 0) return -2;
+        p1.M = min(p1.M, BM);                      // (row blocks: validated as one block)
+        const int rc = check8(p1);
         if (rc) return rc;
         g.p[i] = probs[i];
-        g.start[i + 1] = g.start[i] + (probs[i].N / 64) * probs[i].splits;
+        g.start[i + 1] = g.start[i] + (probs[i].N / 64) * probs[i].splits * row_blocks_of(probs[i].M);
     }
     for (int i = n + 1; i <= kMaxGroup; ++i) g.start[i] = g.start[n];
     const size_t lds = (size_t)kNs8 * (BM + 64) * BK8;

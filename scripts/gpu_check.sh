@@ -70,6 +70,9 @@ for s in "${steps[@]}"; do
         fp8_gate) run fp8_gate 900 python scripts/fp8_gate.py ;;
         prof_small) run prof_small 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_small -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --no-eval --config vae_small ;;
         prof_ln) run prof_ln 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_ln -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --no-eval --config vae_layernorm ;;
+        bench_wide_gemm) run bench_wide_gemm 300 python scripts/bench_wide_gemm.py ;;
+        pmc_fetch) run pmc_fetch 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d gpurun_out/pmc_fetch -o run --output-format csv -- python bench.py --steps 1 --warmup 1 --no-eval ;;
+        pmc_write) run pmc_write 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d gpurun_out/pmc_write -o run --output-format csv -- python bench.py --steps 1 --warmup 1 --no-eval ;;
         bench_b128) run bench_b128 600 python bench.py --steps 10 --warmup 2 --batch 128 ;;
         prof_sample_fused) run prof_sample_fused 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_sample_fused -o run --output-format csv -- python scripts/bench_sample.py --batch 128 --reps 1 --host-steps 2 ;;
         prof_sample_fused8) run prof_sample_fused8 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_sample_fused8 -o run --output-format csv -- python scripts/bench_sample.py --batch 128 --reps 1 --host-steps 2 --dtype fp8 ;;

@@ -315,11 +315,12 @@ GROUP_BN = int(os.environ.get("SKR_GROUP_BN", "0"))
 
 def rec_gemm_group(jobs) -> None:
     """Several independent :func:`rec_gemm` products ``(a, bt, out, splits)``
-    (nd = 1, M <= 128, bf16, splits >= 1) in ONE grouped launch
+    (nd = 1, bf16, splits >= 1; M <= 128, or 128-row blocks up to 1024) in
+    ONE grouped launch
     (csrc/skinny_gemm.hip ``skr_skinny_gemm_group``); falls back to one
     launch per product when a job does not qualify."""
     ok = GROUPED and 1 <= len(jobs) <= 4 and all(
-        a.is_cuda and a.dtype == _BF16 and s >= 1 and a.shape[0] <= 128 for a, _, _, s in jobs)
+        a.is_cuda and a.dtype == _BF16 and s >= 1 and row_blocks(a.shape[0]) > 0 for a, _, _, s in jobs)
     if not ok:
         for a, bt, out, s in jobs:
             rec_gemm(a, bt, out, s)

@@ -67,7 +67,21 @@ def hyper_step_ok(model, B: int) -> bool:
     if get_compute_dtype() not in ("bf16", "fp8") or not model.dec.use_layer_norm:
         return False
     H, Hh = cfg.dec_rnn_size, cfg.hyper_num_units
-    return B <= 128 and H % 64 == 0 and Hh % 64 == 0 and cfg.num_mixture <= 32
+    if B > 128 and not (wide_ok(model) and B % 128 == 0 and B <= 1024):
+        return False
+    return H % 64 == 0 and Hh % 64 == 0 and cfg.num_mixture <= 32
+
+
+def wide_ok(model) -> bool:
+    """One decoder over up to 1024 rows (128-row blocks inside each launch)
+    instead of 128-row chunks on concurrent streams: the four-launch stroke's
+    shape limits (:class:`HyperStepDecoder` ``fused``)."""
+    cfg = model.cfg
+    return (WIDE and cfg.hyper_num_units == 256 and cfg.hyper_embedding_size <= 32 and cfg.dec_rnn_size % 32 == 0
+            and os.environ.get("SKR_DECODE_FUSED", "1") != "0")
+
+
+WIDE = os.environ.get("SKR_WIDE_DECODE", "1") != "0"
 
 
 class HyperStepDecoder:
@@ -121,7 +135,7 @@ class HyperStepDecoder:
         self.ZP = torch.zeros(B, G + Gh, dtype=f32, device=device)   # per-sketch z projections
         self.ZS = torch.empty(self.S_o, B, 128, dtype=f32, device=device)
         self.clm = _ClusterSync(1, B, H, device)
-        if not cluster:
+        if not cluster or B > 128:   # (wide: 1024-thread rows, no co-residency requirement)
             self.clm.C, self.clm.on = 1, False
         self.clh = _ClusterSync(1, B, Hh, device)
         self.sd = _seed_tensor(0, device)
@@ -323,4 +337,8 @@ class HyperStepDecoder:
     @torch.no_grad()
     def head(self) -> None:
         """Head GEMM of the current ``h`` into the split-K slabs ``ZS``."""
-        (gemm.rec_gemm_fp8_v2 if self.fp8 else gemm.rec_gemm)(self.A[:, :self.H], self._w["WoT"], self.ZS, self.S_o)
+        if self.fp8:
+            (gemm.rec_gemm_fp8_v2 if self.B <= 128 else gemm.rec_gemm_fp8)(self.A[:, :self.H], self._w["WoT"], self.ZS,
+                                                                            self.S_o)
+        else:
+            gemm.rec_gemm(self.A[:, :self.H], self._w["WoT"], self.ZS, self.S_o)

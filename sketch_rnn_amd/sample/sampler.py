@@ -269,8 +269,11 @@ class GraphDecoder:
         for residency."""
         if self.kind != "vae" or self.dev.type != "cuda" or os.environ.get("SKR_STEP_DECODER", "1") == "0":
             return None
-        from .hyper_step import HyperStepDecoder, hyper_step_ok
-        chunks = [(r0, min(128, self.B - r0)) for r0 in range(0, self.B, 128)]
+        from .hyper_step import HyperStepDecoder, hyper_step_ok, wide_ok
+        if self.B > 128 and self.B % 128 == 0 and self.B <= 1024 and wide_ok(self.model):
+            chunks = [(0, self.B)]   # one wide decoder: 128-row blocks inside each launch
+        else:
+            chunks = [(r0, min(128, self.B - r0)) for r0 in range(0, self.B, 128)]
         if len(chunks) > self._MAX_CHUNKS or not all(hyper_step_ok(self.model, n) for _, n in chunks):
             return None
         if getattr(self, "_stp", None) is None:

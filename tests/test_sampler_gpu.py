@@ -206,7 +206,7 @@ def _hyper256(seed=1, H=512, E=16):
     return cfg, SketchVAE(cfg, seed=seed).to(DEV).eval()
 
 
-@pytest.mark.parametrize("dtype,B", [("bf16", 100), ("bf16", 128), ("fp8", 96)])
+@pytest.mark.parametrize("dtype,B", [("bf16", 100), ("bf16", 128), ("fp8", 96), ("bf16", 256), ("fp8", 384)])
 def test_hyper_step_fused_matches_decode_step(dtype, B):
     """The four-launch stroke (decode_step.hip hyper cell + hyper_mod decode
     mode + MOD-3 main cell), teacher-forced, against the generic T = 1 path:
@@ -304,6 +304,45 @@ def test_graph_decoder_hyper_fused_chunks():
         assert not torch.equal(sa, sc)
         for r in range(300):
             assert torch.all(sa[r, la[r]:, 4] == 1)
+    finally:
+        ops.set_backend("auto")
+        ops.set_compute_dtype("fp32")
+
+
+def test_graph_decoder_hyper_wide():
+    """B = 256 (a multiple of 128): ONE decoder whose launches run 128-row
+    blocks (grouped GEMM row blocks, hyper_mod over gridDim.z, 1024-thread
+    main-cell rows) instead of concurrent 128-row chunks; graph replay ==
+    eager, deterministic, eos padding intact, and the same first strokes as
+    the chunked decode (identical head inputs before any split-K order
+    difference can flip a draw)."""
+    native.require_hip()
+    ops.set_backend("hip")
+    ops.set_compute_dtype("bf16")
+    try:
+        cfg, m = _hyper256(seed=6)
+        a = SM.GraphDecoder(m, batch=256, steps=24, temperature=0.5, use_graph=True)
+        b = SM.GraphDecoder(m, batch=256, steps=24, temperature=0.5, use_graph=False)
+        stp = a._steppers()
+        assert stp is not None and len(stp) == 1 and stp[0][1] == 256 and stp[0][2].fused
+        sa, la = a.run(seed=4)
+        sa2, _ = a.run(seed=4)
+        sb, lb = b.run(seed=4)
+        torch.cuda.synchronize()
+        assert torch.equal(sa, sa2) and torch.equal(la, lb)
+        assert torch.allclose(sa, sb, atol=1e-4)
+        for r in range(256):
+            assert torch.all(sa[r, la[r]:, 4] == 1)
+        from sketch_rnn_amd.sample import hyper_step
+        hyper_step.WIDE = False
+        try:
+            c = SM.GraphDecoder(m, batch=256, steps=24, temperature=0.5, use_graph=False)
+            assert len(c._steppers()) == 2
+            sc, _ = c.run(seed=4)
+        finally:
+            hyper_step.WIDE = True
+        torch.cuda.synchronize()
+        assert torch.allclose(sa[:, 0], sc[:, 0], atol=1e-4)
     finally:
         ops.set_backend("auto")
         ops.set_compute_dtype("fp32")
