@@ -163,6 +163,18 @@ class PFwdLayer(C.Structure):
     ]
 
 
+class PLn(C.Structure):
+    """Mirror of ``PLn`` in csrc/lstm_persist.hip (LayerNorm-LSTM parameters, saves, exchange scratch)."""
+    _fields_ = [
+        ("g", _p), ("b", _p), ("gc", _p), ("bc", _p),
+        ("xhat", _p), ("rstd", _p), ("chat", _p),
+        ("lp", _i),
+        ("xs", _p),
+        ("dlny", _p), ("dlncy", _p),
+        ("fb", _f),
+    ]
+
+
 class PFwdArgs(C.Structure):
     _fields_ = [
         ("T", _i), ("B", _i), ("nd", _i), ("L", _i), ("H", _i), ("nrb", _i),
@@ -173,6 +185,7 @@ class PFwdArgs(C.Structure):
         ("flags", _p),
         ("err", _p),
         ("tlen", _p),
+        ("ln", PLn),
     ]
 
 
@@ -201,6 +214,7 @@ class PBwdArgs(C.Structure):
         ("flags", _p),
         ("err", _p),
         ("tlen", _p),
+        ("ln", PLn),
     ]
 
 

@@ -445,12 +445,15 @@ def lstm_sequence_hip(xp, W_h, h0, c0, forget_bias=1.0, reset=None, reset_h=None
     if reset is not None and reset_h is None:
         raise ValueError("reset requires reset_h / reset_c")
     from . import persist
-    if (ln[0] is None and reset is None and xp.shape[0] > 1 and not _inference(xp, W_h, h0, c0)
-            and persist.persist_ok(W_h.shape[0], 1, 1, ln=False, B=xp.shape[1])):
-        # a plain layer in training (the vae_small decoder): the whole sequence,
-        # forward and backward, as one persistent launch each (csrc/lstm_persist.hip)
+    lnp = ln[0] is not None
+    if (reset is None and xp.shape[0] > 1 and not _inference(xp, W_h, h0, c0, *(ln if lnp else ()))
+            and persist.persist_ok(W_h.shape[0], 1, 1, ln=lnp, B=xp.shape[1])):
+        # a layer in training (the vae_small / vae_layernorm decoders): the whole
+        # sequence, forward and backward, as one persistent launch each
+        # (csrc/lstm_persist.hip; LayerNorm statistics exchanged in-launch)
         Hout, fin = persist.lstm_stack(xp, [W_h], [h0], [c0], drop_keep=drop_keep, drop_seed=drop_seed,
-                                       drop_stream=drop_stream, forget_bias=forget_bias)
+                                       drop_stream=drop_stream, forget_bias=forget_bias,
+                                       ln=ln if lnp else None)
         return Hout, fin[0]
     Hout, hT, cT = _LSTMSeq.apply(xp, W_h, h0, c0, reset_h, reset_c, *ln, reset, drop_seed,
                                   (float(forget_bias), float(drop_keep), int(drop_stream), 1,
@@ -481,9 +484,10 @@ def bilstm_sequence_packed_hip(xp, W_f, W_b, h0, c0, drop_keep=1.0, drop_seed=0,
     from . import persist
     if persist.persist_ok(W_f.shape[0], 2, 1, ln=ln_f is not None, B=B):
         # both directions, every step, one persistent launch (csrc/lstm_persist.hip)
+        lnp = tuple(torch.stack([a, b], 0) for a, b in zip(ln_f, ln_b)) if ln_f is not None else None
         Hout, _ = persist.lstm_stack(xp, [W], [h], [c], nd=2, drop_keep=drop_keep, drop_seed=drop_seed,
                                      drop_stream=streams[0], forget_bias=forget_bias,
-                                     lengths=lengths if PERSIST_LENGTHS else None)
+                                     lengths=lengths if PERSIST_LENGTHS else None, ln=lnp)
         return Hout[:, :B], Hout[:, B:]
     if ln_f is not None:
         ln = tuple(torch.stack([a, b], 0) for a, b in zip(ln_f, ln_b))

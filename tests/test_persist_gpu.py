@@ -248,13 +248,15 @@ def test_fused_encoder_last_h_matches_unfused_and_oracle():
         assert _rel(g_f[n], g_t[n]) < 5e-2, (n, _rel(g_f[n], g_t[n]))
 
 
-@pytest.mark.parametrize("H,keep", [(512, 0.9), (256, 1.0)])
-def test_plain_training_layer_runs_persistent_and_matches_oracle(H, keep):
-    """A plain LSTM layer in training (the vae_small decoder: z-dependent
-    input projection, initial state with a gradient) takes the persistent
-    kernels (ops.lstm_sequence -> persist.lstm_stack) and matches the fp32
-    PyTorch oracle within bf16 tolerances -- outputs, dh0 / dc0, dW_h, dxp --
-    with the same hashed recurrent-dropout masks."""
+@pytest.mark.parametrize("H,keep,ln", [(512, 0.9, False), (256, 1.0, False), (512, 0.9, True), (256, 1.0, True)])
+def test_plain_training_layer_runs_persistent_and_matches_oracle(H, keep, ln):
+    """An LSTM / LayerNorm-LSTM layer in training (the vae_small /
+    vae_layernorm decoders: z-dependent input projection, initial state with
+    a gradient) takes the persistent kernels (ops.lstm_sequence ->
+    persist.lstm_stack; LayerNorm statistics exchanged in-launch) and matches
+    the fp32 PyTorch oracle within bf16 tolerances -- outputs, dh0 / dc0,
+    dW_h, dxp, the LayerNorm gamma / beta gradients -- with the same hashed
+    recurrent-dropout masks."""
     from sketch_rnn_amd.ops import recurrent
     B, T = 100, 48
     g = torch.Generator(device=DEV).manual_seed(H)
@@ -263,11 +265,13 @@ def test_plain_training_layer_runs_persistent_and_matches_oracle(H, keep):
     h0 = torch.randn(B, H, device=DEV, generator=g) * 0.3
     c0 = torch.randn(B, H, device=DEV, generator=g) * 0.3
     w_out = torch.randn(T, B, H, device=DEV, generator=g)
+    lnp = [1.0 + 0.1 * torch.randn(4 * H, device=DEV, generator=g), 0.1 * torch.randn(4 * H, device=DEV, generator=g),
+           1.0 + 0.1 * torch.randn(H, device=DEV, generator=g), 0.1 * torch.randn(H, device=DEV, generator=g)]
     res = {}
     for name, backend, dt in (("ref", "torch", "fp32"), ("hip", "hip", "bf16")):
         ops.set_backend(backend)
         ops.set_compute_dtype(dt)
-        ins = [t.detach().clone().requires_grad_() for t in (xp, W, h0, c0)]
+        ins = [t.detach().clone().requires_grad_() for t in [xp, W, h0, c0] + (lnp if ln else [])]
         calls = {}
         orig = persist.lstm_stack
 
@@ -277,13 +281,48 @@ def test_plain_training_layer_runs_persistent_and_matches_oracle(H, keep):
         persist.lstm_stack = spy
         try:
             out, (hT, cT) = ops.lstm_sequence(ins[0], ins[1], ins[2], ins[3], drop_keep=keep, drop_seed=7,
-                                              drop_stream=3)
+                                              drop_stream=3, ln=tuple(ins[4:]) if ln else None)
         finally:
             persist.lstm_stack = orig
         ((out * w_out).sum() + hT.sum() + cT.sum()).backward()
         res[name] = (out.detach(), [t.grad for t in ins], calls.get("n", 0))
     assert res["hip"][2] == 1, "the persistent path was not taken"
     assert _rel(res["hip"][0], res["ref"][0]) < 2e-2
-    for n, a, b in zip(("dxp", "dW_h", "dh0", "dc0"), res["hip"][1], res["ref"][1]):
+    for n, a, b in zip(("dxp", "dW_h", "dh0", "dc0", "dln_g", "dln_b", "dlnc_g", "dlnc_b"), res["hip"][1],
+                       res["ref"][1]):
         assert _rel(a, b) < 4e-2, (n, _rel(a, b))
     del recurrent
+
+
+def test_persistent_layernorm_bilstm_matches_per_step():
+    """LayerNorm encoder (both directions in one persistent launch, per-row
+    lengths bounding each row block) against the per-step LayerNorm cells,
+    both bf16: outputs and every gradient agree to bf16 rounding."""
+    from sketch_rnn_amd.ops import recurrent
+    B, T, H = 100, 40, 256
+    g = torch.Generator(device=DEV).manual_seed(5)
+    xp = torch.randn(T, 2 * B, 4 * H, device=DEV, generator=g) * 0.5
+    Wf, Wb = (torch.randn(H, 4 * H, device=DEV, generator=g) / H ** 0.5 for _ in range(2))
+    h0 = torch.zeros(B, H, device=DEV)
+    lnf = [1.0 + 0.1 * torch.randn(n, device=DEV, generator=g) for n in (4 * H, 4 * H, H, H)]
+    lnb = [1.0 + 0.1 * torch.randn(n, device=DEV, generator=g) for n in (4 * H, 4 * H, H, H)]
+    lengths = torch.randint(5, T + 1, (B,), device=DEV, generator=g)
+    wo = torch.randn(T, 2 * B, H, device=DEV, generator=g)
+    res = []
+    ops.set_backend("hip")
+    ops.set_compute_dtype("bf16")
+    for on in (True, False):
+        persist.PERSIST_LN = on
+        ins = [t.detach().clone().requires_grad_() for t in [xp, Wf, Wb] + lnf + lnb]
+        of, ob = recurrent.bilstm_sequence_packed_hip(ins[0], ins[1], ins[2], h0, h0, drop_keep=1.0,
+                                                      ln_f=tuple(ins[3:7]), ln_b=tuple(ins[7:11]),
+                                                      lengths=lengths if on else None)
+        # rows past their length are padding (the persistent path zeroes them): compare valid steps only
+        valid = (torch.arange(T, device=DEV).view(T, 1) < lengths.view(1, B)).float().unsqueeze(-1)
+        out = torch.cat([of * valid, ob * valid], 1)
+        (out * wo).sum().backward()
+        res.append((out.detach(), [t.grad for t in ins]))
+    persist.PERSIST_LN = True
+    assert _rel(res[0][0], res[1][0]) < 2e-2
+    for i, (a, b) in enumerate(zip(res[0][1], res[1][1])):
+        assert _rel(a, b) < 4e-2, (i, _rel(a, b))

@@ -40,6 +40,9 @@ _CFGS = {
                       dec_model="lstm", save_every=0),
     "layer_norm": VAEConfig(enc_rnn_size=128, dec_rnn_size=2048, z_size=32, num_mixture=5, max_seq_len=40,
                             batch_size=8, dec_model="layer_norm", save_every=0),
+    # persistent LayerNorm decoder + encoder (H = 512 / 256)
+    "layer_norm_512": VAEConfig(enc_rnn_size=256, dec_rnn_size=512, z_size=32, num_mixture=5, max_seq_len=40,
+                                batch_size=16, dec_model="layer_norm", enc_model="layer_norm", save_every=0),
 }
 
 
@@ -52,7 +55,7 @@ def test_training_is_bitwise_deterministic(name):
     assert torch.equal(w1, w2), (w1 - w2).abs().max()
 
 
-@pytest.mark.parametrize("name", ["hyper", "lstm"])
+@pytest.mark.parametrize("name", ["hyper", "lstm", "layer_norm_512"])
 def test_graph_step_equals_eager_step(name):
     cg, wg = _run(_CFGS[name], graph=True, steps=3)
     ce, we = _run(_CFGS[name], graph=False, steps=3)
