@@ -88,7 +88,7 @@ def _ln_setup(args, ln, T, NB, nd, nrb, H, dev, lp):
     and (forward) the saves, into ``args.ln``. Returns the tensors to keep."""
     f32 = torch.float32
     g, b, gc, bc = (t.detach().reshape(nd, -1).to(f32).contiguous() for t in ln)
-    xs = torch.empty(nd * nrb * 2 * (H // 16) * 32 * 8, device=dev, dtype=f32)
+    xs = torch.empty(nd * nrb * 2 * (H // 16) * 32 * 8, device=dev, dtype=torch.int64)   # tagged words
     args.ln.g, args.ln.b, args.ln.gc, args.ln.bc = g.data_ptr(), b.data_ptr(), gc.data_ptr(), bc.data_ptr()
     args.ln.xs, args.ln.lp = xs.data_ptr(), int(lp)
     return [g, b, gc, bc, xs]
@@ -127,8 +127,7 @@ def _fwd_launch(xp0, W_in1, b1, W_h0, W_h1, h0a, c0a, h0b, c0b, reset, seed, met
     a = PFwdArgs()
     a.T, a.B, a.nd, a.L, a.H, a.nrb = T, B, nd, L, H, nrb
     a.reset, a.forget_bias, a.seed = _ptr(rst), float(fb), sd.data_ptr()
-    # zeroed by the launcher: the h hand-off epochs (+ two LayerNorm phases)
-    flags = torch.empty(L * nd * nrb * 64 * (3 if ln is not None else 1), dtype=torch.int32, device=dev)
+    flags = torch.empty(L * nd * nrb * 64, dtype=torch.int32, device=dev)   # zeroed by the launcher
     a.flags, a.err = flags.data_ptr(), cluster_error_flag(dev).data_ptr()
     s_ln = None
     if ln is not None:
@@ -206,7 +205,7 @@ def _bwd_launch(s, dims, dtop, dfinal, fp32_dg=True):
     b = PBwdArgs()
     b.T, b.B, b.nd, b.L, b.H, b.nrb = T, B, nd, L, H, nrb
     b.reset, b.seed = _ptr(s.rst), s.seed.data_ptr()
-    flags = torch.empty(L * nd * nrb * 64 * (3 if s.ln is not None else 1), dtype=torch.int32, device=dev)
+    flags = torch.empty(L * nd * nrb * 64, dtype=torch.int32, device=dev)   # zeroed by the launcher
     b.flags, b.err = flags.data_ptr(), cluster_error_flag(dev).data_ptr()
     b.tlen = _ptr(s.tlen)
     ln_keep = dlny = dlncy = None

@@ -82,6 +82,7 @@ def wide_ok(model) -> bool:
 
 
 WIDE = os.environ.get("SKR_WIDE_DECODE", "1") != "0"
+LIB_MAIN = os.environ.get("SKR_WIDE_LIB_MAIN", "1") != "0"
 
 
 class HyperStepDecoder:
@@ -117,6 +118,13 @@ class HyperStepDecoder:
         # E <= 32, 32-unit tiles, <= 4 main-GEMM slabs)
         self.fused = Hh == 256 and self.E <= 32 and H % 32 == 0 and \
             os.environ.get("SKR_DECODE_FUSED", "1") != "0"
+        # wide decoder (B > 128): h @ W_h, [B, H] x [H, 4H], is a plain library-
+        # sized GEMM -- hipBLASLt (bf16, or e4m3 with per-tensor scales) beats
+        # the skinny kernel's row blocks there (scripts/bench_wide_gemm.py:
+        # 39.7 / 21.0 vs 49.7 us at B = 1024)
+        self.lib_main = self.fused and B > 128 and LIB_MAIN
+        if self.lib_main:
+            self.S_m = 1
         if self.fused:
             self.S_m = 4 if self.S_m >= 4 else 2 if self.S_m >= 2 else 1
             self.X = torch.zeros(B, 5, dtype=f32, device=device)
@@ -178,6 +186,16 @@ class HyperStepDecoder:
                 return qb.reshape(12 * H).float().contiguous()
             w["PL"] = P
             w["QB"] = gemm.derived((q, p.bias), "hypQB", qbias)
+        if self.lib_main:   # W_h for the library GEMM: [H, 4H] bf16, or e4m3 [4H, H] (column-major B) + scale
+            if self.fp8:
+                def q8t(W):
+                    sc = (W.detach().abs().amax().float() / gemm.FP8_MAX).clamp_min(1e-12)
+                    return (W.detach().t().float() / sc).to(torch.float8_e4m3fn).contiguous(), sc.reshape(())
+                w["WhL"] = gemm.derived(p.W_h, "hypWh8t", q8t)
+                w["sa8"] = gemm.derived(p.W_h, "fp8act", lambda W: torch.full((), 1.0 / gemm.FP8_ACT_SCALE,
+                                                                              device=W.device))
+            else:
+                w["WhL"] = gemm.derived(p.W_h, "hypWhL", lambda W: W.detach().to(torch.bfloat16).contiguous())
         if self.fp8:   # per-output-column e4m3 weights
             w["WhT"] = gemm.derived(w["WhT"], "q8", gemm.quantize_fp8_rows)
             w["WyT"] = gemm.derived(w["WyT"], "q8", gemm.quantize_fp8_rows)
@@ -309,10 +327,19 @@ class HyperStepDecoder:
         B, H, Hh, G, Gh, K = self.B, self.H, self.Hh, self.G, self.Gh, self.K
         st = torch.cuda.current_stream().cuda_stream
         f8 = self.fp8
-        jobs = [(self.A[:, :H], w["WhT"], self.RM, self.S_m), (self.A, w["WyT"], self.RY, self.S_y)]
+        jobs = [(self.A, w["WyT"], self.RY, self.S_y)]
+        if not self.lib_main:
+            jobs.insert(0, (self.A[:, :H], w["WhT"], self.RM, self.S_m))
         if smp is not None:
             jobs.append((self.A[:, :H], w["WoT"], self.ZS, self.S_o))
         (gemm.rec_gemm_fp8_group if f8 else gemm.rec_gemm_group)(jobs)
+        if self.lib_main:
+            if f8:
+                a8 = self.A[:, :H].view(torch.float8_e4m3fn)
+                W8t, sb = w["WhL"]
+                torch._scaled_mm(a8, W8t.t(), scale_a=w["sa8"], scale_b=sb, out_dtype=torch.float32, out=self.RM[0])
+            else:
+                gemm.mm(self.A[:, :H], w["WhL"], out=self.RM[0])
         ah, am = self._cell_args(t)
         ah.xp = self.ZP[:, G:].data_ptr()          # z part; the stroke part is formed in the kernel
         if smp is None:
