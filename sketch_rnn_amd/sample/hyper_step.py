@@ -215,6 +215,22 @@ class HyperStepDecoder:
         version). Called by :meth:`begin`; callers running several decoders
         on forked streams call it on the parent stream first."""
         self._w = self._weights()
+        if self.lib_main and self.fp8 and not getattr(self, "_probed", False):
+            # the e4m3 library GEMM must take this shape / layout (probed once,
+            # eagerly, before any graph capture); otherwise the skinny fp8 kernel
+            # runs h W_h in 128-row blocks
+            self._probed = True
+            try:
+                W8t, sb = self._w["WhL"]
+                torch._scaled_mm(self.A[:, :self.H].view(torch.float8_e4m3fn), W8t.t(), scale_a=self._w["sa8"],
+                                 scale_b=sb, out_dtype=torch.float32, out=self.RM[0])
+                torch.cuda.current_stream().synchronize()
+            except (RuntimeError, TypeError):
+                self.lib_main = False
+                self.S_m = min(4, max(1, gemm.plan_splits_fp8(self.B, self.G, self.H)))
+                self.S_m = 4 if self.S_m >= 4 else 2 if self.S_m >= 2 else 1
+                self.RM = torch.empty(self.S_m, self.B, self.G, dtype=torch.float32, device=self.dev)
+                self._w = self._weights()
 
     @torch.no_grad()
     def begin(self, zc, state, x0=None) -> None:
