@@ -528,6 +528,12 @@ __device__ void fwd_body(const PFwdArgs& a, int l, int g, int rb, int wu, unsign
                 const int64_t ro = (int64_t)brow[e] * H + u;
                 hl[((int64_t)(t + 1) * B + (brow[e] - grow0)) * H + u] = to_bf16(0.f);
                 if (P.h_out != nullptr) P.h_out[(int64_t)t * nB * H + ro] = 0.f;
+                if constexpr (LN) {   // (read by the gamma / beta column sums)
+                    const int64_t xo = (int64_t)t * nB * 4 * H + (int64_t)brow[e] * 4 * H + u;
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) st_save(a.ln.xhat, xo + q * H, 0.f, a.ln.lp);
+                    st_save(a.ln.chat, (int64_t)t * nB * H + ro, 0.f, a.ln.lp);
+                }
             }
         }
     }
@@ -857,7 +863,9 @@ __device__ void bwd_body(const PBwdArgs& a, int l, int g, int rb, int wu, unsign
                 for (int q = 0; q < 4; ++q) {
                     gl[gb + q * H] = to_bf16(0.f);
                     if (P.dg != nullptr) P.dg[go + q * H] = 0.f;
+                    if constexpr (LN) st_save(a.ln.dlny, go + q * H, 0.f, a.ln.lp);
                 }
+                if constexpr (LN) st_save(a.ln.dlncy, (int64_t)t * nB * H + (int64_t)brow[e] * H + u, 0.f, a.ln.lp);
             }
         }
     }

@@ -73,6 +73,9 @@ for s in "${steps[@]}"; do
         bench_wide_gemm) run bench_wide_gemm 300 python scripts/bench_wide_gemm.py ;;
         pmc_fetch) run pmc_fetch 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d gpurun_out/pmc_fetch -o run --output-format csv -- python bench.py --steps 1 --warmup 1 --no-eval ;;
         pmc_write) run pmc_write 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d gpurun_out/pmc_write -o run --output-format csv -- python bench.py --steps 1 --warmup 1 --no-eval ;;
+        converge_a) run converge_a 1100 python scripts/converge.py --config vae_large --steps 2000 --seeds 0,1 --arms hip-bf16,hip-fp32 --out gpurun_out/converge_large_r4.jsonl ;;
+        converge_b) run converge_b 1100 python scripts/converge.py --config vae_large --steps 2000 --seeds 2 --arms hip-bf16,hip-fp32 --out gpurun_out/converge_large_r4_s2.jsonl ;;
+        ab_persist_ln) SKR_PERSIST_LN=0 run bench_ln_ps0 600 python bench.py --steps 10 --warmup 2 --config vae_layernorm && SKR_PERSIST_LN=1 run bench_ln_ps1 600 python bench.py --steps 10 --warmup 2 --config vae_layernorm ;;
         bench_b128) run bench_b128 600 python bench.py --steps 10 --warmup 2 --batch 128 ;;
         prof_sample_fused) run prof_sample_fused 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_sample_fused -o run --output-format csv -- python scripts/bench_sample.py --batch 128 --reps 1 --host-steps 2 ;;
         prof_sample_fused8) run prof_sample_fused8 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_sample_fused8 -o run --output-format csv -- python scripts/bench_sample.py --batch 128 --reps 1 --host-steps 2 --dtype fp8 ;;

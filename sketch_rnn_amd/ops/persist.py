@@ -21,8 +21,8 @@ step each way (csrc/lstm_persist.hip ``ln_exchange``).
 
 Dispatch: :func:`persist_ok` is the eligibility test (bf16 compute dtype,
 H in {256, 512}); ``SKR_PERSIST=0`` disables the path (the per-step fused
-kernels of :mod:`.recurrent` run instead), ``SKR_PERSIST_LN=0`` only for
-LayerNorm layers.
+kernels of :mod:`.recurrent` run instead); LayerNorm layers take it only
+with ``SKR_PERSIST_LN=1`` (measured slower, see ``PERSIST_LN``).
 """
 from __future__ import annotations
 
@@ -38,7 +38,10 @@ from ._hipapi import PBwdArgs, PFwdArgs
 from .reduce import colsum
 
 PERSIST_ENABLED = os.environ.get("SKR_PERSIST", "1") != "0"
-PERSIST_LN = os.environ.get("SKR_PERSIST_LN", "1") != "0"     # LayerNorm-LSTM layers too
+# LayerNorm-LSTM layers too: opt-in -- measured slower than the per-step
+# clustered cells on vae_layernorm (11.50 vs 10.34 ms/step): each of the two
+# statistics exchanges per step costs ~6 us (payload drain + epoch flag hop)
+PERSIST_LN = os.environ.get("SKR_PERSIST_LN", "0") == "1"
 # debug: fill every handed-off buffer with NaN before the launch, so a read
 # that overtakes its hand-off shows up as a NaN instead of a stale value
 POISON = os.environ.get("SKR_PERSIST_POISON", "0") == "1"
@@ -88,7 +91,7 @@ def _ln_setup(args, ln, T, NB, nd, nrb, H, dev, lp):
     and (forward) the saves, into ``args.ln``. Returns the tensors to keep."""
     f32 = torch.float32
     g, b, gc, bc = (t.detach().reshape(nd, -1).to(f32).contiguous() for t in ln)
-    xs = torch.empty(nd * nrb * 2 * (H // 16) * 32 * 8, device=dev, dtype=torch.int64)   # tagged words
+    xs = torch.empty(nd * nrb * 2 * (H // 16) * 32 * 8, device=dev, dtype=f32)
     args.ln.g, args.ln.b, args.ln.gc, args.ln.bc = g.data_ptr(), b.data_ptr(), gc.data_ptr(), bc.data_ptr()
     args.ln.xs, args.ln.lp = xs.data_ptr(), int(lp)
     return [g, b, gc, bc, xs]
@@ -127,7 +130,8 @@ def _fwd_launch(xp0, W_in1, b1, W_h0, W_h1, h0a, c0a, h0b, c0b, reset, seed, met
     a = PFwdArgs()
     a.T, a.B, a.nd, a.L, a.H, a.nrb = T, B, nd, L, H, nrb
     a.reset, a.forget_bias, a.seed = _ptr(rst), float(fb), sd.data_ptr()
-    flags = torch.empty(L * nd * nrb * 64, dtype=torch.int32, device=dev)   # zeroed by the launcher
+    # zeroed by the launcher: the h hand-off epochs (+ two LayerNorm phases)
+    flags = torch.empty(L * nd * nrb * 64 * (3 if ln is not None else 1), dtype=torch.int32, device=dev)
     a.flags, a.err = flags.data_ptr(), cluster_error_flag(dev).data_ptr()
     s_ln = None
     if ln is not None:
@@ -205,7 +209,7 @@ def _bwd_launch(s, dims, dtop, dfinal, fp32_dg=True):
     b = PBwdArgs()
     b.T, b.B, b.nd, b.L, b.H, b.nrb = T, B, nd, L, H, nrb
     b.reset, b.seed = _ptr(s.rst), s.seed.data_ptr()
-    flags = torch.empty(L * nd * nrb * 64, dtype=torch.int32, device=dev)   # zeroed by the launcher
+    flags = torch.empty(L * nd * nrb * 64 * (3 if s.ln is not None else 1), dtype=torch.int32, device=dev)
     b.flags, b.err = flags.data_ptr(), cluster_error_flag(dev).data_ptr()
     b.tlen = _ptr(s.tlen)
     ln_keep = dlny = dlncy = None

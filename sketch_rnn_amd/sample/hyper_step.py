@@ -82,7 +82,9 @@ def wide_ok(model) -> bool:
 
 
 WIDE = os.environ.get("SKR_WIDE_DECODE", "1") != "0"
-LIB_MAIN = os.environ.get("SKR_WIDE_LIB_MAIN", "1") != "0"
+# h W_h of the wide decoder on hipBLASLt: opt-in (SKR_WIDE_LIB_MAIN=1), not
+# yet measured end to end -- the default is the skinny kernel's row blocks
+LIB_MAIN = os.environ.get("SKR_WIDE_LIB_MAIN", "0") == "1"
 
 
 class HyperStepDecoder:

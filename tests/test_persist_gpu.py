@@ -17,12 +17,16 @@ pytestmark = pytest.mark.gpu
 DEV = "cuda"
 
 
+_LN_DEFAULT = persist.PERSIST_LN
+
+
 @pytest.fixture(autouse=True)
 def _restore():
     yield
     ops.set_backend("auto")
     ops.set_compute_dtype("fp32")
     persist.PERSIST_ENABLED = True
+    persist.PERSIST_LN = _LN_DEFAULT
     from sketch_rnn_amd.ops.recurrent import check_cluster_errors
     torch.cuda.synchronize()
     check_cluster_errors(DEV)
@@ -258,6 +262,7 @@ def test_plain_training_layer_runs_persistent_and_matches_oracle(H, keep, ln):
     dW_h, dxp, the LayerNorm gamma / beta gradients -- with the same hashed
     recurrent-dropout masks."""
     from sketch_rnn_amd.ops import recurrent
+    persist.PERSIST_LN = True     # (LayerNorm layers: opt-in path)
     B, T = 100, 48
     g = torch.Generator(device=DEV).manual_seed(H)
     xp = (torch.randn(T, B, 4 * H, device=DEV, generator=g) * 0.5)
