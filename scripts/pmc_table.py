@@ -1,7 +1,9 @@
 #!/usr/bin/env python3
 """Per-kernel memory traffic table from two rocprofv3 --pmc passes
 (FETCH_SIZE and WRITE_SIZE: kilobytes moved between L2 and memory, i.e.
-HBM / MALL traffic, not L2 hits) plus the kernel-trace durations of a
+HBM / MALL traffic, not L2 hits; on gfx950 FETCH_SIZE counts half the bytes
+of wide coalesced 16-B-per-lane streaming reads -- MI355X_MICROARCH.md, HBM --
+so the "fetch x2" column doubles it as the upper estimate) plus the kernel-trace durations of a
 separate non-counter run (counter passes serialise dispatches, so their own
 timestamps overstate short kernels).
 
@@ -14,10 +16,10 @@ from collections import defaultdict
 
 
 def short(name: str) -> str:
-    n = name.split("(")[0]
+    n = name
     for p in ("void ", "(anonymous namespace)::", "skr::"):
         n = n.replace(p, "")
-    return n.strip()[:70]
+    return n.split("(")[0].strip()[:70]
 
 
 def read_counter(path):
@@ -47,9 +49,12 @@ def main():
         fk, wk = fetch[k] / n, write.get(k, 0.0) / n
         rows.append((fk * n + wk * n, k, n, fk, wk, us, (fk + wk) * 1e3 / us / 1e6 if us > 0 else 0.0))
     rows.sort(reverse=True)
-    print("%-70s %7s %11s %11s %9s %8s" % ("kernel", "calls", "fetch KB", "write KB", "us/call", "TB/s"))
+    print("%-60s %6s %10s %10s %10s %8s %7s %7s %6s" % ("kernel", "calls", "fetch KB", "fetchx2 KB", "write KB",
+                                                        "us/call", "TB/s", "x2 TB/s", "%peak"))
     for _, k, n, fk, wk, us, tbs in rows[:top]:
-        print("%-70s %7d %11.1f %11.1f %9.2f %8.2f" % (k, n, fk, wk, us, tbs))
+        tb2 = (2 * fk + wk) * 1e3 / us / 1e6 if us > 0 else 0.0
+        print("%-60s %6d %10.1f %10.1f %10.1f %8.2f %7.2f %7.2f %5.0f%%" % (k[:60], n, fk, 2 * fk, wk, us, tbs, tb2,
+                                                                        100 * tb2 / 8.0))
 
 
 if __name__ == "__main__":
