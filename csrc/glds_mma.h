@@ -11,8 +11,11 @@
 // per-lane GLOBAL address, since an LDS-DMA wave writes 1 KiB linearly -- so
 // the 16 rows of a ds_read_b128 fragment read hit 16 distinct bank quads.
 //
-// Block: 256 threads (4 waves); wave w owns rows 32w..32w+31 x all BN
-// columns (2 x BN/16 accumulators). MFMA v_mfma_f32_16x16x32_bf16: lane l
+// Block: NW x 64 threads. NW = 4: wave w owns rows 32w..32w+31 x all BN
+// columns (2 x BN/16 accumulators); NW = 8 (the chained launches of
+// csrc/chain_step.hip that share a 512-thread block with the row cells):
+// wave w owns rows 32(w%4).. x column half w/4 (2 x BN/32 accumulators).
+// MFMA v_mfma_f32_16x16x32_bf16: lane l
 // holds A[row l&15][k 8(l>>4) .. +7] and B[k 8(l>>4) .. +7][col l&15];
 // C/D: col = l&15, row = 4(l>>4) + i.
 //
@@ -43,32 +46,39 @@ __device__ __forceinline__ void wait_ahead(int ahead) {
 template <int BN, int NS>
 constexpr int glds_lds_bytes() { return NS * (BM + BN) * BK * 2; }
 
-template <int BN, int NS>
+// Column tiles (16 wide) of one wave's accumulator.
+template <int BN, int NW>
+constexpr int glds_nj() { return BN / 16 / (NW / 4); }
+
+template <int BN, int NS, int NW = 4>
 __device__ __forceinline__ void glds_mma(const __hip_bfloat16* __restrict__ A, int64_t lda,
                                          const __hip_bfloat16* __restrict__ Bt, int64_t ldb, int M, int n0,
-                                         int64_t k0, int kslice, __hip_bfloat16* smem, f32x4_t (&acc)[2][BN / 16]) {
-    constexpr int NJ = BN / 16;
+                                         int64_t k0, int kslice, __hip_bfloat16* smem,
+                                         f32x4_t (&acc)[2][glds_nj<BN, NW>()]) {
+    constexpr int NJ = glds_nj<BN, NW>();
     constexpr int A_CH = BM / 8, B_CH = BN / 8;     // 1-KiB chunks (8 rows) per tile
-    constexpr int GPW = (A_CH + B_CH) / 4;          // glds per wave per tile
+    static_assert((NW == 4 || NW == 8) && A_CH % NW == 0 && B_CH % NW == 0, "glds_mma: wave layout");
+    constexpr int GPW = (A_CH + B_CH) / NW;         // glds per wave per tile
     constexpr int TILE = (BM + BN) * BK;            // bf16 elements per stage
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int wr = w % 4, wc = w / 4;               // row quarter, column part (NW = 8)
     const int n = kslice / BK;
 
     // per-lane source rows / swizzled chunk (fixed across tiles)
     const int r8 = lane >> 3, slot = lane & 7;
-    const __hip_bfloat16* asrc[A_CH / 4];
-    const __hip_bfloat16* bsrc[B_CH / 4];
+    const __hip_bfloat16* asrc[A_CH / NW];
+    const __hip_bfloat16* bsrc[B_CH / NW];
 #pragma unroll
-    for (int i = 0; i < A_CH / 4; ++i) {
-        const int row = (w + 4 * i) * 8 + r8;
+    for (int i = 0; i < A_CH / NW; ++i) {
+        const int row = (w + NW * i) * 8 + r8;
         const int kc = slot ^ ((row >> 1) & 7);
         // rows past M: every lane of the chunk reads the same 16 bytes (one
         // line instead of 1 KiB; the wave's glds count stays uniform)
         asrc[i] = row < M ? A + (int64_t)row * lda + k0 + kc * 8 : A + (int64_t)(M - 1) * lda + k0;
     }
 #pragma unroll
-    for (int i = 0; i < B_CH / 4; ++i) {
-        const int row = (w + 4 * i) * 8 + r8;
+    for (int i = 0; i < B_CH / NW; ++i) {
+        const int row = (w + NW * i) * 8 + r8;
         const int kc = slot ^ ((row >> 1) & 7);
         bsrc[i] = Bt + (int64_t)(n0 + row) * ldb + k0 + kc * 8;
     }
@@ -76,13 +86,13 @@ __device__ __forceinline__ void glds_mma(const __hip_bfloat16* __restrict__ A, i
         __hip_bfloat16* st = smem + (kt % NS) * TILE;
         const int64_t ko = (int64_t)kt * BK;
 #pragma unroll
-        for (int i = 0; i < A_CH / 4; ++i)
+        for (int i = 0; i < A_CH / NW; ++i)
             __builtin_amdgcn_global_load_lds((const void*)(asrc[i] + ko),
-                                             (__attribute__((address_space(3))) void*)(st + (w + 4 * i) * 512), 16, 0, 0);
+                                             (__attribute__((address_space(3))) void*)(st + (w + NW * i) * 512), 16, 0, 0);
 #pragma unroll
-        for (int i = 0; i < B_CH / 4; ++i)
+        for (int i = 0; i < B_CH / NW; ++i)
             __builtin_amdgcn_global_load_lds((const void*)(bsrc[i] + ko),
-                                             (__attribute__((address_space(3))) void*)(st + BM * BK + (w + 4 * i) * 512),
+                                             (__attribute__((address_space(3))) void*)(st + BM * BK + (w + NW * i) * 512),
                                              16, 0, 0);
     };
 
@@ -107,12 +117,12 @@ __device__ __forceinline__ void glds_mma(const __hip_bfloat16* __restrict__ A, i
             bf16x8_t af[2], bfr[NJ];
 #pragma unroll
             for (int i = 0; i < 2; ++i) {
-                const int row = 32 * w + 16 * i + fr;
+                const int row = 32 * wr + 16 * i + fr;
                 af[i] = *(const bf16x8_t*)(&As[row * BK + ((kc ^ ((row >> 1) & 7)) * 8)]);
             }
 #pragma unroll
             for (int j = 0; j < NJ; ++j) {
-                const int row = 16 * j + fr;
+                const int row = 16 * (wc * NJ + j) + fr;
                 bfr[j] = *(const bf16x8_t*)(&Bs[row * BK + ((kc ^ ((row >> 1) & 7)) * 8)]);
             }
 #pragma unroll

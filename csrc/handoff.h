@@ -13,6 +13,14 @@
 #pragma once
 #include "common.h"
 
+// Per-launch state of a chained launch (csrc/chain_step.hip, csrc/hyper_mod.hip;
+// mirrored by sketch_rnn_amd/ops/_hipapi.py ChainSync).
+struct ChainSync {
+    uint32_t* counters;   // [n] rotating arrival counters of this launch kind (zeroed once)
+    int n, k;             // this launch uses counters[k] and zeroes counters[(k + 1) % n]
+    int* err;             // set to 3 by a timed-out wait
+};
+
 namespace skr {
 
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
@@ -69,6 +77,52 @@ __device__ __forceinline__ void publish(uint32_t* flag, uint32_t epoch) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x == 0) __hip_atomic_store(flag, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ f32x4 ld_sc1_f32x4(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+    return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, kSc1));
+}
+
+// ---- chained launches (csrc/chain_step.hip) ---------------------------------------------
+// A grouped GEMM launch whose leading "producer" tiles feed cell rows of the
+// SAME launch. Producer workgroups store their slabs write-through (sc1),
+// drain, join a workgroup barrier and add 1 to the launch's arrival counter
+// (agent scope) from one lane; a cell row polls that counter with sc1 loads
+// from one lane, joins a barrier and then reads the slabs with sc1 loads
+// only (CDNA4 guide, hand-off table row 1). Workgroups are dispatched in id
+// order and the producers have the lowest ids and never wait, so every
+// producer is resident or done by the time a waiting row is dispatched: the
+// waits cannot deadlock on residency. Bounded like wait_flags.
+__device__ __forceinline__ void chain_arrive(uint32_t* counter) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ inline void chain_wait(const uint32_t* counter, uint32_t target, int* err) {
+    if (threadIdx.x == 0) {
+        for (unsigned spins = 0;; ++spins) {
+            if (__hip_atomic_load(counter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target) break;
+            if ((spins & 255) == 255) {
+                if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) break;
+                if (spins > kHandoffSpinLimit) {
+                    __hip_atomic_store(err, 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    break;
+                }
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+    }
+    // compiler barrier + workgroup barrier: no wave's slab loads move above the poll
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    __syncthreads();
+}
+// Rotating counters: launch k of a sequence uses counters[k] and zeroes
+// counters[(k + 1) % n] (last used one call earlier, finished: launches on one
+// stream are ordered), so every counter starts at zero when its launch runs
+// and no reset launch is needed per call (n >= 2; zero-initialised once).
+__device__ __forceinline__ void chain_rotate(uint32_t* counters, int n, int k) {
+    if (threadIdx.x == 0) __hip_atomic_store(counters + (k + 1) % n, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // Flag words are zeroed by a kernel, not hipMemsetAsync: on MI355X with

@@ -23,7 +23,7 @@
 
 #include "common.h"
 #include "cell_bwd_body.h"
-#include "glds_mma.h"
+#include "skinny_tile.h"
 
 namespace {
 
@@ -35,30 +35,6 @@ using skr::BK;
 using skr::wait_ahead;
 
 constexpr int NSTAGE = 4;   // ring depth of the v1 fp8 kernel (the bf16 ring: csrc/glds_mma.h)
-
-template <int BN, int NS, bool CBF16 = false>
-__device__ __forceinline__ void glds_tile(const __hip_bfloat16* __restrict__ A, int64_t lda,
-                                          const __hip_bfloat16* __restrict__ Bt, int64_t ldb,
-                                          void* __restrict__ Cv, int64_t ldc, int M, int n0, int64_t k0, int kslice,
-                                          __hip_bfloat16* smem) {
-    constexpr int NJ = BN / 16;
-    f32x4 acc[2][NJ];
-    skr::glds_mma<BN, NS>(A, lda, Bt, ldb, M, n0, k0, kslice, smem, acc);
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int fr = lane & 15, fq = lane >> 4;
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < NJ; ++j)
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                const int row = 32 * w + 16 * i + fq * 4 + e;
-                if (row < M) {
-                    if constexpr (CBF16) ((__hip_bfloat16*)Cv)[row * ldc + n0 + 16 * j + fr] = skr::to_bf16(acc[i][j][e]);
-                    else ((float*)Cv)[row * ldc + n0 + 16 * j + fr] = acc[i][j][e];
-                }
-            }
-}
 
 template <int BN, int NS, bool CBF16 = false>
 __global__ __launch_bounds__(256) void skinny_gemm_glds_kernel(
@@ -79,59 +55,9 @@ __global__ __launch_bounds__(256) void skinny_gemm_glds_kernel(
 // backward dR_main @ W_h^T and dvec @ P^T) then share one kernel boundary
 // and fill the chip together instead of each leaving most CUs idle.
 // Workgroup id -> (problem, row block, split, N tile) through the prefix
-// sums `start`. A problem with M > 128 rows (M % 128 == 0: the wide decode
-// of sample/hyper_step.py) runs as M / 128 row blocks sharing B.
-}  // namespace
-
-struct GemmProblem {
-    const void* A; int64_t lda;
-    const void* Bt; int64_t ldb;
-    float* C; int64_t ldc; int64_t c_slab;
-    int M, N, K, splits;
-};
-
-namespace {
-
-constexpr int kMaxGroup = 4;
-struct GemmGroup {
-    GemmProblem p[kMaxGroup];
-    int start[kMaxGroup + 1];
-    int n;
-};
-
-// (row block, split, N tile) of workgroup `local` of a problem: row blocks of
-// 128 rows outermost, then splits, then N tiles
-struct TileIdx { int rb, rows, split, nt; };
-__device__ __forceinline__ TileIdx tile_idx(int local, int M, int N, int splits, int bn) {
-    const int ntiles = N / bn, per_rb = ntiles * splits;
-    TileIdx t;
-    t.rb = local / per_rb;
-    const int rem = local - t.rb * per_rb;
-    t.split = rem / ntiles;
-    t.nt = rem - t.split * ntiles;
-    t.rows = min(BM, M - t.rb * BM);
-    return t;
-}
-
-__host__ __device__ constexpr int row_blocks_of(int M) { return M <= BM ? 1 : (M + BM - 1) / BM; }
-
-template <typename P>
-__device__ __forceinline__ int64_t split_off(const P& p, const TileIdx& t) {
-    return (int64_t)t.split * p.c_slab + (int64_t)t.rb * BM * p.ldc;
-}
-
-template <int BN, int NS>
-__device__ __forceinline__ void group_tile(const GemmGroup& g, const int id, __hip_bfloat16* smem) {
-    int q = 0;
-#pragma unroll
-    for (int i = 1; i < kMaxGroup; ++i) q += (i < g.n && id >= g.start[i]) ? 1 : 0;
-    const GemmProblem& p = g.p[q];
-    const TileIdx t = tile_idx(id - g.start[q], p.M, p.N, p.splits, BN);
-    const int kslice = p.K / p.splits;
-    glds_tile<BN, NS>((const __hip_bfloat16*)p.A + (int64_t)t.rb * BM * p.lda, p.lda, (const __hip_bfloat16*)p.Bt,
-                      p.ldb, p.C + split_off(p, t), p.ldc, t.rows, t.nt * BN, (int64_t)t.split * kslice, kslice, smem);
-}
-
+// sums `start` (csrc/skinny_tile.h). A problem with M > 128 rows (M % 128 ==
+// 0: the wide decode of sample/hyper_step.py) runs as M / 128 row blocks
+// sharing B.
 template <int BN, int NS>
 __global__ __launch_bounds__(256) void skinny_gemm_group_kernel(const GemmGroup g) {
     extern __shared__ __attribute__((aligned(16))) __hip_bfloat16 smem[];

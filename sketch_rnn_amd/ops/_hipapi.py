@@ -278,6 +278,12 @@ class GemmProblem(C.Structure):
     ]
 
 
+class ChainSync(C.Structure):
+    """Mirror of ``ChainSync`` in csrc/chain_step.hip (rotating arrival
+    counters of a chained launch kind)."""
+    _fields_ = [("counters", _p), ("n", _i), ("k", _i), ("err", _p)]
+
+
 class GemmProblem8(C.Structure):
     """Mirror of ``GemmProblem8`` in csrc/skinny_gemm.hip (fp8 v2 products)."""
     _fields_ = [
@@ -391,6 +397,8 @@ class HipLib:
         lib.skr_skinny_gemm_group.restype = _i
         lib.skr_skinny_gemm_group_cellbwd.argtypes = [C.POINTER(GemmProblem), _i, C.POINTER(LstmBwdArgs), _p]
         lib.skr_skinny_gemm_group_cellbwd.restype = _i
+        lib.skr_chain_bwd_main.argtypes = [C.POINTER(GemmProblem), _i, C.POINTER(LstmBwdArgs), C.POINTER(ChainSync), _p]
+        lib.skr_chain_bwd_main.restype = _i
         lib.skr_lstm_fused_fwd.argtypes = [C.POINTER(FusedFwdArgs), _p]
         lib.skr_lstm_fused_fwd.restype = _i
         lib.skr_lstm_fused_bwd.argtypes = [C.POINTER(FusedBwdArgs), _p]
@@ -434,7 +442,8 @@ class HipLib:
                           ("skr_decode_ref_args_size", DecArgs),
                           ("skr_gemm_problem_size", GemmProblem),
                           ("skr_decode_sample_size", DecodeSample),
-                          ("skr_gemm_problem8_size", GemmProblem8)):
+                          ("skr_gemm_problem8_size", GemmProblem8),
+                          ("skr_chain_sync_size", ChainSync)):
             fn = getattr(lib, name)
             fn.restype = _i
             if fn() != C.sizeof(cls):

@@ -366,6 +366,47 @@ def rec_gemm_group_cellbwd(jobs, cell_args) -> None:
         raise RuntimeError("skr_skinny_gemm_group_cellbwd failed (%d)" % rc)
 
 
+# ---- chained launches (csrc/chain_step.hip) ----------------------------------------------
+class ChainCounters:
+    """Rotating arrival counters of one chained launch kind over a sequence
+    of ``n`` launches (launch ``k`` uses counter ``k`` and zeroes counter
+    ``k + 1``): zero-initialised once (normally in the eager warm-up, so no
+    fill kernel lands in a captured step), cached per (device, kind, n) so a
+    captured HIP graph keeps replaying on the same words. Sequences of one
+    kind must not run concurrently on different streams."""
+    _cache = {}
+
+    def __init__(self, device, kind: str, n: int):
+        from .recurrent import cluster_error_flag
+        from ._hipapi import ChainSync
+        key = (str(device), kind, n)
+        buf = ChainCounters._cache.get(key)
+        if buf is None:
+            buf = ChainCounters._cache[key] = torch.zeros(max(n, 2), dtype=torch.int32, device=device)
+        self.buf, self.n = buf, n
+        self.sync = ChainSync()
+        self.sync.counters, self.sync.n, self.sync.err = buf.data_ptr(), n, cluster_error_flag(device).data_ptr()
+
+    def at(self, k: int):
+        self.sync.k = k
+        return self.sync
+
+
+def chain_bwd_main(producers, cell_args, sync) -> int:
+    """One launch: ``producers`` feeding the HyperLSTM main cell's dh_rec
+    slabs and the main-cell backward rows (``skr_chain_bwd_main``, H = 2048).
+    Returns the library code: -2 / -3 / -4 mean "shape not taken" (the caller
+    falls back to the unchained launches)."""
+    import ctypes
+    from ..utils import native
+    lib = native.require_hip()
+    rc = lib.lib.skr_chain_bwd_main(_problems(producers), len(producers), ctypes.byref(cell_args), ctypes.byref(sync),
+                                    torch.cuda.current_stream().cuda_stream)
+    if rc not in (0, -2, -3, -4):
+        raise RuntimeError("skr_chain_bwd_main failed (%d)" % rc)
+    return rc
+
+
 # ---- inference-time helpers ------------------------------------------------------------
 _WCACHE = {}
 WEIGHTS_EPOCH = [0]

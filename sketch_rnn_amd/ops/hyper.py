@@ -38,6 +38,12 @@ HYPER_MAIN_C = int(os.environ.get("SKR_HYPER_MAIN_C", "0"))   # workgroups per r
 # product only the next step reads. SKR_HYPER_BWD_FUSE=0 keeps [main cell] ->
 # [dR_main W_h^T + dvec P^T] -> [hyper cell] -> [dR_hyp W_y^T].
 HYPER_BWD_FUSE = os.environ.get("SKR_HYPER_BWD_FUSE", "1") != "0"
+# Chained backward launch (csrc/chain_step.hip): the main-cell backward rows
+# of step t run INSIDE the launch of step t + 1's dR_hyp W_y^T product (their
+# other loads issued before an in-launch wait on the product's tiles): three
+# launches per backward step instead of four. SKR_CHAIN=0 keeps the unchained
+# launches (A/B).
+CHAIN = os.environ.get("SKR_CHAIN", "1") != "0"
 # (Round 4 measured the hyper-norm projections unfolded -- vec = bf16(hh W_z)
 # W_a + q forward, dz = dvec W_a^T / dh = dz W_z^T backward -- at 27.8 vs
 # 24.6 ms per training step: W_z re-read from L2 by every workgroup costs more
@@ -409,6 +415,12 @@ class _HyperSeq(torch.autograd.Function):
         st = _stream()
         group = lp_on and gemm.GROUPED and S_am >= 1 and S_h >= 1
         first = not fin   # (the last time step runs first)
+        # chained launch (csrc/chain_step.hip): the main cell of step t inside
+        # the dR_hyp W_y^T launch of step t + 1 (row kernel geometry: H = 2048,
+        # bf16 vectors, LayerNorm main cell)
+        chain_m = CHAIN and lp_on and dev.type == "cuda" and T >= 3 and H == 2048 and s.mln_on and \
+            s.VEC.dtype == torch.bfloat16 and s.RLP is not None and dHout is not None and S_ay <= 8
+        cm = gemm.ChainCounters(dev, "hyp_bwd_m", T - 1) if chain_m else None
         for t in range(T - 1, -1, -1):
             clm.set(am, t)
             clh.set(ah, t)
@@ -432,7 +444,16 @@ class _HyperSeq(torch.autograd.Function):
             am.dG = None if lp_on else dRM[t].data_ptr()
             am.dG_lp = dRM_lp[t].data_ptr() if lp_on else None
             am.dxp, am.dvec = dXH[t].data_ptr(), dVEC[t].data_ptr()
-            _cell_bwd(lib, am, s.mln_on, 2 if s.VEC.dtype == torch.bfloat16 else 1, st, "hyper_main_bwd_step")
+            ran = False
+            if chain_m and t < T - 1:   # dR_hyp W_y^T of step t + 1 -> this main cell, one launch
+                ran = gemm.chain_bwd_main([(dRY_lp[t + 1], s.Wyl, DAY, S_ay)], am, cm.at(T - 2 - t)) == 0
+                if not ran:   # shape not taken by the chained row: unchained launches from here on
+                    chain_m = False
+                    gemm.rec_gemm(dRY_lp[t + 1], s.Wyl, DAY, S_ay)
+                else:
+                    ROW_STATS["chain"] += 1
+            if not ran:
+                _cell_bwd(lib, am, s.mln_on, 2 if s.VEC.dtype == torch.bfloat16 else 1, st, "hyper_main_bwd_step")
             ah.c_prev = s.HCC[t].data_ptr()
             ah.xhat, ah.rstd, ah.chat = s.HXHAT[t].data_ptr(), s.HRSTD[t].data_ptr(), s.HCHAT[t].data_ptr()
             ah.step = t
@@ -450,7 +471,8 @@ class _HyperSeq(torch.autograd.Function):
                     gemm.rec_gemm(dRM_lp[t], s.Whl, DAM, S_am)
                     gemm.rec_gemm(dVEC[t], s.Pl, DHZ, S_h)
                 _cell_bwd(lib, ah, True, 0, st, "hyper_bwd_step")
-            gemm.rec_gemm(dRY_lp[t], s.Wyl, DAY, S_ay)
+            if not chain_m or t == 0:   # (chained: runs in the next main-cell launch)
+                gemm.rec_gemm(dRY_lp[t], s.Wyl, DAY, S_ay)
         if not DAY.is_cuda:
             dh0 = DAY[:, :, :H].sum(0) + DAM.sum(0)
             dhh0 = DAY[:, :, H:].sum(0)

@@ -217,6 +217,12 @@ class HyperStepDecoder:
         version). Called by :meth:`begin`; callers running several decoders
         on forked streams call it on the parent stream first."""
         self._w = self._weights()
+        if not self.fused:
+            # the seven-launch step's folded (P^T, q): derived HERE, on the
+            # parent stream, never lazily inside step() -- a decoder on a
+            # forked chunk stream would otherwise find another chunk's P in
+            # gemm.derived's global cache before that stream has written it
+            self._pq()
         if self.lib_main and self.fp8 and not getattr(self, "_probed", False):
             # the e4m3 library GEMM must take this shape / layout (probed once,
             # eagerly, before any graph capture); otherwise the skinny fp8 kernel

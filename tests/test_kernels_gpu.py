@@ -332,17 +332,19 @@ def test_hyper_grouped_gemm_path_bitwise(H, Hh, E):
     """bf16 HyperLSTM with the grouped per-step GEMM launches equals the
     one-launch-per-product path bit for bit (same tiles, same sums)."""
     from sketch_rnn_amd.ops import gemm
+    from sketch_rnn_amd.ops import hyper
     p, x, z, st, w = _hyper_setup(3, 4, 100, 13, 0, H, Hh, E, jitter=0.0)
-    saved = gemm.GROUPED
+    saved = gemm.GROUPED, hyper.CHAIN
     res = []
     try:
         ops.set_compute_dtype("bf16")
         ops.set_backend("hip")
+        hyper.CHAIN = False   # (the chained launches: test_hyper_chained_launches_vs_unchained)
         for grouped in (True, False):
             gemm.GROUPED = grouped
             res.append(_hyper_run(p, x, z, st, w))
     finally:
-        gemm.GROUPED = saved
+        gemm.GROUPED, hyper.CHAIN = saved
     for a, b in zip(*res):
         assert torch.equal(a, b)
 
@@ -934,13 +936,53 @@ def test_hyper_backward_fused_cell_launch_bitwise(monkeypatch):
     ops.set_compute_dtype("bf16")
     ops.set_backend("hip")
     res = []
-    saved = hyper.HYPER_BWD_FUSE
+    saved = hyper.HYPER_BWD_FUSE, hyper.CHAIN
     try:
+        hyper.CHAIN = False   # (the chained launches: test_hyper_chained_launches_vs_unchained)
         for fuse in (True, False):
             hyper.HYPER_BWD_FUSE = fuse
             res.append(_hyper_run(p, x, z, st, w))
     finally:
-        hyper.HYPER_BWD_FUSE = saved
+        hyper.HYPER_BWD_FUSE, hyper.CHAIN = saved
     for n, a, b in zip(_names(p), *res):
         assert torch.equal(a, b), n
 
+
+
+@pytest.mark.parametrize("B,T,fin_w", [(100, 7, True), (100, 5, False), (37, 4, True), (128, 3, False)])
+def test_hyper_chained_launches_vs_unchained(B, T, fin_w):
+    """csrc/chain_step.hip: the main-cell backward rows inside the next step's
+    dR_hyp W_y^T launch (an in-launch wait on an arrival counter, sc1 slab
+    reads), against the unchained launches and the fp32 oracle --
+    outputs, final states, dz and every weight gradient, dropout on, from a
+    non-degenerate state (P != 0, h0 != 0). The row is the same source in
+    another kernel (rounding-level differences from fp contraction), so:
+    error(chained) <= 1.5 error(unchained) + 1e-3 of the largest element;
+    and the chained path itself is run twice and must repeat bit for bit
+    (the rotating counters carry over between calls)."""
+    from sketch_rnn_amd.ops import hyper
+    from sketch_rnn_amd.ops.recurrent import ROW_STATS
+    p, x, z, st, w = _hyper_setup(4, T, B, 5, 16, 2048, 256, 32, jitter=0.02, state=0.1)
+    runs, chained = {}, {}
+    saved = hyper.CHAIN
+    try:
+        for name, backend, dt, chain in (("ref", "torch", "fp32", False), ("chain", "hip", "bf16", True),
+                                         ("plain", "hip", "bf16", False), ("chain2", "hip", "bf16", True)):
+            hyper.CHAIN = chain
+            ops.set_backend(backend)
+            ops.set_compute_dtype(dt)
+            n0 = ROW_STATS["chain"]
+            runs[name] = _hyper_run(p, x, z, st, w, keep=0.9, hkeep=0.9, fin_w=fin_w)
+            chained[name] = ROW_STATS["chain"] - n0
+    finally:
+        hyper.CHAIN = saved
+    # backward main cell: T - 1 chained launches (the last time step has no
+    # W_y^T product before it)
+    assert chained["chain"] == chained["chain2"] == T - 1 and chained["plain"] == 0, chained
+    for i, n in enumerate(_names(p)):
+        assert torch.equal(runs["chain"][i], runs["chain2"][i]), n
+        ref = runs["ref"][i].float()
+        scale = max(ref.abs().max().item(), 1e-3)
+        e_c = (runs["chain"][i].float() - ref).abs().max().item()
+        e_p = (runs["plain"][i].float() - ref).abs().max().item()
+        assert e_c <= 1.5 * e_p + 1e-3 * scale, (n, e_c, e_p, scale)

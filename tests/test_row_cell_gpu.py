@@ -62,11 +62,12 @@ def test_row_cells_hyper_vae_large_shapes(B, keep, hkeep, monkeypatch):
     from test_kernels_gpu import _hyper_run, _hyper_setup, _names
     from sketch_rnn_amd.ops import hyper
     monkeypatch.setattr(hyper, "HYPER_BWD_FUSE", False)
+    monkeypatch.setattr(hyper, "CHAIN", False)   # (the chained main-cell launch: test_kernels_gpu.py)
     T = 7
     p, x, z, st, w = _hyper_setup(6, T, B, 5, 16, 2048, 256, 32, jitter=0.02, state=0.1)
     runs = _arms(lambda: _hyper_run(p, x, z, st, w, keep, hkeep))
-    assert runs["row_launches"] == {"row": 4 * T, "cluster": 0}, runs["row_launches"]
-    assert runs["cluster_launches"] == {"row": 0, "cluster": 4 * T}, runs["cluster_launches"]
+    assert runs["row_launches"] == {"row": 4 * T, "cluster": 0, "chain": 0}, runs["row_launches"]
+    assert runs["cluster_launches"] == {"row": 0, "cluster": 4 * T, "chain": 0}, runs["cluster_launches"]
     _compare(runs, _names(p))
 
 
@@ -106,7 +107,9 @@ def test_row_cells_layernorm_lstm(H, nd, B, keep):
 
 def test_default_policy_row_kernels_only_in_main_backward():
     """Default SKR_ROW_CELLS=main: the HyperLSTM main-cell backward runs the
-    row kernel, the other three cell launches per step the clustered ones."""
+    row kernel (the first backward step as its own launch, the rest inside
+    the chained dR_hyp W_y^T launch, csrc/chain_step.hip), the other three
+    cell launches per step the clustered ones."""
     from test_kernels_gpu import _hyper_run, _hyper_setup
     T = 3
     p, x, z, st, w = _hyper_setup(2, T, 100, 5, 16, 2048, 256, 32, jitter=0.02, state=0.1)
@@ -115,4 +118,4 @@ def test_default_policy_row_kernels_only_in_main_backward():
     ops.set_compute_dtype("bf16")
     before = dict(recurrent.ROW_STATS)
     _hyper_run(p, x, z, st, w)
-    assert {k: recurrent.ROW_STATS[k] - before[k] for k in before} == {"row": T, "cluster": 3 * T}
+    assert {k: recurrent.ROW_STATS[k] - before[k] for k in before} == {"row": 1, "chain": T - 1, "cluster": 3 * T}
