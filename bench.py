@@ -149,6 +149,12 @@ def main():
     if not args.no_eval:
         ev = trainer.evaluate(test)      # the whole held-out split (test.num_batches batches)
         recon = ev["r_cost"]
+    probe = next(trainer.model.parameters())
+    backend_resolved = "hip" if ops.use_hip(probe) else "torch"
+    hip_lib = None
+    if backend_resolved == "hip":
+        from sketch_rnn_amd.utils import native
+        hip_lib = native.hip_lib_stamp()
     global_batch = args.batch * world
     positions_per_s = global_batch * args.seq_len * args.steps / elapsed
     value = sum(valid[i % len(valid)] for i in range(args.steps)) / elapsed
@@ -181,6 +187,9 @@ def main():
                 "dist_backend": dp.backend() or "none",
                 "world_size_observed": world,
                 "backend": ops.get_backend(),
+                # what "auto" resolved to on this device, and which kernel build ran
+                "backend_resolved": backend_resolved,
+                "hip_lib": hip_lib,
                 "hip_graph": bool(trainer.use_graph),
             },
             "positions_per_s": round(positions_per_s, 1),

@@ -58,10 +58,10 @@ __global__ __launch_bounds__(256) void skinny_gemm_glds_kernel(
 // sums `start` (csrc/skinny_tile.h). A problem with M > 128 rows (M % 128 ==
 // 0: the wide decode of sample/hyper_step.py) runs as M / 128 row blocks
 // sharing B.
-template <int BN, int NS>
-__global__ __launch_bounds__(256) void skinny_gemm_group_kernel(const GemmGroup g) {
+template <int BN, int NS, int NW = 4>
+__global__ __launch_bounds__(NW * 64) void skinny_gemm_group_kernel(const GemmGroup g) {
     extern __shared__ __attribute__((aligned(16))) __hip_bfloat16 smem[];
-    group_tile<BN, NS>(g, blockIdx.x, smem);
+    group_tile<BN, NS, NW>(g, blockIdx.x, smem);
 }
 
 // Grouped GEMM tiles + the rows of one backward LayerNorm cell step in ONE
@@ -446,11 +446,11 @@ int launch_v2(dim3 grid, hipStream_t s, const void* A, int64_t lda, int64_t a_ba
     return SKR_CHECK_LAUNCH();
 }
 
-template <int BN, int NS>
+template <int BN, int NS, int NW = 4>
 int launch_group(const GemmGroup& g, hipStream_t s) {
     const size_t lds = (size_t)NS * (BM + BN) * BK * 2;
-    set_lds_attr(skinny_gemm_group_kernel<BN, NS>, lds);
-    hipLaunchKernelGGL((skinny_gemm_group_kernel<BN, NS>), dim3(g.start[g.n]), dim3(256), lds, s, g);
+    set_lds_attr(skinny_gemm_group_kernel<BN, NS, NW>, lds);
+    hipLaunchKernelGGL((skinny_gemm_group_kernel<BN, NS, NW>), dim3(g.start[g.n]), dim3(NW * 64), lds, s, g);
     return SKR_CHECK_LAUNCH();
 }
 
@@ -505,7 +505,10 @@ SKR_API int skr_skinny_gemm_group(const GemmProblem* probs, int n, int bn, hipSt
         g.start[i + 1] = g.start[i] + (p.N / bn) * p.splits * row_blocks_of(p.M);
     }
     for (int i = n + 1; i <= kMaxGroup; ++i) g.start[i] = g.start[n];
-    if (bn == 128) return g_nstage == 3 ? launch_group<128, 3>(g, s) : launch_group<128, 4>(g, s);
+    // 128-wide tiles run on 8 waves (512 threads: wave w = row quarter w % 4 x
+    // column half w / 4): the same per-wave work as two 64-wide 4-wave
+    // workgroups, with the activation rows staged once for 128 columns
+    if (bn == 128) return g_nstage == 3 ? launch_group<128, 3, 8>(g, s) : launch_group<128, 4, 8>(g, s);
     return g_nstage == 3 ? launch_group<64, 3>(g, s) : g_nstage == 6 ? launch_group<64, 6>(g, s)
                                                                     : launch_group<64, 4>(g, s);
 }

@@ -101,10 +101,16 @@ class GradReducer:
     RCCL path on a single-GPU box; the result is the identity).
 
     ``fold_scale``: leave the summed gradients unscaled; the consumer applies
-    1/world itself (FlatAdam.set_grad_scale) -- no extra pass over the arena."""
+    1/world itself (FlatAdam.set_grad_scale) -- no extra pass over the arena.
+
+    ``tail``: trailing floats of ``grad`` that always travel in fp32 (the
+    loss scalars and the valid-point count of FlatAdam's tail: with a bf16
+    wire they would be summed to ~3 significant digits). With an fp32 wire
+    they simply ride in the last bucket; with bf16 they are one extra small
+    fp32 all-reduce issued with the last part."""
 
     def __init__(self, grad: torch.Tensor, bucket_mb: float = 32.0, split: Optional[int] = None,
-                 wire_dtype: str = "fp32", force: bool = False, fold_scale: bool = False):
+                 wire_dtype: str = "fp32", force: bool = False, fold_scale: bool = False, tail: int = 0):
         if wire_dtype not in ("fp32", "bf16"):
             raise ValueError("wire_dtype must be fp32 or bf16, got %r" % (wire_dtype,))
         self.grad = grad
@@ -112,7 +118,10 @@ class GradReducer:
         self.fold_scale = fold_scale
         self.world = world_size()
         self.active = self.world > 1 or (force and is_dist())
-        n = grad.numel()
+        n_all = grad.numel()
+        self.tail_n = tail if wire_dtype == "bf16" else 0
+        n = n_all - self.tail_n
+        self.tail = grad[n:] if self.tail_n else None    # fp32, reduced in place with the last part
         esize = 2 if wire_dtype == "bf16" else 4
         per = max(1, int(bucket_mb * 1024 * 1024 // esize))
         per = (per + 63) // 64 * 64
@@ -132,7 +141,10 @@ class GradReducer:
             for (a, b), w in zip(self.ranges[part], self.parts[part]):
                 w.copy_(self.grad[a:b])
         self._started.append(part)
-        return [dist.all_reduce(b, op=dist.ReduceOp.SUM, async_op=True) for b in self.parts[part]]
+        works = [dist.all_reduce(b, op=dist.ReduceOp.SUM, async_op=True) for b in self.parts[part]]
+        if self.tail is not None and part == len(self.parts) - 1:
+            works.append(dist.all_reduce(self.tail, op=dist.ReduceOp.SUM, async_op=True))
+        return works
 
     def all_reduce(self, async_op: bool = False):
         """Sum every bucket across ranks (all in flight at once), then
@@ -160,6 +172,8 @@ class GradReducer:
                     g = self.grad[a:b].copy_(w)
                     if inv != 1.0:
                         g.mul_(inv)
+            if self.tail is not None and inv != 1.0 and len(self.parts) - 1 in self._started:
+                self.tail.mul_(inv)
         elif inv != 1.0:
             self.grad.mul_(inv)
         self._started = []

@@ -263,7 +263,7 @@ class VAETrainer:
         # the arena plus its tail (this step's loss scalars, summed in the last
         # bucket); the 1/world average is folded into the clip + Adam kernels
         self.reducer = dp.GradReducer(self.opt.grad_full, split=split, wire_dtype=wire,
-                                      force=force_reducer, fold_scale=True) if reduce_on else None
+                                      force=force_reducer, fold_scale=True, tail=FlatAdam.TAIL) if reduce_on else None
         if reduce_on:
             self.opt.set_grad_scale(1.0 / self.world)
         self._enc_pending = None
@@ -504,6 +504,8 @@ class VAETrainer:
         pf = self._prefetch
         t0 = time.time()
         valid = 0.0     # this rank's non-padding stroke points since the last log line
+        # every rank's points (DP): summed on the device from each step's reduced arena tail
+        valid_glob = torch.zeros((), dtype=torch.float64, device=self.device)
         n_int = 0       # steps since the last log line (resume / repeated train() safe)
         while self.step < num_steps:
             with phase("data", self.host_times):
@@ -512,18 +514,25 @@ class VAETrainer:
                 batch = self.batch_to_device(raw)
             with phase("step", self.host_times):
                 out = self.train_step(*batch)
+            if self.reducer is not None:
+                # global point count of this step from the reduced arena tail,
+                # accumulated on the device (no host sync, no collective)
+                idx = len([k for k in self._TAIL_KEYS if k in self._last_keys])
+                valid_glob.add_(self.opt.tail[idx].double())
             n_int += 1
             if self.step % log_every == 0 or self.step == num_steps:
                 check_device_faults()
                 if self.reducer is not None:   # global means, from the arena tail (no extra collective)
                     vals = self.reduced_scalars()
                     vals.pop("valid_points")
+                    valid_all = float(valid_glob)           # summed per step from the reduced tails
                 else:
                     vals = {k: float(v) for k, v in out.items()}
+                    valid_all = valid                       # one rank: this rank's batches
                 dt = (time.time() - t0) / n_int
                 t0 = time.time()
-                valid_all = dp.sum_scalar(valid)                # every rank's batches (bench.py's metric)
                 valid = 0.0
+                valid_glob.zero_()
                 if self.rank == 0:
                     self.log("step: %d, lr: %.6f, klw: %0.4f, cost: %.4f, recon: %.4f, kl: %.4f, time/step: %.4f" % (
                         self.step, self.opt.lr, schedules.kl_weight(cfg, self.step - 1), vals["cost"],

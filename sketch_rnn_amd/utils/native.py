@@ -83,3 +83,26 @@ def require_hip():
         raise RuntimeError("libskrnn_hip.so not found at %s: run `python scripts/build_native.py` "
                            "(or __graft_entry__.build()) before using the GPU path" % HIP_LIB)
     return lib
+
+
+def hip_lib_stamp() -> dict:
+    """Identity of the loaded HIP kernel library: its path, the content stamp
+    scripts/build_native.py wrote beside it (sha256 of the sources, headers,
+    flags and toolchain it was built from) and the file's own sha256 prefix."""
+    import hashlib
+    info = {"path": os.path.relpath(HIP_LIB, os.path.dirname(LIB_DIR)) if HIP_LIB.startswith(LIB_DIR) else HIP_LIB}
+    try:
+        with open(HIP_LIB + ".sha256") as f:
+            info["source_stamp"] = f.read().strip()[:16]
+    except OSError:
+        info["source_stamp"] = None
+    try:
+        h = hashlib.sha256()
+        with open(HIP_LIB, "rb") as f:
+            for chunk in iter(lambda: f.read(1 << 20), b""):
+                h.update(chunk)
+        info["file_sha256"] = h.hexdigest()[:16]
+    except OSError:
+        info["file_sha256"] = None
+    return info
+

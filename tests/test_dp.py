@@ -187,10 +187,11 @@ def test_bench_multi_rank_cpu(tmp_path):
     assert 0 < rec["value"] <= rec["positions_per_s"] and 0 < rec["valid_fraction"] <= 1
 
 
-def _scalars_worker(rank, world, port, out_dir):
+def _scalars_worker(rank, world, port, out_dir, wire="fp32"):
     """The loss scalars packed into the arena tail come out of the last
     bucket as the sum over ranks: the trainer's logged cost is the mean of
-    the per-rank costs, and the valid-point count is the global one."""
+    the per-rank costs, and the valid-point count is the global one -- also
+    with the bf16 gradient wire (the tail travels in fp32)."""
     dp = _init(rank, world, port)
     from sketch_rnn_amd.cli.vae_train import make_datasets
     from sketch_rnn_amd.config import VAEConfig
@@ -199,7 +200,8 @@ def _scalars_worker(rank, world, port, out_dir):
                     save_every=0, seed=0)
     (tr_set, va, te), _ = make_datasets(cfg, None, 40, rank=rank)
     logs = []
-    tr = VAETrainer(cfg, tr_set, va, te, save_dir=os.path.join(out_dir, "s"), log=logs.append)
+    tr = VAETrainer(cfg, tr_set, va, te, save_dir=os.path.join(out_dir, "s"), log=logs.append, dp_wire_dtype=wire)
+    assert tr.reducer.wire_dtype == wire
     assert tr.reducer is not None and tr.reducer.fold_scale and float(tr.opt.scalars[6]) == 0.5
     batch = tr.batch_to_device(tr_set.random_batch(rank, world))
     out = tr.train_step(*batch)
@@ -212,8 +214,13 @@ def _scalars_worker(rank, world, port, out_dir):
     torch.distributed.destroy_process_group()
 
 
-def test_dp_loss_scalars_reduced_in_last_bucket(tmp_path):
-    _spawn(_scalars_worker, tmp_path)
+def _scalars_worker_bf16(rank, world, port, out_dir):
+    _scalars_worker(rank, world, port, out_dir, wire="bf16")
+
+
+@pytest.mark.parametrize("wire", ["fp32", "bf16"])
+def test_dp_loss_scalars_reduced_in_last_bucket(tmp_path, wire):
+    _spawn(_scalars_worker if wire == "fp32" else _scalars_worker_bf16, tmp_path)
     s = [torch.load(tmp_path / ("s%d.pt" % k), weights_only=True) for k in range(2)]
     for k in ("cost", "r_cost", "kl_cost"):
         mean = (s[0]["local"][k] + s[1]["local"][k]) / 2
