@@ -288,7 +288,6 @@ __device__ __forceinline__ void cell_fwd_body(const FwdArgs& a, const int c, con
         a.c_carry[ro] = r ? a.init_c[ro] : cn[k];
         if (a.lp_kind == 1) ((__hip_bfloat16*)a.h_lp)[b * a.ld_lp + u] = to_bf16(hc);
         else if (a.lp_kind == 2) ((float*)a.h_lp)[b * a.ld_lp + u] = hc;
-        else if (a.lp_kind == 3) ((uint8_t*)a.h_lp)[b * a.ld_lp + u] = to_fp8(hc * kFp8ActScale);
     }
     SKR_STAMP(4);
 }

@@ -2,7 +2,6 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <hip/hip_bf16.h>
-#include <hip/hip_fp8.h>
 #include <stdint.h>
 
 #define SKR_API extern "C" __attribute__((visibility("default")))
@@ -103,15 +102,6 @@ __device__ __forceinline__ void block_sum(float (&v)[N], float* lds) {
 }
 
 __device__ __forceinline__ __hip_bfloat16 to_bf16(float x) { return __float2bfloat16(x); }
-
-// fp8 (OCP e4m3) GEMM operands for inference: activations are stored
-// multiplied by kFp8ActScale (|h| <= 1 -> |h*64| <= 64 < 448, and values down
-// to ~3e-5 stay representable); the GEMM epilogue multiplies by 1/64.
-constexpr float kFp8ActScale = 64.0f;
-__device__ __forceinline__ uint8_t to_fp8(float x) {
-    const __hip_fp8_e4m3 q(x);
-    return *reinterpret_cast<const uint8_t*>(&q);
-}
 
 // Sum of the NS split-K partial slabs at idx (NS > 0: compile-time count,
 // all loads independent); NS == 0: runtime count n, batches of 8 clamped loads.

@@ -126,7 +126,6 @@ __global__ __launch_bounds__(256) void decode_hyper_cell(const FwdArgs a, const 
     a.c_carry[ro] = cn;
     if (a.lp_kind == 1) ((__hip_bfloat16*)a.h_lp)[b * a.ld_lp + u] = to_bf16(h);
     else if (a.lp_kind == 2) ((float*)a.h_lp)[b * a.ld_lp + u] = h;
-    else if (a.lp_kind == 3) ((uint8_t*)a.h_lp)[b * a.ld_lp + u] = to_fp8(h * kFp8ActScale);
 }
 
 }  // namespace

@@ -48,10 +48,11 @@ __device__ __forceinline__ void st_sc1_f32(__amdgpu_buffer_rsrc_t r, uint32_t of
 }
 
 // One wave waits until every flag of `flags[0..n)` (n <= 64) is >= epoch
-// (lane i polls flag i with sc1 loads). Bounded; on a timeout (or when
-// another wait of this launch already timed out) sets/observes *err and
-// returns false.
-__device__ inline bool wait_flags(const uint32_t* flags, int n, uint32_t epoch, int* err) {
+// (lane i polls flag i with sc1 loads). Bounded by `limit` polls; on a
+// timeout (or when another wait of this launch already timed out)
+// sets/observes *err and returns false.
+__device__ inline bool wait_flags(const uint32_t* flags, int n, uint32_t epoch, int* err,
+                                  unsigned limit = kHandoffSpinLimit) {
     const int lane = threadIdx.x & 63;
     const uint32_t* f = flags + (lane < n ? lane : 0);
     for (unsigned spins = 0;; ++spins) {
@@ -60,7 +61,7 @@ __device__ inline bool wait_flags(const uint32_t* flags, int n, uint32_t epoch, 
         if ((spins & 255) == 255) {
             const int e = __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             if (e != 0) return false;
-            if (spins > kHandoffSpinLimit) {
+            if (spins > limit) {
                 if (lane == 0) __hip_atomic_store(err, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 return false;
             }

@@ -38,3 +38,17 @@ SKR_API int skr_occupancy_hog(int grid, int threads, int lds_bytes, int us, floa
     hipLaunchKernelGGL(hog_kernel, dim3(grid), dim3(threads), lds_bytes, s, ticks, lds_bytes / 4, sink);
     return SKR_CHECK_LAUNCH();
 }
+
+// A stream on its own hardware queue restricted to the first `ncu` CUs of
+// the CU mask (a CU-masked queue): the failure-path test runs the persistent
+// encoder backward on it, so that only part of a row block can be resident
+// -- the state a co-running kernel holding the rest of the chip creates.
+// Tests only.
+SKR_API int skr_stream_create_cu_limited(int ncu, hipStream_t* out) {
+    if (ncu < 1 || ncu > 1024) return -2;
+    uint32_t mask[32] = {};
+    for (int i = 0; i < ncu; ++i) mask[i / 32] |= 1u << (i % 32);
+    return hipExtStreamCreateWithCUMask(out, (uint32_t)((ncu + 31) / 32), mask) == hipSuccess ? 0 : -3;
+}
+
+SKR_API int skr_stream_destroy(hipStream_t s) { return hipStreamDestroy(s) == hipSuccess ? 0 : -1; }

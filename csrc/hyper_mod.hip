@@ -52,13 +52,11 @@ __device__ __forceinline__ uint32_t pack_bf(float a, float b) {
 
 }  // namespace
 
-// Decode-step inputs (sample/hyper_step.py, csrc/decode_step.hip): hh from
-// the hyper cell's fp32 output (the fp8 decode keeps no bf16 copy of it) and
-// the main x-projection formed here from the sampled stroke x [B][5]:
+// Decode-step inputs (sample/hyper_step.py, csrc/decode_step.hip): the main
+// x-projection formed here from the sampled stroke x [B][5]:
 // xh[b][n] = zp[b][n] + sum_k x[b][k] w5[k][n] (skr_bproj_fwd's order). Null
-// members: the training sequence's inputs (bf16 hh operand, precomputed xh).
+// members: the training sequence's input (precomputed xh).
 struct ModDecode {
-    const float* hh32;
     const float* x5;
     const float* w5; int64_t ldw5;
     const float* zp; int64_t ldzp;
@@ -85,7 +83,6 @@ __global__ __launch_bounds__(NTH) void hyper_mod_fwd(ModDecode dec, const __hip_
         B = min(MAXB, B - r0);
         const int64_t G4 = (int64_t)r0 * 4 * H;
         if (hh) hh += (int64_t)r0 * ld_hh;
-        if (dec.hh32) dec.hh32 += (int64_t)r0 * HH;
         if (dec.x5) {
             dec.x5 += (int64_t)r0 * 5;
             dec.zp += (int64_t)r0 * dec.ldzp;
@@ -139,14 +136,7 @@ __global__ __launch_bounds__(NTH) void hyper_mod_fwd(ModDecode dec, const __hip_
 #pragma unroll
     for (int k = 0; k < SPT; ++k) {
         const int i = min(tid + k * NTH, NPC - 1), r = i / (HH / 8), c = i % (HH / 8);
-        if (dec.hh32 != nullptr) {
-            const float* src = dec.hh32 + (int64_t)min(r, B - 1) * HH + 8 * c;
-            const f32x4 lo = *(const f32x4*)src, hi = *(const f32x4*)(src + 4);
-            hv[k] = bf16x8{(__bf16)lo[0], (__bf16)lo[1], (__bf16)lo[2], (__bf16)lo[3],
-                           (__bf16)hi[0], (__bf16)hi[1], (__bf16)hi[2], (__bf16)hi[3]};
-        } else {
-            hv[k] = *(const bf16x8*)(hh + (int64_t)min(r, B - 1) * ld_hh + 8 * c);
-        }
+        hv[k] = *(const bf16x8*)(hh + (int64_t)min(r, B - 1) * ld_hh + 8 * c);
     }
 #pragma unroll
     for (int k = 0; k < SPT; ++k) {
@@ -233,8 +223,7 @@ SKR_API int skr_hyper_mod_fwd(const void* hh, int64_t ld_hh, const void* PlT, co
                               float* stats, int B, int H, int Hh, const ModDecode* dec, hipStream_t s) {
     const ModDecode dz = dec ? *dec : ModDecode{};
     if (dz.x5 && (((uintptr_t)dz.w5 | (uintptr_t)dz.zp) & 15 || dz.ldw5 % 4 || dz.ldzp % 4)) return -4;
-    if (dz.hh32 && ((uintptr_t)dz.hh32 & 15)) return -4;
-    if ((dz.x5 == nullptr && xh == nullptr) || (dz.hh32 == nullptr && hh == nullptr)) return -3;
+    if ((dz.x5 == nullptr && xh == nullptr) || hh == nullptr) return -3;
     if (B <= 0) return 0;
     if ((B > MAXB && B % MAXB != 0) || Hh != HH || H % TU != 0) return -2;
     if (((uintptr_t)hh | (uintptr_t)PlT | (uintptr_t)xh | (uintptr_t)R | (uintptr_t)vec | (uintptr_t)g |

@@ -30,7 +30,7 @@ struct FwdArgs {
     float* rstd;                       // LN: [B, 5]
     float* chat;                       // LN: [B, H]
     float* h_carry;                    // [B, H]
-    void* h_lp; int64_t ld_lp; int lp_kind;  // 0: none, 1: bf16, 2: fp32, 3: fp8 e4m3 (x kFp8ActScale)
+    void* h_lp; int64_t ld_lp; int lp_kind;  // 0: none, 1: bf16, 2: fp32
     float* c_carry;                    // [B, H]
     // rows split over `cluster` workgroups (LayerNorm statistics exchanged in-launch)
     int cluster;                       // <= 1: one workgroup per row

@@ -268,21 +268,10 @@ __global__ __launch_bounds__(64 * NW) void lstm_fused_bwd(const FusedBwdArgs a) 
     }
 }
 
-// SKR_FUSED_BWD_WAVES: 4 or 8 waves per workgroup (default 8)
-inline int bwd_waves() {
-    static int nw = -1;
-    if (nw < 0) {
-        const char* e = getenv("SKR_FUSED_BWD_WAVES");
-        nw = (e != nullptr && atoi(e) == 4) ? 4 : 8;
-    }
-    return nw;
-}
-
 template <int H>
 int launch_bwd(const FusedBwdArgs& a, hipStream_t s) {
     const dim3 grid(H / UB, (a.B + RB - 1) / RB, a.nd);
-    if (bwd_waves() == 4) hipLaunchKernelGGL((lstm_fused_bwd<H, 4>), grid, dim3(256), 0, s, a);
-    else hipLaunchKernelGGL((lstm_fused_bwd<H, 8>), grid, dim3(512), 0, s, a);
+    hipLaunchKernelGGL((lstm_fused_bwd<H, 8>), grid, dim3(512), 0, s, a);   // 8 waves (4 measured slower)
     return SKR_CHECK_LAUNCH();
 }
 

@@ -42,10 +42,11 @@
 // the launcher checks the grid against the occupancy API and refuses a grid
 // that does not fit.
 //
-// LayerNorm-LSTM layers (PLn: the VAE's layer_norm decoder / encoder) add two
-// row-statistics exchanges per step each way (ln_exchange: gate blocks, then
-// c'); the backward recomputes the gates from the saved xhat like
-// csrc/cell_bwd_body.h.
+// (A LayerNorm-LSTM variant -- both LayerNorms' row statistics exchanged
+// in-launch, two hand-offs per step each way -- was built and measured
+// slower than the per-step clustered cells on vae_layernorm, 11.50 vs 10.34
+// ms/step, and removed in round 5; the LayerNorm-LSTM runs on
+// csrc/lstm_cell.hip.)
 //
 // Reference semantics: model.py:19-23 (BasicLSTMCell, forget bias 1),
 // model.py:66-95 (static unroll with the eoc state reset: the carried state
@@ -63,6 +64,12 @@ constexpr int NTHR = 512;           // 8 waves
 constexpr int kFlagStride = 64;     // u32 flag words per (layer, group, row block)
 
 }  // namespace
+
+// Spin bound of this file's hand-off waits (polls; kHandoffSpinLimit, ~seconds).
+// The failure-path test lowers it (skr_persist_set_spin_limit) so that a
+// co-running occupancy hog outlives it: the wait times out, sets *err and
+// the launch drains (tests/test_dp_concurrency_gpu.py).
+__device__ unsigned g_persist_spin_limit = kHandoffSpinLimit;
 
 struct PFwdLayer {
     const __hip_bfloat16* WT; int64_t w_gs;  // [nd][4H][K] B^T: row n = [W_in[:, n] | W_h[:, n]], K = kin + H
@@ -82,33 +89,15 @@ struct PFwdLayer {
                                               // directions side by side (the encoder's [h_fw | h_bw]), or null
 };
 
-// LayerNorm-LSTM (one layer, no eoc resets; null g: a plain layer). Per-gate
-// LayerNorm of the gate pre-activations and LayerNorm of c' (cells.py
-// layer_norm_lstm_step), the row statistics exchanged between the NW
-// workgroups of a row block through `xs` once per LayerNorm per step (the
-// hand-off protocol of the carried h: sc1 payload, drained, epoch flag).
-struct PLn {
-    const float* g; const float* b;           // [nd][4H] gate LayerNorm gamma / beta
-    const float* gc; const float* bc;         // [nd][H] cell LayerNorm gamma / beta
-    void* xhat;                               // [T][nd*B][4H] normalised gates (bf16 if lp, else fp32)
-    float* rstd;                              // [T][nd*B][5] 1/std of the four gate blocks and of c'
-    void* chat;                               // [T][nd*B][H] normalised c'
-    int lp;
-    float* xs;                                // [nd][nrb][2 phases][NW][32 rows][8] partial sums (scratch)
-    void* dlny; void* dlncy;                  // backward saves: d(LN output) [T][nd*B][4H] / [T][nd*B][H]
-    float fb;                                 // forget bias (the backward recomputes the gates)
-};
-
 struct PFwdArgs {
     int T, B, nd, L, H, nrb;                  // nrb row blocks of 16*MTW rows per group
     PFwdLayer ly[2];
     const float* reset;                       // [T][nd*B] or null
     float forget_bias;
     const int64_t* seed;
-    uint32_t* flags;                          // [3][L][nd][nrb][kFlagStride] epochs (zeroed per launch): h, LN x2
+    uint32_t* flags;                          // [L][nd][nrb][kFlagStride] epochs (zeroed per launch)
     int* err;
     const int* tlen;                          // [B] valid lengths (L = 1) or null, see row_block_steps
-    PLn ln;
 };
 
 struct PBwdLayer {
@@ -133,7 +122,6 @@ struct PBwdArgs {
     uint32_t* flags;
     int* err;
     const int* tlen;                          // as PFwdArgs::tlen (the same lengths as the forward)
-    PLn ln;                                   // the forward's LayerNorm parameters and saves
 };
 
 namespace {
@@ -180,86 +168,10 @@ __device__ __forceinline__ int row_last_step(const int* tlen, int T, int r) {
     return tlen == nullptr ? T - 1 : max(min(tlen[r], T), 1) - 1;
 }
 
-// Row statistics of a LayerNorm over all H units of a row: the epilogue lane
-// (fr, fq) of row tile mt holds NV partial values v[e][k] of rows
-// 16 mt + 4 fq + e for its unit. Sums them over the workgroup's 16 units
-// (lanes fr), publishes the workgroup's [32 rows][8] partials (sc1) and its
-// epoch, waits for the NW workgroups of the row block and returns the row
-// totals in v (every epilogue lane). Called by EVERY wave (publish is a
-// workgroup barrier); `epi` marks the lanes that hold data.
-template <int NV>
-__device__ __forceinline__ bool ln_exchange(float (&v)[4][NV], float* xs, int NW, int wu, int mt, bool epi,
-                                            uint32_t* flags, uint32_t epoch, int* err) {
-    const int lane = threadIdx.x & 63, fr = lane & 15, fq = lane >> 4;
-    const __amdgpu_buffer_rsrc_t r = rsrc(xs, (int64_t)NW * 32 * 8 * 4);
-    if (epi) {
-#pragma unroll
-        for (int e = 0; e < 4; ++e)
-#pragma unroll
-            for (int k = 0; k < NV; ++k) {
-                float x = v[e][k];
-                x += __shfl_xor(x, 1, 64);
-                x += __shfl_xor(x, 2, 64);
-                x += __shfl_xor(x, 4, 64);
-                x += __shfl_xor(x, 8, 64);
-                v[e][k] = x;
-            }
-        if (fr == 0) {
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                const uint32_t off = (uint32_t)(((wu * 32 + mt * 16 + 4 * fq + e) * 8) * 4);
-#pragma unroll
-                for (int h = 0; h < (NV + 3) / 4; ++h) {
-                    f32x4 q4 = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-                    for (int k = 0; k < 4; ++k)
-                        if (4 * h + k < NV) q4[k] = v[e][4 * h + k];
-                    st_sc1(r, off + 16 * h, __builtin_bit_cast(u32x4, q4));
-                }
-            }
-        }
-    }
-    publish(flags + wu, epoch);
-    bool ok = true;
-    if (epi) {
-        ok = wait_flags(flags, NW, epoch, err);
-        float acc[4][NV];
-#pragma unroll
-        for (int e = 0; e < 4; ++e)
-#pragma unroll
-            for (int k = 0; k < NV; ++k) acc[e][k] = 0.f;
-        for (int w2 = fr; w2 < NW; w2 += 16) {
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                const uint32_t off = (uint32_t)(((w2 * 32 + mt * 16 + 4 * fq + e) * 8) * 4);
-#pragma unroll
-                for (int h = 0; h < (NV + 3) / 4; ++h) {
-                    const f32x4 q4 = __builtin_bit_cast(f32x4, ld_sc1(r, off + 16 * h));
-#pragma unroll
-                    for (int k = 0; k < 4; ++k)
-                        if (4 * h + k < NV) acc[e][4 * h + k] += q4[k];
-                }
-            }
-        }
-#pragma unroll
-        for (int e = 0; e < 4; ++e)
-#pragma unroll
-            for (int k = 0; k < NV; ++k) {
-                float x = acc[e][k];
-                x += __shfl_xor(x, 1, 64);
-                x += __shfl_xor(x, 2, 64);
-                x += __shfl_xor(x, 4, 64);
-                x += __shfl_xor(x, 8, 64);
-                v[e][k] = x;
-            }
-    }
-    return ok;
-}
-
 // =====================================================================================
 // forward
 // =====================================================================================
-template <int H, int MTW, int KIN, bool LN = false>
+template <int H, int MTW, int KIN>
 __device__ void fwd_body(const PFwdArgs& a, int l, int g, int rb, int wu, unsigned char* smem) {
     constexpr int K = KIN + H, KS = 8 / MTW, KP = K / KS, NKS = KP / 32, NW = H / U;
     const PFwdLayer& P = a.ly[l];
@@ -313,25 +225,6 @@ __device__ void fwd_body(const PFwdArgs& a, int l, int g, int rb, int wu, unsign
     const int arow = (int)grow0 + min(row_t0 + fr, B - 1);
     bool ok = true;
     const int Te = row_block_steps(a.tlen, T, B, rb, 16 * MTW);
-    // LayerNorm: this lane's unit's gamma / beta, the row block's exchange slots
-    float lg[4] = {}, lb[4] = {}, lcg = 0.f, lcb = 0.f;
-    float* xs1 = nullptr;
-    float* xs2 = nullptr;
-    uint32_t *fl1 = nullptr, *fl2 = nullptr;
-    if constexpr (LN) {
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            lg[q] = a.ln.g[g * 4 * H + q * H + u];
-            lb[q] = a.ln.b[g * 4 * H + q * H + u];
-        }
-        lcg = a.ln.gc[g * H + u];
-        lcb = a.ln.bc[g * H + u];
-        xs1 = a.ln.xs + ((int64_t)(g * a.nrb + rb) * 2) * NW * 32 * 8;
-        xs2 = xs1 + NW * 32 * 8;
-        const int64_t FL = (int64_t)a.L * a.nd * a.nrb * kFlagStride;
-        fl1 = my_flags + FL;
-        fl2 = my_flags + 2 * FL;
-    }
 
     for (int t = 0; t < Te; ++t) {
         // ---- epilogue inputs of step t (independent of the recurrence: issued before the wait)
@@ -353,8 +246,8 @@ __device__ void fwd_body(const PFwdArgs& a, int l, int g, int rb, int wu, unsign
         if (tile_on) {
             const int k0 = kp * KP;
             const bool from_in = KIN > 0 && k0 < KIN;
-            if (from_in) ok = ok && wait_flags(in_flags, NW, (uint32_t)(t + 1), a.err);
-            else if (t > 0) ok = ok && wait_flags(my_flags, NW, (uint32_t)t, a.err);
+            if (from_in) ok = ok && wait_flags(in_flags, NW, (uint32_t)(t + 1), a.err, g_persist_spin_limit);
+            else if (t > 0) ok = ok && wait_flags(my_flags, NW, (uint32_t)t, a.err, g_persist_spin_limit);
             // A fragments: row arow, columns k0 + ks*32 + fq*8 (sc1: written by other workgroups)
             bf16x8 af[NKS];
             const int kc = from_in ? k0 : k0 - KIN;     // column within the source matrix
@@ -386,63 +279,10 @@ __device__ void fwd_body(const PFwdArgs& a, int l, int g, int rb, int wu, unsign
                 acc[q] = s;
             }
         }
-        float lnx[4][4], lnr[4][5], lnc[4];   // LN saves: xhat, 1/std, chat
-        if constexpr (LN) {
-            // ---- gate LayerNorm: row sums of g and g^2 per gate block over all H units
-            float gv[4][4], st8[4][8];
-#pragma unroll
-            for (int e = 0; e < 4; ++e)
-#pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    gv[e][q] = epi ? acc[q][e] + xv[e][q] : 0.f;
-                    const float v = bon[e] ? gv[e][q] : 0.f;
-                    st8[e][q] = v;
-                    st8[e][4 + q] = v * v;
-                }
-            ok = ln_exchange<8>(st8, xs1, NW, wu, mt, epi, fl1, (uint32_t)(t + 1), a.err) && ok;
-            const uint32_t key = keep_on ? hash_key(*a.seed, P.stream, (uint32_t)t) : 0u;
-            float st2[4][2], cn_[4], o_[4];
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                float y[4];
-#pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    const float mean = st8[e][q] / (float)H;
-                    const float var = fmaxf(st8[e][4 + q] / (float)H - mean * mean, 0.f);
-                    const float rs = rsqrtf(var + kLnEps);
-                    lnx[e][q] = (gv[e][q] - mean) * rs;
-                    lnr[e][q] = rs;
-                    y[q] = lnx[e][q] * lg[q] + lb[q];
-                }
-                const float i = cell_sig(y[0]), tj = cell_tanh(y[1]), f = cell_sig(y[2] + a.forget_bias);
-                o_[e] = cell_sig(y[3]);
-                const float m = dropout_mult(keep_on, key, (int64_t)brow[e] * H + u, P.keep);
-                cn_[e] = c[e] * f + i * tj * m;
-                const float v = bon[e] ? cn_[e] : 0.f;
-                st2[e][0] = v;
-                st2[e][1] = v * v;
-            }
-            // ---- cell LayerNorm
-            ok = ln_exchange<2>(st2, xs2, NW, wu, mt, epi, fl2, (uint32_t)(t + 1), a.err) && ok;
-            if (epi) {
-#pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    const float mean = st2[e][0] / (float)H;
-                    const float var = fmaxf(st2[e][1] / (float)H - mean * mean, 0.f);
-                    const float rcs = rsqrtf(var + kLnEps);
-                    lnc[e] = (cn_[e] - mean) * rcs;
-                    lnr[e][4] = rcs;
-                    cn[e] = cn_[e];
-                    hn[e] = cell_tanh(lnc[e] * lcg + lcb) * o_[e];
-                    hc[e] = hn[e];      // (no eoc resets with LayerNorm)
-                    c[e] = cn[e];
-                }
-            }
-        }
         if (epi) {
             const uint32_t key = keep_on ? hash_key(*a.seed, P.stream, (uint32_t)t) : 0u;
 #pragma unroll
-            for (int e = 0; e < 4 && !LN; ++e) {
+            for (int e = 0; e < 4; ++e) {
                 const float gi = acc[0][e] + xv[e][0], gj = acc[1][e] + xv[e][1];
                 const float gf = acc[2][e] + xv[e][2], go = acc[3][e] + xv[e][3];
                 const float i = sigmoidf_(gi), tj = tanhf(gj), f = sigmoidf_(gf + a.forget_bias), o = sigmoidf_(go);
@@ -491,21 +331,9 @@ __device__ void fwd_body(const PFwdArgs& a, int l, int g, int rb, int wu, unsign
                 if (!bon[e]) continue;
                 const int64_t ro = (int64_t)brow[e] * H + u;
                 const int64_t so = (int64_t)t * nB * H + ro;
-                if constexpr (LN) {   // xhat / 1/std / chat: the backward recomputes the gates from them
-                    const int64_t xo = (int64_t)t * nB * 4 * H + (int64_t)brow[e] * 4 * H + u;
+                float* ap = P.act + (int64_t)t * nB * 4 * H + (int64_t)brow[e] * 4 * H + u;
 #pragma unroll
-                    for (int q = 0; q < 4; ++q) st_save(a.ln.xhat, xo + q * H, lnx[e][q], a.ln.lp);
-                    st_save(a.ln.chat, so, lnc[e], a.ln.lp);
-                    if (fr == 0) {
-                        float* rp = a.ln.rstd + ((int64_t)t * nB + brow[e]) * 5;
-#pragma unroll
-                        for (int q = 0; q < 5; ++q) rp[q] = lnr[e][q];
-                    }
-                } else {
-                    float* ap = P.act + (int64_t)t * nB * 4 * H + (int64_t)brow[e] * 4 * H + u;
-#pragma unroll
-                    for (int q = 0; q < 4; ++q) ap[q * H] = av[e][q];
-                }
+                for (int q = 0; q < 4; ++q) ap[q * H] = av[e][q];
                 P.c_out[so] = cn[e];
                 if (P.c_carry != nullptr) P.c_carry[so + (int64_t)nB * H] = c[e];
                 if (P.h_out != nullptr) P.h_out[so] = hn[e];
@@ -528,12 +356,6 @@ __device__ void fwd_body(const PFwdArgs& a, int l, int g, int rb, int wu, unsign
                 const int64_t ro = (int64_t)brow[e] * H + u;
                 hl[((int64_t)(t + 1) * B + (brow[e] - grow0)) * H + u] = to_bf16(0.f);
                 if (P.h_out != nullptr) P.h_out[(int64_t)t * nB * H + ro] = 0.f;
-                if constexpr (LN) {   // (read by the gamma / beta column sums)
-                    const int64_t xo = (int64_t)t * nB * 4 * H + (int64_t)brow[e] * 4 * H + u;
-#pragma unroll
-                    for (int q = 0; q < 4; ++q) st_save(a.ln.xhat, xo + q * H, 0.f, a.ln.lp);
-                    st_save(a.ln.chat, (int64_t)t * nB * H + ro, 0.f, a.ln.lp);
-                }
             }
         }
     }
@@ -557,17 +379,13 @@ __global__ __launch_bounds__(NTHR) void lstm_persist_fwd(const PFwdArgs a) {
             return;
         }
     }
-    if (a.ln.g != nullptr) {
-        fwd_body<H, MTW, 0, true>(a, l, g, rb, wu, smem);
-        return;
-    }
     fwd_body<H, MTW, 0>(a, l, g, rb, wu, smem);
 }
 
 // =====================================================================================
 // backward (reverse time)
 // =====================================================================================
-template <int H, int MTW, bool UP, bool LN = false>
+template <int H, int MTW, bool UP>
 __device__ void bwd_body(const PBwdArgs& a, int l, int g, int rb, int wu, unsigned char* smem) {
     constexpr int G = 4 * H, KS = 8 / MTW, KP = G / KS, NKS = KP / 32, NW = H / U;
     constexpr int NCH = NKS > 8 ? 8 : NKS;     // k-steps per load batch
@@ -620,47 +438,19 @@ __device__ void bwd_body(const PBwdArgs& a, int l, int g, int rb, int wu, unsign
     const int arow = (int)grow0 + min(row_t0 + fr, B - 1);
     bool ok = true;
     const int Te = row_block_steps(a.tlen, T, B, rb, 16 * MTW);
-    float lg[4] = {}, lb[4] = {}, lcg = 0.f, lcb = 0.f;
-    float* xs1 = nullptr;
-    float* xs2 = nullptr;
-    uint32_t *fl1 = nullptr, *fl2 = nullptr;
-    if constexpr (LN) {
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            lg[q] = a.ln.g[g * 4 * H + q * H + u];
-            lb[q] = a.ln.b[g * 4 * H + q * H + u];
-        }
-        lcg = a.ln.gc[g * H + u];
-        lcb = a.ln.bc[g * H + u];
-        xs1 = a.ln.xs + ((int64_t)(g * a.nrb + rb) * 2) * NW * 32 * 8;
-        xs2 = xs1 + NW * 32 * 8;
-        const int64_t FL = (int64_t)a.L * a.nd * a.nrb * kFlagStride;
-        fl1 = my_flags + FL;
-        fl2 = my_flags + 2 * FL;
-    }
 
     // t = Te-1 .. 0 are cell steps; t = -1 only forms dh0 = dG_0 @ W_h^T
     for (int t = Te - 1; t >= -1; --t) {
-        float ac[4][4], cnw[4], cpv[4], dho[4], rs[4], rsv[4][5];
+        float ac[4][4], cnw[4], cpv[4], dho[4], rs[4];
         if (epi && t >= 0) {
             const int64_t so = (int64_t)t * nB * H;
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
                 const int64_t ro = (int64_t)brow[e] * H + u;
-                if constexpr (LN) {   // ac = xhat, cnw = chat; rsv = 1/std (gates, c')
-                    const int64_t xo = (int64_t)t * nB * G + (int64_t)brow[e] * G + u;
+                const float* ap = P.act + (int64_t)t * nB * G + (int64_t)brow[e] * G + u;
 #pragma unroll
-                    for (int q = 0; q < 4; ++q) ac[e][q] = ld_save(a.ln.xhat, xo + q * H, a.ln.lp);
-                    cnw[e] = ld_save(a.ln.chat, so + ro, a.ln.lp);
-                    const float* rp = a.ln.rstd + ((int64_t)t * nB + brow[e]) * 5;
-#pragma unroll
-                    for (int q = 0; q < 5; ++q) rsv[e][q] = rp[q];
-                } else {
-                    const float* ap = P.act + (int64_t)t * nB * G + (int64_t)brow[e] * G + u;
-#pragma unroll
-                    for (int q = 0; q < 4; ++q) ac[e][q] = ap[q * H];
-                    cnw[e] = P.c_out[so + ro];
-                }
+                for (int q = 0; q < 4; ++q) ac[e][q] = ap[q * H];
+                cnw[e] = P.c_out[so + ro];
                 cpv[e] = t == 0 ? P.c0[ro] : (P.c_carry != nullptr ? P.c_carry[so + ro] : P.c_out[so - (int64_t)nB * H + ro]);
                 dho[e] = ((!UP && P.dh_out != nullptr) ? P.dh_out[so + ro] : 0.f) + (t == tlast[e] ? dhl[e] : 0.f);
                 rs[e] = a.reset != nullptr ? a.reset[(int64_t)t * nB + brow[e]] : 0.f;
@@ -671,7 +461,7 @@ __device__ void bwd_body(const PBwdArgs& a, int l, int g, int rb, int wu, unsign
             const int k0 = kp * KP;
             // dG_l[t+1] @ W_h^T (own layer, previous reverse step)
             if (t < Te - 1) {
-                ok = ok && wait_flags(my_flags, NW, (uint32_t)(T - 1 - t), a.err);
+                ok = ok && wait_flags(my_flags, NW, (uint32_t)(T - 1 - t), a.err, g_persist_spin_limit);
                 const uint32_t base = (uint32_t)(((int64_t)(t + 1) * B + (arow - grow0)) * G * 2);
 #pragma unroll
                 for (int kb = 0; kb < NKS; kb += NCH) {
@@ -686,7 +476,7 @@ __device__ void bwd_body(const PBwdArgs& a, int l, int g, int rb, int wu, unsign
             }
             // dG_{l+1}[t] @ W_in_{l+1}^T (layer above, same step)
             if (UP && t >= 0) {
-                ok = ok && wait_flags(up_flags, NW, (uint32_t)(T - t), a.err);
+                ok = ok && wait_flags(up_flags, NW, (uint32_t)(T - t), a.err, g_persist_spin_limit);
                 const uint32_t base = (uint32_t)(((int64_t)t * nB + arow) * G * 2);
 #pragma unroll
                 for (int kb = 0; kb < NKS; kb += NCH) {
@@ -722,7 +512,7 @@ __device__ void bwd_body(const PBwdArgs& a, int l, int g, int rb, int wu, unsign
             }
             break;
         }
-        float dy[4][4], dlc[4], dly[4][4];
+        float dy[4][4];
         f32x4 sr = {0.f, 0.f, 0.f, 0.f}, su = {0.f, 0.f, 0.f, 0.f};
         if (epi) {
             sr = part[(mt * 2) * 64 + lane];
@@ -734,60 +524,10 @@ __device__ void bwd_body(const PBwdArgs& a, int l, int g, int rb, int wu, unsign
                 for (int p = 1; p < KS; ++p) su += part[((p * MTW + mt) * 2 + 1) * 64 + lane];
             }
         }
-        if constexpr (LN) {   // (no eoc resets, one layer: no UP)
-            const uint32_t key = keep_on ? hash_key(*a.seed, P.stream, (uint32_t)t) : 0u;
-            float act[4][4], dout[4], dch[4], st2[4][2];
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                const int64_t ro = (int64_t)brow[e] * H + u;
-                float dhr = sr[e];
-                if (t == Te - 1) dhr = (epi && P.dhT != nullptr) ? P.dhT[ro] : 0.f;
-                const float dh = dho[e] + dhr;
-                // gate activations from xhat (the forward's expressions)
-                act[e][0] = cell_sig(ac[e][0] * lg[0] + lb[0]);
-                act[e][1] = cell_tanh(ac[e][1] * lg[1] + lb[1]);
-                act[e][2] = cell_sig(ac[e][2] * lg[2] + lb[2] + a.ln.fb);
-                act[e][3] = cell_sig(ac[e][3] * lg[3] + lb[3]);
-                const float th = cell_tanh(cnw[e] * lcg + lcb);
-                dout[e] = dh * th;
-                const float dcn = dh * act[e][3] * (1.f - th * th);
-                dlc[e] = dcn;
-                dch[e] = bon[e] ? dcn * lcg : 0.f;
-                st2[e][0] = dch[e];
-                st2[e][1] = dch[e] * cnw[e];
-            }
-            ok = ln_exchange<2>(st2, xs1, NW, wu, mt, epi, fl1, (uint32_t)(T - t), a.err) && ok;
-            float acc8[4][8];
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                const int64_t ro = (int64_t)brow[e] * H + u;
-                const float dc = dcr[e] + rsv[e][4] * (dch[e] - st2[e][0] / (float)H - cnw[e] * st2[e][1] / (float)H);
-                const float i = act[e][0], tj = act[e][1], f = act[e][2], o = act[e][3];
-                const float m = dropout_mult(keep_on, key, ro, P.keep);
-                dly[e][0] = dc * tj * m * i * (1.f - i);
-                dly[e][1] = dc * i * m * (1.f - tj * tj);
-                dly[e][2] = dc * cpv[e] * f * (1.f - f);
-                dly[e][3] = dout[e] * o * (1.f - o);
-                dcr[e] = dc * f;
-#pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    const float dgq = bon[e] ? dly[e][q] * lg[q] : 0.f;
-                    dy[e][q] = dgq;
-                    acc8[e][q] = dgq;
-                    acc8[e][4 + q] = dgq * ac[e][q];
-                }
-            }
-            ok = ln_exchange<8>(acc8, xs2, NW, wu, mt, epi, fl2, (uint32_t)(T - t), a.err) && ok;
-#pragma unroll
-            for (int e = 0; e < 4; ++e)
-#pragma unroll
-                for (int q = 0; q < 4; ++q)
-                    dy[e][q] = rsv[e][q] * (dy[e][q] - acc8[e][q] / (float)H - ac[e][q] * acc8[e][4 + q] / (float)H);
-        }
         if (epi) {
             const uint32_t key = keep_on ? hash_key(*a.seed, P.stream, (uint32_t)t) : 0u;
 #pragma unroll
-            for (int e = 0; e < 4 && !LN; ++e) {
+            for (int e = 0; e < 4; ++e) {
                 const int64_t ro = (int64_t)brow[e] * H + u;
                 float dhr = sr[e];
                 if (t == Te - 1) dhr = P.dhT != nullptr ? P.dhT[ro] : 0.f;
@@ -827,19 +567,6 @@ __device__ void bwd_body(const PBwdArgs& a, int l, int g, int rb, int wu, unsign
             }
         }
         publish(my_flags + wu, (uint32_t)(T - t));
-        if constexpr (LN) {   // d(LayerNorm outputs) for the gamma / beta gradients
-            if (epi) {
-#pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    if (!bon[e]) continue;
-                    const int64_t ro = (int64_t)t * nB * H + (int64_t)brow[e] * H + u;
-                    const int64_t go = (int64_t)t * nB * G + (int64_t)brow[e] * G + u;
-                    st_save(a.ln.dlncy, ro, dlc[e], a.ln.lp);
-#pragma unroll
-                    for (int q = 0; q < 4; ++q) st_save(a.ln.dlny, go + q * H, dly[e][q], a.ln.lp);
-                }
-            }
-        }
         if (epi && P.dg != nullptr) {
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
@@ -863,9 +590,7 @@ __device__ void bwd_body(const PBwdArgs& a, int l, int g, int rb, int wu, unsign
                 for (int q = 0; q < 4; ++q) {
                     gl[gb + q * H] = to_bf16(0.f);
                     if (P.dg != nullptr) P.dg[go + q * H] = 0.f;
-                    if constexpr (LN) st_save(a.ln.dlny, go + q * H, 0.f, a.ln.lp);
                 }
-                if constexpr (LN) st_save(a.ln.dlncy, (int64_t)t * nB * H + (int64_t)brow[e] * H + u, 0.f, a.ln.lp);
             }
         }
     }
@@ -888,10 +613,6 @@ __global__ __launch_bounds__(NTHR) void lstm_persist_bwd(const PBwdArgs a) {
             bwd_body<H, MTW, true>(a, l, g, rb, wu, smem);
             return;
         }
-    }
-    if (a.ln.g != nullptr) {
-        bwd_body<H, MTW, false, true>(a, l, g, rb, wu, smem);
-        return;
     }
     bwd_body<H, MTW, false>(a, l, g, rb, wu, smem);
 }
@@ -929,7 +650,7 @@ int launch_persist(KF kern, const A& a, size_t lds, hipStream_t s) {
     // captured persistent launch saw the previous replay's epochs and read
     // hand-off buffers before they were written (tests/test_persist_gpu.py::
     // test_persistent_graph_replay_matches_eager, with poisoned buffers).
-    const int nflags = a.L * a.nd * a.nrb * kFlagStride * (a.ln.g != nullptr ? 3 : 1);   // h (+ 2 LayerNorm phases)
+    const int nflags = a.L * a.nd * a.nrb * kFlagStride;
     hipLaunchKernelGGL(zero_flags, dim3((nflags + 255) / 256), dim3(256), 0, s, a.flags, nflags);
     hipLaunchKernelGGL(kern, dim3(grid), dim3(NTHR), lds, s, a);
     return SKR_CHECK_LAUNCH();
@@ -943,10 +664,6 @@ int check_common(const A& a) {
     if (a.nrb != (a.B + 16 * kMTW - 1) / (16 * kMTW)) return -4;
     if (a.flags == nullptr || a.err == nullptr) return -6;
     if (a.tlen != nullptr && a.L != 1) return -7;   // stacked layers run the full T
-    if (a.ln.g != nullptr && (a.L != 1 || a.reset != nullptr || a.ln.b == nullptr || a.ln.gc == nullptr ||
-                              a.ln.bc == nullptr || a.ln.xhat == nullptr || a.ln.rstd == nullptr ||
-                              a.ln.chat == nullptr || a.ln.xs == nullptr))
-        return -12;   // LayerNorm: one layer, no eoc resets, every save and the exchange scratch
     // 32-bit buffer offsets
     if ((int64_t)(a.T + 1) * a.nd * a.B * 4 * a.H * 2 > 0x7fffffffLL) return -11;
     return 0;
@@ -971,12 +688,18 @@ SKR_API int skr_lstm_persist_bwd(const PBwdArgs* a, hipStream_t s) {
     if (rc) return rc > 0 ? 0 : rc;
     for (int l = 0; l < a->L; ++l)
         if ((a->ly[l].Wu != nullptr) != (l < a->L - 1)) return -3;
-    if (a->ln.g != nullptr && (a->ln.dlny == nullptr || a->ln.dlncy == nullptr)) return -12;
     switch (a->H) {
         case 256: return launch_persist(lstm_persist_bwd<256, kMTW>, *a, bwd_lds(256, a->L), s);
         case 512: return launch_persist(lstm_persist_bwd<512, kMTW>, *a, bwd_lds(512, a->L), s);
     }
     return -2;
+}
+
+// Spin bound of the persistent kernels' waits (0: the default). Host-side,
+// between launches (the value is read at each bound check).
+SKR_API int skr_persist_set_spin_limit(unsigned polls) {
+    const unsigned v = polls ? polls : kHandoffSpinLimit;
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_persist_spin_limit), &v, sizeof v, 0, hipMemcpyHostToDevice) == hipSuccess ? 0 : -1;
 }
 
 SKR_API int skr_lstm_persist_fwd_args_size() { return (int)sizeof(PFwdArgs); }

@@ -164,15 +164,8 @@ using KernelT = void (*)(const A);
 
 
 // Units per thread: 4 (rows up to 2048 units: <= 512 threads, no AGPR spill
-// in the backward), 8 for wider rows. SKR_ROW_V=8 forces 8 at 2048.
-int pick_v(int H) {
-    static const int force = [] {
-        const char* e = getenv("SKR_ROW_V");
-        return e ? atoi(e) : 0;
-    }();
-    if (force == 8 && H >= 2048) return 8;
-    return H > 2048 ? 8 : 4;
-}
+// in the backward), 8 for wider rows.
+int pick_v(int H) { return H > 2048 ? 8 : 4; }
 
 #define SKR_ROW_GEOMS(X) X(64, 4) X(128, 4) X(256, 4) X(512, 4) X(256, 8) X(512, 8)
 

@@ -34,8 +34,6 @@ using skr::BM;
 using skr::BK;
 using skr::wait_ahead;
 
-constexpr int NSTAGE = 4;   // ring depth of the v1 fp8 kernel (the bf16 ring: csrc/glds_mma.h)
-
 template <int BN, int NS, bool CBF16 = false>
 __global__ __launch_bounds__(256) void skinny_gemm_glds_kernel(
     const __hip_bfloat16* __restrict__ A, int64_t lda, int64_t a_batch,
@@ -79,230 +77,6 @@ __global__ __launch_bounds__(256) void skinny_gemm_group_cellbwd_kernel(const Ge
         return;
     }
     group_tile<BN, NS>(g, blockIdx.x - cell.B, smem);
-}
-
-// ---------------------------------------------------------------------------
-// fp8 K-tiles (128 bytes per LDS row, chunk-swizzled like the bf16 ring) go
-// through gfx950's block-scaled v_mfma_scale_f32_16x16x128_f8f6f4 (e4m3 x
-// e4m3, both E8M0 block scales = 127, i.e. x1: the per-column weight scale
-// and the activation scale are applied in the epilogue): ONE instruction per
-// 16 x 16 tile per K-tile, at twice the bf16 rate per clock -- the CDNA3-era
-// v_mfma_f32_16x16x32_fp8_fp8 runs at the bf16 rate, so fp8 operands only
-// halved the bytes (round 3 measured it equal to bf16). Lane (r, g) =
-// (l & 15, l >> 4) feeds row (A) / column (B) r with bytes [32 g, 32 g + 32)
-// of the K-tile -- the same k order on both operands.
-typedef __attribute__((ext_vector_type(8))) int i32x8;
-
-__device__ __forceinline__ i32x8 frag8x32(const uint8_t* S, int row) {
-    const int fq = (threadIdx.x & 63) >> 4, sw = (row >> 1) & 7;
-    const int4 lo = *(const int4*)(&S[row * 128 + (((2 * fq) ^ sw) * 16)]);
-    const int4 hi = *(const int4*)(&S[row * 128 + (((2 * fq + 1) ^ sw) * 16)]);
-    return i32x8{lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
-}
-
-__device__ __forceinline__ f32x4 mfma_fp8_k128(i32x8 a, i32x8 b, f32x4 c) {
-    return __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a, b, c, 0, 0, 0, 127, 0, 127);
-}
-
-// ---------------------------------------------------------------------------
-// fp8 (OCP e4m3) variant of the v2 ring for inference-time recurrent
-// products: operands are bytes, a K-tile is 128 elements (the same 128-byte
-// LDS rows and swizzle as the bf16 kernel), one MX-scaled MFMA per tile pair
-// (mfma_fp8_k128). Epilogue applies the per-output-column weight scale and
-// the activation scale: C = acc * sa * sb[n].
-constexpr int BK8 = 128;
-
-template <int BN>
-__global__ __launch_bounds__(256) void skinny_gemm_fp8_kernel(
-    const uint8_t* __restrict__ A, int64_t lda, int64_t a_batch,
-    const uint8_t* __restrict__ Bt, int64_t ldb, int64_t b_batch, const float* __restrict__ b_scale,
-    int64_t bs_batch, float a_scale,
-    float* __restrict__ C, int64_t ldc, int64_t c_slab, int64_t c_batch, int M, int kslice) {
-    constexpr int NJ = BN / 16;
-    constexpr int A_CH = BM / 8, B_CH = BN / 8;      // 1-KiB chunks (8 rows x 128 B) per tile
-    constexpr int GPW = (A_CH + B_CH) / 4;
-    constexpr int TILE = (BM + BN) * BK8;            // bytes per stage
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem8[];
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const int n0 = blockIdx.x * BN;
-    const int64_t k0 = (int64_t)blockIdx.y * kslice;
-    const int n = kslice / BK8;
-    A += blockIdx.z * a_batch;
-    Bt += blockIdx.z * b_batch;
-    b_scale += blockIdx.z * bs_batch;
-    C += blockIdx.z * c_batch + blockIdx.y * c_slab;
-
-    const int r8 = lane >> 3, slot = lane & 7;
-    const uint8_t* asrc[A_CH / 4];
-    const uint8_t* bsrc[B_CH / 4];
-#pragma unroll
-    for (int i = 0; i < A_CH / 4; ++i) {
-        const int row = (w + 4 * i) * 8 + r8;
-        asrc[i] = A + (int64_t)min(row, M - 1) * lda + k0 + (slot ^ ((row >> 1) & 7)) * 16;
-    }
-#pragma unroll
-    for (int i = 0; i < B_CH / 4; ++i) {
-        const int row = (w + 4 * i) * 8 + r8;
-        bsrc[i] = Bt + (int64_t)(n0 + row) * ldb + k0 + (slot ^ ((row >> 1) & 7)) * 16;
-    }
-    auto issue = [&](int kt) {
-        uint8_t* st = smem8 + (kt % NSTAGE) * TILE;
-        const int64_t ko = (int64_t)kt * BK8;
-#pragma unroll
-        for (int i = 0; i < A_CH / 4; ++i)
-            __builtin_amdgcn_global_load_lds((const void*)(asrc[i] + ko),
-                                             (__attribute__((address_space(3))) void*)(st + (w + 4 * i) * 1024), 16, 0, 0);
-#pragma unroll
-        for (int i = 0; i < B_CH / 4; ++i)
-            __builtin_amdgcn_global_load_lds((const void*)(bsrc[i] + ko),
-                                             (__attribute__((address_space(3))) void*)(st + BM * BK8 + (w + 4 * i) * 1024),
-                                             16, 0, 0);
-    };
-
-    f32x4 acc[2][NJ];
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-    const int fr = lane & 15, fq = lane >> 4;
-#pragma unroll
-    for (int p = 0; p < NSTAGE - 1; ++p)
-        if (p < n) issue(p);
-    for (int kt = 0; kt < n; ++kt) {
-        const int ahead = min(n - 1 - kt, NSTAGE - 2);
-        if (ahead >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * GPW) : "memory");
-        else if (ahead == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GPW) : "memory");
-        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-        if (kt + NSTAGE - 1 < n) issue(kt + NSTAGE - 1);
-        const uint8_t* As = smem8 + (kt % NSTAGE) * TILE;
-        const uint8_t* Bs = As + BM * BK8;
-        {
-            i32x8 af[2], bfr[NJ];
-#pragma unroll
-            for (int i = 0; i < 2; ++i) af[i] = frag8x32(As, 32 * w + 16 * i + fr);
-#pragma unroll
-            for (int j = 0; j < NJ; ++j) bfr[j] = frag8x32(Bs, 16 * j + fr);
-#pragma unroll
-            for (int i = 0; i < 2; ++i)
-#pragma unroll
-                for (int j = 0; j < NJ; ++j) acc[i][j] = mfma_fp8_k128(af[i], bfr[j], acc[i][j]);
-        }
-    }
-#pragma unroll
-    for (int j = 0; j < NJ; ++j) {
-        const float sc = a_scale * b_scale[n0 + 16 * j + fr];
-#pragma unroll
-        for (int i = 0; i < 2; ++i)
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                const int row = 32 * w + 16 * i + fq * 4 + e;
-                if (row < M) C[row * ldc + n0 + 16 * j + fr] = acc[i][j][e] * sc;
-            }
-    }
-}
-
-// fp8 v2: the same tile as glds_tile (ring depth NS, counted waits, grouped
-// launch, optional bf16 output) on e4m3 operands: K-tiles of 128 bytes,
-// one MX-scaled K=128 MFMA per tile pair, epilogue C = acc * a_scale * b_scale[n]. At
-// NS = 3 a stage is (128 + 64) x 128 B = 24 KiB: two workgroups per CU, like
-// the bf16 ring, while every byte moved carries twice the K extent.
-template <int BN, int NS, bool CBF16>
-__device__ __forceinline__ void glds_tile_fp8(const uint8_t* __restrict__ A, int64_t lda,
-                                              const uint8_t* __restrict__ Bt, int64_t ldb,
-                                              const float* __restrict__ b_scale, float a_scale,
-                                              void* __restrict__ Cv, int64_t ldc, int M, int n0, int64_t k0,
-                                              int kslice, uint8_t* smem8) {
-    constexpr int NJ = BN / 16;
-    constexpr int A_CH = BM / 8, B_CH = BN / 8;
-    constexpr int GPW = (A_CH + B_CH) / 4;
-    constexpr int TILE = (BM + BN) * BK8;
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const int n = kslice / BK8;
-    const int r8 = lane >> 3, slot = lane & 7;
-    const uint8_t* asrc[A_CH / 4];
-    const uint8_t* bsrc[B_CH / 4];
-#pragma unroll
-    for (int i = 0; i < A_CH / 4; ++i) {
-        const int row = (w + 4 * i) * 8 + r8;
-        // rows past M: every lane of the chunk reads the same 16 bytes
-        asrc[i] = row < M ? A + (int64_t)row * lda + k0 + (slot ^ ((row >> 1) & 7)) * 16
-                          : A + (int64_t)(M - 1) * lda + k0;
-    }
-#pragma unroll
-    for (int i = 0; i < B_CH / 4; ++i) {
-        const int row = (w + 4 * i) * 8 + r8;
-        bsrc[i] = Bt + (int64_t)(n0 + row) * ldb + k0 + (slot ^ ((row >> 1) & 7)) * 16;
-    }
-    auto issue = [&](int kt) {
-        uint8_t* st = smem8 + (kt % NS) * TILE;
-        const int64_t ko = (int64_t)kt * BK8;
-#pragma unroll
-        for (int i = 0; i < A_CH / 4; ++i)
-            __builtin_amdgcn_global_load_lds((const void*)(asrc[i] + ko),
-                                             (__attribute__((address_space(3))) void*)(st + (w + 4 * i) * 1024), 16, 0, 0);
-#pragma unroll
-        for (int i = 0; i < B_CH / 4; ++i)
-            __builtin_amdgcn_global_load_lds((const void*)(bsrc[i] + ko),
-                                             (__attribute__((address_space(3))) void*)(st + BM * BK8 + (w + 4 * i) * 1024),
-                                             16, 0, 0);
-    };
-    f32x4 acc[2][NJ];
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    const int fr = lane & 15, fq = lane >> 4;
-#pragma unroll
-    for (int p = 0; p < NS - 1; ++p)
-        if (p < n) issue(p);
-    for (int kt = 0; kt < n; ++kt) {
-        wait_ahead<GPW, NS>(min(n - 1 - kt, NS - 2));
-        __builtin_amdgcn_s_barrier();
-        if (kt + NS - 1 < n) issue(kt + NS - 1);
-        const uint8_t* As = smem8 + (kt % NS) * TILE;
-        const uint8_t* Bs = As + BM * BK8;
-        {
-            i32x8 af[2], bfr[NJ];
-#pragma unroll
-            for (int i = 0; i < 2; ++i) af[i] = frag8x32(As, 32 * w + 16 * i + fr);
-#pragma unroll
-            for (int j = 0; j < NJ; ++j) bfr[j] = frag8x32(Bs, 16 * j + fr);
-#pragma unroll
-            for (int i = 0; i < 2; ++i)
-#pragma unroll
-                for (int j = 0; j < NJ; ++j) acc[i][j] = mfma_fp8_k128(af[i], bfr[j], acc[i][j]);
-        }
-    }
-#pragma unroll
-    for (int j = 0; j < NJ; ++j) {
-        const float sc = a_scale * b_scale[n0 + 16 * j + fr];
-#pragma unroll
-        for (int i = 0; i < 2; ++i)
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                const int row = 32 * w + 16 * i + fq * 4 + e;
-                if (row < M) {
-                    const float v = acc[i][j][e] * sc;
-                    if constexpr (CBF16) ((__hip_bfloat16*)Cv)[row * ldc + n0 + 16 * j + fr] = skr::to_bf16(v);
-                    else ((float*)Cv)[row * ldc + n0 + 16 * j + fr] = v;
-                }
-            }
-    }
-}
-
-template <int BN, int NS, bool CBF16>
-__global__ __launch_bounds__(256) void skinny_gemm_fp8v2_kernel(const uint8_t* __restrict__ A, int64_t lda,
-                                                                const uint8_t* __restrict__ Bt, int64_t ldb,
-                                                                const float* __restrict__ b_scale, float a_scale,
-                                                                void* __restrict__ C, int64_t ldc, int64_t c_slab,
-                                                                int M, int kslice) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem8[];
-    const int64_t co = blockIdx.y * c_slab;
-    glds_tile_fp8<BN, NS, CBF16>(A, lda, Bt, ldb, b_scale, a_scale,
-                                 CBF16 ? (void*)((__hip_bfloat16*)C + co) : (void*)((float*)C + co), ldc, M,
-                                 blockIdx.x * BN, (int64_t)blockIdx.y * kslice, kslice, smem8);
 }
 
 // fp32 operands (fp32 parity runs): the same LDS-DMA ring with K-tiles of
@@ -573,137 +347,3 @@ SKR_API int skr_skinny_gemm_f32(const void* A, int64_t lda, int64_t a_batch, con
 }
 
 SKR_API int skr_gemm_problem_size() { return (int)sizeof(GemmProblem); }
-
-// ---- fp8 v2 (inference): single product (optionally bf16 output) and grouped launch
-struct GemmProblem8 {
-    const void* A; int64_t lda;
-    const void* Bt; int64_t ldb;
-    const float* b_scale; float a_scale;
-    float* C; int64_t ldc; int64_t c_slab;
-    int M, N, K, splits;
-};
-
-namespace {
-struct GemmGroup8 {
-    GemmProblem8 p[kMaxGroup];
-    int start[kMaxGroup + 1];
-    int n;
-};
-
-template <int BN, int NS>
-__global__ __launch_bounds__(256) void skinny_gemm_group_fp8_kernel(const GemmGroup8 g) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem8[];
-    const int id = blockIdx.x;
-    int q = 0;
-#pragma unroll
-    for (int i = 1; i < kMaxGroup; ++i) q += (i < g.n && id >= g.start[i]) ? 1 : 0;
-    const GemmProblem8& p = g.p[q];
-    const TileIdx t = tile_idx(id - g.start[q], p.M, p.N, p.splits, BN);
-    const int kslice = p.K / p.splits;
-    glds_tile_fp8<BN, NS, false>((const uint8_t*)p.A + (int64_t)t.rb * BM * p.lda, p.lda, (const uint8_t*)p.Bt,
-                                 p.ldb, p.b_scale, p.a_scale, p.C + split_off(p, t), p.ldc, t.rows, t.nt * BN,
-                                 (int64_t)t.split * kslice, kslice, smem8);
-}
-
-constexpr int kNs8 = 3;
-
-template <typename K>
-void lds_attr_once(K kern, size_t lds) {
-    static bool done = false;
-    if (!done) {
-        (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        done = true;
-    }
-}
-
-int check8(const GemmProblem8& p) {
-    if (p.M < 1 || p.M > BM || p.N % 64 != 0 || p.splits < 1 || p.K % p.splits != 0) return -2;
-    if ((p.K / p.splits) % BK8 != 0 || p.lda % 16 != 0 || p.ldb % 16 != 0) return -3;
-    if (((uintptr_t)p.A | (uintptr_t)p.Bt) & 15) return -4;
-    return 0;
-}
-}  // namespace
-
-// C[s] = a_scale * b_scale[n] * A8[:, ks] . Bt8[:, ks]^T (fp32 slabs), or with
-// cbf16 one bf16 output (splits must be 1). 64-wide N tiles, 3-deep ring.
-SKR_API int skr_skinny_gemm_fp8_v2(const GemmProblem8* p, int cbf16, hipStream_t s) {
-    int rc = check8(*p);
-    if (rc) return rc;
-    if (cbf16 && p->splits != 1) return -2;
-    const dim3 grid(p->N / 64, p->splits);
-    const size_t lds = (size_t)kNs8 * (BM + 64) * BK8;
-    const int kslice = p->K / p->splits;
-    if (cbf16) {
-        auto k = skinny_gemm_fp8v2_kernel<64, kNs8, true>;
-        lds_attr_once(k, lds);
-        hipLaunchKernelGGL(k, grid, dim3(256), lds, s, (const uint8_t*)p->A, p->lda, (const uint8_t*)p->Bt, p->ldb,
-                           p->b_scale, p->a_scale, (void*)p->C, p->ldc, p->c_slab, p->M, kslice);
-    } else {
-        auto k = skinny_gemm_fp8v2_kernel<64, kNs8, false>;
-        lds_attr_once(k, lds);
-        hipLaunchKernelGGL(k, grid, dim3(256), lds, s, (const uint8_t*)p->A, p->lda, (const uint8_t*)p->Bt, p->ldb,
-                           p->b_scale, p->a_scale, (void*)p->C, p->ldc, p->c_slab, p->M, kslice);
-    }
-    return SKR_CHECK_LAUNCH();
-}
-
-SKR_API int skr_skinny_gemm_group_fp8(const GemmProblem8* probs, int n, hipStream_t s) {
-    if (n < 1 || n > kMaxGroup) return -2;
-    GemmGroup8 g{};
-    g.n = n;
-    g.start[0] = 0;
-    for (int i = 0; i < n; ++i) {
-        GemmProblem8 p1 = probs[i];
-        if (p1.M > BM && p1.M % BM != 0) return -2;
-        p1.M = min(p1.M, BM);                      // (row blocks: validated as one block)
-        const int rc = check8(p1);
-        if (rc) return rc;
-        g.p[i] = probs[i];
-        g.start[i + 1] = g.start[i] + (probs[i].N / 64) * probs[i].splits * row_blocks_of(probs[i].M);
-    }
-    for (int i = n + 1; i <= kMaxGroup; ++i) g.start[i] = g.start[n];
-    const size_t lds = (size_t)kNs8 * (BM + 64) * BK8;
-    auto k = skinny_gemm_group_fp8_kernel<64, kNs8>;
-    lds_attr_once(k, lds);
-    hipLaunchKernelGGL(k, dim3(g.start[n]), dim3(256), lds, s, g);
-    return SKR_CHECK_LAUNCH();
-}
-
-SKR_API int skr_gemm_problem8_size() { return (int)sizeof(GemmProblem8); }
-
-// fp8 e4m3 operands (bytes): C[z][s] = a_scale * b_scale[n] * A8[z][:, ks] . Bt8[z][:, ks]^T.
-// Requirements as skr_skinny_gemm_v2 with kslice % 128 == 0 and 16-byte aligned rows.
-SKR_API int skr_skinny_gemm_fp8(const void* A, int64_t lda, int64_t a_batch, const void* Bt, int64_t ldb,
-                                int64_t b_batch, const float* b_scale, int64_t bs_batch, float a_scale, float* C,
-                                int64_t ldc, int64_t c_slab, int64_t c_batch, int M, int N, int K, int splits,
-                                int batch, int bn, hipStream_t s) {
-    if (bn == 0) bn = (N % 128 == 0 && (N / 128) * splits * batch >= 144) ? 128 : 64;
-    if (M < 1 || M > BM || (bn != 64 && bn != 128) || N % bn != 0 || splits < 1 || K % splits != 0) return -2;
-    const int kslice = K / splits;
-    if (kslice % BK8 != 0 || lda % 16 != 0 || ldb % 16 != 0) return -3;
-    if (((uintptr_t)A | (uintptr_t)Bt) & 15) return -4;
-    const dim3 grid(N / bn, splits, batch);
-    const size_t lds = (size_t)NSTAGE * (BM + bn) * BK8;
-    if (bn == 128) {
-        static bool attr = false;
-        if (!attr) {
-            (void)hipFuncSetAttribute((const void*)skinny_gemm_fp8_kernel<128>,
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-            attr = true;
-        }
-        hipLaunchKernelGGL(skinny_gemm_fp8_kernel<128>, grid, dim3(256), lds, s, (const uint8_t*)A, lda, a_batch,
-                           (const uint8_t*)Bt, ldb, b_batch, b_scale, bs_batch, a_scale, C, ldc, c_slab, c_batch,
-                           M, kslice);
-    } else {
-        static bool attr = false;
-        if (!attr) {
-            (void)hipFuncSetAttribute((const void*)skinny_gemm_fp8_kernel<64>,
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-            attr = true;
-        }
-        hipLaunchKernelGGL(skinny_gemm_fp8_kernel<64>, grid, dim3(256), lds, s, (const uint8_t*)A, lda, a_batch,
-                           (const uint8_t*)Bt, ldb, b_batch, b_scale, bs_batch, a_scale, C, ldc, c_slab, c_batch,
-                           M, kslice);
-    }
-    return SKR_CHECK_LAUNCH();
-}

@@ -19,5 +19,4 @@ run ref_miopen_bf16  python scripts/bench_reference.py --cudnn --dtype bf16
 run sample_b128      python scripts/bench_sample.py --batch 128 --host-steps 20
 run sample_b256      python scripts/bench_sample.py --batch 256 --host-steps 20
 run sample_b1024     python scripts/bench_sample.py --batch 1024 --host-steps 20
-run sample_fp8_b256  python scripts/bench_sample.py --batch 256 --dtype fp8 --host-steps 5
 run decode_ref       python scripts/bench_decode.py

@@ -26,7 +26,7 @@ def main():
     ap.add_argument("--steps", type=int, default=250)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--temperature", type=float, default=0.5)
-    ap.add_argument("--dtype", default="bf16", choices=["fp32", "bf16", "fp8"])
+    ap.add_argument("--dtype", default="bf16", choices=["fp32", "bf16"])
     ap.add_argument("--host-steps", type=int, default=50, help="strokes timed for the host-loop comparator")
     a = ap.parse_args()
     import numpy as np

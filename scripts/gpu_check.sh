@@ -30,26 +30,11 @@ for s in "${steps[@]}"; do
         pytest) run pytest_gpu 900 python -u -m pytest tests -m gpu -q --maxfail=10 --timeout 300 --timeout-method thread ;;
         pytest_sel) run pytest_sel 600 python -u -m pytest tests -m gpu -v -x --timeout 240 --timeout-method thread -k "${PYTEST_K:-fused}" ;;
         pytest_file) run pytest_file 600 python -u -m pytest "${PYTEST_FILE:-tests/test_persist_gpu.py}" -m gpu -v -x --timeout 240 --timeout-method thread ;;
-        bench_stride1) SKR_WGRAD_CU_STRIDE=1 run bench_stride1 600 python bench.py --steps 10 --warmup 2 ;;
-        bench_stride2) SKR_WGRAD_CU_STRIDE=2 run bench_stride2 600 python bench.py --steps 10 --warmup 2 ;;
-        bench_stride8) SKR_WGRAD_CU_STRIDE=8 run bench_stride8 600 python bench.py --steps 10 --warmup 2 ;;
-        bench_noov) SKR_WGRAD_OVERLAP=0 run bench_noov 600 python bench.py --steps 10 --warmup 2 ;;
-        bench_ch50) SKR_WGRAD_CHUNK=50 run bench_ch50 600 python bench.py --steps 10 --warmup 2 ;;
         bench_env) run "bench_${BENCH_TAG:-env}" 600 python bench.py --steps 10 --warmup 2 ;;
-        bench_split2) SKR_DEC_SPLIT=2 run bench_split2 600 python bench.py --steps 10 --warmup 2 ;;
-        bench_split3) SKR_DEC_SPLIT=3 run bench_split3 600 python bench.py --steps 10 --warmup 2 ;;
-        prof_split2) SKR_DEC_SPLIT=2 run prof_split2 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_split2 -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --no-eval ;;
         bench_vae_miopen) run bench_vae_miopen 600 python scripts/bench_vae_miopen.py --config vae_small --dtype bf16 ;;
         bench_vae_miopen_fp32) run bench_vae_miopen_fp32 600 python scripts/bench_vae_miopen.py --config vae_small --dtype fp32 ;;
         cli_vae_train) run cli_vae_train 600 python -m sketch_rnn_amd.cli.vae_train --preset vae_large --synthetic 2000 --num_steps 80 --log_every 20 --save_every 0 --save_dir /tmp/skr_cli_vae --metrics gpurun_out/cli_vae_train_metrics.jsonl ;;
-        ab_xcd) SKR_PERSIST_XCD=0 run bench_xcd0 600 python bench.py --steps 20 --warmup 3 && SKR_PERSIST_XCD=1 run bench_xcd1 600 python bench.py --steps 20 --warmup 3 && SKR_PERSIST_XCD=0 run bench_xcd0b 600 python bench.py --steps 20 --warmup 3 && SKR_PERSIST_XCD=1 run bench_xcd1b 600 python bench.py --steps 20 --warmup 3 ;;
-        ab_xcd_ref) SKR_PERSIST_XCD=0 run ref_xcd0 600 python scripts/bench_reference.py --dtype bf16 && SKR_PERSIST_XCD=1 run ref_xcd1 600 python scripts/bench_reference.py --dtype bf16 ;;
         bench_dp1) run bench_dp1 600 python scripts/bench_dp1.py ;;
-        ab_hfuse) SKR_HYPER_FUSE=0 run bench_hf0 600 python bench.py --steps 20 --warmup 3 && SKR_HYPER_FUSE=1 run bench_hf1 600 python bench.py --steps 20 --warmup 3 && SKR_HYPER_FUSE=0 run bench_hf0b 600 python bench.py --steps 20 --warmup 3 && SKR_HYPER_FUSE=1 run bench_hf1b 600 python bench.py --steps 20 --warmup 3 ;;
-        ab_say) SKR_HYP_SAY=8 run bench_say8 600 python bench.py --steps 20 --warmup 3 && SKR_HYP_SAY=4 run bench_say4 600 python bench.py --steps 20 --warmup 3 && SKR_HYP_SAY=8 run bench_say8b 600 python bench.py --steps 20 --warmup 3 && SKR_HYP_SAY=4 run bench_say4b 600 python bench.py --steps 20 --warmup 3 ;;
-        ab_splits) run bench_def 600 python bench.py --steps 20 --warmup 3 && SKR_HYP_SH=16 run bench_sh16 600 python bench.py --steps 20 --warmup 3 && SKR_HYP_SY=2 run bench_sy2 600 python bench.py --steps 20 --warmup 3 && run bench_defb 600 python bench.py --steps 20 --warmup 3 && SKR_HYP_SH=16 run bench_sh16b 600 python bench.py --steps 20 --warmup 3 && SKR_HYP_SY=2 run bench_sy2b 600 python bench.py --steps 20 --warmup 3 ;;
-        ab_headdw) run bench_hd16 600 python bench.py --steps 20 --warmup 3 && SKR_HEAD_DW_SLABS=64 run bench_hd64 600 python bench.py --steps 20 --warmup 3 && SKR_HEAD_DW_SLABS=32 run bench_hd32 600 python bench.py --steps 20 --warmup 3 && run bench_hd16b 600 python bench.py --steps 20 --warmup 3 && SKR_HEAD_DW_SLABS=64 run bench_hd64b 600 python bench.py --steps 20 --warmup 3 && SKR_HEAD_DW_SLABS=32 run bench_hd32b 600 python bench.py --steps 20 --warmup 3 ;;
-        bench_nofused) SKR_FUSED=0 run bench_nofused 600 python bench.py --steps 10 --warmup 2 ;;
         bench_wgrad) run bench_wgrad 600 python scripts/bench_wgrad.py ;;
         bench_gemm) run bench_gemm 600 python scripts/bench_gemm.py ;;
         smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
@@ -61,24 +46,17 @@ for s in "${steps[@]}"; do
         bench_torch) run bench_torch 900 python bench.py --steps 3 --warmup 1 --backend torch --no-eval ;;
         bench_torch_small) run bench_torch_small 600 python bench.py --steps 3 --warmup 1 --backend torch --no-eval --config vae_small ;;
         bench_sample) run bench_sample 600 python scripts/bench_sample.py ;;
-        bench_sample_fp8) run bench_sample_fp8 600 python scripts/bench_sample.py --dtype fp8 ;;
         bench_sample_1k) run bench_sample_1k 600 python scripts/bench_sample.py --batch 1024 ;;
-        bench_sample_1k_fp8) run bench_sample_1k_fp8 600 python scripts/bench_sample.py --batch 1024 --dtype fp8 ;;
-        sample_ab) for bb in 128 1024; do for dt in bf16 fp8; do SKR_DECODE_FUSED=0 run sample_b${bb}_${dt}_f0 300 python scripts/bench_sample.py --batch $bb --dtype $dt --host-steps 2 && SKR_DECODE_FUSED=1 run sample_b${bb}_${dt}_f1 300 python scripts/bench_sample.py --batch $bb --dtype $dt --host-steps 2; done; done ;;
-        sample_f1) for bb in 128 1024; do for dt in bf16 fp8; do run sample_b${bb}_${dt}_f1 300 python scripts/bench_sample.py --batch $bb --dtype $dt --host-steps 2; done; done ;;
-        ab_group_bn) for bn in 64 128 64 128; do SKR_GROUP_BN=$bn run sample_b128_bn${bn} 300 python scripts/bench_sample.py --batch 128 --host-steps 2 && SKR_GROUP_BN=$bn run sample_b1024_bn${bn} 300 python scripts/bench_sample.py --batch 1024 --host-steps 2; done; SKR_GROUP_BN=128 run bench_bn128 600 python bench.py --steps 10 --warmup 2 ;;
-        fp8_gate) run fp8_gate 900 python scripts/fp8_gate.py ;;
+        sample_f1) for bb in 128 1024; do run sample_b${bb}_bf16 300 python scripts/bench_sample.py --batch $bb --host-steps 2; done ;;
         prof_small) run prof_small 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_small -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --no-eval --config vae_small ;;
         prof_ln) run prof_ln 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_ln -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --no-eval --config vae_layernorm ;;
         bench_wide_gemm) run bench_wide_gemm 300 python scripts/bench_wide_gemm.py ;;
         pmc_fetch) run pmc_fetch 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d gpurun_out/pmc_fetch -o run --output-format csv -- python bench.py --steps 1 --warmup 1 --no-eval ;;
         pmc_write) run pmc_write 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d gpurun_out/pmc_write -o run --output-format csv -- python bench.py --steps 1 --warmup 1 --no-eval ;;
-        converge_a) run converge_a 1100 python scripts/converge.py --config vae_large --steps 2000 --seeds 0,1 --arms hip-bf16,hip-fp32 --out gpurun_out/converge_large_r4.jsonl ;;
-        converge_b) run converge_b 1100 python scripts/converge.py --config vae_large --steps 2000 --seeds 2 --arms hip-bf16,hip-fp32 --out gpurun_out/converge_large_r4_s2.jsonl ;;
-        ab_persist_ln) SKR_PERSIST_LN=0 run bench_ln_ps0 600 python bench.py --steps 10 --warmup 2 --config vae_layernorm && SKR_PERSIST_LN=1 run bench_ln_ps1 600 python bench.py --steps 10 --warmup 2 --config vae_layernorm ;;
+        converge_a) run converge_a 1100 python scripts/converge.py --config vae_large --steps 2000 --seeds 0,1 --arms hip-bf16,hip-fp32 --out gpurun_out/converge_large_r5.jsonl ;;
+        converge_b) run converge_b 1100 python scripts/converge.py --config vae_large --steps 2000 --seeds 2 --arms hip-bf16,hip-fp32 --out gpurun_out/converge_large_r5_s2.jsonl ;;
         bench_b128) run bench_b128 600 python bench.py --steps 10 --warmup 2 --batch 128 ;;
         prof_sample_fused) run prof_sample_fused 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_sample_fused -o run --output-format csv -- python scripts/bench_sample.py --batch 128 --reps 1 --host-steps 2 ;;
-        prof_sample_fused8) run prof_sample_fused8 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_sample_fused8 -o run --output-format csv -- python scripts/bench_sample.py --batch 128 --reps 1 --host-steps 2 --dtype fp8 ;;
         bench_ref) run bench_ref 600 python scripts/bench_reference.py ;;
         bench_ref_bf16) run bench_ref_bf16 600 python scripts/bench_reference.py --dtype bf16 ;;
         bench_ref_torch) run bench_ref_torch 600 python scripts/bench_reference.py --backend torch --steps 5 ;;

@@ -131,7 +131,7 @@ class VAEConfig:
 @dataclass
 class RuntimeConfig:
     device: str = "cpu"
-    dtype: str = "fp32"              # fp32 | bf16 | fp8 (recurrent GEMM operand precision)
+    dtype: str = "fp32"              # fp32 | bf16 (recurrent GEMM operand precision)
     backend: str = "auto"            # auto | hip | torch
     cuda_graph: bool = True          # capture the train step into a HIP graph
     dp_bucket_mb: float = 32.0

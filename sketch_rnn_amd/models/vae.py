@@ -31,8 +31,8 @@ from ..ops.inproj import bilstm_input_proj, stroke_input_proj
 
 # dropout hash streams
 _S_ENC_FW, _S_ENC_BW, _S_DEC, _S_IN, _S_OUT, _S_EPS = 11, 13, 17, 23, 29, 31
-# SKR_LATENT_FUSED=0: the latent layer as separate torch ops (the oracle form)
-LATENT_FUSED = __import__("os").environ.get("SKR_LATENT_FUSED", "1") != "0"
+# False: the latent layer as separate torch ops (the oracle form; tests)
+LATENT_FUSED = True
 
 
 def _gaussian(shape, std, gen):

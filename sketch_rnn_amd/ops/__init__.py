@@ -21,10 +21,12 @@ _COMPUTE_DTYPE = "fp32"   # operand precision of the recurrent / head GEMMs on t
 
 
 def set_compute_dtype(name: str) -> None:
-    """``fp32`` | ``bf16`` | ``fp8``: operand precision of the GPU GEMMs.
-    Accumulation, cell state and all pointwise math stay fp32."""
+    """``fp32`` | ``bf16``: operand precision of the GPU GEMMs. Accumulation,
+    cell state and all pointwise math stay fp32. (No fp8: e4m3 recurrent
+    GEMMs were built and measured equal to bf16 on every decode shape --
+    README "fp8" -- and removed.)"""
     global _COMPUTE_DTYPE
-    if name not in ("fp32", "bf16", "fp8"):
+    if name not in ("fp32", "bf16"):
         raise ValueError(name)
     _COMPUTE_DTYPE = name
 

@@ -163,18 +163,6 @@ class PFwdLayer(C.Structure):
     ]
 
 
-class PLn(C.Structure):
-    """Mirror of ``PLn`` in csrc/lstm_persist.hip (LayerNorm-LSTM parameters, saves, exchange scratch)."""
-    _fields_ = [
-        ("g", _p), ("b", _p), ("gc", _p), ("bc", _p),
-        ("xhat", _p), ("rstd", _p), ("chat", _p),
-        ("lp", _i),
-        ("xs", _p),
-        ("dlny", _p), ("dlncy", _p),
-        ("fb", _f),
-    ]
-
-
 class PFwdArgs(C.Structure):
     _fields_ = [
         ("T", _i), ("B", _i), ("nd", _i), ("L", _i), ("H", _i), ("nrb", _i),
@@ -185,7 +173,6 @@ class PFwdArgs(C.Structure):
         ("flags", _p),
         ("err", _p),
         ("tlen", _p),
-        ("ln", PLn),
     ]
 
 
@@ -214,7 +201,6 @@ class PBwdArgs(C.Structure):
         ("flags", _p),
         ("err", _p),
         ("tlen", _p),
-        ("ln", PLn),
     ]
 
 
@@ -284,22 +270,11 @@ class ChainSync(C.Structure):
     _fields_ = [("counters", _p), ("n", _i), ("k", _i), ("err", _p)]
 
 
-class GemmProblem8(C.Structure):
-    """Mirror of ``GemmProblem8`` in csrc/skinny_gemm.hip (fp8 v2 products)."""
-    _fields_ = [
-        ("A", _p), ("lda", _i64),
-        ("Bt", _p), ("ldb", _i64),
-        ("b_scale", _p), ("a_scale", _f),
-        ("C", _p), ("ldc", _i64), ("c_slab", _i64),
-        ("M", _i), ("N", _i), ("K", _i), ("splits", _i),
-    ]
-
-
 class ModDecode(C.Structure):
     """Mirror of ``ModDecode`` in csrc/hyper_mod.hip (decode-mode inputs of the
-    HyperLSTM modulation kernel: fp32 hyper state, x-projection from the stroke)."""
+    HyperLSTM modulation kernel: the x-projection from the stroke)."""
     _fields_ = [
-        ("hh32", _p), ("x5", _p), ("w5", _p), ("ldw5", _i64), ("zp", _p), ("ldzp", _i64),
+        ("x5", _p), ("w5", _p), ("ldw5", _i64), ("zp", _p), ("ldzp", _i64),
     ]
 
 
@@ -353,9 +328,6 @@ class HipLib:
         lib.skr_skinny_gemm_f32.argtypes = [_p, _i64, _i64, _p, _i64, _i64, _p, _i64, _i64, _i64, _i, _i, _i, _i, _i,
                                              _p]
         lib.skr_skinny_gemm_f32.restype = _i
-        lib.skr_skinny_gemm_fp8.argtypes = [_p, _i64, _i64, _p, _i64, _i64, _p, _i64, _f, _p, _i64, _i64, _i64,
-                                             _i, _i, _i, _i, _i, _i, _p]
-        lib.skr_skinny_gemm_fp8.restype = _i
         lib.skr_mdn_sample.restype = _i
         lib.skr_mdn_sample_slabs.argtypes = [_p, _i64, _i, _i64, _p, _i, _i, _i, _f, _i, _i, _p, _u32, _i, _p, _i64,
                                              _p, _i64, _p, _p]
@@ -384,6 +356,10 @@ class HipLib:
         lib.skr_hyper_fold.restype = _i
         lib.skr_occupancy_hog.argtypes = [_i, _i, _i, _i, _p, _p]
         lib.skr_occupancy_hog.restype = _i
+        lib.skr_stream_create_cu_limited.argtypes = [_i, C.POINTER(C.c_void_p)]
+        lib.skr_stream_create_cu_limited.restype = _i
+        lib.skr_stream_destroy.argtypes = [_p]
+        lib.skr_stream_destroy.restype = _i
         lib.skr_gru_fwd.argtypes = [C.POINTER(GruFwdArgs), _i, _p]
         lib.skr_gru_fwd.restype = _i
         lib.skr_gru_bwd.argtypes = [C.POINTER(GruBwdArgs), _i, _p]
@@ -407,6 +383,8 @@ class HipLib:
         lib.skr_lstm_persist_fwd.restype = _i
         lib.skr_lstm_persist_bwd.argtypes = [C.POINTER(PBwdArgs), _p]
         lib.skr_lstm_persist_bwd.restype = _i
+        lib.skr_persist_set_spin_limit.argtypes = [C.c_uint]
+        lib.skr_persist_set_spin_limit.restype = _i
         lib.skr_mdn_head_fwd.argtypes = [C.POINTER(HeadFwd), _p, _p]
         lib.skr_mdn_head_fwd.restype = _i
         lib.skr_mdn_head_nblocks.argtypes = [_i64]
@@ -415,10 +393,6 @@ class HipLib:
         lib.skr_mdn_head_dx.restype = _i
         lib.skr_mdn_head_dw.argtypes = [C.POINTER(HeadDw), _i, _i, _p, _p, _p]
         lib.skr_mdn_head_dw.restype = _i
-        lib.skr_skinny_gemm_fp8_v2.argtypes = [C.POINTER(GemmProblem8), _i, _p]
-        lib.skr_skinny_gemm_fp8_v2.restype = _i
-        lib.skr_skinny_gemm_group_fp8.argtypes = [C.POINTER(GemmProblem8), _i, _p]
-        lib.skr_skinny_gemm_group_fp8.restype = _i
         lib.skr_hyper_mod_fwd.argtypes = [_p, _i64, _p, _p, _p, _p, _i64, _i, _p, _p, _p, _p, _i, _i, _i,
                                           C.POINTER(ModDecode), _p]
         lib.skr_hyper_mod_fwd.restype = _i
@@ -442,7 +416,6 @@ class HipLib:
                           ("skr_decode_ref_args_size", DecArgs),
                           ("skr_gemm_problem_size", GemmProblem),
                           ("skr_decode_sample_size", DecodeSample),
-                          ("skr_gemm_problem8_size", GemmProblem8),
                           ("skr_chain_sync_size", ChainSync)):
             fn = getattr(lib, name)
             fn.restype = _i

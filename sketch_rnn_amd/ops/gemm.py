@@ -1,12 +1,11 @@
-"""GEMM dispatch with a selectable operand precision (fp32 / bf16 / fp8).
+"""GEMM dispatch with a selectable operand precision (fp32 / bf16).
 
 Where each product runs (vae_large: no library GEMM in the profile,
 profiles/r3/vae_large_kernel_summary.txt):
 
 * per-time-step recurrent products (``h @ W_h``, the grouped HyperLSTM
   products, their backward twins): hand-written MFMA skinny split-K GEMMs,
-  ``csrc/skinny_gemm.hip`` (:func:`rec_gemm`, :func:`rec_gemm_group`, the
-  fp8 ``rec_gemm_fp8*`` variants);
+  ``csrc/skinny_gemm.hip`` (:func:`rec_gemm`, :func:`rec_gemm_group`);
 * long-K weight gradients over all T*B rows: ``csrc/wgrad_gemm.hip``
   (:func:`wgrad`; bf16, 256-multiple shapes);
 * small products (z-projections, hyper-norm factors): ``csrc/small_gemm.hip``
@@ -30,7 +29,7 @@ _BF16 = torch.bfloat16
 
 
 def lp_dtype() -> torch.dtype:
-    return _BF16 if get_compute_dtype() in ("bf16", "fp8") else torch.float32
+    return _BF16 if get_compute_dtype() == "bf16" else torch.float32
 
 
 def lp(t: torch.Tensor) -> torch.Tensor:
@@ -128,7 +127,7 @@ def _wgrad_hip_ok(a: torch.Tensor, b: torch.Tensor) -> bool:
             and a.data_ptr() % 16 == 0 and b.data_ptr() % 16 == 0)
 
 
-WGRAD_HIP = os.environ.get("SKR_WGRAD_HIP", "1") != "0"
+WGRAD_HIP = True   # False: hipBLASLt weight gradients (tests / A-B)
 
 
 def grad_slot(param: torch.Tensor, shape) -> Optional[torch.Tensor]:
@@ -227,8 +226,8 @@ def row_blocks(M: int) -> int:
 
 
 # fp32 operands (fp32 parity runs) through the fp32 MFMA skinny kernel
-# (csrc/skinny_gemm.hip skr_skinny_gemm_f32); SKR_GEMM_F32=0: library GEMMs.
-F32_GEMM = os.environ.get("SKR_GEMM_F32", "1") != "0"
+# (csrc/skinny_gemm.hip skr_skinny_gemm_f32); False: library GEMMs (tests).
+F32_GEMM = True
 
 
 def plan_splits(M: int, N: int, K: int, batch: int = 1, dtype: torch.dtype = _BF16, max_splits: int = 32) -> int:
@@ -309,8 +308,9 @@ def rec_gemm_bf16out(a: torch.Tensor, bt: torch.Tensor, out: torch.Tensor) -> to
 GROUPED = os.environ.get("SKR_GEMM_GROUP", "1") != "0"   # SKR_GEMM_GROUP=0: independent per-step products as separate launches
 
 
-# N-tile width of the grouped launch (0: the kernel's default, 64); tuning knob
-GROUP_BN = int(os.environ.get("SKR_GROUP_BN", "0"))
+# N-tile width of the grouped launch (0: the kernel's default, 64; 128: 8-wave
+# tiles, measured slower -- profiles/r5/bench_group.jsonl); sweeps set it
+GROUP_BN = 0
 
 
 def rec_gemm_group(jobs) -> None:
@@ -440,56 +440,6 @@ def derived(W, tag: str, fn):
     return v
 
 
-FP8_MAX = 448.0           # OCP e4m3
-FP8_ACT_SCALE = 64.0      # csrc/common.h kFp8ActScale: activations are stored x64
-
-
-def quantize_fp8_rows(bt: torch.Tensor):
-    """``bt [N, K]`` (B^T) -> ``(q uint8 [N, K] OCP e4m3, scale fp32 [N])`` with
-    one scale per output column: ``bt ~= q * scale[:, None]``."""
-    b = bt.float()
-    scale = (b.abs().amax(1) / FP8_MAX).clamp_min(1e-12)
-    q = (b / scale[:, None]).to(torch.float8_e4m3fn).view(torch.uint8).contiguous()
-    return q, scale.contiguous()
-
-
-def plan_splits_fp8(M: int, N: int, K: int, batch: int = 1, max_splits: int = 32) -> int:
-    """Split-K factor for :func:`rec_gemm_fp8` (K-tiles of 128); 0 = unusable."""
-    mb = row_blocks(M)
-    if mb == 0 or N % 64 or K % 128:
-        return 0
-    tiles = (N // 64) * batch * mb
-    best = 1
-    for s in _SPLITS:
-        if s > max_splits or (K // 128) % s:
-            continue
-        if tiles * s > 512:
-            break
-        best = s
-        if tiles * s >= 256:
-            break
-    return best
-
-
-def rec_gemm_fp8(a8: torch.Tensor, bq, out: torch.Tensor, splits: int, bn: int = 0) -> torch.Tensor:
-    """``sum_s out[s] = (a8 / 64) @ (q * scale)^T`` with fp8 operands:
-    ``a8 [M, K]`` uint8 activations (x64), ``bq = quantize_fp8_rows(B^T)``."""
-    from ..utils import native
-    lib = native.require_hip()
-    q, scale = bq
-    M, K = a8.shape[0], a8.shape[1]
-    N = q.shape[0]
-    mb = row_blocks(M)
-    rows = M if mb == 1 else 128
-    rc = lib.lib.skr_skinny_gemm_fp8(a8.data_ptr(), a8.stride(0), 128 * a8.stride(0), q.data_ptr(), q.stride(0), 0,
-                                     scale.data_ptr(), 0, 1.0 / FP8_ACT_SCALE, out.data_ptr(), N, out.stride(0),
-                                     128 * N, rows, N, K, max(splits, 1), mb, bn,
-                                     torch.cuda.current_stream().cuda_stream)
-    if rc != 0:
-        raise RuntimeError("skr_skinny_gemm_fp8 failed (%d) for M=%d N=%d K=%d S=%d" % (rc, M, N, K, splits))
-    return out
-
-
 def cast_transpose(W: torch.Tensor, plain: Optional[torch.Tensor] = None, trans: Optional[torch.Tensor] = None,
                    want_plain: bool = True, want_trans: bool = True):
     """fp32 ``W [..., R, C]`` -> bf16 ``W`` and bf16 ``W^T [..., C, R]`` in one
@@ -524,41 +474,6 @@ def cast_transpose(W: torch.Tensor, plain: Optional[torch.Tensor] = None, trans:
     if rc != 0:
         raise RuntimeError("skr_cast_transpose_bf16 failed (%d) for %s" % (rc, tuple(W.shape)))
     return plain, trans
-
-
-def _problem8(p, a8, bq, out, splits):
-    q, scale = bq
-    p.A, p.lda, p.Bt, p.ldb = a8.data_ptr(), a8.stride(0), q.data_ptr(), q.stride(0)
-    p.b_scale, p.a_scale = scale.data_ptr(), 1.0 / FP8_ACT_SCALE
-    p.C, p.ldc, p.c_slab = out.data_ptr(), out.stride(-2), out.stride(0) if out.dim() == 3 else 0
-    p.M, p.N, p.K, p.splits = a8.shape[0], q.shape[0], a8.shape[1], max(splits, 1)
-
-
-def rec_gemm_fp8_v2(a8: torch.Tensor, bq, out: torch.Tensor, splits: int) -> torch.Tensor:
-    """fp8 v2 ring (csrc/skinny_gemm.hip ``skr_skinny_gemm_fp8_v2``, M <= 128):
-    ``out [S, M, N]`` fp32 slabs, or ``out [M, N]`` bf16 (one slab)."""
-    from ..utils import native
-    from ._hipapi import GemmProblem8
-    lib = native.require_hip()
-    p = GemmProblem8()
-    _problem8(p, a8, bq, out, splits)
-    rc = lib.lib.skr_skinny_gemm_fp8_v2(p, int(out.dtype == _BF16), torch.cuda.current_stream().cuda_stream)
-    if rc != 0:
-        raise RuntimeError("skr_skinny_gemm_fp8_v2 failed (%d)" % rc)
-    return out
-
-
-def rec_gemm_fp8_group(jobs) -> None:
-    """Independent fp8 products ``(a8, bq, out [S, M, N] fp32, splits)`` in one launch."""
-    from ..utils import native
-    from ._hipapi import GemmProblem8
-    lib = native.require_hip()
-    probs = (GemmProblem8 * len(jobs))()
-    for p, (a8, bq, out, s) in zip(probs, jobs):
-        _problem8(p, a8, bq, out, s)
-    rc = lib.lib.skr_skinny_gemm_group_fp8(probs, len(jobs), torch.cuda.current_stream().cuda_stream)
-    if rc != 0:
-        raise RuntimeError("skr_skinny_gemm_group_fp8 failed (%d)" % rc)
 
 
 class _Linear(torch.autograd.Function):

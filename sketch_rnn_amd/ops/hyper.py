@@ -23,21 +23,22 @@ from ..utils import native
 from . import gemm
 from ._hipapi import LstmBwdArgs, LstmFwdArgs
 from .inproj import bproj_fwd, bproj_ok, bproj_reduce
-from .recurrent import (ROW_STATS, _cell_bwd, _cell_fwd, _check, _ClusterSync, _fp8_ok, _inference, _ln_saves_lp,
-                        _lp_kind, _ptr, _Saved, _seed_tensor, _stream, _to_fp8_act, cell_geometry)
+from .recurrent import (ROW_STATS, _cell_bwd, _cell_fwd, _check, _ClusterSync, _inference, _ln_saves_lp, _lp_kind,
+                        _ptr, _Saved, _seed_tensor, _stream, cell_geometry)
 from .reduce import colsum
 
 # The modulation GEMM fused with the main gates' pre-activations and
-# LayerNorm partial sums (csrc/hyper_mod.hip); SKR_HYPER_MOD=0 keeps the
-# plain bf16-output GEMM + the main cell's in-launch statistics exchange.
-HYPER_MOD = os.environ.get("SKR_HYPER_MOD", "1") != "0"
-HYPER_MAIN_C = int(os.environ.get("SKR_HYPER_MAIN_C", "0"))   # workgroups per row of the MOD-3 main cell (0: policy)
+# LayerNorm partial sums (csrc/hyper_mod.hip). False (tests / shapes it does
+# not take) keeps the plain bf16-output GEMM + the main cell's in-launch
+# statistics exchange.
+HYPER_MOD = True
+HYPER_MAIN_C = 0   # workgroups per row of the MOD-3 main cell (0: policy)
 # Backward step as [main cell] -> [dvec P^T] -> [hyper cell + dR_main W_h^T in
 # one launch, csrc/skinny_gemm.hip skr_skinny_gemm_group_cellbwd] -> [dR_hyp
 # W_y^T]: the hyper cell (one workgroup per row) runs beside the tiles of the
-# product only the next step reads. SKR_HYPER_BWD_FUSE=0 keeps [main cell] ->
-# [dR_main W_h^T + dvec P^T] -> [hyper cell] -> [dR_hyp W_y^T].
-HYPER_BWD_FUSE = os.environ.get("SKR_HYPER_BWD_FUSE", "1") != "0"
+# product only the next step reads. False (tests / shapes it does not take)
+# keeps [main cell] -> [dR_main W_h^T + dvec P^T] -> [hyper cell] -> [dR_hyp W_y^T].
+HYPER_BWD_FUSE = True
 # Chained backward launch (csrc/chain_step.hip): the main-cell backward rows
 # of step t run INSIDE the launch of step t + 1's dR_hyp W_y^T product (their
 # other loads issued before an in-launch wait on the product's tiles): three
@@ -58,10 +59,16 @@ CHAIN = os.environ.get("SKR_CHAIN", "1") != "0"
 # profiles/r3/hyper_fused_cell_ab.txt.)
 
 
-def _split_override(var: str, planned: int, K: int) -> int:
+# Split-K tuning knobs of the per-step products (sweeps set them from Python:
+# "sm" h W_h, "sy" [h | hh] W_y, "sh" dvec P^T, "sam" dR_main W_h^T, "say"
+# dR_hyp W_y^T); empty = the planned factors.
+SPLITS = {}
+
+
+def _split_override(name: str, planned: int, K: int) -> int:
     """Split-K factor of a per-step HyperLSTM product: the planned one, or
-    ``$var`` (tuning sweeps) when it divides K into whole 64-wide K tiles."""
-    v = int(os.environ.get(var, "0"))
+    ``SPLITS[name]`` when it divides K into whole 64-wide K tiles."""
+    v = int(SPLITS.get(name, 0))
     return v if v > 0 and planned > 0 and K % (64 * v) == 0 else planned
 
 
@@ -188,26 +195,17 @@ class _HyperSeq(torch.autograd.Function):
             WyT = Wyl.t().contiguous()           # [Gh, K]
             Pl, q = fold(W_z, b_z, W_a)          # B^T for the backward dvec @ P^T
             PlT = Pl.t().contiguous()            # B^T for the forward  hh @ P
-        fp8 = infer and _fp8_ok(B, G, H, Gh, K, 12 * H, Hh)
-        if fp8:
-            WhT = gemm.derived(WhT, "q8", gemm.quantize_fp8_rows)
-            WyT = gemm.derived(WyT, "q8", gemm.quantize_fp8_rows)
-            PlT = gemm.derived(PlT, "q8", gemm.quantize_fp8_rows)
-            S_m, S_y = gemm.plan_splits_fp8(B, G, H), gemm.plan_splits_fp8(B, Gh, K)
-            S_v = gemm.plan_splits_fp8(B, 12 * H, Hh, max_splits=1)
-        else:
-            S_m = _split_override("SKR_HYP_SM", gemm.plan_splits(B, G, H, 1, dt), H)
-            S_y = _split_override("SKR_HYP_SY", gemm.plan_splits(B, Gh, K, 1, dt), K)
-            S_v = gemm.plan_splits(B, 12 * H, Hh, 1, dt, max_splits=1)
-        rgemm = (lambda a, b, out, S: gemm.rec_gemm_fp8(a, b, out, S)) if fp8 else \
-            (lambda a, b, out, S: gemm.rec_gemm(a, b, out, S))
-        A = torch.empty(T + 1, B, K, device=dev, dtype=torch.uint8 if fp8 else dt)
-        A[0, :, :H].copy_(_to_fp8_act(h0) if fp8 else h0)
-        A[0, :, H:].copy_(_to_fp8_act(hh0) if fp8 else hh0)
+        S_m = _split_override("sm", gemm.plan_splits(B, G, H, 1, dt), H)
+        S_y = _split_override("sy", gemm.plan_splits(B, Gh, K, 1, dt), K)
+        S_v = gemm.plan_splits(B, 12 * H, Hh, 1, dt, max_splits=1)
+        rgemm = gemm.rec_gemm
+        A = torch.empty(T + 1, B, K, device=dev, dtype=dt)
+        A[0, :, :H].copy_(h0)
+        A[0, :, H:].copy_(hh0)
         # R_main: the backward re-reads it (the hyper-modulation gradient
         # dg * R) as the bf16 copy the main cell saves (RLP); with fp32 GEMM
         # operands the fp32 split-K slabs of every step are kept instead
-        vbf = not fp8 and dt == torch.bfloat16 and B <= 128 and S_v == 1
+        vbf = dt == torch.bfloat16 and B <= 128 and S_v == 1
         RLP = torch.empty(T, B, G, device=dev, dtype=torch.bfloat16) if (vbf and not infer) else None
         CC = torch.empty(T + 1, B, H, device=dev, dtype=f32)
         CC[0].copy_(c0)
@@ -279,7 +277,7 @@ class _HyperSeq(torch.autograd.Function):
         clm = _ClusterSync(T, B, H, dev, ln=mln_on, C=HYPER_MAIN_C if hmod else 0)
         clh = _ClusterSync(T, B, Hh, dev)
         st = _stream()
-        group = not fp8 and gemm.GROUPED and S_m >= 1 and S_y >= 1 and dt == torch.bfloat16
+        group = gemm.GROUPED and S_m >= 1 and S_y >= 1 and dt == torch.bfloat16
 
         def _main_saves(am, t):   # the backward's inputs from the main cell (none at inference)
             if infer:
@@ -362,15 +360,15 @@ class _HyperSeq(torch.autograd.Function):
             gemm.plan_splits(B, H, G, 1, ldt) >= 1
         # dvec P^T: the planned 32 splits also in the fused order (64 measured
         # 0.15 ms/step slower: 25.03 / 25.00 vs 24.83 / 24.88, profiles/r3/hyper_fused_cell_ab.txt)
-        S_h = _split_override("SKR_HYP_SH", gemm.plan_splits(B, Hh, 12 * H, 1, ldt), 12 * H)
-        S_am = _split_override("SKR_HYP_SAM", gemm.plan_splits(B, H, G, 1, ldt), G)
+        S_h = _split_override("sh", gemm.plan_splits(B, Hh, 12 * H, 1, ldt), 12 * H)
+        S_am = _split_override("sam", gemm.plan_splits(B, H, G, 1, ldt), G)
         # d[h | hh] = dR_hyp @ W_y^T: at most 4 split-K slabs -- the next step's
         # two cells read every slab; measured on MI355X (vae_large, same box,
         # A/B twice): 4 slabs 26.67 / 26.57 vs 8 (the plan) 26.76 / 26.86 ms/step
         S_ay = gemm.plan_splits(B, K, Gh, 1, ldt)
         if S_ay > 4:
             S_ay = next(d for d in (4, 3, 2, 1) if (Gh // 64) % d == 0)
-        S_ay = _split_override("SKR_HYP_SAY", S_ay, Gh)
+        S_ay = _split_override("say", S_ay, Gh)
         DHZ = torch.empty(max(S_h, 1), B, Hh, device=dev, dtype=f32)    # slabs of dhh from the vec path
         # dh slabs of step t + 1 read by step t; the last step reads none (null
         # sources) unless gradients flow into the final states

@@ -5,7 +5,6 @@ from __future__ import annotations
 
 import ctypes as C
 import math
-import os
 
 import torch
 
@@ -15,8 +14,7 @@ from ..utils import native
 # each workgroup's row loop is latency-bound, so more slabs = more loads in
 # flight. Measured on MI355X (vae_large, same box, A/B twice): 16 slabs
 # 26.72 / 26.65, 32 slabs 26.59 / 26.62, 64 slabs 26.62 / 26.62 ms/step.
-# SKR_HEAD_DW_SLABS overrides.
-HEAD_DW_SLABS = int(os.environ.get("SKR_HEAD_DW_SLABS", "32"))
+HEAD_DW_SLABS = 32
 
 
 def _stream() -> int:
@@ -74,7 +72,7 @@ def head_fused_ok(x: torch.Tensor, W: torch.Tensor, M: int) -> bool:
             and W.shape[0] % 128 == 0 and W.shape[1] == 3 + 6 * M)
 
 
-FUSED_HEAD = __import__("os").environ.get("SKR_FUSED_HEAD", "1") != "0"
+FUSED_HEAD = True   # False: the head GEMM + MDN loss as separate ops (tests)
 
 
 def _noutp(nout: int) -> int:

@@ -14,15 +14,14 @@ with bf16 MFMA operands and fp32 cell state, the reference's eoc state reset
 and the stateless recurrent-dropout hash. Weight gradients are formed after
 the scan as single long-K products over every saved step (``gemm.wgrad``).
 
-LayerNorm-LSTM layers (one layer, no eoc resets: the VAE's ``layer_norm``
-decoder and encoder) run the same way with the per-gate and cell LayerNorm
-row statistics exchanged between the workgroups of a row block twice per
-step each way (csrc/lstm_persist.hip ``ln_exchange``).
+Plain LSTM layers only: a LayerNorm-LSTM variant (both LayerNorms' row
+statistics exchanged in-launch) measured slower than the per-step clustered
+cells on vae_layernorm (11.50 vs 10.34 ms/step: each of the two exchanges
+per step is a ~6 us payload-drain + flag hop) and was removed in round 5.
 
 Dispatch: :func:`persist_ok` is the eligibility test (bf16 compute dtype,
 H in {256, 512}); ``SKR_PERSIST=0`` disables the path (the per-step fused
-kernels of :mod:`.recurrent` run instead); LayerNorm layers take it only
-with ``SKR_PERSIST_LN=1`` (measured slower, see ``PERSIST_LN``).
+kernels of :mod:`.recurrent` run instead).
 """
 from __future__ import annotations
 
@@ -35,13 +34,8 @@ import torch
 from ..utils import native
 from . import gemm
 from ._hipapi import PBwdArgs, PFwdArgs
-from .reduce import colsum
 
 PERSIST_ENABLED = os.environ.get("SKR_PERSIST", "1") != "0"
-# LayerNorm-LSTM layers too: opt-in -- measured slower than the per-step
-# clustered cells on vae_layernorm (11.50 vs 10.34 ms/step): each of the two
-# statistics exchanges per step costs ~6 us (payload drain + epoch flag hop)
-PERSIST_LN = os.environ.get("SKR_PERSIST_LN", "0") == "1"
 # debug: fill every handed-off buffer with NaN before the launch, so a read
 # that overtakes its hand-off shows up as a NaN instead of a stale value
 POISON = os.environ.get("SKR_PERSIST_POISON", "0") == "1"
@@ -60,7 +54,7 @@ def persist_ok(H: int, nd: int = 1, L: int = 1, ln: bool = False, B: Optional[in
     workgroup per CU, since every workgroup spin-waits on its peers (the
     launcher refuses a larger grid: -8). Callers fall back to the per-step
     kernels otherwise."""
-    if not PERSIST_ENABLED or (ln and (not PERSIST_LN or L != 1)) or gemm.lp_dtype() != torch.bfloat16:
+    if not PERSIST_ENABLED or ln or gemm.lp_dtype() != torch.bfloat16:
         return False
     if L == 2:
         shape_ok = nd == 1 and H == 256
@@ -86,19 +80,7 @@ class _Saved:
     pass
 
 
-def _ln_setup(args, ln, T, NB, nd, nrb, H, dev, lp):
-    """LayerNorm parameters ([nd, 4H] / [nd, H] fp32), the exchange scratch
-    and (forward) the saves, into ``args.ln``. Returns the tensors to keep."""
-    f32 = torch.float32
-    g, b, gc, bc = (t.detach().reshape(nd, -1).to(f32).contiguous() for t in ln)
-    xs = torch.empty(nd * nrb * 2 * (H // 16) * 32 * 8, device=dev, dtype=f32)
-    args.ln.g, args.ln.b, args.ln.gc, args.ln.bc = g.data_ptr(), b.data_ptr(), gc.data_ptr(), bc.data_ptr()
-    args.ln.xs, args.ln.lp = xs.data_ptr(), int(lp)
-    return [g, b, gc, bc, xs]
-
-
-def _fwd_launch(xp0, W_in1, b1, W_h0, W_h1, h0a, c0a, h0b, c0b, reset, seed, meta, tlen=None, last=False,
-                ln=None):
+def _fwd_launch(xp0, W_in1, b1, W_h0, W_h1, h0a, c0a, h0b, c0b, reset, seed, meta, tlen=None, last=False):
     """The forward launch of :class:`_PersistLSTM` (also used by
     :class:`_PersistBiEncoder`). ``last``: instead of the top layer's whole
     output sequence, write only h at each row's last valid step
@@ -130,20 +112,9 @@ def _fwd_launch(xp0, W_in1, b1, W_h0, W_h1, h0a, c0a, h0b, c0b, reset, seed, met
     a = PFwdArgs()
     a.T, a.B, a.nd, a.L, a.H, a.nrb = T, B, nd, L, H, nrb
     a.reset, a.forget_bias, a.seed = _ptr(rst), float(fb), sd.data_ptr()
-    # zeroed by the launcher: the h hand-off epochs (+ two LayerNorm phases)
-    flags = torch.empty(L * nd * nrb * 64 * (3 if ln is not None else 1), dtype=torch.int32, device=dev)
+    # zeroed by the launcher: the h hand-off epochs
+    flags = torch.empty(L * nd * nrb * 64, dtype=torch.int32, device=dev)
     a.flags, a.err = flags.data_ptr(), cluster_error_flag(dev).data_ptr()
-    s_ln = None
-    if ln is not None:
-        from .recurrent import _ln_saves_lp
-        lp = _ln_saves_lp(False)
-        sdt = torch.bfloat16 if lp else f32
-        keep_ln = _ln_setup(a, ln, T, NB, nd, nrb, H, dev, lp)
-        xhat = torch.empty(T, NB, G, device=dev, dtype=sdt)
-        rstd = torch.empty(T, NB, 5, device=dev, dtype=f32)
-        chat = torch.empty(T, NB, H, device=dev, dtype=sdt)
-        a.ln.xhat, a.ln.rstd, a.ln.chat, a.ln.fb = xhat.data_ptr(), rstd.data_ptr(), chat.data_ptr(), float(fb)
-        s_ln = dict(params=ln, keep=keep_ln, xhat=xhat, rstd=rstd, chat=chat, lp=lp)
     tl = tlen.to(device=dev, dtype=torch.int32).contiguous() if tlen is not None else None
     assert not last or (tl is not None and L == 1)
     a.tlen = _ptr(tl)
@@ -163,7 +134,7 @@ def _fwd_launch(xp0, W_in1, b1, W_h0, W_h1, h0a, c0a, h0b, c0b, reset, seed, met
         h_last = torch.empty(B, nd * H, dtype=f32, device=dev) if last else None   # [h_fw | h_bw] rows
         c_out = torch.empty(T, NB, H, dtype=f32, device=dev)
         c_carry = torch.empty(T + 1, NB, H, dtype=f32, device=dev) if rst is not None else None
-        act = torch.empty(T, NB, G, dtype=f32, device=dev) if ln is None else None   # (LN: xhat instead)
+        act = torch.empty(T, NB, G, dtype=f32, device=dev)
         hT = torch.empty(NB, H, dtype=f32, device=dev)
         cT = torch.empty(NB, H, dtype=f32, device=dev)
         ly.WT, ly.w_gs, ly.kin = WT[l].data_ptr(), (G * H if (l == 0 and nd > 1) else 0), (0 if l == 0 else H)
@@ -192,7 +163,6 @@ def _fwd_launch(xp0, W_in1, b1, W_h0, W_h1, h0a, c0a, h0b, c0b, reset, seed, met
     s.keep_flags = flags
     s.tlen = tl
     s.last = last
-    s.ln = s_ln
     return top, outs, s, (T, B, H, nrb)
 
 
@@ -209,17 +179,9 @@ def _bwd_launch(s, dims, dtop, dfinal, fp32_dg=True):
     b = PBwdArgs()
     b.T, b.B, b.nd, b.L, b.H, b.nrb = T, B, nd, L, H, nrb
     b.reset, b.seed = _ptr(s.rst), s.seed.data_ptr()
-    flags = torch.empty(L * nd * nrb * 64 * (3 if s.ln is not None else 1), dtype=torch.int32, device=dev)
+    flags = torch.empty(L * nd * nrb * 64, dtype=torch.int32, device=dev)
     b.flags, b.err = flags.data_ptr(), cluster_error_flag(dev).data_ptr()
     b.tlen = _ptr(s.tlen)
-    ln_keep = dlny = dlncy = None
-    if s.ln is not None:
-        ln_keep = _ln_setup(b, s.ln["params"], T, NB, nd, nrb, H, dev, s.ln["lp"])
-        sdt = s.ln["xhat"].dtype
-        dlny = torch.empty(T, NB, G, device=dev, dtype=sdt)
-        dlncy = torch.empty(T, NB, H, device=dev, dtype=sdt)
-        b.ln.xhat, b.ln.rstd, b.ln.chat = s.ln["xhat"].data_ptr(), s.ln["rstd"].data_ptr(), s.ln["chat"].data_ptr()
-        b.ln.dlny, b.ln.dlncy, b.ln.fb = dlny.data_ptr(), dlncy.data_ptr(), float(fb)
     dtop = dtop.contiguous() if dtop is not None else None
     dg_lp, dg, dh0, dc0, dih, dic, keep_alive = [], [], [], [], [], [], []
     for l in range(L):
@@ -271,15 +233,6 @@ def _bwd_launch(s, dims, dtop, dfinal, fp32_dg=True):
     # the eoc-reset targets are the initial states themselves
     dh0t = [dh0[l] + dih[l] if dih[l] is not None else dh0[l] for l in range(L)]
     dc0t = [dc0[l] + dic[l] if dic[l] is not None else dc0[l] for l in range(L)]
-    s.dln = None
-    if s.ln is not None:   # gamma / beta gradients: column sums over every (t, row) of each direction
-        from .reduce import colsum
-        out = []
-        for dy, xh, n in ((dlny, s.ln["xhat"], G), (dlncy, s.ln["chat"], H)):
-            parts = [colsum(dy.view(T, nd, B, n)[:, d], xh.view(T, nd, B, n)[:, d]) for d in range(nd)]
-            out += [torch.stack([p_[0] for p_ in parts]), torch.stack([p_[1] for p_ in parts])]
-        s.dln = out           # [dgamma, dbeta, dgamma_c, dbeta_c], each [nd, n]
-        del ln_keep
     return dg, dg_lp, dWh, dWin1, db1, dh0t, dc0t
 
 
@@ -292,26 +245,19 @@ class _PersistLSTM(torch.autograd.Function):
     carried ``(h, c)``."""
 
     @staticmethod
-    def forward(ctx, xp0, W_in1, b1, W_h0, W_h1, h0a, c0a, h0b, c0b, reset, seed, meta, tlen=None,
-                ln_g=None, ln_b=None, lnc_g=None, lnc_b=None):
-        ln = (ln_g, ln_b, lnc_g, lnc_b) if ln_g is not None else None
-        top, outs, s, dims = _fwd_launch(xp0, W_in1, b1, W_h0, W_h1, h0a, c0a, h0b, c0b, reset, seed, meta, tlen,
-                                         ln=ln)
+    def forward(ctx, xp0, W_in1, b1, W_h0, W_h1, h0a, c0a, h0b, c0b, reset, seed, meta, tlen=None):
+        top, outs, s, dims = _fwd_launch(xp0, W_in1, b1, W_h0, W_h1, h0a, c0a, h0b, c0b, reset, seed, meta, tlen)
         ctx.s, ctx.dims = s, dims
-        ctx.ln_shapes = [t.shape for t in ln] if ln is not None else None
         return (top, *outs)
 
     @staticmethod
     def backward(ctx, dtop, *dfinal):
         L = ctx.s.meta[0]
         dg, _, dWh, dWin1, db1, dh0t, dc0t = _bwd_launch(ctx.s, ctx.dims, dtop, dfinal)
-        dln = [None] * 4
-        if ctx.s.dln is not None:
-            dln = [d.reshape(shp) for d, shp in zip(ctx.s.dln, ctx.ln_shapes)]
         ctx.s = None
         return (dg[0], dWin1, db1, dWh[0], dWh[1] if L == 2 else None,
                 dh0t[0], dc0t[0], dh0t[1] if L == 2 else None, dc0t[1] if L == 2 else None,
-                None, None, None, None, *dln)
+                None, None, None, None)
 
 
 class _PersistBiEncoder(torch.autograd.Function):
@@ -377,14 +323,14 @@ def bilstm_last_ok(x, H: int, B: int) -> bool:
             and not x.requires_grad and persist_ok(H, 2, 1, ln=False, B=B))
 
 
-BI_ENCODER = os.environ.get("SKR_BI_ENCODER", "1") != "0"   # 0: projection + biLSTM + gather as separate ops
+BI_ENCODER = True   # False: projection + biLSTM + gather as separate ops (tests)
 
 
 def lstm_stack(xp0: torch.Tensor, W_h: Sequence[torch.Tensor], h0: Sequence[torch.Tensor],
                c0: Sequence[torch.Tensor], W_in1: Optional[torch.Tensor] = None, b1: Optional[torch.Tensor] = None,
                reset: Optional[torch.Tensor] = None, nd: int = 1, drop_keep: float = 1.0, drop_seed=0,
                drop_stream: int = 0, forget_bias: float = 1.0,
-               lengths: Optional[torch.Tensor] = None, ln=None) -> Tuple[torch.Tensor, List[Tuple]]:
+               lengths: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, List[Tuple]]:
     """Run ``len(W_h)`` (1 or 2) stacked LSTM layers over ``xp0`` in one
     persistent launch. Returns the top layer's outputs ``[T, nd*B, H]`` and
     the final carried ``(h, c)`` of every layer.
@@ -394,16 +340,12 @@ def lstm_stack(xp0: torch.Tensor, W_h: Sequence[torch.Tensor], h0: Sequence[torc
     32-row block stops after its longest row (TF ``dynamic_rnn`` with
     ``sequence_length`` skips those steps the same way). Outputs past a
     block's last step are zero and its final state is the one after that
-    step.
-
-    ``ln = (gamma [nd, 4H] | [4H], beta, gamma_c [nd, H] | [H], beta_c)``: a
-    LayerNorm-LSTM layer (one layer, no ``reset``)."""
+    step."""
     L = len(W_h)
-    assert ln is None or (L == 1 and reset is None)
     meta = (L, nd, float(drop_keep), int(drop_stream), float(forget_bias))
     if L == 2:
         outs = _PersistLSTM.apply(xp0, W_in1, b1, W_h[0], W_h[1], h0[0], c0[0], h0[1], c0[1], reset, drop_seed, meta)
         return outs[0], [(outs[1], outs[2]), (outs[3], outs[4])]
     outs = _PersistLSTM.apply(xp0, None, None, W_h[0], None, h0[0], c0[0], None, None, reset, drop_seed, meta,
-                              lengths, *(ln if ln is not None else (None,) * 4))
+                              lengths)
     return outs[0], [(outs[1], outs[2])]

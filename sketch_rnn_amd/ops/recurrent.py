@@ -61,31 +61,16 @@ def _seed_tensor(seed, device) -> torch.Tensor:
 
 
 def _lp_kind(t: torch.Tensor) -> int:
-    """GEMM-operand encoding written by the cell kernels: 1 bf16, 2 fp32, 3 fp8 e4m3 (x64)."""
-    if t.dtype == torch.uint8:
-        return 3
+    """GEMM-operand encoding written by the cell kernels: 1 bf16, 2 fp32."""
     return 1 if t.dtype == torch.bfloat16 else 2
-
-
-def _fp8_ok(M: int, *nk) -> bool:
-    """fp8 recurrent GEMMs (inference only): compute dtype 'fp8' and every
-    (N, K) pair of the step tileable by the fp8 kernel."""
-    from . import get_compute_dtype
-    if get_compute_dtype() != "fp8":
-        return False
-    return all(gemm.plan_splits_fp8(M, n, k) > 0 for n, k in zip(nk[::2], nk[1::2]))
 
 
 def _inference(*ts) -> bool:
     """True when no backward will run (grad mode off or nothing requires
-    grad): weights are then static, so derived copies are cached and fp8
-    GEMMs are allowed. Evaluated outside the autograd Function, whose
+    grad): weights are then static, so derived copies are cached.
+    Evaluated outside the autograd Function, whose
     forward always runs with grad mode off."""
     return not (torch.is_grad_enabled() and any(t is not None and t.requires_grad for t in ts))
-
-
-def _to_fp8_act(h: torch.Tensor) -> torch.Tensor:
-    return (h.float() * gemm.FP8_ACT_SCALE).to(torch.float8_e4m3fn).view(torch.uint8)
 
 
 class _Saved:
@@ -96,9 +81,9 @@ class _Saved:
 # A row of H hidden units runs on C workgroups (C == 1 and H > 256: one
 # 1024-thread workgroup per row). Policy: 256-unit workgroups (measured
 # fastest at H = 2048 with LayerNorm by the round-2 cell bench, despite the
-# in-launch exchange). SKR_CELL_C overrides C; SKR_CLUSTER=0 forces C = 1.
+# in-launch exchange). CELL_C > 0 overrides C (sweeps); SKR_CLUSTER=0 forces C = 1.
 CLUSTER_ENABLED = os.environ.get("SKR_CLUSTER", "1") != "0"
-CELL_C = int(os.environ.get("SKR_CELL_C", "0"))
+CELL_C = 0
 _ERR_FLAGS = {}
 
 
@@ -222,8 +207,8 @@ def _cell_bwd(lib, a, ln: bool, mod: int, st: int, what: str) -> None:
 FUSED_ENABLED = os.environ.get("SKR_FUSED", "1") != "0"
 
 
-def _fused_ok(H: int, ln: bool, fp8: bool, ldt) -> bool:
-    return FUSED_ENABLED and not ln and not fp8 and ldt == torch.bfloat16 and H in (256, 512)
+def _fused_ok(H: int, ln: bool, ldt) -> bool:
+    return FUSED_ENABLED and not ln and ldt == torch.bfloat16 and H in (256, 512)
 
 
 # =====================================================================================
@@ -241,7 +226,6 @@ class _LSTMSeq(torch.autograd.Function):
         ln = ln_g is not None
         xp = xp.contiguous()
         Bg = BB // nd
-        fp8 = infer and _fp8_ok(Bg, G, H) and nd == 1
         ldt = gemm.lp_dtype()
         if infer and nd == 1:   # (nd > 1: W_h is a per-call stack of the directions -- nothing to cache)
             Wl = None
@@ -249,17 +233,13 @@ class _LSTMSeq(torch.autograd.Function):
         else:
             Wl = gemm.lp(W_h.reshape(nd, H, G)).contiguous()   # B^T of the backward product dG @ W^T
             WlT = Wl.transpose(1, 2).contiguous()              # B^T of the forward product h @ W
-        if fp8:
-            WQ = gemm.derived(W_h, "lstm_fp8", lambda W: gemm.quantize_fp8_rows(W.reshape(H, G).t()))
-            S = gemm.plan_splits_fp8(Bg, G, H)
-        else:
-            S = gemm.plan_splits(Bg, G, H, nd, ldt)
-        A = torch.empty(T + 1, BB, H, device=dev, dtype=torch.uint8 if fp8 else ldt)   # GEMM operands: carried h
-        A[0].copy_(_to_fp8_act(h0) if fp8 else h0)
+        S = gemm.plan_splits(Bg, G, H, nd, ldt)
+        A = torch.empty(T + 1, BB, H, device=dev, dtype=ldt)   # GEMM operands: carried h
+        A[0].copy_(h0)
         CC = torch.empty(T + 1, BB, H, device=dev, dtype=f32)  # carried c
         CC[0].copy_(c0)
         Hout = torch.empty(T, BB, H, device=dev, dtype=f32)
-        fused = _fused_ok(H, ln, fp8, ldt)
+        fused = _fused_ok(H, ln, ldt)
         # saves for the backward: LN layers keep xhat / rstd / chat (the kernel
         # recomputes the gate activations from xhat); plain layers keep act and
         # c'. Nothing is saved at inference (the fused kernel always writes them).
@@ -312,10 +292,7 @@ class _LSTMSeq(torch.autograd.Function):
         cl = _ClusterSync(T, BB, H, dev, ln)
         for t in range(T_loop):
             cl.set(a, t)
-            if fp8:
-                gemm.rec_gemm_fp8(A[t], WQ, R, S)
-            else:
-                gemm.rec_gemm(A[t], WlT, R, S, nd)
+            gemm.rec_gemm(A[t], WlT, R, S, nd)
             a.xp = xp[t].data_ptr()
             a.c_prev = CC[t].data_ptr()
             a.reset = _ptr(rst[t]) if rst is not None else None
@@ -380,7 +357,7 @@ class _LSTMSeq(torch.autograd.Function):
         a.ld_dG, a.ld_dG_lp, a.dG_lp_kind = G, G, 1 if lp_on else 0
         a.dinit_h, a.dinit_c = _ptr(dinit_h), _ptr(dinit_c)
         st = _stream()
-        if lp_on and _fused_ok(H, ln, False, s.Wl.dtype):
+        if lp_on and _fused_ok(H, ln, s.Wl.dtype):
             # one launch per step: dh_rec = dG_{t+1} @ W^T fused with the cell backward
             f = FusedBwdArgs()
             f.B, f.H, f.nd = B, H, nd
@@ -446,14 +423,13 @@ def lstm_sequence_hip(xp, W_h, h0, c0, forget_bias=1.0, reset=None, reset_h=None
         raise ValueError("reset requires reset_h / reset_c")
     from . import persist
     lnp = ln[0] is not None
-    if (reset is None and xp.shape[0] > 1 and not _inference(xp, W_h, h0, c0, *(ln if lnp else ()))
-            and persist.persist_ok(W_h.shape[0], 1, 1, ln=lnp, B=xp.shape[1])):
-        # a layer in training (the vae_small / vae_layernorm decoders): the whole
+    if (reset is None and xp.shape[0] > 1 and not lnp and not _inference(xp, W_h, h0, c0)
+            and persist.persist_ok(W_h.shape[0], 1, 1, B=xp.shape[1])):
+        # a plain layer in training (the vae_small decoder): the whole
         # sequence, forward and backward, as one persistent launch each
-        # (csrc/lstm_persist.hip; LayerNorm statistics exchanged in-launch)
+        # (csrc/lstm_persist.hip)
         Hout, fin = persist.lstm_stack(xp, [W_h], [h0], [c0], drop_keep=drop_keep, drop_seed=drop_seed,
-                                       drop_stream=drop_stream, forget_bias=forget_bias,
-                                       ln=ln if lnp else None)
+                                       drop_stream=drop_stream, forget_bias=forget_bias)
         return Hout, fin[0]
     Hout, hT, cT = _LSTMSeq.apply(xp, W_h, h0, c0, reset_h, reset_c, *ln, reset, drop_seed,
                                   (float(forget_bias), float(drop_keep), int(drop_stream), 1,
@@ -482,12 +458,11 @@ def bilstm_sequence_packed_hip(xp, W_f, W_b, h0, c0, drop_keep=1.0, drop_seed=0,
     h = torch.cat([h0, h0], 0)
     c = torch.cat([c0, c0], 0)
     from . import persist
-    if persist.persist_ok(W_f.shape[0], 2, 1, ln=ln_f is not None, B=B):
+    if ln_f is None and persist.persist_ok(W_f.shape[0], 2, 1, B=B):
         # both directions, every step, one persistent launch (csrc/lstm_persist.hip)
-        lnp = tuple(torch.stack([a, b], 0) for a, b in zip(ln_f, ln_b)) if ln_f is not None else None
         Hout, _ = persist.lstm_stack(xp, [W], [h], [c], nd=2, drop_keep=drop_keep, drop_seed=drop_seed,
                                      drop_stream=streams[0], forget_bias=forget_bias,
-                                     lengths=lengths if PERSIST_LENGTHS else None, ln=lnp)
+                                     lengths=lengths if PERSIST_LENGTHS else None)
         return Hout[:, :B], Hout[:, B:]
     if ln_f is not None:
         ln = tuple(torch.stack([a, b], 0) for a, b in zip(ln_f, ln_b))
@@ -499,17 +474,17 @@ def bilstm_sequence_packed_hip(xp, W_f, W_b, h0, c0, drop_keep=1.0, drop_seed=0,
     return Hout[:, :B], Hout[:, B:]
 
 
-# Length-bounded persistent encoder (SKR_PERSIST_LENGTHS=0 runs every row
-# block for all T steps).
-PERSIST_LENGTHS = os.environ.get("SKR_PERSIST_LENGTHS", "1") != "0"
+# Length-bounded persistent encoder (False: every row block runs all T steps;
+# the equivalence tests compare the two).
+PERSIST_LENGTHS = True
 
 
 # LayerNorm saves (xhat, chat and their gradients dlny / dlncy) in bf16 in
 # bf16 training: half the bytes of the cells' saves and of the gamma / beta
 # reductions (csrc/lstm_args.h save_lp; the forward runs on fp32 values, the
 # backward recomputes the gate activations from the bf16 save, like any bf16
-# activation save). SKR_LN_SAVES_LP=0 keeps them fp32.
-LN_SAVES_LP = os.environ.get("SKR_LN_SAVES_LP", "1") != "0"
+# activation save). False keeps them fp32 (tests).
+LN_SAVES_LP = True
 
 
 def _ln_saves_lp(infer: bool) -> bool:

@@ -3,27 +3,14 @@
 
 The generic path (``SketchVAE.decode_step``) runs a whole T = 1 sequence per
 stroke: per-call state copies into the operand buffers, zero fills, the
-``z`` projections, a library head GEMM -- 20+ launches, ~60 % of them glue
-(rocprofv3: 0.169 ms per step at B = 256, 28 us of it ``copyBuffer``). Here
-the decoder state lives in place for the whole decode, the per-sketch
-constants (``z`` projections) are computed once, and a stroke is exactly
-seven kernels, all hand-written:
-
-1. ``bproj``: ``[x | z] @ [W_x; hW_x]`` for the main and hyper gates at once
-   (stroke rows only; the z rows are a per-sketch constant);
-2. grouped skinny MFMA GEMM: ``h @ W_h`` and ``[h | hh] @ W_y``;
-3. hyper LayerNorm cell (writes ``hh`` in bf16 straight into the operand
-   buffer, ``c`` in place);
-4. modulation vectors ``hh @ P`` (bf16 out);
-5. main LayerNorm + modulation cell (``h`` into the operand buffer);
-6. head ``h @ W_out`` as a skinny split-K GEMM on the bf16 ``h`` operand;
-7. device sampler folding the head's split-K slabs + bias, writing the next
-   input.
-
-Rows are processed in chunks of at most 128 (one MFMA row tile).
+``z`` projections, a library head GEMM -- 20+ launches, ~60 % of them glue.
+Here the decoder state lives in place for the whole decode, the per-sketch
+constants (``z`` projections) are computed once, and every launch is a
+hand-written kernel.
 
 Four-launch stroke (:meth:`HyperStepDecoder.step_fused`, the
-:class:`~.sampler.GraphDecoder` path when ``hyper_num_units == 256``):
+:class:`~.sampler.GraphDecoder` path whenever ``hyper_num_units == 256``,
+embedding <= 32, ``dec_rnn_size % 32 == 0``):
 
 1. grouped skinny GEMM ``{h W_h, [h | hh] W_y, h W_out}`` -- the head of the
    PREVIOUS stroke's ``h`` rides in the step's own GEMM launch;
@@ -37,17 +24,20 @@ Four-launch stroke (:meth:`HyperStepDecoder.step_fused`, the
    partial sums;
 4. the main LayerNorm cell (MOD 3: pre-activations precomputed).
 
-After the last stroke :meth:`finish` runs the head GEMM + sampler once.
+After the last stroke :meth:`finish` runs the head GEMM + sampler once. Up to
+1024 rows run as ONE decoder (128-row MFMA blocks inside each launch).
 
-Compute dtype ``fp8`` (BASELINE config 5): the four GEMMs run on OCP e4m3
-operands (``v_mfma_f32_16x16x32_fp8_fp8``, per-output-column weight scales;
-the cells write the bf16-free operand buffer as e4m3 x 64 -- |h| <= 1, so a
-static scale maps it onto [-64, 64] with subnormals down to ~3e-5).
+Other hyper widths take :meth:`HyperStepDecoder.step` (seven launches:
+stroke projection, grouped GEMM, hyper cell, ``hh P`` GEMM, main cell, head
+GEMM, sampler) on chunks of at most 128 rows.
+
+All GEMMs take bf16 operands with fp32 accumulation. (e4m3 operands on
+gfx950's block-scaled MFMA were built and measured at 1.00-1.01x of bf16 on
+this latency-bound step at B = 128 .. 1024, then removed: README "fp8".)
 """
 from __future__ import annotations
 
 import ctypes
-import os
 
 import torch
 
@@ -64,7 +54,7 @@ def hyper_step_ok(model, B: int) -> bool:
     if next(model.parameters()).device.type != "cuda" or gemm.lp_dtype() != torch.bfloat16:
         return False
     from ..ops import get_compute_dtype
-    if get_compute_dtype() not in ("bf16", "fp8") or not model.dec.use_layer_norm:
+    if get_compute_dtype() != "bf16" or not model.dec.use_layer_norm:
         return False
     H, Hh = cfg.dec_rnn_size, cfg.hyper_num_units
     if B > 128 and not (wide_ok(model) and B % 128 == 0 and B <= 1024):
@@ -77,14 +67,13 @@ def wide_ok(model) -> bool:
     instead of 128-row chunks on concurrent streams: the four-launch stroke's
     shape limits (:class:`HyperStepDecoder` ``fused``)."""
     cfg = model.cfg
-    return (WIDE and cfg.hyper_num_units == 256 and cfg.hyper_embedding_size <= 32 and cfg.dec_rnn_size % 32 == 0
-            and os.environ.get("SKR_DECODE_FUSED", "1") != "0")
+    return WIDE and cfg.hyper_num_units == 256 and cfg.hyper_embedding_size <= 32 and cfg.dec_rnn_size % 32 == 0
 
 
-WIDE = os.environ.get("SKR_WIDE_DECODE", "1") != "0"
-# h W_h of the wide decoder on hipBLASLt: opt-in (SKR_WIDE_LIB_MAIN=1), not
-# yet measured end to end -- the default is the skinny kernel's row blocks
-LIB_MAIN = os.environ.get("SKR_WIDE_LIB_MAIN", "0") == "1"
+WIDE = True   # one decoder over B > 128 rows (False: tests of the 128-row chunked decoders)
+
+
+FUSED = True   # four-launch stroke where its shape limits allow (False: tests of the seven-launch step)
 
 
 class HyperStepDecoder:
@@ -105,35 +94,20 @@ class HyperStepDecoder:
         self.nout = 3 + 6 * self.M
         self.E = p.embed
         bf, f32 = torch.bfloat16, torch.float32
-        from ..ops import get_compute_dtype
-        self.fp8 = get_compute_dtype() == "fp8"
-        if self.fp8:
-            self.S_m = gemm.plan_splits_fp8(B, G, H)
-            self.S_y = gemm.plan_splits_fp8(B, Gh, K)
-            self.S_o = gemm.plan_splits_fp8(B, 128, H)
-        else:
-            self.S_m = gemm.plan_splits(B, G, H, 1, bf)
-            self.S_y = gemm.plan_splits(B, Gh, K, 1, bf)
-            self.S_o = gemm.plan_splits(B, 128, H, 1, bf)
+        self.S_m = gemm.plan_splits(B, G, H, 1, bf)
+        self.S_y = gemm.plan_splits(B, Gh, K, 1, bf)
+        self.S_o = gemm.plan_splits(B, 128, H, 1, bf)
         assert min(self.S_m, self.S_y, self.S_o) >= 1
         # four-launch stroke (step_fused): hyper_mod's shape limits (Hh == 256,
         # E <= 32, 32-unit tiles, <= 4 main-GEMM slabs)
-        self.fused = Hh == 256 and self.E <= 32 and H % 32 == 0 and \
-            os.environ.get("SKR_DECODE_FUSED", "1") != "0"
-        # wide decoder (B > 128): h @ W_h, [B, H] x [H, 4H], is a plain library-
-        # sized GEMM -- hipBLASLt (bf16, or e4m3 with per-tensor scales) beats
-        # the skinny kernel's row blocks there (scripts/bench_wide_gemm.py:
-        # 39.7 / 21.0 vs 49.7 us at B = 1024)
-        self.lib_main = self.fused and B > 128 and LIB_MAIN
-        if self.lib_main:
-            self.S_m = 1
+        self.fused = FUSED and Hh == 256 and self.E <= 32 and H % 32 == 0
         if self.fused:
             self.S_m = 4 if self.S_m >= 4 else 2 if self.S_m >= 2 else 1
             self.X = torch.zeros(B, 5, dtype=f32, device=device)
             self.GP = torch.empty(B, G, dtype=f32, device=device)
             self.GS = torch.empty(B, 4, H // 32, 2, dtype=f32, device=device)
         # state / operand buffers (resident for the whole decode)
-        self.A = torch.zeros(B, K, dtype=torch.uint8 if self.fp8 else bf, device=device)   # [h | hh] GEMM operand
+        self.A = torch.zeros(B, K, dtype=bf, device=device)   # [h | hh] GEMM operand
         self.CC = torch.zeros(B, H, dtype=f32, device=device)
         self.HCC = torch.zeros(B, Hh, dtype=f32, device=device)
         self.Hout = torch.empty(B, H, dtype=f32, device=device)
@@ -188,27 +162,13 @@ class HyperStepDecoder:
                 return qb.reshape(12 * H).float().contiguous()
             w["PL"] = P
             w["QB"] = gemm.derived((q, p.bias), "hypQB", qbias)
-        if self.lib_main:   # W_h for the library GEMM: [H, 4H] bf16, or e4m3 [4H, H] (column-major B) + scale
-            if self.fp8:
-                def q8t(W):
-                    sc = (W.detach().abs().amax().float() / gemm.FP8_MAX).clamp_min(1e-12)
-                    return (W.detach().t().float() / sc).to(torch.float8_e4m3fn).contiguous(), sc.reshape(())
-                w["WhL"] = gemm.derived(p.W_h, "hypWh8t", q8t)
-                w["sa8"] = gemm.derived(p.W_h, "fp8act", lambda W: torch.full((), 1.0 / gemm.FP8_ACT_SCALE,
-                                                                              device=W.device))
-            else:
-                w["WhL"] = gemm.derived(p.W_h, "hypWhL", lambda W: W.detach().to(torch.bfloat16).contiguous())
-        if self.fp8:   # per-output-column e4m3 weights
-            w["WhT"] = gemm.derived(w["WhT"], "q8", gemm.quantize_fp8_rows)
-            w["WyT"] = gemm.derived(w["WyT"], "q8", gemm.quantize_fp8_rows)
-            w["WoT"] = gemm.derived(w["WoT"], "q8", gemm.quantize_fp8_rows)
         return w
 
     def _pq(self):
         """Folded modulation weights (P^T, q) of the seven-launch :meth:`step`."""
         if "PQ" not in self._w:
             P, q = self._fold()
-            self._w["PQ"] = (gemm.derived(P, "q8", gemm.quantize_fp8_rows) if self.fp8 else P, q)
+            self._w["PQ"] = (P, q)
         return self._w["PQ"]
 
     @torch.no_grad()
@@ -223,22 +183,6 @@ class HyperStepDecoder:
             # forked chunk stream would otherwise find another chunk's P in
             # gemm.derived's global cache before that stream has written it
             self._pq()
-        if self.lib_main and self.fp8 and not getattr(self, "_probed", False):
-            # the e4m3 library GEMM must take this shape / layout (probed once,
-            # eagerly, before any graph capture); otherwise the skinny fp8 kernel
-            # runs h W_h in 128-row blocks
-            self._probed = True
-            try:
-                W8t, sb = self._w["WhL"]
-                torch._scaled_mm(self.A[:, :self.H].view(torch.float8_e4m3fn), W8t.t(), scale_a=self._w["sa8"],
-                                 scale_b=sb, out_dtype=torch.float32, out=self.RM[0])
-                torch.cuda.current_stream().synchronize()
-            except (RuntimeError, TypeError):
-                self.lib_main = False
-                self.S_m = min(4, max(1, gemm.plan_splits_fp8(self.B, self.G, self.H)))
-                self.S_m = 4 if self.S_m >= 4 else 2 if self.S_m >= 2 else 1
-                self.RM = torch.empty(self.S_m, self.B, self.G, dtype=torch.float32, device=self.dev)
-                self._w = self._weights()
 
     @torch.no_grad()
     def begin(self, zc, state, x0=None) -> None:
@@ -249,13 +193,8 @@ class HyperStepDecoder:
         p = self.model.dec
         H = self.H
         h0, c0, hh0, hc0 = state
-        if self.fp8:
-            from ..ops.recurrent import _to_fp8_act
-            self.A[:, :H].copy_(_to_fp8_act(h0))
-            self.A[:, H:].copy_(_to_fp8_act(hh0))
-        else:
-            self.A[:, :H].copy_(h0)
-            self.A[:, H:].copy_(hh0)
+        self.A[:, :H].copy_(h0)
+        self.A[:, H:].copy_(hh0)
         self.CC.copy_(c0)
         self.HCC.copy_(hc0)
         if zc is not None:
@@ -283,8 +222,7 @@ class HyperStepDecoder:
         ah.forget_bias, ah.keep = 1.0, 1.0
         ah.seed, ah.stream, ah.step = self.sd.data_ptr(), 1, t
         ah.c_prev, ah.c_carry, ah.h_out = self.HCC.data_ptr(), self.HCC.data_ptr(), self.HH.data_ptr()
-        lpk = 3 if self.fp8 else 1
-        ah.h_lp, ah.ld_lp, ah.lp_kind = self.A[:, H:].data_ptr(), K, lpk
+        ah.h_lp, ah.ld_lp, ah.lp_kind = self.A[:, H:].data_ptr(), K, 1
         self.clh.set(ah, t)
         am = LstmFwdArgs()
         am.B, am.H = B, H
@@ -297,7 +235,7 @@ class HyperStepDecoder:
         am.forget_bias, am.keep = 1.0, 1.0
         am.seed, am.stream, am.step = self.sd.data_ptr(), 0, t
         am.c_prev, am.c_carry, am.h_out = self.CC.data_ptr(), self.CC.data_ptr(), self.Hout.data_ptr()
-        am.h_lp, am.ld_lp, am.lp_kind = self.A.data_ptr(), K, lpk
+        am.h_lp, am.ld_lp, am.lp_kind = self.A.data_ptr(), K, 1
         self.clm.set(am, t)
         return ah, am
 
@@ -313,17 +251,15 @@ class HyperStepDecoder:
                                     1, B, 5, G + Gh, st)
         if rc != 0:
             raise RuntimeError("skr_bproj_fwd failed (%d)" % rc)
-        f8 = self.fp8
         jobs = [(self.A[:, :H], w["WhT"], self.RM, self.S_m), (self.A, w["WyT"], self.RY, self.S_y)]
-        (gemm.rec_gemm_fp8_group if f8 else gemm.rec_gemm_group)(jobs)
+        gemm.rec_gemm_group(jobs)
         ah, am = self._cell_args(t)
         if self.lib.skr_lstm_fwd_step(ctypes.byref(ah), 1, 0, st) != 0:
             raise RuntimeError("hyper cell step failed")
-        (gemm.rec_gemm_fp8_v2(self.A[:, H:], PQ[0], self.VEC, 1) if f8 else
-         gemm.rec_gemm_bf16out(self.A[:, H:], PQ[0], self.VEC))
+        gemm.rec_gemm_bf16out(self.A[:, H:], PQ[0], self.VEC)
         if self.lib.skr_lstm_fwd_step(ctypes.byref(am), 1, 2, st) != 0:
             raise RuntimeError("main cell step failed")
-        (gemm.rec_gemm_fp8_v2 if f8 else gemm.rec_gemm)(self.A[:, :H], w["WoT"], self.ZS, self.S_o)
+        gemm.rec_gemm(self.A[:, :H], w["WoT"], self.ZS, self.S_o)
         sample(self.ZS, 128, self.S_o, B * 128, w["bo"])
 
     # -- four-launch stroke -------------------------------------------------------
@@ -350,20 +286,10 @@ class HyperStepDecoder:
         w, lib = self._w, self.lib
         B, H, Hh, G, Gh, K = self.B, self.H, self.Hh, self.G, self.Gh, self.K
         st = torch.cuda.current_stream().cuda_stream
-        f8 = self.fp8
-        jobs = [(self.A, w["WyT"], self.RY, self.S_y)]
-        if not self.lib_main:
-            jobs.insert(0, (self.A[:, :H], w["WhT"], self.RM, self.S_m))
+        jobs = [(self.A[:, :H], w["WhT"], self.RM, self.S_m), (self.A, w["WyT"], self.RY, self.S_y)]
         if smp is not None:
             jobs.append((self.A[:, :H], w["WoT"], self.ZS, self.S_o))
-        (gemm.rec_gemm_fp8_group if f8 else gemm.rec_gemm_group)(jobs)
-        if self.lib_main:
-            if f8:
-                a8 = self.A[:, :H].view(torch.float8_e4m3fn)
-                W8t, sb = w["WhL"]
-                torch._scaled_mm(a8, W8t.t(), scale_a=w["sa8"], scale_b=sb, out_dtype=torch.float32, out=self.RM[0])
-            else:
-                gemm.mm(self.A[:, :H], w["WhL"], out=self.RM[0])
+        gemm.rec_gemm_group(jobs)
         ah, am = self._cell_args(t)
         ah.xp = self.ZP[:, G:].data_ptr()          # z part; the stroke part is formed in the kernel
         if smp is None:
@@ -373,10 +299,9 @@ class HyperStepDecoder:
         if rc != 0:
             raise RuntimeError("skr_decode_hyper_cell failed (%d)" % rc)
         dec = ModDecode()
-        dec.hh32 = self.HH.data_ptr() if f8 else None
         dec.x5, dec.w5, dec.ldw5 = self.X.data_ptr(), w["W5"].data_ptr(), G + Gh
         dec.zp, dec.ldzp = self.ZP.data_ptr(), G + Gh
-        rc = lib.skr_hyper_mod_fwd(None if f8 else self.A[:, H:].data_ptr(), K, w["PL"].data_ptr(),
+        rc = lib.skr_hyper_mod_fwd(self.A[:, H:].data_ptr(), K, w["PL"].data_ptr(),
                                    w["QB"].data_ptr(), None, self.RM.data_ptr(), B * G, self.S_m, None,
                                    self.GP.data_ptr(), None, self.GS.data_ptr(), B, H, Hh, ctypes.byref(dec), st)
         if rc != 0:
@@ -388,8 +313,4 @@ class HyperStepDecoder:
     @torch.no_grad()
     def head(self) -> None:
         """Head GEMM of the current ``h`` into the split-K slabs ``ZS``."""
-        if self.fp8:
-            (gemm.rec_gemm_fp8_v2 if self.B <= 128 else gemm.rec_gemm_fp8)(self.A[:, :self.H], self._w["WoT"], self.ZS,
-                                                                            self.S_o)
-        else:
-            gemm.rec_gemm(self.A[:, :self.H], self._w["WoT"], self.ZS, self.S_o)
+        gemm.rec_gemm(self.A[:, :self.H], self._w["WoT"], self.ZS, self.S_o)

@@ -148,6 +148,9 @@ def sample_vae(model, seq_len: int = 250, temperature: float = 1.0, greedy: bool
 # device sampler + HIP graph decode
 # =====================================================================================
 _SAMPLE_STREAM = 0x5A3D
+# GraphDecoder steps VAE decoders with the in-place step decoders
+# (sample/hyper_step.py) where they apply; False: the generic decode_step.
+STEP_DECODER = os.environ.get("SKR_STEP_DECODER", "1") != "0"
 
 
 def mdn_sample_torch(zh: torch.Tensor, M_: int, mode: int, temp: float, greedy: bool, fix_pen: bool,
@@ -267,7 +270,7 @@ class GraphDecoder:
         LayerNorm exchange (co-resident spin-waits); the others keep every
         row in one workgroup, so no two spin-waiting launches ever compete
         for residency."""
-        if self.kind != "vae" or self.dev.type != "cuda" or os.environ.get("SKR_STEP_DECODER", "1") == "0":
+        if self.kind != "vae" or self.dev.type != "cuda" or not STEP_DECODER:
             return None
         from .hyper_step import HyperStepDecoder, hyper_step_ok, wide_ok
         if self.B > 128 and self.B % 128 == 0 and self.B <= 1024 and wide_ok(self.model):
@@ -379,7 +382,7 @@ class GraphDecoder:
             self.labels.copy_(labels)
         self.seed.fill_(int(seed))
         if self.use_graph:
-            # the graph holds inference-cached weight copies (bf16 / fp8): re-capture after a weight update
+            # the graph holds inference-cached weight copies (bf16): re-capture after a weight update
             from ..ops import gemm
             sig = (gemm.WEIGHTS_EPOCH[0],) + tuple(p._version for p in self.model.parameters())
             if self.graph is not None and sig != self._sig:

@@ -17,6 +17,7 @@ the delay: workgroups that cannot be placed wait for the hog to retire while
 their placed peers spin -- far inside the spin bound even with a 200 ms hog
 (an all-reduce kernel is resident for milliseconds).
 """
+import ctypes
 import json
 import time
 
@@ -119,3 +120,64 @@ def test_handoff_kernels_survive_concurrent_occupancy(which, hog):
         assert torch.equal(a, b)
     print(json.dumps({"kernels": which, "hog": name, "hog_ms": us / 1e3, "solo_ms": round(solo_ms, 2),
                       "with_hog_ms": round(both_ms, 2)}))
+
+
+def test_wait_timeout_raises_divergence_error_then_next_step_is_clean():
+    """The failure path (reference divergence guard train.py:93-94):
+    a persistent encoder backward whose workgroups can NOT all be resident.
+    Its launch goes to a queue restricted to 16 CUs (a CU-masked stream: the
+    state a co-running kernel holding the rest of the chip for longer than
+    the spin bound creates; deterministic, unlike a hog on a second queue,
+    whose placement against the compute queue the runtime does not promise).
+    Half of the first row block is placed and waits on peers that cannot be;
+    the spin bound is lowered for the test (skr_persist_set_spin_limit; the
+    production bound is ~seconds). Checked: the launch drains (the timed-out
+    wait poisons the launch, the rest of the grid then runs through), the
+    trainer's check raises DivergenceError for that step, and after the flag
+    is cleared the next step is clean and bit-identical to a normal run."""
+    from sketch_rnn_amd.ops import persist
+    from sketch_rnn_amd.train.trainer import DivergenceError, check_device_faults
+    lib = native.require_hip().lib
+    ops.set_backend("hip")
+    ops.set_compute_dtype("bf16")
+    torch.manual_seed(3)
+    T, B, H = 60, 100, 512
+    xp = torch.randn(T, 2 * B, 4 * H, device=DEV) * 0.5
+    W = torch.randn(2, H, 4 * H, device=DEV) / H ** 0.5
+    h = torch.zeros(2 * B, H, device=DEV)
+    dtop = torch.randn(T, 2 * B, H, device=DEV)
+    meta = (1, 2, 0.9, 2, 1.0)
+
+    def step(stream=None):
+        top, outs, s, dims = persist._fwd_launch(xp, None, None, W, None, h, h, None, None, None, 5, meta)
+        if stream is not None:   # the backward launch on the restricted queue
+            stream.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(stream):
+                r = persist._bwd_launch(s, dims, dtop, [None, None])
+            torch.cuda.current_stream().wait_stream(stream)
+        else:
+            r = persist._bwd_launch(s, dims, dtop, [None, None])
+        torch.cuda.synchronize()
+        return [top, r[0][0], r[2][0], r[5][0], r[6][0]]
+
+    ref = step()
+    check_device_faults()                  # clean before
+    raw = ctypes.c_void_p()
+    assert lib.skr_stream_create_cu_limited(16, ctypes.byref(raw)) == 0
+    assert lib.skr_persist_set_spin_limit(1 << 12) == 0
+    try:
+        t0 = time.perf_counter()
+        step(torch.cuda.ExternalStream(raw.value))
+        ms = 1e3 * (time.perf_counter() - t0)
+    finally:
+        assert lib.skr_persist_set_spin_limit(0) == 0
+        torch.cuda.synchronize()
+        lib.skr_stream_destroy(raw.value)
+    assert ms < 5000, ms                   # drained: no hang
+    with pytest.raises(DivergenceError):
+        check_device_faults()
+    out = step()                           # the next step: flag cleared, default bound
+    check_device_faults()
+    for a, b in zip(out, ref):
+        assert torch.equal(a, b)
+    print(json.dumps({"failure_path": "persist_encoder_bwd_16cu", "step_ms": round(ms, 1)}))

@@ -34,7 +34,7 @@ def test_arg_struct_layouts(hip):
 
 def test_exported_entry_points(hip):
     for name in ("skr_lstm_fwd_step", "skr_lstm_bwd_step", "skr_gru_fwd", "skr_gru_bwd", "skr_skinny_gemm_v2",
-                 "skr_skinny_gemm_v2", "skr_skinny_gemm_fp8", "skr_mdn_loss", "skr_adam_step", "skr_global_norm", "skr_mdn_sample",
+                 "skr_skinny_gemm_v2", "skr_mdn_loss", "skr_adam_step", "skr_global_norm", "skr_mdn_sample",
                  "skr_lstm_fused_fwd", "skr_lstm_fused_bwd", "skr_colsum",
                  "skr_skinny_gemm_group"):
         assert hasattr(hip.lib, name), name
