@@ -66,7 +66,7 @@ def run_arm(arm: str, args, seed: int = 0) -> dict:
             print("%s seed %d step %d: test recon NLL %.4f (train cost %.4f, %.0f s)"
                   % (arm, seed, step, ev["r_cost"], float(out["cost"]), time.perf_counter() - t0),
                   file=sys.stderr, flush=True)
-    return {"arm": arm, "seed": seed, "config": args.config, "steps": args.steps, "batch": args.batch, "seq_len": args.seq_len,
+    return {"arm": arm, "seed": seed, "commit": args.commit, "config": args.config, "steps": args.steps, "batch": args.batch, "seq_len": args.seq_len,
             "curve": curve, "final_test_recon_nll": curve[-1]["test_recon_nll"],
             "skipped_steps": trainer.opt.skipped_steps()}
 
@@ -82,6 +82,8 @@ def main():
     ap.add_argument("--arms", default="hip-bf16,hip-fp32")
     ap.add_argument("--seeds", default="0", help="comma list: init, data-order and noise seed of each run")
     ap.add_argument("--out", default=None)
+    ap.add_argument("--commit", default=os.environ.get("SKR_COMMIT", "unknown"),
+                    help="git commit of the tree under test (the GPU box has no .git): stored in every record")
     args = ap.parse_args()
     import numpy as np
     seeds = [int(x) for x in args.seeds.split(",")]
@@ -96,7 +98,7 @@ def main():
                 with open(args.out, "a") as f:
                     f.write(json.dumps(r) + "\n")
     # mean +- std of the final test recon NLL per arm over the seeds
-    summ = {"summary": True, "config": args.config, "steps": args.steps, "seeds": seeds, "arms": {}}
+    summ = {"summary": True, "commit": args.commit, "config": args.config, "steps": args.steps, "seeds": seeds, "arms": {}}
     for a in arms:
         v = np.array([r["final_test_recon_nll"] for r in res if r["arm"] == a])
         summ["arms"][a] = {"mean": round(float(v.mean()), 5), "std": round(float(v.std(ddof=1)) if len(v) > 1 else 0.0, 5),

@@ -17,7 +17,8 @@ def main():
                 if not r.get("summary"):
                     runs.append(r)
     arms = sorted({r["arm"] for r in runs})
-    summ = {"summary": True, "config": runs[0]["config"], "steps": runs[0]["steps"],
+    summ = {"summary": True, "commits": sorted({r.get("commit", "unknown") for r in runs}),
+            "config": runs[0]["config"], "steps": runs[0]["steps"],
             "seeds": sorted({r["seed"] for r in runs}), "arms": {}}
     for a in arms:
         v = np.array([r["final_test_recon_nll"] for r in sorted(runs, key=lambda r: r["seed"]) if r["arm"] == a])
