@@ -80,7 +80,7 @@ int build_group(const GemmProblem* probs, int n, int nprod, GemmGroup& g) {
         const int rc = check_problem64(probs[i]);
         if (rc) return rc;
         g.p[i] = probs[i];
-        g.start[i + 1] = g.start[i] + (probs[i].N / kBn) * probs[i].splits;
+        g.start[i + 1] = g.start[i] + (probs[i].N / kBn) * probs[i].splits * row_blocks_of(probs[i].M);
     }
     for (int i = n + 1; i <= kMaxGroup; ++i) g.start[i] = g.start[n];
     return g.start[nprod];

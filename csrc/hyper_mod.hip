@@ -217,7 +217,7 @@ __global__ __launch_bounds__(NTH) void hyper_mod_fwd(ModDecode dec, const __hip_
 // nslab fp32 slabs [B][4H] (stride r_slab), outputs vec [B][12H] bf16 (blocks
 // 0..7 written; null at inference), g [B][4H] fp32, rlp [B][4H] bf16 (or
 // null), stats [B][4][H/32][2] fp32. dec: decode-step inputs (ModDecode) or
-// null. B > 128 (a multiple of 128): 128-row blocks over gridDim.z.
+// null. B > 128: 128-row blocks over gridDim.z (the last one partial).
 SKR_API int skr_hyper_mod_fwd(const void* hh, int64_t ld_hh, const void* PlT, const float* qb, const float* xh,
                               const float* R, int64_t r_slab, int nslab, void* vec, float* g, void* rlp,
                               float* stats, int B, int H, int Hh, const ModDecode* dec, hipStream_t s) {
@@ -225,7 +225,7 @@ SKR_API int skr_hyper_mod_fwd(const void* hh, int64_t ld_hh, const void* PlT, co
     if (dz.x5 && (((uintptr_t)dz.w5 | (uintptr_t)dz.zp) & 15 || dz.ldw5 % 4 || dz.ldzp % 4)) return -4;
     if ((dz.x5 == nullptr && xh == nullptr) || hh == nullptr) return -3;
     if (B <= 0) return 0;
-    if ((B > MAXB && B % MAXB != 0) || Hh != HH || H % TU != 0) return -2;
+    if (B > 8 * MAXB || Hh != HH || H % TU != 0) return -2;
     if (((uintptr_t)hh | (uintptr_t)PlT | (uintptr_t)xh | (uintptr_t)R | (uintptr_t)vec | (uintptr_t)g |
          (uintptr_t)rlp) & 15 || (ld_hh % 8) || (r_slab % 4))
         return -4;

@@ -618,23 +618,31 @@ __global__ __launch_bounds__(NTHR) void lstm_persist_bwd(const PBwdArgs a) {
 }
 
 // ---- host side ----------------------------------------------------------------------
-constexpr int kMTW = 2;   // 32-row blocks
+// Row blocks of 16 MTW rows: MTW = 2 (32 rows, 4 K-slices per tile) by
+// default; MTW = 4 (64 rows, 2 K-slices) when the 32-row grid would not fit
+// one workgroup per CU -- a 256-row bidirectional 512 encoder is 2 x 4 x 32 =
+// 256 workgroups instead of 512. The caller picks nrb = ceil(B / (16 MTW)).
+inline int mtw_of(int B, int nrb) {
+    if (nrb == (B + 31) / 32) return 2;
+    if (nrb == (B + 63) / 64) return 4;
+    return 0;
+}
 
 // dynamic LDS: weights (K = 2H when a layer reads the layer below) + partial
 // tiles + the transposition buffer
-inline size_t fwd_lds(int H, int L) {
+inline size_t fwd_lds(int H, int L, int mtw) {
     const int K = L > 1 ? 2 * H : H;
-    return (size_t)64 * K * 2 + (size_t)(8 / kMTW) * kMTW * 4 * 64 * 16 + (size_t)kMTW * 256 * 2;
+    return (size_t)64 * K * 2 + (size_t)(8 / mtw) * mtw * 4 * 64 * 16 + (size_t)mtw * 256 * 2;
 }
-inline size_t bwd_lds(int H, int L) {
-    return (size_t)(L > 1 ? 2 : 1) * 16 * 4 * H * 2 + (size_t)(8 / kMTW) * kMTW * 2 * 64 * 16 + (size_t)kMTW * 1024 * 2;
+inline size_t bwd_lds(int H, int L, int mtw) {
+    return (size_t)(L > 1 ? 2 : 1) * 16 * 4 * H * 2 + (size_t)(8 / mtw) * mtw * 2 * 64 * 16 + (size_t)mtw * 1024 * 2;
 }
 
 template <typename A, typename KF>
 int launch_persist(KF kern, const A& a, size_t lds, hipStream_t s) {
     const int NW = a.H / U;
     const int grid = a.L * a.nd * a.nrb * NW;
-    static const void* attr_done[8];
+    static const void* attr_done[16];
     bool have = false;
     for (const void* p : attr_done) have |= (p == (const void*)kern);
     if (!have) {
@@ -661,7 +669,7 @@ int check_common(const A& a) {
     if (a.T <= 0 || a.B <= 0) return 1;
     if (a.L < 1 || a.L > 2 || a.nd < 1 || a.nd > 2 || (a.L == 2 && a.nd != 1)) return -2;
     if (a.H != 256 && (a.H != 512 || a.L > 1)) return -2;   // two stacked 512 layers exceed LDS
-    if (a.nrb != (a.B + 16 * kMTW - 1) / (16 * kMTW)) return -4;
+    if (mtw_of(a.B, a.nrb) == 0) return -4;
     if (a.flags == nullptr || a.err == nullptr) return -6;
     if (a.tlen != nullptr && a.L != 1) return -7;   // stacked layers run the full T
     // 32-bit buffer offsets
@@ -676,9 +684,12 @@ SKR_API int skr_lstm_persist_fwd(const PFwdArgs* a, hipStream_t s) {
     if (rc) return rc > 0 ? 0 : rc;
     for (int l = 0; l < a->L; ++l)
         if (a->ly[l].kin != (l == 0 ? 0 : a->H)) return -3;
-    switch (a->H) {
-        case 256: return launch_persist(lstm_persist_fwd<256, kMTW>, *a, fwd_lds(256, a->L), s);
-        case 512: return launch_persist(lstm_persist_fwd<512, kMTW>, *a, fwd_lds(512, a->L), s);
+    const int m = mtw_of(a->B, a->nrb);
+    switch (a->H * 8 + m) {
+        case 256 * 8 + 2: return launch_persist(lstm_persist_fwd<256, 2>, *a, fwd_lds(256, a->L, 2), s);
+        case 512 * 8 + 2: return launch_persist(lstm_persist_fwd<512, 2>, *a, fwd_lds(512, a->L, 2), s);
+        case 256 * 8 + 4: return launch_persist(lstm_persist_fwd<256, 4>, *a, fwd_lds(256, a->L, 4), s);
+        case 512 * 8 + 4: return launch_persist(lstm_persist_fwd<512, 4>, *a, fwd_lds(512, a->L, 4), s);
     }
     return -2;
 }
@@ -688,9 +699,12 @@ SKR_API int skr_lstm_persist_bwd(const PBwdArgs* a, hipStream_t s) {
     if (rc) return rc > 0 ? 0 : rc;
     for (int l = 0; l < a->L; ++l)
         if ((a->ly[l].Wu != nullptr) != (l < a->L - 1)) return -3;
-    switch (a->H) {
-        case 256: return launch_persist(lstm_persist_bwd<256, kMTW>, *a, bwd_lds(256, a->L), s);
-        case 512: return launch_persist(lstm_persist_bwd<512, kMTW>, *a, bwd_lds(512, a->L), s);
+    const int m = mtw_of(a->B, a->nrb);
+    switch (a->H * 8 + m) {
+        case 256 * 8 + 2: return launch_persist(lstm_persist_bwd<256, 2>, *a, bwd_lds(256, a->L, 2), s);
+        case 512 * 8 + 2: return launch_persist(lstm_persist_bwd<512, 2>, *a, bwd_lds(512, a->L, 2), s);
+        case 256 * 8 + 4: return launch_persist(lstm_persist_bwd<256, 4>, *a, bwd_lds(256, a->L, 4), s);
+        case 512 * 8 + 4: return launch_persist(lstm_persist_bwd<512, 4>, *a, bwd_lds(512, a->L, 4), s);
     }
     return -2;
 }

@@ -272,7 +272,7 @@ SKR_API int skr_skinny_gemm_group(const GemmProblem* probs, int n, int bn, hipSt
     g.start[0] = 0;
     for (int i = 0; i < n; ++i) {
         const GemmProblem& p = probs[i];
-        if (p.M < 1 || (p.M > BM && p.M % BM != 0) || p.N % bn != 0 || p.splits < 1 || p.K % p.splits != 0) return -2;
+        if (p.M < 1 || p.M > 8 * BM || p.N % bn != 0 || p.splits < 1 || p.K % p.splits != 0) return -2;
         if ((p.K / p.splits) % BK != 0 || p.lda % 8 != 0 || p.ldb % 8 != 0) return -3;
         if (((uintptr_t)p.A | (uintptr_t)p.Bt) & 15) return -4;
         g.p[i] = p;
@@ -305,11 +305,10 @@ SKR_API int skr_skinny_gemm_group_cellbwd(const GemmProblem* probs, int n, const
     g.start[0] = 0;
     for (int i = 0; i < n; ++i) {
         const GemmProblem& p = probs[i];
-        if (p.M < 1 || p.M > BM || p.N % 64 != 0 || p.splits < 1 || p.K % p.splits != 0) return -2;
-        if ((p.K / p.splits) % BK != 0 || p.lda % 8 != 0 || p.ldb % 8 != 0) return -3;
-        if (((uintptr_t)p.A | (uintptr_t)p.Bt) & 15) return -4;
+        const int rc = check_problem64(p);
+        if (rc) return rc;
         g.p[i] = p;
-        g.start[i + 1] = g.start[i] + (p.N / 64) * p.splits;
+        g.start[i + 1] = g.start[i] + (p.N / 64) * p.splits * row_blocks_of(p.M);
     }
     for (int i = n + 1; i <= kMaxGroup; ++i) g.start[i] = g.start[n];
     const size_t lds = (size_t)3 * (BM + 64) * BK * 2;

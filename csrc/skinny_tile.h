@@ -101,9 +101,10 @@ __device__ __forceinline__ void group_tile(const GemmGroup& g, const int id, __h
                                       t.nt * BN, (int64_t)t.split * kslice, kslice, smem);
 }
 
-// Host-side validation of one problem for 64-wide tiles (0: ok).
+// Host-side validation of one problem for 64-wide tiles (0: ok). M > 128:
+// ceil(M / 128) row blocks, the last one partial (tile_idx: t.rows).
 inline int check_problem64(const GemmProblem& p) {
-    if (p.M < 1 || p.M > skr::BM || p.N % 64 != 0 || p.splits < 1 || p.K % p.splits != 0) return -2;
+    if (p.M < 1 || p.M > 8 * skr::BM || p.N % 64 != 0 || p.splits < 1 || p.K % p.splits != 0) return -2;
     if ((p.K / p.splits) % skr::BK != 0 || p.lda % 8 != 0 || p.ldb % 8 != 0) return -3;
     if (((uintptr_t)p.A | (uintptr_t)p.Bt) & 15) return -4;
     return 0;

@@ -219,10 +219,12 @@ _SPLITS = (1, 2, 4, 8, 16, 32)  # powers of two: the cell kernels sum <= 8 slabs
 
 def row_blocks(M: int) -> int:
     """128-row blocks the skinny kernels run for M rows (0: not supported):
-    M <= 128 in one block, or a multiple of 128 up to 1024 as a batch of blocks."""
+    M <= 128 in one block, else ceil(M / 128) blocks up to 1024 rows (the
+    grouped kernels take a partial last block; :func:`rec_gemm` routes such
+    a product through them)."""
     if M <= 128:
         return 1
-    return M // 128 if M % 128 == 0 and M <= 1024 else 0
+    return -(-M // 128) if M <= 1024 else 0
 
 
 # fp32 operands (fp32 parity runs) through the fp32 MFMA skinny kernel
@@ -238,6 +240,8 @@ def plan_splits(M: int, N: int, K: int, batch: int = 1, dtype: torch.dtype = _BF
     if dtype not in (_BF16, torch.float32) or (dtype == torch.float32 and not F32_GEMM):
         return 0
     if mb == 0 or (mb > 1 and batch > 1) or N % 64 or K % kt:
+        return 0
+    if M > 128 and M % 128 and dtype != _BF16:   # (partial row blocks: the bf16 grouped kernel only)
         return 0
     tiles = (N // 64) * batch * mb
     best = 1
@@ -276,6 +280,9 @@ def rec_gemm(a: torch.Tensor, bt: torch.Tensor, out: torch.Tensor, splits: int, 
         fn = lambda *args: f32(*args[:-2], args[-1])   # noqa: E731  (drop bn)
     else:
         fn = lib.lib.skr_skinny_gemm_v2
+    if nd == 1 and M > 128 and M % 128:   # a partial last row block: the grouped kernel takes it
+        _launch_group([(a, bt, out, splits)])
+        return out
     if nd == 1 and M > 128:   # 128-row blocks as the kernel's batch dimension, sharing B
         mb = row_blocks(M)
         rc = fn(a.data_ptr(), a.stride(0), 128 * a.stride(0), bt.data_ptr(), bt.stride(-2), 0, out.data_ptr(), N,
@@ -325,6 +332,10 @@ def rec_gemm_group(jobs) -> None:
         for a, bt, out, s in jobs:
             rec_gemm(a, bt, out, s)
         return
+    _launch_group(jobs)
+
+
+def _launch_group(jobs) -> None:
     from ..utils import native
     from ._hipapi import GemmProblem
     lib = native.require_hip()
@@ -343,7 +354,7 @@ def _problems(jobs):
     from ._hipapi import GemmProblem
     probs = (GemmProblem * len(jobs))()
     for p, (a, bt, out, s) in zip(probs, jobs):
-        assert a.is_cuda and a.dtype == _BF16 and s >= 1 and a.shape[0] <= 128
+        assert a.is_cuda and a.dtype == _BF16 and s >= 1 and a.shape[0] <= 1024
         N, K = bt.shape[-2], bt.shape[-1]
         p.A, p.lda, p.Bt, p.ldb = a.data_ptr(), a.stride(0), bt.data_ptr(), bt.stride(-2)
         p.C, p.ldc, p.c_slab = out.data_ptr(), N, out.stride(0)

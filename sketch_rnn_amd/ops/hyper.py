@@ -202,10 +202,17 @@ class _HyperSeq(torch.autograd.Function):
         A = torch.empty(T + 1, B, K, device=dev, dtype=dt)
         A[0, :, :H].copy_(h0)
         A[0, :, H:].copy_(hh0)
+        # modulation step fused with the gate pre-activations and their
+        # LayerNorm partial sums (csrc/hyper_mod.hip, 128-row blocks: B <= 256
+        # here): the main cell then needs no statistics exchange for the gates
+        # (MOD 3) and VEC carries q (and the main bias in its shift block) --
+        # the backward uses a zero vec_bias
+        hm_ok = HYPER_MOD and dev.type == "cuda" and Hh == 256 and H % 32 == 0 and S_m in (1, 2, 4) and B <= 256
+        # bf16 modulation vectors (the bf16-output GEMM takes <= 128 rows, hyper_mod 256)
+        vbf = dt == torch.bfloat16 and S_v == 1 and (B <= 128 or hm_ok)
         # R_main: the backward re-reads it (the hyper-modulation gradient
         # dg * R) as the bf16 copy the main cell saves (RLP); with fp32 GEMM
         # operands the fp32 split-K slabs of every step are kept instead
-        vbf = dt == torch.bfloat16 and B <= 128 and S_v == 1
         RLP = torch.empty(T, B, G, device=dev, dtype=torch.bfloat16) if (vbf and not infer) else None
         CC = torch.empty(T + 1, B, H, device=dev, dtype=f32)
         CC[0].copy_(c0)
@@ -236,12 +243,7 @@ class _HyperSeq(torch.autograd.Function):
         rmi = (lambda t: t) if RM.shape[0] == T else (lambda t: 0)
         RY = torch.empty(max(S_y, 1), B, Gh, device=dev, dtype=f32)
         mod = 2 if vbf else 1
-        # modulation step fused with the gate pre-activations and their
-        # LayerNorm partial sums (csrc/hyper_mod.hip): the main cell then needs
-        # no statistics exchange for the gates (MOD 3) and VEC carries q (and
-        # the main bias in its shift block) -- the backward uses a zero vec_bias
-        hmod = HYPER_MOD and vbf and dev.type == "cuda" and Hh == 256 and B <= 128 and H % 32 == 0 and \
-            S_m in (1, 2, 4)
+        hmod = hm_ok and vbf
         if hmod:
             mod = 3
             if qb_f is not None:   # q + the main bias on the shift block, from the fold kernel

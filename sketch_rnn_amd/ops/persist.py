@@ -39,7 +39,8 @@ PERSIST_ENABLED = os.environ.get("SKR_PERSIST", "1") != "0"
 # debug: fill every handed-off buffer with NaN before the launch, so a read
 # that overtakes its hand-off shows up as a NaN instead of a stale value
 POISON = os.environ.get("SKR_PERSIST_POISON", "0") == "1"
-_ROWS = 32          # rows per workgroup row block (kMTW = 2 sixteen-row tiles)
+_ROWS = 32          # rows per workgroup row block (MTW = 2 sixteen-row tiles) ...
+_ROWS_WIDE = 64     # ... or 64 (MTW = 4) when the 32-row grid exceeds one workgroup per CU
 
 
 def _cu_count() -> int:
@@ -48,12 +49,22 @@ def _cu_count() -> int:
     return torch.cuda.get_device_properties(torch.cuda.current_device()).multi_processor_count
 
 
+def block_rows(H: int, nd: int, L: int, B: int) -> int:
+    """Rows per row block (32, or 64 when the 32-row grid of L * nd *
+    ceil(B / 32) row blocks x H / 16 workgroups exceeds one workgroup per
+    CU); 0 when neither fits."""
+    for rows in (_ROWS, _ROWS_WIDE):
+        if L * nd * (-(-B // rows)) * (H // 16) <= _cu_count():
+            return rows
+    return 0
+
+
 def persist_ok(H: int, nd: int = 1, L: int = 1, ln: bool = False, B: Optional[int] = None) -> bool:
     """Eligibility of the persistent kernels. ``B``: rows per direction; the
-    grid (L * nd * ceil(B / 32) row blocks x H / 16 workgroups) must fit one
-    workgroup per CU, since every workgroup spin-waits on its peers (the
-    launcher refuses a larger grid: -8). Callers fall back to the per-step
-    kernels otherwise."""
+    grid (L * nd * ceil(B / rows) row blocks x H / 16 workgroups, rows 32 or
+    64: :func:`block_rows`) must fit one workgroup per CU, since every
+    workgroup spin-waits on its peers (the launcher refuses a larger grid:
+    -8). Callers fall back to the per-step kernels otherwise."""
     if not PERSIST_ENABLED or ln or gemm.lp_dtype() != torch.bfloat16:
         return False
     if L == 2:
@@ -62,7 +73,7 @@ def persist_ok(H: int, nd: int = 1, L: int = 1, ln: bool = False, B: Optional[in
         shape_ok = L == 1 and nd in (1, 2) and H in (256, 512)
     if not shape_ok:
         return False
-    if B is not None and L * nd * (-(-B // _ROWS)) * (H // 16) > _cu_count():
+    if B is not None and block_rows(H, nd, L, B) == 0:
         return False
     return True
 
@@ -91,7 +102,7 @@ def _fwd_launch(xp0, W_in1, b1, W_h0, W_h1, h0a, c0a, h0b, c0b, reset, seed, met
     T, NB, G = xp0.shape
     H, B = G // 4, NB // nd
     dev, bf, f32 = xp0.device, torch.bfloat16, torch.float32
-    nrb = -(-B // _ROWS)
+    nrb = -(-B // (block_rows(H, nd, L, B) or _ROWS))
     xp0 = xp0.contiguous()
     Wh = [W_h0] + ([W_h1] if L == 2 else [])
     h0s = [h0a.contiguous()] + ([h0b.contiguous()] if L == 2 else [])

@@ -299,7 +299,8 @@ def test_hyper_sequence_bf16_close(H, Hh, E):
     _close(res[0][5:], res[1][5:], 6e-2, 6e-2, "grad")
 
 
-@pytest.mark.parametrize("B,keep,hkeep", [(100, 0.9, 0.9), (37, 1.0, 1.0), (128, 0.9, 1.0)])
+@pytest.mark.parametrize("B,keep,hkeep", [(100, 0.9, 0.9), (37, 1.0, 1.0), (128, 0.9, 1.0), (192, 0.9, 1.0),
+                                          (256, 1.0, 0.9)])
 def test_hyper_mod_path_vs_oracle(B, keep, hkeep):
     """The fused modulation step (csrc/hyper_mod.hip: vec + gate
     pre-activations + LayerNorm partial sums; the main cell without its
@@ -323,7 +324,10 @@ def test_hyper_mod_path_vs_oracle(B, keep, hkeep):
         scale = max(ref.abs().max().item(), 1e-3)
         e_f = (runs["fused"][i].float() - ref).abs().max().item()
         e_p = (runs["plain"][i].float() - ref).abs().max().item()
-        ok = e_f <= 1.5 * e_p + 1e-3 * scale
+        # (B > 128: the plain chain keeps fp32 modulation vectors -- the bf16-
+        # output GEMM takes <= 128 rows -- so it is the stricter yardstick;
+        # the fused path then has to stay within bf16 tolerance of the oracle)
+        ok = e_f <= 1.5 * e_p + 1e-3 * scale or (B > 128 and e_f <= 3e-2 * scale)
         assert ok, (n, e_f, e_p, scale)
 
 
@@ -420,8 +424,10 @@ def test_hyper_bf16_gradients_b100_t50_cosine():
 
 @pytest.mark.parametrize("M,N,K,nd", [(100, 9216, 2304, 1), (100, 2304, 9216, 1), (100, 256, 24576, 1),
                                       (100, 24576, 256, 1), (7, 64, 64, 1), (128, 2048, 512, 2),
-                                      (100, 512, 2048, 2), (256, 8192, 2048, 1), (512, 1024, 256, 1)])
+                                      (100, 512, 2048, 2), (256, 8192, 2048, 1), (512, 1024, 256, 1),
+                                      (192, 8192, 2048, 1), (320, 1024, 2304, 1)])
 def test_skinny_gemm_matches_torch(M, N, K, nd):
+    """(M > 128 and not a multiple of 128: the grouped kernel's partial last row block.)"""
     from sketch_rnn_amd.ops import gemm
     torch.manual_seed(6)
     a = torch.randn(nd * M, K, device=DEV).to(torch.bfloat16)
@@ -887,7 +893,8 @@ def test_hyper_backward_fused_cell_launch_bitwise(monkeypatch):
 
 
 
-@pytest.mark.parametrize("B,T,fin_w", [(100, 7, True), (100, 5, False), (37, 4, True), (128, 3, False)])
+@pytest.mark.parametrize("B,T,fin_w", [(100, 7, True), (100, 5, False), (37, 4, True), (128, 3, False), (192, 4, True),
+                                       (256, 3, False)])
 def test_hyper_chained_launches_vs_unchained(B, T, fin_w):
     """csrc/chain_step.hip: the main-cell backward rows inside the next step's
     dR_hyp W_y^T launch (an in-launch wait on an arrival counter, sc1 slab

@@ -74,9 +74,14 @@ def test_persistent_reference_stack_matches_oracle(B, T, with_reset):
         assert _rel(gr[n], ref) < 4e-2, (n, _rel(gr[n], ref))
 
 
-def test_persistent_bilstm_matches_oracle():
+@pytest.mark.parametrize("B", [100, 192, 256])
+def test_persistent_bilstm_matches_oracle(B):
+    """Both encoder directions in one persistent launch vs the fp32 oracle;
+    B > 128 runs 64-row blocks (2 x ceil(B / 64) x 32 workgroups <= 256 CUs)."""
+    from sketch_rnn_amd.ops import persist as P
     torch.manual_seed(3)
-    T, B, H = 30, 100, 512
+    T, H = 30, 512
+    assert P.block_rows(H, 2, 1, B) == (32 if B <= 128 else 64)
     xp = (torch.randn(T, 2 * B, 4 * H, device=DEV) * 0.5).requires_grad_()
     W_f = (torch.randn(H, 4 * H, device=DEV) / H ** 0.5).requires_grad_()
     W_b = (torch.randn(H, 4 * H, device=DEV) / H ** 0.5).requires_grad_()
@@ -201,7 +206,8 @@ def test_persistent_graph_replay_matches_eager():
         persist.POISON = False
 
 
-def test_fused_encoder_last_h_matches_unfused_and_oracle():
+@pytest.mark.parametrize("B", [100, 256])
+def test_fused_encoder_last_h_matches_unfused_and_oracle(B):
     """The VAE encoder as one node (input projection + persistent biLSTM
     writing only h[len-1], ops/persist.py _PersistBiEncoder) against the
     unfused HIP path (projection, persistent biLSTM with [T, 2B, H] outputs,
@@ -210,10 +216,10 @@ def test_fused_encoder_last_h_matches_unfused_and_oracle():
     against the fp32 torch oracle at bf16 tolerances."""
     from sketch_rnn_amd.config import VAEConfig
     from sketch_rnn_amd.models.vae import Encoder
-    cfg = VAEConfig(enc_rnn_size=512, dec_rnn_size=512, z_size=64, max_seq_len=60, batch_size=100)
+    cfg = VAEConfig(enc_rnn_size=512, dec_rnn_size=512, z_size=64, max_seq_len=60, batch_size=B)
     gen = torch.Generator().manual_seed(2)
     enc = Encoder(cfg, gen).to(DEV)
-    T, B = 60, 100
+    T = 60
     g = torch.Generator().manual_seed(3)
     x = torch.randn(T, B, 5, generator=g) * 0.5
     lengths = torch.randint(5, T + 1, (B,), generator=g)
