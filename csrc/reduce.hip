@@ -182,6 +182,152 @@ SKR_API int skr_colsum2(const void* X, int x_kind, const void* Y, int y_kind, in
     return SKR_CHECK_LAUNCH();
 }
 
+// Several column reductions in ONE launch per pass (the LayerNorm gamma /
+// beta gradients of a HyperLSTM step are four: [T*B, 8192 | 2048 | 1024 |
+// 256]). The narrow ones are latency-bound and would each pay a kernel
+// boundary and a tail on their own; here their workgroups fill the chip
+// beside the wide one's. Vector path only (four columns per thread: C, the
+// strides and the bases multiples of 4 elements / 16 bytes).
+struct CsJob {
+    const void* X; const void* Y;          // Y may be null
+    int64_t R1, s1, R2, s2;
+    int C, RS, xbf, ybf;                    // xbf / ybf: 1 bf16, 0 fp32
+    float* part_xy; float* part_x;          // [RS][C] each
+    float* out_xy; float* out_x;            // [C] (out_xy unused without Y)
+};
+constexpr int kCsMax = 4;
+struct CsJobs {
+    CsJob j[kCsMax];
+    int n;
+    int start[kCsMax + 1];                  // first-pass workgroups: prefix sums of RS * ceil(C / 1024)
+    int fstart[kCsMax + 1];                 // finish workgroups: prefix sums of ceil(C / 64)
+};
+
+namespace {
+
+__device__ __forceinline__ void ld4(const void* x, int64_t i, bool bf, float (&v)[4]) {
+    if (bf) ldv<true, 4>(x, i, v);
+    else ldv<false, 4>(x, i, v);
+}
+
+__global__ __launch_bounds__(256) void colsum_multi_kernel(const CsJobs jobs) {
+    int q = 0;
+    while (q + 1 < jobs.n && (int)blockIdx.x >= jobs.start[q + 1]) ++q;
+    const CsJob& J = jobs.j[q];
+    const int local = blockIdx.x - jobs.start[q];
+    const int cb = (J.C / 4 + 255) / 256;
+    const int rs = local / cb, cbi = local - rs * cb;
+    const int c = (cbi * 256 + threadIdx.x) * 4;
+    if (c >= J.C) return;
+    const int64_t R = J.R1 * J.R2;
+    const int64_t per = (R + J.RS - 1) / J.RS;
+    const int64_t r0 = rs * per, r1 = min(R, r0 + per);
+    float sxy[4] = {0.f, 0.f, 0.f, 0.f}, sx[4] = {0.f, 0.f, 0.f, 0.f};
+    int64_t i = r0 / J.R2, j = r0 % J.R2;
+    int64_t r = r0;
+    for (; r + 2 <= r1; r += 2) {
+        float xv[2][4], yv[2][4];
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            const int64_t off = i * J.s1 + j * J.s2 + c;
+            ld4(J.X, off, J.xbf, xv[k]);
+            if (J.Y) ld4(J.Y, off, J.ybf, yv[k]);
+            else
+#pragma unroll
+                for (int e = 0; e < 4; ++e) yv[k][e] = 0.f;
+            if (++j == J.R2) {
+                j = 0;
+                ++i;
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < 2; ++k)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                sx[e] += xv[k][e];
+                sxy[e] += xv[k][e] * yv[k][e];
+            }
+    }
+    for (; r < r1; ++r) {
+        const int64_t off = i * J.s1 + j * J.s2 + c;
+        float xv[4], yv[4] = {0.f, 0.f, 0.f, 0.f};
+        ld4(J.X, off, J.xbf, xv);
+        if (J.Y) ld4(J.Y, off, J.ybf, yv);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            sx[e] += xv[e];
+            sxy[e] += xv[e] * yv[e];
+        }
+        if (++j == J.R2) {
+            j = 0;
+            ++i;
+        }
+    }
+    const int64_t o = (int64_t)rs * J.C + c;
+    *(float4*)(J.part_x + o) = float4{sx[0], sx[1], sx[2], sx[3]};
+    if (J.Y) *(float4*)(J.part_xy + o) = float4{sxy[0], sxy[1], sxy[2], sxy[3]};
+}
+
+// colsum_finish of every job, one launch (the same fixed summation order)
+__global__ __launch_bounds__(256) void colsum_multi_finish(const CsJobs jobs) {
+    int q = 0;
+    while (q + 1 < jobs.n && (int)blockIdx.x >= jobs.fstart[q + 1]) ++q;
+    const CsJob& J = jobs.j[q];
+    __shared__ float red[2][4][64];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int c = (blockIdx.x - jobs.fstart[q]) * 64 + lane, cc = min(c, J.C - 1);
+    const bool hy = J.Y != nullptr;
+    float sx = 0.f, sxy = 0.f;
+    for (int r0 = w; r0 < J.RS; r0 += 32) {
+        float tx[8], txy[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const int rr = min(r0 + 4 * k, J.RS - 1);
+            tx[k] = J.part_x[(int64_t)rr * J.C + cc];
+            txy[k] = hy ? J.part_xy[(int64_t)rr * J.C + cc] : 0.f;
+        }
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const bool on = r0 + 4 * k < J.RS;
+            sx += on ? tx[k] : 0.f;
+            sxy += on ? txy[k] : 0.f;
+        }
+    }
+    red[0][w][lane] = sx;
+    red[1][w][lane] = sxy;
+    __syncthreads();
+    if (w != 0 || c >= J.C) return;
+    J.out_x[c] = ((red[0][0][lane] + red[0][1][lane]) + red[0][2][lane]) + red[0][3][lane];
+    if (hy) J.out_xy[c] = ((red[1][0][lane] + red[1][1][lane]) + red[1][2][lane]) + red[1][3][lane];
+}
+
+}  // namespace
+
+// n <= 4 column reductions (CsJob each), both passes, two launches in all.
+// Returns -2 / -4 for a job the vector path does not take (callers then use
+// skr_colsum2 per job).
+SKR_API int skr_colsum_multi(const CsJob* jobs, int n, hipStream_t s) {
+    if (n < 1 || n > kCsMax) return -2;
+    CsJobs g{};
+    g.n = n;
+    for (int q = 0; q < n; ++q) {
+        const CsJob& J = jobs[q];
+        if (J.C <= 0 || J.C % 4 || J.RS <= 0 || J.R1 * J.R2 <= 0 || J.s1 % 4 || J.s2 % 4) return -2;
+        if ((((uintptr_t)J.X | (uintptr_t)(J.Y ? J.Y : J.X)) & 15) ||
+            (((uintptr_t)J.part_x | (uintptr_t)(J.Y ? J.part_xy : J.part_x)) & 15))
+            return -4;
+        g.j[q] = J;
+        g.start[q + 1] = g.start[q] + J.RS * ((J.C / 4 + 255) / 256);
+        g.fstart[q + 1] = g.fstart[q] + (J.C + 63) / 64;
+    }
+    for (int q = n + 1; q <= kCsMax; ++q) g.start[q] = g.start[n], g.fstart[q] = g.fstart[n];
+    hipLaunchKernelGGL(colsum_multi_kernel, dim3(g.start[n]), dim3(256), 0, s, g);
+    hipLaunchKernelGGL(colsum_multi_finish, dim3(g.fstart[n]), dim3(256), 0, s, g);
+    return SKR_CHECK_LAUNCH();
+}
+
+SKR_API int skr_colsum_job_size() { return (int)sizeof(CsJob); }
+
 // out[r][c] = sum_s a[s*a_slab + r*a_ld + c] + sum_s b[s*b_slab + r*b_ld + c]
 // (b may be null): the gradient into a recurrence's initial state from the
 // split-K dh slabs of its first step (HyperLSTM: the d[h | hh] and dR_main

@@ -215,6 +215,10 @@ class SketchVAE(nn.Module):
         B = strokes.shape[0]
         Nmax = strokes.shape[1] - 1
         dev = strokes.device
+        # time-major stroke batch, transposed ONCE: the encoder input sT[1:],
+        # the decoder input sT[:Nmax] and the targets are contiguous views
+        # of it (each consumer copied its own transposed slice before)
+        sT = strokes.transpose(0, 1).contiguous()
         z = None
         kl = strokes.new_zeros(())
         from ..ops import latent as L
@@ -224,7 +228,7 @@ class SketchVAE(nn.Module):
         if cfg.conditional and self.class_emb is None and L.latent_ok(self.encoder.mu_w, len(widths)) and \
                 LATENT_FUSED:
             # encoder summary -> (mu, presig, z, KL, decoder state) as one node (ops/latent.py)
-            last_h = self.encoder.last_hidden(strokes[:, 1:].transpose(0, 1), lengths, train, seed)
+            last_h = self.encoder.last_hidden(sT[1:], lengths, train, seed)
             if split_encoder:
                 enc = (last_h,)
                 last_h = last_h.detach().requires_grad_()
@@ -239,7 +243,7 @@ class SketchVAE(nn.Module):
                      "layer_norm": lambda q: (q[0], q[1])}[cfg.dec_model](segs)
             zc = z
         elif cfg.conditional:
-            mu, presig = self.encode(strokes, lengths, train, seed)
+            mu, presig = self.encoder(sT[1:], lengths, train, seed)
             if split_encoder:
                 enc = (mu, presig)
                 mu, presig = mu.detach().requires_grad_(), presig.detach().requires_grad_()
@@ -255,9 +259,9 @@ class SketchVAE(nn.Module):
         else:
             zc = self.condition(z, labels, B, dev)
             state = self.initial_state(zc, B, dev)
-        x_in = strokes[:, :Nmax].transpose(0, 1)
+        x_in = sT[:Nmax]
         out, _ = self.decode(x_in, zc, state, train, seed, out_dropout=False)
-        target = strokes[:, 1:].transpose(0, 1).reshape(-1, 5)
+        target = sT[1:].reshape(-1, 5)
         # head + loss (fused on the GPU: projection, MDN loss and dL/dz in one kernel)
         keep = cfg.output_dropout_prob if (train and cfg.use_output_dropout) else 1.0
         r_cost, shape, pen = ops.mdn_head_loss(out.reshape(-1, out.shape[-1]), self.output_w, self.output_b, target,

@@ -264,6 +264,16 @@ class GemmProblem(C.Structure):
     ]
 
 
+class CsJob(C.Structure):
+    """Mirror of ``CsJob`` in csrc/reduce.hip (one column reduction of skr_colsum_multi)."""
+    _fields_ = [
+        ("X", _p), ("Y", _p),
+        ("R1", _i64), ("s1", _i64), ("R2", _i64), ("s2", _i64),
+        ("C", _i), ("RS", _i), ("xbf", _i), ("ybf", _i),
+        ("part_xy", _p), ("part_x", _p), ("out_xy", _p), ("out_x", _p),
+    ]
+
+
 class ChainSync(C.Structure):
     """Mirror of ``ChainSync`` in csrc/chain_step.hip (rotating arrival
     counters of a chained launch kind)."""
@@ -383,6 +393,8 @@ class HipLib:
         lib.skr_lstm_persist_fwd.restype = _i
         lib.skr_lstm_persist_bwd.argtypes = [C.POINTER(PBwdArgs), _p]
         lib.skr_lstm_persist_bwd.restype = _i
+        lib.skr_colsum_multi.argtypes = [C.POINTER(CsJob), _i, _p]
+        lib.skr_colsum_multi.restype = _i
         lib.skr_persist_set_spin_limit.argtypes = [C.c_uint]
         lib.skr_persist_set_spin_limit.restype = _i
         lib.skr_mdn_head_fwd.argtypes = [C.POINTER(HeadFwd), _p, _p]
@@ -416,7 +428,8 @@ class HipLib:
                           ("skr_decode_ref_args_size", DecArgs),
                           ("skr_gemm_problem_size", GemmProblem),
                           ("skr_decode_sample_size", DecodeSample),
-                          ("skr_chain_sync_size", ChainSync)):
+                          ("skr_chain_sync_size", ChainSync),
+                          ("skr_colsum_job_size", CsJob)):
             fn = getattr(lib, name)
             fn.restype = _i
             if fn() != C.sizeof(cls):

@@ -25,7 +25,7 @@ from ._hipapi import LstmBwdArgs, LstmFwdArgs
 from .inproj import bproj_fwd, bproj_ok, bproj_reduce
 from .recurrent import (ROW_STATS, _cell_bwd, _cell_fwd, _check, _ClusterSync, _inference, _ln_saves_lp, _lp_kind,
                         _ptr, _Saved, _seed_tensor, _stream, cell_geometry)
-from .reduce import colsum
+from .reduce import colsum_many
 
 # The modulation GEMM fused with the main gates' pre-activations and
 # LayerNorm partial sums (csrc/hyper_mod.hip). False (tests / shapes it does
@@ -215,9 +215,9 @@ class _HyperSeq(torch.autograd.Function):
         # operands the fp32 split-K slabs of every step are kept instead
         RLP = torch.empty(T, B, G, device=dev, dtype=torch.bfloat16) if (vbf and not infer) else None
         CC = torch.empty(T + 1, B, H, device=dev, dtype=f32)
-        CC[0].copy_(c0)
+        c0c = c0.contiguous()   # step 0 reads c0 / hc0 in place (CC[0], HCC[0] stay unused: no copies)
         HCC = torch.empty(T + 1, B, Hh, device=dev, dtype=f32)
-        HCC[0].copy_(hc0)
+        hc0c = hc0.contiguous()
         Hout = torch.empty(T, B, H, device=dev, dtype=f32)
         HH = torch.empty(T, B, Hh, device=dev, dtype=f32)
         # saves for the backward (both cells are LayerNorm cells: xhat / rstd /
@@ -291,7 +291,7 @@ class _HyperSeq(torch.autograd.Function):
         for t in range(T):
             clm.set(am, t)
             clh.set(ah, t)
-            ah.xp, ah.c_prev, ah.step = XHY[t].data_ptr(), HCC[t].data_ptr(), t
+            ah.xp, ah.c_prev, ah.step = XHY[t].data_ptr(), (hc0c if t == 0 else HCC[t]).data_ptr(), t
             ah.h_out = HH[t].data_ptr()
             if not infer:
                 ah.xhat, ah.rstd, ah.chat = HXHAT[t].data_ptr(), HRSTD[t].data_ptr(), HCHAT[t].data_ptr()
@@ -314,7 +314,7 @@ class _HyperSeq(torch.autograd.Function):
                 rgemm(A[t + 1, :, H:], PlT, VEC[t].unsqueeze(0), S_v)
             am.xp, am.R, am.vec = XH[t].data_ptr(), RM[rmi(t)].data_ptr(), VEC[t].data_ptr()
             am.r_lp = RLP[t].data_ptr() if (RLP is not None and not hmod) else None
-            am.c_prev, am.step = CC[t].data_ptr(), t
+            am.c_prev, am.step = (c0c if t == 0 else CC[t]).data_ptr(), t
             am.h_out = Hout[t].data_ptr()
             _main_saves(am, t)
             am.h_lp, am.c_carry = A[t + 1, :, :H].data_ptr(), CC[t + 1].data_ptr()
@@ -323,13 +323,14 @@ class _HyperSeq(torch.autograd.Function):
         hhT = HH[T - 1].clone()
         s = _Saved()
         for k, v in dict(xl=xl, x=x, zc=zc, bp=bp, XH=XH, Whl=Whl, Wyl=Wyl, Pl=Pl, q=q, S_m=S_m, A=A, RM=RM,
-                         RLP=RLP, CC=CC, HCC=HCC, XHAT=XHAT, RSTD=RSTD, CHAT=CHAT, HH=HH, HXHAT=HXHAT, HRSTD=HRSTD,
+                         RLP=RLP, CC=CC, HCC=HCC, c0=c0c, hc0=hc0c, XHAT=XHAT, RSTD=RSTD, CHAT=CHAT, HH=HH, HXHAT=HXHAT, HRSTD=HRSTD,
                          HCHAT=HCHAT, VEC=VEC, seed=sd, meta=meta, slp=slp, W_h=W_h, W_x=W_x, hW_x=hW_x, W_z=W_z, b_z=b_z, W_a=W_a,
                          mln=mln, hln=hln, vec_folded=hmod, mln_on=mln_on, ACT=ACT, COUT=COUT).items():
             setattr(s, k, v)
         ctx.s = s
         ctx.dims = (T, B, IX, IN, H, Hh, E)
-        return Hout, hT, CC[T].clone(), hhT, HCC[T].clone()
+        # (views of internal buffers nothing writes again)
+        return Hout, hT, (CC[T] if T > 0 else c0c), hhT, (HCC[T] if T > 0 else hc0c)
 
     @staticmethod
     def backward(ctx, dHout, dhT, dcT, dhhT, dhcT):
@@ -429,7 +430,7 @@ class _HyperSeq(torch.autograd.Function):
                 am.dh_rec2 = None if (first and t == T - 1) else DAM.data_ptr()
                 ah.dh_rec = None if (first and t == T - 1) else DAY[0, :, H:].data_ptr()
             am.dh_out = dHout[t].data_ptr() if dHout is not None else None
-            am.c_prev = s.CC[t].data_ptr()
+            am.c_prev = (s.c0 if t == 0 else s.CC[t]).data_ptr()
             if s.mln_on:
                 am.xhat, am.rstd, am.chat = s.XHAT[t].data_ptr(), s.RSTD[t].data_ptr(), s.CHAT[t].data_ptr()
                 am.dlny, am.dlncy = DLNY[t].data_ptr(), DLNCY[t].data_ptr()
@@ -454,7 +455,7 @@ class _HyperSeq(torch.autograd.Function):
                     ROW_STATS["chain"] += 1
             if not ran:
                 _cell_bwd(lib, am, s.mln_on, 2 if s.VEC.dtype == torch.bfloat16 else 1, st, "hyper_main_bwd_step")
-            ah.c_prev = s.HCC[t].data_ptr()
+            ah.c_prev = (s.hc0 if t == 0 else s.HCC[t]).data_ptr()
             ah.xhat, ah.rstd, ah.chat = s.HXHAT[t].data_ptr(), s.HRSTD[t].data_ptr(), s.HCHAT[t].data_ptr()
             ah.step = t
             ah.dG = None if lp_on else dRY[t].data_ptr()
@@ -494,13 +495,15 @@ class _HyperSeq(torch.autograd.Function):
         # so it is exactly bf16(HH[t])) -- no conversion pass
         HHl = s.A[1:T + 1].reshape(TB, K)[:, H:] if lp_on else s.HH.view(TB, Hh)
         dP1, sV = gemm.wgrad(HHl, dVEC.view(TB, 12 * H), colsum=True)
-        g_ln, g_hln = [], []
-        for dy, xh, n, out in ((DLNY, s.XHAT, G, g_ln), (DLNCY, s.CHAT, H, g_ln), (HDLNY, s.HXHAT, Gh, g_hln),
-                               (HDLNCY, s.HCHAT, Hh, g_hln)):
-            if dy is None:   # plain main cell: no LayerNorm parameters
-                out += [None, None]
-                continue
-            out += list(colsum(dy.view(-1, n), xh.view(-1, n)))
+        # the four LayerNorm gamma / beta reductions in two launches (csrc/reduce.hip)
+        lnp = [(DLNY, s.XHAT, G), (DLNCY, s.CHAT, H)] if DLNY is not None else []
+        lnp += [(HDLNY, s.HXHAT, Gh), (HDLNCY, s.HCHAT, Hh)]
+        sums = colsum_many([(dy.view(-1, n), xh.view(-1, n)) for dy, xh, n in lnp])
+        flat = [v for pr in sums for v in pr]
+        if DLNY is None:   # plain main cell: no LayerNorm parameters
+            g_ln, g_hln = [None] * 4, flat
+        else:
+            g_ln, g_hln = flat[:4], flat[4:]
         dhW_x = torch.empty_like(s.hW_x)
         dhW_x[IN:] = dW_y[:H]
         dhW_h = dW_y[H:]

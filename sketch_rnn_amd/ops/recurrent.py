@@ -29,7 +29,7 @@ import torch
 from ..utils import native
 from . import gemm
 from ._hipapi import FusedBwdArgs, FusedFwdArgs, LstmBwdArgs, LstmFwdArgs
-from .reduce import colsum
+from .reduce import colsum_many
 
 
 def _ptr(t: Optional[torch.Tensor]):
@@ -405,12 +405,15 @@ class _LSTMSeq(torch.autograd.Function):
             dGn = dGs.view(T, nd, B, G).permute(1, 0, 2, 3).reshape(nd, T * B, G)
             dW = gemm.wgrad(An, dGn).view(s.wshape)
         g_ln = [None] * 4
-        if ln:
-            def red(x, y, n):   # per direction group: rows (t, b) of the [T, nd, B, n] stream
-                parts = [colsum(x.view(T, nd, B, n)[:, g], y.view(T, nd, B, n)[:, g]) for g in range(nd)]
+        if ln:   # gamma / beta: per direction group, rows (t, b) of the [T, nd, B, n] streams, one launch pair
+            parts = colsum_many([(x.view(T, nd, B, n)[:, g], y.view(T, nd, B, n)[:, g])
+                                 for x, y, n in ((DLNY, s.XHAT, G), (DLNCY, s.CHAT, H)) for g in range(nd)])
+
+            def red(k, n):
                 shape = s.lnp[0].shape[:-1] + (n,)
-                return torch.stack([p[0] for p in parts]).view(shape), torch.stack([p[1] for p in parts]).view(shape)
-            g_ln = list(red(DLNY, s.XHAT, G) + red(DLNCY, s.CHAT, H))
+                pk = parts[k * nd:(k + 1) * nd]
+                return torch.stack([p[0] for p in pk]).view(shape), torch.stack([p[1] for p in pk]).view(shape)
+            g_ln = list(red(0, G) + red(1, H))
         ctx.s = None
         return (dG, dW, dh_rec, dc_rec, dinit_h, dinit_c, g_ln[0], g_ln[1], g_ln[2], g_ln[3], None, None, None)
 

@@ -46,3 +46,61 @@ def colsum(x: torch.Tensor, y: Optional[torch.Tensor] = None, splits: Optional[i
     if rc != 0:
         raise RuntimeError("skr_colsum failed (%d)" % rc)
     return (tot[0] if y is not None else None), tot[1]
+
+
+def colsum_many(pairs, splits=None):
+    """:func:`colsum` of several ``(x, y)`` pairs (``[R, C]`` or ``[R1, R2, C]``
+    views with a contiguous last dim, y may be None) in two launches for all of them (csrc/reduce.hip
+    ``skr_colsum_multi``): the narrow reductions run beside the wide one
+    instead of each paying a kernel boundary and a tail. ``splits``: a list
+    of row-slice counts (default: :func:`colsum`'s, capped at 256 for
+    C <= 1024 so their second pass stays short). Same per-slice summation
+    order as :func:`colsum` with the same splits. Falls back to one
+    :func:`colsum` per pair off the vector path."""
+    from . import use_hip
+    pairs = [(x.unsqueeze(0), y.unsqueeze(0) if y is not None else None) if x.dim() == 2 else (x, y)
+             for x, y in pairs]
+    if not pairs or len(pairs) > 4 or not all(
+            use_hip(x) and x.dim() == 3 and x.stride(-1) == 1 and x.shape[-1] % 4 == 0 and x.stride(0) % 4 == 0
+            and x.stride(1) % 4 == 0
+            and x.dtype in (torch.bfloat16, torch.float32) and x.data_ptr() % 16 == 0
+            and (y is None or (y.shape == x.shape and y.stride() == x.stride() and y.data_ptr() % 16 == 0
+                               and y.dtype in (torch.bfloat16, torch.float32)))
+            for x, y in pairs):
+        return [colsum(x, y, splits[i] if splits else None) for i, (x, y) in enumerate(pairs)]
+    from ..utils import native
+    from ._hipapi import CsJob
+    lib = native.require_hip()
+    jobs = (CsJob * len(pairs))()
+    keep, outs = [], []
+    # narrow reductions first: dispatched ahead of the wide one's workgroups
+    order = sorted(range(len(pairs)), key=lambda i: pairs[i][0].shape[-1])
+    for slot, i in enumerate(order):
+        x, y = pairs[i]
+        R1, R2, C = x.shape
+        R = R1 * R2
+        if splits:
+            RS = splits[i]
+        else:
+            RS = -(-1024 // -(-C // 1024))
+            if C <= 1024:
+                RS = min(RS, 256)
+        RS = max(1, min(RS, R // 16))
+        part = torch.empty(2, RS, C, device=x.device, dtype=torch.float32)
+        tot = torch.empty(2, C, device=x.device, dtype=torch.float32)
+        J = jobs[slot]
+        J.X, J.Y = x.data_ptr(), (y.data_ptr() if y is not None else None)
+        J.R1, J.s1, J.R2, J.s2 = R1, x.stride(0), R2, x.stride(1)
+        J.C, J.RS = C, RS
+        J.xbf, J.ybf = int(x.dtype == torch.bfloat16), int(y is not None and y.dtype == torch.bfloat16)
+        J.part_xy, J.part_x = part[0].data_ptr(), part[1].data_ptr()
+        J.out_xy, J.out_x = tot[0].data_ptr(), tot[1].data_ptr()
+        keep.append(part)
+        outs.append((i, tot, y is not None))
+    rc = lib.lib.skr_colsum_multi(jobs, len(pairs), torch.cuda.current_stream().cuda_stream)
+    if rc != 0:
+        raise RuntimeError("skr_colsum_multi failed (%d)" % rc)
+    res = [None] * len(pairs)
+    for i, tot, hy in outs:
+        res[i] = ((tot[0] if hy else None), tot[1])
+    return res

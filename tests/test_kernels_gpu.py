@@ -669,6 +669,32 @@ def test_reference_model_bf16_grads_match_fp32():
         assert rel < 3e-2, (n, rel)
 
 
+def test_colsum_many_equals_colsum():
+    """skr_colsum_multi (several column reductions in one launch per pass, the
+    HyperLSTM LayerNorm gamma / beta gradients) equals one colsum per pair
+    bit for bit at the same row-slice counts, and the fp32 oracle."""
+    from sketch_rnn_amd.ops.reduce import colsum, colsum_many
+    torch.manual_seed(3)
+    R = 2500
+    pairs = [(torch.randn(R, C, device=DEV).to(dt), torch.randn(R, C, device=DEV).to(dt) if wy else None)
+             for C, dt, wy in ((8192, torch.bfloat16, True), (2048, torch.bfloat16, True), (256, torch.float32, True),
+                               (1024, torch.bfloat16, False))]
+    splits = [64, 128, 48, 100]
+    got = colsum_many(pairs, splits)
+    for (x, y), sp, (gxy, gx) in zip(pairs, splits, got):
+        rxy, rx = colsum(x, y, sp)
+        assert torch.equal(gx, rx)
+        assert (gxy is None) == (y is None)
+        if y is not None:
+            assert torch.equal(gxy, rxy)
+            ref = (x.float() * y.float()).sum(0)
+            assert (gxy - ref).abs().max().item() <= 1e-3 * ref.abs().max().item() + 1e-3
+    dflt = colsum_many(pairs)       # default slices (narrow ones capped): close to the oracle
+    for (x, y), (gxy, gx) in zip(pairs, dflt):
+        ref = x.float().sum(0)
+        assert (gx - ref).abs().max().item() <= 1e-3 * ref.abs().max().item() + 1e-3
+
+
 @pytest.mark.parametrize("shape,xdt,with_y", [((250, 100, 512), torch.float32, True), ((3, 7, 300), torch.bfloat16, False),
                                               ((250, 2, 100, 64), torch.float32, True),
                                               ((30000, 123), torch.float32, False)])   # the MDN head bias shape
