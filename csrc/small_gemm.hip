@@ -23,18 +23,19 @@ namespace {
 
 constexpr int TM = 64, TN = 64, TK = 32, NT = 256;
 
-__global__ __launch_bounds__(NT) void small_gemm_kernel(const float* __restrict__ A, int64_t sam, int64_t sak,
-                                                        const float* __restrict__ B, int64_t sbk, int64_t sbn,
-                                                        float* __restrict__ C, int64_t ldc, const float* __restrict__ bias,
-                                                        int M, int N, int K, int kslice, int acc,
-                                                        float* __restrict__ work, int S, int64_t a_batch,
-                                                        int64_t b_batch, int64_t c_batch) {
+// One 64 x 64 output tile (bx, by) of split / batch bz (= bt * S + s).
+__device__ __forceinline__ void small_gemm_tile(const float* __restrict__ A, int64_t sam, int64_t sak,
+                                                const float* __restrict__ B, int64_t sbk, int64_t sbn,
+                                                float* __restrict__ C, int64_t ldc, const float* __restrict__ bias,
+                                                int M, int N, int K, int kslice, int acc, float* __restrict__ work,
+                                                int S, int64_t a_batch, int64_t b_batch, int64_t c_batch, int bx, int by,
+                                                int bz) {
     // LDS rows padded to 68 floats: 16-byte aligned, so a thread's 4 rows /
     // 4 columns are one ds_read_b128 each
     __shared__ __attribute__((aligned(16))) float As[TK][TM + 4];
     __shared__ __attribute__((aligned(16))) float Bs[TK][TN + 4];
     const int tid = threadIdx.x, tx = tid & 15, ty = tid >> 4;
-    const int m0 = blockIdx.y * TM, n0 = blockIdx.x * TN, s = blockIdx.z % S, bt = blockIdx.z / S;
+    const int m0 = by * TM, n0 = bx * TN, s = bz % S, bt = bz / S;
     A += bt * a_batch;
     B += bt * b_batch;
     C += bt * c_batch;
@@ -108,18 +109,34 @@ __global__ __launch_bounds__(NT) void small_gemm_kernel(const float* __restrict_
     }
 }
 
-__global__ void small_gemm_reduce(const float* __restrict__ work, int S, int M, int N, float* __restrict__ C,
-                                  int64_t ldc, const float* __restrict__ bias, int acc, int64_t c_batch) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+__global__ __launch_bounds__(NT) void small_gemm_kernel(const float* __restrict__ A, int64_t sam, int64_t sak,
+                                                        const float* __restrict__ B, int64_t sbk, int64_t sbn,
+                                                        float* __restrict__ C, int64_t ldc, const float* __restrict__ bias,
+                                                        int M, int N, int K, int kslice, int acc,
+                                                        float* __restrict__ work, int S, int64_t a_batch,
+                                                        int64_t b_batch, int64_t c_batch) {
+    small_gemm_tile(A, sam, sak, B, sbk, sbn, C, ldc, bias, M, N, K, kslice, acc, work, S, a_batch, b_batch, c_batch,
+                    blockIdx.x, blockIdx.y, blockIdx.z);
+}
+
+__device__ __forceinline__ void small_gemm_sum(const float* __restrict__ work, int S, int M, int N,
+                                               float* __restrict__ C, int64_t ldc, const float* __restrict__ bias,
+                                               int acc, int64_t c_batch, int64_t i, int bt) {
     if (i >= (int64_t)M * N) return;
-    work += (int64_t)blockIdx.y * S * M * N;
-    C += blockIdx.y * c_batch;
+    work += (int64_t)bt * S * M * N;
+    C += bt * c_batch;
     const int m = (int)(i / N), n = (int)(i - (int64_t)m * N);
     float v = 0.f;
     for (int s = 0; s < S; ++s) v += work[(int64_t)s * M * N + i];
     v += bias ? bias[n] : 0.f;
     if (acc) v += C[m * ldc + n];
     C[m * ldc + n] = v;
+}
+
+__global__ void small_gemm_reduce(const float* __restrict__ work, int S, int M, int N, float* __restrict__ C,
+                                  int64_t ldc, const float* __restrict__ bias, int acc, int64_t c_batch) {
+    small_gemm_sum(work, S, M, N, C, ldc, bias, acc, c_batch, (int64_t)blockIdx.x * blockDim.x + threadIdx.x,
+                   blockIdx.y);
 }
 
 }  // namespace
@@ -166,3 +183,79 @@ SKR_API int skr_small_gemm(const float* A, int64_t sam, int64_t sak, const float
     return skr_small_gemm_batched(A, 0, sam, sak, B, 0, sbk, sbn, C, 0, ldc, bias, M, N, K, acc, 1, work, work_elems,
                                   s);
 }
+
+// ---- grouped launch -----------------------------------------------------------------
+// Up to kSgMax independent small products (each with its own shape, strides,
+// batch count and split factor -- the same tiles and the same split-K
+// summation order as skr_small_gemm_batched, so the results are identical)
+// in ONE launch, plus one launch summing the split-K partials of those that
+// split: the latent-node and hyper-projection gradients are groups of 2-4
+// such products per phase, each otherwise a launch (+ a reduce launch) of
+// its own.
+struct SgProb {
+    const float* A; int64_t sam, sak, a_batch;
+    const float* B; int64_t sbk, sbn, b_batch;
+    float* C; int64_t ldc, c_batch;
+    const float* bias;
+    int M, N, K, acc, nbatch;
+    float* work; int64_t work_elems;
+};
+constexpr int kSgMax = 6;
+
+namespace {
+struct SgPlan {
+    SgProb p[kSgMax];
+    int S[kSgMax], kslice[kSgMax];
+    int n;
+    int start[kSgMax + 1];     // tile workgroups: prefix of ntn * ntm * S * nbatch
+    int rstart[kSgMax + 1];    // reduce workgroups: prefix of ceil(M N / 256) * nbatch (S > 1 only)
+};
+
+__global__ __launch_bounds__(NT) void small_gemm_group_kernel(const SgPlan g) {
+    int q = 0;
+    while (q + 1 < g.n && (int)blockIdx.x >= g.start[q + 1]) ++q;
+    const SgProb& P = g.p[q];
+    const int ntn = (P.N + TN - 1) / TN, ntm = (P.M + TM - 1) / TM;
+    const int local = blockIdx.x - g.start[q];
+    const int bz = local / (ntn * ntm), rem = local - bz * ntn * ntm;
+    small_gemm_tile(P.A, P.sam, P.sak, P.B, P.sbk, P.sbn, P.C, P.ldc, P.bias, P.M, P.N, P.K, g.kslice[q], P.acc,
+                    g.S[q] > 1 ? P.work : nullptr, g.S[q], P.a_batch, P.b_batch, P.c_batch, rem % ntn, rem / ntn, bz);
+}
+
+__global__ __launch_bounds__(256) void small_gemm_group_reduce(const SgPlan g) {
+    int q = 0;
+    while (q + 1 < g.n && (int)blockIdx.x >= g.rstart[q + 1]) ++q;
+    const SgProb& P = g.p[q];
+    const int per = (int)(((int64_t)P.M * P.N + 255) / 256);
+    const int local = blockIdx.x - g.rstart[q];
+    const int bt = local / per;
+    small_gemm_sum(P.work, g.S[q], P.M, P.N, P.C, P.ldc, P.bias, P.acc, P.c_batch,
+                   (int64_t)(local - bt * per) * 256 + threadIdx.x, bt);
+}
+}  // namespace
+
+SKR_API int skr_small_gemm_group(const SgProb* probs, int n, hipStream_t s) {
+    if (n < 1 || n > kSgMax) return -2;
+    SgPlan g{};
+    g.n = n;
+    for (int q = 0; q < n; ++q) {
+        const SgProb& P = probs[q];
+        if (P.M <= 0 || P.N <= 0 || P.nbatch <= 0 || P.K <= 0) return -2;
+        int S = skr_small_gemm_splits(P.M, P.N, P.K);
+        int kslice = (P.K + S - 1) / S;
+        kslice = (kslice + TK - 1) / TK * TK;
+        S = (P.K + kslice - 1) / kslice;
+        if (S > 1 && (P.work == nullptr || P.work_elems < (int64_t)P.nbatch * S * P.M * P.N)) return -3;
+        g.p[q] = P;
+        g.S[q] = S;
+        g.kslice[q] = kslice;
+        g.start[q + 1] = g.start[q] + ((P.N + TN - 1) / TN) * ((P.M + TM - 1) / TM) * S * P.nbatch;
+        g.rstart[q + 1] = g.rstart[q] + (S > 1 ? (int)(((int64_t)P.M * P.N + 255) / 256) * P.nbatch : 0);
+    }
+    for (int q = n + 1; q <= kSgMax; ++q) g.start[q] = g.start[n], g.rstart[q] = g.rstart[n];
+    hipLaunchKernelGGL(small_gemm_group_kernel, dim3(g.start[n]), dim3(NT), 0, s, g);
+    if (g.rstart[n] > 0) hipLaunchKernelGGL(small_gemm_group_reduce, dim3(g.rstart[n]), dim3(256), 0, s, g);
+    return SKR_CHECK_LAUNCH();
+}
+
+SKR_API int skr_small_gemm_prob_size() { return (int)sizeof(SgProb); }

@@ -264,6 +264,18 @@ class GemmProblem(C.Structure):
     ]
 
 
+class SgProb(C.Structure):
+    """Mirror of ``SgProb`` in csrc/small_gemm.hip (one product of skr_small_gemm_group)."""
+    _fields_ = [
+        ("A", _p), ("sam", _i64), ("sak", _i64), ("a_batch", _i64),
+        ("B", _p), ("sbk", _i64), ("sbn", _i64), ("b_batch", _i64),
+        ("C", _p), ("ldc", _i64), ("c_batch", _i64),
+        ("bias", _p),
+        ("M", _i), ("N", _i), ("K", _i), ("acc", _i), ("nbatch", _i),
+        ("work", _p), ("work_elems", _i64),
+    ]
+
+
 class CsJob(C.Structure):
     """Mirror of ``CsJob`` in csrc/reduce.hip (one column reduction of skr_colsum_multi)."""
     _fields_ = [
@@ -393,6 +405,8 @@ class HipLib:
         lib.skr_lstm_persist_fwd.restype = _i
         lib.skr_lstm_persist_bwd.argtypes = [C.POINTER(PBwdArgs), _p]
         lib.skr_lstm_persist_bwd.restype = _i
+        lib.skr_small_gemm_group.argtypes = [C.POINTER(SgProb), _i, _p]
+        lib.skr_small_gemm_group.restype = _i
         lib.skr_colsum_multi.argtypes = [C.POINTER(CsJob), _i, _p]
         lib.skr_colsum_multi.restype = _i
         lib.skr_persist_set_spin_limit.argtypes = [C.c_uint]
@@ -429,7 +443,8 @@ class HipLib:
                           ("skr_gemm_problem_size", GemmProblem),
                           ("skr_decode_sample_size", DecodeSample),
                           ("skr_chain_sync_size", ChainSync),
-                          ("skr_colsum_job_size", CsJob)):
+                          ("skr_colsum_job_size", CsJob),
+                          ("skr_small_gemm_prob_size", SgProb)):
             fn = getattr(lib, name)
             fn.restype = _i
             if fn() != C.sizeof(cls):

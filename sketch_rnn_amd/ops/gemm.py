@@ -106,6 +106,73 @@ def small_mm_batched(a: torch.Tensor, a_off: int, a_batch: int, sam: int, sak: i
         raise RuntimeError("skr_small_gemm_batched failed (%d) for M=%d N=%d K=%d x%d" % (rc, M, N, K, nbatch))
 
 
+class SmallGroup:
+    """Independent :func:`small_mm` / :func:`small_mm_batched` products
+    collected and run as ONE grouped launch (+ one split-K sum launch;
+    ``csrc/small_gemm.hip`` ``skr_small_gemm_group``): the same tiles and
+    summation order as the single calls, so the results are identical. On
+    the CPU each product runs immediately. Usage::
+
+        g = SmallGroup(device)
+        mu = g.mm(h, w_mu, b_mu)
+        ps = g.mm(h, w_sig, b_sig)
+        g.run()            # mu, ps are valid after this
+    """
+
+    MAX = 6
+
+    def __init__(self, device):
+        self.dev = torch.device(device)
+        self.items = []
+
+    def mm(self, a, b, bias=None, out=None, acc=False):
+        if not a.is_cuda:
+            return small_mm(a, b, bias, out, acc)
+        M, K = a.shape
+        N = b.shape[1]
+        assert a.dtype == b.dtype == torch.float32 and b.shape[0] == K
+        if out is None:
+            out = torch.empty(M, N, device=a.device)
+        assert out.stride(1) == 1 and out.shape == (M, N)
+        bc = bias.contiguous() if bias is not None else None
+        self.items.append(dict(A=a, a_off=0, sam=a.stride(0), sak=a.stride(1), a_batch=0, B=b, b_off=0,
+                               sbk=b.stride(0), sbn=b.stride(1), b_batch=0, C=out, c_off=0, ldc=out.stride(0),
+                               c_batch=0, bias=bc, M=M, N=N, K=K, acc=int(acc), nbatch=1))
+        return out
+
+    def batched(self, a, a_off, a_batch, sam, sak, b, b_off, b_batch, sbk, sbn, c, c_off, c_batch, ldc, M, N, K,
+                nbatch, acc=False):
+        assert a.is_cuda and a.dtype == b.dtype == c.dtype == torch.float32
+        self.items.append(dict(A=a, a_off=a_off, sam=sam, sak=sak, a_batch=a_batch, B=b, b_off=b_off, sbk=sbk,
+                               sbn=sbn, b_batch=b_batch, C=c, c_off=c_off, ldc=ldc, c_batch=c_batch, bias=None,
+                               M=M, N=N, K=K, acc=int(acc), nbatch=nbatch))
+
+    def run(self) -> None:
+        if not self.items:
+            return
+        from ..utils import native
+        from ._hipapi import SgProb
+        lib = native.require_hip().lib
+        for i0 in range(0, len(self.items), self.MAX):
+            chunk = self.items[i0:i0 + self.MAX]
+            probs = (SgProb * len(chunk))()
+            keep = []
+            for p, it in zip(probs, chunk):
+                S = lib.skr_small_gemm_splits(it["M"], it["N"], it["K"])
+                work = torch.empty(it["nbatch"] * S * it["M"] * it["N"] if S > 1 else 1, device=self.dev)
+                keep.append(work)
+                p.A, p.sam, p.sak, p.a_batch = it["A"].data_ptr() + 4 * it["a_off"], it["sam"], it["sak"], it["a_batch"]
+                p.B, p.sbk, p.sbn, p.b_batch = it["B"].data_ptr() + 4 * it["b_off"], it["sbk"], it["sbn"], it["b_batch"]
+                p.C, p.ldc, p.c_batch = it["C"].data_ptr() + 4 * it["c_off"], it["ldc"], it["c_batch"]
+                p.bias = it["bias"].data_ptr() if it["bias"] is not None else None
+                p.M, p.N, p.K, p.acc, p.nbatch = it["M"], it["N"], it["K"], it["acc"], it["nbatch"]
+                p.work, p.work_elems = work.data_ptr(), work.numel()
+            rc = lib.skr_small_gemm_group(probs, len(chunk), torch.cuda.current_stream().cuda_stream)
+            if rc != 0:
+                raise RuntimeError("skr_small_gemm_group failed (%d)" % rc)
+        self.items = []
+
+
 def bmm(a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
     if a.dtype == torch.float32 and b.dtype == torch.float32:
         return torch.bmm(a, b, out=out) if out is not None else torch.bmm(a, b)

@@ -89,11 +89,14 @@ def _hyper_proj_grads(dP1, sV, s, Hh, H, E):
         db_z = torch.empty(12 * E, device=dev)
         dWa = torch.empty(12, E, H, device=dev)
         # dW_a[j] = W_z[:, jE:(j+1)E]^T dP[:, jH:(j+1)H] + b_z[jE:(j+1)E] (x) sV[jH:(j+1)H]
-        gemm.small_mm_batched(bz, 0, E, 1, 0, sV, 0, H, 0, 1, dWa, 0, E * H, H, E, H, 1, 12)
-        gemm.small_mm_batched(Wz, 0, E, 1, 12 * E, dP1, 0, H, NC, 1, dWa, 0, E * H, H, E, H, Hh, 12, acc=True)
         # dW_z[:, jE:(j+1)E] = dP[:, jH:(j+1)H] W_a[j]^T;  db_z[jE:(j+1)E] = sV[jH:(j+1)H] W_a[j]^T
-        gemm.small_mm_batched(dP1, 0, H, NC, 1, Wa, 0, E * H, 1, H, dW_z, 0, E, 12 * E, Hh, E, H, 12)
-        gemm.small_mm_batched(sV, 0, H, 0, 1, Wa, 0, E * H, 1, H, db_z, 0, E, 0, 1, E, H, 12)
+        # (the three independent products in one launch, then the accumulation into dW_a)
+        g = gemm.SmallGroup(dev)
+        g.batched(bz, 0, E, 1, 0, sV, 0, H, 0, 1, dWa, 0, E * H, H, E, H, 1, 12)
+        g.batched(dP1, 0, H, NC, 1, Wa, 0, E * H, 1, H, dW_z, 0, E, 12 * E, Hh, E, H, 12)
+        g.batched(sV, 0, H, 0, 1, Wa, 0, E * H, 1, H, db_z, 0, E, 0, 1, E, H, 12)
+        g.run()
+        gemm.small_mm_batched(Wz, 0, E, 1, 12 * E, dP1, 0, H, NC, 1, dWa, 0, E * H, H, E, H, Hh, 12, acc=True)
         return dW_z, db_z, dWa, sV[8 * H:].reshape(4 * H)
     dP = dP1.view(Hh, 12, H).transpose(0, 1)                       # [12, Hh, H]
     sV = sV.view(12, H)
@@ -135,8 +138,13 @@ class _HyperSeq(torch.autograd.Function):
         bp = bproj_ok(x) and not x.requires_grad
         xl = None
         if bp:   # stroke rows per position, z rows once per sequence (csrc/inproj.hip)
-            XH = bproj_fwd(x, W_x[:IX], gemm.small_mm(zc, W_x[IX:]) if zc is not None else None)
-            XHY = bproj_fwd(x, hW_x[:IX], gemm.small_mm(zc, hW_x[IX:IN]) if zc is not None else None)
+            zw = zwy = None
+            if zc is not None:   # both z projections in one launch
+                g = gemm.SmallGroup(dev)
+                zw, zwy = g.mm(zc, W_x[IX:]), g.mm(zc, hW_x[IX:IN])
+                g.run()
+            XH = bproj_fwd(x, W_x[:IX], zw)
+            XHY = bproj_fwd(x, hW_x[:IX], zwy)
         else:
             if zc is not None:
                 x = torch.cat([x, zc.unsqueeze(0).expand(T, B, zc.shape[-1])], -1)
@@ -514,10 +522,12 @@ class _HyperSeq(torch.autograd.Function):
             if s.zc is not None:
                 dW_x = torch.empty_like(s.W_x)
                 dW_x[:IX] = P_m
-                gemm.small_mm(s.zc.t(), S_m, out=dW_x[IX:])
                 dhW_x[:IX] = P_y
-                gemm.small_mm(s.zc.t(), S_y, out=dhW_x[IX:IN])
-                dzc = gemm.small_mm(S_m, s.W_x[IX:].t())
+                g = gemm.SmallGroup(dev)   # the three independent z-side products in one launch
+                g.mm(s.zc.t(), S_m, out=dW_x[IX:])
+                g.mm(s.zc.t(), S_y, out=dhW_x[IX:IN])
+                dzc = g.mm(S_m, s.W_x[IX:].t())
+                g.run()
                 gemm.small_mm(S_y, s.hW_x[IX:IN].t(), out=dzc, acc=True)
             else:
                 dW_x = P_m

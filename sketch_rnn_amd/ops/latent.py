@@ -21,8 +21,8 @@ from typing import Optional, Sequence
 import torch
 
 from ..utils import native
-from .gemm import small_mm
-from .reduce import colsum
+from .gemm import SmallGroup, small_mm
+from .reduce import colsum_many
 
 
 def latent_ok(h: torch.Tensor, n_seg: int) -> bool:
@@ -42,8 +42,10 @@ class _Latent(torch.autograd.Function):
         lib = native.require_hip().lib
         st = torch.cuda.current_stream().cuda_stream
         h = h.contiguous()
-        mu = small_mm(h, w_mu, b_mu)
-        ps = small_mm(h, w_sig, b_sig)
+        g = SmallGroup(h.device)   # the two heads in one launch
+        mu = g.mm(h, w_mu, b_mu)
+        ps = g.mm(h, w_sig, b_sig)
+        g.run()
         B, Z = mu.shape
         dev = h.device
         z = torch.empty(B, Z, device=dev)
@@ -82,9 +84,10 @@ class _Latent(torch.autograd.Function):
         rc = lib.skr_tanh_split_bwd(B, S, len(widths), wa, _ptrs(segs), _ptrs(dsegs), dpre.data_ptr(), st)
         if rc != 0:
             raise RuntimeError("skr_tanh_split_bwd failed (%d)" % rc)
-        dW_init = small_mm(z.t(), dpre)
-        db_init = colsum(dpre)[1]
-        dz_int = small_mm(dpre, w_init.t())
+        g = SmallGroup(dev)
+        dW_init = g.mm(z.t(), dpre)
+        dz_int = g.mm(dpre, w_init.t())
+        g.run()
         dmu_t = torch.empty(B, Z, device=dev)
         dps_t = torch.empty(B, Z, device=dev)
         c = lambda t: t.contiguous() if t is not None else None   # noqa: E731
@@ -95,11 +98,14 @@ class _Latent(torch.autograd.Function):
                                     dps_t.data_ptr(), st)
         if rc != 0:
             raise RuntimeError("skr_latent_mid_bwd failed (%d)" % rc)
-        dh = small_mm(dmu_t, w_mu.t())
+        g = SmallGroup(dev)
+        dh = g.mm(dmu_t, w_mu.t())
+        dW_mu = g.mm(h.t(), dmu_t)
+        dW_sig = g.mm(h.t(), dps_t)
+        g.run()
         small_mm(dps_t, w_sig.t(), out=dh, acc=True)
-        dW_mu = small_mm(h.t(), dmu_t)
-        dW_sig = small_mm(h.t(), dps_t)
-        return dh, dW_mu, colsum(dmu_t)[1], dW_sig, colsum(dps_t)[1], dW_init, db_init, None, None, None
+        (_, db_init), (_, db_mu), (_, db_sig) = colsum_many([(dpre, None), (dmu_t, None), (dps_t, None)])
+        return dh, dW_mu, db_mu, dW_sig, db_sig, dW_init, db_init, None, None, None
 
 
 def latent(h, w_mu, b_mu, w_sig, b_sig, w_init, b_init, seed: torch.Tensor, widths: Sequence[int],

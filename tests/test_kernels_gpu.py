@@ -872,6 +872,32 @@ def test_hyper_fold_kernels_vs_torch(Hh, H, E):
         assert torch.allclose(a, b, rtol=1e-4, atol=1e-3 * float(b.abs().max())), float((a - b).abs().max())
 
 
+def test_small_gemm_group_equals_single_launches():
+    """skr_small_gemm_group (several small products -- different shapes,
+    strides, batch counts, split factors, bias / accumulate -- in one launch
+    + one split-K sum launch) equals the one-launch-per-product results bit
+    for bit (same tiles, same split-K order)."""
+    from sketch_rnn_amd.ops import gemm
+    torch.manual_seed(9)
+    h, w1, w2 = torch.randn(100, 1024, device=DEV), torch.randn(1024, 128, device=DEV), torch.randn(1024, 128, device=DEV)
+    b1 = torch.randn(128, device=DEV)
+    z, d = torch.randn(100, 128, device=DEV), torch.randn(100, 4608, device=DEV)
+    acc0 = torch.randn(100, 1024, device=DEV)
+    A, Bm = torch.randn(12 * 32, device=DEV), torch.randn(12 * 512, device=DEV)
+    ref = [gemm.small_mm(h, w1, b1), gemm.small_mm(h, w2), gemm.small_mm(z.t(), d),
+           gemm.small_mm(d[:, :128], w1.t(), out=acc0.clone(), acc=True)]
+    cb = torch.zeros(12, 32, 512, device=DEV)
+    gemm.small_mm_batched(A, 0, 32, 1, 0, Bm, 0, 512, 0, 1, cb, 0, 32 * 512, 512, 32, 512, 1, 12)
+    g = gemm.SmallGroup(DEV)
+    got = [g.mm(h, w1, b1), g.mm(h, w2), g.mm(z.t(), d), g.mm(d[:, :128], w1.t(), out=acc0.clone(), acc=True)]
+    cg = torch.zeros(12, 32, 512, device=DEV)
+    g.batched(A, 0, 32, 1, 0, Bm, 0, 512, 0, 1, cg, 0, 32 * 512, 512, 32, 512, 1, 12)
+    g.run()
+    for a, b in zip(got + [cg], ref + [cb]):
+        assert torch.equal(a, b)
+    assert torch.allclose(ref[0], h @ w1 + b1, rtol=1e-4, atol=1e-3)
+
+
 @pytest.mark.parametrize("M,N,K,ta,tb,bias,acc", [(100, 128, 1024, False, False, True, False),
                                                   (100, 4608, 128, False, False, True, False),
                                                   (128, 4608, 100, True, False, False, False),
