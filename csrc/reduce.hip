@@ -210,62 +210,100 @@ __device__ __forceinline__ void ld4(const void* x, int64_t i, bool bf, float (&v
     else ldv<false, 4>(x, i, v);
 }
 
+// Thread mapping per job: cq = min(C / 4, 256) column quads x rg = 256 / cq
+// row groups per workgroup (narrow reductions: C = 256 -> 64 x 4), the
+// workgroup's rows split over the row groups and the groups summed in LDS
+// in a fixed order, one partial row per workgroup: narrow reductions keep
+// 256 threads busy per workgroup and few rows in flight per thread.
 __global__ __launch_bounds__(256) void colsum_multi_kernel(const CsJobs jobs) {
+    __shared__ float red[2][256][4];
     int q = 0;
     while (q + 1 < jobs.n && (int)blockIdx.x >= jobs.start[q + 1]) ++q;
     const CsJob& J = jobs.j[q];
     const int local = blockIdx.x - jobs.start[q];
-    const int cb = (J.C / 4 + 255) / 256;
+    const int cq = min(J.C / 4, 256), rg = 256 / cq;
+    const int cb = (J.C / 4 + cq - 1) / cq;
     const int rs = local / cb, cbi = local - rs * cb;
-    const int c = (cbi * 256 + threadIdx.x) * 4;
-    if (c >= J.C) return;
+    const int tq = threadIdx.x % cq, grp = threadIdx.x / cq;
+    const int c = (cbi * cq + tq) * 4;
+    const bool on = c < J.C && grp < rg;
     const int64_t R = J.R1 * J.R2;
     const int64_t per = (R + J.RS - 1) / J.RS;
-    const int64_t r0 = rs * per, r1 = min(R, r0 + per);
+    const int64_t w0 = rs * per, w1 = min(R, w0 + per);
+    const int64_t gper = (w1 - w0 + rg - 1) / rg;
+    const int64_t r0 = w0 + grp * gper, r1 = min(w1, r0 + gper);
     float sxy[4] = {0.f, 0.f, 0.f, 0.f}, sx[4] = {0.f, 0.f, 0.f, 0.f};
-    int64_t i = r0 / J.R2, j = r0 % J.R2;
-    int64_t r = r0;
-    for (; r + 2 <= r1; r += 2) {
-        float xv[2][4], yv[2][4];
+    if (on && r0 < r1) {
+        int64_t i = r0 / J.R2, j = r0 % J.R2;
+        int64_t r = r0;
+        for (; r + 2 <= r1; r += 2) {
+            float xv[2][4], yv[2][4];
 #pragma unroll
-        for (int k = 0; k < 2; ++k) {
+            for (int k = 0; k < 2; ++k) {
+                const int64_t off = i * J.s1 + j * J.s2 + c;
+                ld4(J.X, off, J.xbf, xv[k]);
+                if (J.Y) ld4(J.Y, off, J.ybf, yv[k]);
+                else
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) yv[k][e] = 0.f;
+                if (++j == J.R2) {
+                    j = 0;
+                    ++i;
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < 2; ++k)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    sx[e] += xv[k][e];
+                    sxy[e] += xv[k][e] * yv[k][e];
+                }
+        }
+        for (; r < r1; ++r) {
             const int64_t off = i * J.s1 + j * J.s2 + c;
-            ld4(J.X, off, J.xbf, xv[k]);
-            if (J.Y) ld4(J.Y, off, J.ybf, yv[k]);
-            else
+            float xv[4], yv[4] = {0.f, 0.f, 0.f, 0.f};
+            ld4(J.X, off, J.xbf, xv);
+            if (J.Y) ld4(J.Y, off, J.ybf, yv);
 #pragma unroll
-                for (int e = 0; e < 4; ++e) yv[k][e] = 0.f;
+            for (int e = 0; e < 4; ++e) {
+                sx[e] += xv[e];
+                sxy[e] += xv[e] * yv[e];
+            }
             if (++j == J.R2) {
                 j = 0;
                 ++i;
             }
         }
-#pragma unroll
-        for (int k = 0; k < 2; ++k)
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                sx[e] += xv[k][e];
-                sxy[e] += xv[k][e] * yv[k][e];
-            }
-    }
-    for (; r < r1; ++r) {
-        const int64_t off = i * J.s1 + j * J.s2 + c;
-        float xv[4], yv[4] = {0.f, 0.f, 0.f, 0.f};
-        ld4(J.X, off, J.xbf, xv);
-        if (J.Y) ld4(J.Y, off, J.ybf, yv);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-            sx[e] += xv[e];
-            sxy[e] += xv[e] * yv[e];
-        }
-        if (++j == J.R2) {
-            j = 0;
-            ++i;
-        }
     }
     const int64_t o = (int64_t)rs * J.C + c;
-    *(float4*)(J.part_x + o) = float4{sx[0], sx[1], sx[2], sx[3]};
-    if (J.Y) *(float4*)(J.part_xy + o) = float4{sxy[0], sxy[1], sxy[2], sxy[3]};
+    if (rg == 1) {
+        if (on) {
+            *(float4*)(J.part_x + o) = float4{sx[0], sx[1], sx[2], sx[3]};
+            if (J.Y) *(float4*)(J.part_xy + o) = float4{sxy[0], sxy[1], sxy[2], sxy[3]};
+        }
+        return;
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        red[0][threadIdx.x][e] = sx[e];
+        red[1][threadIdx.x][e] = sxy[e];
+    }
+    __syncthreads();
+    if (grp != 0 || !on) return;
+    float tx[4], txy[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        tx[e] = red[0][tq][e];
+        txy[e] = red[1][tq][e];
+    }
+    for (int g2 = 1; g2 < rg; ++g2)   // fixed order: deterministic
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            tx[e] += red[0][g2 * cq + tq][e];
+            txy[e] += red[1][g2 * cq + tq][e];
+        }
+    *(float4*)(J.part_x + o) = float4{tx[0], tx[1], tx[2], tx[3]};
+    if (J.Y) *(float4*)(J.part_xy + o) = float4{txy[0], txy[1], txy[2], txy[3]};
 }
 
 // colsum_finish of every job, one launch (the same fixed summation order)
@@ -317,7 +355,9 @@ SKR_API int skr_colsum_multi(const CsJob* jobs, int n, hipStream_t s) {
             (((uintptr_t)J.part_x | (uintptr_t)(J.Y ? J.part_xy : J.part_x)) & 15))
             return -4;
         g.j[q] = J;
-        g.start[q + 1] = g.start[q] + J.RS * ((J.C / 4 + 255) / 256);
+        const int cq = J.C / 4 < 256 ? J.C / 4 : 256;
+        if (256 % cq != 0 && cq != 256) return -2;   // narrow C: C / 4 must divide 256
+        g.start[q + 1] = g.start[q] + J.RS * ((J.C / 4 + cq - 1) / cq);
         g.fstart[q + 1] = g.fstart[q] + (J.C + 63) / 64;
     }
     for (int q = n + 1; q <= kCsMax; ++q) g.start[q] = g.start[n], g.fstart[q] = g.fstart[n];

@@ -54,14 +54,17 @@ def colsum_many(pairs, splits=None):
     ``skr_colsum_multi``): the narrow reductions run beside the wide one
     instead of each paying a kernel boundary and a tail. ``splits``: a list
     of row-slice counts (default: :func:`colsum`'s, capped at 256 for
-    C <= 1024 so their second pass stays short). Same per-slice summation
-    order as :func:`colsum` with the same splits. Falls back to one
-    :func:`colsum` per pair off the vector path."""
+    C <= 1024 so their second pass stays short). C >= 1024: the same
+    per-slice summation order as :func:`colsum` with the same splits;
+    narrower reductions split each slice over row groups of one workgroup
+    (summed in a fixed order). Falls back to one :func:`colsum` per pair
+    off the vector path."""
     from . import use_hip
     pairs = [(x.unsqueeze(0), y.unsqueeze(0) if y is not None else None) if x.dim() == 2 else (x, y)
              for x, y in pairs]
     if not pairs or len(pairs) > 4 or not all(
             use_hip(x) and x.dim() == 3 and x.stride(-1) == 1 and x.shape[-1] % 4 == 0 and x.stride(0) % 4 == 0
+            and (x.shape[-1] >= 1024 or 256 % (x.shape[-1] // 4) == 0)
             and x.stride(1) % 4 == 0
             and x.dtype in (torch.bfloat16, torch.float32) and x.data_ptr() % 16 == 0
             and (y is None or (y.shape == x.shape and y.stride() == x.stride() and y.data_ptr() % 16 == 0

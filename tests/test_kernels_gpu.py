@@ -386,40 +386,76 @@ def test_hyper_long_sequence_vs_oracle():
     assert ok, ("bf16 out, t < 20", err)
 
 
-def test_hyper_bf16_gradients_b100_t50_cosine():
-    """Shipped numerics at the headline geometry: B = 100 rows (the fused
-    forward / backward launches, the row-kernel backward), H = 2048, T = 50,
-    the model's own initialisation, dropout on. Every weight gradient of the
-    bf16 HIP path points the same way as the fp32 oracle's: cosine >= 0.98
-    (measured 0.996-0.998; b_z >= 0.95, see below); for scale, the same statistic of
-    the oracle against itself with the input perturbed by 1e-6 is recorded
-    in the assertion message."""
-    p, x, z, st, w = _hyper_setup(21, 50, 100, 5, 16, 2048, 256, 32, jitter=0.0, state=0.0)
-    runs = {}
-    for name, backend, dt, xx in (("ref", "torch", "fp32", x), ("pert", "torch", "fp32", x + 1e-6 * torch.randn_like(x)),
-                                  ("bf16", "hip", "bf16", x)):
-        ops.set_backend(backend)
-        ops.set_compute_dtype(dt)
-        runs[name] = _hyper_run(p, xx, z, st, w, keep=0.9, hkeep=0.9, fin_w=False)
-    ops.set_compute_dtype("fp32")
-    names = _names(p)
-    bad, seen = [], {}
+def _grad_cosines(runs, names, arm, ref="ref"):
+    out = {}
     for i, n in enumerate(names):
         if n in ("out", "h", "c", "hh", "hc"):
             continue
-        ref, got, pert = (runs[k][i].double().flatten() for k in ("ref", "bf16", "pert"))
-        if ref.norm() == 0:
+        r, g = runs[ref][i].double().flatten(), runs[arm][i].double().flatten()
+        if r.norm() == 0:
             continue
-        cos = float(got @ ref / (got.norm() * ref.norm()))
-        cos_p = float(pert @ ref / (pert.norm() * ref.norm()))
-        seen[n] = round(cos, 5)
-        # b_z's gradient is a column sum of the bf16-stored dvec over all T*B
-        # rows that cancels to ~1e-2 of its terms' magnitude, so the storage
-        # rounding of the terms (not the kernels) bounds it: measured 0.977
-        if cos < (0.95 if n == "b_z" else 0.98):
-            bad.append((n, cos, cos_p))
-    print("gradient cosines (bf16 HIP vs fp32 oracle):", seen)
-    assert not bad, (bad, seen)
+        out[n] = float(g @ r / (g.norm() * r.norm()))
+    return out
+
+
+def test_hyper_bf16_gradients_b100_t50_cosine():
+    """Shipped numerics at the headline geometry: B = 100 rows (the fused
+    forward / backward launches, the chained row-kernel backward), H = 2048,
+    T = 50, the model's own initialisation, dropout on. Every weight gradient
+    of the bf16 HIP path points the same way as the fp32 oracle's: cosine >=
+    0.98 (measured 0.996-0.998; b_z >= 0.95: its gradient is a column sum of
+    the bf16-stored dvec over all T*B rows that cancels to ~1e-2 of its
+    terms' magnitude, so the storage rounding of the terms bounds it)."""
+    p, x, z, st, w = _hyper_setup(21, 50, 100, 5, 16, 2048, 256, 32, jitter=0.0, state=0.0)
+    runs = {}
+    for name, backend, dt in (("ref", "torch", "fp32"), ("bf16", "hip", "bf16")):
+        ops.set_backend(backend)
+        ops.set_compute_dtype(dt)
+        runs[name] = _hyper_run(p, x, z, st, w, keep=0.9, hkeep=0.9, fin_w=False)
+    ops.set_compute_dtype("fp32")
+    cos = _grad_cosines(runs, _names(p), "bf16")
+    print("T=50 gradient cosines (bf16 HIP vs fp32 oracle):", cos)
+    bad = [(n, c) for n, c in cos.items() if c < (0.95 if n == "b_z" else 0.98)]
+    assert not bad, (bad, cos)
+
+
+def test_hyper_t250_b100_gradients():
+    """The full T = 250 at B = 100, H = 2048. With the model's own
+    initialisation the recurrence is chaotic over 250 steps: bf16 rounding
+    (~1e-2 per step) decorrelates the late trajectory from the fp32 one
+    (measured gradient cosines ~0: no fixed tolerance separates a kernel bug
+    from rounding there -- profiles/r3/long_seq_drift.jsonl). So, at the full
+    geometry: (1) the HIP fp32 path tracks the fp32 oracle -- every weight
+    gradient's cosine within 0.05 of the oracle's own cosine under a 1e-6
+    input perturbation; (2) with contractive recurrent weights (W_h, hyp_W_h
+    x 0.25: perturbations decay instead of growing) the bf16 path -- chained
+    backward launches, bf16 modulation vectors, row kernels -- matches the
+    oracle over all 250 steps: cosine >= 0.98 (b_z >= 0.95)."""
+    p, x, z, st, w = _hyper_setup(21, 250, 100, 5, 16, 2048, 256, 32, jitter=0.0, state=0.0)
+    runs = {}
+    for name, backend, dt, xx in (("ref", "torch", "fp32", x), ("pert", "torch", "fp32", x + 1e-6 * torch.randn_like(x)),
+                                  ("hip32", "hip", "fp32", x), ("bf16", "hip", "bf16", x)):
+        ops.set_backend(backend)
+        ops.set_compute_dtype(dt)
+        runs[name] = _hyper_run(p, xx, z, st, w, keep=0.9, hkeep=0.9, fin_w=False)
+    names = _names(p)
+    c32, cp, c16 = (_grad_cosines(runs, names, a) for a in ("hip32", "pert", "bf16"))
+    print("T=250 cosines: hip fp32", c32, "oracle perturbed", cp, "bf16 (chaotic)", c16)
+    bad = [(n, c32[n], cp[n]) for n in c32 if c32[n] < cp[n] - 0.05]
+    assert not bad, ("hip fp32 vs oracle", bad)
+    with torch.no_grad():
+        p.W_h.mul_(0.25)
+        p.hyp_W_h.mul_(0.25)
+    runs = {}
+    for name, backend, dt in (("ref", "torch", "fp32"), ("bf16", "hip", "bf16")):
+        ops.set_backend(backend)
+        ops.set_compute_dtype(dt)
+        runs[name] = _hyper_run(p, x, z, st, w, keep=0.9, hkeep=0.9, fin_w=False)
+    ops.set_compute_dtype("fp32")
+    c16 = _grad_cosines(runs, names, "bf16")
+    print("T=250 contractive: bf16 cosines", c16)
+    bad = [(n, c) for n, c in c16.items() if c < (0.95 if n == "b_z" else 0.98)]
+    assert not bad, ("bf16 vs oracle, contractive", bad, c16)
 
 
 @pytest.mark.parametrize("M,N,K,nd", [(100, 9216, 2304, 1), (100, 2304, 9216, 1), (100, 256, 24576, 1),
@@ -672,7 +708,9 @@ def test_reference_model_bf16_grads_match_fp32():
 def test_colsum_many_equals_colsum():
     """skr_colsum_multi (several column reductions in one launch per pass, the
     HyperLSTM LayerNorm gamma / beta gradients) equals one colsum per pair
-    bit for bit at the same row-slice counts, and the fp32 oracle."""
+    bit for bit at the same row-slice counts for C >= 1024 (narrower ones
+    split a slice over row groups: a different fixed order), and every
+    result the fp32 oracle."""
     from sketch_rnn_amd.ops.reduce import colsum, colsum_many
     torch.manual_seed(3)
     R = 2500
@@ -683,10 +721,14 @@ def test_colsum_many_equals_colsum():
     got = colsum_many(pairs, splits)
     for (x, y), sp, (gxy, gx) in zip(pairs, splits, got):
         rxy, rx = colsum(x, y, sp)
-        assert torch.equal(gx, rx)
         assert (gxy is None) == (y is None)
+        if x.shape[1] >= 1024:
+            assert torch.equal(gx, rx)
+            if y is not None:
+                assert torch.equal(gxy, rxy)
+        refx = x.float().sum(0)
+        assert (gx - refx).abs().max().item() <= 1e-3 * refx.abs().max().item() + 1e-3
         if y is not None:
-            assert torch.equal(gxy, rxy)
             ref = (x.float() * y.float()).sum(0)
             assert (gxy - ref).abs().max().item() <= 1e-3 * ref.abs().max().item() + 1e-3
     dflt = colsum_many(pairs)       # default slices (narrow ones capped): close to the oracle
