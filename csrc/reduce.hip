@@ -205,8 +205,11 @@ struct CsJobs {
 
 namespace {
 
+// KIND 0: operand dtypes read per job at run time; KIND 1: every X and Y
+// bf16 (the LayerNorm saves of bf16 training), fixed at compile time
+template <int KIND>
 __device__ __forceinline__ void ld4(const void* x, int64_t i, bool bf, float (&v)[4]) {
-    if (bf) ldv<true, 4>(x, i, v);
+    if (KIND == 1 || bf) ldv<true, 4>(x, i, v);
     else ldv<false, 4>(x, i, v);
 }
 
@@ -215,6 +218,7 @@ __device__ __forceinline__ void ld4(const void* x, int64_t i, bool bf, float (&v
 // workgroup's rows split over the row groups and the groups summed in LDS
 // in a fixed order, one partial row per workgroup: narrow reductions keep
 // 256 threads busy per workgroup and few rows in flight per thread.
+template <int KIND>
 __global__ __launch_bounds__(256) void colsum_multi_kernel(const CsJobs jobs) {
     __shared__ float red[2][256][4];
     int q = 0;
@@ -241,8 +245,8 @@ __global__ __launch_bounds__(256) void colsum_multi_kernel(const CsJobs jobs) {
 #pragma unroll
             for (int k = 0; k < 2; ++k) {
                 const int64_t off = i * J.s1 + j * J.s2 + c;
-                ld4(J.X, off, J.xbf, xv[k]);
-                if (J.Y) ld4(J.Y, off, J.ybf, yv[k]);
+                ld4<KIND>(J.X, off, J.xbf, xv[k]);
+                if (J.Y) ld4<KIND>(J.Y, off, J.ybf, yv[k]);
                 else
 #pragma unroll
                     for (int e = 0; e < 4; ++e) yv[k][e] = 0.f;
@@ -262,8 +266,8 @@ __global__ __launch_bounds__(256) void colsum_multi_kernel(const CsJobs jobs) {
         for (; r < r1; ++r) {
             const int64_t off = i * J.s1 + j * J.s2 + c;
             float xv[4], yv[4] = {0.f, 0.f, 0.f, 0.f};
-            ld4(J.X, off, J.xbf, xv);
-            if (J.Y) ld4(J.Y, off, J.ybf, yv);
+            ld4<KIND>(J.X, off, J.xbf, xv);
+            if (J.Y) ld4<KIND>(J.Y, off, J.ybf, yv);
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
                 sx[e] += xv[e];
@@ -361,7 +365,10 @@ SKR_API int skr_colsum_multi(const CsJob* jobs, int n, hipStream_t s) {
         g.fstart[q + 1] = g.fstart[q] + (J.C + 63) / 64;
     }
     for (int q = n + 1; q <= kCsMax; ++q) g.start[q] = g.start[n], g.fstart[q] = g.fstart[n];
-    hipLaunchKernelGGL(colsum_multi_kernel, dim3(g.start[n]), dim3(256), 0, s, g);
+    bool all_bf = true;
+    for (int q = 0; q < n; ++q) all_bf = all_bf && jobs[q].xbf && (jobs[q].Y == nullptr || jobs[q].ybf);
+    if (all_bf) hipLaunchKernelGGL(colsum_multi_kernel<1>, dim3(g.start[n]), dim3(256), 0, s, g);
+    else hipLaunchKernelGGL(colsum_multi_kernel<0>, dim3(g.start[n]), dim3(256), 0, s, g);
     hipLaunchKernelGGL(colsum_multi_finish, dim3(g.fstart[n]), dim3(256), 0, s, g);
     return SKR_CHECK_LAUNCH();
 }

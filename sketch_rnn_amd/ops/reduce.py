@@ -76,8 +76,9 @@ def colsum_many(pairs, splits=None):
     lib = native.require_hip()
     jobs = (CsJob * len(pairs))()
     keep, outs = [], []
-    # narrow reductions first: dispatched ahead of the wide one's workgroups
-    order = sorted(range(len(pairs)), key=lambda i: pairs[i][0].shape[-1])
+    # the widest (longest-running) reduction's workgroups are dispatched
+    # first; the narrow ones fill the slots beside and after it
+    order = sorted(range(len(pairs)), key=lambda i: -pairs[i][0].shape[-1])
     for slot, i in enumerate(order):
         x, y = pairs[i]
         R1, R2, C = x.shape
