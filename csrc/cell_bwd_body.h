@@ -73,7 +73,8 @@ __device__ __forceinline__ void cell_bwd_body(const BwdArgs& a, const int c, con
             const int64_t vo = (int64_t)b * a.vec_ld + uc;
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
-                xv[k][q] = a.xp[b * a.ld_xp + q * H + uc];
+                xv[k][q] = a.xp_lp ? __bfloat162float(((const __hip_bfloat16*)a.xp)[b * a.ld_xp + q * H + uc])
+                                   : a.xp[b * a.ld_xp + q * H + uc];
                 rv[k][q] = a.r_lp != nullptr ? __bfloat162float(a.r_lp[b * a.ld_R + q * H + uc])
                                              : slab_sum<NS>(a.R, b * a.ld_R + q * H + uc, a.R_nslab, a.R_slab);
                 // (vec_bias null: the saved vectors already carry q, csrc/hyper_mod.hip)

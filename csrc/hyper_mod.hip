@@ -57,6 +57,7 @@ __device__ __forceinline__ uint32_t pack_bf(float a, float b) {
 // xh[b][n] = zp[b][n] + sum_k x[b][k] w5[k][n] (skr_bproj_fwd's order). Null
 // members: the training sequence's input (precomputed xh).
 struct ModDecode {
+    int xh_bf16;                              // training: the precomputed xh is bf16 [B][4H] (not decode)
     const float* x5;
     const float* w5; int64_t ldw5;
     const float* zp; int64_t ldzp;
@@ -87,7 +88,7 @@ __global__ __launch_bounds__(NTH) void hyper_mod_fwd(ModDecode dec, const __hip_
             dec.x5 += (int64_t)r0 * 5;
             dec.zp += (int64_t)r0 * dec.ldzp;
         }
-        if (xh) xh += G4;
+        if (xh) xh = dec.xh_bf16 ? (const float*)(const void*)((const __hip_bfloat16*)(const void*)xh + G4) : xh + G4;
         R += G4;
         gout += G4;
         if (rlp) rlp += G4;
@@ -121,6 +122,10 @@ __global__ __launch_bounds__(NTH) void hyper_mod_fwd(ModDecode dec, const __hip_
 #pragma unroll
             for (int k5 = 0; k5 < 5; ++k5) v += dec.x5[rr * 5 + k5] * *(const f32x4*)(dec.w5 + k5 * dec.ldw5 + col);
             x4[k] = v;
+        } else if (dec.xh_bf16) {
+            const uint2 u = *(const uint2*)((const __hip_bfloat16*)(const void*)xh + go);
+            x4[k] = f32x4{__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u),
+                          __uint_as_float(u.y << 16), __uint_as_float(u.y & 0xffff0000u)};
         } else {
             x4[k] = *(const f32x4*)(xh + go);
         }

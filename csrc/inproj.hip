@@ -132,9 +132,11 @@ SKR_API int skr_inproj_bwd(const float* x, const int64_t* len, const void* dxp, 
 //   P[b, i, g] = sum_t x[t, b, i] dxp[t, b, g]     (-> dW[:IN] = sum_b P)
 namespace {
 
-template <int IN>
+// OBF: xp written as bf16 (the HyperLSTM fused-modulation path reads xh as
+// bf16: half the bytes of the largest tensor the decoder forward writes)
+template <int IN, bool OBF>
 __global__ __launch_bounds__(256) void bproj_fwd(const float* __restrict__ x, const float* __restrict__ W,
-                                                 const float* __restrict__ zw, float* __restrict__ xp, int T, int B,
+                                                 const float* __restrict__ zw, void* __restrict__ xp, int T, int B,
                                                  int G, int tpb) {
     const int g = blockIdx.x * 256 + threadIdx.x;
     const int b = blockIdx.y;
@@ -150,7 +152,11 @@ __global__ __launch_bounds__(256) void bproj_fwd(const float* __restrict__ x, co
         float acc = z0;
 #pragma unroll
         for (int i = 0; i < IN; ++i) acc += xr[i] * w[i];
-        __builtin_nontemporal_store(acc, xp + ((int64_t)t * B + b) * G + g);
+        if constexpr (OBF)
+            __builtin_nontemporal_store(__bfloat16_as_ushort(skr::to_bf16(acc)),
+                                        (unsigned short*)xp + ((int64_t)t * B + b) * G + g);
+        else
+            __builtin_nontemporal_store(acc, (float*)xp + ((int64_t)t * B + b) * G + g);
     }
 }
 
@@ -179,10 +185,15 @@ __global__ __launch_bounds__(256) void bproj_bwd(const float* __restrict__ x, co
 }
 
 template <int IN>
-int bproj_launch_fwd(const float* x, const float* W, const float* zw, float* xp, int T, int B, int G, hipStream_t s) {
+int bproj_launch_fwd(const float* x, const float* W, const float* zw, void* xp, int T, int B, int G, int obf,
+                     hipStream_t s) {
     const int tz = (T + 31) / 32;   // time slices: >= 256 workgroups at B ~ 100
-    hipLaunchKernelGGL(bproj_fwd<IN>, dim3((G + 255) / 256, B, tz), dim3(256), 0, s, x, W, zw, xp, T, B, G,
-                       (T + tz - 1) / tz);
+    if (obf)
+        hipLaunchKernelGGL((bproj_fwd<IN, true>), dim3((G + 255) / 256, B, tz), dim3(256), 0, s, x, W, zw, xp, T, B, G,
+                           (T + tz - 1) / tz);
+    else
+        hipLaunchKernelGGL((bproj_fwd<IN, false>), dim3((G + 255) / 256, B, tz), dim3(256), 0, s, x, W, zw, xp, T, B,
+                           G, (T + tz - 1) / tz);
     return SKR_CHECK_LAUNCH();
 }
 
@@ -199,13 +210,13 @@ int bproj_launch_bwd(const float* x, const void* dxp, int kind, int64_t ld, floa
 
 }  // namespace
 
-// x [T, B, IN] fp32, W [IN, G] fp32 (the stroke rows), zw [B, G] fp32 or null -> xp [T, B, G] fp32.
-SKR_API int skr_bproj_fwd(const float* x, const float* W, const float* zw, float* xp, int T, int B, int IN, int G,
-                          hipStream_t s) {
+// x [T, B, IN] fp32, W [IN, G] fp32 (the stroke rows), zw [B, G] fp32 or null -> xp [T, B, G] fp32 (obf: bf16).
+SKR_API int skr_bproj_fwd(const float* x, const float* W, const float* zw, void* xp, int T, int B, int IN, int G,
+                          int obf, hipStream_t s) {
     if (T <= 0 || B <= 0 || G <= 0) return 0;
     switch (IN) {
-        case 3: return bproj_launch_fwd<3>(x, W, zw, xp, T, B, G, s);
-        case 5: return bproj_launch_fwd<5>(x, W, zw, xp, T, B, G, s);
+        case 3: return bproj_launch_fwd<3>(x, W, zw, xp, T, B, G, obf, s);
+        case 5: return bproj_launch_fwd<5>(x, W, zw, xp, T, B, G, obf, s);
         default: return -2;
     }
 }

@@ -82,6 +82,7 @@ struct BwdArgs {
     const float* ln_b; float forget_bias;
     const __hip_bfloat16* r_lp;        // MOD: R from the forward's bf16 copy (stride ld_R) instead of the slabs
     int save_lp;                       // LN: xhat / chat read and dlny / dlncy written as bf16
+    int xp_lp;                         // MOD: xp (xh) stored as bf16 (the fused-modulation training path)
 };
 
 // Gate / cell activations of the LSTM-family cell kernels: the hardware

@@ -153,7 +153,8 @@ __device__ __forceinline__ void row_bwd_body(const BwdArgs& a, const int b, cons
         ldf<V>(ln_b + q * H + u0, lb[q]);
         if constexpr (MOD) {
             const int64_t vo = (int64_t)b * a.vec_ld + u0;
-            ldf<V>(a.xp + b * a.ld_xp + q * H + u0, xv[q]);
+            if (a.xp_lp) ldb<V>((const __hip_bfloat16*)a.xp + b * a.ld_xp + q * H + u0, xv[q]);
+            else ldf<V>(a.xp + b * a.ld_xp + q * H + u0, xv[q]);
             ldb<V>(a.r_lp + b * a.ld_R + q * H + u0, rv[q]);
             ldb<V>((const __hip_bfloat16*)a.vec + q * a.vec_gs + vo, ax[q]);
             ldb<V>((const __hip_bfloat16*)a.vec + (4 + q) * a.vec_gs + vo, ah[q]);

@@ -56,8 +56,11 @@ def run_arm(arm: str, args, seed: int = 0) -> dict:
     trainer.seed.fill_(1000003 * seed)       # dropout / reparameterisation noise stream of this seed
     curve = []
     t0 = time.perf_counter()
+    print("%s seed %d: training %d steps" % (arm, seed, args.steps), file=sys.stderr, flush=True)
     for step in range(1, args.steps + 1):
         out = trainer.train_step(*trainer.batch_to_device(train.random_batch()))
+        if step % 50 == 0:   # heartbeat (the GPU runner kills a silent run)
+            print("%s seed %d step %d" % (arm, seed, step), file=sys.stderr, flush=True)
         if step % args.eval_every == 0 or step == args.steps:
             ev = trainer.evaluate(test)
             curve.append({"step": step, "test_recon_nll": round(ev["r_cost"], 5), "test_kl": round(ev["kl_cost"], 5),

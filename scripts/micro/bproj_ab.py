@@ -1,8 +1,9 @@
 #!/usr/bin/env python3
 """bproj_fwd ([250, 100, 5] x [5, 8192] + z rows -> 819 MB fp32, nontemporal
-stores) timed in isolation: fresh output each call, the same output buffer
-re-used, and an output buffer dirtied by a fill just before (is the write
-rate sensitive to what the destination pages last held?)."""
+stores) timed alone (events around the one launch): into a fresh buffer, into
+the same buffer again, after a 410 MB nontemporal write elsewhere (the
+encoder input projection that precedes it in the training step), and into
+memory that such a write just left dirty (its freed block re-used)."""
 import json
 import os
 import sys
@@ -17,29 +18,56 @@ lib = native.require_hip().lib
 x = torch.randn(T, B, IN, device="cuda")
 W = torch.randn(IN, G, device="cuda")
 zw = torch.randn(B, G, device="cuda")
-out = torch.empty(T, B, G, device="cuda")
+xe = torch.randn(T, B, IN, device="cuda")
+We = torch.randn(2, IN, 2048, device="cuda")
+ln = torch.full((B,), T, dtype=torch.int64, device="cuda")
 st = lambda: torch.cuda.current_stream().cuda_stream   # noqa: E731
 
 
-def run(o):
-    assert lib.skr_bproj_fwd(x.data_ptr(), W.data_ptr(), zw.data_ptr(), o.data_ptr(), T, B, IN, G, st()) == 0
+def bproj(o):
+    assert lib.skr_bproj_fwd(x.data_ptr(), W.data_ptr(), zw.data_ptr(), o.data_ptr(), T, B, IN, G, 0, st()) == 0
 
 
-def timed(fn, reps=10):
-    fn()
-    torch.cuda.synchronize()
-    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+def inproj(o):   # 410 MB nontemporal write, [T, 2B, 2048]
+    assert lib.skr_inproj_fwd(xe.data_ptr(), ln.data_ptr(), We.data_ptr(), None, o.data_ptr(), T, B, IN, 2048, st()) == 0
+
+
+def t_one(pre, mk_out, reps=5):
     best = 1e9
     for _ in range(reps):
+        o = pre()
+        out = mk_out(o)
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
         ev[0].record()
-        fn()
+        bproj(out)
         ev[1].record()
         torch.cuda.synchronize()
         best = min(best, ev[0].elapsed_time(ev[1]) * 1e3)
-    return best
+        del o, out
+    return round(best, 1)
 
 
-res = {"same_buffer_us": timed(lambda: run(out)),
-       "fresh_alloc_us": timed(lambda: run(torch.empty(T, B, G, device="cuda")))}
-res["after_fill_us"] = min(timed(lambda: (out.fill_(1.0), torch.cuda.synchronize(), run(out))) for _ in range(1))
-print(json.dumps({k: round(v, 1) for k, v in res.items()}), flush=True)
+fixed = torch.empty(T, B, G, device="cuda")
+res = {
+    "same_buffer": t_one(lambda: None, lambda o: fixed),
+    "fresh": t_one(lambda: None, lambda o: torch.empty(T, B, G, device="cuda")),
+}
+xp_keep = torch.empty(T, 2 * B, 2048, device="cuda")
+res["after_inproj_write"] = t_one(lambda: inproj(xp_keep), lambda o: fixed)
+
+
+best = 1e9
+for _ in range(5):   # the 410 MB block written, freed, and bproj's output allocated over it
+    t = torch.empty(T, 2 * B, 2048, device="cuda")
+    inproj(t)
+    del t
+    out = torch.empty(T, B, G, device="cuda")
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    ev[0].record()
+    bproj(out)
+    ev[1].record()
+    torch.cuda.synchronize()
+    best = min(best, ev[0].elapsed_time(ev[1]) * 1e3)
+    del out
+res["into_freed_dirty_block"] = round(best, 1)
+print(json.dumps(res), flush=True)

@@ -73,6 +73,7 @@ class LstmBwdArgs(C.Structure):
         ("ln_b", _p), ("forget_bias", _f),
         ("r_lp", _p),
         ("save_lp", _i),
+        ("xp_lp", _i),
     ]
 
 
@@ -296,7 +297,7 @@ class ModDecode(C.Structure):
     """Mirror of ``ModDecode`` in csrc/hyper_mod.hip (decode-mode inputs of the
     HyperLSTM modulation kernel: the x-projection from the stroke)."""
     _fields_ = [
-        ("x5", _p), ("w5", _p), ("ldw5", _i64), ("zp", _p), ("ldzp", _i64),
+        ("xh_bf16", _i), ("x5", _p), ("w5", _p), ("ldw5", _i64), ("zp", _p), ("ldzp", _i64),
     ]
 
 
@@ -358,7 +359,7 @@ class HipLib:
         lib.skr_inproj_fwd.restype = _i
         lib.skr_inproj_bwd.argtypes = [_p, _p, _p, _i, _p, _i, _i, _i, _i, _i, _p]
         lib.skr_inproj_bwd.restype = _i
-        lib.skr_bproj_fwd.argtypes = [_p, _p, _p, _p, _i, _i, _i, _i, _p]
+        lib.skr_bproj_fwd.argtypes = [_p, _p, _p, _p, _i, _i, _i, _i, _i, _p]
         lib.skr_bproj_fwd.restype = _i
         lib.skr_bproj_bwd.argtypes = [_p, _p, _i, _i64, _p, _p, _i, _i, _i, _i, _p]
         lib.skr_bproj_bwd.restype = _i

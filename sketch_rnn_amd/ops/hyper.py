@@ -15,13 +15,14 @@ geometry, seeds) lives in :mod:`.recurrent`.
 """
 from __future__ import annotations
 
+import ctypes
 import os
 
 import torch
 
 from ..utils import native
 from . import gemm
-from ._hipapi import LstmBwdArgs, LstmFwdArgs
+from ._hipapi import LstmBwdArgs, LstmFwdArgs, ModDecode
 from .inproj import bproj_fwd, bproj_ok, bproj_reduce
 from .recurrent import (ROW_STATS, _cell_bwd, _cell_fwd, _check, _ClusterSync, _inference, _ln_saves_lp, _lp_kind,
                         _ptr, _Saved, _seed_tensor, _stream, cell_geometry)
@@ -45,6 +46,10 @@ HYPER_BWD_FUSE = True
 # launches per backward step instead of four. SKR_CHAIN=0 keeps the unchained
 # launches (A/B).
 CHAIN = os.environ.get("SKR_CHAIN", "1") != "0"
+# The main input projection x W_x + z W_z ([T, B, 4H], the largest tensor the
+# forward writes) stored in bf16 on the fused-modulation path; False keeps it
+# fp32 (A/B, scripts/micro/xh_ab.py).
+XH_BF16 = True
 # (Round 4 measured the hyper-norm projections unfolded -- vec = bf16(hh W_z)
 # W_a + q forward, dz = dvec W_a^T / dh = dz W_z^T backward -- at 27.8 vs
 # 24.6 ms per training step: W_z re-read from L2 by every workgroup costs more
@@ -143,7 +148,7 @@ class _HyperSeq(torch.autograd.Function):
                 g = gemm.SmallGroup(dev)
                 zw, zwy = g.mm(zc, W_x[IX:]), g.mm(zc, hW_x[IX:IN])
                 g.run()
-            XH = bproj_fwd(x, W_x[:IX], zw)
+            XH = None   # (after the modulation-path choice below: bf16 when hyper_mod reads it)
             XHY = bproj_fwd(x, hW_x[:IX], zwy)
         else:
             if zc is not None:
@@ -262,7 +267,15 @@ class _HyperSeq(torch.autograd.Function):
                 qb = qb.reshape(12 * H).contiguous()
             GP = torch.empty(B, G, device=dev, dtype=f32)
             GS = torch.empty(B, 4, H // 32, 2, device=dev, dtype=f32)
+        if XH is None:
+            # the main input projection [T, B, 4H]: bf16 on the fused-modulation
+            # path (hyper_mod and the backward main cell read it as bf16 -- half
+            # the bytes of the largest tensor the forward writes), else fp32
+            XH = bproj_fwd(x, W_x[:IX], zw, bf16=hmod and XH_BF16)
+        if hmod:
             XHc = XH.contiguous()
+            xh_dec = ModDecode()
+            xh_dec.xh_bf16 = int(XHc.dtype == torch.bfloat16)
         # hyper cell args (LN-LSTM, no modulation)
         ah = LstmFwdArgs()
         ah.save_lp = int(slp)
@@ -314,7 +327,7 @@ class _HyperSeq(torch.autograd.Function):
                 _check(lib.lib.skr_hyper_mod_fwd(A[t + 1, :, H:].data_ptr(), K, PlT.data_ptr(), qb.data_ptr(),
                                                  XHc[t].data_ptr(), RM[rmi(t)].data_ptr(), B * G, S_m,
                                                  VEC[t].data_ptr(), GP.data_ptr(), _ptr(RLP[t] if RLP is not None else None),
-                                                 GS.data_ptr(), B, H, Hh, None, st), "hyper_mod_fwd")
+                                                 GS.data_ptr(), B, H, Hh, ctypes.byref(xh_dec), st), "hyper_mod_fwd")
                 am.gpre, am.gstats, am.gstat_tiles = GP.data_ptr(), GS.data_ptr(), H // 32
             elif vbf:
                 gemm.rec_gemm_bf16out(A[t + 1, :, H:], PlT, VEC[t])
@@ -445,6 +458,7 @@ class _HyperSeq(torch.autograd.Function):
             else:
                 am.act, am.c_new = s.ACT[t].data_ptr(), s.COUT[t].data_ptr()
             am.xp, am.vec = s.XH[t].data_ptr(), s.VEC[t].data_ptr()
+            am.xp_lp = int(s.XH.dtype == torch.bfloat16)
             if s.RLP is not None:
                 am.R, am.r_lp = None, s.RLP[t].data_ptr()
             else:

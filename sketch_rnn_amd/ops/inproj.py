@@ -89,17 +89,18 @@ def bproj_ok(x) -> bool:
     return x.is_cuda and x.shape[-1] in (3, 5)
 
 
-def bproj_fwd(x, W, zw=None):
-    """``xp[t, b] = x[t, b] @ W + zw[b]`` (csrc/inproj.hip ``skr_bproj_fwd``)."""
+def bproj_fwd(x, W, zw=None, bf16: bool = False):
+    """``xp[t, b] = x[t, b] @ W + zw[b]`` (csrc/inproj.hip ``skr_bproj_fwd``);
+    ``bf16``: xp stored as bf16."""
     lib = native.require_hip()
     T, B, IN = x.shape
     G = W.shape[1]
     x = x.contiguous().float()
     W = W.contiguous().float()
     zw = zw.contiguous().float() if zw is not None else None
-    xp = torch.empty(T, B, G, device=x.device, dtype=torch.float32)
+    xp = torch.empty(T, B, G, device=x.device, dtype=torch.bfloat16 if bf16 else torch.float32)
     rc = lib.lib.skr_bproj_fwd(x.data_ptr(), W.data_ptr(), None if zw is None else zw.data_ptr(), xp.data_ptr(),
-                               T, B, IN, G, torch.cuda.current_stream().cuda_stream)
+                               T, B, IN, G, int(bf16), torch.cuda.current_stream().cuda_stream)
     if rc != 0:
         raise RuntimeError("skr_bproj_fwd failed (%d)" % rc)
     return xp

@@ -43,6 +43,7 @@ import torch
 
 from ..ops import gemm
 from ..ops._hipapi import DecodeSample, LstmFwdArgs, ModDecode
+from ..ops.hyper import _fold_ok
 from ..ops.recurrent import _ClusterSync, _seed_tensor
 from ..utils import native
 
@@ -131,6 +132,17 @@ class HyperStepDecoder:
         IN = p.W_x.shape[0]
 
         def fold(W_z, b_z, W_a):
+            if _fold_ok(H, Hh, E):   # the training path's fold kernel (csrc/hyper_fold.hip): P^T bf16, q
+                Pl = torch.empty(Hh, 12 * H, dtype=dt, device=W_z.device)   # (both layouts are written)
+                PlT = torch.empty(12 * H, Hh, dtype=dt, device=W_z.device)
+                q = torch.empty(12, H, dtype=torch.float32, device=W_z.device)
+                rc = self.lib.skr_hyper_fold(W_z.detach().contiguous().data_ptr(), b_z.detach().contiguous().data_ptr(),
+                                             W_a.detach().contiguous().data_ptr(), None, Hh, H, E, Pl.data_ptr(),
+                                             PlT.data_ptr(), q.data_ptr(), None,
+                                             torch.cuda.current_stream().cuda_stream)
+                if rc != 0:
+                    raise RuntimeError("skr_hyper_fold failed (%d)" % rc)
+                return PlT, q
             Wz3 = W_z.view(Hh, 12, E).permute(1, 0, 2)
             P = torch.bmm(Wz3, W_a).permute(1, 0, 2).reshape(Hh, 12 * H)
             q = torch.bmm(b_z.view(12, 1, E), W_a).reshape(12, H).contiguous()
@@ -197,9 +209,12 @@ class HyperStepDecoder:
         self.A[:, H:].copy_(hh0)
         self.CC.copy_(c0)
         self.HCC.copy_(hc0)
-        if zc is not None:
+        if zc is not None:   # the per-sketch z projections, one grouped small-GEMM launch
             IN = p.W_x.shape[0]
-            torch.mm(zc, torch.cat([p.W_x[5:], p.hyp_W_x[5:IN]], 1), out=self.ZP)
+            g = gemm.SmallGroup(self.dev)
+            g.mm(zc.float().contiguous(), p.W_x[5:].detach(), out=self.ZP[:, :self.G])
+            g.mm(zc.float().contiguous(), p.hyp_W_x[5:IN].detach(), out=self.ZP[:, self.G:])
+            g.run()
         else:
             self.ZP.zero_()
         for cl in (self.clm, self.clh):
@@ -248,7 +263,7 @@ class HyperStepDecoder:
         B, H, G, Gh = self.B, self.H, self.G, self.Gh
         st = torch.cuda.current_stream().cuda_stream
         rc = self.lib.skr_bproj_fwd(x.data_ptr(), w["W5"].data_ptr(), self.ZP.data_ptr(), self.XP.data_ptr(),
-                                    1, B, 5, G + Gh, st)
+                                    1, B, 5, G + Gh, 0, st)
         if rc != 0:
             raise RuntimeError("skr_bproj_fwd failed (%d)" % rc)
         jobs = [(self.A[:, :H], w["WhT"], self.RM, self.S_m), (self.A, w["WyT"], self.RY, self.S_y)]
