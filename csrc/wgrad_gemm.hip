@@ -39,6 +39,10 @@
 // 471 / 143 / 130 us for the dW_h / dP+colsum / dW_y / encoder shapes
 // against hipBLASLt's 837 / 700 / 174 / 168. A variant with fragments
 // double-buffered across K-steps and a 5-stage ring was slower on dW_h (940).
+// Round 5 (profiles/r5/wgrad_sweep.jsonl, one box): both k16 halves'
+// fragment reads issued up front (DB) -- the second half's 12 transposed
+// reads land under the first half's MFMAs -- dW_h 880 -> 785 us; dP + colsum
+// at 5 splits (ops/gemm.py _wgrad_splits) 514 -> 438 us.
 // Optional colsum(B) (the bias gradient folded into a projection's weight
 // gradient: HyperLSTM dVEC): waves wm == 0 add their B fragments in fp32.
 #include "common.h"
@@ -104,7 +108,10 @@ __device__ __forceinline__ bf16x8 join(const s16x4 (&h)[2]) {
     return __builtin_bit_cast(bf16x8, v);
 }
 
-template <bool CS>
+// DB: both k16 halves' fragment sets read up front, the second half's
+// reads in flight under the first half's MFMAs (24 transposed reads per
+// K-step in one batch instead of two exposed read -> wait -> MFMA rounds).
+template <bool CS, bool DB>
 __global__ __launch_bounds__(NT) void wgrad_kernel(const WgArgs g) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     // ---- workgroup -> (batch, split, tile): XCD-major linear order
@@ -233,12 +240,22 @@ __global__ __launch_bounds__(NT) void wgrad_kernel(const WgArgs g) {
         __builtin_amdgcn_s_barrier();     // stage kt landed for every wave; stage kt-1 is free
         if (kt + NSTG - 1 < nk) issue(kt + NSTG - 1);
         if (kt == nk - 1 && tail < BK) zero_tail(smem + (kt % NSTG) * STGB);
+        if constexpr (DB) {
+            Frags f0, f1;
+            read_frags(kt % NSTG, 0, f0);
+            read_frags(kt % NSTG, 1, f1);
+            frag_wait<12>(f0);
+            mfmas(f0);
+            frag_wait<0>(f1);
+            mfmas(f1);
+        } else {
 #pragma unroll
-        for (int ks = 0; ks < 2; ++ks) {
-            Frags f;
-            read_frags(kt % NSTG, ks, f);
-            frag_wait<0>(f);
-            mfmas(f);
+            for (int ks = 0; ks < 2; ++ks) {
+                Frags f;
+                read_frags(kt % NSTG, ks, f);
+                frag_wait<0>(f);
+                mfmas(f);
+            }
         }
     }
     // ---- epilogue: fp32 slab (lane: column r; registers: rows (e&3) + 8(e>>2) + 4h)
@@ -283,6 +300,16 @@ __global__ __launch_bounds__(256) void slab_sum_kernel(const float* __restrict__
 
 }  // namespace
 
+static int g_wgrad_db = 1;   // fragment schedule (DB template argument), skr_wgrad_set_variant
+
+// A/B hook: 1 = both k16 halves' fragments read up front (DB), 0 = per-half,
+// < 0 = leave unchanged. Returns the schedule in force before the call.
+SKR_API int skr_wgrad_set_variant(int db) {
+    const int prev = g_wgrad_db;
+    if (db >= 0) g_wgrad_db = db != 0;
+    return prev;
+}
+
 // C[z] = A[z]^T . B[z] (+ cs[z] = colsum(B[z]) when cs != null) for z < nb.
 // A [K, M] bf16 (lda, batch stride a_bs elements), B [K, N] bf16 (ldb, b_bs).
 // S split-K slabs: slab s of batch z at work + (z * S + s) * M * N (fp32);
@@ -313,13 +340,20 @@ SKR_API int skr_wgrad(const void* A, int64_t lda, int64_t a_bs, const void* B, i
     const size_t lds = (size_t)NSTG * STGB;
     static bool attr = false;
     if (!attr) {
-        if (hipFuncSetAttribute((const void*)wgrad_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess ||
-            hipFuncSetAttribute((const void*)wgrad_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
-            return -6;
+        const void* ks[4] = {(const void*)wgrad_kernel<false, false>, (const void*)wgrad_kernel<true, false>,
+                             (const void*)wgrad_kernel<false, true>, (const void*)wgrad_kernel<true, true>};
+        for (const void* k : ks)
+            if (hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) return -6;
         attr = true;
     }
-    if (g.cs != nullptr) hipLaunchKernelGGL(wgrad_kernel<true>, dim3(grid), dim3(NT), lds, s, g);
-    else hipLaunchKernelGGL(wgrad_kernel<false>, dim3(grid), dim3(NT), lds, s, g);
+    const bool cs_on = g.cs != nullptr;
+    if (g_wgrad_db) {
+        if (cs_on) hipLaunchKernelGGL((wgrad_kernel<true, true>), dim3(grid), dim3(NT), lds, s, g);
+        else hipLaunchKernelGGL((wgrad_kernel<false, true>), dim3(grid), dim3(NT), lds, s, g);
+    } else {
+        if (cs_on) hipLaunchKernelGGL((wgrad_kernel<true, false>), dim3(grid), dim3(NT), lds, s, g);
+        else hipLaunchKernelGGL((wgrad_kernel<false, false>), dim3(grid), dim3(NT), lds, s, g);
+    }
     if (S > 1) {
         const int64_t n = (int64_t)M * N;
         hipLaunchKernelGGL(slab_sum_kernel, dim3((unsigned)((n * nb / 4 + 255) / 256)), dim3(256), 0, s, work, S, n, nb, C);

@@ -45,6 +45,24 @@ def main():
         ("dW_y [2304 x 1024]", lambda: gemm.wgrad(A2, dRY), 2 * TB * 2304 * 1024),
         ("enc dW 2 x [512 x 2048]", lambda: gemm.wgrad(Aenc, dGenc), 2 * 2 * TB * 512 * 2048),
     ]
+    if "--sweep" in sys.argv:   # split-K counts x fragment schedules of the hand-written kernel
+        lib = __import__("sketch_rnn_amd.utils.native", fromlist=["x"]).require_hip().lib
+        shapes = {"dW_h": (2048, 8192, 1), "dP": (256, 24576, 1), "dW_y": (2304, 1024, 1), "enc": (512, 2048, 2)}
+        for (name, fn, fl), key in zip(cases, shapes):
+            for db in (0, 1):
+                lib.skr_wgrad_set_variant(db)
+                for S in (1, 2, 3, 4, 5, 6, 7, 8, 9, 10):
+                    M, N, nb = shapes[key]
+                    tiles = nb * (M // 256) * (N // 256)
+                    if tiles * S > 1024 or (S > 1 and tiles >= 192 and S > 2):
+                        continue
+                    gemm.WGRAD_SPLIT = {shapes[key]: S}
+                    us = timeit(fn)
+                    print(json.dumps({"shape": key, "db": db, "S": S, "us": round(us, 1),
+                                      "tflops": round(fl / us / 1e6, 1)}), flush=True)
+        gemm.WGRAD_SPLIT = {}
+        lib.skr_wgrad_set_variant(0)
+        return
     impls = ("hip", "hipblaslt")
     tot = {k: 0.0 for k in impls}
     for name, fn, fl in cases:

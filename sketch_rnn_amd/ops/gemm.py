@@ -195,6 +195,7 @@ def _wgrad_hip_ok(a: torch.Tensor, b: torch.Tensor) -> bool:
 
 
 WGRAD_HIP = True   # False: hipBLASLt weight gradients (tests / A-B)
+WGRAD_SPLIT = {}   # (M, N, batch) -> split-K count override (scripts/bench_wgrad.py sweeps)
 
 
 def grad_slot(param: torch.Tensor, shape) -> Optional[torch.Tensor]:
@@ -210,14 +211,30 @@ def grad_slot(param: torch.Tensor, shape) -> Optional[torch.Tensor]:
     return t
 
 
+def _wgrad_splits(tiles: int, K: int) -> int:
+    """Split-K count of the long-K weight-gradient kernel: one workgroup per
+    CU holds a 256 x 256 tile, so the run takes ceil(tiles * S / 256) rounds
+    of 1/S of the K range each, plus the partial slabs' extra traffic (~1 % of
+    a round per split). Measured (profiles/r5/wgrad_sweep.jsonl): dP 96 tiles
+    S = 5 (438 us) against the old whole-wave rule's S = 2 (514 us); dW_y 36
+    tiles S = 7; encoder 32 tiles S = 8; dW_h 256 tiles S = 1."""
+    best, pick = None, 1
+    for S in range(1, 9):
+        if S > 1 and S > K // 1024:   # at least 1024 rows per split
+            break
+        cost = -(-tiles * S // 256) / S + 0.01 * S
+        if best is None or cost < best - 1e-9:
+            best, pick = cost, S
+    return pick
+
+
 def _wgrad_hip(a, b, colsum, out=None):
     from ..utils import native
     lib = native.require_hip()
     n, K, M = a.shape
     N = b.shape[-1]
     tiles = n * (M // 256) * (N // 256)
-    # split K only to fill the chip: whole waves of <= 256 workgroups (one per CU)
-    S = max(1, min(256 // tiles, K // 1024)) if tiles < 192 else 1
+    S = WGRAD_SPLIT.get((M, N, n), _wgrad_splits(tiles, K))
     dev = a.device
     out = out.view(n, M, N) if out is not None else torch.empty(n, M, N, device=dev, dtype=torch.float32)
     work = torch.empty(n * S, M, N, device=dev, dtype=torch.float32) if S > 1 else None

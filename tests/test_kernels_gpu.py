@@ -14,6 +14,7 @@ import torch
 from sketch_rnn_amd import ops
 from sketch_rnn_amd.models import cells as C
 from sketch_rnn_amd.models.mdn import mdn_loss_torch
+from sketch_rnn_amd.utils import native
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
@@ -833,7 +834,8 @@ def test_skinny_gemm_f32_matches_torch(M, N, K, nd):
 
 @pytest.mark.parametrize("n,K,M,N,cs,sliced", [(1, 25000, 2048, 8192, False, True), (1, 3001, 256, 2560, True, False),
                                                (2, 1000, 512, 512, False, False), (1, 777, 2304, 1024, True, True)])
-def test_wgrad_kernel_vs_fp32(n, K, M, N, cs, sliced):
+@pytest.mark.parametrize("db", [0, 1])
+def test_wgrad_kernel_vs_fp32(n, K, M, N, cs, sliced, db):
     """Hand-written long-K weight-gradient GEMM (csrc/wgrad_gemm.hip) against
     an fp32 product of the same bf16 operands: headline shape (split-free),
     K tails (K % 32 != 0), batched directions, strided column-slice operands,
@@ -850,8 +852,14 @@ def test_wgrad_kernel_vs_fp32(n, K, M, N, cs, sliced):
     b = torch.randn(n, K, N, device=dev).to(torch.bfloat16)
     aa, bb = (a, b) if n > 1 else (a[0], b[0])
     assert gemm._wgrad_hip_ok(a, b)
-    r1 = gemm.wgrad(aa, bb, colsum=cs)
-    r2 = gemm.wgrad(aa, bb, colsum=cs)
+    lib = native.require_hip().lib
+    prev = lib.skr_wgrad_set_variant(-1)   # (returns the current fragment schedule)
+    assert lib.skr_wgrad_set_variant(db) in (0, 1)
+    try:
+        r1 = gemm.wgrad(aa, bb, colsum=cs)
+        r2 = gemm.wgrad(aa, bb, colsum=cs)
+    finally:
+        lib.skr_wgrad_set_variant(prev)
     out1, cs1 = r1 if cs else (r1, None)
     out2, cs2 = r2 if cs else (r2, None)
     ref = torch.bmm(a.float().transpose(1, 2), b.float())
