@@ -69,13 +69,26 @@ struct HeadFwd {
     int M, NOUT, NOUTP, mode, mask_pen;
     float F, log_floor, inv_n;
     float keep; const int64_t* seed; uint32_t stream;   // dropout on X (keep >= 1: off)
-    __hip_bfloat16* dz;              // [N][NOUTP] bf16, or null (no gradient)
+    __hip_bfloat16* dz;              // [N][ldz] bf16 (columns < NOUTP written), or null (no gradient)
     float* part;                     // [2][nblocks] per-workgroup sums of the shape / pen terms
+    int x_bf16;                      // X is bf16 (the decoder's saved bf16 h rows, row stride ldx)
+    int64_t ldz;                     // dz row stride (>= NOUTP, multiple of 8)
 };
 
 // ---------------------------------------------------------------------------------
 // forward: projection + loss + dz
 // ---------------------------------------------------------------------------------
+// X fragments of one K chunk for lane (fr, fq): row arow, k = kc * kKC +
+// ks * 32 + fq * 8 .. +7 for ks = 0, 1 -- raw, converted at use
+template <bool XB> struct XChunk { f32x4 v[2][2]; };
+template <> struct XChunk<true> { u32x4 v[2]; };
+
+constexpr int kWPieces = kMaxNoutP * (kKC / 8) / 256;   // 16-byte W^T pieces per thread per chunk (5)
+// K chunks of X and W^T in flight per thread: 2 on bf16 X (230 registers, 2
+// waves per SIMD), 1 on fp32 X (a deeper fp32 ring drops to 1 wave per SIMD)
+template <bool XB> constexpr int fwd_ring() { return XB ? 2 : 1; }
+
+template <bool XB>
 __global__ __launch_bounds__(256) void mdn_head_fwd(const HeadFwd a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     __hip_bfloat16* Bs = (__hip_bfloat16*)smem;                 // [2][NOUTP][kLdk]
@@ -93,43 +106,99 @@ __global__ __launch_bounds__(256) void mdn_head_fwd(const HeadFwd a) {
 #pragma unroll
     for (int c = 0; c < kMaxNoutP / 16; ++c) acc[c] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-    // stage W^T chunk [NOUTP][kKC] (16-byte pieces: NOUTP * 8 per chunk)
-    auto stage = [&](int buf, int k0) {
-        __hip_bfloat16* dst = Bs + buf * kMaxNoutP * kLdk;
-        for (int p = tid; p < NOUTP * (kKC / 8); p += 256) {
-            const int n = p >> 3, c = p & 7;
-            const u32x4 v = *(const u32x4*)(a.Wt + (int64_t)n * Hd + k0 + c * 8);
-            *(u32x4*)(dst + n * kLdk + c * 8) = v;
+    // K loop: the W^T chunk [NOUTP][kKC] and this lane's X fragments are
+    // loaded R_ chunks ahead into registers (every wait is for loads
+    // issued a ring ago, not one round trip per chunk); W^T goes through a
+    // double-buffered padded LDS tile, X straight into MFMA operands.
+    constexpr int R_ = fwd_ring<XB>();
+    const int nchunks = Hd / kKC, npieces = NOUTP * (kKC / 8);
+    u32x4 wr[R_][kWPieces];
+    XChunk<XB> xr[R_];
+    auto load_w = [&](u32x4 (&r)[kWPieces], int kc) {
+#pragma unroll
+        for (int j = 0; j < kWPieces; ++j) {
+            const int p = tid + 256 * j;
+            if (p < npieces) r[j] = *(const u32x4*)(a.Wt + (int64_t)(p >> 3) * Hd + kc * kKC + (p & 7) * 8);
         }
     };
-    const int nchunks = Hd / kKC;
-    stage(0, 0);
-    __syncthreads();
-    for (int kc = 0; kc < nchunks; ++kc) {
-        if (kc + 1 < nchunks) stage((kc + 1) & 1, (kc + 1) * kKC);
-        const __hip_bfloat16* Bc = Bs + (kc & 1) * kMaxNoutP * kLdk;
+    auto store_w = [&](const u32x4 (&r)[kWPieces], int buf) {
+        __hip_bfloat16* dst = Bs + buf * kMaxNoutP * kLdk;
 #pragma unroll
-        for (int ks = 0; ks < kKC / 32; ++ks) {
-            const int k = kc * kKC + ks * 32 + fq * 8;
-            const f32x4 x0 = *(const f32x4*)(a.X + arow * a.ldx + k);
-            const f32x4 x1 = *(const f32x4*)(a.X + arow * a.ldx + k + 4);
-            float xs[8] = {x0[0], x0[1], x0[2], x0[3], x1[0], x1[1], x1[2], x1[3]};
-            if (keep_on) {
+        for (int j = 0; j < kWPieces; ++j) {
+            const int p = tid + 256 * j;
+            if (p < npieces) *(u32x4*)(dst + (p >> 3) * kLdk + (p & 7) * 8) = r[j];
+        }
+    };
+    auto load_x = [&](XChunk<XB>& r, int kc) {
 #pragma unroll
-                for (int j = 0; j < 8; ++j) xs[j] *= drop_mult(true, key, arow * Hd + k + j, a.keep);
-            }
-            const u32x4 pk = {pack_bf16(xs[0], xs[1]), pack_bf16(xs[2], xs[3]), pack_bf16(xs[4], xs[5]),
-                              pack_bf16(xs[6], xs[7])};
-            const bf16x8 A = __builtin_bit_cast(bf16x8, pk);
-#pragma unroll
-            for (int c = 0; c < kMaxNoutP / 16; ++c) {
-                if (c < NC) {
-                    const bf16x8 Bf = *(const bf16x8*)(Bc + (c * 16 + fr) * kLdk + ks * 32 + fq * 8);
-                    acc[c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A, Bf, acc[c], 0, 0, 0);
-                }
+        for (int ks = 0; ks < 2; ++ks) {
+            const int64_t o = arow * a.ldx + kc * kKC + ks * 32 + fq * 8;
+            if constexpr (XB) {
+                r.v[ks] = *(const u32x4*)((const __hip_bfloat16*)(const void*)a.X + o);
+            } else {
+                r.v[ks][0] = *(const f32x4*)(a.X + o);
+                r.v[ks][1] = *(const f32x4*)(a.X + o + 4);
             }
         }
-        __syncthreads();
+    };
+    auto frag = [&](const XChunk<XB>& r, int ks, int kc) -> bf16x8 {
+        const int k = kc * kKC + ks * 32 + fq * 8;
+        float xs[8];
+        if constexpr (XB) {
+            if (!keep_on) return __builtin_bit_cast(bf16x8, r.v[ks]);
+            const bf16x8 v = __builtin_bit_cast(bf16x8, r.v[ks]);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) xs[j] = (float)v[j];
+        } else {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                xs[j] = r.v[ks][0][j];
+                xs[4 + j] = r.v[ks][1][j];
+            }
+        }
+        if (keep_on) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) xs[j] *= drop_mult(true, key, arow * Hd + k + j, a.keep);
+        }
+        const u32x4 pk = {pack_bf16(xs[0], xs[1]), pack_bf16(xs[2], xs[3]), pack_bf16(xs[4], xs[5]),
+                          pack_bf16(xs[6], xs[7])};
+        return __builtin_bit_cast(bf16x8, pk);
+    };
+    // prologue: W^T chunk 0 into LDS; W^T chunks 1..R and X chunks 0..R-1 in flight
+    load_w(wr[0], 0);
+    store_w(wr[0], 0);
+#pragma unroll
+    for (int r = 1; r <= R_; ++r)
+        if (r < nchunks) load_w(wr[r % R_], r);
+#pragma unroll
+    for (int r = 0; r < R_; ++r)
+        if (r < nchunks) load_x(xr[r], r);
+    __syncthreads();
+    for (int kc0 = 0; kc0 < nchunks; kc0 += R_) {
+#pragma unroll
+        for (int r = 0; r < R_; ++r) {
+            const int kc = kc0 + r;                       // slot of chunk kc: r; of chunk kc + 1: (r + 1) % R
+            if (kc >= nchunks) break;                     // uniform
+            if (kc + 1 < nchunks) {
+                store_w(wr[(r + 1) % R_], (kc + 1) & 1);
+                if (kc + 1 + R_ < nchunks) load_w(wr[(r + 1) % R_], kc + 1 + R_);
+            }
+            const bf16x8 A0 = frag(xr[r], 0, kc), A1 = frag(xr[r], 1, kc);
+            if (kc + R_ < nchunks) load_x(xr[r], kc + R_);
+            const __hip_bfloat16* Bc = Bs + (kc & 1) * kMaxNoutP * kLdk;
+#pragma unroll
+            for (int ks = 0; ks < kKC / 32; ++ks) {
+                const bf16x8 A = ks == 0 ? A0 : A1;
+#pragma unroll
+                for (int c = 0; c < kMaxNoutP / 16; ++c) {
+                    if (c < NC) {
+                        const bf16x8 Bf = *(const bf16x8*)(Bc + (c * 16 + fr) * kLdk + ks * 32 + fq * 8);
+                        acc[c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A, Bf, acc[c], 0, 0, 0);
+                    }
+                }
+            }
+            __syncthreads();
+        }
     }
     // ---- z tile (+bias) into LDS (reuses the staging buffers)
 #pragma unroll
@@ -257,7 +326,7 @@ __global__ __launch_bounds__(256) void mdn_head_fwd(const HeadFwd a) {
         const float* zr = zt + rr * NOUTP + c8;
         const u32x4 v = {pack_bf16(zr[0], zr[1]), pack_bf16(zr[2], zr[3]), pack_bf16(zr[4], zr[5]),
                          pack_bf16(zr[6], zr[7])};
-        *(u32x4*)(a.dz + row * NOUTP + c8) = v;
+        *(u32x4*)(a.dz + row * a.ldz + c8) = v;
     }
 }
 
@@ -295,6 +364,7 @@ struct HeadDx {
     const float* scale;              // [2]: pen columns, mixture columns
     float keep; const int64_t* seed; uint32_t stream;
     float* dX; int64_t lddx;
+    int64_t ldz;                     // dz row stride
 };
 
 constexpr int kDxCols = 128;
@@ -320,7 +390,7 @@ __global__ __launch_bounds__(256) void mdn_head_dx(const HeadDx a) {
     for (int c = 0; c < kDxCols / 16; ++c) acc[c] = f32x4{0.f, 0.f, 0.f, 0.f};
     for (int ks = 0; ks < NOUTP / 32; ++ks) {
         const int k = ks * 32 + fq * 8;
-        u32x4 raw = *(const u32x4*)(a.dz + arow * NOUTP + k);
+        u32x4 raw = *(const u32x4*)(a.dz + arow * a.ldz + k);
         if (k < 8) {   // pen columns 0..2 carry the pen scale
             bf16x8 v = __builtin_bit_cast(bf16x8, raw);
             float f[8];
@@ -376,11 +446,14 @@ struct HeadDw {
     float keep; const int64_t* seed; uint32_t stream;
     float* slab;                     // [S][Hd + 64][NOUTP]
     int64_t rows_per;                // rows per slab (multiple of 32)
+    int64_t ldz;                     // dz row stride
+    int x_bf16;                      // X is bf16 (row stride ldx)
 };
 
 constexpr int kDwRows = 64;          // input features (dW rows) per workgroup
 constexpr int kRC = 32;              // rows per staged chunk (= MFMA K)
 
+template <bool XB>
 __global__ __launch_bounds__(256) void mdn_head_dw(const HeadDw a) {
     __shared__ __attribute__((aligned(16))) __hip_bfloat16 xt[kDwRows][kRC + 8];        // [feature][row]
     __shared__ __attribute__((aligned(16))) __hip_bfloat16 gt[kMaxNoutP][kRC + 8];      // [out col][row]
@@ -404,8 +477,14 @@ __global__ __launch_bounds__(256) void mdn_head_dw(const HeadDw a) {
             float v[4] = {0.f, 0.f, 0.f, 0.f};
             if (row < r_end) {
                 if (f0 + f4 + 3 < Hd) {
-                    const f32x4 x = *(const f32x4*)(a.X + row * a.ldx + f0 + f4);
-                    v[0] = x[0]; v[1] = x[1]; v[2] = x[2]; v[3] = x[3];
+                    if constexpr (XB) {
+                        const uint2 u = *(const uint2*)((const __hip_bfloat16*)(const void*)a.X + row * a.ldx + f0 + f4);
+                        v[0] = __uint_as_float(u.x << 16); v[1] = __uint_as_float(u.x & 0xffff0000u);
+                        v[2] = __uint_as_float(u.y << 16); v[3] = __uint_as_float(u.y & 0xffff0000u);
+                    } else {
+                        const f32x4 x = *(const f32x4*)(a.X + row * a.ldx + f0 + f4);
+                        v[0] = x[0]; v[1] = x[1]; v[2] = x[2]; v[3] = x[3];
+                    }
                     if (keep_on) {
 #pragma unroll
                         for (int q = 0; q < 4; ++q) v[q] *= drop_mult(true, key, row * Hd + f0 + f4 + q, a.keep);
@@ -414,8 +493,10 @@ __global__ __launch_bounds__(256) void mdn_head_dw(const HeadDw a) {
 #pragma unroll
                     for (int q = 0; q < 4; ++q) {
                         const int f = f0 + f4 + q;
-                        v[q] = f < Hd ? a.X[row * a.ldx + f] * drop_mult(keep_on, key, row * Hd + f, a.keep)
-                                      : (f == Hd ? 1.f : 0.f);
+                        const float xf = f >= Hd ? 0.f
+                                         : XB ? __bfloat162float(((const __hip_bfloat16*)(const void*)a.X)[row * a.ldx + f])
+                                                    : a.X[row * a.ldx + f];
+                        v[q] = f < Hd ? xf * drop_mult(keep_on, key, row * Hd + f, a.keep) : (f == Hd ? 1.f : 0.f);
                     }
                 }
             }
@@ -427,7 +508,7 @@ __global__ __launch_bounds__(256) void mdn_head_dw(const HeadDw a) {
             const int rr = p / (NOUTP / 8), c8 = (p - rr * (NOUTP / 8)) * 8;
             const int64_t row = r0 + rr;
             bf16x8 v = {};
-            if (row < r_end) v = __builtin_bit_cast(bf16x8, *(const u32x4*)(a.dz + row * NOUTP + c8));
+            if (row < r_end) v = __builtin_bit_cast(bf16x8, *(const u32x4*)(a.dz + row * a.ldz + c8));
 #pragma unroll
             for (int j = 0; j < 8; ++j) gt[c8 + j][rr] = to_bf16((float)v[j] * (c8 + j < 3 ? sp : sm));
         }
@@ -473,19 +554,23 @@ SKR_API int skr_mdn_head_fwd(const HeadFwd* a, float* out3, hipStream_t s) {
     if (a->M < 1 || a->M > 24 || a->NOUT != 3 + 6 * a->M || a->NOUTP % 32 || a->NOUTP < a->NOUT ||
         a->NOUTP > kMaxNoutP)
         return -2;
-    if (a->Hd % kKC != 0 || a->ldx % 4 != 0) return -3;
+    if (a->Hd % kKC != 0 || a->ldx % (a->x_bf16 ? 8 : 4) != 0 || ((uintptr_t)a->X & 15)) return -3;
+    if (a->dz != nullptr && (a->ldz < a->NOUTP || a->ldz % 8 || ((uintptr_t)a->dz & 15))) return -4;
     if (a->N <= 0) return 0;
     const int nb = (int)((a->N + kRows - 1) / kRows);
     static bool attr = false;
     if (!attr) {
-        if (hipFuncSetAttribute((const void*)mdn_head_fwd, hipFuncAttributeMaxDynamicSharedMemorySize,
+        if (hipFuncSetAttribute((const void*)mdn_head_fwd<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)fwd_lds()) != hipSuccess ||
+            hipFuncSetAttribute((const void*)mdn_head_fwd<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)fwd_lds()) != hipSuccess)
             return -9;
         attr = true;
     }
     // the z tile reuses the staging buffers: kRows * NOUTP floats must fit
     static_assert((size_t)kRows * kMaxNoutP * 4 <= (size_t)2 * kMaxNoutP * kLdk * 2, "z tile fits");
-    hipLaunchKernelGGL(mdn_head_fwd, dim3(nb), dim3(256), fwd_lds(), s, *a);
+    if (a->x_bf16) hipLaunchKernelGGL(mdn_head_fwd<true>, dim3(nb), dim3(256), fwd_lds(), s, *a);
+    else hipLaunchKernelGGL(mdn_head_fwd<false>, dim3(nb), dim3(256), fwd_lds(), s, *a);
     hipLaunchKernelGGL(mdn_head_finish, dim3(1), dim3(256), 0, s, a->part, nb, a->inv_n, out3);
     return SKR_CHECK_LAUNCH();
 }
@@ -493,7 +578,9 @@ SKR_API int skr_mdn_head_fwd(const HeadFwd* a, float* out3, hipStream_t s) {
 SKR_API int skr_mdn_head_nblocks(int64_t N) { return (int)((N + kRows - 1) / kRows); }
 
 SKR_API int skr_mdn_head_dx(const HeadDx* a, hipStream_t s) {
-    if (a->Hd % kDxCols != 0 || a->NOUTP % 32 || a->NOUTP > kMaxNoutP || a->lddx % 4) return -2;
+    if (a->Hd % kDxCols != 0 || a->NOUTP % 32 || a->NOUTP > kMaxNoutP || a->lddx % 4 || a->ldz < a->NOUTP ||
+        a->ldz % 8)
+        return -2;
     if (a->N <= 0) return 0;
     const size_t lds = (size_t)kDxCols * (a->NOUTP + 8) * 2 + (size_t)4 * 16 * (kDxCols + 4) * 4;
     static bool attr = false;
@@ -511,10 +598,13 @@ SKR_API int skr_mdn_head_dx(const HeadDx* a, hipStream_t s) {
 
 // slab: [S][Hd + 64][NOUTP] fp32 scratch; dW [Hd][NOUT], db [NOUT] outputs.
 SKR_API int skr_mdn_head_dw(const HeadDw* a, int S, int NOUT, float* dW, float* db, hipStream_t s) {
-    if (a->NOUTP % 32 || a->NOUTP > kMaxNoutP || a->rows_per % kRC || a->ldx % 4 || S < 1) return -2;
+    if (a->NOUTP % 32 || a->NOUTP > kMaxNoutP || a->rows_per % kRC || a->ldx % 4 || S < 1 || a->ldz < a->NOUTP ||
+        a->ldz % 8)
+        return -2;
     if (a->N <= 0) return 0;
     const int nf = (a->Hd + 1 + kDwRows - 1) / kDwRows;   // + the ones row (bias)
-    hipLaunchKernelGGL(mdn_head_dw, dim3(nf, S), dim3(256), 0, s, *a);
+    if (a->x_bf16) hipLaunchKernelGGL(mdn_head_dw<true>, dim3(nf, S), dim3(256), 0, s, *a);
+    else hipLaunchKernelGGL(mdn_head_dw<false>, dim3(nf, S), dim3(256), 0, s, *a);
     const int64_t total = (int64_t)(a->Hd + 1) * NOUT;
     hipLaunchKernelGGL(mdn_head_dw_reduce, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, a->slab, S, a->Hd,
                        a->NOUTP, NOUT, dW, db);

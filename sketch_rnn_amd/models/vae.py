@@ -266,7 +266,8 @@ class SketchVAE(nn.Module):
         keep = cfg.output_dropout_prob if (train and cfg.use_output_dropout) else 1.0
         r_cost, shape, pen = ops.mdn_head_loss(out.reshape(-1, out.shape[-1]), self.output_w, self.output_b, target,
                                                cfg.num_mixture, mode="magenta", is_training=cfg.is_training,
-                                               drop_keep=keep, drop_seed=seed, drop_stream=_S_OUT)
+                                               drop_keep=keep, drop_seed=seed, drop_stream=_S_OUT,
+                                               x_lp=getattr(out, "_skr_lp", None))
         cost = r_cost + kl * kl_weight
         out = {"cost": cost, "r_cost": r_cost, "kl_cost": kl, "shape_cost": shape, "pen_cost": pen}
         if split_encoder and cfg.conditional:

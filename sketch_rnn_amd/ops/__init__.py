@@ -143,8 +143,9 @@ def mdn_loss(z, target, M: int, mode: str = "magenta", stroke_importance: float 
 
 def mdn_head_loss(x, W, b, target, M: int, mode: str = "magenta", stroke_importance: float = 200.0,
                   is_training: bool = True, clamp: float = 1e-20, eps: float = 1e-6,
-                  drop_keep: float = 1.0, drop_seed=0, drop_stream: int = 0):
-    """MDN loss of the head ``z = dropout(x) @ W + b`` (``x [..., Hd]``).
+                  drop_keep: float = 1.0, drop_seed=0, drop_stream: int = 0, x_lp=None):
+    """MDN loss of the head ``z = dropout(x) @ W + b`` (``x [..., Hd]``;
+    ``x_lp``: an optional bf16 copy of ``x`` the fused head may read instead).
 
     bf16 HIP training: ONE kernel computes the projection on MFMA, the loss
     and dL/dz (csrc/mdn_head.hip; z never reaches HBM) and the backward runs
@@ -154,7 +155,7 @@ def mdn_head_loss(x, W, b, target, M: int, mode: str = "magenta", stroke_importa
     if head_fused_ok(x, W, M) and torch.is_grad_enabled():
         from .mdn_hip import mdn_head_loss_hip
         return mdn_head_loss_hip(x, W, b, target, M, mode, stroke_importance, is_training, clamp, eps,
-                                 drop_keep, drop_seed, drop_stream)
+                                 drop_keep, drop_seed, drop_stream, x_lp)
     from . import gemm
     from ..models.cells import dropout_mask
     x2 = x.reshape(-1, x.shape[-1])

@@ -213,7 +213,7 @@ class HeadFwd(C.Structure):
         ("M", _i), ("NOUT", _i), ("NOUTP", _i), ("mode", _i), ("mask_pen", _i),
         ("F", _f), ("log_floor", _f), ("inv_n", _f),
         ("keep", _f), ("seed", _p), ("stream", _u32),
-        ("dz", _p), ("part", _p),
+        ("dz", _p), ("part", _p), ("x_bf16", _i), ("ldz", _i64),
     ]
 
 
@@ -222,7 +222,7 @@ class HeadDx(C.Structure):
         ("dz", _p), ("N", _i64), ("NOUTP", _i),
         ("Wb", _p), ("Hd", _i),
         ("scale", _p), ("keep", _f), ("seed", _p), ("stream", _u32),
-        ("dX", _p), ("lddx", _i64),
+        ("dX", _p), ("lddx", _i64), ("ldz", _i64),
     ]
 
 
@@ -231,7 +231,7 @@ class HeadDw(C.Structure):
         ("X", _p), ("ldx", _i64), ("N", _i64), ("Hd", _i),
         ("dz", _p), ("NOUTP", _i),
         ("scale", _p), ("keep", _f), ("seed", _p), ("stream", _u32),
-        ("slab", _p), ("rows_per", _i64),
+        ("slab", _p), ("rows_per", _i64), ("ldz", _i64), ("x_bf16", _i),
     ]
 
 

@@ -212,17 +212,18 @@ def grad_slot(param: torch.Tensor, shape) -> Optional[torch.Tensor]:
 
 
 def _wgrad_splits(tiles: int, K: int) -> int:
-    """Split-K count of the long-K weight-gradient kernel: one workgroup per
+    """Split-K count of the long-K weight-gradient kernel. One workgroup per
     CU holds a 256 x 256 tile, so the run takes ceil(tiles * S / 256) rounds
-    of 1/S of the K range each, plus the partial slabs' extra traffic (~1 % of
-    a round per split). Measured (profiles/r5/wgrad_sweep.jsonl): dP 96 tiles
-    S = 5 (438 us) against the old whole-wave rule's S = 2 (514 us); dW_y 36
-    tiles S = 7; encoder 32 tiles S = 8; dW_h 256 tiles S = 1."""
+    of K / (32 S) K-steps (~1 us each), plus the fp32 partial slabs written
+    and summed (~0.1 us per slab tile). Measured (profiles/r5/wgrad_sweep.jsonl):
+    dP 96 tiles S = 5 (438 us) against the old whole-wave rule's S = 2 (514);
+    dW_y 36 tiles S = 7; encoder 32 tiles S = 8; dW_h 256 tiles S = 1; the
+    MDN head's [Hd x 256] gradient (8 tiles) S = 32."""
     best, pick = None, 1
-    for S in range(1, 9):
-        if S > 1 and S > K // 1024:   # at least 1024 rows per split
+    for S in range(1, 33):
+        if S > 1 and K // S < 512:   # at least 512 rows per split
             break
-        cost = -(-tiles * S // 256) / S + 0.01 * S
+        cost = -(-tiles * S // 256) * (K / 32.0 / S) + 0.1 * tiles * S
         if best is None or cost < best - 1e-9:
             best, pick = cost, S
     return pick

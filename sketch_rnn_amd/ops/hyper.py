@@ -350,6 +350,10 @@ class _HyperSeq(torch.autograd.Function):
             setattr(s, k, v)
         ctx.s = s
         ctx.dims = (T, B, IX, IN, H, Hh, E)
+        if A.dtype == torch.bfloat16:
+            # the bf16 copy of every h the next step's GEMM read: the fused MDN
+            # head reads it instead of Hout (ops.mdn_hip, same bf16 operands)
+            Hout._skr_lp = A[1:, :, :H]
         # (views of internal buffers nothing writes again)
         return Hout, hT, (CC[T] if T > 0 else c0c), hhT, (HCC[T] if T > 0 else hc0c)
 

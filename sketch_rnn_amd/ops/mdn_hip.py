@@ -81,8 +81,9 @@ def _noutp(nout: int) -> int:
 
 class _MDNHead(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, X, W, b, target, seed, meta):
+    def forward(ctx, X, W, b, target, seed, meta, X_lp):
         from ._hipapi import HeadDx, HeadDw, HeadFwd  # noqa: F401 (bound in native)
+        from . import gemm
         M, mode, F, mask_pen, log_floor, keep, stream = meta
         ctx.set_materialize_grads(False)   # the shape / pen terms are usually unused: None grads
         lib = native.require_hip()
@@ -91,6 +92,11 @@ class _MDNHead(torch.autograd.Function):
         X2 = X.reshape(-1, Hd).contiguous().float()
         N = X2.shape[0]
         dev = X2.device
+        XL = _lp_rows(X_lp, X, Hd) if keep >= 1.0 else None
+        # [dW; db] on the long-K weight-gradient GEMM (csrc/wgrad_gemm.hip)
+        # when the bf16 rows exist: dz then carries 256 columns per row (the
+        # kernel's N tile; columns >= NOUTP are never read back)
+        wg = XL is not None and gemm.WGRAD_HIP and Hd % 256 == 0 and NOUTP <= 256
         tgt = target.reshape(-1, 5).contiguous().float()
         Wt = torch.zeros(NOUTP, Hd, device=dev, dtype=torch.bfloat16)
         Wt[:NOUT] = W.t()
@@ -99,11 +105,15 @@ class _MDNHead(torch.autograd.Function):
         part = torch.empty(2 * nb, device=dev, dtype=torch.float32)
         out3 = torch.empty(3, device=dev, dtype=torch.float32)
         need = any(ctx.needs_input_grad[:3])
-        dz = torch.empty(N, NOUTP, device=dev, dtype=torch.bfloat16) if need else None
+        dz = torch.empty(N, 256 if wg else NOUTP, device=dev, dtype=torch.bfloat16) if need else None
         from .recurrent import _seed_tensor
         sd = _seed_tensor(seed, dev)
         a = HeadFwd()
-        a.X, a.ldx, a.N, a.Hd = X2.data_ptr(), X2.stride(0), N, Hd
+        if XL is not None:   # the decoder's bf16 h rows: half the bytes, the same bf16 operands
+            a.X, a.ldx, a.N, a.Hd, a.x_bf16 = XL.data_ptr(), XL.stride(0), N, Hd, 1
+        else:
+            a.X, a.ldx, a.N, a.Hd, a.x_bf16 = X2.data_ptr(), X2.stride(0), N, Hd, 0
+        a.ldz = dz.stride(0) if dz is not None else NOUTP
         a.Wt, a.bias, a.tgt, a.ldt = Wt.data_ptr(), bias.data_ptr(), tgt.data_ptr(), tgt.stride(0)
         a.M, a.NOUT, a.NOUTP, a.mode, a.mask_pen = M, NOUT, NOUTP, mode, mask_pen
         a.F, a.log_floor, a.inv_n = float(F), float(log_floor), 1.0 / max(N, 1)
@@ -114,19 +124,21 @@ class _MDNHead(torch.autograd.Function):
             raise RuntimeError("skr_mdn_head_fwd failed (%d)" % rc)
         ctx.save_for_backward(X2, W)
         ctx.dz, ctx.sd, ctx.meta, ctx.xshape, ctx.keep_alive = dz, sd, meta, X.shape, (Wt, tgt, bias, part)
+        ctx.XL = XL if wg else None
         return out3[0], out3[1], out3[2]
 
     @staticmethod
     def backward(ctx, g_total, g_shape, g_pen):
         from ._hipapi import HeadDw, HeadDx
+        from . import gemm
         X2, W = ctx.saved_tensors
         M, mode, F, mask_pen, log_floor, keep, stream = ctx.meta
         lib = native.require_hip()
-        dz, sd = ctx.dz, ctx.sd
-        ctx.dz = ctx.keep_alive = None
+        dz, sd, XL = ctx.dz, ctx.sd, ctx.XL
+        ctx.dz = ctx.keep_alive = ctx.XL = None
         N, Hd = X2.shape
         NOUT = W.shape[1]
-        NOUTP = dz.shape[1]
+        NOUTP = _noutp(NOUT)
         dev = X2.device
         if g_pen is None and g_shape is None and g_total is not None:   # the training loss: one copy
             scale = g_total.float().reshape(1).expand(2).contiguous()
@@ -143,12 +155,19 @@ class _MDNHead(torch.autograd.Function):
             a = HeadDx()
             a.dz, a.N, a.NOUTP, a.Wb, a.Hd = dz.data_ptr(), N, NOUTP, Wb.data_ptr(), Hd
             a.scale, a.keep, a.seed, a.stream = scale.data_ptr(), float(keep), sd.data_ptr(), int(stream)
-            a.dX, a.lddx = dX.data_ptr(), Hd
+            a.dX, a.lddx, a.ldz = dX.data_ptr(), Hd, dz.stride(0)
             rc = lib.lib.skr_mdn_head_dx(C.byref(a), _stream())
             if rc != 0:
                 raise RuntimeError("skr_mdn_head_dx failed (%d)" % rc)
             dX = dX.view(ctx.xshape)
-        if ctx.needs_input_grad[1] or ctx.needs_input_grad[2]:
+        if (ctx.needs_input_grad[1] or ctx.needs_input_grad[2]) and XL is not None:
+            # [dW | .] = X^T dz and db = colsum(dz) in one long-K GEMM pass, then
+            # the per-column-group upstream scale (pen / mixture columns)
+            full, cs = gemm.wgrad(XL, dz, colsum=True)
+            svec = torch.cat([scale[0:1].expand(3), scale[1:2].expand(NOUT - 3)])
+            dW = full[:, :NOUT] * svec
+            db = cs[:NOUT] * svec
+        elif ctx.needs_input_grad[1] or ctx.needs_input_grad[2]:
             S = HEAD_DW_SLABS   # row slabs: workgroups = (Hd/64 + 1) * S, each a latency-bound row loop
             rows_per = (-(-N // S) + 31) // 32 * 32
             S = -(-N // rows_per)
@@ -159,19 +178,38 @@ class _MDNHead(torch.autograd.Function):
             a.X, a.ldx, a.N, a.Hd = X2.data_ptr(), X2.stride(0), N, Hd
             a.dz, a.NOUTP = dz.data_ptr(), NOUTP
             a.scale, a.keep, a.seed, a.stream = scale.data_ptr(), float(keep), sd.data_ptr(), int(stream)
-            a.slab, a.rows_per = slab.data_ptr(), rows_per
+            a.slab, a.rows_per, a.ldz, a.x_bf16 = slab.data_ptr(), rows_per, dz.stride(0), 0
             rc = lib.lib.skr_mdn_head_dw(C.byref(a), S, NOUT, dW.data_ptr(), db.data_ptr(), _stream())
             if rc != 0:
                 raise RuntimeError("skr_mdn_head_dw failed (%d)" % rc)
-        return dX, dW, db, None, None, None
+        return dX, dW, db, None, None, None, None
+
+
+def _lp_rows(X_lp, X, Hd):
+    """``X_lp`` (a bf16 copy of ``X`` the producer already holds, e.g. the
+    decoder's saved bf16 h rows) as ``[N, Hd]`` rows the head kernels can
+    read directly: unit column stride, 16-byte aligned rows; else None."""
+    if (X_lp is None or X_lp.dtype != torch.bfloat16 or X_lp.shape[-1] != Hd or X_lp.numel() != X.numel()
+            or not X_lp.is_cuda):
+        return None
+    try:
+        XL = X_lp.view(-1, Hd)
+    except RuntimeError:
+        return None
+    if XL.stride(1) != 1 or XL.stride(0) % 8 or XL.data_ptr() % 16:
+        return None
+    return XL
 
 
 def mdn_head_loss_hip(x, W, b, target, M, mode="magenta", stroke_importance=200.0, is_training=True,
-                      clamp=1e-20, eps=1e-6, drop_keep=1.0, drop_seed=0, drop_stream=0):
+                      clamp=1e-20, eps=1e-6, drop_keep=1.0, drop_seed=0, drop_stream=0, x_lp=None):
     """``(total, shape, pen)`` of the MDN loss of ``z = drop(x) @ W + b`` with
-    the projection, loss and dL/dz fused (``x [..., Hd]`` fp32)."""
+    the projection, loss and dL/dz fused (``x [..., Hd]`` fp32). ``x_lp``:
+    an optional bf16 copy of ``x`` (same shape; any strides with unit column
+    stride), read instead of ``x`` when there is no dropout -- the kernels
+    round ``x`` to bf16 anyway, so the result is the same."""
     if mode == "reference":
         meta = (M, 0, float(stroke_importance), 0, math.log(clamp), float(drop_keep), int(drop_stream))
     else:
         meta = (M, 1, 0.0, 0 if is_training else 1, math.log(eps), float(drop_keep), int(drop_stream))
-    return _MDNHead.apply(x, W, b, target, drop_seed, meta)
+    return _MDNHead.apply(x, W, b, target, drop_seed, meta, x_lp)

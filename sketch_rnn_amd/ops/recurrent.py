@@ -318,6 +318,10 @@ class _LSTMSeq(torch.autograd.Function):
         s.wshape = W_h.shape
         ctx.s = s
         ctx.dims = (T, BB, H)
+        if A.dtype == torch.bfloat16 and rst is None and nd == 1:
+            # without resets the carried h is h': A[1:] is a bf16 copy of Hout
+            # (read by the fused MDN head instead of Hout, ops.mdn_hip)
+            Hout._skr_lp = A[1:]
         return Hout, hT, cT
 
     @staticmethod

@@ -112,3 +112,55 @@ def test_reference_model_bf16_head_grads_match_fp32():
     assert abs(c1 - c2) <= 1e-2 * abs(c2) + 1e-3, (c1, c2)
     assert _rel(w1, w2) < 3e-2, _rel(w1, w2)
     assert _rel(b1, b2) < 3e-2, _rel(b1, b2)
+
+
+@pytest.mark.parametrize("N,Hd,M", [(3001, 2048, 20), (777, 512, 24)])
+def test_fused_head_reads_bf16_rows(N, Hd, M):
+    """With a bf16 copy of x (``x_lp``: a column slice of a wider buffer, the
+    decoder's [h | hh] GEMM operand rows) the forward reads it instead of the
+    fp32 x -- the same bf16 MFMA operands, so loss, dz and dX are
+    bit-identical -- and [dW; db] runs on the long-K weight-gradient GEMM
+    (fp32 sums in another order: close to the fp32-rows kernel and to the
+    oracle)."""
+    x, W, b, t = _data(N, Hd, M, "magenta", N)
+    wide = torch.zeros(N, Hd + 256, device=DEV, dtype=torch.bfloat16)
+    wide[:, :Hd] = x.to(torch.bfloat16)
+    x_lp = wide[:, :Hd]
+    res = []
+    for lp in (None, x_lp):
+        ops.set_backend("hip")
+        ops.set_compute_dtype("bf16")
+        xs, Ws, bs = (v.clone().requires_grad_() for v in (x, W, b))
+        tot, shape, pen = ops.mdn_head_loss(xs, Ws, bs, t, M, mode="magenta", x_lp=lp)
+        (0.7 * tot + 0.2 * shape).backward()
+        torch.cuda.synchronize()
+        res.append([tot.detach(), shape.detach(), pen.detach(), xs.grad, Ws.grad, bs.grad])
+    for n, a, c in zip(["total", "shape", "pen", "dx"], res[0][:4], res[1][:4]):
+        assert torch.equal(a, c), n
+    for n, a, c in zip(["dW", "db"], res[0][4:], res[1][4:]):
+        assert _rel(c, a) < 2e-3, (n, _rel(c, a))
+    ref = _run(False, x, W, b, t, M, "magenta", 1.0, (0.7, 0.2, 0.0))
+    for n, a, r in zip(["dW", "db"], res[1][4:], ref[4:]):
+        assert _rel(a, r) < 3e-2, (n, _rel(a, r))
+
+
+def test_recurrences_expose_bf16_h_rows():
+    """The bf16 HyperLSTM and LSTM sequences attach their carried-h GEMM
+    operand rows (``_skr_lp``) to the output: exactly the bf16 rounding of
+    the returned fp32 h (what the fused head reads in its place)."""
+    from sketch_rnn_amd.models import cells as C
+    ops.set_backend("hip")
+    ops.set_compute_dtype("bf16")
+    torch.manual_seed(3)
+    T, B, IN, H = 7, 100, 5, 512
+    p = C.HyperLSTMParams(IN, H, 64, 8).to(DEV)
+    x = torch.randn(T, B, IN, device=DEV)
+    st = [torch.zeros(B, n, device=DEV) for n in (H, H, 64, 64)]
+    out, _ = ops.hyper_sequence(p, x, *st, drop_keep=0.9, drop_seed=4, drop_stream=9)
+    assert torch.equal(out._skr_lp, out.detach().to(torch.bfloat16))
+    W_h = torch.randn(H, 4 * H, device=DEV) / H ** 0.5
+    xp = torch.randn(T, B, 4 * H, device=DEV)
+    out2, _ = ops.lstm_sequence(xp, W_h, torch.zeros(B, H, device=DEV), torch.zeros(B, H, device=DEV),
+                                drop_keep=0.9, drop_seed=4, drop_stream=9)
+    lp = getattr(out2, "_skr_lp", None)   # (the persistent LSTM path keeps no such rows)
+    assert lp is None or torch.equal(lp, out2.detach().to(torch.bfloat16))
