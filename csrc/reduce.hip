@@ -218,6 +218,8 @@ __device__ __forceinline__ void ld4(const void* x, int64_t i, bool bf, float (&v
 // workgroup's rows split over the row groups and the groups summed in LDS
 // in a fixed order, one partial row per workgroup: narrow reductions keep
 // 256 threads busy per workgroup and few rows in flight per thread.
+constexpr int kCsRowsInFlight = 8;
+
 template <int KIND>
 __global__ __launch_bounds__(256) void colsum_multi_kernel(const CsJobs jobs) {
     __shared__ float red[2][256][4];
@@ -240,10 +242,13 @@ __global__ __launch_bounds__(256) void colsum_multi_kernel(const CsJobs jobs) {
     if (on && r0 < r1) {
         int64_t i = r0 / J.R2, j = r0 % J.R2;
         int64_t r = r0;
-        for (; r + 2 <= r1; r += 2) {
-            float xv[2][4], yv[2][4];
+        // kRowsInFlight rows loaded before any is summed (rows still summed in
+        // order: the result does not depend on the unroll)
+        constexpr int U = kCsRowsInFlight;
+        for (; r + U <= r1; r += U) {
+            float xv[U][4], yv[U][4];
 #pragma unroll
-            for (int k = 0; k < 2; ++k) {
+            for (int k = 0; k < U; ++k) {
                 const int64_t off = i * J.s1 + j * J.s2 + c;
                 ld4<KIND>(J.X, off, J.xbf, xv[k]);
                 if (J.Y) ld4<KIND>(J.Y, off, J.ybf, yv[k]);
@@ -256,7 +261,7 @@ __global__ __launch_bounds__(256) void colsum_multi_kernel(const CsJobs jobs) {
                 }
             }
 #pragma unroll
-            for (int k = 0; k < 2; ++k)
+            for (int k = 0; k < U; ++k)
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
                     sx[e] += xv[k][e];

@@ -1033,3 +1033,4 @@ def test_hyper_chained_launches_vs_unchained(B, T, fin_w):
         e_c = (runs["chain"][i].float() - ref).abs().max().item()
         e_p = (runs["plain"][i].float() - ref).abs().max().item()
         assert e_c <= 1.5 * e_p + 1e-3 * scale, (n, e_c, e_p, scale)
+
