@@ -213,7 +213,7 @@ class VAETrainer:
                  save_dir: str = "save/vae", use_graph: Optional[bool] = None,
                  log: Callable[[str], None] = print, metrics_path: Optional[str] = None,
                  compute_dtype: str = "fp32", max_skipped: int = 100, dp_wire_dtype: Optional[str] = None,
-                 force_reducer: bool = False):
+                 force_reducer: bool = False, dp_bucket_mb: float = 32.0):
         self.cfg = cfg
         self.train_set, self.valid_set, self.test_set = train_set, valid_set, test_set
         self.device = torch.device(device)
@@ -262,7 +262,7 @@ class VAETrainer:
         wire = dp_wire_dtype or os.environ.get("SKR_DP_WIRE", "fp32")
         # the arena plus its tail (this step's loss scalars, summed in the last
         # bucket); the 1/world average is folded into the clip + Adam kernels
-        self.reducer = dp.GradReducer(self.opt.grad_full, split=split, wire_dtype=wire,
+        self.reducer = dp.GradReducer(self.opt.grad_full, bucket_mb=dp_bucket_mb, split=split, wire_dtype=wire,
                                       force=force_reducer, fold_scale=True, tail=FlatAdam.TAIL) if reduce_on else None
         if reduce_on:
             self.opt.set_grad_scale(1.0 / self.world)

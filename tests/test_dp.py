@@ -1,4 +1,4 @@
-"""Data parallelism (P1/P2) on CPU with the gloo backend, world_size 2.
+"""Data parallelism (P1/P2) on CPU with the gloo backend, world_size 2 and 4.
 
 * gradient averaging through the bucketed flat-arena reducer equals the
   single-process gradient of the concatenated batch;
@@ -251,3 +251,125 @@ def test_grad_scale_fold_is_bitwise_equal_to_prescaled_arena():
             b.step()
             assert torch.equal(a.flat, b.flat) and torch.equal(a.m, b.m) and torch.equal(a.v, b.v)
             assert torch.equal(a.scalars[2], b.scalars[2])
+
+
+# ---- world size 4: uneven per-rank lengths, >= 3 buckets
+# per arena part, overlapped vs plain step, bf16 wire, loss-tail scalars, bench
+
+def _w4_cfg():
+    from sketch_rnn_amd.config import VAEConfig
+    return VAEConfig(enc_rnn_size=8, dec_rnn_size=16, z_size=4, num_mixture=2, max_seq_len=60, batch_size=3,
+                     save_every=0, seed=0, num_classes=3, random_scale_factor=0.0, augment_stroke_prob=0.0)
+
+
+def _w4_dataset(cfg):
+    """The same synthetic corpus on every rank (and in the reference process):
+    random_batch(rank, 4) then hands rank r rows [3r, 3r + 3) of one global
+    permutation -- sketches of different lengths on every rank."""
+    from sketch_rnn_amd.data.dataset import StrokeDataset
+    from sketch_rnn_amd.data.synthetic import synthetic_corpus
+    s, lab = synthetic_corpus(60, seed=11, max_len=cfg.max_seq_len, n_classes=3)
+    ds = StrokeDataset(s, cfg.batch_size, cfg.max_seq_len, labels=lab, seed=5)
+    ds.normalize()
+    return ds
+
+
+# bucket of 0.001 MB = 256 fp32 / 512 bf16 elements: several buckets in both
+# parts of the ~3.4K-parameter arena (decoder/head part, encoder part)
+_W4_BUCKET_MB = 0.001
+
+
+def _w4_grad_worker(rank, world, port, out_dir):
+    """One training step per mode (overlapped two-phase step / plain step,
+    fp32 / bf16 wire) from the same broadcast weights; saved: the reduced
+    gradient arena (the SUM over ranks: 1/world is folded into Adam), the
+    reduced loss tail and the updated weights."""
+    dp = _init(rank, world, port)
+    torch.set_num_threads(1)
+    from sketch_rnn_amd.train.trainer import VAETrainer
+    cfg = _w4_cfg()
+    res = {}
+    for mode, wire in (("1", "fp32"), ("0", "fp32"), ("1", "bf16")):
+        os.environ["SKR_DP_OVERLAP"] = mode
+        ds = _w4_dataset(cfg)
+        tr = VAETrainer(cfg, ds, None, None, save_dir=os.path.join(out_dir, "w4" + mode + wire), log=lambda s: None,
+                        dp_wire_dtype=wire, dp_bucket_mb=_W4_BUCKET_MB)
+        assert tr.overlap == (mode == "1")
+        parts = tr.reducer.parts if tr.overlap else [tr.reducer.buckets]
+        assert all(len(p) >= 3 for p in parts), [len(p) for p in parts]
+        batch = tr.batch_to_device(ds.random_batch(rank, world))
+        tr.train_step(*batch)
+        key = "ov%s_%s" % (mode, wire)
+        res[key] = {"grad": tr.opt.grad.clone(), "flat": tr.opt.flat.clone(), "red": tr.reduced_scalars(),
+                    "len": batch[1].clone()}
+    os.environ.pop("SKR_DP_OVERLAP")
+    torch.save(res, os.path.join(out_dir, "g4_%d.pt" % rank))
+    dp.barrier()
+    torch.distributed.destroy_process_group()
+
+
+def test_dp_world4_reduced_gradient_equals_mean_of_rank_gradients(tmp_path):
+    """Four gloo ranks, uneven per-rank sketch lengths, >= 3 buckets per part:
+    the reduced gradient equals the mean of the four per-rank gradients
+    recomputed in one process (same weights, same rank batches, same noise
+    seeds), for the overlapped and the plain step; the overlapped step equals
+    the plain one bit for bit; every rank ends with the same weights; the
+    loss tail carries the mean cost and the global valid-point count; the
+    bf16 wire stays within bf16 rounding of the fp32 wire."""
+    world = 4
+    _spawn(_w4_grad_worker, tmp_path, world=world)
+    g = [torch.load(tmp_path / ("g4_%d.pt" % k), weights_only=True) for k in range(world)]
+    lens = [int(r["ov1_fp32"]["len"].sum()) for r in g]
+    assert len(set(lens)) > 1, lens                                   # uneven per-rank lengths
+    for key in ("ov1_fp32", "ov0_fp32", "ov1_bf16"):
+        for r in range(1, world):
+            assert torch.equal(g[0][key]["flat"], g[r][key]["flat"]), (key, r)
+            assert torch.equal(g[0][key]["grad"], g[r][key]["grad"]), (key, r)
+    assert torch.equal(g[0]["ov1_fp32"]["grad"], g[0]["ov0_fp32"]["grad"])
+    assert torch.equal(g[0]["ov1_fp32"]["flat"], g[0]["ov0_fp32"]["flat"])
+    # reference: the same four rank batches in one process
+    from sketch_rnn_amd.train import schedules
+    from sketch_rnn_amd.train.trainer import VAETrainer
+    cfg = _w4_cfg()
+    ds = _w4_dataset(cfg)
+    tr = VAETrainer(cfg, ds, None, None, save_dir=str(tmp_path / "ref"), log=lambda s: None)
+    full = ds.random_batch(0, 1, batch_size=cfg.batch_size * world)
+    tr.kl_w.fill_(schedules.kl_weight(cfg, 0))
+    acc = torch.zeros_like(tr.opt.grad)
+    costs = []
+    for r in range(world):
+        sl = slice(r * cfg.batch_size, (r + 1) * cfg.batch_size)
+        s, l, c = tr.batch_to_device((full[0][sl], full[1][sl], full[2][sl]))
+        assert torch.equal(l, g[r]["ov1_fp32"]["len"])
+        tr.seed.fill_(r)                                              # rank r's noise stream
+        out = tr._fwd_bwd(s, l, c)
+        costs.append(float(out["cost"]))
+        acc += tr.opt.grad
+    dp_grad = g[0]["ov1_fp32"]["grad"]        # (same init: cfg.seed 0 = rank 0's broadcast weights)
+    assert torch.allclose(dp_grad, acc, atol=1e-6, rtol=1e-4), float((dp_grad - acc).abs().max())
+    red = g[0]["ov1_fp32"]["red"]
+    assert abs(red["cost"] - sum(costs) / world) < 1e-5 * max(1.0, abs(red["cost"]))
+    assert red["valid_points"] == sum(lens)
+    b16 = g[0]["ov1_bf16"]["grad"]
+    assert float(((b16 - dp_grad).abs() / dp_grad.abs().clamp_min(1e-3)).median()) < 4e-3
+    assert g[0]["ov1_bf16"]["red"]["valid_points"] == sum(lens)      # the tail travels in fp32
+
+
+def test_bench_world4_cpu(tmp_path):
+    """bench.py under torch.distributed.run with 4 gloo ranks."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "4",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(root, "bench.py"),
+           "--gpus", "4", "--steps", "2", "--warmup", "1", "--config", "plumbing", "--batch", "4",
+           "--seq-len", "24", "--sketches", "80", "--dtype", "fp32", "--backend", "torch", "--no-eval"]
+    env = dict(os.environ, OMP_NUM_THREADS="1", CUDA_VISIBLE_DEVICES="")
+    p = subprocess.run(cmd, cwd=str(tmp_path), env=env, capture_output=True, text=True, timeout=600)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout
+    rec = json.loads(lines[0])
+    assert rec["n_gpus"] == 4 and rec["config"]["global_batch"] == 16 and rec["config"]["parallelism"] == "dp4"
+    assert rec["config"]["world_size_observed"] == 4
