@@ -66,6 +66,8 @@ struct WgArgs {
     float* C; int64_t c_bs;               // slab s of batch z at C + z * c_bs + s * M * N
     float* cs;                            // colsum slabs [batch][S][N] or null
     int64_t K; int M, N, S, kslice, tiles_m, tiles_n, total, per_xcd;
+    int stride;                           // workgroups per XCD slot: tile j, j + stride, ... of one XCD's list
+    int acc;                              // 1: C (and cs) += the product instead of =
 };
 
 __device__ __forceinline__ int swz(int row, int chunk) { return chunk ^ ((row & 3) << 2); }
@@ -111,181 +113,191 @@ __device__ __forceinline__ bf16x8 join(const s16x4 (&h)[2]) {
 // DB: both k16 halves' fragment sets read up front, the second half's
 // reads in flight under the first half's MFMAs (24 transposed reads per
 // K-step in one batch instead of two exposed read -> wait -> MFMA rounds).
-template <bool CS, bool DB>
+// BG: the bounded-grid form (several tiles per workgroup); otherwise one tile.
+template <bool CS, bool DB, bool BG>
 __global__ __launch_bounds__(NT) void wgrad_kernel(const WgArgs g) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    // ---- workgroup -> (batch, split, tile): XCD-major linear order
-    const int xcd = blockIdx.x & 7, lin = xcd * g.per_xcd + (blockIdx.x >> 3);
-    if (lin >= g.total) return;                       // whole workgroup, before any barrier
-    const int tiles = g.tiles_m * g.tiles_n;
-    const int t = lin % tiles, zs = lin / tiles;      // zs = batch * S + split
-    const int split = zs % g.S, z = zs / g.S;
-    const int gsz = 4 * g.tiles_n, grp = t / gsz, fm = grp * 4;
-    const int gm = min(g.tiles_m - fm, 4);
-    const int tm = fm + (t % gsz) % gm, tn = (t % gsz) / gm;
-    const int m0 = tm * TM, n0 = tn * TN;
-    const int64_t k0 = (int64_t)split * g.kslice;
-    const int64_t kend = min(g.K, k0 + g.kslice);
-    const int nk = (int)((kend - k0 + BK - 1) / BK);
-    const int tail = (int)(kend - k0) - (nk - 1) * BK;     // valid rows of the last K-step (1..32)
-    const __hip_bfloat16* A = g.A + z * g.a_bs;
-    const __hip_bfloat16* B = g.B + z * g.b_bs;
+    // ---- workgroup -> (batch, split, tile): XCD-major linear order; a grid
+    // smaller than the tile count (background launches) walks its XCD's list
+    // with stride g.stride
+    const int xcd = blockIdx.x & 7;
+    for (int jx = blockIdx.x >> 3; jx < g.per_xcd; jx += g.stride) {
+        const int lin = xcd * g.per_xcd + jx;
+        if (lin >= g.total) return;                       // whole workgroup, before any barrier
+        const int tiles = g.tiles_m * g.tiles_n;
+        const int t = lin % tiles, zs = lin / tiles;      // zs = batch * S + split
+        const int split = zs % g.S, z = zs / g.S;
+        const int gsz = 4 * g.tiles_n, grp = t / gsz, fm = grp * 4;
+        const int gm = min(g.tiles_m - fm, 4);
+        const int tm = fm + (t % gsz) % gm, tn = (t % gsz) / gm;
+        const int m0 = tm * TM, n0 = tn * TN;
+        const int64_t k0 = (int64_t)split * g.kslice;
+        const int64_t kend = min(g.K, k0 + g.kslice);
+        const int nk = (int)((kend - k0 + BK - 1) / BK);
+        const int tail = (int)(kend - k0) - (nk - 1) * BK;     // valid rows of the last K-step (1..32)
+        const __hip_bfloat16* A = g.A + z * g.a_bs;
+        const __hip_bfloat16* B = g.B + z * g.b_bs;
 
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    // ---- DMA sources: wave w moves tile rows {2w, 2w+1} and {2w+16, 2w+17} of A and of B
-    const int hr = lane >> 5, lc = lane & 31;
-    const __hip_bfloat16* asrc[2];
-    const __hip_bfloat16* bsrc[2];
-    int rowk[2];
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-        const int R = 2 * w + 16 * i + hr;
-        rowk[i] = R;
-        const int c = swz(R, lc);
-        asrc[i] = A + m0 + 8 * c;
-        bsrc[i] = B + n0 + 8 * c;
-    }
-    auto issue = [&](int kt) {
-        char* st = smem + (kt % NSTG) * STGB;
+        const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+        // ---- DMA sources: wave w moves tile rows {2w, 2w+1} and {2w+16, 2w+17} of A and of B
+        const int hr = lane >> 5, lc = lane & 31;
+        const __hip_bfloat16* asrc[2];
+        const __hip_bfloat16* bsrc[2];
+        int rowk[2];
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
-            const int64_t kr = min(k0 + (int64_t)kt * BK + rowk[i], kend - 1);   // clamped: finite data
-            __builtin_amdgcn_global_load_lds((const void*)(asrc[i] + kr * g.lda),
-                                             (__attribute__((address_space(3))) void*)(st + (2 * w + 16 * i) * ROWB),
-                                             16, 0, 0);
-            __builtin_amdgcn_global_load_lds((const void*)(bsrc[i] + kr * g.ldb),
-                                             (__attribute__((address_space(3))) void*)(st + OPB + (2 * w + 16 * i) * ROWB),
-                                             16, 0, 0);
+            const int R = 2 * w + 16 * i + hr;
+            rowk[i] = R;
+            const int c = swz(R, lc);
+            asrc[i] = A + m0 + 8 * c;
+            bsrc[i] = B + n0 + 8 * c;
         }
-    };
-
-    // ---- fragment read offsets (bytes inside an operand tile), fixed across K-steps
-    const int wm = w >> 1, wn = w & 1;
-    const int G = lane >> 4, h = G >> 1, q = (lane >> 2) & 3, p = lane & 3;
-    int aoff[2][2][2], boff[4][2][2];     // [tile][k16 half][read]
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-        for (int rd = 0; rd < 2; ++rd) {
-            const int row = 16 * ks + 8 * h + 4 * rd + q;
+        auto issue = [&](int kt) {
+            char* st = smem + (kt % NSTG) * STGB;
 #pragma unroll
             for (int i = 0; i < 2; ++i) {
-                const int col = 64 * wm + 32 * i + 16 * (G & 1) + 4 * p;
-                aoff[i][ks][rd] = row * ROWB + (swz(row, col >> 3) << 4) + 8 * (p & 1);
+                const int64_t kr = min(k0 + (int64_t)kt * BK + rowk[i], kend - 1);   // clamped: finite data
+                __builtin_amdgcn_global_load_lds((const void*)(asrc[i] + kr * g.lda),
+                                                 (__attribute__((address_space(3))) void*)(st + (2 * w + 16 * i) * ROWB),
+                                                 16, 0, 0);
+                __builtin_amdgcn_global_load_lds((const void*)(bsrc[i] + kr * g.ldb),
+                                                 (__attribute__((address_space(3))) void*)(st + OPB + (2 * w + 16 * i) * ROWB),
+                                                 16, 0, 0);
             }
+        };
+
+        // ---- fragment read offsets (bytes inside an operand tile), fixed across K-steps
+        const int wm = w >> 1, wn = w & 1;
+        const int G = lane >> 4, h = G >> 1, q = (lane >> 2) & 3, p = lane & 3;
+        int aoff[2][2][2], boff[4][2][2];     // [tile][k16 half][read]
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const int col = 128 * wn + 32 * j + 16 * (G & 1) + 4 * p;
-                boff[j][ks][rd] = row * ROWB + (swz(row, col >> 3) << 4) + 8 * (p & 1);
+        for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+            for (int rd = 0; rd < 2; ++rd) {
+                const int row = 16 * ks + 8 * h + 4 * rd + q;
+#pragma unroll
+                for (int i = 0; i < 2; ++i) {
+                    const int col = 64 * wm + 32 * i + 16 * (G & 1) + 4 * p;
+                    aoff[i][ks][rd] = row * ROWB + (swz(row, col >> 3) << 4) + 8 * (p & 1);
+                }
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int col = 128 * wn + 32 * j + 16 * (G & 1) + 4 * p;
+                    boff[j][ks][rd] = row * ROWB + (swz(row, col >> 3) << 4) + 8 * (p & 1);
+                }
             }
-        }
 
-    f32x16 acc[2][4];
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-#pragma unroll
-            for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
-    float cs[4] = {0.f, 0.f, 0.f, 0.f};
-
-    auto zero_tail = [&](char* st) {
-        // rows past kend hold clamped (duplicate) data: zero them in both operands
-        const int per = (BK - tail) * ROWB / 16;              // 16-byte pieces per operand
-        for (int i = tid; i < 2 * per; i += NT) {
-            const int op = i / per, r = i - op * per;
-            *(int4*)(st + op * OPB + tail * ROWB + 16 * r) = int4{0, 0, 0, 0};
-        }
-        skr::lds_barrier();
-    };
-    const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)smem;
-    // 12 transposed reads per fragment set (2 A tiles + 4 B tiles, 2 reads each)
-    auto read_frags = [&](int stage, int ks, Frags& f) {
-        const uint32_t st = lds0 + stage * STGB;
-#pragma unroll
-        for (int i = 0; i < 2; ++i)
-#pragma unroll
-            for (int rd = 0; rd < 2; ++rd) f.a[i][rd] = tr_read(st + aoff[i][ks][rd]);
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-#pragma unroll
-            for (int rd = 0; rd < 2; ++rd) f.b[j][rd] = tr_read(st + OPB + boff[j][ks][rd]);
-    };
-    auto mfmas = [&](const Frags& f) {
-        bf16x8 af[2], bfr[4];
-#pragma unroll
-        for (int i = 0; i < 2; ++i) af[i] = join(f.a[i]);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) bfr[j] = join(f.b[j]);
+        f32x16 acc[2][4];
 #pragma unroll
         for (int i = 0; i < 2; ++i)
 #pragma unroll
             for (int j = 0; j < 4; ++j)
-                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+#pragma unroll
+                for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+        float cs[4] = {0.f, 0.f, 0.f, 0.f};
+
+        auto zero_tail = [&](char* st) {
+            // rows past kend hold clamped (duplicate) data: zero them in both operands
+            const int per = (BK - tail) * ROWB / 16;              // 16-byte pieces per operand
+            for (int i = tid; i < 2 * per; i += NT) {
+                const int op = i / per, r = i - op * per;
+                *(int4*)(st + op * OPB + tail * ROWB + 16 * r) = int4{0, 0, 0, 0};
+            }
+            skr::lds_barrier();
+        };
+        const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)smem;
+        // 12 transposed reads per fragment set (2 A tiles + 4 B tiles, 2 reads each)
+        auto read_frags = [&](int stage, int ks, Frags& f) {
+            const uint32_t st = lds0 + stage * STGB;
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int rd = 0; rd < 2; ++rd) f.a[i][rd] = tr_read(st + aoff[i][ks][rd]);
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+#pragma unroll
+                for (int rd = 0; rd < 2; ++rd) f.b[j][rd] = tr_read(st + OPB + boff[j][ks][rd]);
+        };
+        auto mfmas = [&](const Frags& f) {
+            bf16x8 af[2], bfr[4];
+#pragma unroll
+            for (int i = 0; i < 2; ++i) af[i] = join(f.a[i]);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) bfr[j] = join(f.b[j]);
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+            if constexpr (CS) {
+                if (wm == 0) {
+#pragma unroll
+                    for (int j = 0; j < 4; ++j)
+#pragma unroll
+                        for (int e = 0; e < 8; ++e) cs[j] += (float)bfr[j][e];
+                }
+            }
+        };
+
+#pragma unroll
+        for (int s = 0; s < NSTG - 1; ++s)
+            if (s < nk) issue(s);
+        for (int kt = 0; kt < nk; ++kt) {
+            wait_ahead<NSTG - 2>(min(nk - 1 - kt, NSTG - 2));
+            __builtin_amdgcn_s_barrier();     // stage kt landed for every wave; stage kt-1 is free
+            if (kt + NSTG - 1 < nk) issue(kt + NSTG - 1);
+            if (kt == nk - 1 && tail < BK) zero_tail(smem + (kt % NSTG) * STGB);
+            if constexpr (DB) {
+                Frags f0, f1;
+                read_frags(kt % NSTG, 0, f0);
+                read_frags(kt % NSTG, 1, f1);
+                frag_wait<12>(f0);
+                mfmas(f0);
+                frag_wait<0>(f1);
+                mfmas(f1);
+            } else {
+#pragma unroll
+                for (int ks = 0; ks < 2; ++ks) {
+                    Frags f;
+                    read_frags(kt % NSTG, ks, f);
+                    frag_wait<0>(f);
+                    mfmas(f);
+                }
+            }
+        }
+        // ---- epilogue: fp32 slab (lane: column r; registers: rows (e&3) + 8(e>>2) + 4h)
+        float* C = g.C + z * g.c_bs + (int64_t)split * g.M * g.N;
+        const int r = lane & 31;
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int col = n0 + 128 * wn + 32 * j + r;
+#pragma unroll
+                for (int e = 0; e < 16; ++e) {
+                    const int row = m0 + 64 * wm + 32 * i + (e & 3) + 8 * (e >> 2) + 4 * h;
+                    float* c = C + (int64_t)row * g.N + col;
+                    *c = g.acc ? *c + acc[i][j][e] : acc[i][j][e];
+                }
+            }
         if constexpr (CS) {
             if (wm == 0) {
 #pragma unroll
-                for (int j = 0; j < 4; ++j)
-#pragma unroll
-                    for (int e = 0; e < 8; ++e) cs[j] += (float)bfr[j][e];
+                for (int j = 0; j < 4; ++j) {
+                    const float v = cs[j] + __shfl_xor(cs[j], 32, 64);
+                    float* c = g.cs + (int64_t)zs * g.N + n0 + 128 * wn + 32 * j + r;
+                    if (lane < 32) *c = g.acc ? *c + v : v;
+                }
             }
         }
-    };
-
-#pragma unroll
-    for (int s = 0; s < NSTG - 1; ++s)
-        if (s < nk) issue(s);
-    for (int kt = 0; kt < nk; ++kt) {
-        wait_ahead<NSTG - 2>(min(nk - 1 - kt, NSTG - 2));
-        __builtin_amdgcn_s_barrier();     // stage kt landed for every wave; stage kt-1 is free
-        if (kt + NSTG - 1 < nk) issue(kt + NSTG - 1);
-        if (kt == nk - 1 && tail < BK) zero_tail(smem + (kt % NSTG) * STGB);
-        if constexpr (DB) {
-            Frags f0, f1;
-            read_frags(kt % NSTG, 0, f0);
-            read_frags(kt % NSTG, 1, f1);
-            frag_wait<12>(f0);
-            mfmas(f0);
-            frag_wait<0>(f1);
-            mfmas(f1);
-        } else {
-#pragma unroll
-            for (int ks = 0; ks < 2; ++ks) {
-                Frags f;
-                read_frags(kt % NSTG, ks, f);
-                frag_wait<0>(f);
-                mfmas(f);
-            }
-        }
-    }
-    // ---- epilogue: fp32 slab (lane: column r; registers: rows (e&3) + 8(e>>2) + 4h)
-    float* C = g.C + z * g.c_bs + (int64_t)split * g.M * g.N;
-    const int r = lane & 31;
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const int col = n0 + 128 * wn + 32 * j + r;
-#pragma unroll
-            for (int e = 0; e < 16; ++e) {
-                const int row = m0 + 64 * wm + 32 * i + (e & 3) + 8 * (e >> 2) + 4 * h;
-                C[(int64_t)row * g.N + col] = acc[i][j][e];
-            }
-        }
-    if constexpr (CS) {
-        if (wm == 0) {
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const float v = cs[j] + __shfl_xor(cs[j], 32, 64);
-                if (lane < 32) g.cs[(int64_t)zs * g.N + n0 + 128 * wn + 32 * j + r] = v;
-            }
-        }
+        if constexpr (!BG) break;
+        __syncthreads();   // every wave's LDS reads of this tile are done before the next tile's DMA
     }
 }
 
 // out[z][i] = sum_s slab[z][s][i] (i < n, n % 4 == 0), fixed order: deterministic
 __global__ __launch_bounds__(256) void slab_sum_kernel(const float* __restrict__ src, int S, int64_t n, int nb,
-                                                       float* __restrict__ out) {
+                                                       float* __restrict__ out, int acc) {
     const int64_t i4 = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
     if (i4 >= n * nb) return;
     const int64_t z = i4 / n, i = i4 - z * n;
@@ -294,6 +306,10 @@ __global__ __launch_bounds__(256) void slab_sum_kernel(const float* __restrict__
     for (int s = 1; s < S; ++s) {
         const float4 b = *(const float4*)(p + s * n);
         a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+    }
+    if (acc) {   // added to the destination last: the chunked (background) order of ops/gemm.py
+        const float4 o = *(const float4*)(out + i4);
+        a.x = o.x + a.x; a.y = o.y + a.y; a.z = o.z + a.z; a.w = o.w + a.w;
     }
     *(float4*)(out + i4) = a;
 }
@@ -310,16 +326,20 @@ SKR_API int skr_wgrad_set_variant(int db) {
     return prev;
 }
 
-// C[z] = A[z]^T . B[z] (+ cs[z] = colsum(B[z]) when cs != null) for z < nb.
+// C[z] (+)= A[z]^T . B[z] (+ cs[z] (+)= colsum(B[z]) when cs != null) for z < nb.
 // A [K, M] bf16 (lda, batch stride a_bs elements), B [K, N] bf16 (ldb, b_bs).
 // S split-K slabs: slab s of batch z at work + (z * S + s) * M * N (fp32);
 // with S == 1 the kernel writes C directly (work unused). cs_work [nb][S][N].
 // Requirements: M % 256 == 0, N % 256 == 0, lda, ldb % 8 == 0, 16-byte
 // aligned bases (returns -2 / -4 otherwise: callers use a library GEMM).
-SKR_API int skr_wgrad(const void* A, int64_t lda, int64_t a_bs, const void* B, int64_t ldb, int64_t b_bs,
-                      int64_t K, int M, int N, int nb, int S, float* C, float* work, float* cs, float* cs_work,
-                      hipStream_t s) {
-    if (K <= 0 || M <= 0 || N <= 0 || nb <= 0) return -2;
+// acc: add into C / cs instead of overwriting them. max_grid > 0 (a multiple
+// of 8): at most that many workgroups, each walking several tiles -- the
+// background launches of ops/gemm.py that run beside the HyperLSTM backward
+// scan on a second stream and must leave most CUs to it.
+SKR_API int skr_wgrad2(const void* A, int64_t lda, int64_t a_bs, const void* B, int64_t ldb, int64_t b_bs,
+                       int64_t K, int M, int N, int nb, int S, float* C, float* work, float* cs, float* cs_work,
+                       int acc, int max_grid, hipStream_t s) {
+    if (K <= 0 || M <= 0 || N <= 0 || nb <= 0 || max_grid < 0 || max_grid % 8) return -2;
     if (M % TM || N % TN || lda % 8 || ldb % 8 || a_bs % 8 || b_bs % 8 || S < 1) return -2;
     if (((uintptr_t)A | (uintptr_t)B | (uintptr_t)C) & 15) return -4;
     if (S > 1 && work == nullptr) return -3;
@@ -336,30 +356,48 @@ SKR_API int skr_wgrad(const void* A, int64_t lda, int64_t a_bs, const void* B, i
     g.tiles_m = M / TM; g.tiles_n = N / TN;
     g.total = nb * S * g.tiles_m * g.tiles_n;
     g.per_xcd = (g.total + 7) / 8;
-    const int grid = 8 * g.per_xcd;
+    g.stride = max_grid > 0 ? min(g.per_xcd, max_grid / 8) : g.per_xcd;
+    g.acc = (acc != 0 && S == 1) ? 1 : 0;   // with split-K slabs the sum pass adds instead
+    const int grid = 8 * g.stride;
     const size_t lds = (size_t)NSTG * STGB;
     static bool attr = false;
     if (!attr) {
-        const void* ks[4] = {(const void*)wgrad_kernel<false, false>, (const void*)wgrad_kernel<true, false>,
-                             (const void*)wgrad_kernel<false, true>, (const void*)wgrad_kernel<true, true>};
+        const void* ks[8] = {(const void*)wgrad_kernel<false, false, false>, (const void*)wgrad_kernel<true, false, false>,
+                             (const void*)wgrad_kernel<false, true, false>, (const void*)wgrad_kernel<true, true, false>,
+                             (const void*)wgrad_kernel<false, false, true>, (const void*)wgrad_kernel<true, false, true>,
+                             (const void*)wgrad_kernel<false, true, true>, (const void*)wgrad_kernel<true, true, true>};
         for (const void* k : ks)
             if (hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) return -6;
         attr = true;
     }
-    const bool cs_on = g.cs != nullptr;
+    const bool cs_on = g.cs != nullptr, bg = g.stride < g.per_xcd;
+    const dim3 gd(grid), bd(NT);
+#define SKR_WG_LAUNCH(CS_, DB_)                                                                   \
+    do {                                                                                          \
+        if (bg) hipLaunchKernelGGL((wgrad_kernel<CS_, DB_, true>), gd, bd, lds, s, g);            \
+        else hipLaunchKernelGGL((wgrad_kernel<CS_, DB_, false>), gd, bd, lds, s, g);              \
+    } while (0)
     if (g_wgrad_db) {
-        if (cs_on) hipLaunchKernelGGL((wgrad_kernel<true, true>), dim3(grid), dim3(NT), lds, s, g);
-        else hipLaunchKernelGGL((wgrad_kernel<false, true>), dim3(grid), dim3(NT), lds, s, g);
+        if (cs_on) SKR_WG_LAUNCH(true, true);
+        else SKR_WG_LAUNCH(false, true);
     } else {
-        if (cs_on) hipLaunchKernelGGL((wgrad_kernel<true, false>), dim3(grid), dim3(NT), lds, s, g);
-        else hipLaunchKernelGGL((wgrad_kernel<false, false>), dim3(grid), dim3(NT), lds, s, g);
+        if (cs_on) SKR_WG_LAUNCH(true, false);
+        else SKR_WG_LAUNCH(false, false);
     }
+#undef SKR_WG_LAUNCH
     if (S > 1) {
         const int64_t n = (int64_t)M * N;
-        hipLaunchKernelGGL(slab_sum_kernel, dim3((unsigned)((n * nb / 4 + 255) / 256)), dim3(256), 0, s, work, S, n, nb, C);
+        hipLaunchKernelGGL(slab_sum_kernel, dim3((unsigned)((n * nb / 4 + 255) / 256)), dim3(256), 0, s, work, S, n, nb, C,
+                           acc);
         if (cs != nullptr)
             hipLaunchKernelGGL(slab_sum_kernel, dim3((unsigned)((N * nb / 4 + 255) / 256)), dim3(256), 0, s, cs_work, S,
-                               (int64_t)N, nb, cs);
+                               (int64_t)N, nb, cs, acc);
     }
     return SKR_CHECK_LAUNCH();
+}
+
+SKR_API int skr_wgrad(const void* A, int64_t lda, int64_t a_bs, const void* B, int64_t ldb, int64_t b_bs,
+                      int64_t K, int M, int N, int nb, int S, float* C, float* work, float* cs, float* cs_work,
+                      hipStream_t s) {
+    return skr_wgrad2(A, lda, a_bs, B, ldb, b_bs, K, M, N, nb, S, C, work, cs, cs_work, 0, 0, s);
 }

@@ -1,10 +1,16 @@
 #!/usr/bin/env python3
-"""Per-kernel MFMA utilisation and effective clock from one rocprofv3 --pmc
-pass with SQ_VALU_MFMA_BUSY_CYCLES and GRBM_GUI_ACTIVE (MI355X_MICROARCH.md:
-MFMA busy cycles are summed over the SIMDs, GRBM_GUI_ACTIVE over the 8 XCDs):
+"""Per-kernel MFMA utilisation from one rocprofv3 --pmc pass with
+SQ_VALU_MFMA_BUSY_CYCLES (busy cycles summed over the chip's 1,024 SIMDs).
 
-  util  = SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 * 1024 SIMDs)
-  clock = GRBM_GUI_ACTIVE / 8 / kernel wall time  (reads high below ~0.3 ms)
+  util = SQ_VALU_MFMA_BUSY_CYCLES / (kernel duration x 1024 SIMDs x 2.4 GHz)
+
+The denominator uses the part's MAXIMUM clock (2.4 GHz, MI355X_MICROARCH.md
+chip table) and the kernel-trace duration of the same dispatches, so the
+figure is a LOWER bound on the fraction of available matrix cycles (the chip
+holds a lower clock under MFMA load). No clock is derived from
+GRBM_GUI_ACTIVE: that quotient reads high on dispatches shorter than about
+0.3 ms (it gave 3-11 "GHz" for the recurrent per-step kernels in round 5);
+it is printed only for dispatches of >= 0.3 ms, as a cross-check.
 
 usage: pmc_mfma.py counter_collection.csv [top N]"""
 import csv
@@ -36,13 +42,14 @@ def main():
                 calls[k] += 1
                 dur[k] += (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9
     top = int(sys.argv[2]) if len(sys.argv) > 2 else 25
-    rows = sorted(((active[k], k) for k in active), reverse=True)[:top]
-    print("%-64s %6s %10s %9s %9s" % ("kernel", "calls", "us/call", "MFMA %", "GHz"))
+    rows = sorted(((busy[k], k) for k in busy), reverse=True)[:top]
+    print("%-64s %6s %10s %13s %16s" % ("kernel", "calls", "us/call", "MFMA % (>=)", "GRBM GHz (>=0.3ms)"))
     for _, k in rows:
-        chip = active[k] / 8.0
-        util = 100.0 * busy[k] / (chip * 1024) if chip > 0 else 0.0
-        ghz = chip / dur[k] / 1e9 if dur[k] > 0 else 0.0
-        print("%-64s %6d %10.2f %8.1f%% %9.2f" % (k, calls[k], 1e6 * dur[k] / calls[k], util, ghz))
+        avail = dur[k] * 1024 * 2.4e9
+        util = 100.0 * busy[k] / avail if avail > 0 else 0.0
+        per = dur[k] / calls[k]
+        ghz = "%.2f" % (active[k] / 8.0 / dur[k] / 1e9) if (per >= 3e-4 and active.get(k)) else "-"
+        print("%-64s %6d %10.2f %12.1f%% %16s" % (k, calls[k], 1e6 * per, util, ghz))
 
 
 if __name__ == "__main__":

@@ -367,6 +367,8 @@ class HipLib:
         lib.skr_colsum.restype = _i
         lib.skr_wgrad.argtypes = [_p, _i64, _i64, _p, _i64, _i64, _i64, _i, _i, _i, _i, _p, _p, _p, _p, _p]
         lib.skr_wgrad.restype = _i
+        lib.skr_wgrad2.argtypes = [_p, _i64, _i64, _p, _i64, _i64, _i64, _i, _i, _i, _i, _p, _p, _p, _p, _i, _i, _p]
+        lib.skr_wgrad2.restype = _i
         lib.skr_wgrad_set_variant.argtypes = [_i]
         lib.skr_wgrad_set_variant.restype = _i
         lib.skr_latent_mid.argtypes = [_p, _p, _p, _p, _u32, _i, _f, _p, _p, _p, _p, _p]

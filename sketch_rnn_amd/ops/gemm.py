@@ -229,34 +229,77 @@ def _wgrad_splits(tiles: int, K: int) -> int:
     return pick
 
 
-def _wgrad_hip(a, b, colsum, out=None):
+def _wgrad_hip(a, b, colsum, out=None, acc=False, max_grid=0, cs=None):
     from ..utils import native
     lib = native.require_hip()
     n, K, M = a.shape
     N = b.shape[-1]
     tiles = n * (M // 256) * (N // 256)
-    S = WGRAD_SPLIT.get((M, N, n), _wgrad_splits(tiles, K))
+    # a bounded grid walks the tiles itself: no split-K (the launch is meant
+    # to leave most CUs to the stream it runs beside)
+    S = 1 if max_grid > 0 else WGRAD_SPLIT.get((M, N, n), _wgrad_splits(tiles, K))
     dev = a.device
     out = out.view(n, M, N) if out is not None else torch.empty(n, M, N, device=dev, dtype=torch.float32)
     work = torch.empty(n * S, M, N, device=dev, dtype=torch.float32) if S > 1 else None
-    cs = torch.empty(n, N, device=dev, dtype=torch.float32) if colsum else None
+    if colsum:
+        cs = cs.view(n, N) if cs is not None else torch.empty(n, N, device=dev, dtype=torch.float32)
+    else:
+        cs = None
     csw = torch.empty(n * S, N, device=dev, dtype=torch.float32) if (colsum and S > 1) else None
     ptr = lambda t: t.data_ptr() if t is not None else None
-    rc = lib.lib.skr_wgrad(a.data_ptr(), a.stride(1), a.stride(0) if n > 1 else 0, b.data_ptr(), b.stride(1),
-                           b.stride(0) if n > 1 else 0, K, M, N, n, S, out.data_ptr(), ptr(work), ptr(cs), ptr(csw),
-                           torch.cuda.current_stream().cuda_stream)
+    rc = lib.lib.skr_wgrad2(a.data_ptr(), a.stride(1), a.stride(0) if n > 1 else 0, b.data_ptr(), b.stride(1),
+                            b.stride(0) if n > 1 else 0, K, M, N, n, S, out.data_ptr(), ptr(work), ptr(cs), ptr(csw),
+                            int(acc), int(max_grid), torch.cuda.current_stream().cuda_stream)
     if rc != 0:
         raise RuntimeError("skr_wgrad failed (%d) for [%d, %d]^T [%d, %d] x %d" % (rc, K, M, K, N, n))
     return out, cs
 
 
-def wgrad(a: torch.Tensor, b: torch.Tensor, colsum: bool = False, out: Optional[torch.Tensor] = None):
+class Background:
+    """Kernels issued on a per-device side stream behind everything the
+    current stream has queued so far (an event wait), joined back with
+    :meth:`join`. Inside a graph capture the side stream joins the capture
+    through that wait, so the captured graph holds the side work as a
+    parallel branch. Used for the HyperLSTM weight gradients that run beside
+    the backward scan (ops/hyper.py): callers allocate every tensor the side
+    work writes on the current stream first and join before those tensors
+    (or the inputs the side work reads) are used or freed."""
+
+    _streams = {}
+
+    def __init__(self, device):
+        device = torch.device(device)
+        self.main = torch.cuda.current_stream(device)
+        key = device.index if device.index is not None else torch.cuda.current_device()
+        if key not in Background._streams:
+            Background._streams[key] = torch.cuda.Stream(device)
+        self.side = Background._streams[key]
+        self.pending = False
+
+    def run(self, fn):
+        self.side.wait_stream(self.main)
+        with torch.cuda.stream(self.side):
+            fn()
+        self.pending = True
+
+    def join(self):
+        if self.pending:
+            self.main.wait_stream(self.side)
+            self.pending = False
+
+
+def wgrad(a: torch.Tensor, b: torch.Tensor, colsum: bool = False, out: Optional[torch.Tensor] = None,
+          acc: bool = False, max_grid: int = 0, cs_out: Optional[torch.Tensor] = None):
     """Weight gradient ``a^T @ b`` over a long row dimension (K = T*B rows):
     ``a [K, M], b [K, N] -> [M, N]`` (or batched ``[n, K, *] -> [n, M, N]``),
     fp32 output. ``colsum``: also return the column sums of ``b`` (a bias
     gradient that rides on the same pass over ``b``): ``(out, colsum)``.
     ``out``: a contiguous fp32 destination (e.g. :func:`grad_slot`), used by
-    the hand-written kernel path.
+    the hand-written kernel path. ``acc``: add into ``out`` (and ``cs_out``,
+    the colsum destination) instead of overwriting -- row chunks of one
+    product summed in a fixed order. ``max_grid`` (a multiple of 8): at most
+    that many workgroups, each walking several output tiles (background
+    launches beside the recurrent scan); both need the hand-written kernel.
 
     bf16 operands on the GPU run the hand-written MFMA kernel
     (csrc/wgrad_gemm.hip: 256 x 256 tiles, ds_read_b64_tr_b16 operands,
@@ -271,10 +314,12 @@ def wgrad(a: torch.Tensor, b: torch.Tensor, colsum: bool = False, out: Optional[
     if not batched:
         a, b = a.unsqueeze(0), b.unsqueeze(0)
     if _wgrad_hip_ok(a, b):
-        out, cs = _wgrad_hip(a, b, colsum, out)
+        out, cs = _wgrad_hip(a, b, colsum, out, acc, max_grid, cs_out)
         if not batched:
             out, cs = out[0], (cs[0] if cs is not None else None)
         return (out, cs) if colsum else out
+    if acc or max_grid:
+        raise ValueError("wgrad: acc / max_grid need the hand-written bf16 kernel (shape or dtype not taken)")
     if colsum:   # ones column appended to a: the extra output row is colsum(b)
         ones = torch.ones(a.shape[:-1] + (8,), device=a.device, dtype=a.dtype)
         a = torch.cat([a, ones], -1)

@@ -46,10 +46,28 @@ HYPER_BWD_FUSE = True
 # launches per backward step instead of four. SKR_CHAIN=0 keeps the unchained
 # launches (A/B).
 CHAIN = os.environ.get("SKR_CHAIN", "1") != "0"
+# Debug (tests): NaN-fill the d[h | hh] slabs before every chained launch, so
+# a main-cell row that read them ahead of its producer tiles shows up as NaN.
+CHAIN_POISON = False
 # The main input projection x W_x + z W_z ([T, B, 4H], the largest tensor the
 # forward writes) stored in bf16 on the fused-modulation path; False keeps it
 # fp32 (A/B, scripts/micro/xh_ab.py).
 XH_BF16 = True
+# The three long-K weight gradients of the backward (dW_h, dW_y, dP + its
+# column sums) computed in T-chunks on a side stream WHILE the scan runs: once
+# the scan has finished time steps [t, t + BG_CHUNK), their rows of dR_main /
+# dR_hyp / dvec are final, and a bounded-grid launch (BG_GRID workgroups,
+# csrc/wgrad_gemm.hip max_grid) adds that chunk's product into the gradient
+# (fixed chunk order: deterministic); the last chunk runs at full width beside
+# the post-scan reductions. OFF: measured on MI355X (round 6, same box, A B A B,
+# profiles/r6/bg_wgrad_ab.log) 24.06 / 24.01 ms/step serial against 26.17 /
+# 26.24 (64 workgroups), 28.60 / 28.42 (32) and 37.29 / 37.17 (16). The scan's
+# own kernels slow only 2-5 % beside the side stream, but its 250-step span
+# grows from ~10 to ~14 ms (profiles/r6/bg_wgrad_step_summary.txt): the gaps
+# between its dependent launches widen while a second queue is active.
+BG_WGRAD = False
+BG_GRID = 32
+BG_CHUNK = 50
 # (Round 4 measured the hyper-norm projections unfolded -- vec = bf16(hh W_z)
 # W_a + q forward, dz = dvec W_a^T / dh = dz W_z^T backward -- at 27.8 vs
 # 24.6 ms per training step: W_z re-read from L2 by every workgroup costs more
@@ -447,6 +465,27 @@ class _HyperSeq(torch.autograd.Function):
         chain_m = CHAIN and lp_on and dev.type == "cuda" and T >= 3 and H == 2048 and s.mln_on and \
             s.VEC.dtype == torch.bfloat16 and s.RLP is not None and dHout is not None and S_ay <= 8
         cm = gemm.ChainCounters(dev, "hyp_bwd_m", T - 1) if chain_m else None
+        # weight gradients beside the scan (BG_WGRAD): destinations allocated
+        # here, on the scan's stream; chunks [t, hi) issued as the scan passes t
+        A2 = s.A[:T].reshape(TB, K)
+        HHl = s.A[1:T + 1].reshape(TB, K)[:, H:] if lp_on else s.HH.view(TB, Hh)
+        bg = None
+        if BG_WGRAD and lp_on and dev.type == "cuda" and T >= 2 * BG_CHUNK and gemm._wgrad_hip_ok(A2[:, :H], dRM_lp.view(TB, G)) \
+                and gemm._wgrad_hip_ok(A2, dRY_lp.view(TB, Gh)) and gemm._wgrad_hip_ok(HHl, dVEC.view(TB, 12 * H)):
+            bg = gemm.Background(dev)
+            dW_h = gemm.grad_slot(s.W_h, (H, G))
+            dW_h = dW_h if dW_h is not None else torch.empty(H, G, device=dev, dtype=f32)
+            dW_y = torch.empty(K, Gh, device=dev, dtype=f32)
+            dP1 = torch.empty(Hh, 12 * H, device=dev, dtype=f32)
+            sV = torch.empty(12 * H, device=dev, dtype=f32)
+            bg_hi, bg_first = T, True
+
+            def bg_chunk(lo, hi, first, grid):
+                r0, r1 = lo * B, hi * B
+                gemm.wgrad(A2[r0:r1, :H], dRM_lp.view(TB, G)[r0:r1], out=dW_h, acc=not first, max_grid=grid)
+                gemm.wgrad(A2[r0:r1], dRY_lp.view(TB, Gh)[r0:r1], out=dW_y, acc=not first, max_grid=grid)
+                gemm.wgrad(HHl[r0:r1], dVEC.view(TB, 12 * H)[r0:r1], colsum=True, out=dP1, cs_out=sV,
+                           acc=not first, max_grid=grid)
         for t in range(T - 1, -1, -1):
             clm.set(am, t)
             clh.set(ah, t)
@@ -473,9 +512,14 @@ class _HyperSeq(torch.autograd.Function):
             am.dxp, am.dvec = dXH[t].data_ptr(), dVEC[t].data_ptr()
             ran = False
             if chain_m and t < T - 1:   # dR_hyp W_y^T of step t + 1 -> this main cell, one launch
+                if CHAIN_POISON:
+                    DAY.fill_(float("nan"))
                 ran = gemm.chain_bwd_main([(dRY_lp[t + 1], s.Wyl, DAY, S_ay)], am, cm.at(T - 2 - t)) == 0
                 if not ran:   # shape not taken by the chained row: unchained launches from here on
                     chain_m = False
+                    # launches 0 .. k-1 left counts in their counters (only launch
+                    # n - 1 clears counter 0): reset, so the next sequence starts clean
+                    cm.buf.zero_()
                     gemm.rec_gemm(dRY_lp[t + 1], s.Wyl, DAY, S_ay)
                 else:
                     ROW_STATS["chain"] += 1
@@ -500,6 +544,11 @@ class _HyperSeq(torch.autograd.Function):
                 _cell_bwd(lib, ah, True, 0, st, "hyper_bwd_step")
             if not chain_m or t == 0:   # (chained: runs in the next main-cell launch)
                 gemm.rec_gemm(dRY_lp[t], s.Wyl, DAY, S_ay)
+            if bg is not None and t > 0 and bg_hi - t >= BG_CHUNK:   # rows [t, bg_hi) are final
+                bg.run(lambda lo=t, hi=bg_hi, f=bg_first: bg_chunk(lo, hi, f, BG_GRID))
+                bg_hi, bg_first = t, False
+        if bg is not None:   # the last chunk at full width, beside the reductions below
+            bg.run(lambda: bg_chunk(0, bg_hi, bg_first, 0))
         if not DAY.is_cuda:
             dh0 = DAY[:, :, :H].sum(0) + DAM.sum(0)
             dhh0 = DAY[:, :, H:].sum(0)
@@ -511,16 +560,15 @@ class _HyperSeq(torch.autograd.Function):
             _check(lib.lib.skr_slab_sum2(DAY[0, :, H:].data_ptr(), DAY.shape[0], B * K, K, None, 0, 0, 0, B, Hh,
                                          dhh0.data_ptr(), st), "slab_sum2 dhh0")
         # weight / LayerNorm-parameter gradients: long-K products over the T*B saved rows
-        A2 = s.A[:T].reshape(TB, K)
         # hyper-norm projections, vec_k = (hh @ W_z_k + b_z_k) @ W_a_k: ONE long-K
         # GEMM dP = hh^T @ dvec gives dP_k = hh^T dvec_k, and the same pass over
-        # dvec its column sums; the per-k factors are then tiny batched products
-        dW_h = gemm.wgrad(A2[:, :H], dRM_lp.view(TB, G), out=gemm.grad_slot(s.W_h, (H, G)))
-        dW_y = gemm.wgrad(A2, dRY_lp.view(TB, Gh))
-        # hh_t rows: the bf16 GEMM operand of step t + 1 (no resets on this path,
-        # so it is exactly bf16(HH[t])) -- no conversion pass
-        HHl = s.A[1:T + 1].reshape(TB, K)[:, H:] if lp_on else s.HH.view(TB, Hh)
-        dP1, sV = gemm.wgrad(HHl, dVEC.view(TB, 12 * H), colsum=True)
+        # dvec its column sums; the per-k factors are then tiny batched products.
+        # (hh_t rows, HHl: the bf16 GEMM operand of step t + 1 -- no resets on
+        # this path, so it is exactly bf16(HH[t]) -- no conversion pass)
+        if bg is None:
+            dW_h = gemm.wgrad(A2[:, :H], dRM_lp.view(TB, G), out=gemm.grad_slot(s.W_h, (H, G)))
+            dW_y = gemm.wgrad(A2, dRY_lp.view(TB, Gh))
+            dP1, sV = gemm.wgrad(HHl, dVEC.view(TB, 12 * H), colsum=True)
         # the four LayerNorm gamma / beta reductions in two launches (csrc/reduce.hip)
         lnp = [(DLNY, s.XHAT, G), (DLNCY, s.CHAT, H)] if DLNY is not None else []
         lnp += [(HDLNY, s.HXHAT, Gh), (HDLNCY, s.HCHAT, Hh)]
@@ -531,8 +579,6 @@ class _HyperSeq(torch.autograd.Function):
         else:
             g_ln, g_hln = flat[:4], flat[4:]
         dhW_x = torch.empty_like(s.hW_x)
-        dhW_x[IN:] = dW_y[:H]
-        dhW_h = dW_y[H:]
         dx = dzc = None
         if s.bp:   # input-side gradients from one read of dXH / dR_hyp each
             S_m, P_m = bproj_reduce(s.x, dXH)
@@ -561,6 +607,10 @@ class _HyperSeq(torch.autograd.Function):
                 dx, dzc = dxf[..., :IX], dxf[..., IX:].sum(0)
             else:
                 dx = dxf
+        if bg is not None:   # the side stream's products are complete from here on
+            bg.join()
+        dhW_x[IN:] = dW_y[:H]
+        dhW_h = dW_y[H:]
         dW_z, db_z, dWa, dbias = _hyper_proj_grads(dP1, sV, s, Hh, H, E)
         ctx.s = None
         return (dx, dzc, dh0, dc_rec, dhh0, dhc_rec, None, dW_x, dW_h, dbias, dhW_x, dhW_h,

@@ -93,11 +93,20 @@ def _hyper():
 
 
 @pytest.mark.parametrize("hog", HOGS, ids=[h[0] for h in HOGS])
-@pytest.mark.parametrize("which", ["persist_encoder", "clustered_hyper"])
-def test_handoff_kernels_survive_concurrent_occupancy(which, hog):
+@pytest.mark.parametrize("which", ["persist_encoder", "clustered_hyper", "chain_bwd_main"])
+def test_handoff_kernels_survive_concurrent_occupancy(which, hog, monkeypatch):
+    """``clustered_hyper``: the HyperLSTM with the unchained backward
+    launches; ``chain_bwd_main``: the same run with the chained backward
+    launch on and counted (csrc/chain_step.hip: main-cell rows spin on the
+    arrival counter of producer tiles of their own launch; producers never
+    wait, so a hog can only delay them) -- T - 1 = 11 chained launches per run."""
+    from sketch_rnn_amd.ops import hyper
+    from sketch_rnn_amd.ops.recurrent import ROW_STATS
     ops.set_backend("hip")
     ops.set_compute_dtype("bf16")
+    monkeypatch.setattr(hyper, "CHAIN", which == "chain_bwd_main")
     run = _encoder() if which == "persist_encoder" else _hyper()
+    n_chain = ROW_STATS["chain"]
     run()                                  # lazy setup (weight caches, occupancy queries)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -118,6 +127,8 @@ def test_handoff_kernels_survive_concurrent_occupancy(which, hog):
     recurrent.check_cluster_errors(DEV)    # raises if any in-launch wait timed out
     for a, b in zip(out, ref):
         assert torch.equal(a, b)
+    if which == "chain_bwd_main":   # setup + solo + hog runs, 11 chained launches each
+        assert ROW_STATS["chain"] - n_chain == 3 * 11, ROW_STATS["chain"] - n_chain
     print(json.dumps({"kernels": which, "hog": name, "hog_ms": us / 1e3, "solo_ms": round(solo_ms, 2),
                       "with_hog_ms": round(both_ms, 2)}))
 

@@ -977,7 +977,7 @@ def test_hyper_backward_fused_cell_launch_bitwise(monkeypatch):
     equals the unfused order bit for bit at equal split counts, and stays as
     close to the fp32 oracle as the bf16 tolerance test requires."""
     from sketch_rnn_amd.ops import hyper
-    monkeypatch.setenv("SKR_HYP_SH", "64")
+    monkeypatch.setitem(hyper.SPLITS, "sh", 64)   # dvec P^T at 64 splits in both orders
     p, x, z, st, w = _hyper_setup(4, 6, 100, 5, 16, 2048, 256, 32, jitter=0.02, state=0.1)
     ops.set_compute_dtype("bf16")
     ops.set_backend("hip")
@@ -1033,4 +1033,62 @@ def test_hyper_chained_launches_vs_unchained(B, T, fin_w):
         e_c = (runs["chain"][i].float() - ref).abs().max().item()
         e_p = (runs["plain"][i].float() - ref).abs().max().item()
         assert e_c <= 1.5 * e_p + 1e-3 * scale, (n, e_c, e_p, scale)
+
+
+@pytest.mark.parametrize("B,T", [(100, 7), (192, 4)])
+def test_hyper_chained_rows_never_overtake_the_counter(B, T):
+    """Poison mode (ops.hyper.CHAIN_POISON): the d[h | hh] slabs are NaN-filled
+    before every chained launch, so a main-cell row that read them before its
+    producer tiles had written them would carry NaN into h / c gradients and
+    every weight gradient. Every output and gradient must be finite and equal
+    to the unpoisoned chained run bit for bit."""
+    from sketch_rnn_amd.ops import hyper
+    p, x, z, st, w = _hyper_setup(5, T, B, 5, 16, 2048, 256, 32, jitter=0.02, state=0.1)
+    ops.set_backend("hip")
+    ops.set_compute_dtype("bf16")
+    saved = hyper.CHAIN, hyper.CHAIN_POISON
+    try:
+        hyper.CHAIN = True
+        hyper.CHAIN_POISON = False
+        clean = _hyper_run(p, x, z, st, w, keep=0.9, hkeep=0.9)
+        hyper.CHAIN_POISON = True
+        pois = _hyper_run(p, x, z, st, w, keep=0.9, hkeep=0.9)
+    finally:
+        hyper.CHAIN, hyper.CHAIN_POISON = saved
+    for n, a, b in zip(_names(p), clean, pois):
+        assert torch.isfinite(b).all(), n
+        assert torch.equal(a, b), n
+
+
+def test_hyper_background_weight_grads_vs_serial():
+    """ops.hyper.BG_WGRAD: dW_h, dW_y and dP (+ its column sums) computed in
+    T-chunks on a side stream while the backward scan runs, with bounded
+    grids and in-place accumulation, against the same products after the
+    scan: equal up to fp32 summation order (the chunk partial sums are added
+    in a different association), bit-identical outputs and non-weight
+    gradients, and bit-identical repeats (fixed chunk order)."""
+    from sketch_rnn_amd.ops import hyper
+    T, B = 64, 100
+    p, x, z, st, w = _hyper_setup(9, T, B, 5, 16, 2048, 256, 32, jitter=0.02, state=0.1)
+    ops.set_backend("hip")
+    ops.set_compute_dtype("bf16")
+    saved = hyper.BG_WGRAD, hyper.BG_CHUNK, hyper.BG_GRID
+    try:
+        hyper.BG_CHUNK, hyper.BG_GRID = 20, 16   # chunks [44, 64) [24, 44) [4, 24) on the side stream, [0, 4) last
+        hyper.BG_WGRAD = False
+        ser = _hyper_run(p, x, z, st, w)
+        hyper.BG_WGRAD = True
+        bg1 = _hyper_run(p, x, z, st, w)
+        bg2 = _hyper_run(p, x, z, st, w)
+    finally:
+        hyper.BG_WGRAD, hyper.BG_CHUNK, hyper.BG_GRID = saved
+    names = _names(p)
+    chunked = {"W_h", "hyp_W_h", "hyp_W_x", "W_z", "b_z", "W_a", "bias"}
+    for n, a, b, c in zip(names, ser, bg1, bg2):
+        assert torch.equal(b, c), n
+        if n in chunked:
+            scale = max(a.abs().max().item(), 1e-6)
+            assert (a - b).abs().max().item() <= 1e-5 * scale, (n, (a - b).abs().max().item(), scale)
+        else:
+            assert torch.equal(a, b), n
 
