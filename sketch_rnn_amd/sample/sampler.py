@@ -227,17 +227,30 @@ def mdn_sample_device(zh: torch.Tensor, M_: int, mode: int, temp: float, greedy:
 
 
 class GraphDecoder:
-    """Batched autoregressive decode captured in one HIP graph.
+    """Batched autoregressive decode captured in HIP graphs.
 
     ``model`` is a :class:`~sketch_rnn_amd.models.reference.SketchRNN` (mode
     ``reference``) or :class:`~sketch_rnn_amd.models.vae.SketchVAE` (mode
-    ``vae``). ``run()`` replays the graph and returns ``strokes [B, N, 5]``
-    (offsets in model units; reference mode multiplies by ``data_scale``)
-    plus the per-row number of valid steps.
+    ``vae``). ``run()`` returns ``strokes [B, N, 5]`` (offsets in model
+    units; reference mode multiplies by ``data_scale``) plus the per-row
+    number of valid steps.
+
+    The N steps are captured as consecutive chunks of ``chunk`` steps, one
+    graph each (one memory pool). After each chunk the host reads whether
+    every row has drawn its end-of-sketch pen state; if so the remaining
+    chunks are skipped and their output rows are filled with the padding
+    row the sampler would have emitted (reference: model.py:254-257, the
+    ``stop_if_eoc`` break). The emitted sketches are identical to the
+    full-length decode: finished rows only ever emit padding, and the
+    sampler's noise is keyed by (seed, step, row), not by a running state.
+    ``steps_run`` records how many decode steps the last ``run()`` executed.
     """
 
+    CHUNK = 25               # steps per captured graph (one host read of the all-done flag per chunk)
+
     def __init__(self, model, batch: int, steps: int, temperature: float = 1.0, greedy: bool = False,
-                 fix_pen_temperature: bool = False, use_graph: bool = True):
+                 fix_pen_temperature: bool = False, use_graph: bool = True, chunk: Optional[int] = None,
+                 early_exit: bool = True):
         self.model = model
         self.kind = "vae" if hasattr(model, "encoder") else "reference"
         self.B, self.N = batch, steps
@@ -255,8 +268,13 @@ class GraphDecoder:
             self.x0[:, 2] = 1.0
             self.z = torch.zeros(batch, max(cfg.z_size, 1), device=dev)
             self.labels = torch.zeros(batch, dtype=torch.int64, device=dev)
-        self.graph = None
+        self.graphs = None
         self.use_graph = use_graph and dev.type == "cuda"
+        c = int(chunk or self.CHUNK)
+        self.ranges = [(t, min(t + c, steps)) for t in range(0, steps, c)] if steps > 0 else []
+        self.early_exit = bool(early_exit)
+        self.steps_run = 0
+        self._carry = {}     # tensors handed from one chunk to the next (state, next input, zc)
 
     _MAX_CHUNKS = 8          # concurrent 128-row step decoders (one HIP stream each)
 
@@ -287,48 +305,55 @@ class GraphDecoder:
         return self._stp
 
     @torch.no_grad()
-    def _decode_steppers(self, stp):
+    def _decode_steppers(self, stp, t0, t1):
         import ctypes
         from ..utils import native
         lib = native.require_hip().lib
         model, B, N = self.model, self.B, self.N
         cfg = model.cfg
-        lab = self.labels if cfg.num_classes > 0 else None
-        zc = model.condition(self.z if cfg.conditional else None, lab, B, self.dev)
-        state = model.initial_state(zc, B, self.dev)
-        x0 = self.x0.clone()
         ld_out = self.out.stride(0)
         main = torch.cuda.current_stream(self.dev)
         stp = [(r0, n, st, main if stream is None else stream) for r0, n, st, stream in stp]
-        for _, _, st, _ in stp:                  # weight operands on the parent stream
-            st.prepare()
+        cy = self._carry
+        if t0 == 0:
+            lab = self.labels if cfg.num_classes > 0 else None
+            cy["zc"] = zc = model.condition(self.z if cfg.conditional else None, lab, B, self.dev)
+            cy["state"] = model.initial_state(zc, B, self.dev)
+            cy["x0"] = self.x0.clone()
+            for _, _, st, _ in stp:              # weight operands on the parent stream
+                st.prepare()
+        zc, state, x0 = cy["zc"], cy["state"], cy["x0"]
         for _, _, _, stream in stp:              # fork: inputs above are ready
             if stream != main:
                 stream.wait_stream(main)
-        for r0, n, st, stream in stp:
+        for i, (r0, n, st, stream) in enumerate(stp):
             if st.fused:       # four launches per stroke (hyper_step.py module docstring)
                 with torch.cuda.stream(stream):
-                    st.begin(zc[r0:r0 + n] if zc is not None else None, [s[r0:r0 + n] for s in state],
-                             x0=x0[r0:r0 + n])
+                    if t0 == 0:
+                        st.begin(zc[r0:r0 + n] if zc is not None else None, [s[r0:r0 + n] for s in state],
+                                 x0=x0[r0:r0 + n])
                     done = self.done[r0:r0 + n]
-                    for t in range(N):
+                    for t in range(t0, t1):
                         smp = None if t == 0 else st.sample_args(
                             t - 1, r0, self.out[r0:r0 + n, t - 1], done, self.seed, self.Mx, self.mode, self.temp,
                             self.greedy, self.fix_pen)
                         st.step_fused(t, smp)
-                    st.head()          # the last stroke: head + sampler
-                    rc = lib.skr_mdn_sample_slabs(
-                        st.ZS.data_ptr(), 128, st.S_o, n * 128, st._w["bo"].data_ptr(), n, self.Mx, self.mode,
-                        self.temp, int(self.greedy), int(self.fix_pen), self.seed.data_ptr(), N - 1, r0,
-                        self.out[r0, N - 1].data_ptr(), ld_out, st.X.data_ptr(), 5, done.data_ptr(),
-                        ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
-                    if rc != 0:
-                        raise RuntimeError("skr_mdn_sample_slabs failed (%d)" % rc)
+                    if t1 == N:
+                        st.head()          # the last stroke: head + sampler
+                        rc = lib.skr_mdn_sample_slabs(
+                            st.ZS.data_ptr(), 128, st.S_o, n * 128, st._w["bo"].data_ptr(), n, self.Mx, self.mode,
+                            self.temp, int(self.greedy), int(self.fix_pen), self.seed.data_ptr(), N - 1, r0,
+                            self.out[r0, N - 1].data_ptr(), ld_out, st.X.data_ptr(), 5, done.data_ptr(),
+                            ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
+                        if rc != 0:
+                            raise RuntimeError("skr_mdn_sample_slabs failed (%d)" % rc)
                 continue
             with torch.cuda.stream(stream):
-                st.begin(zc[r0:r0 + n] if zc is not None else None, [s[r0:r0 + n] for s in state])
-                x = x0[r0:r0 + n].contiguous()
-                for t in range(N):
+                if t0 == 0:
+                    st.begin(zc[r0:r0 + n] if zc is not None else None, [s[r0:r0 + n] for s in state])
+                    cy["x%d" % i] = x0[r0:r0 + n].contiguous()
+                x = cy["x%d" % i]
+                for t in range(t0, t1):
                     nx = torch.empty(n, 5, device=self.dev)
 
                     def sample(zs, ldz, nslab, slab, bias, r0=r0, n=n, t=t, nx=nx):
@@ -341,27 +366,38 @@ class GraphDecoder:
                             raise RuntimeError("skr_mdn_sample_slabs failed (%d)" % rc)
                     st.step(x, t, sample)
                     x = nx
+                cy["x%d" % i] = x
         for _, _, _, stream in stp:
             if stream != main:
                 main.wait_stream(stream)          # join
 
     @torch.no_grad()
-    def _decode(self):
+    def _decode(self, t0: int, t1: int):
+        """Decode steps [t0, t1); t0 == 0 starts a sketch (state, done flags)."""
         model, B = self.model, self.B
-        self.done.zero_()
+        if t0 == 0:
+            self.done.zero_()
         stp = self._steppers()
         if stp is not None:
-            return self._decode_steppers(stp)
-        x = self.x0.clone()
-        if self.kind == "vae":
-            cfg = model.cfg
-            lab = self.labels if cfg.num_classes > 0 else None
-            zc = model.condition(self.z if cfg.conditional else None, lab, B, self.dev)
-            state = model.initial_state(zc, B, self.dev)
-        else:
-            zc = None
-            state = model.zero_state(B, self.dev)
-        for t in range(self.N):
+            fused = {st.fused for _, _, st, _ in stp}
+            # fused step decoders draw stroke t inside step t + 1's launch: after
+            # steps [t0, t1) the done flags cover strokes < t1 - 1
+            self._lag = 1 if fused == {True} else (0 if fused == {False} else None)
+            return self._decode_steppers(stp, t0, t1)
+        self._lag = 0
+        cy = self._carry
+        if t0 == 0:
+            cy["x"] = self.x0.clone()
+            if self.kind == "vae":
+                cfg = model.cfg
+                lab = self.labels if cfg.num_classes > 0 else None
+                cy["zc"] = model.condition(self.z if cfg.conditional else None, lab, B, self.dev)
+                cy["state"] = model.initial_state(cy["zc"], B, self.dev)
+            else:
+                cy["zc"] = None
+                cy["state"] = model.zero_state(B, self.dev)
+        x, zc, state = cy["x"], cy["zc"], cy["state"]
+        for t in range(t0, t1):
             if self.kind == "vae":
                 zh, state = model.decode_step(x, zc, state)
             else:
@@ -370,6 +406,16 @@ class GraphDecoder:
             mdn_sample_device(zh.contiguous(), self.Mx, self.mode, self.temp, self.greedy, self.fix_pen, self.seed, t,
                               self.out[:, t], nx, self.done)
             x = nx
+        cy["x"], cy["state"] = x, state
+
+    def _exit_after(self, t1: int) -> bool:
+        return self.early_exit and self._lag is not None and t1 < self.N and bool(self.done.all())
+
+    def _pad_from(self, t: int):
+        """Rows of steps [t, N) as the sampler emits them for finished rows."""
+        if t < self.N:
+            self.out[:, t:].zero_()
+            self.out[:, t:, 4 if self.kind == "vae" else 3] = 1.0
 
     @torch.no_grad()
     def run(self, seed: int = 0, z: Optional[torch.Tensor] = None, labels: Optional[torch.Tensor] = None):
@@ -381,25 +427,42 @@ class GraphDecoder:
         if labels is not None:
             self.labels.copy_(labels)
         self.seed.fill_(int(seed))
+        ran = self.N
         if self.use_graph:
-            # the graph holds inference-cached weight copies (bf16): re-capture after a weight update
+            # the graphs hold inference-cached weight copies (bf16): re-capture after a weight update
             from ..ops import gemm
             sig = (gemm.WEIGHTS_EPOCH[0],) + tuple(p._version for p in self.model.parameters())
-            if self.graph is not None and sig != self._sig:
-                self.graph = None
+            if self.graphs is not None and sig != self._sig:
+                self.graphs = None
             self._sig = sig
-            if self.graph is None:
+            if self.graphs is None:
                 s = torch.cuda.Stream()
                 s.wait_stream(torch.cuda.current_stream())
                 with torch.cuda.stream(s):
-                    self._decode()
+                    for t0, t1 in self.ranges:
+                        self._decode(t0, t1)
                 torch.cuda.current_stream().wait_stream(s)
-                self.graph = torch.cuda.CUDAGraph()
-                with capture(self.graph):
-                    self._decode()
-            self.graph.replay()
+                self.graphs, pool = [], None
+                for t0, t1 in self.ranges:
+                    g = torch.cuda.CUDAGraph()
+                    with capture(g, pool=pool):
+                        self._decode(t0, t1)
+                    pool = g.pool() if pool is None else pool
+                    self.graphs.append(g)
+            for (t0, t1), g in zip(self.ranges, self.graphs):
+                g.replay()
+                ran = t1
+                if self._exit_after(t1):   # one host read per chunk
+                    break
         else:
-            self._decode()
+            for t0, t1 in self.ranges:
+                self._decode(t0, t1)
+                ran = t1
+                if self._exit_after(t1):
+                    break
+        if ran < self.N:
+            self._pad_from(ran - self._lag)   # strokes the skipped launches would have drawn: all padding
+        self.steps_run = ran
         strokes = self.out.clone()
         stop_col = 4 if self.kind == "vae" else 3
         hits = strokes[:, :, stop_col] > 0

@@ -126,3 +126,35 @@ def test_graph_decoder_cpu_reference_and_vae():
     assert s.shape == (3, 12, 5) and torch.all((lens >= 1) & (lens <= 12))
     for b in range(3):
         assert torch.all(s[b, lens[b]:, 4] == 1)
+
+
+def _stop_biased_vae(bias):
+    cfg = VAEConfig(enc_rnn_size=16, dec_rnn_size=32, z_size=8, num_mixture=3, max_seq_len=40, dec_model="hyper",
+                    hyper_num_units=16, hyper_embedding_size=4)
+    vm = SketchVAE(cfg, seed=0).eval()
+    ob = [p for n, p in vm.named_parameters() if n.endswith("output_b")][0]
+    with torch.no_grad():
+        ob[2] += bias            # the end-of-sketch pen logit (stroke-5 p3): sketches end after a few strokes
+    return vm
+
+
+def test_graph_decoder_early_exit_equals_full_decode():
+    """Chunked decode with the all-done exit (reference model.py:254-257,
+    stop_if_eoc): the emitted sketches and lengths are identical to the
+    full-length decode, and the decode stops well before N once every row
+    has drawn its end-of-sketch stroke."""
+    vm = _stop_biased_vae(3.0)
+    full = SM.GraphDecoder(vm, batch=6, steps=40, temperature=0.4, chunk=4, early_exit=False)
+    early = SM.GraphDecoder(vm, batch=6, steps=40, temperature=0.4, chunk=4, early_exit=True)
+    for seed in (1, 2, 3):
+        sf, lf = full.run(seed=seed)
+        early.out.fill_(7.0)     # stale contents from an earlier run must not survive the exit
+        se, le = early.run(seed=seed)
+        assert full.steps_run == 40 and early.steps_run < 40, early.steps_run
+        assert early.steps_run % 4 == 0 and early.steps_run >= int(le.max())
+        assert torch.equal(lf, le) and torch.equal(sf, se), seed
+    # a chunk size that does not divide N
+    odd = SM.GraphDecoder(vm, batch=6, steps=40, temperature=0.4, chunk=7)
+    so, lo = odd.run(seed=2)
+    sf, lf = full.run(seed=2)
+    assert torch.equal(so, sf) and torch.equal(lo, lf)

@@ -296,3 +296,39 @@ def test_graph_decoder_hyper_wide():
     finally:
         ops.set_backend("auto")
         ops.set_compute_dtype("fp32")
+
+
+@pytest.mark.parametrize("B,fused", [(128, True), (128, False), (256, True)])
+def test_graph_decoder_early_exit_hyper_steppers(B, fused):
+    """Chunked HIP-graph decode with the all-done exit on the in-place
+    HyperLSTM step decoders (fused four-launch stroke, whose sampler draws
+    stroke t inside step t + 1's launch, and the seven-launch step): the
+    sketches are identical to the full-length decode of the same graphs, and
+    the decode stops early once every row has ended."""
+    from sketch_rnn_amd.sample import hyper_step
+    native.require_hip()
+    ops.set_backend("hip")
+    ops.set_compute_dtype("bf16")
+    saved = hyper_step.FUSED
+    try:
+        hyper_step.FUSED = fused
+        cfg = VAEConfig(enc_rnn_size=64, dec_rnn_size=512, z_size=32, dec_model="hyper", hyper_num_units=256,
+                        hyper_embedding_size=32, num_classes=0, max_seq_len=60)
+        m = SketchVAE(cfg, seed=5).to(DEV).eval()
+        with torch.no_grad():
+            [p for n, p in m.named_parameters() if n.endswith("output_b")][0][2] += 2.5
+        full = SM.GraphDecoder(m, batch=B, steps=60, temperature=0.5, chunk=5, early_exit=False)
+        early = SM.GraphDecoder(m, batch=B, steps=60, temperature=0.5, chunk=5, early_exit=True)
+        assert early._steppers() is not None
+        for seed in (1, 2):
+            sf, lf = full.run(seed=seed)
+            early.out.fill_(7.0)
+            se, le = early.run(seed=seed)
+            torch.cuda.synchronize()
+            assert early._lag == (1 if fused else 0)
+            assert early.steps_run < 60, early.steps_run
+            assert torch.equal(lf, le) and torch.equal(sf, se), seed
+    finally:
+        hyper_step.FUSED = saved
+        ops.set_backend("auto")
+        ops.set_compute_dtype("fp32")
