@@ -82,6 +82,7 @@ def main():
     import torch
     from sketch_rnn_amd import ops
     from sketch_rnn_amd.config import PRESETS
+    from sketch_rnn_amd.utils.provenance import tree_identity
     from sketch_rnn_amd.data.dataset import StrokeDataset
     from sketch_rnn_amd.data.synthetic import synthetic_corpus
     from sketch_rnn_amd.parallel import dp
@@ -190,6 +191,7 @@ def main():
                 # what "auto" resolved to on this device, and which kernel build ran
                 "backend_resolved": backend_resolved,
                 "hip_lib": hip_lib,
+                "tree": tree_identity(),
                 "hip_graph": bool(trainer.use_graph),
             },
             "positions_per_s": round(positions_per_s, 1),

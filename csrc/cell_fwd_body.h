@@ -269,6 +269,29 @@ __device__ __forceinline__ void cell_fwd_body(const FwdArgs& a, const int c, con
 #pragma unroll
         for (int k = 0; k < UPT; ++k) th[k] = cell_tanh(cn[k]);
     }
+    // ---- MX-fp8 copy of the carried h (FwdArgs::h_q8): 32 consecutive units
+    // are 32 consecutive lanes, so each block's amax is 5 xor shuffles; every
+    // lane takes part (units past H count as 0)
+    if (a.h_q8 != nullptr) {
+#pragma unroll
+        for (int k = 0; k < UPT; ++k) {
+            const int u = base + k * NT + tid;
+            const int64_t ro = (int64_t)b * H + min(u, H - 1);
+            const float hc = !on[k] ? 0.f : (r ? a.init_h[ro] : th[k] * og[k]);
+            float m = fabsf(hc);
+#pragma unroll
+            for (int o = 1; o < 32; o <<= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+            const int X = min(max((int)((__float_as_uint(m) >> 23) & 0xff) - 7, 0), 254);
+            const float q = hc * __uint_as_float((uint32_t)(254 - X) << 23);
+            if (on[k]) {
+                a.h_q8[(int64_t)b * a.ld_q8 + u] = (uint8_t)(__builtin_amdgcn_cvt_pk_fp8_f32(q, 0.f, 0, false) & 0xff);
+                if ((tid & 31) == 0) {
+                    const int blk = u >> 5;
+                    a.h_qs[(int64_t)b * (H / 32) + (blk & 3) * (H / 128) + (blk >> 2)] = (uint8_t)X;
+                }
+            }
+        }
+    }
     // ---- outputs + carry (reference eoc reset)
 #pragma unroll
     for (int k = 0; k < UPT; ++k) {

@@ -47,6 +47,8 @@ __device__ __forceinline__ void producer_tile(const GemmGroup& g, const ChainSyn
 }
 
 // backward, main cell: [producers (dR_hyp W_y^T of step t + 1), 8 waves][main cell rows of step t]
+// POLL: the rows' poll period (s_sleep units), skr_chain_set_poll
+template <int POLL>
 __global__ __launch_bounds__(512) void chain_bwd_main_kernel(const GemmGroup g, const int nprod, const skr::BwdArgs cell,
                                                              const ChainSync cs) {
     extern __shared__ __attribute__((aligned(16))) __hip_bfloat16 smem[];
@@ -55,7 +57,154 @@ __global__ __launch_bounds__(512) void chain_bwd_main_kernel(const GemmGroup g, 
         producer_tile<8>(g, cs, smem);
         return;
     }
-    row_bwd_body<512, 4, true, 1, true>(cell, id - nprod, cs.counters + cs.k, (uint32_t)nprod, cs.err);
+    row_bwd_body<512, 4, true, 1, true, false, POLL>(cell, id - nprod, cs.counters + cs.k, (uint32_t)nprod, cs.err);
+}
+
+static int g_row_poll = 1;
+
+// ---- three-stage launch: + the dvec P^T product of step t ------------------------------
+// [producers: dR_hyp W_y^T of step t + 1] -> [main-cell rows of step t] ->
+// [dvec P^T tiles of step t]. The first nprod2 producer workgroups switch
+// role once their producer tile has arrived: they DMA their whole P^T weight
+// slice (BN x kslice bf16, <= 96 KB) into the LDS the producer ring used --
+// while the rows compute -- then wait on the rows' counter and run the tile
+// from LDS with the A operand (the dvec rows) read through sc1 loads. Same
+// fragments, k order and MFMA as glds_mma: the slabs are bit-identical to the
+// separate launch (skinny_gemm_glds_kernel). Residency: producers never wait
+// before their arrival; rows wait only on producers; tiles wait only on rows,
+// and a row that cannot be placed gets the CU of a row that finished.
+template <int BN, int NW>
+__device__ __forceinline__ void resident_issue(const GemmProblem& p, const TileIdx& t, __hip_bfloat16* smem) {
+    constexpr int B_CH = BN / 8;                    // 1-KiB chunks (8 rows x 64 k) per stage
+    static_assert(B_CH % NW == 0, "resident tile: wave layout");
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int kslice = p.K / p.splits, nst = kslice / skr::BK;
+    const int64_t k0 = (int64_t)t.split * kslice;
+    const int r8 = lane >> 3, slot = lane & 7;
+    const __hip_bfloat16* Bt = (const __hip_bfloat16*)p.Bt;
+    for (int st = 0; st < nst; ++st) {
+#pragma unroll
+        for (int i = 0; i < B_CH / NW; ++i) {
+            const int row = (w + NW * i) * 8 + r8;
+            const int kc = slot ^ ((row >> 1) & 7);
+            __builtin_amdgcn_global_load_lds((const void*)(Bt + (int64_t)(t.nt * BN + row) * p.ldb + k0 + st * skr::BK + kc * 8),
+                                             (__attribute__((address_space(3))) void*)(smem + st * BN * skr::BK + (w + NW * i) * 512),
+                                             16, 0, 0);
+        }
+    }
+}
+
+template <int BN, int NW>
+__device__ __forceinline__ void resident_finish(const GemmProblem& p, const TileIdx& t, const __hip_bfloat16* smem) {
+    constexpr int NJ = skr::glds_nj<BN, NW>();
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int wr = w % 4, wc = w / 4;
+    const int fr = lane & 15, fq = lane >> 4;
+    const int kslice = p.K / p.splits, nk = kslice / 32;
+    const int64_t k0 = (int64_t)t.split * kslice;
+    const int M = t.rows;
+    const __hip_bfloat16* A = (const __hip_bfloat16*)p.A + (int64_t)t.rb * skr::BM * p.lda;
+    const __amdgpu_buffer_rsrc_t ra = rsrc(A, (int64_t)M * p.lda * 2);
+    bool live[2];
+    uint32_t aoff[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const int row = 32 * wr + 16 * i + fr;
+        live[i] = 32 * wr + 16 * i < M;                      // uniform per wave
+        aoff[i] = (uint32_t)(((int64_t)min(row, M - 1) * p.lda + k0 + 8 * fq) * 2);
+    }
+    tile_f32x4 acc[2][NJ];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) acc[i][j] = tile_f32x4{0.f, 0.f, 0.f, 0.f};
+    constexpr int G = 4;                                     // k32 steps of A in flight per batch
+    // two register sets with compile-time indices only (a runtime-indexed
+    // double buffer is placed in scratch memory)
+    skr::bf16x8 cur[G][2], nxt[G][2];
+    auto load = [&](skr::bf16x8 (&dst)[G][2], int kk0) {
+#pragma unroll
+        for (int g = 0; g < G; ++g)
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+                if (live[i] && kk0 + g < nk) dst[g][i] = ld_sc1(ra, aoff[i] + (uint32_t)(kk0 + g) * 64);
+    };
+    load(cur, 0);
+    for (int kb = 0; kb < nk; kb += G) {
+        if (kb + G < nk) load(nxt, kb + G);
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            const int kk = kb + g;
+            if (kk >= nk) break;
+            const __hip_bfloat16* Bs = smem + (kk >> 1) * BN * skr::BK;
+            const int kc = (kk & 1) * 4 + fq;
+            skr::bf16x8_t bfr[NJ];
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) {
+                const int row = 16 * (wc * NJ + j) + fr;
+                bfr[j] = *(const skr::bf16x8_t*)(&Bs[row * skr::BK + ((kc ^ ((row >> 1) & 7)) * 8)]);
+            }
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                if (!live[i]) continue;
+                const skr::bf16x8_t a = __builtin_bit_cast(skr::bf16x8_t, cur[g][i]);
+#pragma unroll
+                for (int j = 0; j < NJ; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bfr[j], acc[i][j], 0, 0, 0);
+            }
+        }
+#pragma unroll
+        for (int g = 0; g < G; ++g)
+#pragma unroll
+            for (int i = 0; i < 2; ++i) cur[g][i] = nxt[g][i];
+    }
+    float* C = p.C + split_off(p, t);
+    const int c0 = t.nt * BN + wc * NJ * 16;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int row = 32 * wr + 16 * i + fq * 4 + e;
+                if (row < M) C[row * p.ldc + c0 + 16 * j + fr] = acc[i][j][e];
+            }
+}
+
+struct Chain3 {
+    GemmProblem tail;      // dvec P^T: A = dvec rows (written by this launch's rows), Bt = P^T weights
+    int ntail;             // its tile count (<= producer count)
+    ChainSync rows;        // the rows' arrival counters
+    int probe;             // timing probes (skr_chain3_set_probe; results invalid)
+};
+
+static int g_chain3_probe = 0;
+
+__global__ __launch_bounds__(512) void chain_bwd_main3_kernel(const GemmGroup g, const int nprod, const skr::BwdArgs cell,
+                                                              const ChainSync cs, const Chain3 c3) {
+    extern __shared__ __attribute__((aligned(16))) __hip_bfloat16 smem[];
+    const int id = blockIdx.x;
+    if (id < nprod) {
+        if (id == 0) chain_rotate(c3.rows.counters, c3.rows.n, c3.rows.k);
+        producer_tile<8>(g, cs, smem);      // ends with the arrival (vmcnt(0) + barrier): the ring is free
+        if (id >= c3.ntail || c3.probe == 1) return;
+        // tiles of one split (the same dvec K slice, read with sc1 loads) on one
+        // XCD: workgroup id -> (xcd = id % 8, j = id / 8), N tile j % NTL, split
+        // (j / NTL) * 8 + xcd -- the later readers of a slice hit that XCD's L2
+        const int ntl = c3.tail.N / kBn, x = id & 7, j = id >> 3;
+        const int local = (((j / ntl) * 8 + x) * ntl) + j % ntl;
+        if (local >= c3.ntail) return;
+        const TileIdx t = tile_idx(local, c3.tail.M, c3.tail.N, c3.tail.splits, kBn);
+        if (c3.probe != 3) resident_issue<kBn, 8>(c3.tail, t, smem);
+        chain_wait<16>(c3.rows.counters + c3.rows.k, (uint32_t)cell.B, cs.err);   // (a ~10 us wait: poll sparsely)
+        if (c3.probe == 3) return;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's weight DMAs landed ...
+        __syncthreads();                                   // ... and every other wave's
+        if (c3.probe == 2) return;
+        resident_finish<kBn, 8>(c3.tail, t, smem);
+        return;
+    }
+    row_bwd_body<512, 4, true, 1, true, true>(cell, id - nprod, cs.counters + cs.k, (uint32_t)nprod, cs.err);
+    chain_arrive(c3.rows.counters + c3.rows.k);
 }
 
 template <typename K>
@@ -108,9 +257,70 @@ SKR_API int skr_chain_bwd_main(const GemmProblem* probs, int n, const skr::BwdAr
     GemmGroup g;
     const int np = build_group(probs, n, n, g);
     if (np < 0) return np;
-    lds_attr(chain_bwd_main_kernel, kLds);
-    hipLaunchKernelGGL(chain_bwd_main_kernel, dim3(np + a.B), dim3(512), kLds, s, g, np, a, *cs);
+    if (g_row_poll >= 16) {
+        lds_attr(chain_bwd_main_kernel<16>, kLds);
+        hipLaunchKernelGGL(chain_bwd_main_kernel<16>, dim3(np + a.B), dim3(512), kLds, s, g, np, a, *cs);
+    } else if (g_row_poll >= 4) {
+        lds_attr(chain_bwd_main_kernel<4>, kLds);
+        hipLaunchKernelGGL(chain_bwd_main_kernel<4>, dim3(np + a.B), dim3(512), kLds, s, g, np, a, *cs);
+    } else {
+        lds_attr(chain_bwd_main_kernel<1>, kLds);
+        hipLaunchKernelGGL(chain_bwd_main_kernel<1>, dim3(np + a.B), dim3(512), kLds, s, g, np, a, *cs);
+    }
     return SKR_CHECK_LAUNCH();
+}
+
+// Three-stage backward launch: as skr_chain_bwd_main, plus the dvec P^T
+// product `tail` (A = cell.dvec rows, M = cell.B; Bt = P^T) run by the first
+// tail-tile-count producer workgroups after their producer tile, on the rows'
+// counters `rows`. Returns -2 (shape not taken: callers keep the separate
+// launch) when the tail has more tiles than there are producers, a K slice
+// that is not a whole number of 64-wide steps, or a weight slice over 96 KB.
+SKR_API int skr_chain_bwd_main3(const GemmProblem* probs, int n, const GemmProblem* tail, const skr::BwdArgs* cell,
+                                const ChainSync* cs, const ChainSync* rows, hipStream_t s) {
+    if (cell == nullptr || tail == nullptr || check_sync(cs) || check_sync(rows)) return -6;
+    const skr::BwdArgs& a = *cell;
+    if (a.H != 2048 || a.dh_rec == nullptr || a.dhr_nslab < 1 || a.dhr_nslab > 8) return -2;
+    if (a.dh_out && a.dho_nslab != 1) return -2;
+    int rc = row_bwd_check(a, 2);
+    if (rc) return rc;
+    rc = check_problem64(*tail);
+    if (rc) return rc;
+    if (tail->M != a.B || tail->M > skr::BM || tail->A != a.dvec) return -2;
+    const int kslice = tail->K / tail->splits;
+    const size_t slice_lds = (size_t)kBn * kslice * 2;
+    if (slice_lds > 96 * 1024) return -2;
+    GemmGroup g;
+    const int np = build_group(probs, n, n, g);
+    if (np < 0) return np;
+    Chain3 c3;
+    c3.tail = *tail;
+    c3.ntail = (tail->N / kBn) * tail->splits;
+    c3.rows = *rows;
+    c3.probe = g_chain3_probe;
+    if (c3.ntail > np || c3.ntail % (8 * (tail->N / kBn))) return -2;   // (the XCD-grouped tile map is a bijection)
+    const size_t lds = slice_lds > kLds ? slice_lds : kLds;
+    lds_attr(chain_bwd_main3_kernel, 96 * 1024);
+    hipLaunchKernelGGL(chain_bwd_main3_kernel, dim3(np + a.B), dim3(512), lds, s, g, np, a, *cs, c3);
+    return SKR_CHECK_LAUNCH();
+}
+
+// Timing probes of the three-stage launch (scripts/micro/chain3_probe.py; the
+// gradients are WRONG while a probe is set): 0 off, 1 producers exit after
+// their tile (no dvec P^T), 2 the tail stages its weights and waits on the
+// rows but computes nothing, 3 the tail only waits (no weight staging).
+SKR_API int skr_chain3_set_probe(int p) {
+    const int prev = g_chain3_probe;
+    g_chain3_probe = p;
+    return prev;
+}
+
+// A/B hook: poll period of the chained main-cell rows (1, 4 or 16 s_sleep
+// units); returns the previous one.
+SKR_API int skr_chain_set_poll(int p) {
+    const int prev = g_row_poll;
+    if (p > 0) g_row_poll = p;
+    return prev;
 }
 
 SKR_API int skr_chain_sync_size() { return (int)sizeof(ChainSync); }

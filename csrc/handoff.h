@@ -100,9 +100,14 @@ __device__ __forceinline__ void chain_arrive(uint32_t* counter) {
     if (threadIdx.x == 0) __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// SLEEP: s_sleep units (64 clocks each) between polls -- a longer period
+// puts fewer poll requests beside the streams of the workgroups that are
+// still producing (128 tiles polling one word every 64 clocks measurably
+// slowed a chained launch's rows: scripts/micro/chain3_probe.py).
+template <int SLEEP = 1>
 __device__ inline void chain_wait(const uint32_t* counter, uint32_t target, int* err) {
     if (threadIdx.x == 0) {
-        for (unsigned spins = 0;; ++spins) {
+        for (unsigned spins = 0;; spins += SLEEP) {
             if (__hip_atomic_load(counter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target) break;
             if ((spins & 255) == 255) {
                 if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) break;
@@ -111,7 +116,7 @@ __device__ inline void chain_wait(const uint32_t* counter, uint32_t target, int*
                     break;
                 }
             }
-            __builtin_amdgcn_s_sleep(1);
+            __builtin_amdgcn_s_sleep(SLEEP);
         }
     }
     // compiler barrier + workgroup barrier: no wave's slab loads move above the poll

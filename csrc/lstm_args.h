@@ -45,6 +45,10 @@ struct FwdArgs {
     // LN saves in bf16 (xhat / chat buffers hold __hip_bfloat16; the forward
     // itself runs on the fp32 values, like a bf16 activation save)
     int save_lp;
+    // MX-fp8 copy of the carried h (csrc/mx8_gemm.hip operand; null: none):
+    // e4m3 bytes [B, ld_q8] and one E8M0 scale per 32 units in the
+    // [B][4][H/128] layout (H % 128 == 0)
+    uint8_t* h_q8; int64_t ld_q8; uint8_t* h_qs;
 };
 
 struct BwdArgs {

@@ -163,6 +163,9 @@ int launch(const A& a, bool ln, int mod, hipStream_t s) {
     if constexpr (std::is_same<A, BwdArgs>::value) {
         if (mod == 3) return -3;
     }
+    if constexpr (std::is_same<A, FwdArgs>::value) {
+        if (a.h_q8 != nullptr && (a.H % 128 != 0 || a.h_qs == nullptr)) return -3;
+    }
     if (a.B <= 0) return 0;
     const int H = a.H;
     const int C = a.cluster > 1 ? a.cluster : 1;

@@ -116,7 +116,17 @@ __device__ __forceinline__ float pick(const float (&v)[N], int i) {
 // the SAME launch -- every other load is issued first, then the row waits on
 // the launch's arrival counter and reads them with sc1 loads (16-byte
 // buffer loads); the arithmetic is unchanged.
-template <int NT, int V, bool MOD, int DO, bool CHAIN = false>
+// DVSC1 (csrc/chain_step.hip, three-stage launch): dvec is read by GEMM tiles
+// of the SAME launch after the rows' arrival counter, so its stores are
+// write-through (sc1, 8-byte relaxed agent-scope atomic stores).
+template <int V>
+__device__ __forceinline__ void stb_sc1(void* p, const float (&v)[V]) {
+    static_assert(V == 4, "8-byte sc1 stores");
+    const uint64_t w = (uint64_t)pack2(v[0], v[1]) | ((uint64_t)pack2(v[2], v[3]) << 32);
+    __hip_atomic_store((uint64_t*)p, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+template <int NT, int V, bool MOD, int DO, bool CHAIN = false, bool DVSC1 = false, int POLL = 1>
 __device__ __forceinline__ void row_bwd_body(const BwdArgs& a, const int b, const uint32_t* chain_cnt = nullptr,
                                              uint32_t chain_target = 0, int* chain_err = nullptr) {
     static_assert(!CHAIN || V == 4, "chained row: 16-byte slab loads");
@@ -161,7 +171,7 @@ __device__ __forceinline__ void row_bwd_body(const BwdArgs& a, const int b, cons
         }
     }
     if constexpr (CHAIN) {
-        chain_wait(chain_cnt, chain_target, chain_err);
+        chain_wait<POLL>(chain_cnt, chain_target, chain_err);
         if (n1) {
             const __amdgpu_buffer_rsrc_t r = rsrc(a.dh_rec, 0x7fffffff);
             const int64_t base = (int64_t)b * a.ld_dh_rec + u0;
@@ -270,11 +280,17 @@ __device__ __forceinline__ void row_bwd_body(const BwdArgs& a, const int b, cons
             stb<V>((__hip_bfloat16*)a.dxp + b * a.ld_dxp + q * H + u0, t);
 #pragma unroll
             for (int j = 0; j < V; ++j) t[j] = dg[q][j] * xv[q][j];
-            stb<V>((__hip_bfloat16*)a.dvec + q * a.vec_gs + o0, t);
+            if constexpr (DVSC1) stb_sc1<V>((__hip_bfloat16*)a.dvec + q * a.vec_gs + o0, t);
+            else stb<V>((__hip_bfloat16*)a.dvec + q * a.vec_gs + o0, t);
 #pragma unroll
             for (int j = 0; j < V; ++j) t[j] = dg[q][j] * rv[q][j];
-            stb<V>((__hip_bfloat16*)a.dvec + (4 + q) * a.vec_gs + o0, t);
-            stb<V>((__hip_bfloat16*)a.dvec + (8 + q) * a.vec_gs + o0, dg[q]);
+            if constexpr (DVSC1) {
+                stb_sc1<V>((__hip_bfloat16*)a.dvec + (4 + q) * a.vec_gs + o0, t);
+                stb_sc1<V>((__hip_bfloat16*)a.dvec + (8 + q) * a.vec_gs + o0, dg[q]);
+            } else {
+                stb<V>((__hip_bfloat16*)a.dvec + (4 + q) * a.vec_gs + o0, t);
+                stb<V>((__hip_bfloat16*)a.dvec + (8 + q) * a.vec_gs + o0, dg[q]);
+            }
 #pragma unroll
             for (int j = 0; j < V; ++j) dr[j] = dg[q][j] * ah[q][j];
         } else {

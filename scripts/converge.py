@@ -85,9 +85,11 @@ def main():
     ap.add_argument("--arms", default="hip-bf16,hip-fp32")
     ap.add_argument("--seeds", default="0", help="comma list: init, data-order and noise seed of each run")
     ap.add_argument("--out", default=None)
-    ap.add_argument("--commit", default=os.environ.get("SKR_COMMIT", "unknown"),
-                    help="git commit of the tree under test (the GPU box has no .git): stored in every record")
     args = ap.parse_args()
+    # the tree's identity, taken by the run itself: git HEAD + dirty flag (or
+    # TREE_COMMIT on a box without .git) and a recomputable source hash
+    from sketch_rnn_amd.utils.provenance import tree_identity
+    args.commit = tree_identity()
     import numpy as np
     seeds = [int(x) for x in args.seeds.split(",")]
     arms = args.arms.split(",")

@@ -39,6 +39,7 @@ class LstmFwdArgs(C.Structure):
         ("r_lp", _p),
         ("gpre", _p), ("gstats", _p), ("gstat_tiles", _i),
         ("save_lp", _i),
+        ("h_q8", _p), ("ld_q8", _i64), ("h_qs", _p),
     ]
 
 
@@ -402,6 +403,21 @@ class HipLib:
         lib.skr_skinny_gemm_group_cellbwd.restype = _i
         lib.skr_chain_bwd_main.argtypes = [C.POINTER(GemmProblem), _i, C.POINTER(LstmBwdArgs), C.POINTER(ChainSync), _p]
         lib.skr_chain_bwd_main.restype = _i
+        lib.skr_chain_bwd_main3.argtypes = [C.POINTER(GemmProblem), _i, C.POINTER(GemmProblem), C.POINTER(LstmBwdArgs),
+                                            C.POINTER(ChainSync), C.POINTER(ChainSync), _p]
+        lib.skr_chain_bwd_main3.restype = _i
+        lib.skr_mx8_quant_t.argtypes = [_p, _i64, _i, _i, _p, _p, _p]
+        lib.skr_mx8_quant_t.restype = _i
+        lib.skr_mx8_quant_rows.argtypes = [_p, _i64, _i, _i, _i, _p, _i64, _p, _p]
+        lib.skr_mx8_quant_rows.restype = _i
+        lib.skr_mx8_gemm.argtypes = [_p, _i64, _p, _p, _i64, _p, _p, _i64, _i, _i, _i, _p]
+        lib.skr_mx8_gemm.restype = _i
+        lib.skr_mx8_set_layout.argtypes = [_i]
+        lib.skr_mx8_set_layout.restype = _i
+        lib.skr_chain_set_poll.argtypes = [_i]
+        lib.skr_chain_set_poll.restype = _i
+        lib.skr_chain3_set_probe.argtypes = [_i]
+        lib.skr_chain3_set_probe.restype = _i
         lib.skr_lstm_fused_fwd.argtypes = [C.POINTER(FusedFwdArgs), _p]
         lib.skr_lstm_fused_fwd.restype = _i
         lib.skr_lstm_fused_bwd.argtypes = [C.POINTER(FusedBwdArgs), _p]

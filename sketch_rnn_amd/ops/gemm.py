@@ -548,6 +548,23 @@ def chain_bwd_main(producers, cell_args, sync) -> int:
     return rc
 
 
+def chain_bwd_main3(producers, tail, cell_args, sync, rows_sync) -> int:
+    """:func:`chain_bwd_main` plus the ``tail`` product ``(dvec, P^T, out,
+    splits)`` in the SAME launch (``skr_chain_bwd_main3``): the first producer
+    workgroups, once their producer tile is done, stage their P^T weight slice
+    in LDS while the main-cell rows compute, then run the dvec P^T tile on the
+    rows' arrival counters ``rows_sync``. Returns the library code (-2 / -3 /
+    -4: not taken, the caller keeps the separate launches)."""
+    import ctypes
+    from ..utils import native
+    lib = native.require_hip()
+    rc = lib.lib.skr_chain_bwd_main3(_problems(producers), len(producers), _problems([tail]), ctypes.byref(cell_args),
+                                     ctypes.byref(sync), ctypes.byref(rows_sync), torch.cuda.current_stream().cuda_stream)
+    if rc not in (0, -2, -3, -4):
+        raise RuntimeError("skr_chain_bwd_main3 failed (%d)" % rc)
+    return rc
+
+
 # ---- inference-time helpers ------------------------------------------------------------
 _WCACHE = {}
 WEIGHTS_EPOCH = [0]

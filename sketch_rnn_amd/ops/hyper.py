@@ -33,7 +33,7 @@ from .reduce import colsum_many
 # not take) keeps the plain bf16-output GEMM + the main cell's in-launch
 # statistics exchange.
 HYPER_MOD = True
-HYPER_MAIN_C = 0   # workgroups per row of the MOD-3 main cell (0: policy)
+HYPER_MAIN_C = 4   # workgroups per row of the MOD-3 main cell (0: policy; 4 measured 0.1 ms/step faster than the policy's 8, profiles/r6/main_cell_c_ab.log)
 # Backward step as [main cell] -> [dvec P^T] -> [hyper cell + dR_main W_h^T in
 # one launch, csrc/skinny_gemm.hip skr_skinny_gemm_group_cellbwd] -> [dR_hyp
 # W_y^T]: the hyper cell (one workgroup per row) runs beside the tiles of the
@@ -46,6 +46,18 @@ HYPER_BWD_FUSE = True
 # launches per backward step instead of four. SKR_CHAIN=0 keeps the unchained
 # launches (A/B).
 CHAIN = os.environ.get("SKR_CHAIN", "1") != "0"
+# Three-stage chained launch (csrc/chain_step.hip skr_chain_bwd_main3): the
+# dvec P^T product of step t joins the chained launch too -- producer
+# workgroups that finished their dR_hyp W_y^T tile stage their P^T slice in
+# LDS while the main-cell rows compute, then run the tile on the rows' arrival
+# counter: two launches per backward step instead of three. Bit-identical to
+# the separate launch, but OFF: measured (profiles/r6/chain3_probe.jsonl, B =
+# 100) 60.8 us per backward step against 50.9 for two-stage chain + separate
+# launch. Producers that stay resident waiting on the rows cost 7.4 us by
+# themselves (probe 3: no staging, no tile), and the tile tail -- 154 KB of
+# dvec per workgroup through sc1 loads from the fabric -- another ~10 us,
+# more than the 8 us launch it replaces.
+CHAIN3 = False
 # Debug (tests): NaN-fill the d[h | hh] slabs before every chained launch, so
 # a main-cell row that read them ahead of its producer tiles shows up as NaN.
 CHAIN_POISON = False
@@ -465,6 +477,10 @@ class _HyperSeq(torch.autograd.Function):
         chain_m = CHAIN and lp_on and dev.type == "cuda" and T >= 3 and H == 2048 and s.mln_on and \
             s.VEC.dtype == torch.bfloat16 and s.RLP is not None and dHout is not None and S_ay <= 8
         cm = gemm.ChainCounters(dev, "hyp_bwd_m", T - 1) if chain_m else None
+        # three-stage launches (CHAIN3): dvec P^T inside the chained launch, on
+        # the rows' own rotating counters; the bf16 fused-order backward only
+        chain3 = chain_m and CHAIN3 and bfuse
+        cm3 = gemm.ChainCounters(dev, "hyp_bwd_m3", T - 1) if chain3 else None
         # weight gradients beside the scan (BG_WGRAD): destinations allocated
         # here, on the scan's stream; chunks [t, hi) issued as the scan passes t
         A2 = s.A[:T].reshape(TB, K)
@@ -510,11 +526,21 @@ class _HyperSeq(torch.autograd.Function):
             am.dG = None if lp_on else dRM[t].data_ptr()
             am.dG_lp = dRM_lp[t].data_ptr() if lp_on else None
             am.dxp, am.dvec = dXH[t].data_ptr(), dVEC[t].data_ptr()
-            ran = False
+            ran = ran3 = False
             if chain_m and t < T - 1:   # dR_hyp W_y^T of step t + 1 -> this main cell, one launch
                 if CHAIN_POISON:
                     DAY.fill_(float("nan"))
-                ran = gemm.chain_bwd_main([(dRY_lp[t + 1], s.Wyl, DAY, S_ay)], am, cm.at(T - 2 - t)) == 0
+                    if chain3:
+                        dVEC[t].fill_(float("nan"))
+                if chain3:   # ... -> dvec P^T of this step, the same launch
+                    ran3 = gemm.chain_bwd_main3([(dRY_lp[t + 1], s.Wyl, DAY, S_ay)], (dVEC[t], s.Pl, DHZ, S_h), am,
+                                                cm.at(T - 2 - t), cm3.at(T - 2 - t)) == 0
+                    if not ran3:
+                        chain3 = False
+                        cm3.buf.zero_()
+                    ran = ran3
+                if not ran:
+                    ran = gemm.chain_bwd_main([(dRY_lp[t + 1], s.Wyl, DAY, S_ay)], am, cm.at(T - 2 - t)) == 0
                 if not ran:   # shape not taken by the chained row: unchained launches from here on
                     chain_m = False
                     # launches 0 .. k-1 left counts in their counters (only launch
@@ -523,6 +549,7 @@ class _HyperSeq(torch.autograd.Function):
                     gemm.rec_gemm(dRY_lp[t + 1], s.Wyl, DAY, S_ay)
                 else:
                     ROW_STATS["chain"] += 1
+                    ROW_STATS["chain3"] += int(ran3)
             if not ran:
                 _cell_bwd(lib, am, s.mln_on, 2 if s.VEC.dtype == torch.bfloat16 else 1, st, "hyper_main_bwd_step")
             ah.c_prev = (s.hc0 if t == 0 else s.HCC[t]).data_ptr()
@@ -532,7 +559,8 @@ class _HyperSeq(torch.autograd.Function):
             ah.dG_lp = dRY_lp[t].data_ptr() if lp_on else None
             ah.dlny, ah.dlncy = HDLNY[t].data_ptr(), HDLNCY[t].data_ptr()
             if bfuse:   # dvec P^T, then the hyper cell beside dR_main W_h^T (one launch)
-                gemm.rec_gemm(dVEC[t], s.Pl, DHZ, S_h)
+                if not ran3:   # (chained: ran in the launch above)
+                    gemm.rec_gemm(dVEC[t], s.Pl, DHZ, S_h)
                 gemm.rec_gemm_group_cellbwd([(dRM_lp[t], s.Whl, DAM, S_am)], ah)
                 ROW_STATS["cluster"] += 1   # (the clustered cell body, C = 1)
             else:

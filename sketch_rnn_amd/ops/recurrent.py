@@ -168,7 +168,7 @@ class _ClusterSync:
 # (default: the main-cell backward only), "all" (every eligible LayerNorm
 # cell), "0" (none).
 ROW_CELLS = os.environ.get("SKR_ROW_CELLS", "main")
-ROW_STATS = {"row": 0, "cluster": 0, "chain": 0}   # launches by kind (tests check which kernels the hot path takes)
+ROW_STATS = {"row": 0, "cluster": 0, "chain": 0, "chain3": 0}   # launches by kind (tests check which kernels the hot path takes)
 
 
 def _row_on(mod: int, fwd: bool) -> bool:

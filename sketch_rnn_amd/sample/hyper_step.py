@@ -31,9 +31,14 @@ Other hyper widths take :meth:`HyperStepDecoder.step` (seven launches:
 stroke projection, grouped GEMM, hyper cell, ``hh P`` GEMM, main cell, head
 GEMM, sampler) on chunks of at most 128 rows.
 
-All GEMMs take bf16 operands with fp32 accumulation. (e4m3 operands on
-gfx950's block-scaled MFMA were built and measured at 1.00-1.01x of bf16 on
-this latency-bound step at B = 128 .. 1024, then removed: README "fp8".)
+GEMMs take bf16 operands with fp32 accumulation, except with ``fp8=True``
+(BASELINE config 5, the fused stroke only): ``h W_h`` -- 80 % of the
+stroke's GEMM FLOPs -- runs as an MX-fp8 GEMM (``ops/mx8.py``,
+``csrc/mx8_gemm.hip``: e4m3 with one E8M0 scale per 32 k, twice the bf16
+MFMA rate, half the weight bytes). ``W_h`` is quantized once per weight
+version; the main cell writes the fp8 copy of ``h`` beside its bf16 copy
+(``FwdArgs::h_q8``), so the stroke gains no conversion launch -- one launch
+more than the bf16 stroke (the fp8 product leaves the grouped bf16 launch).
 """
 from __future__ import annotations
 
@@ -41,7 +46,7 @@ import ctypes
 
 import torch
 
-from ..ops import gemm
+from ..ops import gemm, mx8
 from ..ops._hipapi import DecodeSample, LstmFwdArgs, ModDecode
 from ..ops.hyper import _fold_ok
 from ..ops.recurrent import _ClusterSync, _seed_tensor
@@ -80,11 +85,12 @@ FUSED = True   # four-launch stroke where its shape limits allow (False: tests o
 class HyperStepDecoder:
     """In-place decoder state of B <= 128 rows + the per-step launch sequence."""
 
-    def __init__(self, model, B: int, device, cluster: bool = True):
+    def __init__(self, model, B: int, device, cluster: bool = True, fp8: bool = False):
         """``cluster=False``: the main cell keeps each row in ONE workgroup (no
         in-launch LayerNorm exchange), so this decoder can run on a stream
         concurrent with another one's clustered cells without any
-        co-residency requirement."""
+        co-residency requirement. ``fp8``: ``h W_h`` as an MX-fp8 GEMM (fused
+        stroke, ``dec_rnn_size % 512 == 0`` and ``<= 2048``; else bf16)."""
         self.lib = native.require_hip().lib
         cfg, p = model.cfg, model.dec
         self.model, self.B, self.dev = model, B, device
@@ -102,7 +108,12 @@ class HyperStepDecoder:
         # four-launch stroke (step_fused): hyper_mod's shape limits (Hh == 256,
         # E <= 32, 32-unit tiles, <= 4 main-GEMM slabs)
         self.fused = FUSED and Hh == 256 and self.E <= 32 and H % 32 == 0
-        if self.fused:
+        self.fp8 = bool(fp8) and self.fused and H % 512 == 0 and H <= 2048 and G % 128 == 0
+        if self.fp8:   # MX-fp8 h W_h: one fp32 output (no split-K), h's fp8 copy from the main cell
+            self.S_m = 1
+            self.A8 = torch.zeros(B, H, dtype=torch.uint8, device=device)
+            self.SA = torch.zeros(B, H // 32, dtype=torch.uint8, device=device)
+        elif self.fused:
             self.S_m = 4 if self.S_m >= 4 else 2 if self.S_m >= 2 else 1
             self.X = torch.zeros(B, 5, dtype=f32, device=device)
             self.GP = torch.empty(B, G, dtype=f32, device=device)
@@ -165,6 +176,8 @@ class HyperStepDecoder:
             WoT=gemm.derived(m.output_w, "stepWoT", wout),
             bo=m.output_b.detach().float().contiguous(),
         )
+        if self.fp8:     # W_h [H, 4H] -> e4m3 [4H, H] + E8M0 block scales, once per weight version
+            w["Wh8"] = gemm.derived(p.W_h, "hypWh8", lambda W: mx8.quant_t(W.detach().float().contiguous()))
         if self.fused:   # bf16 folded P^T for csrc/hyper_mod.hip, q + the main bias on the shift block
             P, q = self._fold()
 
@@ -222,6 +235,8 @@ class HyperStepDecoder:
                 cl.part.zero_()
         if x0 is not None and self.fused:
             self.X.copy_(x0)
+        if self.fp8:   # the initial h's fp8 copy (later ones come from the main cell)
+            mx8.quant_rows(self.A[:, :H], self.A8, self.SA)
 
     def _cell_args(self, t: int):
         p, w = self.model.dec, self._w
@@ -251,6 +266,8 @@ class HyperStepDecoder:
         am.seed, am.stream, am.step = self.sd.data_ptr(), 0, t
         am.c_prev, am.c_carry, am.h_out = self.CC.data_ptr(), self.CC.data_ptr(), self.Hout.data_ptr()
         am.h_lp, am.ld_lp, am.lp_kind = self.A.data_ptr(), K, 1
+        if self.fp8:
+            am.h_q8, am.ld_q8, am.h_qs = self.A8.data_ptr(), H, self.SA.data_ptr()
         self.clm.set(am, t)
         return ah, am
 
@@ -301,7 +318,11 @@ class HyperStepDecoder:
         w, lib = self._w, self.lib
         B, H, Hh, G, Gh, K = self.B, self.H, self.Hh, self.G, self.Gh, self.K
         st = torch.cuda.current_stream().cuda_stream
-        jobs = [(self.A[:, :H], w["WhT"], self.RM, self.S_m), (self.A, w["WyT"], self.RY, self.S_y)]
+        jobs = [(self.A, w["WyT"], self.RY, self.S_y)]
+        if self.fp8:   # h W_h on the MX-fp8 GEMM, the rest grouped in bf16
+            mx8.gemm(self.A8, self.SA, w["Wh8"][0], w["Wh8"][1], out=self.RM[0])
+        else:
+            jobs.insert(0, (self.A[:, :H], w["WhT"], self.RM, self.S_m))
         if smp is not None:
             jobs.append((self.A[:, :H], w["WoT"], self.ZS, self.S_o))
         gemm.rec_gemm_group(jobs)

@@ -250,7 +250,7 @@ class GraphDecoder:
 
     def __init__(self, model, batch: int, steps: int, temperature: float = 1.0, greedy: bool = False,
                  fix_pen_temperature: bool = False, use_graph: bool = True, chunk: Optional[int] = None,
-                 early_exit: bool = True):
+                 early_exit: bool = True, fp8: bool = False):
         self.model = model
         self.kind = "vae" if hasattr(model, "encoder") else "reference"
         self.B, self.N = batch, steps
@@ -273,6 +273,7 @@ class GraphDecoder:
         c = int(chunk or self.CHUNK)
         self.ranges = [(t, min(t + c, steps)) for t in range(0, steps, c)] if steps > 0 else []
         self.early_exit = bool(early_exit)
+        self.fp8 = bool(fp8)   # MX-fp8 h W_h in the HyperLSTM step decoders (BASELINE config 5)
         self.steps_run = 0
         self._carry = {}     # tensors handed from one chunk to the next (state, next input, zc)
 
@@ -299,7 +300,7 @@ class GraphDecoder:
             return None
         if getattr(self, "_stp", None) is None:
             # chunk 0 runs on whatever stream is current at decode time (None)
-            self._stp = [(r0, n, HyperStepDecoder(self.model, n, self.dev, cluster=(i == 0)),
+            self._stp = [(r0, n, HyperStepDecoder(self.model, n, self.dev, cluster=(i == 0), fp8=self.fp8),
                           None if i == 0 else torch.cuda.Stream(device=self.dev))
                          for i, (r0, n) in enumerate(chunks)]
         return self._stp

@@ -1035,13 +1035,45 @@ def test_hyper_chained_launches_vs_unchained(B, T, fin_w):
         assert e_c <= 1.5 * e_p + 1e-3 * scale, (n, e_c, e_p, scale)
 
 
+@pytest.mark.parametrize("B,T,fin_w", [(100, 7, True), (100, 5, False), (37, 4, True), (128, 3, False),
+                                       (192, 4, True), (256, 3, False)])
+def test_hyper_three_stage_chain_bitwise(B, T, fin_w):
+    """csrc/chain_step.hip skr_chain_bwd_main3: dvec P^T computed by the
+    producer workgroups of the chained launch (weight slice staged in LDS
+    while the rows compute, A operand through sc1 loads after the rows'
+    counter) equals the separate dvec P^T launch bit for bit -- the same
+    fragments, k order and MFMA -- for every output and gradient; and the
+    launch really ran T - 1 times (B <= 128)."""
+    from sketch_rnn_amd.ops import hyper
+    from sketch_rnn_amd.ops.recurrent import ROW_STATS
+    p, x, z, st, w = _hyper_setup(8, T, B, 5, 16, 2048, 256, 32, jitter=0.02, state=0.1)
+    ops.set_backend("hip")
+    ops.set_compute_dtype("bf16")
+    saved = hyper.CHAIN, hyper.CHAIN3
+    runs = {}
+    try:
+        hyper.CHAIN = True
+        for c3 in (True, False, True):
+            hyper.CHAIN3 = c3
+            n0 = ROW_STATS["chain3"]
+            runs.setdefault(c3, []).append(_hyper_run(p, x, z, st, w, keep=0.9, hkeep=0.9, fin_w=fin_w))
+            # (B > 128: the tail is one 128-row block only -- not taken, two-stage chain)
+            assert ROW_STATS["chain3"] - n0 == ((T - 1) if (c3 and B <= 128) else 0)
+    finally:
+        hyper.CHAIN, hyper.CHAIN3 = saved
+    for n, a, b, c in zip(_names(p), runs[True][0], runs[False][0], runs[True][1]):
+        assert torch.equal(a, c), n
+        assert torch.equal(a, b), n
+
+
 @pytest.mark.parametrize("B,T", [(100, 7), (192, 4)])
 def test_hyper_chained_rows_never_overtake_the_counter(B, T):
-    """Poison mode (ops.hyper.CHAIN_POISON): the d[h | hh] slabs are NaN-filled
-    before every chained launch, so a main-cell row that read them before its
-    producer tiles had written them would carry NaN into h / c gradients and
-    every weight gradient. Every output and gradient must be finite and equal
-    to the unpoisoned chained run bit for bit."""
+    """Poison mode (ops.hyper.CHAIN_POISON): the d[h | hh] slabs (and, for the
+    three-stage launch, the dvec rows) are NaN-filled before every chained
+    launch, so a main-cell row that read them before its producer tiles had
+    written them -- or a dvec P^T tile that read dvec before the rows had --
+    would carry NaN into the gradients. Every output and gradient must be
+    finite and equal to the unpoisoned chained run bit for bit."""
     from sketch_rnn_amd.ops import hyper
     p, x, z, st, w = _hyper_setup(5, T, B, 5, 16, 2048, 256, 32, jitter=0.02, state=0.1)
     ops.set_backend("hip")
