@@ -17,17 +17,21 @@
 // the scales of ALL its K-steps in K/128 consecutive bytes -- one 16-byte
 // load per fragment for K <= 2048.
 //
-// Tile 128 x 128 x K, 512 threads (8 waves, 4 x 2, each 32 x 64 = 2 x 4 MFMA
-// tiles), K-steps of 128 through a 2-stage LDS-DMA ring (global_load_lds
+// Tile 256 x 128 x K, 512 threads (8 waves, 4 x 2, each 64 x 64 = 4 x 4 MFMA
+// tiles), K-steps of 128 through a 3-stage LDS-DMA ring, two K-steps in
+// flight behind counted vmcnt waits (global_load_lds
 // 16 B per lane, 128-byte LDS rows with the 16-byte chunk index XOR
 // (row >> 1) & 7 applied on the global address, like csrc/glds_mma.h):
-// 64 KB of LDS, two workgroups per CU (<= 128 VGPRs). MFMA lane l holds bytes [32 (l >> 4),
-// +32) of row / column l & 15 for both operands (the same k order), C/D:
-// col = l & 15, rows 4 (l >> 4) + i. Tile order is XCD-aware: the 8 row
+// 144 KB of LDS, one 8-wave workgroup per CU. MFMA operands (measured,
+// scripts/micro/mx8_diag.py): lane l holds row / column l & 15, bytes 0-15 =
+// k [16 g, +16) and bytes 16-31 = k [64 + 16 g, +16) of the K-step, g = l >> 4,
+// and its scale operand applies to k [32 g, +32) -- so 32-k block g of a
+// row is scaled by lane group g's byte (a contiguous 32-byte fragment is
+// exact with unit scales but scales the wrong k: profiles/r6/mx8_diag.jsonl).
+// C/D: col = l & 15, rows 4 (l >> 4) + i. Tile order is XCD-aware: the 8 row
 // blocks that read one W column band share an XCD's L2.
 #include "common.h"
 
-#include <type_traits>
 
 namespace {
 
@@ -35,9 +39,9 @@ typedef __attribute__((ext_vector_type(8))) int i32x8;
 typedef __attribute__((ext_vector_type(4))) float f32x4;
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
-constexpr int TM = 128, TN = 128, TK = 128, NT = 512, NSTG = 2;
+constexpr int TM = 256, TN = 128, TK = 128, NT = 512, NSTG = 3;
 constexpr int STG = (TM + TN) * TK;          // bytes per stage
-constexpr int GPW = (TM + TN) / 8 / 8;       // 1-KiB DMA pieces per wave per stage
+constexpr int GPW = (TM + TN) / 8 / 8;       // 1-KiB DMA pieces per wave per stage (6)
 
 __device__ __forceinline__ int scale_off(int r, int b, int K) { return r * (K / 32) + (b & 3) * (K / 128) + (b >> 2); }
 
@@ -126,13 +130,17 @@ __device__ __forceinline__ i32x8 frag(const uint8_t* S, int row) {
     return i32x8{lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
 }
 
-template <int SEL>
 __device__ __forceinline__ f32x4 mma(i32x8 a, i32x8 b, f32x4 c, int sa, int sb) {
-    // formats 0 / 0: e4m3 x e4m3; the scale operands' byte SEL is this lane's block scale
-    return __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a, b, c, 0, 0, SEL, sa, SEL, sb);
+    // formats 0 / 0: e4m3 x e4m3; byte 0 of each scale operand is this lane's block scale
+    return __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a, b, c, 0, 0, 0, sa, 0, sb);
 }
 
-__device__ __forceinline__ uint32_t word(const u32x4& v, int i) { return i == 0 ? v[0] : i == 1 ? v[1] : i == 2 ? v[2] : v[3]; }
+// byte kt of a lane's 16 scale bytes (one per K-step), as the low byte
+__device__ __forceinline__ int scale_byte(const u32x4& v, int kt) {
+    const int q = kt >> 2;
+    const uint32_t w = q == 0 ? v[0] : q == 1 ? v[1] : q == 2 ? v[2] : v[3];
+    return (int)(w >> (8 * (kt & 3)));
+}
 
 template <int LAYOUT>
 __global__ __launch_bounds__(NT) void mx8_gemm_kernel(const uint8_t* __restrict__ A8, int64_t lda,
@@ -146,19 +154,20 @@ __global__ __launch_bounds__(NT) void mx8_gemm_kernel(const uint8_t* __restrict_
     if (lin >= mb * (N / TN)) return;
     const int m0 = (lin % mb) * TM, n0 = (lin / mb) * TN;     // the row blocks of one column band: consecutive
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const int wm = w >> 1, wn = w & 1, fr = lane & 15, fq = lane >> 4;   // wave: rows 32 wm.., columns 64 wn..
+    const int wm = w >> 1, wn = w & 1, fr = lane & 15, fq = lane >> 4;   // wave: rows 64 wm.., columns 64 wn..
     const int nk = K / TK;
 
-    // ---- DMA sources: wave w moves 1-KiB pieces w, w + 8, ... (8 rows x 128 B each) of A then W
+    // ---- DMA sources: wave w moves 1-KiB pieces w, w + 8, ... (8 rows x 128 B each): A rows, then W rows
+    constexpr int APC = TM / 8;                                // A pieces per stage
     const int r8 = lane >> 3, slot = lane & 7;
     const uint8_t* src[GPW];
 #pragma unroll
     for (int i = 0; i < GPW; ++i) {
-        const int piece = w + 8 * i;                       // 0..15: A rows, 16..31: W rows
-        const int row = (piece & 15) * 8 + r8;
+        const int piece = w + 8 * i;
+        const int row = (piece < APC ? piece : piece - APC) * 8 + r8;
         const int c = slot ^ ((row >> 1) & 7);
-        src[i] = piece < 16 ? A8 + (int64_t)min(m0 + row, M - 1) * lda + 16 * c
-                            : W8 + (int64_t)(n0 + row) * ldw + 16 * c;
+        src[i] = piece < APC ? A8 + (int64_t)min(m0 + row, M - 1) * lda + 16 * c
+                             : W8 + (int64_t)(n0 + row) * ldw + 16 * c;
     }
     auto issue = [&](int kt) {
         uint8_t* st = smem + (kt % NSTG) * STG;
@@ -168,66 +177,59 @@ __global__ __launch_bounds__(NT) void mx8_gemm_kernel(const uint8_t* __restrict_
                                              (__attribute__((address_space(3))) void*)(st + (w + 8 * i) * 1024), 16, 0, 0);
     };
     // ---- this lane's block scales for every K-step: K / 128 bytes per fragment (K <= 2048)
-    u32x4 sa[2], sb[4];
+    u32x4 sa[4], sb[4];
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-        const int r = min(m0 + 32 * wm + 16 * i + fr, M - 1);
+    for (int i = 0; i < 4; ++i) {
+        const int r = min(m0 + 64 * wm + 16 * i + fr, M - 1);
         const uint32_t* pa = (const uint32_t*)(SA + (int64_t)r * (K / 32) + fq * (K / 128));
-#pragma unroll
-        for (int q = 0; q < 4; ++q) sa[i][q] = q < K / 512 ? pa[q] : 0u;   // K / 512 words: one per 4 K-steps
-    }
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        const int c = n0 + 64 * wn + 16 * j + fr;
+        const int c = n0 + 64 * wn + 16 * i + fr;
         const uint32_t* pb = (const uint32_t*)(SW + (int64_t)c * (K / 32) + fq * (K / 128));
 #pragma unroll
-        for (int q = 0; q < 4; ++q) sb[j][q] = q < K / 512 ? pb[q] : 0u;
+        for (int q = 0; q < 4; ++q) {                          // K / 512 words: one per 4 K-steps
+            sa[i][q] = q < K / 512 ? pa[q] : 0u;
+            sb[i][q] = q < K / 512 ? pb[q] : 0u;
+        }
     }
-    f32x4 acc[2][4];
+    f32x4 acc[4][4];
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-    // one K-step; SEL (= kt % 4) is the scale byte, an immediate of the MFMA
-    auto kstep = [&](int kq, auto sel) {
-        constexpr int S = decltype(sel)::value;
-        const int kt = kq + S;
-        // stage kt landed for this wave (the scale loads above are older: vmcnt counts them too)
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();                   // ... for every wave; stage kt - 1 is free
-        if (kt + 1 < nk) issue(kt + 1);
+#pragma unroll
+    for (int p = 0; p < NSTG - 1; ++p)
+        if (p < nk) issue(p);
+    for (int kt = 0; kt < nk; ++kt) {
+        // stage kt landed for this wave: all but the (up to) NSTG - 2 younger
+        // stages' DMAs are done (the scale loads above are older still)
+        if (kt + 1 < nk) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GPW) : "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();                       // ... for every wave; stage kt - 1 is free
+        if (kt + NSTG - 1 < nk) issue(kt + NSTG - 1);
         const uint8_t* As = smem + (kt % NSTG) * STG;
         const uint8_t* Ws = As + TM * TK;
-        i32x8 af[2];
-        int a_s[2];
+        i32x8 af[4];
+        int a_s[4];
 #pragma unroll
-        for (int i = 0; i < 2; ++i) {
-            af[i] = frag<LAYOUT>(As, 32 * wm + 16 * i + fr);
-            a_s[i] = (int)word(sa[i], kq >> 2);
+        for (int i = 0; i < 4; ++i) {
+            af[i] = frag<LAYOUT>(As, 64 * wm + 16 * i + fr);
+            a_s[i] = scale_byte(sa[i], kt);
         }
 #pragma unroll
         for (int j = 0; j < 4; ++j) {          // one W fragment live at a time
             const i32x8 bf = frag<LAYOUT>(Ws, 64 * wn + 16 * j + fr);
-            const int b_s = (int)word(sb[j], kq >> 2);
+            const int b_s = scale_byte(sb[j], kt);
 #pragma unroll
-            for (int i = 0; i < 2; ++i) acc[i][j] = mma<S>(af[i], bf, acc[i][j], a_s[i], b_s);
+            for (int i = 0; i < 4; ++i) acc[i][j] = mma(af[i], bf, acc[i][j], a_s[i], b_s);
         }
-    };
-    issue(0);
-    for (int kq = 0; kq < nk; kq += 4) {                    // K-steps in groups of 4
-        kstep(kq, std::integral_constant<int, 0>{});
-        kstep(kq, std::integral_constant<int, 1>{});
-        kstep(kq, std::integral_constant<int, 2>{});
-        kstep(kq, std::integral_constant<int, 3>{});
     }
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j)
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
-                const int row = m0 + 32 * wm + 16 * i + 4 * fq + e;
+                const int row = m0 + 64 * wm + 16 * i + 4 * fq + e;
                 if (row < M) C[(int64_t)row * ldc + n0 + 64 * wn + 16 * j + fr] = acc[i][j][e];
             }
 }

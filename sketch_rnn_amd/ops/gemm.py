@@ -208,7 +208,31 @@ def grad_slot(param: torch.Tensor, shape) -> Optional[torch.Tensor]:
     # param.grad set to the slot, autograd would add the slot to itself
     if t is None or param.grad is not None or tuple(t.shape) != tuple(shape) or not t.is_contiguous() or t.dtype != torch.float32:
         return None
-    return t
+    # a FRESH view: autograd's AccumulateGrad adopts a gradient tensor only
+    # when nothing else references it -- the slot tensor itself (held by
+    # param._grad_slot) would be cloned, and gather_grads would copy it back
+    return t.view(t.shape)
+
+
+def grad_span(first: torch.Tensor, last: torch.Tensor, start: int, shape) -> Optional[torch.Tensor]:
+    """A fresh view of the optimizer arena covering ``numel(shape)`` floats
+    from element ``start`` of ``first``'s gradient slot -- reaching into the
+    slots of the parameters that follow it, up to ``last`` -- when those
+    slots are consecutive in the arena and every gradient is unbound (else
+    None). One kernel then writes a product whose rows are split over several
+    parameters (the HyperLSTM's [W_y_h; W_y_hh] weight gradient) in place."""
+    a, b = getattr(first, "_grad_slot", None), getattr(last, "_grad_slot", None)
+    if a is None or b is None or first.grad is not None or last.grad is not None:
+        return None
+    n = 1
+    for d in shape:
+        n *= d
+    end = b.data_ptr() + b.numel() * 4
+    if a.dtype != torch.float32 or a.data_ptr() + (start + n) * 4 != end:
+        return None
+    base = a.view(-1)
+    full = torch.as_strided(base, (n,), (1,), base.storage_offset() + start)
+    return full.view(*shape)
 
 
 def _wgrad_splits(tiles: int, K: int) -> int:

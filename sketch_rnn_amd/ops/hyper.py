@@ -375,7 +375,8 @@ class _HyperSeq(torch.autograd.Function):
         s = _Saved()
         for k, v in dict(xl=xl, x=x, zc=zc, bp=bp, XH=XH, Whl=Whl, Wyl=Wyl, Pl=Pl, q=q, S_m=S_m, A=A, RM=RM,
                          RLP=RLP, CC=CC, HCC=HCC, c0=c0c, hc0=hc0c, XHAT=XHAT, RSTD=RSTD, CHAT=CHAT, HH=HH, HXHAT=HXHAT, HRSTD=HRSTD,
-                         HCHAT=HCHAT, VEC=VEC, seed=sd, meta=meta, slp=slp, W_h=W_h, W_x=W_x, hW_x=hW_x, W_z=W_z, b_z=b_z, W_a=W_a,
+                         HCHAT=HCHAT, VEC=VEC, seed=sd, meta=meta, slp=slp, W_h=W_h, W_x=W_x, hW_x=hW_x, hW_h=hW_h, W_z=W_z,
+                         b_z=b_z, W_a=W_a,
                          mln=mln, hln=hln, vec_folded=hmod, mln_on=mln_on, ACT=ACT, COUT=COUT).items():
             setattr(s, k, v)
         ctx.s = s
@@ -593,9 +594,13 @@ class _HyperSeq(torch.autograd.Function):
         # dvec its column sums; the per-k factors are then tiny batched products.
         # (hh_t rows, HHl: the bf16 GEMM operand of step t + 1 -- no resets on
         # this path, so it is exactly bf16(HH[t]) -- no conversion pass)
+        # dW_y = [dW_y_h; dW_y_hh] straight into the arena when hW_x's slot (rows
+        # IN..) and hW_h's follow each other there: no gather copy afterwards
+        dW_y_arena = None if (bg is not None or s.hW_x.shape[0] != IN + H) else \
+            gemm.grad_span(s.hW_x, s.hW_h, IN * Gh, (K, Gh))
         if bg is None:
             dW_h = gemm.wgrad(A2[:, :H], dRM_lp.view(TB, G), out=gemm.grad_slot(s.W_h, (H, G)))
-            dW_y = gemm.wgrad(A2, dRY_lp.view(TB, Gh))
+            dW_y = gemm.wgrad(A2, dRY_lp.view(TB, Gh), out=dW_y_arena)
             dP1, sV = gemm.wgrad(HHl, dVEC.view(TB, 12 * H), colsum=True)
         # the four LayerNorm gamma / beta reductions in two launches (csrc/reduce.hip)
         lnp = [(DLNY, s.XHAT, G), (DLNCY, s.CHAT, H)] if DLNY is not None else []
@@ -606,13 +611,17 @@ class _HyperSeq(torch.autograd.Function):
             g_ln, g_hln = [None] * 4, flat
         else:
             g_ln, g_hln = flat[:4], flat[4:]
-        dhW_x = torch.empty_like(s.hW_x)
+        if dW_y_arena is not None:   # the slots themselves (fresh views: autograd adopts them, no copies)
+            dhW_x, dhW_h = gemm.grad_slot(s.hW_x, tuple(s.hW_x.shape)), gemm.grad_slot(s.hW_h, tuple(s.hW_h.shape))
+        else:
+            dhW_x, dhW_h = torch.empty_like(s.hW_x), None
         dx = dzc = None
         if s.bp:   # input-side gradients from one read of dXH / dR_hyp each
             S_m, P_m = bproj_reduce(s.x, dXH)
             S_y, P_y = bproj_reduce(s.x, dRY_lp)
             if s.zc is not None:
-                dW_x = torch.empty_like(s.W_x)
+                dW_x = gemm.grad_slot(s.W_x, tuple(s.W_x.shape))
+                dW_x = torch.empty_like(s.W_x) if dW_x is None else dW_x
                 dW_x[:IX] = P_m
                 dhW_x[:IX] = P_y
                 g = gemm.SmallGroup(dev)   # the three independent z-side products in one launch
@@ -637,8 +646,9 @@ class _HyperSeq(torch.autograd.Function):
                 dx = dxf
         if bg is not None:   # the side stream's products are complete from here on
             bg.join()
-        dhW_x[IN:] = dW_y[:H]
-        dhW_h = dW_y[H:]
+        if dW_y_arena is None:
+            dhW_x[IN:] = dW_y[:H]
+            dhW_h = dW_y[H:]
         dW_z, db_z, dWa, dbias = _hyper_proj_grads(dP1, sV, s, Hh, H, E)
         ctx.s = None
         return (dx, dzc, dh0, dc_rec, dhh0, dhc_rec, None, dW_x, dW_h, dbias, dhW_x, dhW_h,

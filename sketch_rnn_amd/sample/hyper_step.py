@@ -109,12 +109,12 @@ class HyperStepDecoder:
         # E <= 32, 32-unit tiles, <= 4 main-GEMM slabs)
         self.fused = FUSED and Hh == 256 and self.E <= 32 and H % 32 == 0
         self.fp8 = bool(fp8) and self.fused and H % 512 == 0 and H <= 2048 and G % 128 == 0
-        if self.fp8:   # MX-fp8 h W_h: one fp32 output (no split-K), h's fp8 copy from the main cell
-            self.S_m = 1
-            self.A8 = torch.zeros(B, H, dtype=torch.uint8, device=device)
-            self.SA = torch.zeros(B, H // 32, dtype=torch.uint8, device=device)
-        elif self.fused:
+        if self.fused:
             self.S_m = 4 if self.S_m >= 4 else 2 if self.S_m >= 2 else 1
+            if self.fp8:   # MX-fp8 h W_h: one fp32 output (no split-K), h's fp8 copy from the main cell
+                self.S_m = 1
+                self.A8 = torch.zeros(B, H, dtype=torch.uint8, device=device)
+                self.SA = torch.zeros(B, H // 32, dtype=torch.uint8, device=device)
             self.X = torch.zeros(B, 5, dtype=f32, device=device)
             self.GP = torch.empty(B, G, dtype=f32, device=device)
             self.GS = torch.empty(B, 4, H // 32, 2, dtype=f32, device=device)

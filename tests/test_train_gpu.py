@@ -163,3 +163,33 @@ def test_hip_adam_grad_scale_fold_bitwise():
         torch.cuda.synchronize()
         assert torch.equal(a.flat, b.flat) and torch.equal(a.m, b.m) and torch.equal(a.v, b.v)
         assert torch.equal(a.scalars[:6], b.scalars[:6])
+
+
+def test_arena_gradients_equal_plain_autograd():
+    """Weight gradients written straight into the optimizer arena (the
+    HyperLSTM's W_h slot, the [W_y_h; W_y_hh] span across two slots, W_x's
+    slot: ops.gemm.grad_slot / grad_span, adopted by autograd without a
+    copy) equal the gradients of the same loss computed with plain autograd
+    on an arena-free copy of the model, bit for bit: placing a result
+    changes no arithmetic. Also checks that the big slots really were
+    adopted (p.grad shares the arena's storage)."""
+    from sketch_rnn_amd import ops
+    from sketch_rnn_amd.models.vae import SketchVAE
+    cfg = VAEConfig(enc_rnn_size=256, dec_rnn_size=512, z_size=32, num_mixture=5, max_seq_len=60, batch_size=16,
+                    dec_model="hyper", hyper_num_units=256, hyper_embedding_size=32, save_every=0)
+    tr, train = _trainer(cfg, graph=False)
+    s, l, c = tr.batch_to_device(train.random_batch())
+    tr._fwd_bwd(s, l, c)
+    torch.cuda.synchronize()
+    ref = SketchVAE(cfg).to("cuda")
+    ref.load_state_dict(tr.model.state_dict())
+    ops.set_compute_dtype("bf16")
+    out = ref.loss(s, l, None, kl_weight=tr.kl_w, train=True, seed=tr.seed)
+    out["cost"].backward()
+    torch.cuda.synchronize()
+    arena = tr.opt.grad
+    for (n, p), (_, q) in zip(tr.model.named_parameters(), ref.named_parameters()):
+        assert torch.equal(p.grad, q.grad), n
+    for n in ("dec.W_h", "dec.hyp_W_x", "dec.hyp_W_h", "dec.W_x"):
+        p = dict(tr.model.named_parameters())[n]
+        assert p.grad.untyped_storage().data_ptr() == arena.untyped_storage().data_ptr(), n
