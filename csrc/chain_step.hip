@@ -47,8 +47,12 @@ __device__ __forceinline__ void producer_tile(const GemmGroup& g, const ChainSyn
 }
 
 // backward, main cell: [producers (dR_hyp W_y^T of step t + 1), 8 waves][main cell rows of step t]
-// POLL: the rows' poll period (s_sleep units), skr_chain_set_poll
-template <int POLL>
+// POLL: the rows' poll period (s_sleep units), skr_chain_set_poll.
+// CL = 2: each row on two workgroups (1024 units each: waves 0-3 of the
+// 512-thread workgroup; waves 4-7 end at once -- a barrier waits only on the
+// waves still running), the two LayerNorm-backward row sums exchanged
+// in-launch (row_bwd_body CL): half of the row's ~300 KB of loads per CU.
+template <int POLL, int CL>
 __global__ __launch_bounds__(512) void chain_bwd_main_kernel(const GemmGroup g, const int nprod, const skr::BwdArgs cell,
                                                              const ChainSync cs) {
     extern __shared__ __attribute__((aligned(16))) __hip_bfloat16 smem[];
@@ -57,7 +61,14 @@ __global__ __launch_bounds__(512) void chain_bwd_main_kernel(const GemmGroup g, 
         producer_tile<8>(g, cs, smem);
         return;
     }
-    row_bwd_body<512, 4, true, 1, true, false, POLL>(cell, id - nprod, cs.counters + cs.k, (uint32_t)nprod, cs.err);
+    if constexpr (CL == 1) {
+        row_bwd_body<512, 4, true, 1, true, false, POLL>(cell, id - nprod, cs.counters + cs.k, (uint32_t)nprod, cs.err);
+    } else {
+        if (__builtin_amdgcn_readfirstlane(threadIdx.x) >= 512 / CL) return;   // (wave-uniform)
+        const int r = id - nprod;
+        row_bwd_body<512 / CL, 4, true, 1, true, false, POLL, CL>(cell, r / CL, cs.counters + cs.k, (uint32_t)nprod,
+                                                                   cs.err, r % CL);
+    }
 }
 
 static int g_row_poll = 1;
@@ -245,7 +256,8 @@ int check_sync(const ChainSync* cs) {
 
 // Backward main-cell chain: probs[0 .. n) (all producers) produce the row's
 // dh_rec slabs (<= 8); everything else as skr_row_bwd_step mod 2 with
-// H = 2048 (512 threads x 4 units) and a single dh_out slab.
+// H = 2048 (512 threads x 4 units) and a single dh_out slab; cell->cluster
+// == 2 splits every row over two workgroups (exchange buffer cell->part).
 SKR_API int skr_chain_bwd_main(const GemmProblem* probs, int n, const skr::BwdArgs* cell, const ChainSync* cs,
                                hipStream_t s) {
     if (cell == nullptr || check_sync(cs)) return -6;
@@ -257,16 +269,19 @@ SKR_API int skr_chain_bwd_main(const GemmProblem* probs, int n, const skr::BwdAr
     GemmGroup g;
     const int np = build_group(probs, n, n, g);
     if (np < 0) return np;
-    if (g_row_poll >= 16) {
-        lds_attr(chain_bwd_main_kernel<16>, kLds);
-        hipLaunchKernelGGL(chain_bwd_main_kernel<16>, dim3(np + a.B), dim3(512), kLds, s, g, np, a, *cs);
-    } else if (g_row_poll >= 4) {
-        lds_attr(chain_bwd_main_kernel<4>, kLds);
-        hipLaunchKernelGGL(chain_bwd_main_kernel<4>, dim3(np + a.B), dim3(512), kLds, s, g, np, a, *cs);
-    } else {
-        lds_attr(chain_bwd_main_kernel<1>, kLds);
-        hipLaunchKernelGGL(chain_bwd_main_kernel<1>, dim3(np + a.B), dim3(512), kLds, s, g, np, a, *cs);
-    }
+    // cell.cluster == 2: two workgroups per row (a.part / a.err: the exchange buffer, [2][B][2][16])
+    const int cl = a.cluster == 2 ? 2 : 1;
+    if (cl == 2 && (a.part == nullptr || a.err == nullptr)) return -6;
+#define SKR_CBM(P_, CL_)                                                                              \
+    do {                                                                                              \
+        lds_attr(chain_bwd_main_kernel<P_, CL_>, kLds);                                               \
+        hipLaunchKernelGGL((chain_bwd_main_kernel<P_, CL_>), dim3(np + a.B * CL_), dim3(512), kLds, s, g, np, a, *cs); \
+    } while (0)
+    if (cl == 2) SKR_CBM(1, 2);
+    else if (g_row_poll >= 16) SKR_CBM(16, 1);
+    else if (g_row_poll >= 4) SKR_CBM(4, 1);
+    else SKR_CBM(1, 1);
+#undef SKR_CBM
     return SKR_CHECK_LAUNCH();
 }
 

@@ -30,14 +30,13 @@
 // (Round 4 measured an unfolded variant -- vec = bf16(hh W_z) W_a + q on two
 // MFMA stages, W_z L2-resident instead of the 12.6 MB folded P -- at 12.9 vs
 // 10.2 us per step, with a slower backward; profiles/r4/unfold_ab.txt.)
-#include "common.h"
+#include "cell_fwd_body.h"
+#include "handoff.h"
 
 namespace {
 
 using namespace skr;
 
-typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
-typedef __attribute__((ext_vector_type(4))) float f32x4;
 typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 
 constexpr int HH = 256, NTH = 384, TU = 32;      // hyper units (K), threads, units per tile
@@ -65,22 +64,24 @@ struct ModDecode {
 
 namespace {
 
+// One modulation tile: gate q, hidden units [TU tile, +TU), row block z.
 // NRT: 16-row tiles staged and multiplied (rows up to 16 NRT; a B = 100 launch
-// pays for 112 rows, not MAXB).
-template <int NS, int NRT>
-__global__ __launch_bounds__(NTH) void hyper_mod_fwd(ModDecode dec, const __hip_bfloat16* __restrict__ hh, int64_t ld_hh,
-                                                     const __hip_bfloat16* __restrict__ PlT,   // [12H][HH]
-                                                     const float* __restrict__ qb,             // [12H]
-                                                     const float* __restrict__ xh,             // [B][4H]
-                                                     const float* __restrict__ R, int64_t r_slab,   // [NS][B][4H]
-                                                     __hip_bfloat16* __restrict__ vec,          // [B][12H]
-                                                     float* __restrict__ gout,                  // [B][4H]
-                                                     __hip_bfloat16* __restrict__ rlp,          // [B][4H] or null
-                                                     float* __restrict__ stats,                 // [B][4][H/TU][2]
-                                                     int B, int H) {
+// pays for 112 rows, not MAXB). SC1: g and the partial sums are read by
+// workgroups of the SAME launch (hyper_mod_chain): write-through stores.
+template <int NS, int NRT, bool SC1>
+__device__ __forceinline__ void mod_tile(ModDecode dec, const __hip_bfloat16* __restrict__ hh, int64_t ld_hh,
+                                         const __hip_bfloat16* __restrict__ PlT,   // [12H][HH]
+                                         const float* __restrict__ qb,             // [12H]
+                                         const float* __restrict__ xh,             // [B][4H]
+                                         const float* __restrict__ R, int64_t r_slab,   // [NS][B][4H]
+                                         __hip_bfloat16* __restrict__ vec,          // [B][12H]
+                                         float* __restrict__ gout,                  // [B][4H]
+                                         __hip_bfloat16* __restrict__ rlp,          // [B][4H] or null
+                                         float* __restrict__ stats,                 // [B][4][H/TU][2]
+                                         int B, int H, const int q, const int tile, const int z) {
     constexpr int MB = 16 * NRT;
-    {   // row block blockIdx.z (B > MAXB: the wide decode): rows r0 .. r0 + MAXB - 1
-        const int r0 = blockIdx.z * MAXB;
+    {   // row block z (B > MAXB: the wide decode): rows r0 .. r0 + MAXB - 1
+        const int r0 = z * MAXB;
         B = min(MAXB, B - r0);
         const int64_t G4 = (int64_t)r0 * 4 * H;
         if (hh) hh += (int64_t)r0 * ld_hh;
@@ -97,7 +98,7 @@ __global__ __launch_bounds__(NTH) void hyper_mod_fwd(ModDecode dec, const __hip_
     }
     __shared__ __attribute__((aligned(16))) __hip_bfloat16 sA[MB * HH];     // <= 64 KB
     __shared__ __attribute__((aligned(16))) float sV[6][MB][16];            // <= 48 KB
-    const int q = blockIdx.y, u0 = blockIdx.x * TU, ntile = H / TU;
+    const int u0 = tile * TU, ntile = H / TU;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int fr = lane & 15, fq = lane >> 4;
     const int G = 4 * H, NV = 12 * H;
@@ -172,6 +173,8 @@ __global__ __launch_bounds__(NTH) void hyper_mod_fwd(ModDecode dec, const __hip_
     __syncthreads();
     // ---- epilogue (no loads left): 8 threads per row (lanes 8k..8k+7)
     const int ch = ul >> 4, cu = ul & 15;          // column tile half, column inside it
+    const __amdgpu_buffer_rsrc_t gr = rsrc(gout, (int64_t)B * G * 4);
+    const __amdgpu_buffer_rsrc_t sr = rsrc(stats, (int64_t)B * 4 * ntile * 8);
 #pragma unroll
     for (int k = 0; k < RPT; ++k) {
         const int r = rg + k * (NTH / 8);
@@ -197,7 +200,9 @@ __global__ __launch_bounds__(NTH) void hyper_mod_fwd(ModDecode dec, const __hip_
         s2 += __shfl_xor(s2, 4, 64);
         if (on) {
             const int64_t go = (int64_t)rr * G + q * H + u0 + ul;
-            *(f32x4*)(gout + go) = f32x4{g[0], g[1], g[2], g[3]};
+            if constexpr (SC1) st_sc1(gr, (uint32_t)(go * 4), u32x4{__float_as_uint(g[0]), __float_as_uint(g[1]),
+                                                                     __float_as_uint(g[2]), __float_as_uint(g[3])});
+            else *(f32x4*)(gout + go) = f32x4{g[0], g[1], g[2], g[3]};
             if (rlp) *(u32x2*)(rlp + go) = u32x2{pack_bf(r4[k][0], r4[k][1]), pack_bf(r4[k][2], r4[k][3])};
             const int64_t vo = (int64_t)rr * NV + u0 + ul;
             if (vec) {   // (null at inference)
@@ -207,12 +212,170 @@ __global__ __launch_bounds__(NTH) void hyper_mod_fwd(ModDecode dec, const __hip_
             // (the shift block 8..11 is not stored: the backward reads only
             // the x and h modulations -- d(shift) = dg needs no saved value)
             if (ug == 0) {
-                float* sp = stats + (((int64_t)rr * 4 + q) * ntile + blockIdx.x) * 2;
-                sp[0] = s1;
-                sp[1] = s2;
+                const int64_t so = (((int64_t)rr * 4 + q) * ntile + tile) * 2;
+                if constexpr (SC1) {
+                    st_sc1_f32(sr, (uint32_t)(so * 4), s1);
+                    st_sc1_f32(sr, (uint32_t)(so * 4 + 4), s2);
+                } else {
+                    stats[so] = s1;
+                    stats[so + 1] = s2;
+                }
             }
         }
     }
+}
+
+template <int NS, int NRT>
+__global__ __launch_bounds__(NTH) void hyper_mod_fwd(ModDecode dec, const __hip_bfloat16* __restrict__ hh, int64_t ld_hh,
+                                                     const __hip_bfloat16* __restrict__ PlT, const float* __restrict__ qb,
+                                                     const float* __restrict__ xh, const float* __restrict__ R,
+                                                     int64_t r_slab, __hip_bfloat16* __restrict__ vec,
+                                                     float* __restrict__ gout, __hip_bfloat16* __restrict__ rlp,
+                                                     float* __restrict__ stats, int B, int H) {
+    mod_tile<NS, NRT, false>(dec, hh, ld_hh, PlT, qb, xh, R, r_slab, vec, gout, rlp, stats, B, H, blockIdx.y, blockIdx.x,
+                             blockIdx.z);
+}
+
+// ---- chained launch: the modulation tiles + the main LayerNorm cell rows -----------------
+// Every workgroup first runs its modulation tile (gate q, 32 units: all rows,
+// one row block), stores g and the tile partial sums write-through and
+// arrives on the launch's counter; workgroups [0, B C) then run the main cell
+// of row b = id / C over units [c H / C, (c + 1) H / C), c = id % C: the loads
+// that do not depend on the tiles (c_prev, the LayerNorm parameters) are
+// issued before the wait, g and the partial sums are read with sc1 loads
+// after it. Every workgroup arrives before any waits, so the launch needs all
+// of its workgroups resident at once (the host checks the grid against the
+// occupancy API; the waits are bounded and set *err).
+// Arithmetic: cell_fwd_body MOD 3 (csrc/cell_fwd_body.h) with NT = NTH
+// threads and UPT units per thread (per-thread unit u = base + k NTH + tid).
+__device__ __forceinline__ float pick4(const float (&v)[4], int i) {
+    return i == 0 ? v[0] : i == 1 ? v[1] : i == 2 ? v[2] : v[3];
+}
+
+template <int UPT>
+__device__ __forceinline__ void main_rows(const FwdArgs& a, const int b, const int c, const int C,
+                                          const uint32_t* cnt, uint32_t target, int* err) {
+    constexpr int NT = NTH, NW = NT / 64;
+    __shared__ float lds[NW * 8];
+    __shared__ float mine[8];
+    __shared__ float all[kMaxCluster * 8];
+    const int tid = threadIdx.x, H = a.H, per = H / C, base = c * per;
+    const bool keep_on = a.keep < 1.0f;
+    const uint32_t key = keep_on ? hash_key(*a.seed, a.stream, a.step) : 0u;
+    const bool r = a.reset != nullptr && a.reset[b] != 0.f;
+    const bool save = a.xhat != nullptr;
+    // ---- loads that do not depend on this launch's tiles
+    float cp[UPT], lg[UPT][4], lb[UPT][4], lcg[UPT], lcb[UPT];
+    bool on[UPT];
+    int uc[UPT];
+#pragma unroll
+    for (int k = 0; k < UPT; ++k) {
+        const int u = base + k * NT + tid;
+        on[k] = u < base + per;
+        uc[k] = min(u, base + per - 1);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            lg[k][q] = a.ln_g[q * H + uc[k]];
+            lb[k][q] = a.ln_b[q * H + uc[k]];
+        }
+        cp[k] = a.c_prev[(int64_t)b * H + uc[k]];
+        lcg[k] = a.lnc_g[uc[k]];
+        lcb[k] = a.lnc_b[uc[k]];
+    }
+    chain_wait<1>(cnt, target, err);
+    // ---- g and the row's per-tile partial sums (stored by other workgroups of this launch)
+    const __amdgpu_buffer_rsrc_t gr = rsrc(a.gpre + (int64_t)b * 4 * H, (int64_t)4 * H * 4);
+    const __amdgpu_buffer_rsrc_t sr = rsrc(a.gstats + (int64_t)b * 4 * a.gstat_tiles * 2, (int64_t)a.gstat_tiles * 32);
+    float g[UPT][4];
+#pragma unroll
+    for (int k = 0; k < UPT; ++k)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) g[k][q] = ld_sc1_f32(gr, (uint32_t)((q * H + uc[k]) * 4));
+    float s[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) s[q] = 0.f;
+    for (int i = tid; i < 4 * a.gstat_tiles; i += NT) {
+        const int gq = i / a.gstat_tiles;
+        const float v1 = ld_sc1_f32(sr, (uint32_t)(i * 8)), v2 = ld_sc1_f32(sr, (uint32_t)(i * 8 + 4));
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            if (q == gq) {
+                s[q] += v1;
+                s[4 + q] += v2;
+            }
+        }
+    }
+    block_sum<8, NW>(s, lds);
+    float mean[4], rs[4], xs[UPT][4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        mean[q] = s[q] / (float)H;
+        rs[q] = rsqrtf(fmaxf(s[4 + q] / (float)H - mean[q] * mean[q], 0.f) + kLnEps);
+    }
+#pragma unroll
+    for (int k = 0; k < UPT; ++k)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            xs[k][q] = (g[k][q] - mean[q]) * rs[q];
+            g[k][q] = xs[k][q] * lg[k][q] + lb[k][q];
+        }
+    if (save && c == 0 && tid < 4) a.rstd[b * 5 + tid] = pick4(rs, tid);
+    // ---- cell
+    float cn[UPT], og[UPT], s2[2] = {0.f, 0.f};
+#pragma unroll
+    for (int k = 0; k < UPT; ++k) {
+        const int64_t ro = (int64_t)b * H + base + k * NT + tid;
+        const float i = cell_sig(g[k][0]);
+        const float tj = cell_tanh(g[k][1]);
+        const float f = cell_sig(g[k][2] + a.forget_bias);
+        og[k] = cell_sig(g[k][3]);
+        const float m = dropout_mult(keep_on, key, ro, a.keep);
+        cn[k] = on[k] ? cp[k] * f + i * tj * m : 0.f;
+        s2[0] += cn[k];
+        s2[1] += cn[k] * cn[k];
+    }
+    row_sum<2, NW>(s2, lds, mine, all, a.part + (int64_t)a.B * C * kSlots, a.err, a.step + 1, b, c, C);
+    const float mc = s2[0] / (float)H;
+    const float rc = rsqrtf(fmaxf(s2[1] / (float)H - mc * mc, 0.f) + kLnEps);
+    if (save && c == 0 && tid == 0) a.rstd[b * 5 + 4] = rc;
+#pragma unroll
+    for (int k = 0; k < UPT; ++k) {
+        if (!on[k]) continue;
+        const int u = base + k * NT + tid;
+        const int64_t ro = (int64_t)b * H + u;
+        const float ch = (cn[k] - mc) * rc;
+        const float h = cell_tanh(ch * lcg[k] + lcb[k]) * og[k];
+        if (save) {
+            st_save(a.chat, ro, ch, a.save_lp);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) st_save(a.xhat, (int64_t)b * 4 * H + q * H + u, xs[k][q], a.save_lp);
+        }
+        if (a.c_out != nullptr) a.c_out[ro] = cn[k];
+        a.h_out[ro] = h;
+        const float hc = r ? a.init_h[ro] : h;
+        if (a.h_carry != nullptr) a.h_carry[ro] = hc;
+        a.c_carry[ro] = r ? a.init_c[ro] : cn[k];
+        if (a.lp_kind == 1) ((__hip_bfloat16*)a.h_lp)[b * a.ld_lp + u] = to_bf16(hc);
+        else if (a.lp_kind == 2) ((float*)a.h_lp)[b * a.ld_lp + u] = hc;
+    }
+}
+
+template <int NS, int NRT, int UPT>
+__global__ __launch_bounds__(NTH) void hyper_mod_chain(const __hip_bfloat16* __restrict__ hh, int64_t ld_hh,
+                                                       const __hip_bfloat16* __restrict__ PlT, const float* __restrict__ qb,
+                                                       const float* __restrict__ xh, int xh_bf16, const float* __restrict__ R,
+                                                       int64_t r_slab, __hip_bfloat16* __restrict__ vec,
+                                                       __hip_bfloat16* __restrict__ rlp, const FwdArgs cell, const int C,
+                                                       const ChainSync cs) {
+    const int id = blockIdx.x, H = cell.H, ntile = H / TU;
+    if (id == 0) chain_rotate(cs.counters, cs.n, cs.k);
+    ModDecode dec{};
+    dec.xh_bf16 = xh_bf16;
+    mod_tile<NS, NRT, true>(dec, hh, ld_hh, PlT, qb, xh, R, r_slab, vec, const_cast<float*>(cell.gpre), rlp,
+                            const_cast<float*>(cell.gstats), cell.B, H, id / ntile, id % ntile, 0);
+    chain_arrive(cs.counters + cs.k);
+    if (id >= cell.B * C) return;
+    main_rows<UPT>(cell, id / C, id % C, C, cs.counters + cs.k, (uint32_t)gridDim.x, cs.err);
 }
 
 }  // namespace
@@ -253,5 +416,56 @@ SKR_API int skr_hyper_mod_fwd(const void* hh, int64_t ld_hh, const void* PlT, co
     }
 #undef SKR_HM_NS
 #undef SKR_HM
+    return SKR_CHECK_LAUNCH();
+}
+
+// Chained modulation step + main LayerNorm cell (hyper_mod_chain above): the
+// modulation operands as skr_hyper_mod_fwd (training layout: xh precomputed,
+// fp32 or bf16), cell = the MOD-3 main-cell arguments (gpre / gstats = this
+// launch's g and partial-sum outputs) with cell->cluster = C workgroups per
+// row. One row block (B <= 128) and B C <= 4 H / 32 rows' workgroups.
+// Returns -2 / -3 / -4 when the shape is not taken (callers keep the two
+// launches), -8 when the grid cannot be resident at once.
+SKR_API int skr_hyper_mod_chain(const void* hh, int64_t ld_hh, const void* PlT, const float* qb, const float* xh,
+                                int xh_bf16, const float* R, int64_t r_slab, int nslab, void* vec, void* rlp,
+                                const skr::FwdArgs* cell, const ChainSync* cs, hipStream_t s) {
+    if (cell == nullptr || cs == nullptr || cs->counters == nullptr || cs->err == nullptr || cs->n < 2 || cs->k < 0 ||
+        cs->k >= cs->n)
+        return -6;
+    const skr::FwdArgs& a = *cell;
+    const int B = a.B, H = a.H, C = a.cluster > 1 ? a.cluster : 1;
+    if (B <= 0) return 0;
+    if (B > MAXB || H % TU != 0 || xh == nullptr || hh == nullptr || a.gpre == nullptr || a.gstats == nullptr ||
+        a.gstat_tiles != H / TU || a.h_q8 != nullptr || a.r_lp != nullptr || a.ln_g == nullptr || a.grp_rows > 0)
+        return -3;
+    if (nslab != 1 && nslab != 2 && nslab != 4) return -3;
+    if (H % C != 0 || (C > 1 && (a.part == nullptr || a.err == nullptr)) || C > kMaxCluster) return -3;
+    const int per = H / C, upt = (per + NTH - 1) / NTH;
+    const int grid = 4 * (H / TU);
+    if (B * C > grid) return -2;
+    if (((uintptr_t)hh | (uintptr_t)PlT | (uintptr_t)xh | (uintptr_t)R | (uintptr_t)vec | (uintptr_t)a.gpre |
+         (uintptr_t)rlp) & 15 || (ld_hh % 8) || (r_slab % 4))
+        return -4;
+    const auto* ap = (const __hip_bfloat16*)hh;
+    const auto* pp = (const __hip_bfloat16*)PlT;
+    auto* v = (__hip_bfloat16*)vec;
+    auto* rl = (__hip_bfloat16*)rlp;
+    const int nrt = B <= 32 ? 2 : B <= 64 ? 4 : B <= 112 ? 7 : 8;
+    const void* k = nullptr;
+#define SKR_HC_PICK(NS_, NRT_, UPT_) if (nslab == NS_ && nrt == NRT_ && upt == UPT_) k = (const void*)hyper_mod_chain<NS_, NRT_, UPT_>
+#define SKR_HC_NRT(NS_, UPT_) SKR_HC_PICK(NS_, 2, UPT_); SKR_HC_PICK(NS_, 4, UPT_); SKR_HC_PICK(NS_, 7, UPT_); SKR_HC_PICK(NS_, 8, UPT_)
+#define SKR_HC_UPT(NS_) SKR_HC_NRT(NS_, 2); SKR_HC_NRT(NS_, 3); SKR_HC_NRT(NS_, 6)
+    SKR_HC_UPT(1);
+    SKR_HC_UPT(2);
+    SKR_HC_UPT(4);
+#undef SKR_HC_UPT
+#undef SKR_HC_NRT
+#undef SKR_HC_PICK
+    if (k == nullptr) return -2;
+    // every workgroup waits on every other one: all must be resident at once
+    if (!grid_fits(k, NTH, 0, grid, 1)) return -8;
+    void* args[] = {(void*)&ap, (void*)&ld_hh, (void*)&pp, (void*)&qb, (void*)&xh, (void*)&xh_bf16, (void*)&R,
+                    (void*)&r_slab, (void*)&v, (void*)&rl, (void*)&a, (void*)&C, (void*)cs};
+    if (hipLaunchKernel(k, dim3(grid), dim3(NTH), args, 0, s) != hipSuccess) return -1;
     return SKR_CHECK_LAUNCH();
 }

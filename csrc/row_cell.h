@@ -3,8 +3,8 @@
 // same body as the waiting rows of a chained launch). Design and semantics:
 // csrc/row_cell.hip header comment.
 #pragma once
+#include "cell_fwd_body.h"
 #include "handoff.h"
-#include "lstm_args.h"
 
 namespace {
 
@@ -107,6 +107,24 @@ __device__ __forceinline__ float pick(const float (&v)[N], int i) {
     return r;
 }
 
+// Row sums of a row split over C workgroups: each workgroup's block sums
+// (already in every thread) published and the C partials added in part order.
+template <int N>
+__device__ __forceinline__ void row_exchange(float (&v)[N], float* mine, float* all, uint64_t* part, int* err,
+                                             uint32_t tag, int b, int c, int C) {
+    if (threadIdx.x == 0) {
+#pragma unroll
+        for (int i = 0; i < N; ++i) mine[i] = v[i];
+    }
+    cluster_allgather(part, err, b, c, C, mine, N, tag, all);
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+        float s = 0.f;
+        for (int cc = 0; cc < C; ++cc) s += all[cc * N + i];
+        v[i] = s;
+    }
+}
+
 // ---- backward ------------------------------------------------------------------------
 // MOD: HyperLSTM main cell (bf16 modulation vectors, bf16 R copy; writes
 // dxh = dg*ax, dvec = [dg*xh | dg*R | dg] and dR = dg*ah); otherwise dG = dg.
@@ -126,13 +144,19 @@ __device__ __forceinline__ void stb_sc1(void* p, const float (&v)[V]) {
     __hip_atomic_store((uint64_t*)p, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-template <int NT, int V, bool MOD, int DO, bool CHAIN = false, bool DVSC1 = false, int POLL = 1>
+// CL > 1: the row is split over CL workgroups (part c of CL owns units
+// [c H / CL, (c + 1) H / CL), NT V == H / CL), and its two LayerNorm-backward
+// row sums are exchanged between them in-launch as tagged granules
+// (cluster_allgather, csrc/cell_fwd_body.h; a.part / a.err, tag = step + 1).
+template <int NT, int V, bool MOD, int DO, bool CHAIN = false, bool DVSC1 = false, int POLL = 1, int CL = 1>
 __device__ __forceinline__ void row_bwd_body(const BwdArgs& a, const int b, const uint32_t* chain_cnt = nullptr,
-                                             uint32_t chain_target = 0, int* chain_err = nullptr) {
+                                             uint32_t chain_target = 0, int* chain_err = nullptr, const int c = 0) {
     static_assert(!CHAIN || V == 4, "chained row: 16-byte slab loads");
     constexpr int NW = NT / 64;
     __shared__ float lds[NW * 8];
-    const int tid = threadIdx.x, H = a.H, u0 = tid * V;
+    __shared__ float mine[8];
+    __shared__ float all[kMaxCluster * 8];
+    const int tid = threadIdx.x, H = a.H, u0 = c * (H / CL) + tid * V;
     const int grp = a.grp_rows > 0 ? b / a.grp_rows : 0;
     const float* ln_g = a.ln_g + grp * 4 * H;
     const float* ln_b = a.ln_b + grp * 4 * H;
@@ -230,6 +254,7 @@ __device__ __forceinline__ void row_bwd_body(const BwdArgs& a, const int b, cons
         s2[1] += dch[j] * cx[j];
     }
     block_sum<2, NW>(s2, lds);
+    if constexpr (CL > 1) row_exchange<2>(s2, mine, all, a.part, a.err, a.step + 1, b, c, CL);
     const float rc = a.rstd[b * 5 + 4];
     const float m1 = s2[0] * invH, m2 = s2[1] * invH;
     // ---- c' = c*f + i*tj*m
@@ -258,6 +283,7 @@ __device__ __forceinline__ void row_bwd_body(const BwdArgs& a, const int b, cons
             acc[4 + q] += dg[q][j] * xh[q][j];
         }
     block_sum<8, NW>(acc, lds);
+    if constexpr (CL > 1) row_exchange<8>(acc, mine, all, a.part + (int64_t)a.B * CL * kSlots, a.err, a.step + 1, b, c, CL);
     st_sv<V>(a.dlncy, ro, a.save_lp, dlc);
     stf<V>(a.dc_rec + ro, dcr);
 #pragma unroll

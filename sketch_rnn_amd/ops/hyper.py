@@ -58,8 +58,31 @@ CHAIN = os.environ.get("SKR_CHAIN", "1") != "0"
 # dvec per workgroup through sc1 loads from the fabric -- another ~10 us,
 # more than the 8 us launch it replaces.
 CHAIN3 = False
-# Debug (tests): NaN-fill the d[h | hh] slabs before every chained launch, so
-# a main-cell row that read them ahead of its producer tiles shows up as NaN.
+# Workgroups per main-cell row in the chained backward launch (1 or 2): 2
+# splits each row's ~300 KB of loads over two CUs and exchanges the two
+# LayerNorm-backward row sums in-launch (csrc/chain_step.hip CL). Tested,
+# 1 by default: measured 24.63 / 24.64 ms/step against 23.91 / 23.89
+# (profiles/r6/chain_fwd_ab.log) -- the two exchanges (each both
+# workgroups' arrival) cost more than the halved per-CU stream saves.
+CHAIN_CL = 1
+# Chained forward step (csrc/hyper_mod.hip skr_hyper_mod_chain): the main
+# LayerNorm cell rows of step t run INSIDE step t's modulation launch -- every
+# workgroup runs its modulation tile, arrives, and the first B * CHAIN_FWD_C
+# then run the main cell over H / CHAIN_FWD_C units of one row (their c_prev
+# and LayerNorm-parameter loads issued before the in-launch wait): three
+# launches per forward step instead of four. Tested (oracle, poison, repeat),
+# OFF: measured on MI355X (same box, A B C A B C, profiles/r6/chain_fwd_ab.log)
+# 24.01 / 24.04 ms/step (C = 2) and 24.23 / 24.26 (C = 1) against 23.91 /
+# 23.89 for the two launches: the chained launch takes 19.75 us per step
+# against 10.5 + 8.8 for the pair -- the grid-wide arrival costs what the
+# kernel boundary did, and the rows cannot keep the faster four-workgroup
+# geometry (B * 4 > the 256 resident modulation workgroups).
+CHAIN_FWD = False
+CHAIN_FWD_C = 2
+CHAIN_FWD_STATS = {"launches": 0}
+# Debug (tests): NaN-fill the d[h | hh] slabs before every chained launch (and
+# g / its partial sums before every chained forward launch), so a main-cell
+# row that read them ahead of its producer tiles shows up as NaN.
 CHAIN_POISON = False
 # The main input projection x W_x + z W_z ([T, B, 4H], the largest tensor the
 # forward writes) stored in bf16 on the fused-modulation path; False keeps it
@@ -327,7 +350,11 @@ class _HyperSeq(torch.autograd.Function):
         am.forget_bias, am.keep = float(forget_bias), float(keep)
         am.seed, am.stream = sd.data_ptr(), int(stream)
         am.ld_lp, am.lp_kind = K, _lp_kind(A)
-        clm = _ClusterSync(T, B, H, dev, ln=mln_on, C=HYPER_MAIN_C if hmod else 0)
+        # chained modulation + main cell (one row block, LayerNorm main cell, no fp8 copy)
+        chain_f = CHAIN_FWD and hmod and mln_on and B <= 128 and T >= 2 and H % max(CHAIN_FWD_C, 1) == 0
+        cf = gemm.ChainCounters(dev, "hyp_fwd_m", T) if chain_f else None
+        clm = _ClusterSync(T, B, H, dev, ln=mln_on,
+                           C=(max(CHAIN_FWD_C, 1) if chain_f else HYPER_MAIN_C) if hmod else 0)
         clh = _ClusterSync(T, B, Hh, dev)
         st = _stream()
         group = gemm.GROUPED and S_m >= 1 and S_y >= 1 and dt == torch.bfloat16
@@ -353,22 +380,41 @@ class _HyperSeq(torch.autograd.Function):
                 rgemm(A[t, :, :H], WhT, RM[rmi(t)], S_m)
                 rgemm(A[t], WyT, RY, S_y)
             _cell_fwd(lib, ah, True, 0, st, "hyper_fwd_step")
-            if hmod:
-                _check(lib.lib.skr_hyper_mod_fwd(A[t + 1, :, H:].data_ptr(), K, PlT.data_ptr(), qb.data_ptr(),
-                                                 XHc[t].data_ptr(), RM[rmi(t)].data_ptr(), B * G, S_m,
-                                                 VEC[t].data_ptr(), GP.data_ptr(), _ptr(RLP[t] if RLP is not None else None),
-                                                 GS.data_ptr(), B, H, Hh, ctypes.byref(xh_dec), st), "hyper_mod_fwd")
-                am.gpre, am.gstats, am.gstat_tiles = GP.data_ptr(), GS.data_ptr(), H // 32
-            elif vbf:
-                gemm.rec_gemm_bf16out(A[t + 1, :, H:], PlT, VEC[t])
-            else:
-                rgemm(A[t + 1, :, H:], PlT, VEC[t].unsqueeze(0), S_v)
             am.xp, am.R, am.vec = XH[t].data_ptr(), RM[rmi(t)].data_ptr(), VEC[t].data_ptr()
             am.r_lp = RLP[t].data_ptr() if (RLP is not None and not hmod) else None
             am.c_prev, am.step = (c0c if t == 0 else CC[t]).data_ptr(), t
             am.h_out = Hout[t].data_ptr()
             _main_saves(am, t)
             am.h_lp, am.c_carry = A[t + 1, :, :H].data_ptr(), CC[t + 1].data_ptr()
+            if hmod:
+                am.gpre, am.gstats, am.gstat_tiles = GP.data_ptr(), GS.data_ptr(), H // 32
+            if chain_f:   # modulation tiles -> this step's main cell rows, one launch
+                if CHAIN_POISON:
+                    GP.fill_(float("nan"))
+                    GS.fill_(float("nan"))
+                rc = lib.lib.skr_hyper_mod_chain(A[t + 1, :, H:].data_ptr(), K, PlT.data_ptr(), qb.data_ptr(),
+                                                 XHc[t].data_ptr(), xh_dec.xh_bf16, RM[rmi(t)].data_ptr(), B * G, S_m,
+                                                 VEC[t].data_ptr(), _ptr(RLP[t] if RLP is not None else None),
+                                                 ctypes.byref(am), ctypes.byref(cf.at(t)), st)
+                if rc == 0:
+                    CHAIN_FWD_STATS["launches"] += 1
+                    continue
+                if rc not in (-2, -3, -4, -8):
+                    _check(rc, "hyper_mod_chain")
+                # shape or residency not taken: two launches from here on (the
+                # counters of launches 0 .. t-1 are cleared for the next sequence;
+                # the cluster buffer keeps its C: the MOD-3 cell takes C = 2 too)
+                chain_f = False
+                cf.buf.zero_()
+            if hmod:
+                _check(lib.lib.skr_hyper_mod_fwd(A[t + 1, :, H:].data_ptr(), K, PlT.data_ptr(), qb.data_ptr(),
+                                                 XHc[t].data_ptr(), RM[rmi(t)].data_ptr(), B * G, S_m,
+                                                 VEC[t].data_ptr(), GP.data_ptr(), _ptr(RLP[t] if RLP is not None else None),
+                                                 GS.data_ptr(), B, H, Hh, ctypes.byref(xh_dec), st), "hyper_mod_fwd")
+            elif vbf:
+                gemm.rec_gemm_bf16out(A[t + 1, :, H:], PlT, VEC[t])
+            else:
+                rgemm(A[t + 1, :, H:], PlT, VEC[t].unsqueeze(0), S_v)
             _cell_fwd(lib, am, mln_on, mod, st, "hyper_main_fwd_step")
         hT = Hout[T - 1].clone()    # no resets: the carried h is h'
         hhT = HH[T - 1].clone()
@@ -481,6 +527,8 @@ class _HyperSeq(torch.autograd.Function):
         # three-stage launches (CHAIN3): dvec P^T inside the chained launch, on
         # the rows' own rotating counters; the bf16 fused-order backward only
         chain3 = chain_m and CHAIN3 and bfuse
+        if chain_m and CHAIN_CL == 2 and not chain3:   # two workgroups per chained row (exchange buffer C = 2)
+            clm = _ClusterSync(T, B, H, dev, ln=s.mln_on, C=2)
         cm3 = gemm.ChainCounters(dev, "hyp_bwd_m3", T - 1) if chain3 else None
         # weight gradients beside the scan (BG_WGRAD): destinations allocated
         # here, on the scan's stream; chunks [t, hi) issued as the scan passes t

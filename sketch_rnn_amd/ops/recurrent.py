@@ -211,6 +211,18 @@ def _fused_ok(H: int, ln: bool, ldt) -> bool:
     return FUSED_ENABLED and not ln and ldt == torch.bfloat16 and H in (256, 512)
 
 
+# Split-K overrides of the per-step products of the LSTM / LayerNorm-LSTM
+# sequence (0: gemm.plan_splits): FWD_SPLITS for h @ W_h (the cell sums the
+# slabs), BWD_SPLITS for dG @ W_h^T (the next cell step sums them; counts up
+# to kRecSlabs = 8 take the unrolled slab loads). A/B: scripts/micro/knob_ab.py.
+FWD_SPLITS = 0
+BWD_SPLITS = 0
+
+
+def _lstm_splits(planned: int, override: int, K: int) -> int:
+    return override if override > 0 and planned > 0 and K % (64 * override) == 0 else planned
+
+
 # =====================================================================================
 # LSTM / LayerNorm-LSTM sequence (nd groups)
 # =====================================================================================
@@ -233,7 +245,7 @@ class _LSTMSeq(torch.autograd.Function):
         else:
             Wl = gemm.lp(W_h.reshape(nd, H, G)).contiguous()   # B^T of the backward product dG @ W^T
             WlT = Wl.transpose(1, 2).contiguous()              # B^T of the forward product h @ W
-        S = gemm.plan_splits(Bg, G, H, nd, ldt)
+        S = _lstm_splits(gemm.plan_splits(Bg, G, H, nd, ldt), FWD_SPLITS, H)
         A = torch.empty(T + 1, BB, H, device=dev, dtype=ldt)   # GEMM operands: carried h
         A[0].copy_(h0)
         CC = torch.empty(T + 1, BB, H, device=dev, dtype=f32)  # carried c
@@ -338,7 +350,7 @@ class _LSTMSeq(torch.autograd.Function):
         dG = torch.empty(T, BB, G, device=dev, dtype=f32)
         lp_on = s.Wl.dtype == torch.bfloat16
         dG_lp = torch.empty(T, BB, G, device=dev, dtype=torch.bfloat16) if lp_on else None
-        S = gemm.plan_splits(B, H, G, nd, s.Wl.dtype)
+        S = _lstm_splits(gemm.plan_splits(B, H, G, nd, s.Wl.dtype), BWD_SPLITS, G)
         DH = torch.zeros(max(S, 1), BB, H, device=dev, dtype=f32)   # split-K slabs of dh into carried h
         if dhT is not None:
             DH[0].copy_(dhT)

@@ -1035,6 +1035,79 @@ def test_hyper_chained_launches_vs_unchained(B, T, fin_w):
         assert e_c <= 1.5 * e_p + 1e-3 * scale, (n, e_c, e_p, scale)
 
 
+@pytest.mark.parametrize("B,T,fin_w", [(100, 7, True), (100, 5, False), (37, 4, True), (128, 3, False), (192, 4, True)])
+def test_hyper_forward_chain_vs_unchained(B, T, fin_w):
+    """csrc/hyper_mod.hip skr_hyper_mod_chain: the main-cell rows of step t
+    inside step t's modulation launch (every workgroup runs its modulation
+    tile, arrives, then B * CHAIN_FWD_C of them run the main cell after an
+    in-launch wait, g and the partial sums read with sc1 loads) against the
+    two-launch path and the fp32 oracle -- outputs, final states, dz and every
+    weight gradient, dropout on. Same arithmetic in another thread layout
+    (row sums in another order), so error(chained) <= 1.5 error(two
+    launches) + 1e-3 of the largest element; the chained path repeats bit for
+    bit; it ran T times for B <= 128 and not at all above (two row blocks)."""
+    from sketch_rnn_amd.ops import hyper
+    p, x, z, st, w = _hyper_setup(5, T, B, 5, 16, 2048, 256, 32, jitter=0.02, state=0.1)
+    runs, launched = {}, {}
+    saved = hyper.CHAIN_FWD
+    try:
+        for name, backend, dt, chain in (("ref", "torch", "fp32", False), ("chain", "hip", "bf16", True),
+                                         ("plain", "hip", "bf16", False), ("chain2", "hip", "bf16", True)):
+            hyper.CHAIN_FWD = chain
+            ops.set_backend(backend)
+            ops.set_compute_dtype(dt)
+            n0 = hyper.CHAIN_FWD_STATS["launches"]
+            runs[name] = _hyper_run(p, x, z, st, w, keep=0.9, hkeep=0.9, fin_w=fin_w)
+            launched[name] = hyper.CHAIN_FWD_STATS["launches"] - n0
+    finally:
+        hyper.CHAIN_FWD = saved
+    assert launched["chain"] == launched["chain2"] == (T if B <= 128 else 0) and launched["plain"] == 0, launched
+    for i, n in enumerate(_names(p)):
+        assert torch.equal(runs["chain"][i], runs["chain2"][i]), n
+        ref = runs["ref"][i].float()
+        scale = max(ref.abs().max().item(), 1e-3)
+        e_c = (runs["chain"][i].float() - ref).abs().max().item()
+        e_p = (runs["plain"][i].float() - ref).abs().max().item()
+        assert e_c <= 1.5 * e_p + 1e-3 * scale, (n, e_c, e_p, scale)
+
+
+@pytest.mark.parametrize("C,B", [(1, 100), (2, 100), (4, 64)])
+def test_hyper_forward_chain_row_split(C, B):
+    """The chained forward with one, two and four workgroups per main-cell row
+    (ops.hyper.CHAIN_FWD_C) against the two-launch path: the first step's
+    output -- no recurrence between them, only the row sums' order differs --
+    within 1e-5 of the largest element; every output and gradient of the
+    4-step sequence against the fp32 oracle as in
+    test_hyper_forward_chain_vs_unchained (later steps see the first step's
+    differences through bf16 roundings of h, amplified by the LayerNorms);
+    and the chained launch ran every step (B C <= 256 workgroups: the
+    launch's grid at H = 2048)."""
+    from sketch_rnn_amd.ops import hyper
+    T = 4
+    p, x, z, st, w = _hyper_setup(6, T, B, 5, 16, 2048, 256, 32, jitter=0.02, state=0.1)
+    saved = hyper.CHAIN_FWD, hyper.CHAIN_FWD_C
+    runs = {}
+    try:
+        for name, backend, dt, chain in (("ref", "torch", "fp32", False), ("plain", "hip", "bf16", False),
+                                         ("chain", "hip", "bf16", True)):
+            hyper.CHAIN_FWD, hyper.CHAIN_FWD_C = chain, C
+            ops.set_backend(backend)
+            ops.set_compute_dtype(dt)
+            n0 = hyper.CHAIN_FWD_STATS["launches"]
+            runs[name] = _hyper_run(p, x, z, st, w, keep=0.9, hkeep=0.9)
+            assert hyper.CHAIN_FWD_STATS["launches"] - n0 == (T if chain else 0)
+    finally:
+        hyper.CHAIN_FWD, hyper.CHAIN_FWD_C = saved
+    o_p, o_c = runs["plain"][0][0], runs["chain"][0][0]
+    assert (o_p - o_c).abs().max().item() <= 1e-5 * o_p.abs().max().item()
+    for i, n in enumerate(_names(p)):
+        ref = runs["ref"][i].float()
+        scale = max(ref.abs().max().item(), 1e-3)
+        e_c = (runs["chain"][i].float() - ref).abs().max().item()
+        e_p = (runs["plain"][i].float() - ref).abs().max().item()
+        assert e_c <= 1.5 * e_p + 1e-3 * scale, (n, e_c, e_p, scale)
+
+
 @pytest.mark.parametrize("B,T,fin_w", [(100, 7, True), (100, 5, False), (37, 4, True), (128, 3, False),
                                        (192, 4, True), (256, 3, False)])
 def test_hyper_three_stage_chain_bitwise(B, T, fin_w):
@@ -1066,27 +1139,64 @@ def test_hyper_three_stage_chain_bitwise(B, T, fin_w):
         assert torch.equal(a, b), n
 
 
+@pytest.mark.parametrize("B,T", [(100, 7), (37, 4), (128, 3), (192, 4)])
+def test_hyper_chained_rows_split_over_two_workgroups(B, T):
+    """ops.hyper.CHAIN_CL = 2: each chained main-cell backward row on two
+    workgroups (waves 4-7 of each end at once; the LayerNorm-backward row
+    sums exchanged in-launch) against one workgroup per row and the fp32
+    oracle: error <= 1.5 x the one-workgroup error + 1e-3 of the largest
+    element for every output and gradient, NaN-poisoned slabs never read
+    early, and bit-identical repeats."""
+    from sketch_rnn_amd.ops import hyper
+    from sketch_rnn_amd.ops.recurrent import ROW_STATS
+    p, x, z, st, w = _hyper_setup(11, T, B, 5, 16, 2048, 256, 32, jitter=0.02, state=0.1)
+    saved = hyper.CHAIN, hyper.CHAIN_CL, hyper.CHAIN_POISON
+    runs = {}
+    try:
+        hyper.CHAIN = True
+        for name, backend, dt, cl, pois in (("ref", "torch", "fp32", 1, False), ("one", "hip", "bf16", 1, False),
+                                            ("two", "hip", "bf16", 2, False), ("two_p", "hip", "bf16", 2, True)):
+            hyper.CHAIN_CL, hyper.CHAIN_POISON = cl, pois
+            ops.set_backend(backend)
+            ops.set_compute_dtype(dt)
+            n0 = ROW_STATS["chain"]
+            runs[name] = _hyper_run(p, x, z, st, w, keep=0.9, hkeep=0.9)
+            if backend == "hip":
+                assert ROW_STATS["chain"] - n0 == T - 1
+    finally:
+        hyper.CHAIN, hyper.CHAIN_CL, hyper.CHAIN_POISON = saved
+    for i, n in enumerate(_names(p)):
+        assert torch.equal(runs["two"][i], runs["two_p"][i]), n
+        ref = runs["ref"][i].float()
+        scale = max(ref.abs().max().item(), 1e-3)
+        e_2 = (runs["two"][i].float() - ref).abs().max().item()
+        e_1 = (runs["one"][i].float() - ref).abs().max().item()
+        assert e_2 <= 1.5 * e_1 + 1e-3 * scale, (n, e_2, e_1, scale)
+
+
 @pytest.mark.parametrize("B,T", [(100, 7), (192, 4)])
 def test_hyper_chained_rows_never_overtake_the_counter(B, T):
     """Poison mode (ops.hyper.CHAIN_POISON): the d[h | hh] slabs (and, for the
     three-stage launch, the dvec rows) are NaN-filled before every chained
     launch, so a main-cell row that read them before its producer tiles had
     written them -- or a dvec P^T tile that read dvec before the rows had --
-    would carry NaN into the gradients. Every output and gradient must be
-    finite and equal to the unpoisoned chained run bit for bit."""
+    would carry NaN into the gradients. The forward chain (ops.hyper.CHAIN_FWD,
+    switched on here) is poisoned the same way: g and its partial sums are
+    NaN-filled before every chained modulation launch. Every output and
+    gradient must be finite and equal to the unpoisoned chained run bit for bit."""
     from sketch_rnn_amd.ops import hyper
     p, x, z, st, w = _hyper_setup(5, T, B, 5, 16, 2048, 256, 32, jitter=0.02, state=0.1)
     ops.set_backend("hip")
     ops.set_compute_dtype("bf16")
-    saved = hyper.CHAIN, hyper.CHAIN_POISON
+    saved = hyper.CHAIN, hyper.CHAIN_POISON, hyper.CHAIN_FWD
     try:
-        hyper.CHAIN = True
+        hyper.CHAIN = hyper.CHAIN_FWD = True
         hyper.CHAIN_POISON = False
         clean = _hyper_run(p, x, z, st, w, keep=0.9, hkeep=0.9)
         hyper.CHAIN_POISON = True
         pois = _hyper_run(p, x, z, st, w, keep=0.9, hkeep=0.9)
     finally:
-        hyper.CHAIN, hyper.CHAIN_POISON = saved
+        hyper.CHAIN, hyper.CHAIN_POISON, hyper.CHAIN_FWD = saved
     for n, a, b in zip(_names(p), clean, pois):
         assert torch.isfinite(b).all(), n
         assert torch.equal(a, b), n

@@ -66,8 +66,8 @@ def test_row_cells_hyper_vae_large_shapes(B, keep, hkeep, monkeypatch):
     T = 7
     p, x, z, st, w = _hyper_setup(6, T, B, 5, 16, 2048, 256, 32, jitter=0.02, state=0.1)
     runs = _arms(lambda: _hyper_run(p, x, z, st, w, keep, hkeep))
-    assert runs["row_launches"] == {"row": 4 * T, "cluster": 0, "chain": 0}, runs["row_launches"]
-    assert runs["cluster_launches"] == {"row": 0, "cluster": 4 * T, "chain": 0}, runs["cluster_launches"]
+    assert runs["row_launches"] == {"row": 4 * T, "cluster": 0, "chain": 0, "chain3": 0}, runs["row_launches"]
+    assert runs["cluster_launches"] == {"row": 0, "cluster": 4 * T, "chain": 0, "chain3": 0}, runs["cluster_launches"]
     _compare(runs, _names(p))
 
 
