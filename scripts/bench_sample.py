@@ -41,6 +41,7 @@ def main():
     ap.add_argument("--host-steps", type=int, default=50, help="strokes timed for the host-loop comparator")
     ap.add_argument("--train-steps", type=int, default=0, help="train this many steps first (synthetic data)")
     ap.add_argument("--no-early-exit", action="store_true")
+    ap.add_argument("--fp8", action="store_true", help="MX-fp8 h W_h in the HyperLSTM step decoder (BASELINE config 5)")
     a = ap.parse_args()
     import numpy as np
     import torch
@@ -69,7 +70,7 @@ def main():
         model = tr.model.eval()
     else:
         model = SketchVAE(cfg, seed=0).cuda().eval()
-    dec = GraphDecoder(model, a.batch, a.steps, a.temperature, early_exit=not a.no_early_exit)
+    dec = GraphDecoder(model, a.batch, a.steps, a.temperature, early_exit=not a.no_early_exit, fp8=a.fp8)
     dec.run(seed=0)  # capture
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -89,7 +90,7 @@ def main():
     host_sps = a.host_steps / hdt
     valid_sps = total_len / wall
     print(json.dumps({"metric": "sampled valid strokes/sec (temperature %.2f)" % a.temperature, "config": a.config,
-                      "dtype": a.dtype, "batch": a.batch, "steps": a.steps, "train_steps": a.train_steps,
+                      "dtype": a.dtype, "fp8_gemm": bool(a.fp8), "batch": a.batch, "steps": a.steps, "train_steps": a.train_steps,
                       "train_cost": train_cost, "early_exit": not a.no_early_exit,
                       "valid_strokes_per_s": round(valid_sps, 1),
                       "decode_positions_per_s": round(total_pos / wall, 1),

@@ -70,6 +70,18 @@ def main():
     print("\nper kernel, mean per step over %d step(s):" % last)
     for n, (c, d) in sorted(agg.items(), key=lambda kv: -kv[1][1])[:40]:
         print("%9.1f us %7.1f x %7.2f us  %s" % (d / last, c / last, d / c, n))
+    # glue: PyTorch's own kernels, runtime copies / fills and library GEMMs
+    # on the step (everything not hand-written in csrc/)
+    kinds = (("at::native", "PyTorch elementwise / reduce / fill / cat"), ("rocclr", "runtime copy / fill"),
+             ("Cijk_", "library GEMM"))
+    print("\nglue per step (kernel time, mean over %d step(s)):" % last)
+    tot = 0.0
+    for key, what in kinds:
+        c = sum(v[0] for n, v in agg.items() if key in n) / last
+        d = sum(v[1] for n, v in agg.items() if key in n) / last
+        tot += d
+        print("%9.1f us %7.1f x  %s (%s)" % (d, c, what, key))
+    print("%9.1f us total" % tot)
 
 
 if __name__ == "__main__":

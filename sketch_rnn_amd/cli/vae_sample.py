@@ -36,6 +36,9 @@ def main(argv=None) -> int:
     p.add_argument("--seed", type=int, default=0)
     p.add_argument("--device", default=None)
     p.add_argument("--device_sampler", action="store_true")
+    p.add_argument("--fp8", action="store_true",
+                   help="device sampler: h W_h of the HyperLSTM decoder as an MX-fp8 GEMM (BASELINE config 5; "
+                        "pays at >= 1024 sketches per call)")
     a = p.parse_args(argv)
     import torch
     from ..ckpt import checkpoint as ckpt
@@ -59,7 +62,7 @@ def main(argv=None) -> int:
     labels = np.full(a.n, a.label if a.mode == "class" else 0)
     sketches = []
     if a.device_sampler and device.startswith("cuda"):
-        dec = GraphDecoder(model, a.n, cfg.max_seq_len, a.temperature, a.greedy)
+        dec = GraphDecoder(model, a.n, cfg.max_seq_len, a.temperature, a.greedy, fp8=a.fp8)
         s, _ = dec.run(seed=a.seed, z=torch.as_tensor(zs, dtype=torch.float32, device=device),
                        labels=torch.as_tensor(labels, device=device))
         sketches = [to_normal_strokes(x) for x in s.cpu().numpy()]

@@ -140,6 +140,10 @@ class _ClusterSync:
     (zeroed once per pass; tags = step + 1 make earlier steps' slots stale)."""
 
     def __init__(self, T: int, BB: int, H: int, device, ln: bool = True, C: int = 0):
+        if C > 0:   # a requested C: at least 256 units per workgroup, every workgroup co-resident
+            C = min(C, max(1, H // 256))
+            while ln and C > 1 and BB * C > _coresident_capacity():
+                C //= 2
         self.C = C if C > 0 else cell_geometry(H, BB, ln)
         self.on = ln and self.C > 1
         if self.on:
@@ -211,16 +215,21 @@ def _fused_ok(H: int, ln: bool, ldt) -> bool:
     return FUSED_ENABLED and not ln and ldt == torch.bfloat16 and H in (256, 512)
 
 
-# Split-K overrides of the per-step products of the LSTM / LayerNorm-LSTM
-# sequence (0: gemm.plan_splits): FWD_SPLITS for h @ W_h (the cell sums the
-# slabs), BWD_SPLITS for dG @ W_h^T (the next cell step sums them; counts up
-# to kRecSlabs = 8 take the unrolled slab loads). A/B: scripts/micro/knob_ab.py.
-FWD_SPLITS = 0
-BWD_SPLITS = 0
+# Split-K of the per-step products of a LayerNorm-LSTM sequence: the planned
+# factor (gemm.plan_splits) capped -- LN_FWD_SPLIT_CAP for h @ W_h (the cell
+# sums the slabs while loading), LN_BWD_SPLIT_CAP for dG @ W_h^T (the next
+# cell step sums them; up to kRecSlabs = 8 take the unrolled slab loads).
+# Measured on vae_layernorm (H = 512; planned 8 / 32; same box, A B A B,
+# profiles/r6/ln_split_ab.log): 10.25 / 10.31 ms/step uncapped, 9.51 / 9.52
+# with the backward at 8, 9.15 / 9.16 with 2 / 8. 0: no cap. Plain LSTM
+# sequences keep the planned factors.
+LN_FWD_SPLIT_CAP = 2
+LN_BWD_SPLIT_CAP = 8
 
 
-def _lstm_splits(planned: int, override: int, K: int) -> int:
-    return override if override > 0 and planned > 0 and K % (64 * override) == 0 else planned
+def _lstm_splits(planned: int, cap: int, K: int) -> int:
+    s = min(planned, cap) if cap > 0 and planned > 0 else planned
+    return s if s > 0 and K % (64 * s) == 0 else planned
 
 
 # =====================================================================================
@@ -245,7 +254,7 @@ class _LSTMSeq(torch.autograd.Function):
         else:
             Wl = gemm.lp(W_h.reshape(nd, H, G)).contiguous()   # B^T of the backward product dG @ W^T
             WlT = Wl.transpose(1, 2).contiguous()              # B^T of the forward product h @ W
-        S = _lstm_splits(gemm.plan_splits(Bg, G, H, nd, ldt), FWD_SPLITS, H)
+        S = _lstm_splits(gemm.plan_splits(Bg, G, H, nd, ldt), LN_FWD_SPLIT_CAP if ln else 0, H)
         A = torch.empty(T + 1, BB, H, device=dev, dtype=ldt)   # GEMM operands: carried h
         A[0].copy_(h0)
         CC = torch.empty(T + 1, BB, H, device=dev, dtype=f32)  # carried c
@@ -350,7 +359,7 @@ class _LSTMSeq(torch.autograd.Function):
         dG = torch.empty(T, BB, G, device=dev, dtype=f32)
         lp_on = s.Wl.dtype == torch.bfloat16
         dG_lp = torch.empty(T, BB, G, device=dev, dtype=torch.bfloat16) if lp_on else None
-        S = _lstm_splits(gemm.plan_splits(B, H, G, nd, s.Wl.dtype), BWD_SPLITS, G)
+        S = _lstm_splits(gemm.plan_splits(B, H, G, nd, s.Wl.dtype), LN_BWD_SPLIT_CAP if ln else 0, G)
         DH = torch.zeros(max(S, 1), BB, H, device=dev, dtype=f32)   # split-K slabs of dh into carried h
         if dhT is not None:
             DH[0].copy_(dhT)

@@ -118,4 +118,4 @@ def test_default_policy_row_kernels_only_in_main_backward():
     ops.set_compute_dtype("bf16")
     before = dict(recurrent.ROW_STATS)
     _hyper_run(p, x, z, st, w)
-    assert {k: recurrent.ROW_STATS[k] - before[k] for k in before} == {"row": 1, "chain": T - 1, "cluster": 3 * T}
+    assert {k: recurrent.ROW_STATS[k] - before[k] for k in before} == {"row": 1, "chain": T - 1, "chain3": 0, "cluster": 3 * T}
