@@ -96,15 +96,11 @@ __device__ __forceinline__ void mod_tile(ModDecode dec, const __hip_bfloat16* __
         if (vec) vec += (int64_t)r0 * 12 * H;
         stats += (int64_t)r0 * 4 * (H / TU) * 2;
     }
-    // one LDS buffer: hh staged for the MFMAs (<= 64 KB), then -- after a
-    // barrier -- the modulation vectors for the epilogue (<= 48 KB): 64 KB in
-    // all, so two workgroups fit one CU (the wide decode's row blocks over
-    // gridDim.z; with two separate arrays the kernel took 112 KB -- and the
-    // compiler 248 VGPRs instead of 130 -- and one workgroup per CU)
-    constexpr int LDSB = MB * HH * 2 > 6 * MB * 16 * 4 ? MB * HH * 2 : 6 * MB * 16 * 4;
-    __shared__ __attribute__((aligned(16))) char hm_lds[LDSB];
-    __hip_bfloat16* sA = (__hip_bfloat16*)hm_lds;
-    float(*sV)[MB][16] = (float(*)[MB][16])hm_lds;
+    // (hh and the modulation vectors in one overlaid 64 KB buffer -- two
+    // workgroups per CU, 130 VGPRs instead of 248 -- measured slower: the wide
+    // decode's launch 64.2 vs 60.9 us, profiles/r6/dec2_kernels_bf16.txt)
+    __shared__ __attribute__((aligned(16))) __hip_bfloat16 sA[MB * HH];     // <= 64 KB
+    __shared__ __attribute__((aligned(16))) float sV[6][MB][16];            // <= 48 KB
     const int u0 = tile * TU, ntile = H / TU;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int fr = lane & 15, fq = lane >> 4;
@@ -171,9 +167,7 @@ __device__ __forceinline__ void mod_tile(ModDecode dec, const __hip_bfloat16* __
         }
     // modulation vectors (+ q) -> bf16 -> LDS: the epilogue needs all three
     // blocks of a unit in one thread. The bf16-rounded value is what the
-    // backward will read, so g is formed from it too. (Every wave's hh reads
-    // are done first: the vectors reuse that LDS.)
-    lds_barrier();
+    // backward will read, so g is formed from it too.
 #pragma unroll
     for (int rt = 0; rt < NRT; ++rt)
 #pragma unroll
