@@ -17,7 +17,10 @@ def main():
                 if not r.get("summary"):
                     runs.append(r)
     arms = sorted({r["arm"] for r in runs})
-    summ = {"summary": True, "commits": sorted({r.get("commit", "unknown") for r in runs}),
+    # commit: a tree identity dict (utils/provenance.py) or an older string label
+    ident = lambda c: json.dumps(c, sort_keys=True) if isinstance(c, dict) else str(c)  # noqa: E731
+    summ = {"summary": True, "commits": [json.loads(c) if c.startswith("{") else c
+                                         for c in sorted({ident(r.get("commit", "unknown")) for r in runs})],
             "config": runs[0]["config"], "steps": runs[0]["steps"],
             "seeds": sorted({r["seed"] for r in runs}), "arms": {}}
     for a in arms:
