@@ -230,7 +230,7 @@ __global__ __launch_bounds__(NT) void wgrad_kernel(const WgArgs g) {
                 for (int j = 0; j < 4; ++j)
                     acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
             if constexpr (CS) {
-                if (wm == 0) {
+                if (wm == 0 && tm == 0) {   // (one tile row sums each column: several would race under acc)
 #pragma unroll
                     for (int j = 0; j < 4; ++j)
 #pragma unroll
@@ -281,7 +281,7 @@ __global__ __launch_bounds__(NT) void wgrad_kernel(const WgArgs g) {
                 }
             }
         if constexpr (CS) {
-            if (wm == 0) {
+            if (wm == 0 && tm == 0) {
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
                     const float v = cs[j] + __shfl_xor(cs[j], 32, 64);
@@ -292,6 +292,242 @@ __global__ __launch_bounds__(NT) void wgrad_kernel(const WgArgs g) {
         }
         if constexpr (!BG) break;
         __syncthreads();   // every wave's LDS reads of this tile are done before the next tile's DMA
+    }
+}
+
+// ---- one wave per SIMD: 4 waves, each 128 x 128 of the 256 x 256 tile ------------------
+// Variant 2 (skr_wgrad_set_variant): bit-identical to the 8-wave kernel and
+// measured SLOWER on every shape of the step (profiles/r6/wgrad_variant_ab.jsonl:
+// dW_h 836-869 vs 776-898 us, dP + colsum 452-456 vs 425-437, dW_y 138-140 vs
+// 131, encoder 126-128 vs 116-117; step 23.97 / 23.99 vs 23.91 / 23.85 ms):
+// a second wave per SIMD covers the LDS-read and barrier latencies better
+// than the cross-K-step fragment pipeline of one wave does.
+// (4 x 4 MFMA 32x32 tiles: 256 accumulators per lane; up to 512 registers per
+// lane at one wave per SIMD). Fragments are software-pipelined across the
+// K-step: half 1's transposed reads are in flight under half 0's MFMAs, and
+// the NEXT K-step's half-0 reads under half 1's -- the ring's barrier sits
+// between the two halves, so the MFMA pipe never waits on a barrier + first
+// LDS read. Same staging (4-stage LDS-DMA ring, XOR-swizzled 512-byte rows),
+// same fragment layout and k order per output element as wgrad_kernel.
+constexpr int NT4 = 256, GPW4 = 8;
+
+struct Frags4 {
+    s16x4 a[4][2], b[4][2];   // [tile][read]: one k16 half
+};
+
+template <int N>
+__device__ __forceinline__ void frag_wait4(Frags4& f) {
+    asm volatile("s_waitcnt lgkmcnt(%16)"
+                 : "+v"(f.a[0][0]), "+v"(f.a[0][1]), "+v"(f.a[1][0]), "+v"(f.a[1][1]), "+v"(f.a[2][0]),
+                   "+v"(f.a[2][1]), "+v"(f.a[3][0]), "+v"(f.a[3][1]), "+v"(f.b[0][0]), "+v"(f.b[0][1]),
+                   "+v"(f.b[1][0]), "+v"(f.b[1][1]), "+v"(f.b[2][0]), "+v"(f.b[2][1]), "+v"(f.b[3][0]),
+                   "+v"(f.b[3][1])
+                 : "n"(N));
+}
+
+// transposed read at base + a compile-time byte offset (the instruction's
+// offset field: no address register per (k half, read) pair)
+template <int OFF>
+__device__ __forceinline__ s16x4 tr_read_at(uint32_t addr) {
+    s16x4 v;
+    asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(v) : "v"(addr), "n"(OFF));
+    return v;
+}
+
+// the 8 reads of one operand for k16 half KS: tile i at base[i]; read rd at
+// +4 rows (row = 16 KS + 8 h + 4 rd + q: the XOR swizzle depends on q only)
+template <int KS>
+__device__ __forceinline__ void read_op4(const uint32_t (&base)[4], s16x4 (&f)[4][2]) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        f[i][0] = tr_read_at<KS * 16 * ROWB>(base[i]);
+        f[i][1] = tr_read_at<KS * 16 * ROWB + 4 * ROWB>(base[i]);
+    }
+}
+
+template <bool CS, bool BG>
+__global__ __launch_bounds__(NT4) __attribute__((amdgpu_waves_per_eu(1, 1))) void wgrad_kernel4(const WgArgs g) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int xcd = blockIdx.x & 7;
+    for (int jx = blockIdx.x >> 3; jx < g.per_xcd; jx += g.stride) {
+        const int lin = xcd * g.per_xcd + jx;
+        if (lin >= g.total) return;
+        const int tiles = g.tiles_m * g.tiles_n;
+        const int t = lin % tiles, zs = lin / tiles;
+        const int split = zs % g.S, z = zs / g.S;
+        const int gsz = 4 * g.tiles_n, grp = t / gsz, fm = grp * 4;
+        const int gm = min(g.tiles_m - fm, 4);
+        const int tm = fm + (t % gsz) % gm, tn = (t % gsz) / gm;
+        const int m0 = tm * TM, n0 = tn * TN;
+        const int64_t k0 = (int64_t)split * g.kslice;
+        const int64_t kend = min(g.K, k0 + g.kslice);
+        const int nk = (int)((kend - k0 + BK - 1) / BK);
+        const int tail = (int)(kend - k0) - (nk - 1) * BK;
+        const __hip_bfloat16* A = g.A + z * g.a_bs;
+        const __hip_bfloat16* B = g.B + z * g.b_bs;
+
+        const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+        // ---- DMA sources: wave w moves tile rows {2w + 8i, 2w + 8i + 1}, i < 4, of A and of B
+        const int hr = lane >> 5, lc = lane & 31;
+        const __hip_bfloat16* asrc[4];
+        const __hip_bfloat16* bsrc[4];
+        int rowk[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int R = 2 * w + 8 * i + hr;
+            rowk[i] = R;
+            const int c = swz(R, lc);
+            asrc[i] = A + m0 + 8 * c;
+            bsrc[i] = B + n0 + 8 * c;
+        }
+        auto issue = [&](int kt) {
+            char* st = smem + (kt % NSTG) * STGB;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int64_t kr = min(k0 + (int64_t)kt * BK + rowk[i], kend - 1);
+                __builtin_amdgcn_global_load_lds((const void*)(asrc[i] + kr * g.lda),
+                                                 (__attribute__((address_space(3))) void*)(st + (2 * w + 8 * i) * ROWB),
+                                                 16, 0, 0);
+                __builtin_amdgcn_global_load_lds((const void*)(bsrc[i] + kr * g.ldb),
+                                                 (__attribute__((address_space(3))) void*)(st + OPB + (2 * w + 8 * i) * ROWB),
+                                                 16, 0, 0);
+            }
+        };
+        // ---- fragment read offsets: wave (wm, wn) owns rows 128 wm.., columns
+        // 128 wn..; per tile the (k half, read) pairs differ by whole rows (the
+        // swizzle depends on row & 3 = q only), folded into the offset field
+        const int wm = w >> 1, wn = w & 1;
+        const int G = lane >> 4, h = G >> 1, q = (lane >> 2) & 3, p = lane & 3;
+        int aoff[4], boff[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int row = 8 * h + q;
+            const int ca = 128 * wm + 32 * i + 16 * (G & 1) + 4 * p;
+            aoff[i] = row * ROWB + (swz(row, ca >> 3) << 4) + 8 * (p & 1);
+            const int cb = 128 * wn + 32 * i + 16 * (G & 1) + 4 * p;
+            boff[i] = OPB + row * ROWB + (swz(row, cb >> 3) << 4) + 8 * (p & 1);
+        }
+        f32x16 acc[4][4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+#pragma unroll
+                for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+        float cs[4] = {0.f, 0.f, 0.f, 0.f};
+        const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)smem;
+        // a half's 16 transposed reads in two groups of 8 (A, then B): the wait
+        // for the previous set is issued between them, so no wait ever needs a
+        // count above lgkmcnt's 4-bit field
+        auto bases = [&](int kt, uint32_t (&ba)[4], uint32_t (&bb)[4]) {
+            const uint32_t st = lds0 + (kt % NSTG) * STGB;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                ba[i] = st + aoff[i];
+                bb[i] = st + boff[i];
+            }
+        };
+        auto mfmas = [&](const Frags4& f) {
+            bf16x8 af[4], bfr[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                af[i] = join(f.a[i]);
+                bfr[i] = join(f.b[i]);
+            }
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+            if constexpr (CS) {
+                if (wm == 0 && tm == 0) {   // (one tile row sums each column: several would race under acc)
+#pragma unroll
+                    for (int j = 0; j < 4; ++j)
+#pragma unroll
+                        for (int e = 0; e < 8; ++e) cs[j] += (float)bfr[j][e];
+                }
+            }
+        };
+        auto zero_tail = [&](char* st) {
+            const int per = (BK - tail) * ROWB / 16;
+            for (int i = tid; i < 2 * per; i += NT4) {
+                const int op = i / per, r = i - op * per;
+                *(int4*)(st + op * OPB + tail * ROWB + 16 * r) = int4{0, 0, 0, 0};
+            }
+        };
+        auto wait_stage = [&](int ahead) {   // this wave's DMAs of the stage `ahead` steps before the newest landed
+            if (ahead >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * GPW4) : "memory");
+            else if (ahead == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GPW4) : "memory");
+            else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        };
+        // ---- prologue: stages 0 .. NSTG-2 in flight; stage 0 visible; its half 0 read
+#pragma unroll
+        for (int s = 0; s < NSTG - 1; ++s)
+            if (s < nk) issue(s);
+        wait_stage(min(nk - 1, NSTG - 2));   // stage 0 landed (stages 1, 2 may fly)
+        __builtin_amdgcn_s_barrier();
+        if (nk == 1 && tail < BK) {
+            zero_tail(smem);
+            skr::lds_barrier();
+        }
+        Frags4 f0, f1;
+        uint32_t ba[4], bb[4];
+        bases(0, ba, bb);
+        read_op4<0>(ba, f0.a);
+        read_op4<0>(bb, f0.b);
+        for (int kt = 0; kt < nk; ++kt) {
+            // stage kt is visible (barrier passed); f0 = its half 0 (in flight)
+            read_op4<1>(ba, f1.a);
+            frag_wait4<8>(f0);            // (LDS reads complete in order: f0 is older than these 8)
+            read_op4<1>(bb, f1.b);
+            mfmas(f0);
+            // stage kt + 1: this wave's DMAs landed (stage kt + 2, if issued, may
+            // still fly), then every wave's; every wave is past its reads of
+            // stage kt - 1, whose buffer the next DMA refills
+            if (kt + 1 < nk) {
+                wait_stage(min(nk - 2 - kt, 1));
+                __builtin_amdgcn_s_barrier();
+                if (kt + NSTG - 1 < nk) issue(kt + NSTG - 1);
+                if (kt + 1 == nk - 1 && tail < BK) {   // the last stage's rows past kend: zeroed before any read
+                    zero_tail(smem + ((kt + 1) % NSTG) * STGB);
+                    skr::lds_barrier();
+                }
+                bases(kt + 1, ba, bb);
+                read_op4<0>(ba, f0.a);
+                frag_wait4<8>(f1);
+                read_op4<0>(bb, f0.b);
+            } else {
+                frag_wait4<0>(f1);
+            }
+            mfmas(f1);
+        }
+        // ---- epilogue (lane: column r; registers: rows (e&3) + 8(e>>2) + 4h)
+        float* C = g.C + z * g.c_bs + (int64_t)split * g.M * g.N;
+        const int r = lane & 31;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int col = n0 + 128 * wn + 32 * j + r;
+#pragma unroll
+                for (int e = 0; e < 16; ++e) {
+                    const int row = m0 + 128 * wm + 32 * i + (e & 3) + 8 * (e >> 2) + 4 * h;
+                    float* c = C + (int64_t)row * g.N + col;
+                    *c = g.acc ? *c + acc[i][j][e] : acc[i][j][e];
+                }
+            }
+        if constexpr (CS) {
+            if (wm == 0 && tm == 0) {
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const float v = cs[j] + __shfl_xor(cs[j], 32, 64);
+                    float* c = g.cs + (int64_t)zs * g.N + n0 + 128 * wn + 32 * j + r;
+                    if (lane < 32) *c = g.acc ? *c + v : v;
+                }
+            }
+        }
+        if constexpr (!BG) break;
+        __syncthreads();
     }
 }
 
@@ -319,10 +555,11 @@ __global__ __launch_bounds__(256) void slab_sum_kernel(const float* __restrict__
 static int g_wgrad_db = 1;   // fragment schedule (DB template argument), skr_wgrad_set_variant
 
 // A/B hook: 1 = both k16 halves' fragments read up front (DB), 0 = per-half,
-// < 0 = leave unchanged. Returns the schedule in force before the call.
+// 2 = the one-wave-per-SIMD kernel (wgrad_kernel4); < 0 = leave unchanged.
+// Returns the schedule in force before the call.
 SKR_API int skr_wgrad_set_variant(int db) {
     const int prev = g_wgrad_db;
-    if (db >= 0) g_wgrad_db = db != 0;
+    if (db >= 0) g_wgrad_db = db > 2 ? 1 : db;
     return prev;
 }
 
@@ -368,6 +605,10 @@ SKR_API int skr_wgrad2(const void* A, int64_t lda, int64_t a_bs, const void* B, 
                              (const void*)wgrad_kernel<false, true, true>, (const void*)wgrad_kernel<true, true, true>};
         for (const void* k : ks)
             if (hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) return -6;
+        const void* k4[4] = {(const void*)wgrad_kernel4<false, false>, (const void*)wgrad_kernel4<true, false>,
+                             (const void*)wgrad_kernel4<false, true>, (const void*)wgrad_kernel4<true, true>};
+        for (const void* k : k4)
+            if (hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) return -6;
         attr = true;
     }
     const bool cs_on = g.cs != nullptr, bg = g.stride < g.per_xcd;
@@ -377,7 +618,16 @@ SKR_API int skr_wgrad2(const void* A, int64_t lda, int64_t a_bs, const void* B, 
         if (bg) hipLaunchKernelGGL((wgrad_kernel<CS_, DB_, true>), gd, bd, lds, s, g);            \
         else hipLaunchKernelGGL((wgrad_kernel<CS_, DB_, false>), gd, bd, lds, s, g);              \
     } while (0)
-    if (g_wgrad_db) {
+    if (g_wgrad_db == 2) {   // one wave per SIMD, fragments pipelined across the K-step
+        const dim3 bd4(NT4);
+        if (bg) {
+            if (cs_on) hipLaunchKernelGGL((wgrad_kernel4<true, true>), gd, bd4, lds, s, g);
+            else hipLaunchKernelGGL((wgrad_kernel4<false, true>), gd, bd4, lds, s, g);
+        } else {
+            if (cs_on) hipLaunchKernelGGL((wgrad_kernel4<true, false>), gd, bd4, lds, s, g);
+            else hipLaunchKernelGGL((wgrad_kernel4<false, false>), gd, bd4, lds, s, g);
+        }
+    } else if (g_wgrad_db) {
         if (cs_on) SKR_WG_LAUNCH(true, true);
         else SKR_WG_LAUNCH(false, true);
     } else {

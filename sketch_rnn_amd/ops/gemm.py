@@ -196,6 +196,12 @@ def _wgrad_hip_ok(a: torch.Tensor, b: torch.Tensor) -> bool:
 
 WGRAD_HIP = True   # False: hipBLASLt weight gradients (tests / A-B)
 WGRAD_SPLIT = {}   # (M, N, batch) -> split-K count override (scripts/bench_wgrad.py sweeps)
+# Weight-gradient kernel schedule (csrc/wgrad_gemm.hip skr_wgrad_set_variant):
+# 1 = 8 waves of 64 x 128, both k16 halves' fragments read up front; 2 = 4
+# waves of 128 x 128, fragments pipelined across the K-step (bit-identical
+# products; measured slower on every step shape, profiles/r6/wgrad_variant_ab.jsonl).
+# None leaves the library's setting.
+WGRAD_KERNEL = None
 
 
 def grad_slot(param: torch.Tensor, shape) -> Optional[torch.Tensor]:
@@ -256,6 +262,8 @@ def _wgrad_splits(tiles: int, K: int) -> int:
 def _wgrad_hip(a, b, colsum, out=None, acc=False, max_grid=0, cs=None):
     from ..utils import native
     lib = native.require_hip()
+    if WGRAD_KERNEL is not None:
+        lib.lib.skr_wgrad_set_variant(int(WGRAD_KERNEL))
     n, K, M = a.shape
     N = b.shape[-1]
     tiles = n * (M // 256) * (N // 256)

@@ -834,7 +834,7 @@ def test_skinny_gemm_f32_matches_torch(M, N, K, nd):
 
 @pytest.mark.parametrize("n,K,M,N,cs,sliced", [(1, 25000, 2048, 8192, False, True), (1, 3001, 256, 2560, True, False),
                                                (2, 1000, 512, 512, False, False), (1, 777, 2304, 1024, True, True)])
-@pytest.mark.parametrize("db", [0, 1])
+@pytest.mark.parametrize("db", [0, 1, 2])
 def test_wgrad_kernel_vs_fp32(n, K, M, N, cs, sliced, db):
     """Hand-written long-K weight-gradient GEMM (csrc/wgrad_gemm.hip) against
     an fp32 product of the same bf16 operands: headline shape (split-free),
@@ -854,7 +854,7 @@ def test_wgrad_kernel_vs_fp32(n, K, M, N, cs, sliced, db):
     assert gemm._wgrad_hip_ok(a, b)
     lib = native.require_hip().lib
     prev = lib.skr_wgrad_set_variant(-1)   # (returns the current fragment schedule)
-    assert lib.skr_wgrad_set_variant(db) in (0, 1)
+    assert lib.skr_wgrad_set_variant(db) in (0, 1, 2)
     try:
         r1 = gemm.wgrad(aa, bb, colsum=cs)
         r2 = gemm.wgrad(aa, bb, colsum=cs)
@@ -874,6 +874,49 @@ def test_wgrad_kernel_vs_fp32(n, K, M, N, cs, sliced, db):
         cerr = float((cs1 - cref).abs().max())
         assert cerr <= 1e-4 * float(cref.abs().max()) + 1e-3, cerr
         assert torch.equal(cs1, cs2)
+
+
+@pytest.mark.parametrize("n,K,M,N,cs,sliced", [(1, 25000, 2048, 8192, False, True), (1, 3001, 256, 2560, True, False),
+                                               (2, 1000, 512, 512, False, False), (1, 777, 2304, 1024, True, True),
+                                               (1, 33, 256, 256, True, False)])
+def test_wgrad_one_wave_kernel_bitwise(n, K, M, N, cs, sliced):
+    """The one-wave-per-SIMD weight-gradient kernel (skr_wgrad_set_variant(2):
+    4 waves of 128 x 128, fragments pipelined across the K-step) against the
+    8-wave kernel (variant 1): the same fragments in the same k order per
+    output element, so bit-identical products and column sums -- split-free,
+    split-K, K tails (K = 33: one full and one 1-row K-step), batched,
+    strided; and the bounded-grid accumulate form (background launches)."""
+    from sketch_rnn_amd.ops import gemm
+    ops.set_backend("hip")
+    ops.set_compute_dtype("bf16")
+    torch.manual_seed(K + 1)
+    dev = torch.device("cuda")
+    if sliced:
+        a = torch.randn(n, K, M + 256, device=dev).to(torch.bfloat16)[:, :, :M]
+    else:
+        a = torch.randn(n, K, M, device=dev).to(torch.bfloat16)
+    b = torch.randn(n, K, N, device=dev).to(torch.bfloat16)
+    aa, bb = (a, b) if n > 1 else (a[0], b[0])
+    lib = native.require_hip().lib
+    prev = lib.skr_wgrad_set_variant(-1)
+    res = {}
+    try:
+        for v in (1, 2):
+            lib.skr_wgrad_set_variant(v)
+            r = gemm.wgrad(aa, bb, colsum=cs)
+            out, c = r if cs else (r, None)
+            acc = out.clone()
+            acc_cs = c.clone() if cs else None
+            gemm.wgrad(aa, bb, colsum=cs, out=acc, cs_out=acc_cs, acc=True, max_grid=16)
+            res[v] = (out, c, acc, acc_cs)
+    finally:
+        lib.skr_wgrad_set_variant(prev)
+    for k in range(4):
+        if res[1][k] is None:
+            continue
+        assert torch.equal(res[1][k], res[2][k]), k
+    scale = float(res[2][0].abs().max())
+    assert torch.allclose(res[2][2], 2 * res[2][0], rtol=1e-5, atol=1e-5 * scale)
 
 
 @pytest.mark.parametrize("Hh,H,E", [(256, 2048, 32), (64, 256, 8)])
