@@ -73,6 +73,38 @@ __global__ __launch_bounds__(512) void chain_bwd_main_kernel(const GemmGroup g, 
 
 static int g_row_poll = 1;
 
+// ---- LayerNorm-LSTM chained steps (ops/recurrent.py) ----------------------------------
+// forward: [h_{t-1} W_h tiles -> R slabs][cell rows of step t]; backward:
+// [dG_{t+1} W_h^T tiles -> dh slabs][cell backward rows of step t]. One row
+// per workgroup: NTR = H / 4 threads (waves past NTR / 64 end at once), every
+// load but the slabs issued before the in-launch wait (row_fwd_body /
+// row_bwd_body CHAIN); the arithmetic of the row kernels (csrc/row_cell.hip).
+template <int NTR, int DS>
+__global__ __launch_bounds__(512) void chain_ln_fwd_kernel(const GemmGroup g, const int nprod, const skr::FwdArgs cell,
+                                                           const ChainSync cs) {
+    extern __shared__ __attribute__((aligned(16))) __hip_bfloat16 smem[];
+    const int id = blockIdx.x;
+    if (id < nprod) {
+        producer_tile<8>(g, cs, smem);
+        return;
+    }
+    if (__builtin_amdgcn_readfirstlane(threadIdx.x) >= NTR) return;   // (wave-uniform)
+    row_fwd_body<NTR, 4, 0, DS, true>(cell, id - nprod, cs.counters + cs.k, (uint32_t)nprod, cs.err);
+}
+
+template <int NTR>
+__global__ __launch_bounds__(512) void chain_ln_bwd_kernel(const GemmGroup g, const int nprod, const skr::BwdArgs cell,
+                                                           const ChainSync cs) {
+    extern __shared__ __attribute__((aligned(16))) __hip_bfloat16 smem[];
+    const int id = blockIdx.x;
+    if (id < nprod) {
+        producer_tile<8>(g, cs, smem);
+        return;
+    }
+    if (__builtin_amdgcn_readfirstlane(threadIdx.x) >= NTR) return;
+    row_bwd_body<NTR, 4, false, 1, true>(cell, id - nprod, cs.counters + cs.k, (uint32_t)nprod, cs.err);
+}
+
 // ---- three-stage launch: + the dvec P^T product of step t ------------------------------
 // [producers: dR_hyp W_y^T of step t + 1] -> [main-cell rows of step t] ->
 // [dvec P^T tiles of step t]. The first nprod2 producer workgroups switch
@@ -339,3 +371,73 @@ SKR_API int skr_chain_set_poll(int p) {
 }
 
 SKR_API int skr_chain_sync_size() { return (int)sizeof(ChainSync); }
+
+// LayerNorm-LSTM forward step chained: probs (all producers) write the R
+// slabs (cell->R, <= 8) the rows of this step sum; rows as skr_row_fwd_step
+// mod 0 with H in {256, 512, 1024, 2048}. Returns -2 / -3 / -4 when not taken.
+SKR_API int skr_chain_ln_fwd(const GemmProblem* probs, int n, const skr::FwdArgs* cell, const ChainSync* cs,
+                             hipStream_t s) {
+    if (cell == nullptr || check_sync(cs)) return -6;
+    const skr::FwdArgs& a = *cell;
+    if (a.B <= 0) return 0;
+    if (a.H % 256 != 0 || a.H > 2048 || a.R_nslab < 1 || a.R_nslab > 8 || a.grp_rows > 0) return -2;
+    const int rc = row_fwd_check(a, 0);
+    if (rc) return rc;
+    GemmGroup g;
+    const int np = build_group(probs, n, n, g);
+    if (np < 0) return np;
+    const int ntr = a.H / 4, ds = a.R_nslab <= 1 ? 1 : a.R_nslab <= 2 ? 2 : a.R_nslab <= 4 ? 4 : 8;
+    const void* k = nullptr;
+#define SKR_CLF(NTR_, DS_) if (ntr == NTR_ && ds == DS_) k = (const void*)chain_ln_fwd_kernel<NTR_, DS_>;
+#define SKR_CLF_DS(NTR_) SKR_CLF(NTR_, 1) SKR_CLF(NTR_, 2) SKR_CLF(NTR_, 4) SKR_CLF(NTR_, 8)
+    SKR_CLF_DS(64) SKR_CLF_DS(128) SKR_CLF_DS(256) SKR_CLF_DS(512)
+#undef SKR_CLF_DS
+#undef SKR_CLF
+    if (k == nullptr) return -2;
+    static const void* attr_done[16];
+    static int n_attr = 0;
+    bool done = false;
+    for (int i = 0; i < n_attr; ++i) done |= attr_done[i] == k;
+    if (!done && n_attr < 16) {
+        (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLds);
+        attr_done[n_attr++] = k;
+    }
+    int npv = np;
+    void* args[] = {(void*)&g, (void*)&npv, (void*)&a, (void*)cs};
+    if (hipLaunchKernel(k, dim3(np + a.B), dim3(512), args, kLds, s) != hipSuccess) return -1;
+    return SKR_CHECK_LAUNCH();
+}
+
+// LayerNorm-LSTM backward step chained: probs (all producers) write the dh_rec
+// slabs (cell->dh_rec, <= 8) of this step's rows; rows as skr_row_bwd_step
+// mod 0 with a single dh_out slab (or none).
+SKR_API int skr_chain_ln_bwd(const GemmProblem* probs, int n, const skr::BwdArgs* cell, const ChainSync* cs,
+                             hipStream_t s) {
+    if (cell == nullptr || check_sync(cs)) return -6;
+    const skr::BwdArgs& a = *cell;
+    if (a.B <= 0) return 0;
+    if (a.H % 256 != 0 || a.H > 2048 || a.dh_rec == nullptr || a.dhr_nslab < 1 || a.dhr_nslab > 8 ||
+        a.dh_rec2 != nullptr || a.grp_rows > 0)
+        return -2;
+    if (a.dh_out && a.dho_nslab != 1) return -2;
+    const int rc = row_bwd_check(a, 0);
+    if (rc) return rc;
+    GemmGroup g;
+    const int np = build_group(probs, n, n, g);
+    if (np < 0) return np;
+    const int ntr = a.H / 4;
+    const void* k = ntr == 64 ? (const void*)chain_ln_bwd_kernel<64> : ntr == 128 ? (const void*)chain_ln_bwd_kernel<128>
+                  : ntr == 256 ? (const void*)chain_ln_bwd_kernel<256> : (const void*)chain_ln_bwd_kernel<512>;
+    static const void* attr_done[4];
+    static int n_attr = 0;
+    bool done = false;
+    for (int i = 0; i < n_attr; ++i) done |= attr_done[i] == k;
+    if (!done && n_attr < 4) {
+        (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLds);
+        attr_done[n_attr++] = k;
+    }
+    int npv = np;
+    void* args[] = {(void*)&g, (void*)&npv, (void*)&a, (void*)cs};
+    if (hipLaunchKernel(k, dim3(np + a.B), dim3(512), args, kLds, s) != hipSuccess) return -1;
+    return SKR_CHECK_LAUNCH();
+}

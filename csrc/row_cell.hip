@@ -30,127 +30,10 @@ namespace {
 
 using namespace skr;
 
-// ---- forward -------------------------------------------------------------------------
-// MOD 0: g = xp + sum of the R slabs (LN-LSTM / hyper cell; DS = compile-time
-// slab ceiling); MOD 3: g = gpre with the gate statistics summed from gstats
-// (HyperLSTM main cell).
+// ---- forward / backward step kernels (bodies: csrc/row_cell.h) -----------------------
 template <int NT, int V, int MOD, int DS>
 __global__ __launch_bounds__(NT) void row_fwd(const FwdArgs a) {
-    constexpr int NW = NT / 64;
-    __shared__ float lds[NW * 8];
-    const int b = blockIdx.x, tid = threadIdx.x, H = a.H, u0 = tid * V;
-    const int grp = a.grp_rows > 0 ? b / a.grp_rows : 0;
-    const float* ln_g = a.ln_g + grp * 4 * H;
-    const float* ln_b = a.ln_b + grp * 4 * H;
-    const int64_t ro = (int64_t)b * H + u0;
-    const bool save = a.xhat != nullptr;
-    const float invH = 1.0f / (float)H;
-    const bool keep_on = a.keep < 1.0f;
-    const uint32_t key = keep_on ? hash_key(*a.seed, a.stream, a.step) : 0u;
-
-    // ---- every load up front
-    float g[4][V], lg[4][V], lb[4][V], cp[V], lcg[V], lcb[V];
-    float rt[MOD == 0 ? 4 : 1][DS][V];
-    const int nr = min(a.R_nslab, DS);
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        if constexpr (MOD == 3) {
-            ldf<V>(a.gpre + (int64_t)b * 4 * H + q * H + u0, g[q]);
-        } else {
-            ldf<V>(a.xp + b * a.ld_xp + q * H + u0, g[q]);
-            load_slabs<V, DS>(a.R + b * a.ld_R + q * H + u0, nr, a.R_slab, rt[q]);
-        }
-        ldf<V>(ln_g + q * H + u0, lg[q]);
-        ldf<V>(ln_b + q * H + u0, lb[q]);
-    }
-    ldf<V>(a.c_prev + ro, cp);
-    ldf<V>(a.lnc_g + grp * H + u0, lcg);
-    ldf<V>(a.lnc_b + grp * H + u0, lcb);
-    if constexpr (MOD == 0) {
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            fold_slabs<V, DS>(rt[q], nr, g[q]);
-            if (a.R_nslab > DS) add_slabs<V>(a.R + DS * a.R_slab + b * a.ld_R + q * H + u0, a.R_nslab - DS, a.R_slab, g[q]);
-        }
-    }
-
-    // ---- LayerNorm statistics of the four gate blocks
-    float s[8];
-    if constexpr (MOD == 3) {
-#pragma unroll
-        for (int q = 0; q < 8; ++q) s[q] = 0.f;
-        const float* gs = a.gstats + (int64_t)b * 4 * a.gstat_tiles * 2;
-        for (int i = tid; i < 4 * a.gstat_tiles; i += NT) {
-            const int gq = i / a.gstat_tiles;
-            const float v0 = gs[2 * i], v1 = gs[2 * i + 1];
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                s[q] += q == gq ? v0 : 0.f;
-                s[4 + q] += q == gq ? v1 : 0.f;
-            }
-        }
-    } else {
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            s[q] = 0.f;
-            s[4 + q] = 0.f;
-#pragma unroll
-            for (int j = 0; j < V; ++j) {
-                s[q] += g[q][j];
-                s[4 + q] += g[q][j] * g[q][j];
-            }
-        }
-    }
-    block_sum<8, NW>(s, lds);
-    float rs[4], xs[4][V];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        const float mean = s[q] * invH;
-        const float var = fmaxf(s[4 + q] * invH - mean * mean, 0.f);
-        rs[q] = rsqrtf(var + kLnEps);
-#pragma unroll
-        for (int j = 0; j < V; ++j) {
-            xs[q][j] = (g[q][j] - mean) * rs[q];
-            g[q][j] = xs[q][j] * lg[q][j] + lb[q][j];
-        }
-    }
-    // ---- cell
-    float cn[V], og[V], s2[2] = {0.f, 0.f};
-#pragma unroll
-    for (int j = 0; j < V; ++j) {
-        const float i = cell_sig(g[0][j]);
-        const float tj = cell_tanh(g[1][j]);
-        const float f = cell_sig(g[2][j] + a.forget_bias);
-        og[j] = cell_sig(g[3][j]);
-        const float m = dropout_mult(keep_on, key, ro + j, a.keep);
-        cn[j] = cp[j] * f + i * tj * m;
-        s2[0] += cn[j];
-        s2[1] += cn[j] * cn[j];
-    }
-    block_sum<2, NW>(s2, lds);
-    const float mean = s2[0] * invH;
-    const float var = fmaxf(s2[1] * invH - mean * mean, 0.f);
-    const float rc = rsqrtf(var + kLnEps);
-    float ch[V], h[V];
-#pragma unroll
-    for (int j = 0; j < V; ++j) {
-        ch[j] = (cn[j] - mean) * rc;
-        h[j] = cell_tanh(ch[j] * lcg[j] + lcb[j]) * og[j];
-    }
-    // ---- stores
-    if (save) {
-        if (tid < 4) a.rstd[b * 5 + tid] = pick<4>(rs, tid);
-        if (tid == 0) a.rstd[b * 5 + 4] = rc;
-        st_sv<V>(a.chat, ro, a.save_lp, ch);
-#pragma unroll
-        for (int q = 0; q < 4; ++q) st_sv<V>(a.xhat, (int64_t)b * 4 * H + q * H + u0, a.save_lp, xs[q]);
-    }
-    stf<V>(a.h_out + ro, h);
-    if (a.h_carry != nullptr) stf<V>(a.h_carry + ro, h);
-    if (a.c_out != nullptr) stf<V>(a.c_out + ro, cn);
-    stf<V>(a.c_carry + ro, cn);
-    if (a.lp_kind == 1) stb<V>((__hip_bfloat16*)a.h_lp + b * a.ld_lp + u0, h);
-    else stf<V>((float*)a.h_lp + b * a.ld_lp + u0, h);
+    row_fwd_body<NT, V, MOD, DS>(a, blockIdx.x);
 }
 
 template <int NT, int V, bool MOD, int DO>
@@ -202,14 +85,8 @@ SKR_API int skr_row_fwd_step(const FwdArgs* args, int mod, hipStream_t s) {
     const FwdArgs& a = *args;
     if (a.B <= 0) return 0;
     if (skr_row_supported(a.H) != 0) return -2;
-    if (a.reset != nullptr || (mod != 0 && mod != 3) || (a.lp_kind != 1 && a.lp_kind != 2)) return -3;
-    if (mod == 3 && (a.gpre == nullptr || a.gstats == nullptr || a.gstat_tiles < 1)) return -3;
-    if (mod == 0 && (a.xp == nullptr || a.R == nullptr || a.R_nslab < 1)) return -3;
-    if (!al16(a.xp) || !al16(a.R) || !al16(a.gpre) || !al16(a.c_prev) || !al16(a.h_out) || !al16(a.c_carry) ||
-        !al16(a.h_lp) || !al16(a.xhat) || !al16(a.chat) || !al16(a.c_out) || !al16(a.h_carry) || !al16(a.ln_g) ||
-        !al16(a.ln_b) || !al16(a.lnc_g) || !al16(a.lnc_b))
-        return -4;
-    if (!mul8(a.ld_xp) || !mul8(a.ld_R) || !mul8(a.R_slab) || !mul8(a.ld_lp)) return -4;
+    const int rc = row_fwd_check(a, mod);
+    if (rc) return rc;
     const int v = pick_v(a.H), nt = a.H / v;
     KernelT<FwdArgs> k = nullptr;
     if (mod == 3) k = fwd_kernel<3, 1>(nt, v);

@@ -597,6 +597,34 @@ def chain_bwd_main3(producers, tail, cell_args, sync, rows_sync) -> int:
     return rc
 
 
+def chain_ln_fwd(producers, cell_args, sync) -> int:
+    """One launch: ``producers`` writing the R slabs of a LayerNorm-LSTM step
+    and that step's forward cell rows (``skr_chain_ln_fwd``). Returns the
+    library code: -2 / -3 / -4 mean "shape not taken"."""
+    import ctypes
+    from ..utils import native
+    lib = native.require_hip()
+    rc = lib.lib.skr_chain_ln_fwd(_problems(producers), len(producers), ctypes.byref(cell_args), ctypes.byref(sync),
+                                  torch.cuda.current_stream().cuda_stream)
+    if rc not in (0, -2, -3, -4):
+        raise RuntimeError("skr_chain_ln_fwd failed (%d)" % rc)
+    return rc
+
+
+def chain_ln_bwd(producers, cell_args, sync) -> int:
+    """One launch: ``producers`` writing the dh slabs of a LayerNorm-LSTM
+    backward step and that step's cell backward rows (``skr_chain_ln_bwd``).
+    Returns the library code: -2 / -3 / -4 mean "shape not taken"."""
+    import ctypes
+    from ..utils import native
+    lib = native.require_hip()
+    rc = lib.lib.skr_chain_ln_bwd(_problems(producers), len(producers), ctypes.byref(cell_args), ctypes.byref(sync),
+                                  torch.cuda.current_stream().cuda_stream)
+    if rc not in (0, -2, -3, -4):
+        raise RuntimeError("skr_chain_ln_bwd failed (%d)" % rc)
+    return rc
+
+
 # ---- inference-time helpers ------------------------------------------------------------
 _WCACHE = {}
 WEIGHTS_EPOCH = [0]

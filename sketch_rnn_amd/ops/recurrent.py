@@ -225,6 +225,15 @@ def _fused_ok(H: int, ln: bool, ldt) -> bool:
 # sequences keep the planned factors.
 LN_FWD_SPLIT_CAP = 2
 LN_BWD_SPLIT_CAP = 8
+# Chained LayerNorm-LSTM steps (csrc/chain_step.hip skr_chain_ln_fwd / _bwd):
+# the cell rows of a step run INSIDE the launch of the product that feeds
+# them (forward: h_{t-1} W_h; backward: dG_{t+1} W_h^T), with every operand
+# but the slabs loaded before an in-launch wait -- one launch per step each
+# way instead of two. LN_CHAIN_POISON (tests): NaN-fill the slabs before
+# every chained launch, so a row reading ahead of its producers shows.
+LN_CHAIN = True
+LN_CHAIN_POISON = False
+LN_CHAIN_STATS = {"fwd": 0, "bwd": 0}
 
 
 def _lstm_splits(planned: int, cap: int, K: int) -> int:
@@ -311,9 +320,13 @@ class _LSTMSeq(torch.autograd.Function):
         else:
             T_loop = T
         cl = _ClusterSync(T, BB, H, dev, ln)
+        # chained steps: one launch per step (product tiles + cell rows)
+        chain_f = LN_CHAIN and ln and nd == 1 and rst is None and ldt == torch.bfloat16 and dev.type == "cuda" \
+            and T_loop > 0 and H % 256 == 0 and H <= 2048 and 1 <= S <= 8
+        cf = gemm.ChainCounters(dev, "ln_fwd", T) if chain_f else None
+        WlT2 = WlT if WlT.dim() == 2 else WlT[0]
         for t in range(T_loop):
             cl.set(a, t)
-            gemm.rec_gemm(A[t], WlT, R, S, nd)
             a.xp = xp[t].data_ptr()
             a.c_prev = CC[t].data_ptr()
             a.reset = _ptr(rst[t]) if rst is not None else None
@@ -326,6 +339,15 @@ class _LSTMSeq(torch.autograd.Function):
             a.h_carry = HC[t % 2].data_ptr() if HC is not None else None
             a.h_lp = A[t + 1].data_ptr()
             a.c_carry = CC[t + 1].data_ptr()
+            if chain_f:
+                if LN_CHAIN_POISON:
+                    R.fill_(float("nan"))
+                if gemm.chain_ln_fwd([(A[t], WlT2, R, S)], a, cf.at(t)) == 0:
+                    LN_CHAIN_STATS["fwd"] += 1
+                    continue
+                chain_f = False   # shape not taken: two launches from here on (counters cleared)
+                cf.buf.zero_()
+            gemm.rec_gemm(A[t], WlT, R, S, nd)
             _cell_fwd(lib, a, ln, 0, st, "lstm_fwd_step")
         if T == 0:
             hT = h0.clone()
@@ -406,6 +428,10 @@ class _LSTMSeq(torch.autograd.Function):
         else:
             T_loop = T
         cl = _ClusterSync(T, BB, H, dev, ln)
+        # chained steps: the cell rows of step t inside the dG_{t+1} W_h^T launch
+        chain_b = LN_CHAIN and ln and nd == 1 and s.reset is None and lp_on and dev.type == "cuda" \
+            and T_loop >= 2 and H % 256 == 0 and H <= 2048 and 1 <= S <= 8
+        cb = gemm.ChainCounters(dev, "ln_bwd", T - 1) if chain_b else None
         for t in range(T_loop - 1, -1, -1):
             cl.set(a, t)
             a.dh_out = dHout[t].data_ptr() if dHout is not None else None
@@ -419,8 +445,21 @@ class _LSTMSeq(torch.autograd.Function):
             a.step = t
             a.dG = dG[t].data_ptr()
             a.dG_lp = dG_lp[t].data_ptr() if lp_on else None
-            _cell_bwd(lib, a, ln, 0, st, "lstm_bwd_step")
-            gemm.rec_gemm(dG_lp[t] if lp_on else dG[t], s.Wl, DH, S, nd)
+            ran = False
+            if chain_b and t < T - 1:   # dG_{t+1} W_h^T -> this step's rows, one launch
+                if LN_CHAIN_POISON:
+                    DH.fill_(float("nan"))
+                ran = gemm.chain_ln_bwd([(dG_lp[t + 1], s.Wl[0], DH, S)], a, cb.at(T - 2 - t)) == 0
+                if ran:
+                    LN_CHAIN_STATS["bwd"] += 1
+                else:   # shape not taken: unchained from here on (counters cleared)
+                    chain_b = False
+                    cb.buf.zero_()
+                    gemm.rec_gemm(dG_lp[t + 1], s.Wl, DH, S, nd)
+            if not ran:
+                _cell_bwd(lib, a, ln, 0, st, "lstm_bwd_step")
+            if not chain_b or t == 0:   # (chained: runs in the next step's launch)
+                gemm.rec_gemm(dG_lp[t] if lp_on else dG[t], s.Wl, DH, S, nd)
         dh_rec = DH.sum(0) if DH.shape[0] > 1 else DH[0]
         dGs = dG_lp if lp_on else dG
         if nd == 1:

@@ -123,6 +123,57 @@ def test_bilstm_sequence_matches_oracle(H, ln, keep):
     _close(g_h, g_t, 1e-3, 1e-4, "grad")
 
 
+@pytest.mark.parametrize("H,B,T,keep", [(512, 100, 9, 0.9), (256, 37, 6, 1.0), (2048, 64, 4, 0.9), (512, 128, 3, 0.8)])
+def test_ln_lstm_chained_steps(H, B, T, keep):
+    """ops.recurrent.LN_CHAIN (csrc/chain_step.hip skr_chain_ln_fwd / _bwd):
+    the LayerNorm-LSTM cell rows of each step inside the launch of the
+    product that feeds them, against the two-launch path and the fp32 oracle
+    -- outputs, final states and every gradient, dropout on: error <= 1.5 x
+    the two-launch error + 1e-3 of the largest element; NaN-poisoned slabs
+    (a row reading ahead of its producer tiles) must not change a bit; the
+    chained launches ran T times forward and T - 1 backward."""
+    from sketch_rnn_amd.ops import recurrent
+    torch.manual_seed(H + B)
+    xp = torch.randn(T, B, 4 * H, device=DEV, requires_grad=True)
+    W = (torch.randn(H, 4 * H, device=DEV) / math.sqrt(H)).requires_grad_()
+    h0 = (torch.randn(B, H, device=DEV) * 0.5).requires_grad_()
+    c0 = (torch.randn(B, H, device=DEV) * 0.5).requires_grad_()
+    lnp = [torch.randn(4 * H, device=DEV).mul(0.1).add(1).requires_grad_(),
+           torch.randn(4 * H, device=DEV).mul(0.1).requires_grad_(),
+           torch.randn(H, device=DEV).mul(0.1).add(1).requires_grad_(),
+           torch.randn(H, device=DEV).mul(0.1).requires_grad_()]
+    seed = torch.tensor([23], device=DEV)
+
+    def fn(xp, W, h0, c0, *lnp):
+        out, (hT, cT) = ops.lstm_sequence(xp, W, h0, c0, drop_keep=keep, drop_seed=seed, drop_stream=5, ln=tuple(lnp))
+        return [out, hT, cT]
+
+    inputs = [xp, W, h0, c0] + lnp
+    saved = recurrent.LN_CHAIN, recurrent.LN_CHAIN_POISON
+    res = {}
+    try:
+        for name, backend, dt, chain, pois in (("ref", "torch", "fp32", False, False), ("plain", "hip", "bf16", False, False),
+                                               ("chain", "hip", "bf16", True, False), ("chain_p", "hip", "bf16", True, True)):
+            recurrent.LN_CHAIN, recurrent.LN_CHAIN_POISON = chain, pois
+            ops.set_compute_dtype(dt)
+            n0 = dict(recurrent.LN_CHAIN_STATS)
+            o, g = _run(backend, fn, inputs)
+            res[name] = o + g
+            if chain:
+                assert recurrent.LN_CHAIN_STATS["fwd"] - n0["fwd"] == T
+                assert recurrent.LN_CHAIN_STATS["bwd"] - n0["bwd"] == T - 1
+    finally:
+        recurrent.LN_CHAIN, recurrent.LN_CHAIN_POISON = saved
+        ops.set_compute_dtype("fp32")
+    for i, (c, cp, p_, r) in enumerate(zip(res["chain"], res["chain_p"], res["plain"], res["ref"])):
+        assert torch.isfinite(cp).all(), i
+        assert torch.equal(c, cp), i
+        scale = max(r.abs().max().item(), 1e-3)
+        e_c = (c.float() - r).abs().max().item()
+        e_p = (p_.float() - r).abs().max().item()
+        assert e_c <= 1.5 * e_p + 1e-3 * scale, (i, e_c, e_p, scale)
+
+
 def test_lstm_sequence_bf16_close():
     torch.manual_seed(1)
     T, B, H = 9, 8, 512

@@ -72,9 +72,10 @@ def test_row_cells_hyper_vae_large_shapes(B, keep, hkeep, monkeypatch):
 
 
 @pytest.mark.parametrize("H,nd,B,keep", [(512, 1, 100, 0.9), (256, 2, 100, 1.0), (1024, 1, 24, 0.85)])
-def test_row_cells_layernorm_lstm(H, nd, B, keep):
+def test_row_cells_layernorm_lstm(H, nd, B, keep, monkeypatch):
     """LayerNorm-LSTM sequences (the vae_layernorm decoder, a bidirectional LN
     encoder with per-direction LayerNorm parameters) through the row kernels."""
+    monkeypatch.setattr(recurrent, "LN_CHAIN", False)   # (the chained steps: test_kernels_gpu.py)
     torch.manual_seed(1)
     T = 9
     xs = [torch.randn(T, B, 4 * H, device=DEV) for _ in range(nd)]
