@@ -134,4 +134,91 @@ __device__ __forceinline__ void glds_mma(const __hip_bfloat16* __restrict__ A, i
     }
 }
 
+// A-in-registers variant (RA): each wave reads ITS OWN rows of A (rows
+// 32 (w % 4) .. + 31; no other wave needs them) straight into MFMA fragment
+// registers with 16-byte global loads -- A[row][k 8 fq .. +7] is the
+// fragment, contiguous in memory -- NS - 1 stages ahead in an NS-deep
+// register ring; only B (shared by the waves) goes through the LDS-DMA ring
+// (BN x BK per stage: 8 KiB at BN = 64). Same fragments, same k order per
+// output element as glds_mma: bit-identical accumulators. Measured SLOWER
+// (ops.gemm.SKINNY_RA; profiles/r6/skinny_ra_ab.log: vae_large 25.47 / 25.47
+// ms/step at depth 3, 25.59 at 6, against 24.00 / 23.99): the LDS-DMA ring
+// is not the bottleneck of these tiles -- it streams 84 GB/s per CU from an
+// L2- or Infinity-Cache-resident footprint (scripts/micro/l2_rate.hip,
+// profiles/r6/l2_rate.jsonl) -- and the register loads put their latency
+// in front of every stage's MFMAs.
+template <int BN, int NS, int NW = 4>
+__device__ __forceinline__ void ra_mma(const __hip_bfloat16* __restrict__ A, int64_t lda,
+                                       const __hip_bfloat16* __restrict__ Bt, int64_t ldb, int M, int n0,
+                                       int64_t k0, int kslice, __hip_bfloat16* smem,
+                                       f32x4_t (&acc)[2][glds_nj<BN, NW>()]) {
+    constexpr int NJ = glds_nj<BN, NW>();
+    constexpr int B_CH = BN / 8;                    // 1-KiB chunks (8 rows) of B per stage
+    static_assert((NW == 4 || NW == 8) && B_CH % NW == 0, "ra_mma: wave layout");
+    constexpr int GPWB = B_CH / NW;
+    constexpr int GPW = GPWB + 4;                   // VMEM instructions per wave per stage (4 A fragment loads)
+    constexpr int TILE = BN * BK;                   // bf16 elements per LDS stage (B only)
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int wr = w % 4, wc = w / 4;
+    const int n = kslice / BK;
+    const int fr = lane & 15, fq = lane >> 4;
+    const int r8 = lane >> 3, slot = lane & 7;
+    const __hip_bfloat16* bsrc[GPWB];
+#pragma unroll
+    for (int i = 0; i < GPWB; ++i) {
+        const int row = (w + NW * i) * 8 + r8;
+        const int kc = slot ^ ((row >> 1) & 7);
+        bsrc[i] = Bt + (int64_t)(n0 + row) * ldb + k0 + kc * 8;
+    }
+    const __hip_bfloat16* arow[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) arow[i] = A + (int64_t)min(32 * wr + 16 * i + fr, M - 1) * lda + k0 + 8 * fq;
+    bf16x8_t ar[NS][2][2];                          // [register stage][row tile][k32 half]
+    auto issue = [&](int kt, bf16x8_t (&dst)[2][2]) {
+        const int64_t ko = (int64_t)kt * BK;
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int h = 0; h < 2; ++h) dst[i][h] = *(const bf16x8_t*)(arow[i] + ko + 32 * h);
+        __hip_bfloat16* st = smem + (kt % NS) * TILE;
+#pragma unroll
+        for (int i = 0; i < GPWB; ++i)
+            __builtin_amdgcn_global_load_lds((const void*)(bsrc[i] + ko),
+                                             (__attribute__((address_space(3))) void*)(st + (w + NW * i) * 512), 16, 0, 0);
+    };
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int p = 0; p < NS - 1; ++p)
+        if (p < n) issue(p, ar[p]);
+    for (int kb = 0; kb < n; kb += NS) {
+#pragma unroll
+        for (int u = 0; u < NS; ++u) {              // stage kt = kb + u: register set u, LDS buffer u
+            const int kt = kb + u;
+            if (kt >= n) break;
+            wait_ahead<GPW, NS>(min(n - 1 - kt, NS - 2));
+            __builtin_amdgcn_s_barrier();           // B of stage kt landed for every wave; buffer (kt-1) % NS is free
+            if (kt + NS - 1 < n) issue(kt + NS - 1, ar[(u + NS - 1) % NS]);
+            const __hip_bfloat16* Bs = smem + u * TILE;
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int kc = 4 * h + fq;
+                bf16x8_t bfr[NJ];
+#pragma unroll
+                for (int j = 0; j < NJ; ++j) {
+                    const int row = 16 * (wc * NJ + j) + fr;
+                    bfr[j] = *(const bf16x8_t*)(&Bs[row * BK + ((kc ^ ((row >> 1) & 7)) * 8)]);
+                }
+#pragma unroll
+                for (int i = 0; i < 2; ++i)
+#pragma unroll
+                    for (int j = 0; j < NJ; ++j)
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ar[u][i][h], bfr[j], acc[i][j], 0, 0, 0);
+            }
+        }
+    }
+}
+
 }  // namespace skr

@@ -34,14 +34,14 @@ using skr::BM;
 using skr::BK;
 using skr::wait_ahead;
 
-template <int BN, int NS, bool CBF16 = false>
+template <int BN, int NS, bool CBF16 = false, bool RA = false>
 __global__ __launch_bounds__(256) void skinny_gemm_glds_kernel(
     const __hip_bfloat16* __restrict__ A, int64_t lda, int64_t a_batch,
     const __hip_bfloat16* __restrict__ Bt, int64_t ldb, int64_t b_batch,
     void* __restrict__ C, int64_t ldc, int64_t c_slab, int64_t c_batch, int M, int kslice) {
     extern __shared__ __attribute__((aligned(16))) __hip_bfloat16 smem[];
     const int64_t co = blockIdx.z * c_batch + blockIdx.y * c_slab;
-    glds_tile<BN, NS, CBF16>(A + blockIdx.z * a_batch, lda, Bt + blockIdx.z * b_batch, ldb,
+    glds_tile<BN, NS, CBF16, 4, false, RA>(A + blockIdx.z * a_batch, lda, Bt + blockIdx.z * b_batch, ldb,
                   CBF16 ? (void*)((__hip_bfloat16*)C + co) : (void*)((float*)C + co), ldc, M, blockIdx.x * BN,
                   (int64_t)blockIdx.y * kslice, kslice, smem);
 }
@@ -56,10 +56,10 @@ __global__ __launch_bounds__(256) void skinny_gemm_glds_kernel(
 // sums `start` (csrc/skinny_tile.h). A problem with M > 128 rows (M % 128 ==
 // 0: the wide decode of sample/hyper_step.py) runs as M / 128 row blocks
 // sharing B.
-template <int BN, int NS, int NW = 4>
+template <int BN, int NS, int NW = 4, bool RA = false>
 __global__ __launch_bounds__(NW * 64) void skinny_gemm_group_kernel(const GemmGroup g) {
     extern __shared__ __attribute__((aligned(16))) __hip_bfloat16 smem[];
-    group_tile<BN, NS, NW>(g, blockIdx.x, smem);
+    group_tile<BN, NS, NW, false, RA>(g, blockIdx.x, smem);
 }
 
 // Grouped GEMM tiles + the rows of one backward LayerNorm cell step in ONE
@@ -192,6 +192,14 @@ __global__ __launch_bounds__(256) void skinny_gemm_f32_kernel(const float* __res
 // 3, 4 or 6 (6 only with BN = 64: 144 KiB). skr_gemm_set_nstage() tunes it
 // (scripts/bench_gemm.py sweeps it).
 static int g_nstage = 3;   // measured best: 2 workgroups per CU fit (72 KiB at BN = 64)
+// A in registers (skr::ra_mma) for the plain and grouped launches: 0 off, or
+// the register / B-ring depth (3, 4 or 6); skr_gemm_set_ra.
+static int g_ra = 0;
+SKR_API int skr_gemm_set_ra(int ns) {
+    const int prev = g_ra;
+    if (ns == 0 || ns == 3 || ns == 4 || ns == 6) g_ra = ns;
+    return prev;
+}
 SKR_API int skr_gemm_set_nstage(int ns) {
     if (ns != 3 && ns != 4 && ns != 6) return -2;
     g_nstage = ns;
@@ -210,22 +218,43 @@ void set_lds_attr(K k, size_t lds) {
     }
 }
 
+template <int BN, int NS, bool CBF16 = false, bool RA = false>
+int launch_v2_k(dim3 grid, hipStream_t s, const void* A, int64_t lda, int64_t a_batch, const void* Bt, int64_t ldb,
+                int64_t b_batch, void* C, int64_t ldc, int64_t c_slab, int64_t c_batch, int M, int kslice) {
+    const size_t lds = (size_t)NS * ((RA ? 0 : BM) + BN) * BK * 2;
+    set_lds_attr(skinny_gemm_glds_kernel<BN, NS, CBF16, RA>, lds);
+    hipLaunchKernelGGL((skinny_gemm_glds_kernel<BN, NS, CBF16, RA>), grid, dim3(256), lds, s, (const __hip_bfloat16*)A,
+                       lda, a_batch, (const __hip_bfloat16*)Bt, ldb, b_batch, C, ldc, c_slab, c_batch, M, kslice);
+    return SKR_CHECK_LAUNCH();
+}
+
 template <int BN, int NS, bool CBF16 = false>
 int launch_v2(dim3 grid, hipStream_t s, const void* A, int64_t lda, int64_t a_batch, const void* Bt, int64_t ldb,
               int64_t b_batch, void* C, int64_t ldc, int64_t c_slab, int64_t c_batch, int M, int kslice) {
-    const size_t lds = (size_t)NS * (BM + BN) * BK * 2;
-    set_lds_attr(skinny_gemm_glds_kernel<BN, NS, CBF16>, lds);
-    hipLaunchKernelGGL((skinny_gemm_glds_kernel<BN, NS, CBF16>), grid, dim3(256), lds, s, (const __hip_bfloat16*)A,
-                       lda, a_batch, (const __hip_bfloat16*)Bt, ldb, b_batch, C, ldc, c_slab, c_batch, M, kslice);
+    if (BN == 64 && g_ra) {   // A in registers (4-wave 64-wide tiles)
+        if (g_ra == 3) return launch_v2_k<64, 3, CBF16, true>(grid, s, A, lda, a_batch, Bt, ldb, b_batch, C, ldc, c_slab, c_batch, M, kslice);
+        if (g_ra == 4) return launch_v2_k<64, 4, CBF16, true>(grid, s, A, lda, a_batch, Bt, ldb, b_batch, C, ldc, c_slab, c_batch, M, kslice);
+        return launch_v2_k<64, 6, CBF16, true>(grid, s, A, lda, a_batch, Bt, ldb, b_batch, C, ldc, c_slab, c_batch, M, kslice);
+    }
+    return launch_v2_k<BN, NS, CBF16, false>(grid, s, A, lda, a_batch, Bt, ldb, b_batch, C, ldc, c_slab, c_batch, M, kslice);
+}
+
+template <int BN, int NS, int NW = 4, bool RA = false>
+int launch_group_k(const GemmGroup& g, hipStream_t s) {
+    const size_t lds = (size_t)NS * ((RA ? 0 : BM) + BN) * BK * 2;
+    set_lds_attr(skinny_gemm_group_kernel<BN, NS, NW, RA>, lds);
+    hipLaunchKernelGGL((skinny_gemm_group_kernel<BN, NS, NW, RA>), dim3(g.start[g.n]), dim3(NW * 64), lds, s, g);
     return SKR_CHECK_LAUNCH();
 }
 
 template <int BN, int NS, int NW = 4>
 int launch_group(const GemmGroup& g, hipStream_t s) {
-    const size_t lds = (size_t)NS * (BM + BN) * BK * 2;
-    set_lds_attr(skinny_gemm_group_kernel<BN, NS, NW>, lds);
-    hipLaunchKernelGGL((skinny_gemm_group_kernel<BN, NS, NW>), dim3(g.start[g.n]), dim3(NW * 64), lds, s, g);
-    return SKR_CHECK_LAUNCH();
+    if (BN == 64 && NW == 4 && g_ra) {
+        if (g_ra == 3) return launch_group_k<64, 3, 4, true>(g, s);
+        if (g_ra == 4) return launch_group_k<64, 4, 4, true>(g, s);
+        return launch_group_k<64, 6, 4, true>(g, s);
+    }
+    return launch_group_k<BN, NS, NW, false>(g, s);
 }
 
 }  // namespace

@@ -55,14 +55,16 @@ __device__ __forceinline__ int64_t split_off(const P& p, const TileIdx& t) {
 // vector first: __builtin_bit_cast of an ext-vector ELEMENT (acc[i][j][e])
 // reads element 0 for every e on ROCm 7.2 (measured: rows 1-3 of every
 // 4-row accumulator group held row 0's values).
-template <int BN, int NS, bool CBF16 = false, int NW = 4, bool SC1 = false>
+// RA: A in registers, only B through the LDS ring (skr::ra_mma).
+template <int BN, int NS, bool CBF16 = false, int NW = 4, bool SC1 = false, bool RA = false>
 __device__ __forceinline__ void glds_tile(const __hip_bfloat16* __restrict__ A, int64_t lda,
                                           const __hip_bfloat16* __restrict__ Bt, int64_t ldb,
                                           void* __restrict__ Cv, int64_t ldc, int M, int n0, int64_t k0, int kslice,
                                           __hip_bfloat16* smem) {
     constexpr int NJ = skr::glds_nj<BN, NW>();
     tile_f32x4 acc[2][NJ];
-    skr::glds_mma<BN, NS, NW>(A, lda, Bt, ldb, M, n0, k0, kslice, smem, acc);
+    if constexpr (RA) skr::ra_mma<BN, NS, NW>(A, lda, Bt, ldb, M, n0, k0, kslice, smem, acc);
+    else skr::glds_mma<BN, NS, NW>(A, lda, Bt, ldb, M, n0, k0, kslice, smem, acc);
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int wr = w % 4, c0 = n0 + (w / 4) * NJ * 16;
     const int fr = lane & 15, fq = lane >> 4;
@@ -88,7 +90,7 @@ __device__ __forceinline__ void glds_tile(const __hip_bfloat16* __restrict__ A, 
 
 // Workgroup `id` of a grouped launch: find its problem through the prefix
 // sums `start` and run that tile.
-template <int BN, int NS, int NW = 4, bool SC1 = false>
+template <int BN, int NS, int NW = 4, bool SC1 = false, bool RA = false>
 __device__ __forceinline__ void group_tile(const GemmGroup& g, const int id, __hip_bfloat16* smem) {
     int q = 0;
 #pragma unroll
@@ -96,7 +98,7 @@ __device__ __forceinline__ void group_tile(const GemmGroup& g, const int id, __h
     const GemmProblem& p = g.p[q];
     const TileIdx t = tile_idx(id - g.start[q], p.M, p.N, p.splits, BN);
     const int kslice = p.K / p.splits;
-    glds_tile<BN, NS, false, NW, SC1>((const __hip_bfloat16*)p.A + (int64_t)t.rb * skr::BM * p.lda, p.lda,
+    glds_tile<BN, NS, false, NW, SC1, RA>((const __hip_bfloat16*)p.A + (int64_t)t.rb * skr::BM * p.lda, p.lda,
                                       (const __hip_bfloat16*)p.Bt, p.ldb, p.C + split_off(p, t), p.ldc, t.rows,
                                       t.nt * BN, (int64_t)t.split * kslice, kslice, smem);
 }

@@ -25,6 +25,40 @@ __global__ __launch_bounds__(256) void shared_stream(const f4* __restrict__ src,
     if (acc.x == 1234.5f) out[0] = acc.y;
 }
 
+// the same footprints through LDS-DMA (global_load_lds_dwordx4 into an NS-deep
+// ring of 24 KB stages, counted vmcnt + barrier: the skinny GEMM's pattern)
+template <int NS>
+__global__ __launch_bounds__(256) void shared_stream_lds(const char* __restrict__ src, int64_t fp, int64_t per_wg,
+                                                         float* out) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    constexpr int TILE = 24 * 1024;
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int n = (int)(per_wg / TILE);
+    const int64_t rot = ((int64_t)blockIdx.x * 4099 * 4096) & (fp - 1);
+    auto issue = [&](int kt) {
+        char* st = smem + (kt % NS) * TILE;
+#pragma unroll
+        for (int i = 0; i < 6; ++i) {
+            const int64_t off = (rot + (int64_t)kt * TILE + (w + 4 * i) * 1024 + lane * 16) & (fp - 1);
+            __builtin_amdgcn_global_load_lds((const void*)(src + off),
+                                             (__attribute__((address_space(3))) void*)(st + (w + 4 * i) * 1024), 16, 0, 0);
+        }
+    };
+    float acc = 0.f;
+    for (int p = 0; p < NS - 1; ++p) issue(p);
+    for (int kt = 0; kt < n; ++kt) {
+        if (kt + NS - 1 < n) {
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(6 * (NS - 2)) : "memory");
+        } else {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        __builtin_amdgcn_s_barrier();
+        if (kt + NS - 1 < n) issue(kt + NS - 1);
+        acc += *(const float*)(smem + (kt % NS) * TILE + threadIdx.x * 16);
+    }
+    if (acc == 1234.5f) out[0] = acc;
+}
+
 int main() {
     int cus = 0;
     hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0);
@@ -49,9 +83,30 @@ int main() {
             float ms = 0;
             hipEventElapsedTime(&ms, e0, e1);
             if (rep == 2)
-                printf("{\"footprint_MB\": %lld, \"per_wg_MB\": %lld, \"us\": %.1f, \"GBps_per_wg\": %.1f, \"TBps_chip\": %.2f}\n",
+                printf("{\"mode\": \"reg D8\", \"footprint_MB\": %lld, \"per_wg_MB\": %lld, \"us\": %.1f, \"GBps_per_wg\": %.1f, \"TBps_chip\": %.2f}\n",
                        (long long)(fp >> 20), (long long)(per_wg >> 20), ms * 1e3, per_wg / (ms * 1e-3) / 1e9,
                        per_wg * (double)cus / (ms * 1e-3) / 1e12);
+        }
+    }
+    // LDS-DMA: 3- and 6-deep rings (72 / 144 KB)
+    (void)hipFuncSetAttribute((const void*)shared_stream_lds<3>, hipFuncAttributeMaxDynamicSharedMemorySize, 3 * 24 * 1024);
+    (void)hipFuncSetAttribute((const void*)shared_stream_lds<6>, hipFuncAttributeMaxDynamicSharedMemorySize, 6 * 24 * 1024);
+    for (int f = 0; f < 3; ++f) {
+        const int64_t fp = fps[f];
+        for (int ns = 3; ns <= 6; ns += 3) {
+            for (int rep = 0; rep < 3; ++rep) {
+                hipEventRecord(e0);
+                if (ns == 3) shared_stream_lds<3><<<cus, 256, 3 * 24 * 1024>>>((const char*)buf, fp, per_wg, out);
+                else shared_stream_lds<6><<<cus, 256, 6 * 24 * 1024>>>((const char*)buf, fp, per_wg, out);
+                hipEventRecord(e1);
+                hipEventSynchronize(e1);
+                float ms = 0;
+                hipEventElapsedTime(&ms, e0, e1);
+                if (rep == 2)
+                    printf("{\"mode\": \"lds_dma NS%d\", \"footprint_MB\": %lld, \"us\": %.1f, \"GBps_per_wg\": %.1f, \"TBps_chip\": %.2f}\n",
+                           ns, (long long)(fp >> 20), ms * 1e3, per_wg / (ms * 1e-3) / 1e9,
+                           per_wg * (double)cus / (ms * 1e-3) / 1e12);
+            }
         }
     }
     return 0;

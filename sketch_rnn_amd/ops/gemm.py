@@ -418,6 +418,20 @@ def plan_splits(M: int, N: int, K: int, batch: int = 1, dtype: torch.dtype = _BF
     return best
 
 
+# Skinny products with A in registers (csrc/glds_mma.h ra_mma: only B through
+# the LDS-DMA ring): 0 off, else the ring depth (3, 4, 6). Applies to the
+# plain and grouped launches (rec_gemm, rec_gemm_group); bit-identical, and
+# measured slower (25.5 vs 24.0 ms/step, profiles/r6/skinny_ra_ab.log): off.
+SKINNY_RA = 0
+_RA_SET = [0]
+
+
+def _apply_ra(lib) -> None:
+    if SKINNY_RA != _RA_SET[0]:
+        lib.lib.skr_gemm_set_ra(int(SKINNY_RA))
+        _RA_SET[0] = SKINNY_RA
+
+
 def rec_gemm(a: torch.Tensor, bt: torch.Tensor, out: torch.Tensor, splits: int, nd: int = 1,
              bn: int = 0) -> torch.Tensor:
     """Per-step recurrent product with split-K partial slabs.
@@ -437,6 +451,7 @@ def rec_gemm(a: torch.Tensor, bt: torch.Tensor, out: torch.Tensor, splits: int, 
         return out
     from ..utils import native
     lib = native.require_hip()
+    _apply_ra(lib)
     if a.dtype == torch.float32:   # fp32 ring: same arguments, no N-tile choice
         f32 = lib.lib.skr_skinny_gemm_f32
         fn = lambda *args: f32(*args[:-2], args[-1])   # noqa: E731  (drop bn)
@@ -501,6 +516,7 @@ def _launch_group(jobs) -> None:
     from ..utils import native
     from ._hipapi import GemmProblem
     lib = native.require_hip()
+    _apply_ra(lib)
     probs = (GemmProblem * len(jobs))()
     for p, (a, bt, out, s) in zip(probs, jobs):
         N, K = bt.shape[-2], bt.shape[-1]

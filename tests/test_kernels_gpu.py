@@ -927,6 +927,44 @@ def test_wgrad_kernel_vs_fp32(n, K, M, N, cs, sliced, db):
         assert torch.equal(cs1, cs2)
 
 
+@pytest.mark.parametrize("M,ra", [(100, 3), (37, 4), (128, 6), (256, 3), (200, 3)])
+def test_skinny_register_a_bitwise(M, ra):
+    """ops.gemm.SKINNY_RA (csrc/glds_mma.h ra_mma: each wave's A fragments
+    loaded straight into registers, only B through the LDS-DMA ring) against
+    the LDS-staged kernel: the same fragments and k order, so bit-identical
+    slabs for the plain launch (split-K, a column slice of a wider A like the
+    HyperLSTM's [h | hh] rows) and the grouped launch (two problems, row
+    blocks past 128, a partial last block)."""
+    from sketch_rnn_amd.ops import gemm
+    torch.manual_seed(M + ra)
+    dev = torch.device("cuda")
+    A = torch.randn(M, 2304, device=dev).to(torch.bfloat16)
+    W1 = torch.randn(8192, 2048, device=dev).to(torch.bfloat16)     # B^T of h @ W_h
+    W2 = torch.randn(1024, 2304, device=dev).to(torch.bfloat16)     # B^T of [h | hh] @ W_y
+    saved = gemm.SKINNY_RA
+    out = {}
+    try:
+        for v in (0, ra):
+            gemm.SKINNY_RA = v
+            o1 = torch.full((2, M, 8192), float("nan"), device=dev)
+            o2 = torch.full((4, M, 1024), float("nan"), device=dev)
+            if M <= 128:
+                gemm.rec_gemm(A[:, :2048], W1, o1, 2)
+                gemm.rec_gemm(A, W2, o2, 4)
+            p1 = torch.full((2, M, 8192), float("nan"), device=dev)
+            p2 = torch.full((4, M, 1024), float("nan"), device=dev)
+            gemm.rec_gemm_group([(A[:, :2048], W1, p1, 2), (A, W2, p2, 4)])
+            out[v] = (o1, o2, p1, p2)
+    finally:
+        gemm.SKINNY_RA = saved
+    for k in range(4):
+        if M > 128 and k < 2:
+            continue
+        assert torch.equal(out[0][k], out[ra][k]), k
+    ref = A[:, :2048].float() @ W1.float().t()
+    assert (out[ra][2].sum(0) - ref).abs().max().item() <= 1e-3 * ref.abs().max().item()
+
+
 @pytest.mark.parametrize("n,K,M,N,cs,sliced", [(1, 25000, 2048, 8192, False, True), (1, 3001, 256, 2560, True, False),
                                                (2, 1000, 512, 512, False, False), (1, 777, 2304, 1024, True, True),
                                                (1, 33, 256, 256, True, False)])
