@@ -69,6 +69,16 @@ namespace {
 // pays for 112 rows, not MAXB). SC1: g and the partial sums are read by
 // workgroups of the SAME launch (hyper_mod_chain): write-through stores.
 template <int NS, int NRT, bool SC1>
+__device__ __forceinline__ void mod_block(ModDecode dec, const __hip_bfloat16* __restrict__ hh, int64_t ld_hh,
+                                          const float* __restrict__ xh, const float* __restrict__ R, int64_t r_slab,
+                                          __hip_bfloat16* __restrict__ vec, float* __restrict__ gout,
+                                          __hip_bfloat16* __restrict__ rlp, float* __restrict__ stats, int B, int H,
+                                          const int q, const int tile, const int z, const bf16x8 (&pf)[8],
+                                          const float qv);
+
+// One modulation tile: gate q, hidden units [TU tile, +TU), row blocks z0,
+// z0 + zs, ... of B rows (the P fragments loaded once for all of them).
+template <int NS, int NRT, bool SC1>
 __device__ __forceinline__ void mod_tile(ModDecode dec, const __hip_bfloat16* __restrict__ hh, int64_t ld_hh,
                                          const __hip_bfloat16* __restrict__ PlT,   // [12H][HH]
                                          const float* __restrict__ qb,             // [12H]
@@ -78,9 +88,34 @@ __device__ __forceinline__ void mod_tile(ModDecode dec, const __hip_bfloat16* __
                                          float* __restrict__ gout,                  // [B][4H]
                                          __hip_bfloat16* __restrict__ rlp,          // [B][4H] or null
                                          float* __restrict__ stats,                 // [B][4][H/TU][2]
-                                         int B, int H, const int q, const int tile, const int z) {
+                                         int B, int H, const int q, const int tile, const int z0, const int zs) {
+    const int u0 = tile * TU;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int fr = lane & 15, fq = lane >> 4;
+    const int vcol = (q + 4 * (w >> 1)) * H + u0 + 16 * (w & 1);   // first modulation column of tile w
+    bf16x8 pf[8];
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks) pf[ks] = *(const bf16x8*)(PlT + (int64_t)(vcol + fr) * HH + 32 * ks + 8 * fq);
+    const float qv = qb[vcol + fr];
+    const int nblk = (B + MAXB - 1) / MAXB;
+    // (consecutive blocks reuse the LDS: the next block's hh stage is written
+    // after this block's MFMAs -- every wave passed this block's second
+    // barrier -- and its vectors after the next block's first barrier)
+    for (int z = z0; z < nblk; z += zs)
+        mod_block<NS, NRT, SC1>(dec, hh, ld_hh, xh, R, r_slab, vec, gout, rlp, stats, B, H, q, tile, z, pf, qv);
+}
+
+// Row block z of a modulation tile (B > MAXB: the wide decode): rows
+// r0 .. r0 + MAXB - 1.
+template <int NS, int NRT, bool SC1>
+__device__ __forceinline__ void mod_block(ModDecode dec, const __hip_bfloat16* __restrict__ hh, int64_t ld_hh,
+                                          const float* __restrict__ xh, const float* __restrict__ R, int64_t r_slab,
+                                          __hip_bfloat16* __restrict__ vec, float* __restrict__ gout,
+                                          __hip_bfloat16* __restrict__ rlp, float* __restrict__ stats, int B, int H,
+                                          const int q, const int tile, const int z, const bf16x8 (&pf)[8],
+                                          const float qv) {
     constexpr int MB = 16 * NRT;
-    {   // row block z (B > MAXB: the wide decode): rows r0 .. r0 + MAXB - 1
+    {
         const int r0 = z * MAXB;
         B = min(MAXB, B - r0);
         const int64_t G4 = (int64_t)r0 * 4 * H;
@@ -105,14 +140,9 @@ __device__ __forceinline__ void mod_tile(ModDecode dec, const __hip_bfloat16* __
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int fr = lane & 15, fq = lane >> 4;
     const int G = 4 * H, NV = 12 * H;
-    // ---- every global load up front: this wave's P fragments, the
+    // ---- every global load up front (the P fragments: mod_tile): the
     // epilogue's x-projection and R slabs (thread -> rows rg, rg + 48, rg + 96;
     // units u0 + 4 ug .. +3), and hh for the LDS stage
-    const int vcol = (q + 4 * (w >> 1)) * H + u0 + 16 * (w & 1);   // first modulation column of tile w
-    bf16x8 pf[8];
-#pragma unroll
-    for (int ks = 0; ks < 8; ++ks) pf[ks] = *(const bf16x8*)(PlT + (int64_t)(vcol + fr) * HH + 32 * ks + 8 * fq);
-    const float qv = qb[vcol + fr];
     constexpr int RPT = (MB + NTH / 8 - 1) / (NTH / 8);      // rows per thread (<= 3)
     const int rg = tid >> 3, ug = tid & 7, ul = 4 * ug;
     f32x4 x4[RPT], r4[RPT];
@@ -236,7 +266,7 @@ __global__ __launch_bounds__(NTH) void hyper_mod_fwd(ModDecode dec, const __hip_
                                                      float* __restrict__ gout, __hip_bfloat16* __restrict__ rlp,
                                                      float* __restrict__ stats, int B, int H) {
     mod_tile<NS, NRT, false>(dec, hh, ld_hh, PlT, qb, xh, R, r_slab, vec, gout, rlp, stats, B, H, blockIdx.y, blockIdx.x,
-                             blockIdx.z);
+                             blockIdx.z, gridDim.z);
 }
 
 // ---- chained launch: the modulation tiles + the main LayerNorm cell rows -----------------
@@ -375,13 +405,23 @@ __global__ __launch_bounds__(NTH) void hyper_mod_chain(const __hip_bfloat16* __r
     ModDecode dec{};
     dec.xh_bf16 = xh_bf16;
     mod_tile<NS, NRT, true>(dec, hh, ld_hh, PlT, qb, xh, R, r_slab, vec, const_cast<float*>(cell.gpre), rlp,
-                            const_cast<float*>(cell.gstats), cell.B, H, id / ntile, id % ntile, 0);
+                            const_cast<float*>(cell.gstats), cell.B, H, id / ntile, id % ntile, 0, 1);
     chain_arrive(cs.counters + cs.k);
     if (id >= cell.B * C) return;
     main_rows<UPT>(cell, id / C, id % C, C, cs.counters + cs.k, (uint32_t)gridDim.x, cs.err);
 }
 
 }  // namespace
+
+static int g_hm_zgrid = 0;   // row blocks in parallel (0: all); skr_hyper_mod_set_zgrid
+
+// A/B hook: parallel row blocks of the wide (B > 128) launches; 0 = one
+// workgroup per row block. Returns the previous setting.
+SKR_API int skr_hyper_mod_set_zgrid(int zg) {
+    const int prev = g_hm_zgrid;
+    if (zg >= 0) g_hm_zgrid = zg;
+    return prev;
+}
 
 // hh [B][Hh] bf16 rows (stride ld_hh), PlT [12H][Hh] bf16, qb [12H] fp32
 // (q, with the main bias added to blocks 8..11), xh [B][4H] fp32, R = sum of
@@ -400,7 +440,10 @@ SKR_API int skr_hyper_mod_fwd(const void* hh, int64_t ld_hh, const void* PlT, co
     if (((uintptr_t)hh | (uintptr_t)PlT | (uintptr_t)xh | (uintptr_t)R | (uintptr_t)vec | (uintptr_t)g |
          (uintptr_t)rlp) & 15 || (ld_hh % 8) || (r_slab % 4))
         return -4;
-    const dim3 grid(H / TU, 4, (B + MAXB - 1) / MAXB);
+    // row blocks: gridDim.z of them in parallel, each workgroup walking
+    // blocks z, z + gridDim.z, ... with its P fragments loaded once
+    const int nblk = (B + MAXB - 1) / MAXB;
+    const dim3 grid(H / TU, 4, g_hm_zgrid > 0 ? (nblk < g_hm_zgrid ? nblk : g_hm_zgrid) : nblk);
     const auto* a = (const __hip_bfloat16*)hh;
     const auto* p = (const __hip_bfloat16*)PlT;
     auto* v = (__hip_bfloat16*)vec;

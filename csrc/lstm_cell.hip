@@ -152,6 +152,8 @@ inline int64_t coresident_capacity(const void* k, int nt) {
     return cap;
 }
 
+static int g_cell_oversub = 0;
+
 // Geometry: C = args->cluster workgroups per row. C == 1 rows wider than 256
 // units run on 1024-thread workgroups (one row per CU, no exchange);
 // otherwise 256 threads with UPT units each.
@@ -193,7 +195,11 @@ int launch(const A& a, bool ln, int mod, hipStream_t s) {
     // occupancy API (capped at 4 per CU, below the API's answer near the
     // SGPR edges where it reads one block high) -- a grid that could strand
     // a workgroup is refused instead of spinning into the timeout.
-    if (C > 1 && ln && (int64_t)a.B * C > coresident_capacity((const void*)k, nt)) return -8;
+    // (g_cell_oversub: the caller accepts rows past the resident capacity --
+    // a row's C workgroups are consecutive ids, so on every XCD they share one
+    // in-order dispatch position: a waiting row's partners are dispatched no
+    // later than the rows ahead of them finish)
+    if (C > 1 && ln && !g_cell_oversub && (int64_t)a.B * C > coresident_capacity((const void*)k, nt)) return -8;
     hipLaunchKernelGGL(k, dim3(C, a.B), dim3(nt), 0, s, a);
     return SKR_CHECK_LAUNCH();
 }
@@ -213,3 +219,11 @@ SKR_API int skr_lstm_bwd_step(const BwdArgs* args, int ln, int mod, hipStream_t 
 
 SKR_API int skr_lstm_fwd_args_size() { return (int)sizeof(FwdArgs); }
 SKR_API int skr_lstm_bwd_args_size() { return (int)sizeof(BwdArgs); }
+
+// Clustered rows beyond the co-resident capacity (see launch): 1 allows them
+// for the next launches, 0 restores the check. Returns the previous setting.
+SKR_API int skr_cell_set_oversub(int on) {
+    const int prev = g_cell_oversub;
+    if (on >= 0) g_cell_oversub = on != 0;
+    return prev;
+}

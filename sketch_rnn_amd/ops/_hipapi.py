@@ -402,6 +402,10 @@ class HipLib:
         lib.skr_skinny_gemm_group_cellbwd.argtypes = [C.POINTER(GemmProblem), _i, C.POINTER(LstmBwdArgs), _p]
         lib.skr_skinny_gemm_group_cellbwd.restype = _i
         lib.skr_chain_bwd_main.argtypes = [C.POINTER(GemmProblem), _i, C.POINTER(LstmBwdArgs), C.POINTER(ChainSync), _p]
+        lib.skr_cell_set_oversub.argtypes = [_i]
+        lib.skr_cell_set_oversub.restype = _i
+        lib.skr_hyper_mod_set_zgrid.argtypes = [_i]
+        lib.skr_hyper_mod_set_zgrid.restype = _i
         lib.skr_gemm_set_ra.argtypes = [_i]
         lib.skr_gemm_set_ra.restype = _i
         lib.skr_chain_ln_fwd.argtypes = [C.POINTER(GemmProblem), _i, C.POINTER(LstmFwdArgs), C.POINTER(ChainSync), _p]

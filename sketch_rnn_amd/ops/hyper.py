@@ -117,6 +117,22 @@ BG_CHUNK = 50
 # profiles/r3/hyper_fused_cell_ab.txt.)
 
 
+# Row blocks of a wide (B > 128) modulation launch run in parallel (0: all,
+# one workgroup per block) or walked by HM_ZGRID workgroups per tile, each
+# loading its P fragments once (csrc/hyper_mod.hip skr_hyper_mod_set_zgrid).
+# Measured on GraphDecoder steps (profiles/r6/decode_wide_knobs_ab.jsonl):
+# 1 walker per tile 0.146 vs 0.157 ms per step at B = 1024, 0.084 vs 0.090 at
+# B = 512 (2: 0.148 / 0.087, 4: 0.153 / 0.089). Bit-identical.
+HM_ZGRID = 1
+_ZGRID_SET = [0]
+
+
+def apply_hm_zgrid(lib) -> None:
+    if HM_ZGRID != _ZGRID_SET[0]:
+        lib.lib.skr_hyper_mod_set_zgrid(int(HM_ZGRID))
+        _ZGRID_SET[0] = HM_ZGRID
+
+
 # Split-K tuning knobs of the per-step products (sweeps set them from Python:
 # "sm" h W_h, "sy" [h | hh] W_y, "sh" dvec P^T, "sam" dR_main W_h^T, "say"
 # dR_hyp W_y^T); empty = the planned factors.
@@ -407,6 +423,7 @@ class _HyperSeq(torch.autograd.Function):
                 chain_f = False
                 cf.buf.zero_()
             if hmod:
+                apply_hm_zgrid(lib)
                 _check(lib.lib.skr_hyper_mod_fwd(A[t + 1, :, H:].data_ptr(), K, PlT.data_ptr(), qb.data_ptr(),
                                                  XHc[t].data_ptr(), RM[rmi(t)].data_ptr(), B * G, S_m,
                                                  VEC[t].data_ptr(), GP.data_ptr(), _ptr(RLP[t] if RLP is not None else None),

@@ -139,10 +139,13 @@ class _ClusterSync:
     """Per-pass cell geometry + the tagged partial-statistics exchange buffer
     (zeroed once per pass; tags = step + 1 make earlier steps' slots stale)."""
 
-    def __init__(self, T: int, BB: int, H: int, device, ln: bool = True, C: int = 0):
+    def __init__(self, T: int, BB: int, H: int, device, ln: bool = True, C: int = 0, oversub: bool = False):
+        # oversub: rows past the co-resident capacity are accepted (the cell
+        # launch is then made under skr_cell_set_oversub; see csrc/lstm_cell.hip)
+        self.oversub = oversub
         if C > 0:   # a requested C: at least 256 units per workgroup, every workgroup co-resident
             C = min(C, max(1, H // 256))
-            while ln and C > 1 and BB * C > _coresident_capacity():
+            while ln and C > 1 and BB * C > _coresident_capacity() and not oversub:
                 C //= 2
         self.C = C if C > 0 else cell_geometry(H, BB, ln)
         self.on = ln and self.C > 1

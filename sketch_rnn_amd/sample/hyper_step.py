@@ -52,6 +52,15 @@ from ..ops.hyper import _fold_ok
 from ..ops.recurrent import _ClusterSync, _seed_tensor
 from ..utils import native
 
+# Main-cell workgroups per row above 128 rows (the wide decode): 1 keeps
+# one 1024-thread workgroup per row; C > 1 splits rows over C workgroups with
+# more rows than can be resident at once (consecutive workgroup ids share
+# one dispatch position per XCD, so partners are never stranded). Measured
+# (profiles/r6/decode_wide_knobs_ab.jsonl): C = 2 0.144 vs 0.157 ms per decode
+# step at B = 1024, 0.084 vs 0.090 at B = 512 (4: 0.149 / 0.087, 8: 0.159 /
+# 0.092).
+WIDE_MAIN_C = 2
+
 
 def hyper_step_ok(model, B: int) -> bool:
     cfg = model.cfg
@@ -133,6 +142,8 @@ class HyperStepDecoder:
         self.clm = _ClusterSync(1, B, H, device)
         if not cluster or B > 128:   # (wide: 1024-thread rows, no co-residency requirement)
             self.clm.C, self.clm.on = 1, False
+            if cluster and WIDE_MAIN_C > 1:   # wide rows split over C workgroups anyway (oversubscribed)
+                self.clm = _ClusterSync(1, B, H, device, C=WIDE_MAIN_C, oversub=True)
         self.clh = _ClusterSync(1, B, Hh, device)
         self.sd = _seed_tensor(0, device)
 
@@ -289,8 +300,14 @@ class HyperStepDecoder:
         if self.lib.skr_lstm_fwd_step(ctypes.byref(ah), 1, 0, st) != 0:
             raise RuntimeError("hyper cell step failed")
         gemm.rec_gemm_bf16out(self.A[:, H:], PQ[0], self.VEC)
-        if self.lib.skr_lstm_fwd_step(ctypes.byref(am), 1, 2, st) != 0:
-            raise RuntimeError("main cell step failed")
+        prev = self.lib.skr_cell_set_oversub(1) if self.clm.oversub else None
+        try:
+            rc = self.lib.skr_lstm_fwd_step(ctypes.byref(am), 1, 2, st)
+        finally:
+            if prev is not None:
+                self.lib.skr_cell_set_oversub(prev)
+        if rc != 0:
+            raise RuntimeError("main cell step failed (%d)" % rc)
         gemm.rec_gemm(self.A[:, :H], w["WoT"], self.ZS, self.S_o)
         sample(self.ZS, 128, self.S_o, B * 128, w["bo"])
 
@@ -337,14 +354,22 @@ class HyperStepDecoder:
         dec = ModDecode()
         dec.x5, dec.w5, dec.ldw5 = self.X.data_ptr(), w["W5"].data_ptr(), G + Gh
         dec.zp, dec.ldzp = self.ZP.data_ptr(), G + Gh
+        from ..ops.hyper import apply_hm_zgrid
+        apply_hm_zgrid(native.require_hip())
         rc = lib.skr_hyper_mod_fwd(self.A[:, H:].data_ptr(), K, w["PL"].data_ptr(),
                                    w["QB"].data_ptr(), None, self.RM.data_ptr(), B * G, self.S_m, None,
                                    self.GP.data_ptr(), None, self.GS.data_ptr(), B, H, Hh, ctypes.byref(dec), st)
         if rc != 0:
             raise RuntimeError("skr_hyper_mod_fwd (decode) failed (%d)" % rc)
         am.gpre, am.gstats, am.gstat_tiles = self.GP.data_ptr(), self.GS.data_ptr(), H // 32
-        if lib.skr_lstm_fwd_step(ctypes.byref(am), 1, 3, st) != 0:
-            raise RuntimeError("main cell step failed")
+        prev = lib.skr_cell_set_oversub(1) if self.clm.oversub else None
+        try:
+            rc = lib.skr_lstm_fwd_step(ctypes.byref(am), 1, 3, st)
+        finally:
+            if prev is not None:
+                lib.skr_cell_set_oversub(prev)
+        if rc != 0:
+            raise RuntimeError("main cell step failed (%d)" % rc)
 
     @torch.no_grad()
     def head(self) -> None:

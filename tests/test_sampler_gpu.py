@@ -332,3 +332,99 @@ def test_graph_decoder_early_exit_hyper_steppers(B, fused):
         hyper_step.FUSED = saved
         ops.set_backend("auto")
         ops.set_compute_dtype("fp32")
+
+
+@pytest.mark.parametrize("B", [384, 1024])
+def test_hyper_mod_row_block_walk_bitwise(B):
+    """ops.hyper.HM_ZGRID: the wide decode's modulation launch with its row
+    blocks walked by 1 or 2 workgroups per tile (P fragments loaded once)
+    against one workgroup per row block: the same per-block arithmetic, so
+    the head outputs of several teacher-forced strokes are bit-identical."""
+    from sketch_rnn_amd.ops import hyper
+    from sketch_rnn_amd.sample.hyper_step import HyperStepDecoder
+    native.require_hip()
+    ops.set_backend("hip")
+    ops.set_compute_dtype("bf16")
+    cfg, m = _hyper256(H=2048, E=32)
+    g = torch.Generator(device=DEV).manual_seed(5)
+    z = torch.randn(B, cfg.z_size, device=DEV, generator=g)
+    xs = []
+    for t in range(4):
+        x = torch.zeros(B, 5, device=DEV)
+        x[:, :2] = torch.randn(B, 2, device=DEV, generator=g) * 0.5
+        x[:, 2] = 1.0
+        xs.append(x)
+    saved = hyper.HM_ZGRID
+    outs = {}
+    try:
+        for zg in (0, 1, 2):
+            hyper.HM_ZGRID = zg
+            with torch.no_grad():
+                zc = m.condition(z, None, B, DEV)
+                st = HyperStepDecoder(m, B, torch.device(DEV))
+                assert st.fused
+                st.begin(zc, m.initial_state(zc, B, DEV))
+                res = []
+                for t, x in enumerate(xs):
+                    st.X.copy_(x)
+                    st.step_fused(t, None)
+                    st.head()
+                    res.append(st.ZS.clone())
+                torch.cuda.synchronize()
+            outs[zg] = res
+    finally:
+        hyper.HM_ZGRID = saved
+    for zg in (1, 2):
+        for t in range(len(xs)):
+            assert torch.equal(outs[0][t], outs[zg][t]), (zg, t)
+
+
+@pytest.mark.parametrize("C", [2, 4])
+def test_wide_decode_main_cell_split_rows(C):
+    """sample.hyper_step.WIDE_MAIN_C: the wide decode's main cell (B = 1024
+    rows) split over C workgroups per row -- more workgroups than can be
+    resident at once, each row's exchange among consecutive ids -- against
+    one 1024-thread workgroup per row: the same outputs up to the LayerNorm
+    sums' order (1e-3 of the largest element) over several strokes, and the
+    launch never raises a cluster timeout."""
+    from sketch_rnn_amd.ops.recurrent import check_cluster_errors
+    from sketch_rnn_amd.sample import hyper_step
+    from sketch_rnn_amd.sample.hyper_step import HyperStepDecoder
+    native.require_hip()
+    ops.set_backend("hip")
+    ops.set_compute_dtype("bf16")
+    B = 1024
+    cfg, m = _hyper256(H=2048, E=32)
+    g = torch.Generator(device=DEV).manual_seed(9)
+    z = torch.randn(B, cfg.z_size, device=DEV, generator=g)
+    xs = []
+    for t in range(3):
+        x = torch.zeros(B, 5, device=DEV)
+        x[:, :2] = torch.randn(B, 2, device=DEV, generator=g) * 0.5
+        x[:, 2] = 1.0
+        xs.append(x)
+    saved = hyper_step.WIDE_MAIN_C
+    outs = {}
+    try:
+        for c in (1, C):
+            hyper_step.WIDE_MAIN_C = c
+            with torch.no_grad():
+                zc = m.condition(z, None, B, DEV)
+                st = HyperStepDecoder(m, B, torch.device(DEV))
+                assert (st.clm.C == c) if c > 1 else True
+                st.begin(zc, m.initial_state(zc, B, DEV))
+                res = []
+                for t, x in enumerate(xs):
+                    st.X.copy_(x)
+                    st.step_fused(t, None)
+                    st.head()
+                    res.append(st.ZS.sum(0).clone())
+                torch.cuda.synchronize()
+                check_cluster_errors(DEV)
+            outs[c] = res
+    finally:
+        hyper_step.WIDE_MAIN_C = saved
+    for t in range(len(xs)):
+        a, b = outs[1][t], outs[C][t]
+        assert (a - b).abs().max().item() <= 1e-3 * a.abs().max().item() + 1e-5, t
+
