@@ -21,8 +21,10 @@ import bench  # noqa: E402
 
 
 def parse_arm(spec):
+    import re
     out = []
-    for item in filter(None, spec.split(",")):
+    # items split at commas that start a new "module.ATTR=" (values may hold commas)
+    for item in filter(None, re.split(r",(?=\s*[A-Za-z_][\w.]*\.[A-Za-z_]\w*\s*=)", spec)):
         key, val = item.split("=", 1)
         mod, attr = key.rsplit(".", 1)
         out.append((importlib.import_module("sketch_rnn_amd.ops." + mod), attr, ast.literal_eval(val)))

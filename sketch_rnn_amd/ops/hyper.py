@@ -133,6 +133,8 @@ def apply_hm_zgrid(lib) -> None:
         _ZGRID_SET[0] = HM_ZGRID
 
 
+SAY_CAP = 2   # split-K ceiling of dR_hyp W_y^T (backward; see _HyperSeq.backward)
+
 # Split-K tuning knobs of the per-step products (sweeps set them from Python:
 # "sm" h W_h, "sy" [h | hh] W_y, "sh" dvec P^T, "sam" dR_main W_h^T, "say"
 # dR_hyp W_y^T); empty = the planned factors.
@@ -484,12 +486,15 @@ class _HyperSeq(torch.autograd.Function):
         # 0.15 ms/step slower: 25.03 / 25.00 vs 24.83 / 24.88, profiles/r3/hyper_fused_cell_ab.txt)
         S_h = _split_override("sh", gemm.plan_splits(B, Hh, 12 * H, 1, ldt), 12 * H)
         S_am = _split_override("sam", gemm.plan_splits(B, H, G, 1, ldt), G)
-        # d[h | hh] = dR_hyp @ W_y^T: at most 4 split-K slabs -- the next step's
-        # two cells read every slab; measured on MI355X (vae_large, same box,
-        # A/B twice): 4 slabs 26.67 / 26.57 vs 8 (the plan) 26.76 / 26.86 ms/step
+        # d[h | hh] = dR_hyp @ W_y^T: at most SAY_CAP split-K slabs -- the next
+        # step's two cells read every slab (the main-cell rows with sc1 loads
+        # inside the chained launch); measured on MI355X (vae_large, same box):
+        # round 3, 4 slabs 26.67 / 26.57 vs 8 (the plan) 26.76 / 26.86 ms/step;
+        # round 6 (profiles/r6/hyper_splits2_ab.log, A B C D x3), 2 slabs
+        # 23.67 / 23.68 / 23.69 vs 4 23.89 / 23.91 / 23.86, 1 slab 24.46-24.48
         S_ay = gemm.plan_splits(B, K, Gh, 1, ldt)
-        if S_ay > 4:
-            S_ay = next(d for d in (4, 3, 2, 1) if (Gh // 64) % d == 0)
+        if S_ay > SAY_CAP:
+            S_ay = next(d for d in (SAY_CAP, 4, 3, 2, 1) if d <= SAY_CAP and (Gh // 64) % d == 0)
         S_ay = _split_override("say", S_ay, Gh)
         DHZ = torch.empty(max(S_h, 1), B, Hh, device=dev, dtype=f32)    # slabs of dhh from the vec path
         # dh slabs of step t + 1 read by step t; the last step reads none (null
