@@ -56,7 +56,9 @@ CHAIN = os.environ.get("SKR_CHAIN", "1") != "0"
 # launch. Producers that stay resident waiting on the rows cost 7.4 us by
 # themselves (probe 3: no staging, no tile), and the tile tail -- 154 KB of
 # dvec per workgroup through sc1 loads from the fabric -- another ~10 us,
-# more than the 8 us launch it replaces.
+# more than the 8 us launch it replaces. It also needs at least as many
+# producer tiles as dvec P^T tail tiles: at SAY_CAP = 2 (below) the launch
+# declines and the two-stage chain runs (the bitwise test pins SAY_CAP = 4).
 CHAIN3 = False
 # Workgroups per main-cell row in the chained backward launch (1 or 2): 2
 # splits each row's ~300 KB of loads over two CUs and exchanges the two

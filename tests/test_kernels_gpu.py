@@ -1248,16 +1248,18 @@ def test_hyper_three_stage_chain_bitwise(B, T, fin_w):
     while the rows compute, A operand through sc1 loads after the rows'
     counter) equals the separate dvec P^T launch bit for bit -- the same
     fragments, k order and MFMA -- for every output and gradient; and the
-    launch really ran T - 1 times (B <= 128)."""
+    launch really ran T - 1 times (B <= 128).  At 4 dR_hyp W_y^T slabs: the
+    default cap of 2 leaves fewer producer tiles than dvec P^T tail tiles, so
+    the three-stage launch declines (-2) and the two-stage chain runs."""
     from sketch_rnn_amd.ops import hyper
     from sketch_rnn_amd.ops.recurrent import ROW_STATS
     p, x, z, st, w = _hyper_setup(8, T, B, 5, 16, 2048, 256, 32, jitter=0.02, state=0.1)
     ops.set_backend("hip")
     ops.set_compute_dtype("bf16")
-    saved = hyper.CHAIN, hyper.CHAIN3
+    saved = hyper.CHAIN, hyper.CHAIN3, hyper.SAY_CAP
     runs = {}
     try:
-        hyper.CHAIN = True
+        hyper.CHAIN, hyper.SAY_CAP = True, 4
         for c3 in (True, False, True):
             hyper.CHAIN3 = c3
             n0 = ROW_STATS["chain3"]
@@ -1265,7 +1267,7 @@ def test_hyper_three_stage_chain_bitwise(B, T, fin_w):
             # (B > 128: the tail is one 128-row block only -- not taken, two-stage chain)
             assert ROW_STATS["chain3"] - n0 == ((T - 1) if (c3 and B <= 128) else 0)
     finally:
-        hyper.CHAIN, hyper.CHAIN3 = saved
+        hyper.CHAIN, hyper.CHAIN3, hyper.SAY_CAP = saved
     for n, a, b, c in zip(_names(p), runs[True][0], runs[False][0], runs[True][1]):
         assert torch.equal(a, c), n
         assert torch.equal(a, b), n
