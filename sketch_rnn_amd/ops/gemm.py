@@ -48,6 +48,25 @@ def mm(a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor] = None) -> 
     return torch.mm(a, b, out_dtype=torch.float32)
 
 
+_ONES = {}
+
+
+def ones_row(n: int, device) -> torch.Tensor:
+    """``[1, n]`` fp32 ones: the A operand that turns a :class:`SmallGroup`
+    product into a column sum (``ones @ P`` = ``P.sum(0)``) inside the same
+    grouped launch. Cached per (device, n) when created eagerly; a tensor
+    first asked for during HIP-graph capture is not cached (it lives in the
+    graph's pool)."""
+    dev = torch.device(device)
+    key = (dev, int(n))
+    t = _ONES.get(key)
+    if t is None:
+        t = torch.ones(1, n, device=dev)
+        if not (dev.type == "cuda" and torch.cuda.is_current_stream_capturing()):
+            _ONES[key] = t
+    return t
+
+
 def small_mm(a: torch.Tensor, b: torch.Tensor, bias: Optional[torch.Tensor] = None,
              out: Optional[torch.Tensor] = None, acc: bool = False) -> torch.Tensor:
     """fp32 ``a @ b (+ bias) (+ out if acc)`` for the small per-sequence

@@ -23,6 +23,7 @@ import torch
 from ..utils import native
 from . import gemm
 from ._hipapi import LstmBwdArgs, LstmFwdArgs, ModDecode
+from . import inproj
 from .inproj import bproj_fwd, bproj_ok, bproj_reduce
 from .recurrent import (ROW_STATS, _cell_bwd, _cell_fwd, _check, _ClusterSync, _inference, _ln_saves_lp, _lp_kind,
                         _ptr, _Saved, _seed_tensor, _stream, cell_geometry)
@@ -689,22 +690,36 @@ class _HyperSeq(torch.autograd.Function):
             dhW_x, dhW_h = torch.empty_like(s.hW_x), None
         dx = dzc = None
         if s.bp:   # input-side gradients from one read of dXH / dR_hyp each
-            S_m, P_m = bproj_reduce(s.x, dXH)
-            S_y, P_y = bproj_reduce(s.x, dRY_lp)
-            if s.zc is not None:
+            if s.zc is not None and not inproj.GROUPED_REDUCE:
+                S_m, P_m = bproj_reduce(s.x, dXH)
+                S_y, P_y = bproj_reduce(s.x, dRY_lp)
                 dW_x = gemm.grad_slot(s.W_x, tuple(s.W_x.shape))
                 dW_x = torch.empty_like(s.W_x) if dW_x is None else dW_x
                 dW_x[:IX] = P_m
                 dhW_x[:IX] = P_y
-                g = gemm.SmallGroup(dev)   # the three independent z-side products in one launch
+                g = gemm.SmallGroup(dev)
+                g.mm(s.zc.t(), S_m, out=dW_x[IX:])
+                g.mm(s.zc.t(), S_y, out=dhW_x[IX:IN])
+                dzc = g.mm(S_m, s.W_x[IX:].t())
+                g.run()
+                gemm.small_mm(S_y, s.hW_x[IX:IN].t(), out=dzc, acc=True)
+            elif s.zc is not None:
+                S_m, P_m = bproj_reduce(s.x, dXH, raw=True)      # P: per-row partials [B, IX, *]
+                S_y, P_y = bproj_reduce(s.x, dRY_lp, raw=True)
+                dW_x = gemm.grad_slot(s.W_x, tuple(s.W_x.shape))
+                dW_x = torch.empty_like(s.W_x) if dW_x is None else dW_x
+                one = gemm.ones_row(B, dev)
+                g = gemm.SmallGroup(dev)   # the row sums of P and the three z-side products in one launch
+                g.mm(one, P_m.view(B, IX * G), out=dW_x[:IX].view(1, IX * G))
+                g.mm(one, P_y.view(B, IX * Gh), out=dhW_x[:IX].view(1, IX * Gh))
                 g.mm(s.zc.t(), S_m, out=dW_x[IX:])
                 g.mm(s.zc.t(), S_y, out=dhW_x[IX:IN])
                 dzc = g.mm(S_m, s.W_x[IX:].t())
                 g.run()
                 gemm.small_mm(S_y, s.hW_x[IX:IN].t(), out=dzc, acc=True)
             else:
-                dW_x = P_m
-                dhW_x[:IN] = P_y
+                S_m, dW_x = bproj_reduce(s.x, dXH)
+                S_y, dhW_x[:IN] = bproj_reduce(s.x, dRY_lp)
         else:
             dXHl, dXHYl = gemm.lp(dXH.view(TB, G)), gemm.lp(dRY_lp.view(TB, Gh))
             dW_x = gemm.wgrad(s.xl, dXHl)

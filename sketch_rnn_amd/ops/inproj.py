@@ -106,9 +106,11 @@ def bproj_fwd(x, W, zw=None, bf16: bool = False):
     return xp
 
 
-def bproj_reduce(x, dxp):
+def bproj_reduce(x, dxp, raw: bool = False):
     """One read of ``dxp [T, B, G]`` (fp32 or bf16, rows may be strided):
-    ``S[b] = sum_t dxp[t, b]`` and ``P = sum_{t,b} x[t, b]^T dxp[t, b]`` ([IN, G])."""
+    ``S[b] = sum_t dxp[t, b]`` and ``P = sum_{t,b} x[t, b]^T dxp[t, b]`` ([IN, G]);
+    ``raw``: P as the kernel's per-row partials ``[B, IN, G]`` (the caller
+    sums them inside a grouped small-GEMM launch, :func:`gemm.ones_row`)."""
     lib = native.require_hip()
     T, B, IN = x.shape
     G = dxp.shape[-1]
@@ -122,17 +124,29 @@ def bproj_reduce(x, dxp):
                                P.data_ptr(), T, B, IN, G, torch.cuda.current_stream().cuda_stream)
     if rc != 0:
         raise RuntimeError("skr_bproj_bwd failed (%d)" % rc)
-    return S, P.sum(0)
+    return (S, P) if raw else (S, P.sum(0))
+
+
+# Backward reductions of the stroke projections (row sums of the per-row
+# partials, the bias and z-side products) as ONE grouped small-GEMM launch;
+# False: torch reduce / cat / library GEMMs (the A/B arm).
+GROUPED_REDUCE = True
 
 
 class _BProj(torch.autograd.Function):
+    """The z part once per sequence (``csrc/small_gemm.hip``, bias folded in),
+    the stroke part per (t, b) in ``skr_bproj_fwd``; backward: one read of
+    dxp, then every reduction and z-side product in ONE grouped small-GEMM
+    launch (no library GEMM, cat or reduce kernels on the step)."""
+
     @staticmethod
     def forward(ctx, x, zc, W, bias):
+        from . import gemm
         IN = x.shape[-1]
         zw = None
         if zc is not None:
-            zw = zc @ W[IN:]
-        if bias is not None:
+            zw = gemm.small_mm(zc, W[IN:], bias) if GROUPED_REDUCE else zc @ W[IN:]
+        if bias is not None and not (zc is not None and GROUPED_REDUCE):
             zw = bias.expand(x.shape[1], -1) if zw is None else zw + bias
         ctx.save_for_backward(x, zc, W)
         ctx.has_bias = bias is not None
@@ -140,12 +154,28 @@ class _BProj(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dxp):
+        from . import gemm
         x, zc, W = ctx.saved_tensors
-        IN = x.shape[-1]
-        S, P = bproj_reduce(x, dxp.contiguous())
-        dW = P if zc is None else torch.cat([P, zc.t() @ S], 0)
-        dzc = S @ W[IN:].t() if zc is not None and ctx.needs_input_grad[1] else None
-        db = S.sum(0) if ctx.has_bias else None
+        T, B, IN = x.shape
+        G = W.shape[1]
+        if not GROUPED_REDUCE:
+            S, P = bproj_reduce(x, dxp.contiguous())
+            dW = P if zc is None else torch.cat([P, zc.t() @ S], 0)
+            dzc = S @ W[IN:].t() if zc is not None and ctx.needs_input_grad[1] else None
+            return None, dzc, dW, S.sum(0) if ctx.has_bias else None
+        S, P = bproj_reduce(x, dxp.contiguous(), raw=True)
+        one = gemm.ones_row(B, x.device)
+        dW = torch.empty_like(W)
+        g = gemm.SmallGroup(x.device)
+        g.mm(one, P.view(B, IN * G), out=dW[:IN].view(1, IN * G))   # sum over rows of the per-row partials
+        dzc = db = None
+        if zc is not None:
+            g.mm(zc.t(), S, out=dW[IN:])
+            if ctx.needs_input_grad[1]:
+                dzc = g.mm(S, W[IN:].t())
+        if ctx.has_bias:
+            db = g.mm(one, S).view(G)
+        g.run()
         return None, dzc, dW, db
 
 

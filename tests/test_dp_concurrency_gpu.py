@@ -92,21 +92,46 @@ def _hyper():
     return run
 
 
+def _ln_lstm():
+    """vae_layernorm decoder shape: LayerNorm-LSTM H 512, B 100 (chained steps
+    both ways when ops.recurrent.LN_CHAIN is on)."""
+    torch.manual_seed(5)
+    T, B, H = 12, 100, 512
+    xp = (torch.randn(T, B, 4 * H, device=DEV) * 0.5).requires_grad_()
+    W = (torch.randn(H, 4 * H, device=DEV) / H ** 0.5).requires_grad_()
+    h0 = torch.zeros(B, H, device=DEV)
+    lnp = [torch.ones(4 * H, device=DEV).requires_grad_(), torch.zeros(4 * H, device=DEV).requires_grad_(),
+           torch.ones(H, device=DEV).requires_grad_(), torch.zeros(H, device=DEV).requires_grad_()]
+    seed = torch.tensor([7], device=DEV)
+    w = torch.randn(T, B, H, device=DEV)
+    params = [xp, W] + lnp
+
+    def run():
+        out, _ = ops.lstm_sequence(xp, W, h0, h0, drop_keep=0.9, drop_seed=seed, drop_stream=4, ln=tuple(lnp))
+        g = torch.autograd.grad((out * w).sum(), params)
+        return [out.detach()] + [t.clone() for t in g]
+    return run
+
+
 @pytest.mark.parametrize("hog", HOGS, ids=[h[0] for h in HOGS])
-@pytest.mark.parametrize("which", ["persist_encoder", "clustered_hyper", "chain_bwd_main"])
+@pytest.mark.parametrize("which", ["persist_encoder", "clustered_hyper", "chain_bwd_main", "chain_ln"])
 def test_handoff_kernels_survive_concurrent_occupancy(which, hog, monkeypatch):
     """``clustered_hyper``: the HyperLSTM with the unchained backward
     launches; ``chain_bwd_main``: the same run with the chained backward
     launch on and counted (csrc/chain_step.hip: main-cell rows spin on the
     arrival counter of producer tiles of their own launch; producers never
-    wait, so a hog can only delay them) -- T - 1 = 11 chained launches per run."""
+    wait, so a hog can only delay them) -- T - 1 = 11 chained launches per
+    run; ``chain_ln``: the LayerNorm-LSTM's chained steps (skr_chain_ln_fwd /
+    _bwd, the same producer-rows construction), T + T - 1 launches per run."""
     from sketch_rnn_amd.ops import hyper
-    from sketch_rnn_amd.ops.recurrent import ROW_STATS
+    from sketch_rnn_amd.ops.recurrent import LN_CHAIN_STATS, ROW_STATS
     ops.set_backend("hip")
     ops.set_compute_dtype("bf16")
     monkeypatch.setattr(hyper, "CHAIN", which == "chain_bwd_main")
-    run = _encoder() if which == "persist_encoder" else _hyper()
+    monkeypatch.setattr(recurrent, "LN_CHAIN", which == "chain_ln")
+    run = {"persist_encoder": _encoder, "chain_ln": _ln_lstm}.get(which, _hyper)()
     n_chain = ROW_STATS["chain"]
+    n_ln = dict(LN_CHAIN_STATS)
     run()                                  # lazy setup (weight caches, occupancy queries)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -129,6 +154,8 @@ def test_handoff_kernels_survive_concurrent_occupancy(which, hog, monkeypatch):
         assert torch.equal(a, b)
     if which == "chain_bwd_main":   # setup + solo + hog runs, 11 chained launches each
         assert ROW_STATS["chain"] - n_chain == 3 * 11, ROW_STATS["chain"] - n_chain
+    if which == "chain_ln":         # setup + solo + hog runs, T = 12 forward and 11 backward launches each
+        assert (LN_CHAIN_STATS["fwd"] - n_ln["fwd"], LN_CHAIN_STATS["bwd"] - n_ln["bwd"]) == (3 * 12, 3 * 11)
     print(json.dumps({"kernels": which, "hog": name, "hog_ms": us / 1e3, "solo_ms": round(solo_ms, 2),
                       "with_hog_ms": round(both_ms, 2)}))
 
