@@ -22,11 +22,20 @@ __device__ __forceinline__ float ldx(const void* x, int64_t i) {
     else return ((const float*)x)[i];
 }
 
-// V consecutive columns from element offset i (V = 4: one 8-byte bf16 or
-// 16-byte fp32 vector load per row; V = 1: scalar)
+// V consecutive columns from element offset i (V = 8: one 16-byte bf16 load;
+// V = 4: one 8-byte bf16 or 16-byte fp32 vector load per row; V = 1: scalar)
 template <bool BF, int V>
 __device__ __forceinline__ void ldv(const void* x, int64_t i, float (&v)[V]) {
-    if constexpr (V == 4) {
+    if constexpr (V == 8) {
+        static_assert(BF, "8-column loads: bf16 only");
+        const uint4 u = *(const uint4*)((const __hip_bfloat16*)x + i);
+        const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            v[2 * k] = __uint_as_float(w[k] << 16);
+            v[2 * k + 1] = __uint_as_float(w[k] & 0xffff0000u);
+        }
+    } else if constexpr (V == 4) {
         if constexpr (BF) {
             const uint2 u = *(const uint2*)((const __hip_bfloat16*)x + i);
             v[0] = __uint_as_float(u.x << 16);
@@ -186,8 +195,9 @@ SKR_API int skr_colsum2(const void* X, int x_kind, const void* Y, int y_kind, in
 // beta gradients of a HyperLSTM step are four: [T*B, 8192 | 2048 | 1024 |
 // 256]). The narrow ones are latency-bound and would each pay a kernel
 // boundary and a tail on their own; here their workgroups fill the chip
-// beside the wide one's. Vector path only (four columns per thread: C, the
-// strides and the bases multiples of 4 elements / 16 bytes).
+// beside the wide one's. Vector path only (NC columns per thread: C, the
+// strides and the bases multiples of NC elements; NC = 8 -- one 16-byte load
+// per row and operand -- when every operand is bf16, else 4).
 struct CsJob {
     const void* X; const void* Y;          // Y may be null
     int64_t R1, s1, R2, s2;
@@ -199,7 +209,7 @@ constexpr int kCsMax = 4;
 struct CsJobs {
     CsJob j[kCsMax];
     int n;
-    int start[kCsMax + 1];                  // first-pass workgroups: prefix sums of RS * ceil(C / 1024)
+    int start[kCsMax + 1];                  // first-pass workgroups: prefix sums of RS * ceil(C / (256 NC))
     int fstart[kCsMax + 1];                 // finish workgroups: prefix sums of ceil(C / 64)
 };
 
@@ -207,38 +217,42 @@ namespace {
 
 // KIND 0: operand dtypes read per job at run time; KIND 1: every X and Y
 // bf16 (the LayerNorm saves of bf16 training), fixed at compile time
-template <int KIND>
-__device__ __forceinline__ void ld4(const void* x, int64_t i, bool bf, float (&v)[4]) {
-    if (KIND == 1 || bf) ldv<true, 4>(x, i, v);
+template <int KIND, int NC>
+__device__ __forceinline__ void ldn(const void* x, int64_t i, bool bf, float (&v)[NC]) {
+    if constexpr (NC == 8) ldv<true, 8>(x, i, v);
+    else if (KIND == 1 || bf) ldv<true, 4>(x, i, v);
     else ldv<false, 4>(x, i, v);
 }
 
-// Thread mapping per job: cq = min(C / 4, 256) column quads x rg = 256 / cq
-// row groups per workgroup (narrow reductions: C = 256 -> 64 x 4), the
+// Thread mapping per job: cq = min(C / NC, 256) column groups x rg = 256 / cq
+// row groups per workgroup (narrow reductions: C = 256, NC = 4 -> 64 x 4), the
 // workgroup's rows split over the row groups and the groups summed in LDS
 // in a fixed order, one partial row per workgroup: narrow reductions keep
 // 256 threads busy per workgroup and few rows in flight per thread.
 constexpr int kCsRowsInFlight = 8;
 
-template <int KIND>
+template <int KIND, int NC>
 __global__ __launch_bounds__(256) void colsum_multi_kernel(const CsJobs jobs) {
-    __shared__ float red[2][256][4];
+    static_assert(NC == 4 || (NC == 8 && KIND == 1), "8 columns per thread: bf16 operands");
+    __shared__ float red[2][256][NC];
     int q = 0;
     while (q + 1 < jobs.n && (int)blockIdx.x >= jobs.start[q + 1]) ++q;
     const CsJob& J = jobs.j[q];
     const int local = blockIdx.x - jobs.start[q];
-    const int cq = min(J.C / 4, 256), rg = 256 / cq;
-    const int cb = (J.C / 4 + cq - 1) / cq;
+    const int cq = min(J.C / NC, 256), rg = 256 / cq;
+    const int cb = (J.C / NC + cq - 1) / cq;
     const int rs = local / cb, cbi = local - rs * cb;
     const int tq = threadIdx.x % cq, grp = threadIdx.x / cq;
-    const int c = (cbi * cq + tq) * 4;
+    const int c = (cbi * cq + tq) * NC;
     const bool on = c < J.C && grp < rg;
     const int64_t R = J.R1 * J.R2;
     const int64_t per = (R + J.RS - 1) / J.RS;
     const int64_t w0 = rs * per, w1 = min(R, w0 + per);
     const int64_t gper = (w1 - w0 + rg - 1) / rg;
     const int64_t r0 = w0 + grp * gper, r1 = min(w1, r0 + gper);
-    float sxy[4] = {0.f, 0.f, 0.f, 0.f}, sx[4] = {0.f, 0.f, 0.f, 0.f};
+    float sxy[NC], sx[NC];
+#pragma unroll
+    for (int e = 0; e < NC; ++e) sxy[e] = sx[e] = 0.f;
     if (on && r0 < r1) {
         int64_t i = r0 / J.R2, j = r0 % J.R2;
         int64_t r = r0;
@@ -246,15 +260,15 @@ __global__ __launch_bounds__(256) void colsum_multi_kernel(const CsJobs jobs) {
         // order: the result does not depend on the unroll)
         constexpr int U = kCsRowsInFlight;
         for (; r + U <= r1; r += U) {
-            float xv[U][4], yv[U][4];
+            float xv[U][NC], yv[U][NC];
 #pragma unroll
             for (int k = 0; k < U; ++k) {
                 const int64_t off = i * J.s1 + j * J.s2 + c;
-                ld4<KIND>(J.X, off, J.xbf, xv[k]);
-                if (J.Y) ld4<KIND>(J.Y, off, J.ybf, yv[k]);
+                ldn<KIND, NC>(J.X, off, J.xbf, xv[k]);
+                if (J.Y) ldn<KIND, NC>(J.Y, off, J.ybf, yv[k]);
                 else
 #pragma unroll
-                    for (int e = 0; e < 4; ++e) yv[k][e] = 0.f;
+                    for (int e = 0; e < NC; ++e) yv[k][e] = 0.f;
                 if (++j == J.R2) {
                     j = 0;
                     ++i;
@@ -263,18 +277,21 @@ __global__ __launch_bounds__(256) void colsum_multi_kernel(const CsJobs jobs) {
 #pragma unroll
             for (int k = 0; k < U; ++k)
 #pragma unroll
-                for (int e = 0; e < 4; ++e) {
+                for (int e = 0; e < NC; ++e) {
                     sx[e] += xv[k][e];
                     sxy[e] += xv[k][e] * yv[k][e];
                 }
         }
         for (; r < r1; ++r) {
             const int64_t off = i * J.s1 + j * J.s2 + c;
-            float xv[4], yv[4] = {0.f, 0.f, 0.f, 0.f};
-            ld4<KIND>(J.X, off, J.xbf, xv);
-            if (J.Y) ld4<KIND>(J.Y, off, J.ybf, yv);
+            float xv[NC], yv[NC];
+            ldn<KIND, NC>(J.X, off, J.xbf, xv);
+            if (J.Y) ldn<KIND, NC>(J.Y, off, J.ybf, yv);
+            else
 #pragma unroll
-            for (int e = 0; e < 4; ++e) {
+                for (int e = 0; e < NC; ++e) yv[e] = 0.f;
+#pragma unroll
+            for (int e = 0; e < NC; ++e) {
                 sx[e] += xv[e];
                 sxy[e] += xv[e] * yv[e];
             }
@@ -287,32 +304,38 @@ __global__ __launch_bounds__(256) void colsum_multi_kernel(const CsJobs jobs) {
     const int64_t o = (int64_t)rs * J.C + c;
     if (rg == 1) {
         if (on) {
-            *(float4*)(J.part_x + o) = float4{sx[0], sx[1], sx[2], sx[3]};
-            if (J.Y) *(float4*)(J.part_xy + o) = float4{sxy[0], sxy[1], sxy[2], sxy[3]};
+#pragma unroll
+            for (int e = 0; e < NC; e += 4) {
+                *(float4*)(J.part_x + o + e) = float4{sx[e], sx[e + 1], sx[e + 2], sx[e + 3]};
+                if (J.Y) *(float4*)(J.part_xy + o + e) = float4{sxy[e], sxy[e + 1], sxy[e + 2], sxy[e + 3]};
+            }
         }
         return;
     }
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
+    for (int e = 0; e < NC; ++e) {
         red[0][threadIdx.x][e] = sx[e];
         red[1][threadIdx.x][e] = sxy[e];
     }
     __syncthreads();
     if (grp != 0 || !on) return;
-    float tx[4], txy[4];
+    float tx[NC], txy[NC];
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
+    for (int e = 0; e < NC; ++e) {
         tx[e] = red[0][tq][e];
         txy[e] = red[1][tq][e];
     }
     for (int g2 = 1; g2 < rg; ++g2)   // fixed order: deterministic
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
+        for (int e = 0; e < NC; ++e) {
             tx[e] += red[0][g2 * cq + tq][e];
             txy[e] += red[1][g2 * cq + tq][e];
         }
-    *(float4*)(J.part_x + o) = float4{tx[0], tx[1], tx[2], tx[3]};
-    if (J.Y) *(float4*)(J.part_xy + o) = float4{txy[0], txy[1], txy[2], txy[3]};
+#pragma unroll
+    for (int e = 0; e < NC; e += 4) {
+        *(float4*)(J.part_x + o + e) = float4{tx[e], tx[e + 1], tx[e + 2], tx[e + 3]};
+        if (J.Y) *(float4*)(J.part_xy + o + e) = float4{txy[e], txy[e + 1], txy[e + 2], txy[e + 3]};
+    }
 }
 
 // colsum_finish of every job, one launch (the same fixed summation order)
@@ -350,30 +373,34 @@ __global__ __launch_bounds__(256) void colsum_multi_finish(const CsJobs jobs) {
 
 }  // namespace
 
-// n <= 4 column reductions (CsJob each), both passes, two launches in all.
-// Returns -2 / -4 for a job the vector path does not take (callers then use
-// skr_colsum2 per job).
-SKR_API int skr_colsum_multi(const CsJob* jobs, int n, hipStream_t s) {
-    if (n < 1 || n > kCsMax) return -2;
+// n <= 4 column reductions (CsJob each), both passes, two launches in all;
+// nc: columns per thread (8: every operand bf16, C / strides multiples of 8,
+// 16-byte aligned bases; else 4) -- the caller sizes RS for it
+// (ops/reduce.py colsum_many). Returns -2 / -4 for a job the vector path
+// does not take (callers then use skr_colsum2 per job).
+SKR_API int skr_colsum_multi(const CsJob* jobs, int n, int nc, hipStream_t s) {
+    if (n < 1 || n > kCsMax || (nc != 4 && nc != 8)) return -2;
     CsJobs g{};
     g.n = n;
+    bool all_bf = true;
+    for (int q = 0; q < n; ++q) all_bf = all_bf && jobs[q].xbf && (jobs[q].Y == nullptr || jobs[q].ybf);
+    if (nc == 8 && !all_bf) return -2;
     for (int q = 0; q < n; ++q) {
         const CsJob& J = jobs[q];
-        if (J.C <= 0 || J.C % 4 || J.RS <= 0 || J.R1 * J.R2 <= 0 || J.s1 % 4 || J.s2 % 4) return -2;
+        if (J.C <= 0 || J.C % nc || J.RS <= 0 || J.R1 * J.R2 <= 0 || J.s1 % nc || J.s2 % nc) return -2;
         if ((((uintptr_t)J.X | (uintptr_t)(J.Y ? J.Y : J.X)) & 15) ||
             (((uintptr_t)J.part_x | (uintptr_t)(J.Y ? J.part_xy : J.part_x)) & 15))
             return -4;
         g.j[q] = J;
-        const int cq = J.C / 4 < 256 ? J.C / 4 : 256;
-        if (256 % cq != 0 && cq != 256) return -2;   // narrow C: C / 4 must divide 256
-        g.start[q + 1] = g.start[q] + J.RS * ((J.C / 4 + cq - 1) / cq);
+        const int cq = J.C / nc < 256 ? J.C / nc : 256;
+        if (256 % cq != 0 && cq != 256) return -2;   // narrow C: C / nc must divide 256
+        g.start[q + 1] = g.start[q] + J.RS * ((J.C / nc + cq - 1) / cq);
         g.fstart[q + 1] = g.fstart[q] + (J.C + 63) / 64;
     }
     for (int q = n + 1; q <= kCsMax; ++q) g.start[q] = g.start[n], g.fstart[q] = g.fstart[n];
-    bool all_bf = true;
-    for (int q = 0; q < n; ++q) all_bf = all_bf && jobs[q].xbf && (jobs[q].Y == nullptr || jobs[q].ybf);
-    if (all_bf) hipLaunchKernelGGL(colsum_multi_kernel<1>, dim3(g.start[n]), dim3(256), 0, s, g);
-    else hipLaunchKernelGGL(colsum_multi_kernel<0>, dim3(g.start[n]), dim3(256), 0, s, g);
+    if (nc == 8) hipLaunchKernelGGL((colsum_multi_kernel<1, 8>), dim3(g.start[n]), dim3(256), 0, s, g);
+    else if (all_bf) hipLaunchKernelGGL((colsum_multi_kernel<1, 4>), dim3(g.start[n]), dim3(256), 0, s, g);
+    else hipLaunchKernelGGL((colsum_multi_kernel<0, 4>), dim3(g.start[n]), dim3(256), 0, s, g);
     hipLaunchKernelGGL(colsum_multi_finish, dim3(g.fstart[n]), dim3(256), 0, s, g);
     return SKR_CHECK_LAUNCH();
 }

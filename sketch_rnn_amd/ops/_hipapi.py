@@ -364,6 +364,8 @@ class HipLib:
         lib.skr_bproj_fwd.restype = _i
         lib.skr_bproj_bwd.argtypes = [_p, _p, _i, _i64, _p, _p, _i, _i, _i, _i, _p]
         lib.skr_bproj_bwd.restype = _i
+        lib.skr_bproj_set_wide.argtypes = [_i]
+        lib.skr_bproj_set_wide.restype = _i
         lib.skr_colsum.argtypes = [_p, _i, _p, _i, _i64, _i64, _i64, _i64, _i, _i, _p, _p, _p]
         lib.skr_colsum.restype = _i
         lib.skr_wgrad.argtypes = [_p, _i64, _i64, _p, _i64, _i64, _i64, _i, _i, _i, _i, _p, _p, _p, _p, _p]
@@ -438,7 +440,7 @@ class HipLib:
         lib.skr_lstm_persist_bwd.restype = _i
         lib.skr_small_gemm_group.argtypes = [C.POINTER(SgProb), _i, _p]
         lib.skr_small_gemm_group.restype = _i
-        lib.skr_colsum_multi.argtypes = [C.POINTER(CsJob), _i, _p]
+        lib.skr_colsum_multi.argtypes = [C.POINTER(CsJob), _i, _i, _p]
         lib.skr_colsum_multi.restype = _i
         lib.skr_persist_set_spin_limit.argtypes = [C.c_uint]
         lib.skr_persist_set_spin_limit.restype = _i

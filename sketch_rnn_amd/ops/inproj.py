@@ -106,6 +106,13 @@ def bproj_fwd(x, W, zw=None, bf16: bool = False):
     return xp
 
 
+# bproj_reduce on the wide kernel (csrc/inproj.hip bproj_bwd_wide: 16-byte
+# loads, the T steps split over 4 waves) where its alignment holds; False:
+# the narrow kernel (the A/B arm).
+BPROJ_WIDE = True
+_WIDE_SET = [None]
+
+
 def bproj_reduce(x, dxp, raw: bool = False):
     """One read of ``dxp [T, B, G]`` (fp32 or bf16, rows may be strided):
     ``S[b] = sum_t dxp[t, b]`` and ``P = sum_{t,b} x[t, b]^T dxp[t, b]`` ([IN, G]);
@@ -118,6 +125,9 @@ def bproj_reduce(x, dxp, raw: bool = False):
     kind = 1 if dxp.dtype == torch.bfloat16 else 2
     if kind == 2 and dxp.dtype != torch.float32:
         dxp = dxp.float().contiguous()
+    if _WIDE_SET[0] != BPROJ_WIDE:
+        lib.lib.skr_bproj_set_wide(int(BPROJ_WIDE))
+        _WIDE_SET[0] = BPROJ_WIDE
     S = torch.empty(B, G, device=x.device, dtype=torch.float32)
     P = torch.empty(B, IN, G, device=x.device, dtype=torch.float32)
     rc = lib.lib.skr_bproj_bwd(x.contiguous().data_ptr(), dxp.data_ptr(), kind, dxp.stride(1), S.data_ptr(),

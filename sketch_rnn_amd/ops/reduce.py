@@ -48,6 +48,11 @@ def colsum(x: torch.Tensor, y: Optional[torch.Tensor] = None, splits: Optional[i
     return (tot[0] if y is not None else None), tot[1]
 
 
+# Columns per thread of colsum_many when every operand is bf16 (8: one
+# 16-byte load per row and operand; 4: the A/B arm, 8-byte loads).
+COLSUM_NC = 8
+
+
 def colsum_many(pairs, splits=None):
     """:func:`colsum` of several ``(x, y)`` pairs (``[R, C]`` or ``[R1, R2, C]``
     views with a contiguous last dim, y may be None) in two launches for all of them (csrc/reduce.hip
@@ -76,6 +81,13 @@ def colsum_many(pairs, splits=None):
     lib = native.require_hip()
     jobs = (CsJob * len(pairs))()
     keep, outs = [], []
+    # 8 columns per thread: bf16 operands, C and the row strides multiples of 8
+    # (narrow C: C / 8 divides 256); the row slices are sized for the
+    # workgroup's 256 * nc columns
+    nc = 8 if COLSUM_NC == 8 and all(
+        x.dtype == torch.bfloat16 and (y is None or y.dtype == torch.bfloat16) and x.shape[-1] % 8 == 0
+        and x.stride(0) % 8 == 0 and x.stride(1) % 8 == 0 and (x.shape[-1] >= 2048 or 256 % (x.shape[-1] // 8) == 0)
+        for x, y in pairs) else 4
     # the widest (longest-running) reduction's workgroups are dispatched
     # first; the narrow ones fill the slots beside and after it
     order = sorted(range(len(pairs)), key=lambda i: -pairs[i][0].shape[-1])
@@ -86,8 +98,8 @@ def colsum_many(pairs, splits=None):
         if splits:
             RS = splits[i]
         else:
-            RS = -(-1024 // -(-C // 1024))
-            if C <= 1024:
+            RS = -(-1024 // -(-C // (256 * nc)))
+            if C <= 256 * nc:
                 RS = min(RS, 256)
         RS = max(1, min(RS, R // 16))
         part = torch.empty(2, RS, C, device=x.device, dtype=torch.float32)
@@ -101,7 +113,7 @@ def colsum_many(pairs, splits=None):
         J.out_xy, J.out_x = tot[0].data_ptr(), tot[1].data_ptr()
         keep.append(part)
         outs.append((i, tot, y is not None))
-    rc = lib.lib.skr_colsum_multi(jobs, len(pairs), torch.cuda.current_stream().cuda_stream)
+    rc = lib.lib.skr_colsum_multi(jobs, len(pairs), nc, torch.cuda.current_stream().cuda_stream)
     if rc != 0:
         raise RuntimeError("skr_colsum_multi failed (%d)" % rc)
     res = [None] * len(pairs)

@@ -576,6 +576,37 @@ def test_stroke_input_proj_matches_torch(with_z, with_bias):
     _close(res[0][1:], res[1][1:], 1e-4, 1e-3, "grad")
 
 
+@pytest.mark.parametrize("T,B,G,dt,pad", [(250, 100, 8192, torch.bfloat16, 0), (37, 11, 1000, torch.bfloat16, 24),
+                                          (29, 7, 2052, torch.float32, 0), (5, 3, 1001, torch.float32, 0)])
+def test_bproj_reduce_wide_vs_narrow(T, B, G, dt, pad):
+    """csrc/inproj.hip bproj_bwd_wide (16-byte loads, T split over 4 waves,
+    wave-order LDS sum) against the narrow kernel and the fp32 oracle: S =
+    sum_t dxp, P = sum_t x^T dxp per row, strided rows (pad) and partial
+    column blocks included; G = 1001 takes the narrow kernel (no 16-byte
+    alignment) under both settings."""
+    from sketch_rnn_amd.ops import inproj
+    torch.manual_seed(G)
+    x = torch.randn(T, B, 5, device=DEV)
+    buf = torch.randn(T, B, G + pad, device=DEV).to(dt)
+    dxp = buf[..., :G]
+    res = {}
+    saved = inproj.BPROJ_WIDE
+    try:
+        for wide in (False, True):
+            inproj.BPROJ_WIDE = wide
+            res[wide] = inproj.bproj_reduce(x, dxp, raw=True)
+    finally:
+        inproj.BPROJ_WIDE = saved
+    d = dxp.float()
+    refS = d.sum(0)
+    refP = torch.einsum("tbi,tbg->big", x, d)
+    for S, P in res.values():
+        assert (S - refS).abs().max().item() <= 1e-4 * refS.abs().max().item() + 1e-4
+        assert (P - refP).abs().max().item() <= 1e-4 * refP.abs().max().item() + 1e-4
+    if G % (8 if dt == torch.bfloat16 else 4):
+        assert torch.equal(res[True][0], res[False][0]) and torch.equal(res[True][1], res[False][1])
+
+
 def test_hyper_sequence_with_broadcast_z_matches_oracle():
     """HyperLSTM with a stroke-5 input + per-sequence z (bproj path) vs the
     oracle on the concatenated input."""
@@ -787,6 +818,39 @@ def test_colsum_many_equals_colsum():
     for (x, y), (gxy, gx) in zip(pairs, dflt):
         ref = x.float().sum(0)
         assert (gx - ref).abs().max().item() <= 1e-3 * ref.abs().max().item() + 1e-3
+
+
+def test_colsum_many_eight_columns_per_thread(monkeypatch):
+    """skr_colsum_multi nc = 8 (every operand bf16: one 16-byte load per row
+    and operand) against nc = 4 at the same row slices: bit for bit where
+    both keep one row group per column (C >= 2048), and every result -- the
+    narrow row-group layouts and a strided [T, nd, B, C] direction view
+    included -- against the fp32 oracle, at explicit and default slices."""
+    from sketch_rnn_amd.ops import reduce
+    torch.manual_seed(4)
+    bf = torch.bfloat16
+    T, nd, B = 50, 2, 50
+    enc = torch.randn(T, nd, B, 512, device=DEV).to(bf)
+    ency = torch.randn(T, nd, B, 512, device=DEV).to(bf)
+    pairs = [(torch.randn(2500, 8192, device=DEV).to(bf), torch.randn(2500, 8192, device=DEV).to(bf)),
+             (torch.randn(2500, 2048, device=DEV).to(bf), None),
+             (torch.randn(2500, 256, device=DEV).to(bf), torch.randn(2500, 256, device=DEV).to(bf)),
+             (enc[:, 1], ency[:, 1])]
+    for splits in ([64, 100, 48, 30], None):
+        res = {}
+        for nc in (4, 8):
+            monkeypatch.setattr(reduce, "COLSUM_NC", nc)
+            res[nc] = reduce.colsum_many(pairs, splits)
+        for (x, y), (a_xy, a_x), (b_xy, b_x) in zip(pairs, res[4], res[8]):
+            if splits is not None and x.shape[-1] >= 2048:
+                assert torch.equal(a_x, b_x)
+                if y is not None:
+                    assert torch.equal(a_xy, b_xy)
+            refx = x.float().sum((0, 1)) if x.dim() == 3 else x.float().sum(0)
+            assert (b_x - refx).abs().max().item() <= 1e-3 * refx.abs().max().item() + 1e-3
+            if y is not None:
+                ref = (x.float() * y.float()).sum((0, 1)) if x.dim() == 3 else (x.float() * y.float()).sum(0)
+                assert (b_xy - ref).abs().max().item() <= 1e-3 * ref.abs().max().item() + 1e-3
 
 
 @pytest.mark.parametrize("shape,xdt,with_y", [((250, 100, 512), torch.float32, True), ((3, 7, 300), torch.bfloat16, False),
