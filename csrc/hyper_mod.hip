@@ -60,6 +60,7 @@ struct ModDecode {
     const float* x5;
     const float* w5; int64_t ldw5;
     const float* zp; int64_t ldzp;
+    int probe;                                // timing probe (skr_hyper_mod_set_probe; 0 = off), set by the host
 };
 
 namespace {
@@ -170,6 +171,7 @@ __device__ __forceinline__ void mod_block(ModDecode dec, const __hip_bfloat16* _
             r4[k] += t;
         }
     }
+    if (dec.probe == 1) return;                 // (timing probe: dispatch + the P fragments only)
     constexpr int NPC = MB * (HH / 8), SPT = (NPC + NTH - 1) / NTH;     // 16-byte hh pieces per thread
     bf16x8 hv[SPT];
 #pragma unroll
@@ -185,6 +187,13 @@ __device__ __forceinline__ void mod_block(ModDecode dec, const __hip_bfloat16* _
         *(bf16x8*)(sA + sw(r, c)) = hv[k];
     }
     __syncthreads();
+    if (dec.probe == 2) {                       // (timing probe: every load and the LDS stage, no MFMA / epilogue)
+        float t = (float)pf[0][0] + __bfloat162float(sA[tid]);
+#pragma unroll
+        for (int k = 0; k < RPT; ++k) t += x4[k][0] + r4[k][0];
+        if (t == 1.2345e-30f) gout[tid] = t;
+        return;
+    }
     f32x4 acc[NRT];
 #pragma unroll
     for (int rt = 0; rt < NRT; ++rt) acc[rt] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -195,6 +204,15 @@ __device__ __forceinline__ void mod_block(ModDecode dec, const __hip_bfloat16* _
             const bf16x8 a = *(const bf16x8*)(sA + sw(16 * rt + fr, 4 * ks + fq));
             acc[rt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, pf[ks], acc[rt], 0, 0, 0);
         }
+    if (dec.probe == 3) {                       // (timing probe: loads + MFMA, no vector stage / epilogue)
+        float t = 0.f;
+#pragma unroll
+        for (int rt = 0; rt < NRT; ++rt) t += acc[rt][0];
+#pragma unroll
+        for (int k = 0; k < RPT; ++k) t += x4[k][0] + r4[k][0];
+        if (t == 1.2345e-30f) gout[tid] = t;
+        return;
+    }
     // modulation vectors (+ q) -> bf16 -> LDS: the epilogue needs all three
     // blocks of a unit in one thread. The bf16-rounded value is what the
     // backward will read, so g is formed from it too.
@@ -265,6 +283,7 @@ __global__ __launch_bounds__(NTH) void hyper_mod_fwd(ModDecode dec, const __hip_
                                                      int64_t r_slab, __hip_bfloat16* __restrict__ vec,
                                                      float* __restrict__ gout, __hip_bfloat16* __restrict__ rlp,
                                                      float* __restrict__ stats, int B, int H) {
+    if (dec.probe == 4) return;   // (timing probe: dispatch only)
     mod_tile<NS, NRT, false>(dec, hh, ld_hh, PlT, qb, xh, R, r_slab, vec, gout, rlp, stats, B, H, blockIdx.y, blockIdx.x,
                              blockIdx.z, gridDim.z);
 }
@@ -414,6 +433,17 @@ __global__ __launch_bounds__(NTH) void hyper_mod_chain(const __hip_bfloat16* __r
 }  // namespace
 
 static int g_hm_zgrid = 0;   // row blocks in parallel (0: all); skr_hyper_mod_set_zgrid
+static int g_hm_probe = 0;   // timing probe of skr_hyper_mod_fwd (the outputs are WRONG while set)
+
+// Timing probes (scripts/micro/hm_probe.py): 0 off, 1 each row block returns
+// at once (dispatch + P fragment loads), 2 after every load and the hh LDS
+// stage, 3 after the MFMAs (no vector stage, epilogue or stores), 4 every
+// workgroup returns at entry (dispatch only). Returns the previous setting.
+SKR_API int skr_hyper_mod_set_probe(int p) {
+    const int prev = g_hm_probe;
+    if (p >= 0) g_hm_probe = p;
+    return prev;
+}
 
 // A/B hook: parallel row blocks of the wide (B > 128) launches; 0 = one
 // workgroup per row block. Returns the previous setting.
@@ -432,7 +462,8 @@ SKR_API int skr_hyper_mod_set_zgrid(int zg) {
 SKR_API int skr_hyper_mod_fwd(const void* hh, int64_t ld_hh, const void* PlT, const float* qb, const float* xh,
                               const float* R, int64_t r_slab, int nslab, void* vec, float* g, void* rlp,
                               float* stats, int B, int H, int Hh, const ModDecode* dec, hipStream_t s) {
-    const ModDecode dz = dec ? *dec : ModDecode{};
+    ModDecode dz = dec ? *dec : ModDecode{};
+    dz.probe = g_hm_probe;
     if (dz.x5 && (((uintptr_t)dz.w5 | (uintptr_t)dz.zp) & 15 || dz.ldw5 % 4 || dz.ldzp % 4)) return -4;
     if ((dz.x5 == nullptr && xh == nullptr) || hh == nullptr) return -3;
     if (B <= 0) return 0;

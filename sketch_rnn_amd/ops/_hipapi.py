@@ -298,7 +298,7 @@ class ModDecode(C.Structure):
     """Mirror of ``ModDecode`` in csrc/hyper_mod.hip (decode-mode inputs of the
     HyperLSTM modulation kernel: the x-projection from the stroke)."""
     _fields_ = [
-        ("xh_bf16", _i), ("x5", _p), ("w5", _p), ("ldw5", _i64), ("zp", _p), ("ldzp", _i64),
+        ("xh_bf16", _i), ("x5", _p), ("w5", _p), ("ldw5", _i64), ("zp", _p), ("ldzp", _i64), ("probe", _i),
     ]
 
 
@@ -364,6 +364,8 @@ class HipLib:
         lib.skr_bproj_fwd.restype = _i
         lib.skr_bproj_bwd.argtypes = [_p, _p, _i, _i64, _p, _p, _i, _i, _i, _i, _p]
         lib.skr_bproj_bwd.restype = _i
+        lib.skr_hyper_mod_set_probe.argtypes = [_i]
+        lib.skr_hyper_mod_set_probe.restype = _i
         lib.skr_bproj_set_wide.argtypes = [_i]
         lib.skr_bproj_set_wide.restype = _i
         lib.skr_colsum.argtypes = [_p, _i, _p, _i, _i64, _i64, _i64, _i64, _i, _i, _p, _p, _p]
