@@ -86,6 +86,13 @@ __device__ __forceinline__ void block_sum(float (&v)[N], float* lds) {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
 #pragma unroll
     for (int i = 0; i < N; ++i) v[i] = wave_sum(v[i]);
+    if constexpr (NW == 1) {   // one wave: no LDS round trip and no barrier (the same 0 + v as below)
+#pragma unroll
+        for (int i = 0; i < N; ++i) v[i] = 0.f + v[i];
+        (void)lane;
+        (void)lds;
+        return;
+    }
     if (lane == 0) {
 #pragma unroll
         for (int i = 0; i < N; ++i) lds[w * N + i] = v[i];

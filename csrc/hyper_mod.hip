@@ -32,6 +32,7 @@
 // 10.2 us per step, with a slower backward; profiles/r4/unfold_ab.txt.)
 #include "cell_fwd_body.h"
 #include "handoff.h"
+#include "row_cell.h"
 
 namespace {
 
@@ -69,17 +70,21 @@ namespace {
 // NRT: 16-row tiles staged and multiplied (rows up to 16 NRT; a B = 100 launch
 // pays for 112 rows, not MAXB). SC1: g and the partial sums are read by
 // workgroups of the SAME launch (hyper_mod_chain): write-through stores.
-template <int NS, int NRT, bool SC1>
+// WAITHH (hyper_cell_mod): hh is written by workgroups of the SAME launch --
+// every other load is issued first, then the tile waits on the launch's
+// arrival counter (wcnt >= wtarget) and reads hh with sc1 loads.
+template <int NS, int NRT, bool SC1, bool WAITHH = false>
 __device__ __forceinline__ void mod_block(ModDecode dec, const __hip_bfloat16* __restrict__ hh, int64_t ld_hh,
                                           const float* __restrict__ xh, const float* __restrict__ R, int64_t r_slab,
                                           __hip_bfloat16* __restrict__ vec, float* __restrict__ gout,
                                           __hip_bfloat16* __restrict__ rlp, float* __restrict__ stats, int B, int H,
                                           const int q, const int tile, const int z, const bf16x8 (&pf)[8],
-                                          const float qv);
+                                          const float qv, const uint32_t* wcnt = nullptr, uint32_t wtarget = 0,
+                                          int* werr = nullptr);
 
 // One modulation tile: gate q, hidden units [TU tile, +TU), row blocks z0,
 // z0 + zs, ... of B rows (the P fragments loaded once for all of them).
-template <int NS, int NRT, bool SC1>
+template <int NS, int NRT, bool SC1, bool WAITHH = false>
 __device__ __forceinline__ void mod_tile(ModDecode dec, const __hip_bfloat16* __restrict__ hh, int64_t ld_hh,
                                          const __hip_bfloat16* __restrict__ PlT,   // [12H][HH]
                                          const float* __restrict__ qb,             // [12H]
@@ -89,7 +94,8 @@ __device__ __forceinline__ void mod_tile(ModDecode dec, const __hip_bfloat16* __
                                          float* __restrict__ gout,                  // [B][4H]
                                          __hip_bfloat16* __restrict__ rlp,          // [B][4H] or null
                                          float* __restrict__ stats,                 // [B][4][H/TU][2]
-                                         int B, int H, const int q, const int tile, const int z0, const int zs) {
+                                         int B, int H, const int q, const int tile, const int z0, const int zs,
+                                         const uint32_t* wcnt = nullptr, uint32_t wtarget = 0, int* werr = nullptr) {
     const int u0 = tile * TU;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int fr = lane & 15, fq = lane >> 4;
@@ -103,18 +109,19 @@ __device__ __forceinline__ void mod_tile(ModDecode dec, const __hip_bfloat16* __
     // after this block's MFMAs -- every wave passed this block's second
     // barrier -- and its vectors after the next block's first barrier)
     for (int z = z0; z < nblk; z += zs)
-        mod_block<NS, NRT, SC1>(dec, hh, ld_hh, xh, R, r_slab, vec, gout, rlp, stats, B, H, q, tile, z, pf, qv);
+        mod_block<NS, NRT, SC1, WAITHH>(dec, hh, ld_hh, xh, R, r_slab, vec, gout, rlp, stats, B, H, q, tile, z, pf, qv,
+                                        wcnt, wtarget, werr);
 }
 
 // Row block z of a modulation tile (B > MAXB: the wide decode): rows
 // r0 .. r0 + MAXB - 1.
-template <int NS, int NRT, bool SC1>
+template <int NS, int NRT, bool SC1, bool WAITHH>
 __device__ __forceinline__ void mod_block(ModDecode dec, const __hip_bfloat16* __restrict__ hh, int64_t ld_hh,
                                           const float* __restrict__ xh, const float* __restrict__ R, int64_t r_slab,
                                           __hip_bfloat16* __restrict__ vec, float* __restrict__ gout,
                                           __hip_bfloat16* __restrict__ rlp, float* __restrict__ stats, int B, int H,
                                           const int q, const int tile, const int z, const bf16x8 (&pf)[8],
-                                          const float qv) {
+                                          const float qv, const uint32_t* wcnt, uint32_t wtarget, int* werr) {
     constexpr int MB = 16 * NRT;
     {
         const int r0 = z * MAXB;
@@ -174,10 +181,25 @@ __device__ __forceinline__ void mod_block(ModDecode dec, const __hip_bfloat16* _
     if (dec.probe == 1) return;                 // (timing probe: dispatch + the P fragments only)
     constexpr int NPC = MB * (HH / 8), SPT = (NPC + NTH - 1) / NTH;     // 16-byte hh pieces per thread
     bf16x8 hv[SPT];
+    if constexpr (WAITHH) {   // hh from the rows of this launch: after their arrival, sc1 loads
+        if (wcnt != nullptr) {   // (three workgroup barriers per block on every path: hyper_cell_mod's row wave)
+            if (dec.probe == 8) chain_wait<8>(wcnt, wtarget, werr);
+            else chain_wait<1>(wcnt, wtarget, werr);
+        } else {
+            __syncthreads();
+        }
+        const __amdgpu_buffer_rsrc_t hr = rsrc(hh, (int64_t)B * ld_hh * 2);
 #pragma unroll
-    for (int k = 0; k < SPT; ++k) {
-        const int i = min(tid + k * NTH, NPC - 1), r = i / (HH / 8), c = i % (HH / 8);
-        hv[k] = *(const bf16x8*)(hh + (int64_t)min(r, B - 1) * ld_hh + 8 * c);
+        for (int k = 0; k < SPT; ++k) {
+            const int i = min(tid + k * NTH, NPC - 1), r = i / (HH / 8), c = i % (HH / 8);
+            hv[k] = ld_sc1(hr, (uint32_t)(((int64_t)min(r, B - 1) * ld_hh + 8 * c) * 2));
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < SPT; ++k) {
+            const int i = min(tid + k * NTH, NPC - 1), r = i / (HH / 8), c = i % (HH / 8);
+            hv[k] = *(const bf16x8*)(hh + (int64_t)min(r, B - 1) * ld_hh + 8 * c);
+        }
     }
 #pragma unroll
     for (int k = 0; k < SPT; ++k) {
@@ -430,6 +452,59 @@ __global__ __launch_bounds__(NTH) void hyper_mod_chain(const __hip_bfloat16* __r
     main_rows<UPT>(cell, id / C, id % C, C, cs.counters + cs.k, (uint32_t)gridDim.x, cs.err);
 }
 
+// ---- chained launch: the hyper cell rows + the modulation tiles --------------------------
+// One workgroup per modulation tile (gate q, 32 units), as hyper_mod_fwd, plus
+// a seventh wave. In workgroups b < B that wave runs the hyper LayerNorm cell
+// of row b (csrc/row_cell.h row_fwd_body, one wave of Hh / 4 lanes: its block
+// sums need no barrier), stores the bf16 hh row write-through, drains and
+// adds 1 to the launch's arrival counter; then (every workgroup) it joins
+// the tile's three workgroup barriers and ends. The six tile waves issue
+// every load that does not depend on hh -- the P fragments (12.6 MB over
+// the chip: 4.8 of the separate launch's 10.9 us, scripts/micro/hm_probe.py),
+// the x-projection and the R slabs -- then wait for all B rows and read hh
+// with sc1 loads. Rows never wait before they arrive and every workgroup is
+// one per CU (LDS), so the waits cannot starve a row of residency. One launch
+// per forward step instead of the hyper cell + modulation pair.
+// Measured and NOT adopted (ops.hyper.CELL_MOD, default off): 28.2 us per
+// launch against 4.9 + 10.9 for the pair (vae_large 26.2 vs 23.65 ms/step,
+// profiles/r6/cm2/); probes: tiles that do not wait 24.9 us, no rows 13.5 --
+// the one-wave row takes ~11 us inside the launch, where the clustered hyper
+// cell spends 4.9 on four 256-thread workgroups per row. (Run by wave 0 of
+// the tile instead: 20.8 us, its row serialised before the wave's own P
+// fetch; inside the tile after the loads are in flight: 122 VGPRs spilled.)
+constexpr int NTH_HCM = NTH + 64;
+
+template <int NS, int NRT>
+__global__ __launch_bounds__(NTH_HCM) void hyper_cell_mod(const FwdArgs hc, const __hip_bfloat16* __restrict__ PlT,
+                                                          const float* __restrict__ qb, const float* __restrict__ xh,
+                                                          int xh_bf16, const float* __restrict__ R, int64_t r_slab,
+                                                          __hip_bfloat16* __restrict__ vec, float* __restrict__ gout,
+                                                          __hip_bfloat16* __restrict__ rlp, float* __restrict__ stats,
+                                                          int H, const ChainSync cs, const int probe) {
+    const int id = blockIdx.x, B = hc.B, ntile = H / TU;
+    if (id == 0) chain_rotate(cs.counters, cs.n, cs.k);
+    // (timing probes, skr_hyper_mod_set_probe; outputs WRONG: 5 the tiles do not
+    // wait, 6 no rows and no wait; 8: poll period 8 s_sleep units -- correct)
+    if (__builtin_amdgcn_readfirstlane(threadIdx.x) >= NTH) {   // the row wave
+        if (id < B && probe != 6) {
+            row_fwd_body<HH / 4, 4, 0, 4, false, true>(hc, id, nullptr, 0, nullptr, NTH);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if (threadIdx.x == NTH)
+                __hip_atomic_fetch_add(cs.counters + cs.k, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        __syncthreads();   // the tile's barriers: after the wait, the hh stage, the vector stage
+        __syncthreads();
+        __syncthreads();
+        return;
+    }
+    ModDecode dec{};
+    dec.xh_bf16 = xh_bf16;
+    dec.probe = probe == 8 ? 8 : 0;
+    mod_tile<NS, NRT, false, true>(dec, (const __hip_bfloat16*)hc.h_lp, hc.ld_lp, PlT, qb, xh, R, r_slab, vec, gout,
+                                   rlp, stats, B, H, id / ntile, id % ntile, 0, 1,
+                                   (probe == 5 || probe == 6) ? nullptr : cs.counters + cs.k, (uint32_t)B, cs.err);
+}
+
 }  // namespace
 
 static int g_hm_zgrid = 0;   // row blocks in parallel (0: all); skr_hyper_mod_set_zgrid
@@ -544,5 +619,44 @@ SKR_API int skr_hyper_mod_chain(const void* hh, int64_t ld_hh, const void* PlT, 
     void* args[] = {(void*)&ap, (void*)&ld_hh, (void*)&pp, (void*)&qb, (void*)&xh, (void*)&xh_bf16, (void*)&R,
                     (void*)&r_slab, (void*)&v, (void*)&rl, (void*)&a, (void*)&C, (void*)cs};
     if (hipLaunchKernel(k, dim3(grid), dim3(NTH), args, 0, s) != hipSuccess) return -1;
+    return SKR_CHECK_LAUNCH();
+}
+
+// Hyper cell step + modulation step in one launch (hyper_cell_mod). hc: the
+// hyper LayerNorm cell (H = 256 units, mod 0: xp + the R slabs, bf16 h_lp =
+// the tiles' hh operand, no resets); the modulation operands as
+// skr_hyper_mod_fwd with the training layout (xh precomputed). 65 <= B <= 128.
+// Returns -2 / -3 / -4 when not taken (the caller runs the two launches).
+SKR_API int skr_hyper_cell_mod(const FwdArgs* hc, const void* PlT, const float* qb, const float* xh, int xh_bf16,
+                               const float* R, int64_t r_slab, int nslab, void* vec, float* g, void* rlp, float* stats,
+                               int H, const ChainSync* cs, hipStream_t s) {
+    if (hc == nullptr || cs == nullptr || cs->counters == nullptr || cs->n < 2 || cs->k < 0 || cs->k >= cs->n ||
+        cs->err == nullptr)
+        return -6;
+    const FwdArgs& a = *hc;
+    const int B = a.B;
+    if (B < 65 || B > MAXB || a.H != HH || H % TU != 0 || a.lp_kind != 1 || a.h_lp == nullptr || a.grp_rows > 0 ||
+        a.R_nslab < 1 || xh == nullptr)
+        return -2;
+    const int rc = row_fwd_check(a, 0);
+    if (rc) return rc;
+    if (((uintptr_t)a.h_lp | (uintptr_t)PlT | (uintptr_t)xh | (uintptr_t)R | (uintptr_t)vec | (uintptr_t)g |
+         (uintptr_t)rlp) & 15 || (a.ld_lp % 8) || (r_slab % 4))
+        return -4;
+    if (nslab != 1 && nslab != 2 && nslab != 4) return -3;
+    const int grid = 4 * (H / TU);
+    if (grid < B) return -2;   // (every row needs a host workgroup)
+    const auto* p = (const __hip_bfloat16*)PlT;
+    auto* v = (__hip_bfloat16*)vec;
+    auto* rl = (__hip_bfloat16*)rlp;
+#define SKR_HCM(NS_, NRT_) \
+    hipLaunchKernelGGL((hyper_cell_mod<NS_, NRT_>), dim3(grid), dim3(NTH_HCM), 0, s, a, p, qb, xh, xh_bf16, R, r_slab, v, \
+                       g, rl, stats, H, *cs, g_hm_probe)
+#define SKR_HCM_NS(NRT_) \
+    do { if (nslab == 1) SKR_HCM(1, NRT_); else if (nslab == 2) SKR_HCM(2, NRT_); else SKR_HCM(4, NRT_); } while (0)
+    if (B <= 112) SKR_HCM_NS(7);
+    else SKR_HCM_NS(8);
+#undef SKR_HCM_NS
+#undef SKR_HCM
     return SKR_CHECK_LAUNCH();
 }

@@ -133,13 +133,17 @@ __device__ __forceinline__ void row_exchange(float (&v)[N], float* mine, float* 
 // CHAIN (csrc/chain_step.hip, MOD 0): the R slabs are produced by tiles of
 // the SAME launch -- every other load is issued first, then the row waits on
 // the launch's arrival counter and reads the slabs with sc1 loads.
-template <int NT, int V, int MOD, int DS, bool CHAIN = false>
+// HSC1 (csrc/hyper_mod.hip hyper_cell_mod): the bf16 next-step operand h_lp
+// is read by workgroups of the SAME launch after the row's arrival, so it is
+// stored write-through (8-byte relaxed agent-scope stores, lp_kind 1 only).
+template <int NT, int V, int MOD, int DS, bool CHAIN = false, bool HSC1 = false>
 __device__ __forceinline__ void row_fwd_body(const FwdArgs& a, const int b, const uint32_t* chain_cnt = nullptr,
-                                             uint32_t chain_target = 0, int* chain_err = nullptr) {
+                                             uint32_t chain_target = 0, int* chain_err = nullptr, const int tid0 = 0) {
     static_assert(!CHAIN || (V == 4 && MOD == 0), "chained forward row: MOD 0, 16-byte slab loads");
+    static_assert(!HSC1 || V == 4, "write-through h_lp: 8-byte stores");
     constexpr int NW = NT / 64;
     __shared__ float lds[NW * 8];
-    const int tid = threadIdx.x, H = a.H, u0 = tid * V;
+    const int tid = threadIdx.x - tid0, H = a.H, u0 = tid * V;   // tid0: first thread of the row (one-wave rows)
     const int grp = a.grp_rows > 0 ? b / a.grp_rows : 0;
     const float* ln_g = a.ln_g + grp * 4 * H;
     const float* ln_b = a.ln_b + grp * 4 * H;
@@ -263,8 +267,15 @@ __device__ __forceinline__ void row_fwd_body(const FwdArgs& a, const int b, cons
     if (a.h_carry != nullptr) stf<V>(a.h_carry + ro, h);
     if (a.c_out != nullptr) stf<V>(a.c_out + ro, cn);
     stf<V>(a.c_carry + ro, cn);
-    if (a.lp_kind == 1) stb<V>((__hip_bfloat16*)a.h_lp + b * a.ld_lp + u0, h);
-    else stf<V>((float*)a.h_lp + b * a.ld_lp + u0, h);
+    if constexpr (HSC1) {
+        const uint64_t w = (uint64_t)pack2(h[0], h[1]) | ((uint64_t)pack2(h[2], h[3]) << 32);
+        __hip_atomic_store((uint64_t*)((__hip_bfloat16*)a.h_lp + b * a.ld_lp + u0), w, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    } else if (a.lp_kind == 1) {
+        stb<V>((__hip_bfloat16*)a.h_lp + b * a.ld_lp + u0, h);
+    } else {
+        stf<V>((float*)a.h_lp + b * a.ld_lp + u0, h);
+    }
 }
 
 // ---- backward ------------------------------------------------------------------------

@@ -460,6 +460,9 @@ class HipLib:
         lib.skr_hyper_mod_chain.argtypes = [_p, _i64, _p, _p, _p, _i, _p, _i64, _i, _p, _p, C.POINTER(LstmFwdArgs),
                                             C.POINTER(ChainSync), _p]
         lib.skr_hyper_mod_chain.restype = _i
+        lib.skr_hyper_cell_mod.argtypes = [C.POINTER(LstmFwdArgs), _p, _p, _p, _i, _p, _i64, _i, _p, _p, _p, _p, _i,
+                                           C.POINTER(ChainSync), _p]
+        lib.skr_hyper_cell_mod.restype = _i
         lib.skr_cast_transpose_bf16.argtypes = [_p, _i64, _i64, _i, _i, _i, _p, _i64, _i64, _p, _i64, _i64, _p]
         lib.skr_cast_transpose_bf16.restype = _i
         lib.skr_hash_normal.argtypes = [_p, _u32, _u32, _p, _i64, _p]

@@ -87,6 +87,18 @@ CHAIN_FWD_STATS = {"launches": 0}
 # g / its partial sums before every chained forward launch), so a main-cell
 # row that read them ahead of its producer tiles shows up as NaN.
 CHAIN_POISON = False
+# Hyper cell + modulation step in ONE forward launch (csrc/hyper_mod.hip
+# hyper_cell_mod): wave 0 of modulation workgroup b runs the hyper cell of row
+# b and publishes its hh row; every modulation tile fetches its P fragments,
+# x-projection and R slabs while the rows compute, then waits for all rows
+# (timing probes: the P fetch is 4.8 of the separate modulation launch's
+# 10.9 us). 65 <= B <= 128. OFF: measured 28.2 us per launch against 4.9 + 10.9
+# for the pair, vae_large 26.2 vs 23.65 ms/step (profiles/r6/cm2/): the
+# one-wave hyper cell row takes ~11 us inside the launch (probes: no wait
+# 24.9, no rows 13.5 us).
+CELL_MOD = False
+CELL_MOD_POISON = False   # tests: NaN-fill the hh rows before each such launch
+CELL_MOD_STATS = {"launches": 0}
 # The main input projection x W_x + z W_z ([T, B, 4H], the largest tensor the
 # forward writes) stored in bf16 on the fused-modulation path; False keeps it
 # fp32 (A/B, scripts/micro/xh_ab.py).
@@ -374,6 +386,9 @@ class _HyperSeq(torch.autograd.Function):
         # chained modulation + main cell (one row block, LayerNorm main cell, no fp8 copy)
         chain_f = CHAIN_FWD and hmod and mln_on and B <= 128 and T >= 2 and H % max(CHAIN_FWD_C, 1) == 0
         cf = gemm.ChainCounters(dev, "hyp_fwd_m", T) if chain_f else None
+        cell_mod = CELL_MOD and hmod and not chain_f and 65 <= B <= 128 and T >= 2 and Hh == 256 and \
+            _lp_kind(A) == 1
+        cmc = gemm.ChainCounters(dev, "hyp_cell_mod", T) if cell_mod else None
         clm = _ClusterSync(T, B, H, dev, ln=mln_on,
                            C=(max(CHAIN_FWD_C, 1) if chain_f else HYPER_MAIN_C) if hmod else 0)
         clh = _ClusterSync(T, B, Hh, dev)
@@ -400,7 +415,8 @@ class _HyperSeq(torch.autograd.Function):
             else:
                 rgemm(A[t, :, :H], WhT, RM[rmi(t)], S_m)
                 rgemm(A[t], WyT, RY, S_y)
-            _cell_fwd(lib, ah, True, 0, st, "hyper_fwd_step")
+            if not cell_mod:
+                _cell_fwd(lib, ah, True, 0, st, "hyper_fwd_step")
             am.xp, am.R, am.vec = XH[t].data_ptr(), RM[rmi(t)].data_ptr(), VEC[t].data_ptr()
             am.r_lp = RLP[t].data_ptr() if (RLP is not None and not hmod) else None
             am.c_prev, am.step = (c0c if t == 0 else CC[t]).data_ptr(), t
@@ -427,6 +443,23 @@ class _HyperSeq(torch.autograd.Function):
                 # the cluster buffer keeps its C: the MOD-3 cell takes C = 2 too)
                 chain_f = False
                 cf.buf.zero_()
+            if cell_mod:   # hyper cell rows + modulation tiles, one launch
+                if CELL_MOD_POISON:
+                    A[t + 1, :, H:].fill_(float("nan"))
+                rc = lib.lib.skr_hyper_cell_mod(ctypes.byref(ah), PlT.data_ptr(), qb.data_ptr(), XHc[t].data_ptr(),
+                                                xh_dec.xh_bf16, RM[rmi(t)].data_ptr(), B * G, S_m, VEC[t].data_ptr(),
+                                                GP.data_ptr(), _ptr(RLP[t] if RLP is not None else None),
+                                                GS.data_ptr(), H, ctypes.byref(cmc.at(t)), st)
+                if rc == 0:
+                    CELL_MOD_STATS["launches"] += 1
+                    _cell_fwd(lib, am, mln_on, mod, st, "hyper_main_fwd_step")
+                    continue
+                if rc not in (-2, -3, -4):
+                    _check(rc, "hyper_cell_mod")
+                # not taken: the two launches from here on (counters cleared for the next sequence)
+                cell_mod = False
+                cmc.buf.zero_()
+                _cell_fwd(lib, ah, True, 0, st, "hyper_fwd_step")
             if hmod:
                 apply_hm_zgrid(lib)
                 _check(lib.lib.skr_hyper_mod_fwd(A[t + 1, :, H:].data_ptr(), K, PlT.data_ptr(), qb.data_ptr(),

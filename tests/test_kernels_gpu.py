@@ -1245,7 +1245,8 @@ def test_hyper_forward_chain_vs_unchained(B, T, fin_w):
     from sketch_rnn_amd.ops import hyper
     p, x, z, st, w = _hyper_setup(5, T, B, 5, 16, 2048, 256, 32, jitter=0.02, state=0.1)
     runs, launched = {}, {}
-    saved = hyper.CHAIN_FWD
+    saved = hyper.CHAIN_FWD, hyper.CELL_MOD
+    hyper.CELL_MOD = False   # (the plain arm: the hyper cell and modulation as two launches)
     try:
         for name, backend, dt, chain in (("ref", "torch", "fp32", False), ("chain", "hip", "bf16", True),
                                          ("plain", "hip", "bf16", False), ("chain2", "hip", "bf16", True)):
@@ -1256,7 +1257,7 @@ def test_hyper_forward_chain_vs_unchained(B, T, fin_w):
             runs[name] = _hyper_run(p, x, z, st, w, keep=0.9, hkeep=0.9, fin_w=fin_w)
             launched[name] = hyper.CHAIN_FWD_STATS["launches"] - n0
     finally:
-        hyper.CHAIN_FWD = saved
+        hyper.CHAIN_FWD, hyper.CELL_MOD = saved
     assert launched["chain"] == launched["chain2"] == (T if B <= 128 else 0) and launched["plain"] == 0, launched
     for i, n in enumerate(_names(p)):
         assert torch.equal(runs["chain"][i], runs["chain2"][i]), n
@@ -1281,7 +1282,8 @@ def test_hyper_forward_chain_row_split(C, B):
     from sketch_rnn_amd.ops import hyper
     T = 4
     p, x, z, st, w = _hyper_setup(6, T, B, 5, 16, 2048, 256, 32, jitter=0.02, state=0.1)
-    saved = hyper.CHAIN_FWD, hyper.CHAIN_FWD_C
+    saved = hyper.CHAIN_FWD, hyper.CHAIN_FWD_C, hyper.CELL_MOD
+    hyper.CELL_MOD = False   # (the plain arm: the hyper cell and modulation as two launches)
     runs = {}
     try:
         for name, backend, dt, chain in (("ref", "torch", "fp32", False), ("plain", "hip", "bf16", False),
@@ -1293,13 +1295,51 @@ def test_hyper_forward_chain_row_split(C, B):
             runs[name] = _hyper_run(p, x, z, st, w, keep=0.9, hkeep=0.9)
             assert hyper.CHAIN_FWD_STATS["launches"] - n0 == (T if chain else 0)
     finally:
-        hyper.CHAIN_FWD, hyper.CHAIN_FWD_C = saved
+        hyper.CHAIN_FWD, hyper.CHAIN_FWD_C, hyper.CELL_MOD = saved
     o_p, o_c = runs["plain"][0][0], runs["chain"][0][0]
     assert (o_p - o_c).abs().max().item() <= 1e-5 * o_p.abs().max().item()
     for i, n in enumerate(_names(p)):
         ref = runs["ref"][i].float()
         scale = max(ref.abs().max().item(), 1e-3)
         e_c = (runs["chain"][i].float() - ref).abs().max().item()
+        e_p = (runs["plain"][i].float() - ref).abs().max().item()
+        assert e_c <= 1.5 * e_p + 1e-3 * scale, (n, e_c, e_p, scale)
+
+
+@pytest.mark.parametrize("B,T", [(100, 6), (128, 3), (65, 4), (37, 3)])
+def test_hyper_cell_and_modulation_one_launch(B, T):
+    """csrc/hyper_mod.hip skr_hyper_cell_mod: wave 0 of modulation workgroup b
+    runs the hyper cell of row b (row kernel body, hh stored write-through),
+    every tile prefetches P / xh / R, waits for all rows and reads hh with sc1
+    loads -- against the two launches and the fp32 oracle (outputs, finals,
+    dz, every gradient; dropout on): error <= 1.5 x the two-launch error +
+    1e-3 of the largest element (the row body sums in another order than the
+    clustered hyper cell); NaN-poisoned hh rows before every launch (a tile
+    reading ahead of the rows) must not change a bit; it ran T times for
+    65 <= B <= 128 and not at all outside."""
+    from sketch_rnn_amd.ops import hyper
+    p, x, z, st, w = _hyper_setup(7, T, B, 5, 16, 2048, 256, 32, jitter=0.02, state=0.1)
+    runs, launched = {}, {}
+    saved = hyper.CELL_MOD, hyper.CELL_MOD_POISON
+    try:
+        for name, backend, dt, on, pois in (("ref", "torch", "fp32", False, False), ("cm", "hip", "bf16", True, False),
+                                            ("plain", "hip", "bf16", False, False), ("cm_p", "hip", "bf16", True, True)):
+            hyper.CELL_MOD, hyper.CELL_MOD_POISON = on, pois
+            ops.set_backend(backend)
+            ops.set_compute_dtype(dt)
+            n0 = hyper.CELL_MOD_STATS["launches"]
+            runs[name] = _hyper_run(p, x, z, st, w, keep=0.9, hkeep=0.9)
+            launched[name] = hyper.CELL_MOD_STATS["launches"] - n0
+    finally:
+        hyper.CELL_MOD, hyper.CELL_MOD_POISON = saved
+    want = T if 65 <= B <= 128 else 0
+    assert launched["cm"] == launched["cm_p"] == want and launched["plain"] == 0, launched
+    for i, n in enumerate(_names(p)):
+        assert torch.isfinite(runs["cm_p"][i]).all(), n
+        assert torch.equal(runs["cm"][i], runs["cm_p"][i]), n
+        ref = runs["ref"][i].float()
+        scale = max(ref.abs().max().item(), 1e-3)
+        e_c = (runs["cm"][i].float() - ref).abs().max().item()
         e_p = (runs["plain"][i].float() - ref).abs().max().item()
         assert e_c <= 1.5 * e_p + 1e-3 * scale, (n, e_c, e_p, scale)
 

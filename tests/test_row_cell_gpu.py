@@ -63,6 +63,7 @@ def test_row_cells_hyper_vae_large_shapes(B, keep, hkeep, monkeypatch):
     from sketch_rnn_amd.ops import hyper
     monkeypatch.setattr(hyper, "HYPER_BWD_FUSE", False)
     monkeypatch.setattr(hyper, "CHAIN", False)   # (the chained main-cell launch: test_kernels_gpu.py)
+    monkeypatch.setattr(hyper, "CELL_MOD", False)   # (the hyper cell inside the modulation launch: ditto)
     T = 7
     p, x, z, st, w = _hyper_setup(6, T, B, 5, 16, 2048, 256, 32, jitter=0.02, state=0.1)
     runs = _arms(lambda: _hyper_run(p, x, z, st, w, keep, hkeep))
@@ -110,13 +111,17 @@ def test_default_policy_row_kernels_only_in_main_backward():
     """Default SKR_ROW_CELLS=main: the HyperLSTM main-cell backward runs the
     row kernel (the first backward step as its own launch, the rest inside
     the chained dR_hyp W_y^T launch, csrc/chain_step.hip), the other three
-    cell launches per step the clustered ones."""
+    cell launches per step the clustered ones (the hyper cell inside the
+    modulation launch, hyper.CELL_MOD, is off)."""
     from test_kernels_gpu import _hyper_run, _hyper_setup
+    from sketch_rnn_amd.ops import hyper
     T = 3
     p, x, z, st, w = _hyper_setup(2, T, 100, 5, 16, 2048, 256, 32, jitter=0.02, state=0.1)
     recurrent.ROW_CELLS = "main"
     ops.set_backend("hip")
     ops.set_compute_dtype("bf16")
     before = dict(recurrent.ROW_STATS)
+    n0 = hyper.CELL_MOD_STATS["launches"]
     _hyper_run(p, x, z, st, w)
     assert {k: recurrent.ROW_STATS[k] - before[k] for k in before} == {"row": 1, "chain": T - 1, "chain3": 0, "cluster": 3 * T}
+    assert hyper.CELL_MOD_STATS["launches"] - n0 == 0
