@@ -79,29 +79,41 @@ static int g_row_poll = 1;
 // per workgroup: NTR = H / 4 threads (waves past NTR / 64 end at once), every
 // load but the slabs issued before the in-launch wait (row_fwd_body /
 // row_bwd_body CHAIN); the arithmetic of the row kernels (csrc/row_cell.hip).
+// probe (skr_chain_ln_set_probe; outputs WRONG while set): 1 the rows end at
+// once (producers only), 2 the producers only arrive (rows only, no GEMM).
 template <int NTR, int DS>
 __global__ __launch_bounds__(512) void chain_ln_fwd_kernel(const GemmGroup g, const int nprod, const skr::FwdArgs cell,
-                                                           const ChainSync cs) {
+                                                           const ChainSync cs, const int probe) {
     extern __shared__ __attribute__((aligned(16))) __hip_bfloat16 smem[];
     const int id = blockIdx.x;
     if (id < nprod) {
+        if (probe == 2) {
+            if (blockIdx.x == 0) chain_rotate(cs.counters, cs.n, cs.k);
+            chain_arrive(cs.counters + cs.k);
+            return;
+        }
         producer_tile<8>(g, cs, smem);
         return;
     }
-    if (__builtin_amdgcn_readfirstlane(threadIdx.x) >= NTR) return;   // (wave-uniform)
+    if (probe == 1 || __builtin_amdgcn_readfirstlane(threadIdx.x) >= NTR) return;   // (wave-uniform)
     row_fwd_body<NTR, 4, 0, DS, true>(cell, id - nprod, cs.counters + cs.k, (uint32_t)nprod, cs.err);
 }
 
 template <int NTR>
 __global__ __launch_bounds__(512) void chain_ln_bwd_kernel(const GemmGroup g, const int nprod, const skr::BwdArgs cell,
-                                                           const ChainSync cs) {
+                                                           const ChainSync cs, const int probe) {
     extern __shared__ __attribute__((aligned(16))) __hip_bfloat16 smem[];
     const int id = blockIdx.x;
     if (id < nprod) {
+        if (probe == 2) {
+            if (blockIdx.x == 0) chain_rotate(cs.counters, cs.n, cs.k);
+            chain_arrive(cs.counters + cs.k);
+            return;
+        }
         producer_tile<8>(g, cs, smem);
         return;
     }
-    if (__builtin_amdgcn_readfirstlane(threadIdx.x) >= NTR) return;
+    if (probe == 1 || __builtin_amdgcn_readfirstlane(threadIdx.x) >= NTR) return;
     row_bwd_body<NTR, 4, false, 1, true>(cell, id - nprod, cs.counters + cs.k, (uint32_t)nprod, cs.err);
 }
 
@@ -372,6 +384,122 @@ SKR_API int skr_chain_set_poll(int p) {
 
 SKR_API int skr_chain_sync_size() { return (int)sizeof(ChainSync); }
 
+static int g_chain_ln_probe = 0;
+
+// ---- skewed LayerNorm-LSTM forward step ---------------------------------------------------
+// Launch t: [cell rows of step t][h_t W_h tiles of step t + 1]. The rows'
+// R slabs were written by the previous launch, so they load everything at
+// once (no wait); they store their bf16 h_t row write-through and arrive.
+// The tiles of step t + 1 stage their whole 64-column weight slice in LDS
+// (the latency that does not depend on h_t) while the rows compute, wait
+// for all B rows, then load their h_t fragments with sc1 loads and run the
+// K-steps from LDS (v_mfma_f32_16x16x32_bf16, ascending k, as the grouped
+// tiles). Rows have the lowest ids and never wait. Tile: 128 rows (8 waves x
+// one 16-row tile) x 64 columns x kslice = 32 KS; LDS row r of the slice
+// keeps its 16-byte chunk c at c ^ (r & 15) (conflict-free fragment reads).
+template <int KS>
+__device__ __forceinline__ void skew_tile(const __hip_bfloat16* __restrict__ WT, int H, const __hip_bfloat16* __restrict__ A,
+                                          int64_t lda, int B, float* __restrict__ Rn, int64_t r_slab, int64_t ld_r, int p,
+                                          const uint32_t* cnt, uint32_t target, int* err, __hip_bfloat16* lds) {
+    constexpr int KSL = 32 * KS, CPR = KSL / 8;          // slice width, 16-byte chunks per LDS row
+    const int G = 4 * H, ntile = G / kBn;
+    const int n0 = (p % ntile) * kBn, k0 = (p / ntile) * KSL, sl = p / ntile;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, fr = lane & 15, fq = lane >> 4;
+    for (int i = tid; i < kBn * CPR; i += 512) {          // the weight slice: independent of h_t
+        const int r = i / CPR, c = i - r * CPR;
+        const bf16x8 v = *(const bf16x8*)(WT + (int64_t)(n0 + r) * H + k0 + 8 * c);
+        *(bf16x8*)(lds + r * KSL + ((c ^ (r & 15)) * 8)) = v;
+    }
+    chain_wait(cnt, target, err);                          // (its barrier also publishes the LDS slice)
+    const int row = 16 * w + fr;
+    const __amdgpu_buffer_rsrc_t ar = rsrc(A, (int64_t)B * lda * 2);
+    bf16x8 af[KS];
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) af[ks] = ld_sc1(ar, (uint32_t)(((int64_t)min(row, B - 1) * lda + k0 + 32 * ks + 8 * fq) * 2));
+    f32x4 acc[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int r = 16 * j + fr;
+            const bf16x8 b = *(const bf16x8*)(lds + r * KSL + (((4 * ks + fq) ^ (r & 15)) * 8));
+            acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ks], b, acc[j], 0, 0, 0);
+        }
+    if (16 * w >= B) return;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int rr = 16 * w + 4 * fq + i;
+            if (rr < B) Rn[(int64_t)sl * r_slab + (int64_t)rr * ld_r + n0 + 16 * j + fr] = acc[j][i];
+        }
+}
+
+template <int NTR, int DS, int KS>
+__global__ __launch_bounds__(512) void skew_ln_fwd_kernel(const skr::FwdArgs cell, const __hip_bfloat16* __restrict__ WT,
+                                                          float* __restrict__ Rn, const ChainSync cs) {
+    extern __shared__ __attribute__((aligned(16))) __hip_bfloat16 smem[];
+    const int id = blockIdx.x, B = cell.B;
+    if (id == 0) chain_rotate(cs.counters, cs.n, cs.k);
+    if (id < B) {
+        if (__builtin_amdgcn_readfirstlane(threadIdx.x) >= NTR) return;   // (wave-uniform)
+        row_fwd_body<NTR, 4, 0, DS, false, true>(cell, id);
+        chain_arrive(cs.counters + cs.k);
+        return;
+    }
+    skew_tile<KS>(WT, cell.H, (const __hip_bfloat16*)cell.h_lp, cell.ld_lp, B, Rn, cell.R_slab, cell.ld_R, id - B,
+                  cs.counters + cs.k, (uint32_t)B, cs.err, smem);
+}
+
+// Skewed LayerNorm-LSTM forward step t: the cell rows of step t (cell: R =
+// the slabs of step t, written by an earlier launch; lp_kind 1) and, when
+// Rn != null, the tiles of step t + 1 writing its S = R_nslab slabs into Rn
+// (same slab stride and row stride as cell.R) from WT [4H][H] bf16 and the
+// rows' h_t. H in {256, 512, 1024}, B <= 128, H / S in {128, 256, 512}.
+// Returns -2 / -3 / -4 when not taken.
+SKR_API int skr_skew_ln_fwd(const skr::FwdArgs* cell, const void* WT, float* Rn, const ChainSync* cs, hipStream_t s) {
+    if (cell == nullptr || check_sync(cs)) return -6;
+    const skr::FwdArgs& a = *cell;
+    if (a.B <= 0) return 0;
+    const int H = a.H, S = a.R_nslab;
+    if ((H != 256 && H != 512 && H != 1024) || a.B > 128 || a.lp_kind != 1 || a.grp_rows > 0 || S < 1 || S > 4 ||
+        H % S != 0)
+        return -2;
+    const int rc = row_fwd_check(a, 0);
+    if (rc) return rc;
+    const int kslice = H / S;
+    if (kslice != 128 && kslice != 256 && kslice != 512) return -2;
+    if ((((uintptr_t)WT | (uintptr_t)Rn | (uintptr_t)a.h_lp) & 15) || a.ld_lp % 8) return -4;
+    const int ntr = H / 4, ds = S <= 1 ? 1 : S <= 2 ? 2 : 4, ks = kslice / 32;
+    const int nprod = Rn ? (4 * H / kBn) * S : 0;
+    const size_t lds = (size_t)kBn * kslice * 2;
+    const void* k = nullptr;
+#define SKR_SK(NTR_, DS_, KS_) if (ntr == NTR_ && ds == DS_ && ks == KS_) k = (const void*)skew_ln_fwd_kernel<NTR_, DS_, KS_>;
+#define SKR_SK_KS(NTR_, DS_) SKR_SK(NTR_, DS_, 4) SKR_SK(NTR_, DS_, 8) SKR_SK(NTR_, DS_, 16)
+#define SKR_SK_DS(NTR_) SKR_SK_KS(NTR_, 1) SKR_SK_KS(NTR_, 2) SKR_SK_KS(NTR_, 4)
+    SKR_SK_DS(64) SKR_SK_DS(128) SKR_SK_DS(256)
+#undef SKR_SK_DS
+#undef SKR_SK_KS
+#undef SKR_SK
+    if (k == nullptr) return -2;
+    if (lds > 48 * 1024) (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    const __hip_bfloat16* wt = (const __hip_bfloat16*)WT;
+    float* rn = Rn;
+    void* args[] = {(void*)&a, (void*)&wt, (void*)&rn, (void*)cs};
+    if (hipLaunchKernel(k, dim3(a.B + nprod), dim3(512), args, lds, s) != hipSuccess) return -1;
+    return SKR_CHECK_LAUNCH();
+}
+
+// Timing probes of the chained LayerNorm-LSTM steps (scripts/micro/ln_probe.py;
+// outputs WRONG while set): 1 producers only, 2 rows only. Returns the previous.
+SKR_API int skr_chain_ln_set_probe(int p) {
+    const int prev = g_chain_ln_probe;
+    if (p >= 0) g_chain_ln_probe = p;
+    return prev;
+}
+
 // LayerNorm-LSTM forward step chained: probs (all producers) write the R
 // slabs (cell->R, <= 8) the rows of this step sum; rows as skr_row_fwd_step
 // mod 0 with H in {256, 512, 1024, 2048}. Returns -2 / -3 / -4 when not taken.
@@ -402,8 +530,8 @@ SKR_API int skr_chain_ln_fwd(const GemmProblem* probs, int n, const skr::FwdArgs
         (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLds);
         attr_done[n_attr++] = k;
     }
-    int npv = np;
-    void* args[] = {(void*)&g, (void*)&npv, (void*)&a, (void*)cs};
+    int npv = np, prb = g_chain_ln_probe;
+    void* args[] = {(void*)&g, (void*)&npv, (void*)&a, (void*)cs, (void*)&prb};
     if (hipLaunchKernel(k, dim3(np + a.B), dim3(512), args, kLds, s) != hipSuccess) return -1;
     return SKR_CHECK_LAUNCH();
 }
@@ -436,8 +564,8 @@ SKR_API int skr_chain_ln_bwd(const GemmProblem* probs, int n, const skr::BwdArgs
         (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLds);
         attr_done[n_attr++] = k;
     }
-    int npv = np;
-    void* args[] = {(void*)&g, (void*)&npv, (void*)&a, (void*)cs};
+    int npv = np, prb = g_chain_ln_probe;
+    void* args[] = {(void*)&g, (void*)&npv, (void*)&a, (void*)cs, (void*)&prb};
     if (hipLaunchKernel(k, dim3(np + a.B), dim3(512), args, kLds, s) != hipSuccess) return -1;
     return SKR_CHECK_LAUNCH();
 }

@@ -364,6 +364,10 @@ class HipLib:
         lib.skr_bproj_fwd.restype = _i
         lib.skr_bproj_bwd.argtypes = [_p, _p, _i, _i64, _p, _p, _i, _i, _i, _i, _p]
         lib.skr_bproj_bwd.restype = _i
+        lib.skr_skew_ln_fwd.argtypes = [C.POINTER(LstmFwdArgs), _p, _p, C.POINTER(ChainSync), _p]
+        lib.skr_skew_ln_fwd.restype = _i
+        lib.skr_chain_ln_set_probe.argtypes = [_i]
+        lib.skr_chain_ln_set_probe.restype = _i
         lib.skr_hyper_mod_set_probe.argtypes = [_i]
         lib.skr_hyper_mod_set_probe.restype = _i
         lib.skr_bproj_set_wide.argtypes = [_i]

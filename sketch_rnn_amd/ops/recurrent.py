@@ -240,6 +240,14 @@ LN_BWD_SPLIT_CAP = 8
 LN_CHAIN = True
 LN_CHAIN_POISON = False
 LN_CHAIN_STATS = {"fwd": 0, "bwd": 0}
+# Skewed forward (csrc/chain_step.hip skr_skew_ln_fwd): launch t runs the cell
+# rows of step t (their R slabs complete at launch start) and the h W_h tiles
+# of step t + 1, which stage their weight slice in LDS while the rows compute
+# and then wait for h_t -- the weight fetch off the critical path (probes,
+# scripts/micro/ln_probe.py: the chained step is producers 5.7 + rows 5.9 us,
+# fully serialised). Step 0's product is its own launch.
+LN_SKEW = False
+LN_SKEW_STATS = {"fwd": 0}
 
 
 def _lstm_splits(planned: int, cap: int, K: int) -> int:
@@ -331,6 +339,13 @@ class _LSTMSeq(torch.autograd.Function):
             and T_loop > 0 and H % 256 == 0 and H <= 2048 and 1 <= S <= 8
         cf = gemm.ChainCounters(dev, "ln_fwd", T) if chain_f else None
         WlT2 = WlT if WlT.dim() == 2 else WlT[0]
+        skew = chain_f and LN_SKEW and BB <= 128 and H in (256, 512, 1024) and S in (1, 2, 4) and \
+            H // S in (128, 256, 512) and T >= 2
+        if skew:   # double-buffered slabs: launch t reads R2[t % 2], writes R2[(t + 1) % 2]
+            R2 = torch.empty(2, S, BB, G, device=dev, dtype=f32)
+            sk = gemm.ChainCounters(dev, "ln_skew", T)
+            gemm.rec_gemm(A[0], WlT2, R2[0], S)
+            a.R_nslab, a.R_slab = S, BB * G
         for t in range(T_loop):
             cl.set(a, t)
             a.xp = xp[t].data_ptr()
@@ -345,6 +360,24 @@ class _LSTMSeq(torch.autograd.Function):
             a.h_carry = HC[t % 2].data_ptr() if HC is not None else None
             a.h_lp = A[t + 1].data_ptr()
             a.c_carry = CC[t + 1].data_ptr()
+            if skew:
+                a.R = R2[t % 2].data_ptr()
+                if LN_CHAIN_POISON:
+                    A[t + 1].fill_(float("nan"))
+                rc = lib.lib.skr_skew_ln_fwd(ctypes.byref(a), WlT2.data_ptr(),
+                                             R2[(t + 1) % 2].data_ptr() if t + 1 < T else None,
+                                             ctypes.byref(sk.at(t)), st)
+                if rc == 0:
+                    LN_SKEW_STATS["fwd"] += 1
+                    continue
+                if t > 0 or rc not in (-2, -3, -4):
+                    _check(rc if rc != 0 else -1, "skew_ln_fwd")
+                skew = False   # step 0 not taken: the chained / two-launch steps (R2[0] holds step 0's product)
+                sk.buf.zero_()
+                a.R = R2[0].data_ptr()
+                _cell_fwd(lib, a, ln, 0, st, "lstm_fwd_step")
+                a.R = R.data_ptr()
+                continue
             if chain_f:
                 if LN_CHAIN_POISON:
                     R.fill_(float("nan"))

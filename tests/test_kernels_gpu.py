@@ -174,6 +174,56 @@ def test_ln_lstm_chained_steps(H, B, T, keep):
         assert e_c <= 1.5 * e_p + 1e-3 * scale, (i, e_c, e_p, scale)
 
 
+@pytest.mark.parametrize("H,B,T,keep", [(512, 100, 9, 0.9), (256, 37, 6, 1.0), (1024, 64, 4, 0.9), (512, 128, 3, 0.8)])
+def test_ln_lstm_skewed_forward(H, B, T, keep):
+    """ops.recurrent.LN_SKEW (csrc/chain_step.hip skr_skew_ln_fwd): launch t
+    runs the cell rows of step t and the h_t W_h tiles of step t + 1 (weight
+    slice staged before the wait, h_t read with sc1 loads) -- against the
+    chained steps and the fp32 oracle, outputs, final states and every
+    gradient: error <= 1.5 x the chained error + 1e-3 of the largest
+    element; NaN-poisoned h_t rows before every launch (a tile reading ahead
+    of the rows) must not change a bit; T skewed launches per sequence."""
+    from sketch_rnn_amd.ops import recurrent
+    torch.manual_seed(H + B + 1)
+    xp = torch.randn(T, B, 4 * H, device=DEV, requires_grad=True)
+    W = (torch.randn(H, 4 * H, device=DEV) / math.sqrt(H)).requires_grad_()
+    h0 = (torch.randn(B, H, device=DEV) * 0.5).requires_grad_()
+    c0 = (torch.randn(B, H, device=DEV) * 0.5).requires_grad_()
+    lnp = [torch.randn(4 * H, device=DEV).mul(0.1).add(1).requires_grad_(),
+           torch.randn(4 * H, device=DEV).mul(0.1).requires_grad_(),
+           torch.randn(H, device=DEV).mul(0.1).add(1).requires_grad_(),
+           torch.randn(H, device=DEV).mul(0.1).requires_grad_()]
+    seed = torch.tensor([29], device=DEV)
+
+    def fn(xp, W, h0, c0, *lnp):
+        out, (hT, cT) = ops.lstm_sequence(xp, W, h0, c0, drop_keep=keep, drop_seed=seed, drop_stream=5, ln=tuple(lnp))
+        return [out, hT, cT]
+
+    inputs = [xp, W, h0, c0] + lnp
+    saved = recurrent.LN_CHAIN, recurrent.LN_SKEW, recurrent.LN_CHAIN_POISON
+    res = {}
+    try:
+        for name, backend, dt, skew, pois in (("ref", "torch", "fp32", False, False), ("chain", "hip", "bf16", False, False),
+                                              ("skew", "hip", "bf16", True, False), ("skew_p", "hip", "bf16", True, True)):
+            recurrent.LN_CHAIN, recurrent.LN_SKEW, recurrent.LN_CHAIN_POISON = True, skew, pois
+            ops.set_compute_dtype(dt)
+            n0 = recurrent.LN_SKEW_STATS["fwd"]
+            o, g = _run(backend, fn, inputs)
+            res[name] = o + g
+            if skew:
+                assert recurrent.LN_SKEW_STATS["fwd"] - n0 == T
+    finally:
+        recurrent.LN_CHAIN, recurrent.LN_SKEW, recurrent.LN_CHAIN_POISON = saved
+        ops.set_compute_dtype("fp32")
+    for i, (c, k, kp, r) in enumerate(zip(res["chain"], res["skew"], res["skew_p"], res["ref"])):
+        assert torch.isfinite(kp).all(), i
+        assert torch.equal(k, kp), i
+        scale = max(r.abs().max().item(), 1e-3)
+        e_k = (k.float() - r).abs().max().item()
+        e_c = (c.float() - r).abs().max().item()
+        assert e_k <= 1.5 * e_c + 1e-3 * scale, (i, e_k, e_c, scale)
+
+
 def test_lstm_sequence_bf16_close():
     torch.manual_seed(1)
     T, B, H = 9, 8, 512
