@@ -245,7 +245,9 @@ LN_CHAIN_STATS = {"fwd": 0, "bwd": 0}
 # of step t + 1, which stage their weight slice in LDS while the rows compute
 # and then wait for h_t -- the weight fetch off the critical path (probes,
 # scripts/micro/ln_probe.py: the chained step is producers 5.7 + rows 5.9 us,
-# fully serialised). Step 0's product is its own launch.
+# fully serialised). Step 0's product is its own launch. OFF: measured
+# slower, vae_layernorm 8.97 vs 8.76 ms/step (profiles/r6/skew/ab_ln.log;
+# correct and poison-tested, tests/test_kernels_gpu.py).
 LN_SKEW = False
 LN_SKEW_STATS = {"fwd": 0}
 
